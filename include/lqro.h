@@ -1,0 +1,157 @@
+/*
+ * lqro.h — C-ABI of the MI355X-native LQR-Obstacle step (liblqro.so).
+ *
+ * This is the drop-in boundary for the per-timestep pair loop of the
+ * reference simulator (hihixuyang/LQR-Obstacles,
+ * QuadrotorHoverController/LQRObstacles.cpp, "LQRO" below).  The reference
+ * has no plugin/FFI API: the path is a set of free functions driven by the
+ * loop at LQRO:1391-1436.  Each entry point below names the reference code it
+ * replaces.  Conventions:
+ *   - every function returns an int status: 0 = LQRO_OK, negative = error;
+ *     no C++ exception crosses the ABI;
+ *   - the caller owns every host array; the context owns device buffers and
+ *     its HIP stream;
+ *   - one context per host thread; contexts are independent of each other;
+ *   - matrices are row-major fp64, exactly the element order of the
+ *     reference's Matrix<R,C> (include/matrix.h:16,48).
+ */
+#ifndef LQRO_H
+#define LQRO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------ */
+enum {
+  LQRO_OK = 0,
+  LQRO_E_ARG = -1,       /* bad argument / config                          */
+  LQRO_E_HIP = -2,       /* a HIP runtime call failed                      */
+  LQRO_E_NOMEM = -3,     /* device or host allocation failed               */
+  LQRO_E_STATE = -4,     /* call order violated (e.g. step before gains)   */
+  LQRO_E_SINGULAR = -5,  /* singular 3x3 C*G_k (reference asserts, MAT:632) */
+  LQRO_E_NODEVICE = -6,  /* no usable gfx950 device                        */
+  LQRO_E_OVERFLOW = -7   /* an internal work queue overflowed              */
+};
+
+/* ---- flags ------------------------------------------------------------- */
+#define LQRO_FLAG_RECORDS     0x1  /* keep per-pair records for lqro_get_records */
+
+/* per-pair record flags (lqro_pair_record.flags) */
+#define LQRO_REC_PLANE    0x01  /* n_reach > min_reach: a half-plane was emitted (LQRO:1409) */
+#define LQRO_REC_INSIDE   0x02  /* GJK put vrel inside the hull (LQRO:855-864)          */
+#define LQRO_REC_BACKUP   0x04  /* GJK took its backup procedure (GJK:663-706)          */
+#define LQRO_REC_HULL     0x08  /* the in-kernel hull produced the plane (LQRO:867-969) */
+#define LQRO_REC_HULLFAIL 0x10  /* hull degenerate / capacity exceeded                  */
+
+/* Static configuration.  The names follow the reference's compile-time
+ * macros (LQRO:9-14) and the constants of its driver (LQRO:1387, 1224). */
+typedef struct lqro_config {
+  int32_t n_agents;      /* NUM_QUADS                                             */
+  int32_t x_dim;         /* X_DIM (simulator2.h:4) — 16                           */
+  int32_t u_dim;         /* U_DIM — 4                                             */
+  int32_t horizon;       /* OBSTACLE_STEPS (LQRO:11)                              */
+  int32_t n_points;      /* NUM_POINTS (LQRO:12) points per sampled ellipsoid     */
+  int32_t min_reach;     /* pairs with n_reach <= min_reach emit no plane (4, LQRO:1409) */
+  double  xy_radius;     /* XYRADIUS (LQRO:13); the sphere uses 2*XYRADIUS        */
+  double  z_radius;      /* ZRADIUS  (LQRO:14)                                    */
+  double  vmax_reach;    /* reachable-velocity radius, 30 (LQRO:1387)             */
+  double  vmax_lp;       /* LP speed bound, 100 (LQRO:1224)                        */
+  int32_t row_begin;     /* agents [row_begin,row_end) are this context's rows    */
+  int32_t row_end;       /*   (multi-GPU sharding; 0,0 = all rows)                 */
+  int32_t device;        /* HIP device ordinal                                    */
+  int32_t flags;         /* LQRO_FLAG_*                                           */
+} lqro_config;
+
+/* Physical model + cost weights: the globals set by setup() and _tmain
+ * (LQRO:169-189, 1275-1286, 559-561). */
+typedef struct lqro_model {
+  double dt, gravity, mass, inertia, moment_const, thrust_latency, length;
+  double j_step;          /* central-difference step (LQRO:189)   */
+  double qv, qp, r;       /* Qv = qv*I3, Qp = qp*I3, R = r*I4     */
+  double pos_weight;      /* 0.05 in LQRO:559-561 (0.25 in PCW)   */
+} lqro_model;
+
+/* One record per ordered pair (i, j), j != i, kept when LQRO_FLAG_RECORDS
+ * is set.  Field-for-field what the reference computes in LQRO:1401-1417. */
+typedef struct lqro_pair_record {
+  int32_t i, j;
+  int32_t n_reach;        /* reachablePoints.size() (LQRO:1408)              */
+  int32_t flags;          /* LQRO_REC_*                                      */
+  int32_t gjk_iters;      /* G-tests performed by gjk_distance               */
+  int32_t simplex_n;      /* final GJK simplex size                          */
+  int32_t simplex[4];     /* final GJK simplex: indices into reachablePoints */
+  int32_t facet[3];       /* hull branch: arg-min facet (reachable indices)  */
+  int32_t n_facets;       /* hull branch: number of hull facets              */
+  uint64_t reach_hash;    /* FNV-1a over the reachable index list            */
+  double dist;            /* distance before the *0.5 of LQRO:1416           */
+  double normal[3];       /* normalVector fed to createHalfPlanes            */
+  double wpt_vrel[3];     /* GJK witness on the vrel point                   */
+  double wpt_hull[3];     /* GJK witness on the hull                         */
+  float  plane_point[3];  /* Plane.point  (fp32, LQRO:1217-1219)             */
+  float  plane_normal[3]; /* Plane.normal (fp32, LQRO:1210)                  */
+} lqro_pair_record;
+
+typedef struct lqro_ctx lqro_ctx;
+
+/* Defaults: LQRO's constants (N given by the caller). */
+void lqro_config_default(lqro_config* cfg, int32_t n_agents, int32_t horizon, int32_t n_points);
+void lqro_model_default(lqro_model* m);
+
+/* Replaces controlMatrices (LQRO:520-582) and linearizeDiscretize (LQRO:456-471):
+ * the velocity LQR (A,B,c,L,E) and the position LQR (Lh,Eh) at hover.
+ * Host C++ (setup time, once per agent type).  Any out pointer may be NULL. */
+int lqro_synthesize_gains(const lqro_model* m,
+                          double* A  /* X*X */, double* B  /* X*U */, double* c /* X */,
+                          double* L  /* U*X */, double* E  /* U*3 */,
+                          double* Lh /* 3*X */, double* Eh /* 3*3 */);
+
+/* Replaces createSpheres (LQRO:735-750): NP Fibonacci-sphere points. */
+int lqro_sphere(int32_t n_points, double xy_radius, double z_radius, double* out /* NP*3 */);
+
+int  lqro_create(const lqro_config* cfg, lqro_ctx** out);
+void lqro_destroy(lqro_ctx* ctx);
+
+/* Gains read by the pair loop: A, B shared (LQRO:1265-1266, 1371); L_i, E_i
+ * per agent (Quadrotor::L,E, LQRO:90-91).  per_agent = 0: one L,E for all
+ * agents (the reference's case: every agent gets the same gains, LQRO:1371);
+ * per_agent = 1: L is n_agents*U*X, E is n_agents*U*3.  Builds the per-agent
+ * horizon tables on the device (findFG + createObstacle's Transform, LQRO:723-732,
+ * 770-773). */
+int lqro_set_gains(lqro_ctx* ctx, const double* A, const double* B,
+                   const double* L, const double* E, int32_t per_agent);
+
+/* One control step: the pair loop LQRO:1393-1436 for the context's rows.
+ * x: n_agents*X agent states (Quadrotor::x), vgoal: n_agents*3,
+ * newv: n_agents*3 (only rows [row_begin,row_end) are written).  Host
+ * pointers; blocks until newv is ready. */
+int lqro_step(lqro_ctx* ctx, const double* x, const double* vgoal, double* newv);
+
+/* Same, device-resident: d_x, d_vgoal, d_newv are device pointers on the
+ * context's device; the work is enqueued on `stream` (hipStream_t, NULL =
+ * the context's own stream) and the call returns without synchronising. */
+int lqro_step_device(lqro_ctx* ctx, const double* d_x, const double* d_vgoal,
+                     double* d_newv, void* stream);
+
+/* Per-pair records of the last step (LQRO_FLAG_RECORDS): rows
+ * [row_begin,row_end) x (n_agents-1) neighbours in j order. */
+int lqro_get_records(lqro_ctx* ctx, lqro_pair_record* out, int64_t capacity, int64_t* n_out);
+
+/* Counters of the last step: [0]=pairs, [1]=planes, [2]=inside, [3]=hull ok,
+ * [4]=hull fail, [5]=gjk backups, [6]=sum n_reach, [7]=sum G-tests. */
+int lqro_get_stats(lqro_ctx* ctx, int64_t* stats8);
+
+/* Device time of the kernels of the last step, ms, measured with HIP events on
+ * the context's stream: [0]=pair sweep+GJK, [1]=hull, [2]=LP, [3]=whole step. */
+int lqro_get_timings(lqro_ctx* ctx, float* ms4);
+
+const char* lqro_status_string(int status);
+int lqro_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LQRO_H */

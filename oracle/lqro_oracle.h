@@ -1,0 +1,109 @@
+/*
+ * lqro_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C, single-threaded CPU restatement of the reference's per-timestep
+ * LQR-Obstacle path (hihixuyang/LQR-Obstacles, QuadrotorHoverController/
+ * LQRObstacles.cpp = "LQRO", gjk.cpp = "GJK", include/matrix.h = "MAT",
+ * Vector3.h = "V3").  Every function cites the reference lines it restates.
+ *
+ * Who may use it: tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg — as the checker / the timed CPU baseline only.  The
+ * product (liblqro.so) never links, loads or calls anything here.
+ *
+ * Pinning: tests/test_oracle_vs_ref.py compares it bit-for-bit against the
+ * reference's own functions compiled from /root/reference (oracle/_ref, see
+ * oracle/Makefile) and against the hull fixture the reference ships
+ * (pointList.txt / Planes.txt / facetVertices.txt); tests/golden/ holds the
+ * vectors generated from oracle/_ref for use where /root/reference is absent.
+ */
+#ifndef LQRO_ORACLE_H
+#define LQRO_ORACLE_H
+
+#include <stdint.h>
+#include "../include/lqro.h"   /* record / config / model layouts only */
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int  orc_version(void);
+
+/* LQRO:169-189 + 1275-1286 + 559-561 (same numbers as lqro_model_default). */
+void orc_model_default(lqro_model* m);
+
+/* controlMatrices (LQRO:520-582) incl. linearizeDiscretize (LQRO:456-471),
+ * f (LQRO:368-397), Jacobian_fx/fu (LQRO:421-441), exp (MAT:773-790).
+ * X = 16, U = 4, V = 3.  `l` (LQRO:552,557) is not produced: it needs
+ * pseudoInverse and is not read by the pair path. */
+int  orc_synthesize(const lqro_model* m, double* A, double* B, double* c,
+                    double* L, double* E, double* Lh, double* Eh);
+
+/* createSpheres (LQRO:735-750). */
+void orc_sphere(int np, double xy_radius, double z_radius, double* s);
+
+/* The per-agent horizon tables: findFG (LQRO:723-732) iterated H times from
+ * F=I, G=0 (LQRO:1401-1404), and for every step k the two factors of
+ * createObstacle (LQRO:771-773): T_k = !(C*G_k) (3x3) and NCF_k = (-C)*F_k
+ * (3xX).  Depends on agent i only, never on j — computing it once per agent
+ * is bit-identical to the reference's per-pair recomputation. */
+int  orc_tables(int X, int U, int H, const double* A, const double* B,
+                const double* L, const double* E, double* T /* H*9 */,
+                double* NCF /* H*3*X */);
+
+/* One ordered pair (i,j): LQRO:1401-1417 with the reference's operation
+ * order.  Writes the record; if reach_idx != NULL it receives the reachable
+ * point indices (k*NP+p order), if reach_pts != NULL their coordinates.
+ * Returns 0, or LQRO_E_OVERFLOW/LQRO_E_ARG. */
+int  orc_pair(int X, int H, int NP, int min_reach, double vmax_reach,
+              const double* T, const double* NCF, const double* S,
+              const double* xi, const double* xj, int i, int j,
+              lqro_pair_record* rec, int32_t* reach_idx, double* reach_pts);
+
+/* calculateNewV (LQRO:1223-1234) with linearProgram1-4 (LQRO:1001-1206),
+ * fp32 Vector3 arithmetic (V3).  planes: m x {point[3], normal[3]} floats. */
+void orc_newv(int m, const float* planes, const double* vgoal, double vmax_lp,
+              double* newv);
+
+/* Whole step (LQRO:1393-1436): rows [r0,r1), all j.  Tables are per agent
+ * (per_agent=1: T is N*H*9, NCF is N*H*3*X) or shared (per_agent=0).
+ * recs: (r1-r0)*(N-1) records or NULL.  newv: N*3 (rows r0..r1 written). */
+int  orc_step(int N, int X, int H, int NP, int min_reach, double vmax_reach,
+              double vmax_lp, int per_agent, const double* T, const double* NCF,
+              const double* S, const double* x, const double* vgoal,
+              int r0, int r1, double* newv, lqro_pair_record* recs);
+
+/* Same as orc_step, rows split over `threads` POSIX threads (private
+ * scratch per thread; the reference itself is single-threaded). */
+int  orc_step_mt(int N, int X, int H, int NP, int min_reach, double vmax_reach,
+                 double vmax_lp, int per_agent, const double* T, const double* NCF,
+                 const double* S, const double* x, const double* vgoal,
+                 int r0, int r1, double* newv, lqro_pair_record* recs, int threads);
+
+/* GJK restatement (GJK:296-501) for the path's call run_gjk (LQRO:814-853):
+ * object 1 = the single point vrel, object 2 = pts[n][3].  Returns dist^2;
+ * wpt1/wpt2 = witnesses; iters/simplex as in lqro_pair_record. */
+double orc_gjk(const double vrel[3], int n, const double* pts, double wpt1[3],
+               double wpt2[3], int* iters, int* simplex_n, int simplex[4],
+               int* backup);
+
+/* Hull branch (LQRO:867-969 + qconvex): hull of the %g-rounded points
+ * (LQRO:871-873), then min_f |n_f . (vrel - P[v_f])| over facets.  Qhull's
+ * facet order and per-facet first vertex are history-dependent artefacts of
+ * qconvex; this restatement uses the canonical facet order (sorted vertex
+ * triples) and the lowest-index vertex of each facet.
+ * Returns number of facets (<=0 on failure). */
+int  orc_hull_branch(int n, const double* pts_full, const double vrel[3],
+                     double* dist, double normal[3], int facet[3]);
+
+/* Full hull of n points (no rounding applied here): writes up to cap facets
+ * as outward-oriented index triples; returns the facet count or <0. */
+int  orc_hull(int n, const double* pts, int32_t* facets, int cap);
+
+/* %g (6 significant digits) round trip of one double: what qconvex reads
+ * back from pointList.txt (LQRO:871-873). */
+double orc_round6(double v);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
