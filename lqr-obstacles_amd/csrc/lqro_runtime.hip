@@ -1,0 +1,1548 @@
+// lqro_runtime.hip — liblqro.so: HIP kernels for gfx950 and the C-ABI of
+// include/lqro.h.
+//
+// One control step = the pair loop of LQRObstacles.cpp:1393-1436:
+//   k_pair  — one wavefront per ordered pair (i, j): sweep of the H x NP
+//             LQR-obstacle point cloud (createObstacle :770-783), reachable
+//             filter (:786-812), GJK point-in-hull / distance (:814-864,
+//             gjk.cpp:296-501), half-plane (:1208-1221).  Workgroup = one row
+//             agent i; its horizon tables live in LDS.
+//   k_hull  — inside-hull pairs (queue): in-kernel convex hull of the
+//             %g-rounded reachable points, replacing qconvex.exe + files
+//             (:867-969).
+//   k_lp    — per agent, the fp32 RVO2-3D linear program (:1001-1234).
+// k_tables builds the per-agent horizon tables once per set of gains
+// (findFG :723-732 and the two factors of createObstacle :771-773).
+//
+// Exactness: see lqro_device.hpp.  Everything on the pair path is fp64 in the
+// reference's operation order, so reachable sets, GJK results and half-planes
+// are bit-identical to the reference's CPU path (tests/test_gpu_parity.py).
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/lqro.h"
+#include "lqro_device.hpp"
+
+using namespace lqro;
+
+#define LQRO_MAXX 16
+#define PAIR_WAVES 8                 // waves per pair workgroup (one row agent)
+#define HULL_THREADS 256
+#define HULL_FMAX 8192               // face slots per hull workgroup (global scratch)
+#define HULL_VMAX 2048               // visible faces per insertion
+#define HULL_HMAX 256                // horizon edges per insertion
+
+// ---------------------------------------------------------------------------
+// Horizon tables (per agent): T_k = !(C*G_k) (3x3), NCF_k = (-C)*F_k (3xX),
+// with F_k, G_k from findFG iterated from F=I, G=0.  One workgroup per agent;
+// thread (r, c) owns entry (r, c) of the X x X recursion.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_tables(int X, int U, int H, const double* __restrict__ A,
+                                                const double* __restrict__ B,
+                                                const double* __restrict__ L,
+                                                const double* __restrict__ E, int per_agent,
+                                                double* __restrict__ Tout,
+                                                double* __restrict__ Nout, int* __restrict__ err) {
+  __shared__ double sAt[LQRO_MAXX * LQRO_MAXX], sBt[LQRO_MAXX * 3];
+  __shared__ double sF[LQRO_MAXX * LQRO_MAXX], sG[LQRO_MAXX * 3];
+  __shared__ double sFn[LQRO_MAXX * LQRO_MAXX], sGn[LQRO_MAXX * 3];
+  __shared__ double sA[LQRO_MAXX * LQRO_MAXX], sB[LQRO_MAXX * 4], sL[4 * LQRO_MAXX], sE[4 * 3];
+  const int agent = blockIdx.x;
+  const double* Li = L + (per_agent ? (size_t)agent * U * X : 0);
+  const double* Ei = E + (per_agent ? (size_t)agent * U * 3 : 0);
+  const int t = threadIdx.x;
+  for (int q = t; q < X * X; q += blockDim.x) sA[q] = A[q];
+  for (int q = t; q < X * U; q += blockDim.x) sB[q] = B[q];
+  for (int q = t; q < U * X; q += blockDim.x) sL[q] = Li[q];
+  for (int q = t; q < U * 3; q += blockDim.x) sE[q] = Ei[q];
+  __syncthreads();
+  const int r = t / X, c = t % X;
+  const bool act = t < X * X;
+  if (act) {
+    // Atilde = A + (B*L), Btilde = B*E   (LQRObstacles.cpp:725-728)
+    double bl = 0.0;
+    for (int k = 0; k < U; ++k) bl += sB[r * U + k] * sL[k * X + c];
+    sAt[r * X + c] = sA[r * X + c] + bl;
+    if (c < 3) {
+      double be = 0.0;
+      for (int k = 0; k < U; ++k) be += sB[r * U + k] * sE[k * 3 + c];
+      sBt[r * 3 + c] = be;
+    }
+    sF[r * X + c] = (r == c) ? 1.0 : 0.0;   // Ft = identity (:1401)
+    if (c < 3) sG[r * 3 + c] = 0.0;          // Gt = zeros   (:1402)
+  }
+  __syncthreads();
+  double* Ta = Tout + (size_t)agent * H * 9;
+  double* Na = Nout + (size_t)agent * H * 3 * X;
+  for (int k = 0; k < H; ++k) {
+    if (act) {
+      double f = 0.0;
+      for (int m = 0; m < X; ++m) f += sAt[r * X + m] * sF[m * X + c];
+      sFn[r * X + c] = f;
+      if (c < 3) {
+        double g = 0.0;
+        for (int m = 0; m < X; ++m) g += sAt[r * X + m] * sG[m * 3 + c];
+        sGn[r * 3 + c] = g + sBt[r * 3 + c];
+      }
+    }
+    __syncthreads();
+    if (act) {
+      sF[r * X + c] = sFn[r * X + c];
+      if (c < 3) sG[r * 3 + c] = sGn[r * 3 + c];
+    }
+    __syncthreads();
+    // NCF_k = (-C)*F_k, entries of -C are -1.0 / -0.0 (:773)
+    if (t < 3 * X) {
+      const int rr = t / X, cc = t % X;
+      double s = 0.0;
+      for (int m = 0; m < X; ++m) {
+        double nc = (m == rr) ? -1.0 : -0.0;
+        s += nc * sF[m * X + cc];
+      }
+      Na[(size_t)k * 3 * X + rr * X + cc] = s;
+    }
+    if (t == 0) {
+      // T_k = !(C*G_k)  (:771)
+      double cg[9], inv[9];
+      for (int rr = 0; rr < 3; ++rr)
+        for (int cc = 0; cc < 3; ++cc) {
+          double s = 0.0;
+          for (int m = 0; m < X; ++m) s += ((m == rr) ? 1.0 : 0.0) * sG[m * 3 + cc];
+          cg[rr * 3 + cc] = s;
+        }
+      inverse3(cg, inv);
+      for (int q = 0; q < 9; ++q) {
+        Ta[(size_t)k * 9 + q] = inv[q];
+        if (!isfinite(inv[q])) atomicOr(err, 1);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Pair kernel
+// ---------------------------------------------------------------------------
+struct PairArgs {
+  int N, X, H, NP, min_reach;
+  int row_begin, nrows, npr;        // npr = pairs per row = N-1
+  int blocks_per_row, pairs_per_block;
+  int per_agent;
+  int chunks, words;                // ceil(H*NP/64), ceil(chunks/32)
+  double r2, r2_lo, r2_hi;          // vmax_reach^2 and the fast-test bounds
+  const double* T;
+  const double* NCF;
+  const double* S;                  // NP x 3
+  const double* x;                  // N x X
+  float* planes;                    // nrows*npr x 8
+  lqro_pair_record* recs;           // nullable
+  int* hull_queue;
+  int* hull_count;
+  int hull_cap;
+  unsigned long long* stats;        // 8 counters
+  int lds_T, lds_N, lds_S, lds_wave, wave_doubles, XP;
+};
+
+struct PairLds {
+  const double* sT;    // H x 9
+  const double* sN;    // H x 3 x XP
+  const double* sS;    // 3 x NP (SoA)
+  double* tr;          // H x 3 (this wave)
+  uint32_t* mask;      // words x 64 (this wave)
+};
+
+// exact reachable test of findReachableObstacle (:799): the fast bounds
+// decide unless the point is within 1e-12 (relative) of the sphere, where the
+// reference's three divisions are evaluated literally.
+__device__ __forceinline__ bool reach_test(double a, double b, double c, const PairArgs& P) {
+  double t = a * a + b * b + c * c;
+  if (t < P.r2_lo) return true;
+  if (t > P.r2_hi) return false;
+  return (a * a) / P.r2 + (b * b) / P.r2 + (c * c) / P.r2 < 1.0;
+}
+
+// Transform*(points[p] + Translate)  (:776), accumulating from 0.0 as
+// Matrix::operator* does.
+__device__ __forceinline__ void obstacle_point(const PairLds& L, int NP, int k, int p, double& x0,
+                                               double& x1, double& x2) {
+  const double* Tk = L.sT + k * 9;
+  const double* tk = L.tr + k * 3;
+  double u0 = L.sS[p] + tk[0];
+  double u1 = L.sS[NP + p] + tk[1];
+  double u2 = L.sS[2 * NP + p] + tk[2];
+  x0 = ((0.0 + Tk[0] * u0) + Tk[1] * u1) + Tk[2] * u2;
+  x1 = ((0.0 + Tk[3] * u0) + Tk[4] * u1) + Tk[5] * u2;
+  x2 = ((0.0 + Tk[6] * u0) + Tk[7] * u1) + Tk[8] * u2;
+}
+
+// point q (k*NP + p) computed uniformly in every lane
+__device__ __forceinline__ void point_q(const PairLds& L, int NP, int q, double* pt) {
+  obstacle_point(L, NP, q / NP, q % NP, pt[0], pt[1], pt[2]);
+}
+
+// Support of the reachable set in direction d: the first (lowest index)
+// maximiser of p.d, as support_simple's strict '>' scan (gjk.cpp:770-794).
+__device__ void support_scan(const PairLds& L, const PairArgs& P, int lane, int qfirst, double d0,
+                             double d1, double d2, double& bestv, int& bestq) {
+  double bv = -INFINITY;
+  int bq = INT_MAX;
+  int k = lane / P.NP, p = lane % P.NP;
+  for (int w = 0; w < P.words; ++w) {
+    uint32_t bits = L.mask[w * kWave + lane];
+    if (__ballot(bits != 0) == 0) {
+      int adv = 32 * kWave;
+      p += adv;
+      k += p / P.NP;
+      p %= P.NP;
+      continue;
+    }
+    for (int b = 0; b < 32; ++b) {
+      if (bits & (1u << b)) {
+        double x0, x1, x2;
+        obstacle_point(L, P.NP, k, p, x0, x1, x2);
+        double v = x0 * d0 + x1 * d1 + x2 * d2;
+        if (v > bv) { bv = v; bq = (w * 32 + b) * kWave + lane; }
+      }
+      p += kWave;
+      while (p >= P.NP) { p -= P.NP; ++k; }
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    double ov = __shfl_xor(bv, off);
+    int oq = __shfl_xor(bq, off);
+    if (ov > bv || (ov == bv && oq < bq)) { bv = ov; bq = oq; }
+  }
+  // sequential semantics when the first point's value is NaN: nothing beats it
+  double f[3];
+  point_q(L, P.NP, qfirst, f);
+  double vf = f[0] * d0 + f[1] * d1 + f[2] * d2;
+  if (isnan(vf) || bq == INT_MAX) { bv = vf; bq = qfirst; }
+  bestv = bv;
+  bestq = bq;
+}
+
+// rank of reachable point q in the reachable list (= reachablePoints index)
+__device__ int reach_rank(const PairLds& L, const PairArgs& P, int lane, int q) {
+  int mt = q / kWave, lt = q % kWave;
+  int cnt = 0;
+  for (int w = 0; w < P.words; ++w) {
+    uint32_t bits = L.mask[w * kWave + lane];
+    int lo = w * 32;
+    if (lo + 32 <= mt) cnt += __popc(bits);
+    else if (lo <= mt) {
+      int nb = mt - lo;               // chunks before mt in this word
+      uint32_t below = nb >= 32 ? bits : (bits & ((1u << nb) - 1u));
+      cnt += __popc(below);
+      if (lane < lt && ((bits >> nb) & 1u)) cnt += 1;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
+  return cnt;
+}
+
+// --- GJK (gjk.cpp), run uniformly by every lane of the wave -----------------
+__constant__ int g_card[16] = {0, 1, 1, 2, 1, 2, 2, 3, 1, 2, 2, 3, 2, 3, 3, 4};
+__constant__ int g_maxe[16] = {-1, 0, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 3, 3, 3, 3};
+__constant__ int g_elts[16][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {1, 0, 0, 0}, {0, 1, 0, 0},
+                                  {2, 0, 0, 0}, {0, 2, 0, 0}, {1, 2, 0, 0}, {0, 1, 2, 0},
+                                  {3, 0, 0, 0}, {0, 3, 0, 0}, {1, 3, 0, 0}, {0, 1, 3, 0},
+                                  {2, 3, 0, 0}, {0, 2, 3, 0}, {1, 2, 3, 0}, {0, 1, 2, 3}};
+__constant__ int g_nonelts[16][4] = {{0, 1, 2, 3}, {1, 2, 3, 0}, {0, 2, 3, 0}, {2, 3, 0, 0},
+                                     {0, 1, 3, 0}, {1, 3, 0, 0}, {0, 3, 0, 0}, {3, 0, 0, 0},
+                                     {0, 1, 2, 0}, {1, 2, 0, 0}, {0, 2, 0, 0}, {2, 0, 0, 0},
+                                     {0, 1, 0, 0}, {1, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+__constant__ int g_pred[16][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {2, 1, 0, 0},
+                                  {0, 0, 0, 0}, {4, 1, 0, 0}, {4, 2, 0, 0}, {6, 5, 3, 0},
+                                  {0, 0, 0, 0}, {8, 1, 0, 0}, {8, 2, 0, 0}, {10, 9, 3, 0},
+                                  {8, 4, 0, 0}, {12, 9, 5, 0}, {12, 10, 6, 0}, {14, 13, 11, 7}};
+__constant__ int g_succ[16][4] = {{1, 2, 4, 8}, {3, 5, 9, 0}, {3, 6, 10, 0}, {7, 11, 0, 0},
+                                  {5, 6, 12, 0}, {7, 13, 0, 0}, {7, 14, 0, 0}, {15, 0, 0, 0},
+                                  {9, 10, 12, 0}, {11, 13, 0, 0}, {11, 14, 0, 0}, {15, 0, 0, 0},
+                                  {13, 14, 0, 0}, {15, 0, 0, 0}, {15, 0, 0, 0}, {0, 0, 0, 0}};
+
+struct GjkState {
+  int npts;
+  int s2[4];          // point ids (q) of the hull-side simplex vertices
+  double lambdas[4];
+  double c1[4][3], c2[4][3];
+  double dv[16][4];
+  double dp[4][4];
+  double dsum[16];
+};
+
+__device__ void gjk_subterms(GjkState& g) {
+  const int size = g.npts;
+  double csp[4][3];
+  for (int i = 0; i < size; i++)
+    for (int j = 0; j < 3; j++) csp[i][j] = g.c1[i][j] - g.c2[i][j];
+  for (int i = 0; i < size; i++)
+    for (int j = i; j < size; j++)
+      g.dp[i][j] = g.dp[j][i] = csp[i][0] * csp[j][0] + csp[i][1] * csp[j][1] + csp[i][2] * csp[j][2];
+  for (int s = 1; s < 16 && g_maxe[s] < size; s++) {
+    if (g_card[s] <= 1) { g.dv[s][g_elts[s][0]] = 1.0; continue; }
+    if (g_card[s] == 2) {
+      int e0 = g_elts[s][0], e1 = g_elts[s][1];
+      g.dv[s][e0] = g.dp[e1][e1] - g.dp[e1][e0];
+      g.dv[s][e1] = g.dp[e0][e0] - g.dp[e0][e1];
+      continue;
+    }
+    for (int j = 0; j < g_card[s]; j++) {
+      int jelt = g_elts[s][j], jsub = g_pred[s][j];
+      double sum = 0;
+      for (int i = 0; i < g_card[jsub]; i++) {
+        int ielt = g_elts[jsub][i];
+        sum += g.dv[jsub][ielt] * (g.dp[ielt][g_elts[jsub][0]] - g.dp[ielt][jelt]);
+      }
+      g.dv[s][jelt] = sum;
+    }
+  }
+}
+
+__device__ void gjk_reset(GjkState& g, int subset) {
+  for (int j = 0; j < g_card[subset]; j++) {
+    int oldpos = g_elts[subset][j];
+    if (oldpos != j) {
+      g.s2[j] = g.s2[oldpos];
+      for (int i = 0; i < 3; i++) { g.c1[j][i] = g.c1[oldpos][i]; g.c2[j][i] = g.c2[oldpos][i]; }
+    }
+    g.lambdas[j] = g.dv[subset][g_elts[subset][j]] / g.dsum[subset];
+  }
+  g.npts = g_card[subset];
+}
+
+__device__ int gjk_default(GjkState& g) {
+  int s, ok = 0, size = g.npts;
+  for (s = 1; s < 16 && g_maxe[s] < size; s++) {
+    g.dsum[s] = 0.0; ok = 1;
+    for (int j = 0; ok && j < g_card[s]; j++) {
+      if (g.dv[s][g_elts[s][j]] > 0.0) g.dsum[s] += g.dv[s][g_elts[s][j]];
+      else ok = 0;
+    }
+    for (int k = 0; ok && k < size - g_card[s]; k++)
+      if (g.dv[g_succ[s][k]][g_nonelts[s][k]] > 0) ok = 0;
+    if (ok && g.dsum[s] >= 1.0e-20) break;
+  }
+  if (ok) { gjk_reset(g, s); return 1; }
+  return 0;
+}
+
+__device__ void gjk_backup(GjkState& g) {
+  int size = g.npts, bests = 0;
+  double num[16], den[16];
+  for (int s = 1; s < 16 && g_maxe[s] < size; s++) {
+    if (g.dsum[s] <= 0.0) continue;
+    int i;
+    for (i = 0; i < g_card[s]; i++)
+      if (g.dv[s][g_elts[s][i]] <= 0.0) break;
+    if (i < g_card[s]) continue;
+    num[s] = 0.0;
+    for (int j = 0; j < g_card[s]; j++)
+      for (int k = 0; k < g_card[s]; k++)
+        num[s] += (g.dv[s][g_elts[s][j]] * g.dv[s][g_elts[s][k]]) * g.dp[g_elts[s][j]][g_elts[s][k]];
+    den[s] = g.dsum[s] * g.dsum[s];
+    if ((bests < 1) || (num[s] * den[bests] < num[bests] * den[s])) bests = s;
+  }
+  gjk_reset(g, bests);
+}
+
+__device__ __forceinline__ void gjk_point(double* pt, int len, const double (*v)[3], const double* lam) {
+  for (int d = 0; d < 3; d++) {
+    pt[d] = 0;
+    for (int i = 0; i < len; i++) pt[d] += v[i][d] * lam[i];
+  }
+}
+
+struct GjkOut {
+  double sqrd, w1[3], w2[3];
+  int iters, backup;
+};
+
+// gjk_distance (gjk.cpp:296-501) for object 1 = {vrel}, object 2 = the
+// reachable points (support by support_scan).
+__device__ void gjk_run(const PairLds& L, const PairArgs& P, int lane, int qfirst, int n,
+                        const double* vrel, GjkState& g, GjkOut& o) {
+  for (int s = 0; s < 16; ++s) {
+    g.dsum[s] = 0.0;
+    for (int k = 0; k < 4; ++k) g.dv[s][k] = 0.0;
+  }
+  int use_default = 1, first_iteration = 1, max_iterations = n;
+  double oldsqrd = 0.0, sqrd = 0.0;
+  double disp[3], rdisp[3];
+  o.iters = 0; o.backup = 0;
+  g.npts = 1; g.s2[0] = qfirst; g.lambdas[0] = 1.0;
+  {
+    double f[3];
+    point_q(L, P.NP, qfirst, f);
+    for (int d = 0; d < 3; d++) { g.c1[0][d] = vrel[d]; g.c2[0][d] = f[d]; }
+  }
+  while (max_iterations-- > 0) {
+    if (g.npts == 1) g.lambdas[0] = 1.0;
+    else {
+      gjk_subterms(g);
+      if (use_default) use_default = gjk_default(g);
+      if (!use_default) { gjk_backup(g); o.backup = 1; }
+    }
+    gjk_point(o.w1, g.npts, g.c1, g.lambdas);
+    gjk_point(o.w2, g.npts, g.c2, g.lambdas);
+    for (int d = 0; d < 3; d++) { disp[d] = o.w2[d] - o.w1[d]; rdisp[d] = -disp[d]; }
+    sqrd = disp[0] * disp[0] + disp[1] * disp[1] + disp[2] * disp[2];
+    if (sqrd < 1.0e-8) { o.sqrd = sqrd; return; }
+    double maxv = vrel[0] * disp[0] + vrel[1] * disp[1] + vrel[2] * disp[2];
+    double minus_minv;
+    int minq;
+    support_scan(L, P, lane, qfirst, rdisp[0], rdisp[1], rdisp[2], minus_minv, minq);
+    o.iters++;
+    double g_val = sqrd + maxv + minus_minv;
+    if (g_val < 0.0) g_val = 0;
+    if (g_val < 1.0e-8) { o.sqrd = sqrd; return; }
+    if ((first_iteration || (sqrd < oldsqrd)) && (g.npts <= 3)) {
+      double f[3];
+      point_q(L, P.NP, minq, f);
+      int np_ = g.npts;
+      g.s2[np_] = minq;
+      g.lambdas[np_] = 0.0;
+      for (int d = 0; d < 3; d++) { g.c1[np_][d] = vrel[d]; g.c2[np_][d] = f[d]; }
+      g.npts++;
+      oldsqrd = sqrd;
+      first_iteration = 0;
+      use_default = 1;
+      continue;
+    }
+    if (use_default) use_default = 0;
+    else { o.sqrd = sqrd; return; }
+  }
+  o.sqrd = 0.0;
+}
+
+template <int XT>
+__global__ void __launch_bounds__(PAIR_WAVES * 64) k_pair(PairArgs P) {
+  extern __shared__ double lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int lrow = blockIdx.x / P.blocks_per_row;
+  const int chunk = blockIdx.x % P.blocks_per_row;
+  const int i = P.row_begin + lrow;
+  constexpr int X = XT;
+  const int H = P.H, NP = P.NP, XP = P.XP;
+
+  // stage agent i's horizon tables and the sphere into LDS
+  const double* Ti = P.T + (P.per_agent ? (size_t)i * H * 9 : 0);
+  const double* Ni = P.NCF + (P.per_agent ? (size_t)i * H * 3 * X : 0);
+  double* sT = lds + P.lds_T;
+  double* sN = lds + P.lds_N;
+  double* sS = lds + P.lds_S;
+  for (int q = threadIdx.x; q < H * 9; q += blockDim.x) sT[q] = Ti[q];
+  for (int q = threadIdx.x; q < H * 3 * X; q += blockDim.x) {
+    int kr = q / X, c = q % X;
+    sN[kr * XP + c] = Ni[q];
+  }
+  for (int q = threadIdx.x; q < NP * 3; q += blockDim.x) {
+    int p = q / 3, d = q % 3;
+    sS[d * NP + p] = P.S[q];
+  }
+  __syncthreads();
+
+  PairLds L;
+  L.sT = sT; L.sN = sN; L.sS = sS;
+  L.tr = lds + P.lds_wave + (size_t)wave * P.wave_doubles;
+  L.mask = reinterpret_cast<uint32_t*>(L.tr + 3 * H);
+
+  const double* xi = P.x + (size_t)i * X;
+  const int jj_begin = chunk * P.pairs_per_block;
+  const int jj_end = min(P.npr, jj_begin + P.pairs_per_block);
+  unsigned long long st_reach = 0, st_iters = 0, st_planes = 0, st_inside = 0, st_backup = 0;
+
+  for (int jj = jj_begin + wave; jj < jj_end; jj += PAIR_WAVES) {
+    const int j = jj < i ? jj : jj + 1;
+    const double* xj = P.x + (size_t)j * X;
+    double d[X];
+#pragma unroll
+    for (int c = 0; c < X; ++c) d[c] = xi[c] - xj[c];                        // (xInit1-xInit2)
+    const double vrel[3] = {xi[3] - xj[3], xi[4] - xj[4], xi[5] - xj[5]};     // :794-796
+
+    // Translate_k = NCF_k * d for every k (:773): item (k, r) per lane
+    for (int it = lane; it < 3 * H; it += kWave) {
+      const double* row = sN + (size_t)it * XP;
+      double s = 0.0;
+#pragma unroll
+      for (int c = 0; c < X; ++c) s += row[c] * d[c];
+      L.tr[it] = s;
+    }
+    wave_lds_sync();
+
+    // sweep + reachable filter; bit m of lane l <=> point q = 64 m + l
+    int n = 0, qfirst = INT_MAX;
+    uint64_t hsh = 0;
+    {
+      int k = lane / NP, p = lane % NP;
+      for (int w = 0; w < P.words; ++w) {
+        uint32_t bits = 0;
+        for (int b = 0; b < 32; ++b) {
+          const int m = w * 32 + b;
+          if (m >= P.chunks) break;
+          const int q = m * kWave + lane;
+          bool ok = false;
+          if (q < H * NP) {
+            double x0, x1, x2;
+            obstacle_point(L, NP, k, p, x0, x1, x2);
+            ok = reach_test(x0 - vrel[0], x1 - vrel[1], x2 - vrel[2], P);
+          }
+          if (ok) { bits |= 1u << b; hsh += mix64((uint64_t)q); }
+          const unsigned long long bal = __ballot(ok);
+          if (bal) {
+            n += __popcll(bal);
+            if (qfirst == INT_MAX) qfirst = m * kWave + __ffsll((long long)bal) - 1;
+          }
+          p += kWave;
+          while (p >= NP) { p -= NP; ++k; }
+        }
+        L.mask[w * kWave + lane] = bits;
+      }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) hsh += __shfl_xor(hsh, off);
+    wave_lds_sync();
+    st_reach += n;
+
+    lqro_pair_record rec;
+    const bool want_rec = P.recs != nullptr;
+    int flags = 0;
+    float pl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    double dist = 0.0, nrm[3] = {0, 0, 0};
+    GjkOut go;
+    go.iters = 0; go.backup = 0; go.sqrd = 0;
+    for (int q = 0; q < 3; ++q) { go.w1[q] = 0; go.w2[q] = 0; }
+    GjkState g;
+    g.npts = 0;
+    bool inside = false;
+    if (n > P.min_reach) {                                   // :1409
+      gjk_run(L, P, lane, qfirst, n, vrel, g, go);
+      double distance = sqrt(go.sqrd);                         // :843
+      nrm[0] = (go.w1[0] - go.w2[0]) / distance;               // :850-852
+      nrm[1] = (go.w1[1] - go.w2[1]) / distance;
+      nrm[2] = (go.w1[2] - go.w2[2]) / distance;
+      inside = (distance < 0.0001 && distance > -1 * 0.0001); // :860
+      flags = LQRO_REC_PLANE | (inside ? LQRO_REC_INSIDE : 0) | (go.backup ? LQRO_REC_BACKUP : 0);
+      st_iters += go.iters;
+      st_backup += go.backup;
+      dist = distance;
+      if (!inside) {
+        st_planes += 1;
+        distance *= 0.5;                                       // :1416
+        const double mult = -1.0;                              // :1215
+        pl[0] = (float)(xi[3] + mult * distance * nrm[0]);     // :1217
+        pl[1] = (float)(xi[4] + mult * distance * nrm[1]);
+        pl[2] = (float)(xi[5] + mult * distance * nrm[2]);
+        pl[3] = (float)nrm[0]; pl[4] = (float)nrm[1]; pl[5] = (float)nrm[2];
+        pl[6] = __int_as_float(1);
+      } else {
+        st_inside += 1;
+        pl[6] = __int_as_float(2);                             // filled in by k_hull
+      }
+    }
+    const size_t slot = (size_t)lrow * P.npr + jj;
+    int sranks[4] = {-1, -1, -1, -1};
+    if (want_rec && g.npts > 0)
+      for (int s = 0; s < 4; ++s)
+        if (s < g.npts) sranks[s] = reach_rank(L, P, lane, g.s2[s]);
+    if (lane == 0) {
+      float4* dst = reinterpret_cast<float4*>(P.planes + slot * 8);
+      dst[0] = make_float4(pl[0], pl[1], pl[2], pl[3]);
+      dst[1] = make_float4(pl[4], pl[5], pl[6], pl[7]);
+      if (inside) {
+        int qi = atomicAdd(P.hull_count, 1);
+        if (qi < P.hull_cap) P.hull_queue[qi] = (int)slot;
+      }
+      if (want_rec) {
+        rec.i = i; rec.j = j; rec.n_reach = n; rec.flags = flags;
+        rec.gjk_iters = go.iters; rec.simplex_n = g.npts;
+        for (int s = 0; s < 4; ++s) rec.simplex[s] = sranks[s];
+        rec.facet[0] = rec.facet[1] = rec.facet[2] = -1;
+        rec.n_facets = 0;
+        rec.reach_hash = hsh;
+        rec.dist = dist;
+        for (int q = 0; q < 3; ++q) {
+          rec.normal[q] = nrm[q];
+          rec.wpt_vrel[q] = go.w1[q];
+          rec.wpt_hull[q] = go.w2[q];
+          rec.plane_point[q] = pl[q];
+          rec.plane_normal[q] = pl[3 + q];
+        }
+        P.recs[slot] = rec;
+      }
+    }
+    wave_lds_sync();
+  }
+  if (lane == 0) {
+    atomicAdd(&P.stats[1], st_planes);
+    atomicAdd(&P.stats[2], st_inside);
+    atomicAdd(&P.stats[5], st_backup);
+    atomicAdd(&P.stats[6], st_reach);
+    atomicAdd(&P.stats[7], st_iters);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Hull kernel: one workgroup per inside-hull pair (persistent over the queue)
+// ---------------------------------------------------------------------------
+struct HullArgs {
+  int N, X, H, NP;
+  int row_begin, npr, per_agent;
+  double r2, r2_lo, r2_hi;
+  const double* T;
+  const double* NCF;
+  const double* S;
+  const double* x;
+  float* planes;
+  lqro_pair_record* recs;
+  const int* queue;
+  const int* count;
+  int cap;
+  int* next;
+  double* scratch;                  // per block: H*NP*6 doubles (rounded, full)
+  int* iscratch;                    // per block: H*NP ints (conflict face)
+  float* fscratch;                  // per block: H*NP floats (conflict distance)
+  void* faces;                      // per block: HULL_FMAX HFace + HULL_FMAX free-list ints
+  unsigned long long* stats;
+};
+
+struct HFace {
+  int v[3];
+  int adj[3];    // adj[e] = face across edge (v[e], v[e+1])
+  double n[3];
+  int alive;
+};
+
+__device__ __forceinline__ double hface_dist(const HFace& f, const double* P, int p) {
+  const double* a = P + 3 * f.v[0];
+  const double* q = P + 3 * p;
+  return f.n[0] * (q[0] - a[0]) + f.n[1] * (q[1] - a[1]) + f.n[2] * (q[2] - a[2]);
+}
+__device__ __forceinline__ void hface_plane(HFace& f, const double* P) {
+  const double *a = P + 3 * f.v[0], *b = P + 3 * f.v[1], *c = P + 3 * f.v[2];
+  double e1[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+  double e2[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
+  f.n[0] = e1[1] * e2[2] - e1[2] * e2[1];
+  f.n[1] = e1[2] * e2[0] - e1[0] * e2[2];
+  f.n[2] = e1[0] * e2[1] - e1[1] * e2[0];
+}
+
+// block-wide argmax of (key, idx) with lowest idx on ties
+__device__ void block_argmax(double& key, int& idx, double* sk, int* si) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    double ok = __shfl_xor(key, off);
+    int oi = __shfl_xor(idx, off);
+    if (ok > key || (ok == key && oi < idx)) { key = ok; idx = oi; }
+  }
+  if (lane == 0) { sk[wave] = key; si[wave] = idx; }
+  __syncthreads();
+  key = sk[0]; idx = si[0];
+  for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
+    if (sk[w] > key || (sk[w] == key && si[w] < idx)) { key = sk[w]; idx = si[w]; }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(HULL_THREADS) k_hull(HullArgs A) {
+  __shared__ unsigned char vis[HULL_FMAX];
+  __shared__ int s_job, s_n, s_nf, s_fail, s_apex, s_nvis, s_nh, s_nnew;
+  __shared__ int s_nfree;
+  __shared__ int s_vis[HULL_VMAX];
+  __shared__ int h_a[HULL_HMAX], h_b[HULL_HMAX], h_out[HULL_HMAX], h_new[HULL_HMAX];
+  __shared__ double sk[HULL_THREADS / 64];
+  __shared__ int si[HULL_THREADS / 64];
+  __shared__ int s_scan[HULL_THREADS];
+  __shared__ double s_tr[3 * 256];
+  __shared__ int s_init[4];
+  __shared__ double s_eps;
+
+  const int tid = threadIdx.x;
+  const int HNP = A.H * A.NP;
+  double* Pr = A.scratch + (size_t)blockIdx.x * HNP * 6;    // rounded points
+  double* Pf = Pr + (size_t)HNP * 3;                         // full-precision points
+  int* conf = A.iscratch + (size_t)blockIdx.x * HNP;
+  float* cd = A.fscratch + (size_t)blockIdx.x * HNP;
+  HFace* F = reinterpret_cast<HFace*>(A.faces) + (size_t)blockIdx.x * HULL_FMAX;
+  int* s_free = reinterpret_cast<int*>(reinterpret_cast<HFace*>(A.faces) + (size_t)gridDim.x * HULL_FMAX) +
+               (size_t)blockIdx.x * HULL_FMAX;
+
+  for (;;) {
+    if (tid == 0) s_job = atomicAdd(A.next, 1);
+    __syncthreads();
+    const int job = s_job;
+    __syncthreads();
+    if (job >= min(*A.count, A.cap)) break;
+    const int slot = A.queue[job];
+    const int lrow = slot / A.npr, jj = slot % A.npr;
+    const int i = A.row_begin + lrow;
+    const int j = jj < i ? jj : jj + 1;
+    const double* xi = A.x + (size_t)i * A.X;
+    const double* xj = A.x + (size_t)j * A.X;
+    const double* Ti = A.T + (A.per_agent ? (size_t)i * A.H * 9 : 0);
+    const double* Ni = A.NCF + (A.per_agent ? (size_t)i * A.H * 3 * A.X : 0);
+    const double vrel[3] = {xi[3] - xj[3], xi[4] - xj[4], xi[5] - xj[5]};
+
+    // 1. reachable points in reference order (compacted), full + %g-rounded
+    if (tid == 0) { s_n = 0; s_fail = 0; }
+    __syncthreads();
+    for (int k0 = 0; k0 < A.H; k0 += 256) {
+      for (int it = tid; it < 3 * 256; it += blockDim.x) {
+        int k = k0 + it / 3, r = it % 3;
+        if (k < A.H) {
+          double d = 0.0;
+          for (int c = 0; c < A.X; ++c) d += Ni[((size_t)k * 3 + r) * A.X + c] * (xi[c] - xj[c]);
+          s_tr[it] = d;
+        }
+      }
+      __syncthreads();
+      const int kend = min(A.H, k0 + 256);
+      for (int q0 = k0 * A.NP; q0 < kend * A.NP; q0 += blockDim.x) {
+        const int q = q0 + tid;
+        bool ok = false;
+        double p0 = 0, p1 = 0, p2 = 0;
+        if (q < kend * A.NP) {
+          const int k = q / A.NP, p = q % A.NP;
+          const double* Tk = Ti + (size_t)k * 9;
+          const double* tk = s_tr + (k - k0) * 3;
+          double u0 = A.S[3 * p] + tk[0], u1 = A.S[3 * p + 1] + tk[1], u2 = A.S[3 * p + 2] + tk[2];
+          p0 = ((0.0 + Tk[0] * u0) + Tk[1] * u1) + Tk[2] * u2;
+          p1 = ((0.0 + Tk[3] * u0) + Tk[4] * u1) + Tk[5] * u2;
+          p2 = ((0.0 + Tk[6] * u0) + Tk[7] * u1) + Tk[8] * u2;
+          double a = p0 - vrel[0], b = p1 - vrel[1], c = p2 - vrel[2];
+          double t = a * a + b * b + c * c;
+          if (t < A.r2_lo) ok = true;
+          else if (t > A.r2_hi) ok = false;
+          else ok = (a * a) / A.r2 + (b * b) / A.r2 + (c * c) / A.r2 < 1.0;
+        }
+        // block exclusive scan of ok
+        s_scan[tid] = ok ? 1 : 0;
+        __syncthreads();
+        for (int off = 1; off < (int)blockDim.x; off <<= 1) {
+          int v = tid >= off ? s_scan[tid - off] : 0;
+          __syncthreads();
+          s_scan[tid] += v;
+          __syncthreads();
+        }
+        const int base = s_n;
+        const int pos = base + s_scan[tid] - (ok ? 1 : 0);
+        if (ok) {
+          int oor = 0;
+          Pf[3 * pos] = p0; Pf[3 * pos + 1] = p1; Pf[3 * pos + 2] = p2;
+          Pr[3 * pos] = round6(p0, &oor);
+          Pr[3 * pos + 1] = round6(p1, &oor);
+          Pr[3 * pos + 2] = round6(p2, &oor);
+          if (oor) s_fail = 1;
+        }
+        __syncthreads();
+        if (tid == blockDim.x - 1) s_n = base + s_scan[tid];
+        __syncthreads();
+      }
+    }
+    const int n = s_n;
+
+    // 2. scale-aware coplanarity tolerance (as the oracle's hull)
+    {
+      double mx = 0.0;
+      for (int q = tid; q < 3 * n; q += blockDim.x) mx = fmax(mx, fabs(Pr[q]));
+      int dummy = tid;
+      block_argmax(mx, dummy, sk, si);
+      if (tid == 0) s_eps = 1e-13 * (mx + 1.0);
+      __syncthreads();
+    }
+    const double eps = s_eps;
+
+    // 3. initial tetrahedron (extreme points)
+    if (n < 4) { if (tid == 0) s_fail = 1; }
+    __syncthreads();
+    if (!s_fail) {
+      double key; int idx;
+      // i0: min x
+      key = -INFINITY; idx = INT_MAX;
+      for (int q = tid; q < n; q += blockDim.x) {
+        double v = -Pr[3 * q];
+        if (v > key || (v == key && q < idx)) { key = v; idx = q; }
+      }
+      block_argmax(key, idx, sk, si);
+      const int i0 = idx;
+      key = -INFINITY; idx = INT_MAX;
+      for (int q = tid; q < n; q += blockDim.x) {
+        double dx = Pr[3 * q] - Pr[3 * i0], dy = Pr[3 * q + 1] - Pr[3 * i0 + 1], dz = Pr[3 * q + 2] - Pr[3 * i0 + 2];
+        double v = dx * dx + dy * dy + dz * dz;
+        if (v > key || (v == key && q < idx)) { key = v; idx = q; }
+      }
+      block_argmax(key, idx, sk, si);
+      const int i1 = idx;
+      key = -INFINITY; idx = INT_MAX;
+      for (int q = tid; q < n; q += blockDim.x) {
+        double e1[3] = {Pr[3 * i1] - Pr[3 * i0], Pr[3 * i1 + 1] - Pr[3 * i0 + 1], Pr[3 * i1 + 2] - Pr[3 * i0 + 2]};
+        double e2[3] = {Pr[3 * q] - Pr[3 * i0], Pr[3 * q + 1] - Pr[3 * i0 + 1], Pr[3 * q + 2] - Pr[3 * i0 + 2]};
+        double cx = e1[1] * e2[2] - e1[2] * e2[1], cy = e1[2] * e2[0] - e1[0] * e2[2], cz = e1[0] * e2[1] - e1[1] * e2[0];
+        double v = cx * cx + cy * cy + cz * cz;
+        if (v > key || (v == key && q < idx)) { key = v; idx = q; }
+      }
+      block_argmax(key, idx, sk, si);
+      const int i2 = idx;
+      HFace tf;
+      tf.v[0] = i0; tf.v[1] = i1; tf.v[2] = i2;
+      hface_plane(tf, Pr);
+      const double nn = sqrt(tf.n[0] * tf.n[0] + tf.n[1] * tf.n[1] + tf.n[2] * tf.n[2]);
+      key = -INFINITY; idx = INT_MAX;
+      for (int q = tid; q < n; q += blockDim.x) {
+        double v = fabs(hface_dist(tf, Pr, q)) / nn;
+        if (v > key || (v == key && q < idx)) { key = v; idx = q; }
+      }
+      block_argmax(key, idx, sk, si);
+      const int i3 = idx;
+      if (tid == 0) {
+        if (!(key > eps) || i0 == i1 || i1 == i2 || i2 == i3) s_fail = 1;
+        s_init[0] = i0; s_init[1] = i1; s_init[2] = i2; s_init[3] = i3;
+      }
+      __syncthreads();
+    }
+    if (!s_fail && tid == 0) {
+      const int tet[4] = {s_init[0], s_init[1], s_init[2], s_init[3]};
+      const int fv[4][3] = {{0, 1, 2}, {0, 3, 1}, {1, 3, 2}, {0, 2, 3}};
+      for (int f = 0; f < 4; ++f) {
+        HFace h;
+        h.v[0] = tet[fv[f][0]]; h.v[1] = tet[fv[f][1]]; h.v[2] = tet[fv[f][2]];
+        hface_plane(h, Pr);
+        const int other = tet[6 - fv[f][0] - fv[f][1] - fv[f][2]];
+        if (hface_dist(h, Pr, other) > 0) {
+          int t = h.v[1]; h.v[1] = h.v[2]; h.v[2] = t;
+          hface_plane(h, Pr);
+        }
+        h.alive = 1;
+        F[f] = h;
+      }
+      // adjacency by matching reversed edges
+      for (int f = 0; f < 4; ++f)
+        for (int e = 0; e < 3; ++e) {
+          int a = F[f].v[e], b = F[f].v[(e + 1) % 3];
+          F[f].adj[e] = -1;
+          for (int g = 0; g < 4; ++g)
+            for (int e2 = 0; e2 < 3; ++e2)
+              if (F[g].v[e2] == b && F[g].v[(e2 + 1) % 3] == a) F[f].adj[e] = g;
+        }
+      s_nf = 4;
+      s_nfree = 0;
+    }
+    __syncthreads();
+    if (!s_fail) {
+      // 4. initial conflict assignment
+      for (int q = tid; q < n; q += blockDim.x) {
+        int c = -1; double dd = 0.0;
+        if (q != s_init[0] && q != s_init[1] && q != s_init[2] && q != s_init[3]) {
+          for (int f = 0; f < 4; ++f) {
+            const double nl = sqrt(F[f].n[0] * F[f].n[0] + F[f].n[1] * F[f].n[1] + F[f].n[2] * F[f].n[2]);
+            const double dist = hface_dist(F[f], Pr, q);
+            if (dist > eps * nl) { c = f; dd = dist / nl; break; }
+          }
+        }
+        conf[q] = c;
+        cd[q] = (float)dd;
+      }
+      __syncthreads();
+      // 5. quickhull iterations
+      for (int iter = 0; iter < 100000; ++iter) {
+        double key = -INFINITY; int idx = INT_MAX;
+        for (int q = tid; q < n; q += blockDim.x) {
+          if (conf[q] >= 0) {
+            double v = (double)cd[q];
+            if (v > key || (v == key && q < idx)) { key = v; idx = q; }
+          }
+        }
+        block_argmax(key, idx, sk, si);
+        if (idx == INT_MAX) break;
+        const int apex = idx;
+        // visible region: BFS from the apex's conflict face (thread 0)
+        for (int f = tid; f < s_nf; f += blockDim.x) vis[f] = 0;
+        __syncthreads();
+        if (tid == 0) {
+          s_apex = apex;
+          int nv = 0, nh = 0;
+          const int f0 = conf[apex];
+          vis[f0] = 1; s_vis[nv++] = f0;
+          for (int h = 0; h < nv; ++h) {
+            const HFace& fh = F[s_vis[h]];
+            for (int e = 0; e < 3; ++e) {
+              const int nb = fh.adj[e];
+              if (nb < 0) { s_fail = 1; continue; }
+              if (vis[nb]) continue;
+              const double nl = sqrt(F[nb].n[0] * F[nb].n[0] + F[nb].n[1] * F[nb].n[1] + F[nb].n[2] * F[nb].n[2]);
+              if (hface_dist(F[nb], Pr, apex) > eps * nl) {
+                vis[nb] = 1;
+                if (nv < HULL_VMAX) s_vis[nv++] = nb; else s_fail = 1;
+              }
+            }
+          }
+          // horizon
+          for (int h = 0; h < nv; ++h) {
+            const HFace& fh = F[s_vis[h]];
+            for (int e = 0; e < 3; ++e) {
+              const int nb = fh.adj[e];
+              if (nb >= 0 && !vis[nb]) {
+                if (nh < HULL_HMAX) { h_a[nh] = fh.v[e]; h_b[nh] = fh.v[(e + 1) % 3]; h_out[nh] = nb; nh++; }
+                else s_fail = 1;
+              }
+            }
+          }
+          // retire the visible faces, make the cone (a slot retired in this
+          // round is reused only from the next round on, after the
+          // reassignment below has seen it dead)
+          for (int h = 0; h < nv; ++h) F[s_vis[h]].alive = 0;
+          for (int h = 0; h < nh && !s_fail; ++h) {
+            int slotf;
+            if (s_nfree > 0) slotf = s_free[--s_nfree];
+            else if (s_nf < HULL_FMAX) slotf = s_nf++;
+            else { s_fail = 1; break; }
+            h_new[h] = slotf;
+            HFace nf;
+            nf.v[0] = h_a[h]; nf.v[1] = h_b[h]; nf.v[2] = apex;
+            nf.alive = 1;
+            nf.adj[0] = h_out[h];
+            nf.adj[1] = -1; nf.adj[2] = -1;
+            hface_plane(nf, Pr);
+            F[slotf] = nf;
+            vis[slotf] = 0;
+            // outer neighbour: its edge (b, a) now faces the new face
+            HFace& on = F[h_out[h]];
+            for (int e = 0; e < 3; ++e)
+              if (on.v[e] == h_b[h] && on.v[(e + 1) % 3] == h_a[h]) on.adj[e] = slotf;
+          }
+          if (!s_fail)
+            for (int h = 0; h < nh; ++h) {
+              // edge (b, apex) <-> face whose horizon edge starts at b
+              // edge (apex, a) <-> face whose horizon edge ends at a
+              for (int g = 0; g < nh; ++g) {
+                if (h_a[g] == h_b[h]) F[h_new[h]].adj[1] = h_new[g];
+                if (h_b[g] == h_a[h]) F[h_new[h]].adj[2] = h_new[g];
+              }
+              if (F[h_new[h]].adj[1] < 0 || F[h_new[h]].adj[2] < 0) s_fail = 1;
+            }
+          for (int h = 0; h < nv; ++h) s_free[s_nfree++] = s_vis[h];
+          s_nvis = nv;
+          s_nh = nh;
+        }
+        __syncthreads();
+        if (s_fail) break;
+        // reassign the conflict points of the visible faces
+        const int nh = s_nh;
+        for (int q = tid; q < n; q += blockDim.x) {
+          const int c = conf[q];
+          if (c < 0) continue;
+          if (q == apex) { conf[q] = -1; continue; }
+          if (F[c].alive) continue;          // c was visible (freed) this round
+          int nc = -1; double dd = 0.0;
+          for (int h = 0; h < nh; ++h) {
+            const HFace& f = F[h_new[h]];
+            const double nl = sqrt(f.n[0] * f.n[0] + f.n[1] * f.n[1] + f.n[2] * f.n[2]);
+            const double dist = hface_dist(f, Pr, q);
+            if (dist > eps * nl) { nc = h_new[h]; dd = dist / nl; break; }
+          }
+          conf[q] = nc;
+          cd[q] = (float)dd;
+        }
+        __syncthreads();
+      }
+    }
+    __syncthreads();
+
+    // 6. arg-min facet (LQRObstacles.cpp:955-968) in canonical facet order:
+    //    normal from the rounded vertices (lowest index first), distance from
+    //    the full-precision lowest-index vertex.
+    double best = INFINITY;
+    int bt0 = INT_MAX, bt1 = INT_MAX, bt2 = INT_MAX;
+    double bn[3] = {0, 0, 0};
+    int nfac = 0;
+    if (!s_fail) {
+      for (int f = tid; f < s_nf; f += blockDim.x) {
+        if (!F[f].alive) continue;
+        nfac++;
+        int t0 = F[f].v[0], t1 = F[f].v[1], t2 = F[f].v[2];
+        while (!(t0 < t1 && t0 < t2)) { int a = t0; t0 = t1; t1 = t2; t2 = a; }
+        const double *a = Pr + 3 * t0, *b = Pr + 3 * t1, *c = Pr + 3 * t2;
+        double e1[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+        double e2[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
+        double nv[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+        double len = sqrt(nv[0] * nv[0] + nv[1] * nv[1] + nv[2] * nv[2]);
+        nv[0] /= len; nv[1] /= len; nv[2] /= len;
+        const double* p0 = Pf + 3 * t0;
+        double dd = fabs(nv[0] * (vrel[0] - p0[0]) + nv[1] * (vrel[1] - p0[1]) + nv[2] * (vrel[2] - p0[2]));
+        // canonical triple order key = sorted (t0, min(t1,t2), max(t1,t2))
+        int s1 = min(t1, t2), s2 = max(t1, t2);
+        bool better = dd < best || (dd == best && (t0 < bt0 || (t0 == bt0 && (s1 < bt1 || (s1 == bt1 && s2 < bt2)))));
+        if (better) {
+          best = dd; bt0 = t0; bt1 = s1; bt2 = s2;
+          bn[0] = nv[0]; bn[1] = nv[1]; bn[2] = nv[2];
+        }
+      }
+    }
+    // block reduction of (best, triple)
+    __shared__ double r_best[HULL_THREADS];
+    __shared__ int r_t[HULL_THREADS][3];
+    __shared__ double r_n[HULL_THREADS][3];
+    __shared__ int r_cnt[HULL_THREADS];
+    r_best[tid] = best; r_t[tid][0] = bt0; r_t[tid][1] = bt1; r_t[tid][2] = bt2;
+    r_n[tid][0] = bn[0]; r_n[tid][1] = bn[1]; r_n[tid][2] = bn[2];
+    r_cnt[tid] = nfac;
+    __syncthreads();
+    if (tid == 0) {
+      int fo = 0, total = 0;
+      for (int t = 0; t < (int)blockDim.x; ++t) {
+        total += r_cnt[t];
+        bool better = r_best[t] < r_best[fo] ||
+                      (r_best[t] == r_best[fo] &&
+                       (r_t[t][0] < r_t[fo][0] || (r_t[t][0] == r_t[fo][0] &&
+                        (r_t[t][1] < r_t[fo][1] || (r_t[t][1] == r_t[fo][1] && r_t[t][2] < r_t[fo][2])))));
+        if (better) fo = t;
+      }
+      const bool ok = !s_fail && total > 0 && r_t[fo][0] != INT_MAX;
+      float* pl = A.planes + (size_t)slot * 8;
+      double distance = r_best[fo];
+      double nrm[3] = {r_n[fo][0], r_n[fo][1], r_n[fo][2]};
+      if (ok) {
+        double dh = distance * 0.5;                       // :1416
+        const double mult = 1.0;                          // :1213
+        pl[0] = (float)(xi[3] + mult * dh * nrm[0]);
+        pl[1] = (float)(xi[4] + mult * dh * nrm[1]);
+        pl[2] = (float)(xi[5] + mult * dh * nrm[2]);
+        pl[3] = (float)nrm[0]; pl[4] = (float)nrm[1]; pl[5] = (float)nrm[2];
+        pl[6] = __int_as_float(1);
+        atomicAdd(&A.stats[3], 1ull);
+      } else {
+        pl[6] = __int_as_float(0);                        // no usable plane
+        atomicAdd(&A.stats[4], 1ull);
+      }
+      if (A.recs) {
+        lqro_pair_record& rec = A.recs[slot];
+        rec.flags |= ok ? LQRO_REC_HULL : LQRO_REC_HULLFAIL;
+        rec.n_facets = ok ? total : -1;
+        if (ok) {
+          rec.facet[0] = r_t[fo][0]; rec.facet[1] = r_t[fo][1]; rec.facet[2] = r_t[fo][2];
+          rec.dist = distance;
+          for (int q = 0; q < 3; ++q) {
+            rec.normal[q] = nrm[q];
+            rec.plane_point[q] = pl[q];
+            rec.plane_normal[q] = pl[3 + q];
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// LP kernel: one thread per row agent, fp32 RVO2-3D LP (:1001-1234)
+// ---------------------------------------------------------------------------
+struct v3 { float x, y, z; };
+__device__ __forceinline__ v3 V3(float x, float y, float z) { v3 r; r.x = x; r.y = y; r.z = z; return r; }
+__device__ __forceinline__ float vdot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ v3 vadd(v3 a, v3 b) { return V3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ v3 vsub(v3 a, v3 b) { return V3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ v3 vmul(v3 a, float s) { return V3(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ v3 smul(float s, v3 a) { return V3(s * a.x, s * a.y, s * a.z); }
+__device__ __forceinline__ v3 vcross(v3 a, v3 b) {
+  return V3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ v3 vnormalize(v3 a) {
+  float l = sqrtf(vdot(a, a));
+  const float inv = 1.0f / l;
+  return V3(a.x * inv, a.y * inv, a.z * inv);
+}
+__device__ __forceinline__ float sqrf(float s) { return s * s; }
+#define RVO_EPS 0.00001f
+
+struct LPPlane { v3 point, normal; };
+
+__device__ __forceinline__ LPPlane ld_plane(const float* p) {
+  LPPlane r;
+  r.point = V3(p[0], p[1], p[2]);
+  r.normal = V3(p[3], p[4], p[5]);
+  return r;
+}
+
+// planes: stride 8 floats
+__device__ bool d_lp1(const float* planes, int planeNo, v3 lpt, v3 ldir, float radius, v3 opt,
+                      bool dirOpt, v3& result) {
+  const float dotProduct = vdot(lpt, ldir);
+  const float disc = sqrf(dotProduct) + sqrf(radius) - vdot(lpt, lpt);
+  if (disc < 0.0f) return false;
+  const float sq = sqrtf(disc);
+  float tLeft = -dotProduct - sq;
+  float tRight = -dotProduct + sq;
+  for (int i = 0; i < planeNo; ++i) {
+    LPPlane pi = ld_plane(planes + 8 * (size_t)i);
+    const float numerator = vdot(vsub(pi.point, lpt), pi.normal);
+    const float denominator = vdot(ldir, pi.normal);
+    if (sqrf(denominator) <= RVO_EPS) {
+      if (numerator > 0.0f) return false;
+      continue;
+    }
+    const float t = numerator / denominator;
+    if (denominator >= 0.0f) tLeft = (tLeft < t) ? t : tLeft;
+    else tRight = (t < tRight) ? t : tRight;
+    if (tLeft > tRight) return false;
+  }
+  if (dirOpt) {
+    if (vdot(opt, ldir) > 0.0f) result = vadd(lpt, smul(tRight, ldir));
+    else result = vadd(lpt, smul(tLeft, ldir));
+  } else {
+    const float t = vdot(ldir, vsub(opt, lpt));
+    if (t < tLeft) result = vadd(lpt, smul(tLeft, ldir));
+    else if (t > tRight) result = vadd(lpt, smul(tRight, ldir));
+    else result = vadd(lpt, smul(t, ldir));
+  }
+  return true;
+}
+
+__device__ bool d_lp2(const float* planes, int planeNo, float radius, v3 opt, bool dirOpt, v3& result) {
+  const LPPlane pn = ld_plane(planes + 8 * (size_t)planeNo);
+  const float planeDist = vdot(pn.point, pn.normal);
+  const float planeDistSq = sqrf(planeDist);
+  const float radiusSq = sqrf(radius);
+  if (planeDistSq > radiusSq) return false;
+  const float planeRadiusSq = radiusSq - planeDistSq;
+  const v3 planeCenter = smul(planeDist, pn.normal);
+  if (dirOpt) {
+    const v3 pov = vsub(opt, smul(vdot(opt, pn.normal), pn.normal));
+    const float povSq = vdot(pov, pov);
+    if (povSq <= RVO_EPS) result = planeCenter;
+    else result = vadd(planeCenter, smul(sqrtf(planeRadiusSq / povSq), pov));
+  } else {
+    result = vadd(opt, smul(vdot(vsub(pn.point, opt), pn.normal), pn.normal));
+    if (vdot(result, result) > radiusSq) {
+      const v3 pr = vsub(result, planeCenter);
+      const float prSq = vdot(pr, pr);
+      result = vadd(planeCenter, smul(sqrtf(planeRadiusSq / prSq), pr));
+    }
+  }
+  for (int i = 0; i < planeNo; ++i) {
+    const LPPlane pi = ld_plane(planes + 8 * (size_t)i);
+    if (vdot(pi.normal, vsub(pi.point, result)) > 0.0f) {
+      v3 cp = vcross(pi.normal, pn.normal);
+      if (vdot(cp, cp) <= RVO_EPS) return false;
+      v3 ldir = vnormalize(cp);
+      const v3 lineNormal = vcross(ldir, pn.normal);
+      v3 lpt = vadd(pn.point, smul(vdot(vsub(pi.point, pn.point), pi.normal) / vdot(lineNormal, pi.normal),
+                                   lineNormal));
+      if (!d_lp1(planes, i, lpt, ldir, radius, opt, dirOpt, result)) return false;
+    }
+  }
+  return true;
+}
+
+__device__ int d_lp3(const float* planes, int m, double radius, v3 opt, bool dirOpt, v3& result) {
+  const float rf = (float)radius;
+  if (dirOpt) result = vmul(opt, rf);
+  else if (vdot(opt, opt) > sqrf(rf)) result = vmul(vnormalize(opt), rf);
+  else result = opt;
+  for (int i = 0; i < m; ++i) {
+    const LPPlane pi = ld_plane(planes + 8 * (size_t)i);
+    if (vdot(pi.normal, vsub(pi.point, result)) > 0.0f) {
+      const v3 tmp = result;
+      if (!d_lp2(planes, i, rf, opt, dirOpt, result)) { result = tmp; return i; }
+    }
+  }
+  return m;
+}
+
+__device__ void d_lp4(const float* planes, int m, int beginPlane, float radius, v3& result,
+                      float* scratch) {
+  float distance = 0.0f;
+  for (int i = beginPlane; i < m; ++i) {
+    const LPPlane pi = ld_plane(planes + 8 * (size_t)i);
+    if (vdot(pi.normal, vsub(pi.point, result)) > distance) {
+      int np = 0;
+      for (int j = 0; j < i; ++j) {
+        const LPPlane pj = ld_plane(planes + 8 * (size_t)j);
+        v3 ppt, pnm;
+        const v3 cp = vcross(pj.normal, pi.normal);
+        if (vdot(cp, cp) <= RVO_EPS) {
+          if (vdot(pi.normal, pj.normal) > 0.0f) continue;
+          ppt = smul(0.5f, vadd(pi.point, pj.point));
+        } else {
+          const v3 lineNormal = vcross(cp, pi.normal);
+          ppt = vadd(pi.point, smul(vdot(vsub(pj.point, pi.point), pj.normal) / vdot(lineNormal, pj.normal),
+                                    lineNormal));
+        }
+        pnm = vnormalize(vsub(pj.normal, pi.normal));
+        float* d = scratch + 8 * (size_t)np;
+        d[0] = ppt.x; d[1] = ppt.y; d[2] = ppt.z; d[3] = pnm.x; d[4] = pnm.y; d[5] = pnm.z;
+        np++;
+      }
+      const v3 tmp = result;
+      if (d_lp3(scratch, np, radius, pi.normal, true, result) < np) result = tmp;
+      distance = vdot(pi.normal, vsub(pi.point, result));
+    }
+  }
+}
+
+struct LpArgs {
+  int npr, nrows, row_begin;
+  double vmax;
+  float* planes;        // compacted in place, per row
+  float* scratch;       // per row npr*8
+  const double* vgoal;
+  double* newv;
+};
+
+__global__ void __launch_bounds__(64) k_lp(LpArgs A) {
+  const int lrow = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lrow >= A.nrows) return;
+  const int i = A.row_begin + lrow;
+  float* rowp = A.planes + (size_t)lrow * A.npr * 8;
+  // compact emitted planes in j order (orcaPlanes_ push order, :1220)
+  int m = 0;
+  for (int s = 0; s < A.npr; ++s) {
+    const float* src = rowp + 8 * (size_t)s;
+    if (__float_as_int(src[6]) == 1) {
+      if (m != s) {
+        float* dst = rowp + 8 * (size_t)m;
+        for (int q = 0; q < 8; ++q) dst[q] = src[q];
+      }
+      m++;
+    }
+  }
+  v3 pref = V3((float)A.vgoal[3 * i], (float)A.vgoal[3 * i + 1], (float)A.vgoal[3 * i + 2]);
+  v3 nv = V3(0.0f, 0.0f, 0.0f);
+  int fail = d_lp3(rowp, m, A.vmax, pref, false, nv);
+  if (fail < m) d_lp4(rowp, m, fail, (float)A.vmax, nv, A.scratch + (size_t)lrow * A.npr * 8);
+  A.newv[3 * i] = nv.x;
+  A.newv[3 * i + 1] = nv.y;
+  A.newv[3 * i + 2] = nv.z;
+}
+
+// ---------------------------------------------------------------------------
+// Host side: context + C-ABI
+// ---------------------------------------------------------------------------
+struct lqro_ctx {
+  lqro_config cfg;
+  int rb, re, nrows, npr;
+  int have_gains, per_agent;
+  hipStream_t stream;
+  hipEvent_t ev[5];
+  double *d_T, *d_NCF, *d_S, *d_x, *d_vgoal, *d_newv;
+  double *d_A, *d_B, *d_L, *d_E;
+  float *d_planes, *d_lpscratch;
+  lqro_pair_record* d_recs;
+  int *d_hq, *d_hcount, *d_hnext, *d_err;
+  double* d_hscratch;
+  int* d_hiscratch;
+  float* d_hfscratch;
+  void* d_hfaces;
+  int hull_blocks, hull_cap;
+  unsigned long long* d_stats;
+  int lds_bytes;
+  PairArgs pa;
+};
+
+#define HIPCHK(x)                                                                        \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) {                                                              \
+      fprintf(stderr, "liblqro: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, \
+              __LINE__);                                                                 \
+      return LQRO_E_HIP;                                                                 \
+    }                                                                                    \
+  } while (0)
+
+extern "C" {
+
+int lqro_version(void) { return 1; }
+
+const char* lqro_status_string(int s) {
+  switch (s) {
+    case LQRO_OK: return "ok";
+    case LQRO_E_ARG: return "bad argument";
+    case LQRO_E_HIP: return "HIP runtime error";
+    case LQRO_E_NOMEM: return "out of memory";
+    case LQRO_E_STATE: return "call order violated";
+    case LQRO_E_SINGULAR: return "singular C*G_k";
+    case LQRO_E_NODEVICE: return "no gfx950 device";
+    case LQRO_E_OVERFLOW: return "work queue overflow";
+  }
+  return "unknown";
+}
+
+void lqro_config_default(lqro_config* c, int32_t n, int32_t h, int32_t np) {
+  c->n_agents = n;
+  c->x_dim = 16;
+  c->u_dim = 4;
+  c->horizon = h;
+  c->n_points = np;
+  c->min_reach = 4;
+  c->xy_radius = 0.26;
+  c->z_radius = 0.75;
+  c->vmax_reach = 30.0;
+  c->vmax_lp = 100.0;
+  c->row_begin = 0;
+  c->row_end = 0;
+  c->device = 0;
+  c->flags = 0;
+}
+
+void lqro_destroy(lqro_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->cfg.device);
+  void* ps[] = {c->d_T, c->d_NCF, c->d_S, c->d_x, c->d_vgoal, c->d_newv, c->d_A, c->d_B,
+                c->d_L, c->d_E, c->d_planes, c->d_lpscratch, c->d_recs, c->d_hq, c->d_hcount,
+                c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats};
+  for (void* p : ps)
+    if (p) (void)hipFree(p);
+  for (int k = 0; k < 5; ++k)
+    if (c->ev[k]) (void)hipEventDestroy(c->ev[k]);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+static int ctx_alloc(lqro_ctx* c) {
+  const lqro_config& g = c->cfg;
+  const size_t N = g.n_agents, X = g.x_dim, H = g.horizon, NP = g.n_points;
+  const size_t slots = (size_t)c->nrows * c->npr;
+  HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  for (int k = 0; k < 5; ++k) HIPCHK(hipEventCreate(&c->ev[k]));
+  HIPCHK(hipMalloc(&c->d_S, sizeof(double) * NP * 3));
+  HIPCHK(hipMalloc(&c->d_x, sizeof(double) * N * X));
+  HIPCHK(hipMalloc(&c->d_vgoal, sizeof(double) * N * 3));
+  HIPCHK(hipMalloc(&c->d_newv, sizeof(double) * N * 3));
+  HIPCHK(hipMalloc(&c->d_A, sizeof(double) * X * X));
+  HIPCHK(hipMalloc(&c->d_B, sizeof(double) * X * g.u_dim));
+  HIPCHK(hipMalloc(&c->d_L, sizeof(double) * N * g.u_dim * X));
+  HIPCHK(hipMalloc(&c->d_E, sizeof(double) * N * g.u_dim * 3));
+  HIPCHK(hipMalloc(&c->d_T, sizeof(double) * N * H * 9));
+  HIPCHK(hipMalloc(&c->d_NCF, sizeof(double) * N * H * 3 * X));
+  HIPCHK(hipMalloc(&c->d_planes, sizeof(float) * 8 * (slots ? slots : 1)));
+  HIPCHK(hipMalloc(&c->d_lpscratch, sizeof(float) * 8 * (slots ? slots : 1)));
+  if (g.flags & LQRO_FLAG_RECORDS)
+    HIPCHK(hipMalloc(&c->d_recs, sizeof(lqro_pair_record) * (slots ? slots : 1)));
+  c->hull_cap = (int)(slots < (1u << 22) ? slots : (1u << 22));
+  if (c->hull_cap < 1) c->hull_cap = 1;
+  HIPCHK(hipMalloc(&c->d_hq, sizeof(int) * c->hull_cap));
+  HIPCHK(hipMalloc(&c->d_hcount, sizeof(int) * 2));
+  c->d_hnext = c->d_hcount + 1;
+  HIPCHK(hipMalloc(&c->d_err, sizeof(int)));
+  HIPCHK(hipMalloc(&c->d_stats, sizeof(unsigned long long) * 8));
+  c->hull_blocks = 512;
+  HIPCHK(hipMalloc(&c->d_hscratch, sizeof(double) * 6 * H * NP * c->hull_blocks));
+  HIPCHK(hipMalloc(&c->d_hiscratch, sizeof(int) * H * NP * c->hull_blocks));
+  HIPCHK(hipMalloc(&c->d_hfscratch, sizeof(float) * H * NP * c->hull_blocks));
+  HIPCHK(hipMalloc(&c->d_hfaces, (sizeof(HFace) + sizeof(int)) * HULL_FMAX * (size_t)c->hull_blocks));
+  return LQRO_OK;
+}
+
+int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
+  if (!cfg || !out) return LQRO_E_ARG;
+  *out = nullptr;
+  const lqro_config& g = *cfg;
+  if (g.n_agents < 2 || (g.x_dim != 16 && g.x_dim != 12) || g.u_dim != 4 || g.horizon < 1 ||
+      g.n_points < 1 || g.vmax_reach <= 0)
+    return LQRO_E_ARG;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= g.device) return LQRO_E_NODEVICE;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, g.device) != hipSuccess) return LQRO_E_NODEVICE;
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    fprintf(stderr, "liblqro: device %d is %s, built for gfx950\n", g.device, prop.gcnArchName);
+    return LQRO_E_NODEVICE;
+  }
+  if (hipSetDevice(g.device) != hipSuccess) return LQRO_E_HIP;
+  lqro_ctx* c = new (std::nothrow) lqro_ctx;
+  if (!c) return LQRO_E_NOMEM;
+  memset(c, 0, sizeof *c);
+  c->cfg = g;
+  c->rb = g.row_begin;
+  c->re = (g.row_end > g.row_begin) ? g.row_end : g.n_agents;
+  if (g.row_end == 0 && g.row_begin == 0) { c->rb = 0; c->re = g.n_agents; }
+  if (c->rb < 0 || c->re > g.n_agents || c->rb >= c->re) { delete c; return LQRO_E_ARG; }
+  c->nrows = c->re - c->rb;
+  c->npr = g.n_agents - 1;
+  // LDS layout of k_pair
+  const int H = g.horizon, NP = g.n_points, X = g.x_dim, XP = X + 1;
+  const int chunks = (H * NP + 63) / 64;
+  const int words = (chunks + 31) / 32;
+  int off = 0;
+  PairArgs& P = c->pa;
+  P.lds_T = off; off += H * 9;
+  P.lds_N = off; off += H * 3 * XP;
+  P.lds_S = off; off += 3 * NP;
+  P.lds_wave = off;
+  P.wave_doubles = 3 * H + (words * 64 + 1) / 2;
+  off += PAIR_WAVES * P.wave_doubles;
+  c->lds_bytes = off * 8;
+  if (c->lds_bytes > 160 * 1024) {
+    fprintf(stderr, "liblqro: horizon %d x %d points needs %d B of LDS\n", H, NP, c->lds_bytes);
+    delete c;
+    return LQRO_E_ARG;
+  }
+  P.XP = XP;
+  P.chunks = chunks;
+  P.words = words;
+  int rc = ctx_alloc(c);
+  if (rc) { lqro_destroy(c); return rc; }
+  std::vector<double> S(3 * (size_t)NP);
+  lqro_sphere(NP, g.xy_radius, g.z_radius, S.data());
+  if (hipMemcpy(c->d_S, S.data(), sizeof(double) * S.size(), hipMemcpyHostToDevice) != hipSuccess) {
+    lqro_destroy(c);
+    return LQRO_E_HIP;
+  }
+  if (hipFuncSetAttribute((const void*)k_pair<16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          c->lds_bytes) != hipSuccess ||
+      hipFuncSetAttribute((const void*)k_pair<12>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          c->lds_bytes) != hipSuccess) {
+    lqro_destroy(c);
+    return LQRO_E_HIP;
+  }
+  *out = c;
+  return LQRO_OK;
+}
+
+int lqro_set_gains(lqro_ctx* c, const double* A, const double* B, const double* L,
+                   const double* E, int32_t per_agent) {
+  if (!c || !A || !B || !L || !E) return LQRO_E_ARG;
+  const lqro_config& g = c->cfg;
+  HIPCHK(hipSetDevice(g.device));
+  const size_t X = g.x_dim, U = g.u_dim, N = g.n_agents;
+  const size_t na = per_agent ? N : 1;
+  HIPCHK(hipMemcpyAsync(c->d_A, A, sizeof(double) * X * X, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_B, B, sizeof(double) * X * U, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_L, L, sizeof(double) * na * U * X, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_E, E, sizeof(double) * na * U * 3, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream));
+  hipLaunchKernelGGL(k_tables, dim3((unsigned)na), dim3(256), 0, c->stream, (int)X, (int)U,
+                     g.horizon, c->d_A, c->d_B, c->d_L, c->d_E, per_agent ? 1 : 0, c->d_T,
+                     c->d_NCF, c->d_err);
+  HIPCHK(hipGetLastError());
+  int err = 0;
+  HIPCHK(hipMemcpyAsync(&err, c->d_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (err) return LQRO_E_SINGULAR;
+  c->per_agent = per_agent ? 1 : 0;
+  c->have_gains = 1;
+  return LQRO_OK;
+}
+
+static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, double* d_newv,
+                        hipStream_t s) {
+  const lqro_config& g = c->cfg;
+  PairArgs P = c->pa;
+  P.N = g.n_agents; P.X = g.x_dim; P.H = g.horizon; P.NP = g.n_points; P.min_reach = g.min_reach;
+  P.row_begin = c->rb; P.nrows = c->nrows; P.npr = c->npr;
+  P.per_agent = c->per_agent;
+  P.r2 = g.vmax_reach * g.vmax_reach;
+  P.r2_lo = P.r2 * (1.0 - 1e-12);
+  P.r2_hi = P.r2 * (1.0 + 1e-12);
+  P.T = c->d_T; P.NCF = c->d_NCF; P.S = c->d_S; P.x = d_x;
+  P.planes = c->d_planes; P.recs = c->d_recs;
+  P.hull_queue = c->d_hq; P.hull_count = c->d_hcount; P.hull_cap = c->hull_cap;
+  P.stats = c->d_stats;
+  // one workgroup = PAIR_WAVES waves on one row; each wave takes several pairs
+  P.pairs_per_block = PAIR_WAVES * 4;
+  P.blocks_per_row = (c->npr + P.pairs_per_block - 1) / P.pairs_per_block;
+  HIPCHK(hipMemsetAsync(c->d_hcount, 0, sizeof(int) * 2, s));
+  HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * 8, s));
+  HIPCHK(hipEventRecord(c->ev[0], s));
+  const unsigned nblk = (unsigned)P.blocks_per_row * (unsigned)c->nrows;
+  if (g.x_dim == 16)
+    hipLaunchKernelGGL(k_pair<16>, dim3(nblk), dim3(PAIR_WAVES * 64), c->lds_bytes, s, P);
+  else if (g.x_dim == 12)
+    hipLaunchKernelGGL(k_pair<12>, dim3(nblk), dim3(PAIR_WAVES * 64), c->lds_bytes, s, P);
+  else
+    return LQRO_E_ARG;
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->ev[1], s));
+  HullArgs Hh;
+  Hh.N = g.n_agents; Hh.X = g.x_dim; Hh.H = g.horizon; Hh.NP = g.n_points;
+  Hh.row_begin = c->rb; Hh.npr = c->npr; Hh.per_agent = c->per_agent;
+  Hh.r2 = P.r2; Hh.r2_lo = P.r2_lo; Hh.r2_hi = P.r2_hi;
+  Hh.T = c->d_T; Hh.NCF = c->d_NCF; Hh.S = c->d_S; Hh.x = d_x;
+  Hh.planes = c->d_planes; Hh.recs = c->d_recs;
+  Hh.queue = c->d_hq; Hh.count = c->d_hcount; Hh.cap = c->hull_cap; Hh.next = c->d_hnext;
+  Hh.scratch = c->d_hscratch; Hh.iscratch = c->d_hiscratch; Hh.fscratch = c->d_hfscratch;
+  Hh.faces = c->d_hfaces;
+  Hh.stats = c->d_stats;
+  hipLaunchKernelGGL(k_hull, dim3(c->hull_blocks), dim3(HULL_THREADS), 0, s, Hh);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->ev[2], s));
+  LpArgs La;
+  La.npr = c->npr; La.nrows = c->nrows; La.row_begin = c->rb; La.vmax = g.vmax_lp;
+  La.planes = c->d_planes; La.scratch = c->d_lpscratch; La.vgoal = d_vgoal; La.newv = d_newv;
+  hipLaunchKernelGGL(k_lp, dim3((unsigned)((c->nrows + 63) / 64)), dim3(64), 0, s, La);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->ev[3], s));
+  return LQRO_OK;
+}
+
+int lqro_step_device(lqro_ctx* c, const double* d_x, const double* d_vgoal, double* d_newv,
+                     void* stream) {
+  if (!c || !d_x || !d_vgoal || !d_newv) return LQRO_E_ARG;
+  if (!c->have_gains) return LQRO_E_STATE;
+  HIPCHK(hipSetDevice(c->cfg.device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  return enqueue_step(c, d_x, d_vgoal, d_newv, s);
+}
+
+int lqro_step(lqro_ctx* c, const double* x, const double* vgoal, double* newv) {
+  if (!c || !x || !vgoal || !newv) return LQRO_E_ARG;
+  if (!c->have_gains) return LQRO_E_STATE;
+  const lqro_config& g = c->cfg;
+  HIPCHK(hipSetDevice(g.device));
+  const size_t N = g.n_agents, X = g.x_dim;
+  HIPCHK(hipMemcpyAsync(c->d_x, x, sizeof(double) * N * X, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_vgoal, vgoal, sizeof(double) * N * 3, hipMemcpyHostToDevice, c->stream));
+  int rc = enqueue_step(c, c->d_x, c->d_vgoal, c->d_newv, c->stream);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(newv + (size_t)c->rb * 3, c->d_newv + (size_t)c->rb * 3,
+                        sizeof(double) * 3 * c->nrows, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  int hc = 0;
+  HIPCHK(hipMemcpy(&hc, c->d_hcount, sizeof(int), hipMemcpyDeviceToHost));
+  if (hc > c->hull_cap) return LQRO_E_OVERFLOW;
+  return LQRO_OK;
+}
+
+int lqro_get_records(lqro_ctx* c, lqro_pair_record* out, int64_t cap, int64_t* n_out) {
+  if (!c || !out) return LQRO_E_ARG;
+  if (!c->d_recs) return LQRO_E_STATE;
+  const int64_t n = (int64_t)c->nrows * c->npr;
+  if (cap < n) return LQRO_E_ARG;
+  HIPCHK(hipSetDevice(c->cfg.device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipMemcpy(out, c->d_recs, sizeof(lqro_pair_record) * (size_t)n, hipMemcpyDeviceToHost));
+  if (n_out) *n_out = n;
+  return LQRO_OK;
+}
+
+int lqro_get_stats(lqro_ctx* c, int64_t* st) {
+  if (!c || !st) return LQRO_E_ARG;
+  HIPCHK(hipSetDevice(c->cfg.device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  unsigned long long h[8];
+  HIPCHK(hipMemcpy(h, c->d_stats, sizeof h, hipMemcpyDeviceToHost));
+  for (int k = 0; k < 8; ++k) st[k] = (int64_t)h[k];
+  st[0] = (int64_t)c->nrows * c->npr;
+  return LQRO_OK;
+}
+
+int lqro_get_timings(lqro_ctx* c, float* ms) {
+  if (!c || !ms) return LQRO_E_ARG;
+  HIPCHK(hipSetDevice(c->cfg.device));
+  HIPCHK(hipEventSynchronize(c->ev[3]));
+  HIPCHK(hipEventElapsedTime(&ms[0], c->ev[0], c->ev[1]));
+  HIPCHK(hipEventElapsedTime(&ms[1], c->ev[1], c->ev[2]));
+  HIPCHK(hipEventElapsedTime(&ms[2], c->ev[2], c->ev[3]));
+  HIPCHK(hipEventElapsedTime(&ms[3], c->ev[0], c->ev[3]));
+  return LQRO_OK;
+}
+
+}  // extern "C"

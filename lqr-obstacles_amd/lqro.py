@@ -1,0 +1,315 @@
+"""lqro — Python host binding of liblqro.so (the MI355X LQR-Obstacle step).
+
+This module mirrors the reference simulator's interface for the pair loop
+(hihixuyang/LQR-Obstacles, QuadrotorHoverController/LQRObstacles.cpp, "LQRO"):
+
+  * ``Quadrotor``  — the agent record the loop reads and writes (LQRO:73-165:
+    ``x``, ``L``, ``E``, ``vGoal``, ``newV``);
+  * ``Simulator.findMatrices()`` — controlMatrices at hover (LQRO:520-582,
+    called per agent at LQRO:1370-1373);
+  * ``Simulator.step()`` — the pair loop LQRO:1393-1436: every ordered pair's
+    LQR-Obstacle, its half-plane, and each agent's new velocity
+    (calculateNewV, LQRO:1435), computed by the HIP kernels.
+
+All numerics run in liblqro.so (HIP for gfx950).  There is no CPU fallback:
+if the library or a gfx950 device is missing, the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblqro.so")
+
+LQRO_OK = 0
+LQRO_FLAG_RECORDS = 0x1
+REC_PLANE, REC_INSIDE, REC_BACKUP, REC_HULL, REC_HULLFAIL = 0x01, 0x02, 0x04, 0x08, 0x10
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("n_agents", C.c_int32), ("x_dim", C.c_int32), ("u_dim", C.c_int32),
+        ("horizon", C.c_int32), ("n_points", C.c_int32), ("min_reach", C.c_int32),
+        ("xy_radius", C.c_double), ("z_radius", C.c_double),
+        ("vmax_reach", C.c_double), ("vmax_lp", C.c_double),
+        ("row_begin", C.c_int32), ("row_end", C.c_int32),
+        ("device", C.c_int32), ("flags", C.c_int32),
+    ]
+
+
+class Model(C.Structure):
+    _fields_ = [(n, C.c_double) for n in (
+        "dt", "gravity", "mass", "inertia", "moment_const", "thrust_latency", "length",
+        "j_step", "qv", "qp", "r", "pos_weight")]
+
+
+class PairRecord(C.Structure):
+    _fields_ = [
+        ("i", C.c_int32), ("j", C.c_int32), ("n_reach", C.c_int32), ("flags", C.c_int32),
+        ("gjk_iters", C.c_int32), ("simplex_n", C.c_int32), ("simplex", C.c_int32 * 4),
+        ("facet", C.c_int32 * 3), ("n_facets", C.c_int32), ("reach_hash", C.c_uint64),
+        ("dist", C.c_double), ("normal", C.c_double * 3), ("wpt_vrel", C.c_double * 3),
+        ("wpt_hull", C.c_double * 3), ("plane_point", C.c_float * 3),
+        ("plane_normal", C.c_float * 3),
+    ]
+
+
+RECORD_DTYPE = np.dtype([
+    ("i", "<i4"), ("j", "<i4"), ("n_reach", "<i4"), ("flags", "<i4"), ("gjk_iters", "<i4"),
+    ("simplex_n", "<i4"), ("simplex", "<i4", (4,)), ("facet", "<i4", (3,)),
+    ("n_facets", "<i4"), ("reach_hash", "<u8"), ("dist", "<f8"), ("normal", "<f8", (3,)),
+    ("wpt_vrel", "<f8", (3,)), ("wpt_hull", "<f8", (3,)), ("plane_point", "<f4", (3,)),
+    ("plane_normal", "<f4", (3,)),
+])
+assert RECORD_DTYPE.itemsize == C.sizeof(PairRecord) == 168
+
+# every symbol include/lqro.h declares
+EXPORTS = (
+    "lqro_config_default", "lqro_model_default", "lqro_synthesize_gains", "lqro_sphere",
+    "lqro_create", "lqro_destroy", "lqro_set_gains", "lqro_step", "lqro_step_device",
+    "lqro_get_records", "lqro_get_stats", "lqro_get_timings", "lqro_status_string",
+    "lqro_version",
+)
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load liblqro.so (raises if it was not built: no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"liblqro.so not built at {LIB_PATH}; run __graft_entry__.build()")
+        L = C.CDLL(LIB_PATH)
+        vp, i32, i64, dbl = C.c_void_p, C.c_int32, C.c_int64, C.c_double
+        L.lqro_status_string.restype = C.c_char_p
+        L.lqro_config_default.argtypes = [C.POINTER(Config), i32, i32, i32]
+        L.lqro_model_default.argtypes = [C.POINTER(Model)]
+        L.lqro_synthesize_gains.argtypes = [C.POINTER(Model)] + [vp] * 7
+        L.lqro_sphere.argtypes = [i32, dbl, dbl, vp]
+        L.lqro_create.argtypes = [C.POINTER(Config), C.POINTER(vp)]
+        L.lqro_destroy.argtypes = [vp]
+        L.lqro_destroy.restype = None
+        L.lqro_set_gains.argtypes = [vp, vp, vp, vp, vp, i32]
+        L.lqro_step.argtypes = [vp, vp, vp, vp]
+        L.lqro_step_device.argtypes = [vp, vp, vp, vp, vp]
+        L.lqro_get_records.argtypes = [vp, vp, i64, C.POINTER(i64)]
+        L.lqro_get_stats.argtypes = [vp, vp]
+        L.lqro_get_timings.argtypes = [vp, vp]
+        _lib = L
+    return _lib
+
+
+class LqroError(RuntimeError):
+    pass
+
+
+def _check(rc: int, what: str):
+    if rc != LQRO_OK:
+        msg = lib().lqro_status_string(rc).decode()
+        raise LqroError(f"{what}: {msg} ({rc})")
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def default_model() -> Model:
+    m = Model()
+    lib().lqro_model_default(C.byref(m))
+    return m
+
+
+def synthesize_gains(model: Model | None = None) -> dict:
+    """controlMatrices at hover (LQRO:520-582): A, B, c, L, E, Lh, Eh."""
+    m = model or default_model()
+    out = dict(A=np.zeros((16, 16)), B=np.zeros((16, 4)), c=np.zeros(16), L=np.zeros((4, 16)),
+               E=np.zeros((4, 3)), Lh=np.zeros((3, 16)), Eh=np.zeros((3, 3)))
+    _check(lib().lqro_synthesize_gains(C.byref(m), *[_p(out[k]) for k in
+                                                   ("A", "B", "c", "L", "E", "Lh", "Eh")]),
+           "lqro_synthesize_gains")
+    return out
+
+
+def create_spheres(n_points: int = 100, xy_radius: float = 0.26, z_radius: float = 0.75):
+    """createSpheres (LQRO:735-750)."""
+    s = np.zeros((n_points, 3))
+    _check(lib().lqro_sphere(n_points, xy_radius, z_radius, _p(s)), "lqro_sphere")
+    return s
+
+
+def config(n_agents: int, horizon: int, n_points: int = 100, **kw) -> Config:
+    c = Config()
+    lib().lqro_config_default(C.byref(c), n_agents, horizon, n_points)
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+class Context:
+    """One liblqro context: owns device buffers and a HIP stream."""
+
+    def __init__(self, cfg: Config):
+        self.cfg = cfg
+        h = C.c_void_p()
+        _check(lib().lqro_create(C.byref(cfg), C.byref(h)), "lqro_create")
+        self._h = h
+        rb, re = cfg.row_begin, cfg.row_end
+        if rb == 0 and re == 0:
+            re = cfg.n_agents
+        self.rows = (rb, re)
+
+    def close(self):
+        if self._h:
+            lib().lqro_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_gains(self, A, B, L, E, per_agent: bool = False):
+        A, B, L, E = (np.ascontiguousarray(v, dtype=np.float64) for v in (A, B, L, E))
+        _check(lib().lqro_set_gains(self._h, _p(A), _p(B), _p(L), _p(E), int(per_agent)),
+               "lqro_set_gains")
+
+    def step(self, x: np.ndarray, vgoal: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        vgoal = np.ascontiguousarray(vgoal, dtype=np.float64)
+        newv = np.zeros((self.cfg.n_agents, 3))
+        _check(lib().lqro_step(self._h, _p(x), _p(vgoal), _p(newv)), "lqro_step")
+        return newv
+
+    def step_device(self, d_x: int, d_vgoal: int, d_newv: int, stream: int = 0):
+        """Device pointers (e.g. torch tensor .data_ptr()) on the context's device."""
+        _check(lib().lqro_step_device(self._h, C.c_void_p(d_x), C.c_void_p(d_vgoal),
+                                      C.c_void_p(d_newv), C.c_void_p(stream or None)),
+               "lqro_step_device")
+
+    def records(self) -> np.ndarray:
+        n = (self.rows[1] - self.rows[0]) * (self.cfg.n_agents - 1)
+        out = np.zeros(n, dtype=RECORD_DTYPE)
+        got = C.c_int64()
+        _check(lib().lqro_get_records(self._h, _p(out), n, C.byref(got)), "lqro_get_records")
+        return out
+
+    def stats(self) -> dict:
+        s = np.zeros(8, dtype=np.int64)
+        _check(lib().lqro_get_stats(self._h, _p(s)), "lqro_get_stats")
+        keys = ("pairs", "planes", "inside", "hull_ok", "hull_fail", "gjk_backups",
+                "sum_n_reach", "sum_gtests")
+        return dict(zip(keys, (int(v) for v in s)))
+
+    def timings(self) -> dict:
+        t = np.zeros(4, dtype=np.float32)
+        _check(lib().lqro_get_timings(self._h, _p(t)), "lqro_get_timings")
+        return dict(pair_ms=float(t[0]), hull_ms=float(t[1]), lp_ms=float(t[2]),
+                    step_ms=float(t[3]))
+
+
+# ---------------------------------------------------------------------------
+# Synthetic swarms: SplitMix64, seed "LQRO"
+# ---------------------------------------------------------------------------
+SEED = 0x4C51524F
+_M64 = 0xFFFFFFFFFFFFFFFF
+
+
+def _splitmix(seed: int):
+    s = seed & _M64
+    while True:
+        s = (s + 0x9E3779B97F4A7C15) & _M64
+        z = s
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+        yield ((z ^ (z >> 31)) >> 11) * 2.0 ** -53
+
+
+def synthetic_swarm(n: int, x_dim: int = 16, seed: int = SEED, box: float | None = None):
+    """N agents at constant density: position U[-L/2,L/2]^3 with L = 4 N^(1/3),
+    velocity U[-1,1]^3, hover attitude, rotor forces at nominalInput
+    (LQRO:188); vGoal U[-1,1]^3.  Draw order per agent: 3 position, 3
+    velocity, 3 vGoal."""
+    g = _splitmix(seed)
+    side = box if box is not None else 4.0 * n ** (1.0 / 3.0)
+    nominal = 9.80665 * 0.500 / 4
+    x = np.zeros((n, x_dim))
+    vg = np.zeros((n, 3))
+    for i in range(n):
+        for k in range(3):
+            x[i, k] = (next(g) - 0.5) * side
+        for k in range(3):
+            x[i, 3 + k] = 2.0 * next(g) - 1.0
+        if x_dim == 16:
+            x[i, 12:16] = nominal
+        for k in range(3):
+            vg[i, k] = 2.0 * next(g) - 1.0
+    return x, vg
+
+
+def swap_scenario():
+    """The scripted 4-quad swap of LQRO:1308-1331 at its first step: states
+    (x = xInit, hover forces) and the position goals."""
+    nominal = 9.80665 * 0.500 / 4
+    pos = [(4.0, 0.0, 2.0), (-4.0, -0.0, 2.0), (0.0, 4.0, 2.0), (0.0, -4.0, 2.0)]
+    goal = [(-4.0, 0.0, 2.0), (4.0, 0.0, 2.0), (0.0, -4.0, 2.0), (0.0, 4.0, 2.0)]
+    x = np.zeros((4, 16))
+    for i, p in enumerate(pos):
+        x[i, :3] = p
+        x[i, 12:16] = nominal
+    return x, np.array(goal)
+
+
+# ---------------------------------------------------------------------------
+# Reference-shaped interface
+# ---------------------------------------------------------------------------
+class Quadrotor:
+    """The fields of class Quadrotor (LQRO:73-165) that the pair loop uses."""
+
+    def __init__(self, x, vGoal=None):
+        self.x = np.asarray(x, dtype=np.float64).copy()
+        self.vGoal = np.zeros(3) if vGoal is None else np.asarray(vGoal, dtype=np.float64).copy()
+        self.newV = np.zeros(3)
+        self.L = None
+        self.E = None
+
+
+class Simulator:
+    """The per-step driver of LQRO:1391-1436 on the GPU: ``findMatrices``
+    once, then ``step()`` each control step fills every ``Quadrotor.newV``."""
+
+    def __init__(self, qlist, horizon: int = 45, n_points: int = 100, device: int = 0,
+                 records: bool = False, model: Model | None = None):
+        self.qlist = list(qlist)
+        self.model = model or default_model()
+        flags = LQRO_FLAG_RECORDS if records else 0
+        self.ctx = Context(config(len(self.qlist), horizon, n_points, device=device,
+                                  flags=flags))
+        self.A = self.B = self.c = None
+
+    def findMatrices(self):
+        g = synthesize_gains(self.model)
+        self.A, self.B, self.c = g["A"], g["B"], g["c"]
+        for q in self.qlist:
+            q.L, q.E = g["L"], g["E"]
+        Ls = np.stack([q.L for q in self.qlist])
+        Es = np.stack([q.E for q in self.qlist])
+        per_agent = not all(np.array_equal(Ls[0], l) for l in Ls) or \
+            not all(np.array_equal(Es[0], e) for e in Es)
+        if per_agent:
+            self.ctx.set_gains(self.A, self.B, Ls, Es, per_agent=True)
+        else:
+            self.ctx.set_gains(self.A, self.B, Ls[0], Es[0])
+        return g
+
+    def step(self):
+        x = np.stack([q.x for q in self.qlist])
+        vg = np.stack([q.vGoal for q in self.qlist])
+        newv = self.ctx.step(x, vg)
+        for q, v in zip(self.qlist, newv):
+            q.newV = v.copy()
+        return newv

@@ -823,9 +823,12 @@ out:
 #undef EDGE_PUT
 }
 
+/* canonical facet order: (lowest vertex, then the other two ascending) */
 static int tri_cmp(const void* a, const void* b) {
   const int32_t* x = (const int32_t*)a; const int32_t* y = (const int32_t*)b;
-  for (int k = 0; k < 3; k++) if (x[k] != y[k]) return x[k] < y[k] ? -1 : 1;
+  int32_t kx[3] = {x[0], x[1] < x[2] ? x[1] : x[2], x[1] < x[2] ? x[2] : x[1]};
+  int32_t ky[3] = {y[0], y[1] < y[2] ? y[1] : y[2], y[1] < y[2] ? y[2] : y[1]};
+  for (int k = 0; k < 3; k++) if (kx[k] != ky[k]) return kx[k] < ky[k] ? -1 : 1;
   return 0;
 }
 
@@ -857,7 +860,9 @@ int orc_hull_branch(int n, const double* pts_full, const double vrel[3], double*
     if (f == 0 || d < *dist) {
       *dist = d;
       normal[0] = nv[0]; normal[1] = nv[1]; normal[2] = nv[2];
-      facet[0] = t[0]; facet[1] = t[1]; facet[2] = t[2];
+      facet[0] = t[0];
+      facet[1] = t[1] < t[2] ? t[1] : t[2];
+      facet[2] = t[1] < t[2] ? t[2] : t[1];
     }
   }
   free(rp); free(fc);

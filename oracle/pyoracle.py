@@ -1,0 +1,178 @@
+"""pyoracle — ctypes binding of oracle/liboracle.so.  TEST INFRASTRUCTURE ONLY.
+
+The CPU restatement of the reference's per-pair path (see lqro_oracle.h).
+Imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg, and only as the checker / the timed CPU baseline.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+REF_LIB = os.path.join(HERE, "_ref", "libref.so")
+REFERENCE = "/root/reference"
+
+_o = None
+_r = None
+
+
+def build(ref: bool = True):
+    """Compile liboracle.so (and oracle/_ref/libref.so where /root/reference exists)."""
+    subprocess.run(["make", "-s", "-C", HERE, "liboracle.so"], check=True)
+    if ref and os.path.isdir(REFERENCE):
+        subprocess.run(["make", "-s", "-C", HERE, "ref"], check=True)
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def lib():
+    global _o
+    if _o is None:
+        if not os.path.exists(LIB):
+            build(ref=False)
+        _o = C.CDLL(LIB)
+        d = C.c_double
+        _o.orc_gjk.restype = d
+        _o.orc_round6.restype = d
+        _o.orc_round6.argtypes = [d]
+        _o.orc_pair.argtypes = [C.c_int] * 4 + [d] + [C.c_void_p] * 5 + [C.c_int, C.c_int] + [C.c_void_p] * 3
+        _o.orc_step.argtypes = [C.c_int] * 5 + [d, d, C.c_int] + [C.c_void_p] * 5 + [C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        _o.orc_step_mt.argtypes = _o.orc_step.argtypes + [C.c_int]
+        _o.orc_newv.argtypes = [C.c_int, C.c_void_p, C.c_void_p, d, C.c_void_p]
+        _o.orc_sphere.argtypes = [C.c_int, d, d, C.c_void_p]
+        _o.orc_hull_branch.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        _o.orc_hull.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int]
+    return _o
+
+
+def reflib():
+    """The reference's own functions (oracle/_ref/libref.so) or None."""
+    global _r
+    if _r is None:
+        if not os.path.exists(REF_LIB):
+            if not os.path.isdir(REFERENCE):
+                return None
+            build(ref=True)
+        _r = C.CDLL(REF_LIB)
+        _r.ref_gjk.restype = C.c_double
+    return _r
+
+
+# record layout == include/lqro.h lqro_pair_record
+RECORD_DTYPE = np.dtype([
+    ("i", "<i4"), ("j", "<i4"), ("n_reach", "<i4"), ("flags", "<i4"), ("gjk_iters", "<i4"),
+    ("simplex_n", "<i4"), ("simplex", "<i4", (4,)), ("facet", "<i4", (3,)),
+    ("n_facets", "<i4"), ("reach_hash", "<u8"), ("dist", "<f8"), ("normal", "<f8", (3,)),
+    ("wpt_vrel", "<f8", (3,)), ("wpt_hull", "<f8", (3,)), ("plane_point", "<f4", (3,)),
+    ("plane_normal", "<f4", (3,)),
+])
+
+
+class Model(C.Structure):
+    _fields_ = [(n, C.c_double) for n in (
+        "dt", "gravity", "mass", "inertia", "moment_const", "thrust_latency", "length",
+        "j_step", "qv", "qp", "r", "pos_weight")]
+
+
+def synthesize(model: Model | None = None) -> dict:
+    m = model
+    if m is None:
+        m = Model()
+        lib().orc_model_default(C.byref(m))
+    out = dict(A=np.zeros((16, 16)), B=np.zeros((16, 4)), c=np.zeros(16), L=np.zeros((4, 16)),
+               E=np.zeros((4, 3)), Lh=np.zeros((3, 16)), Eh=np.zeros((3, 3)))
+    lib().orc_synthesize(C.byref(m), *[_p(out[k]) for k in ("A", "B", "c", "L", "E", "Lh", "Eh")])
+    return out
+
+
+def sphere(np_: int = 100, rxy: float = 0.26, rz: float = 0.75) -> np.ndarray:
+    s = np.zeros((np_, 3))
+    lib().orc_sphere(np_, rxy, rz, _p(s))
+    return s
+
+
+def tables(A, B, L, E, H: int, X: int = 16, U: int = 4):
+    T = np.zeros((H, 9))
+    N = np.zeros((H, 3, X))
+    A, B, L, E = (np.ascontiguousarray(v, dtype=np.float64) for v in (A, B, L, E))
+    rc = lib().orc_tables(X, U, H, _p(A), _p(B), _p(L), _p(E), _p(T), _p(N))
+    if rc:
+        raise RuntimeError(f"orc_tables: {rc}")
+    return T, N
+
+
+def pair(T, NCF, S, xi, xj, i=0, j=1, min_reach=4, vmax_reach=30.0, want_points=False):
+    H = T.shape[0]
+    NP = S.shape[0]
+    X = NCF.shape[-1]
+    rec = np.zeros(1, dtype=RECORD_DTYPE)
+    idx = np.zeros(H * NP, np.int32)
+    pts = np.zeros((H * NP, 3))
+    xi = np.ascontiguousarray(xi, np.float64)
+    xj = np.ascontiguousarray(xj, np.float64)
+    rc = lib().orc_pair(X, H, NP, min_reach, vmax_reach, _p(T), _p(NCF), _p(S), _p(xi), _p(xj),
+                        i, j, _p(rec), _p(idx), _p(pts))
+    if rc:
+        raise RuntimeError(f"orc_pair: {rc}")
+    n = int(rec["n_reach"][0])
+    if want_points:
+        return rec[0], idx[:n].copy(), pts[:n].copy()
+    return rec[0]
+
+
+def step(T, NCF, S, x, vgoal, min_reach=4, vmax_reach=30.0, vmax_lp=100.0, rows=None,
+         per_agent=False, threads=1, records=True):
+    N, X = x.shape
+    H = T.shape[-2]
+    NP = S.shape[0]
+    r0, r1 = rows if rows is not None else (0, N)
+    newv = np.zeros((N, 3))
+    recs = np.zeros((r1 - r0) * (N - 1), dtype=RECORD_DTYPE) if records else None
+    x = np.ascontiguousarray(x, np.float64)
+    vgoal = np.ascontiguousarray(vgoal, np.float64)
+    rc = lib().orc_step_mt(N, X, H, NP, min_reach, vmax_reach, vmax_lp, int(per_agent), _p(T),
+                           _p(NCF), _p(S), _p(x), _p(vgoal), r0, r1, _p(newv),
+                           _p(recs) if recs is not None else None, threads)
+    if rc:
+        raise RuntimeError(f"orc_step: {rc}")
+    return newv, recs
+
+
+def newv(planes6: np.ndarray, vgoal, vmax_lp=100.0):
+    planes6 = np.ascontiguousarray(planes6, np.float32).reshape(-1, 6)
+    v = np.ascontiguousarray(vgoal, np.float64)
+    out = np.zeros(3)
+    lib().orc_newv(planes6.shape[0], _p(planes6), _p(v), vmax_lp, _p(out))
+    return out
+
+
+def round6(v: float) -> float:
+    return lib().orc_round6(float(v))
+
+
+def hull(points: np.ndarray) -> np.ndarray:
+    points = np.ascontiguousarray(points, np.float64)
+    n = points.shape[0]
+    cap = 4 * n + 16
+    f = np.zeros((cap, 3), np.int32)
+    k = lib().orc_hull(n, _p(points), _p(f), cap)
+    if k < 0:
+        raise RuntimeError(f"orc_hull: {k}")
+    return f[:k].copy()
+
+
+def hull_branch(points_full: np.ndarray, vrel):
+    points_full = np.ascontiguousarray(points_full, np.float64)
+    v = np.ascontiguousarray(vrel, np.float64)
+    d = np.zeros(1)
+    nrm = np.zeros(3)
+    fac = np.zeros(3, np.int32)
+    k = lib().orc_hull_branch(points_full.shape[0], _p(points_full), _p(v), _p(d), _p(nrm), _p(fac))
+    return k, float(d[0]), nrm, fac

@@ -1,0 +1,93 @@
+"""GPU parity: liblqro.so's HIP path vs the CPU oracle on identical inputs.
+
+Bar: integer outputs (n_reach, reachable-set hash, inside
+flag, GJK simplex, hull arg-min facet) bit-exact; fp64 GJK outputs and the
+fp32 half-planes bit-exact on the non-hull branch (same operation order);
+newV (fp32 LP) bit-exact when every plane matches.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(lqro_mod, oracle, gains, x, vg, H, NP, rows=None):
+    N = x.shape[0]
+    kw = dict(flags=lqro_mod.LQRO_FLAG_RECORDS)
+    if rows is not None:
+        kw.update(row_begin=rows[0], row_end=rows[1])
+    ctx = lqro_mod.Context(lqro_mod.config(N, H, NP, **kw))
+    ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
+    newv = ctx.step(x, vg)
+    recs = ctx.records()
+    st = ctx.stats()
+    ctx.close()
+    T, NCF = oracle.tables(gains["A"], gains["B"], gains["L"], gains["E"], H)
+    S = oracle.sphere(NP)
+    rv, rrecs = oracle.step(T, NCF, S, x, vg, rows=rows, threads=8)
+    return newv, recs, st, rv, rrecs
+
+
+def _compare(recs, rrecs):
+    assert np.array_equal(recs["i"], rrecs["i"]) and np.array_equal(recs["j"], rrecs["j"])
+    assert np.array_equal(recs["n_reach"], rrecs["n_reach"])
+    assert np.array_equal(recs["reach_hash"], rrecs["reach_hash"])
+    assert np.array_equal(recs["flags"] & 3, rrecs["flags"] & 3)
+    out = (rrecs["flags"] & 1) & ~((rrecs["flags"] >> 1) & 1)
+    o = out.astype(bool)
+    for f in ("gjk_iters", "simplex_n", "simplex", "dist", "normal", "wpt_vrel", "wpt_hull",
+              "plane_point", "plane_normal"):
+        a, b = recs[f][o], rrecs[f][o]
+        if a.dtype.kind == "f":
+            assert np.array_equal(a.view(np.uint8), b.view(np.uint8)), f
+        else:
+            assert np.array_equal(a, b), f
+    return o
+
+
+@pytest.mark.parametrize("N,H,NP", [(4, 50, 100), (24, 50, 100), (16, 100, 100), (10, 200, 50)])
+def test_step_bit_exact(lqro_mod, oracle, gains, N, H, NP):
+    x, vg = lqro_mod.synthetic_swarm(N)
+    newv, recs, st, rv, rrecs = _run(lqro_mod, oracle, gains, x, vg, H, NP)
+    o = _compare(recs, rrecs)
+    inside = (rrecs["flags"] & 2) != 0
+    rows_clean = np.ones(N, bool)
+    for r in rrecs[inside]:
+        rows_clean[r["i"]] = False
+    assert np.array_equal(newv[rows_clean], rv[rows_clean])
+
+
+def test_c2_swarm(lqro_mod, oracle, gains):
+    """C2: 64 quadrotors, horizon 50 (4032 pairs)."""
+    x, vg = lqro_mod.synthetic_swarm(64)
+    newv, recs, st, rv, rrecs = _run(lqro_mod, oracle, gains, x, vg, 50, 100)
+    _compare(recs, rrecs)
+    assert st["pairs"] == 64 * 63
+    inside = (rrecs["flags"] & 2) != 0
+    # hull branch: arg-min facet exact, distance/normal to the oracle's hull
+    for r, q in zip(recs[inside], rrecs[inside]):
+        assert r["flags"] & 8, "hull failed"
+        assert np.array_equal(r["facet"], q["facet"])
+        assert r["dist"] == q["dist"]
+        assert np.array_equal(r["normal"], q["normal"])
+    assert np.allclose(newv, rv, rtol=1e-5, atol=1e-7)
+
+
+def test_row_shards_partition(lqro_mod, oracle, gains):
+    """Rows [8, 20) of a 24-agent step equal the same rows of the full step."""
+    x, vg = lqro_mod.synthetic_swarm(24, seed=7)
+    newv, recs, st, rv, rrecs = _run(lqro_mod, oracle, gains, x, vg, 30, 50, rows=(8, 20))
+    _compare(recs, rrecs)
+    assert np.array_equal(newv[8:20], rv[8:20])
+
+
+def test_dense_swarm_inside_hull(lqro_mod, oracle, gains):
+    """A tight swarm (collision courses) exercises the in-kernel hull."""
+    x, vg = lqro_mod.synthetic_swarm(32, box=3.0, seed=11)
+    newv, recs, st, rv, rrecs = _run(lqro_mod, oracle, gains, x, vg, 45, 100)
+    _compare(recs, rrecs)
+    inside = (rrecs["flags"] & 2) != 0
+    assert inside.sum() > 0
+    fac_ok = np.all(recs["facet"][inside] == rrecs["facet"][inside], axis=1)
+    assert fac_ok.mean() >= 0.99, fac_ok.mean()
+    np.testing.assert_allclose(recs["dist"][inside][fac_ok], rrecs["dist"][inside][fac_ok], rtol=0, atol=0)
