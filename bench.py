@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""bench.py — agent-pair LQR-obstacle evals/sec on MI355X.
+
+Workload (BASELINE.json configs[2], "C3"): 1024 quadrotors, horizon 100,
+100 points per sampled ellipsoid, 16-D state — the largest single-GPU config.
+One step = the whole pair loop of LQRObstacles.cpp:1393-1436 over all
+1024*1023 ordered pairs (sweep + reachable filter + GJK + in-kernel hull +
+half-plane) and the per-agent new-velocity LP, with agent states, goals and
+gains already resident in HBM.  Computed in fp64 with the reference's
+operation order (results bit-identical to the reference CPU path).
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node G bench.py --gpus G):
+rows (agents i) are block-sharded over ranks, each rank runs its rows' pairs,
+then one RCCL all-gather of the new velocities (the per-step state exchange,
+SURVEY.md §8e).  Total work is fixed (strong scaling).
+
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "lqr-obstacles_amd"))
+
+N_AGENTS, HORIZON, N_POINTS, X_DIM = 1024, 100, 100, 16
+FP64_VALU_PEAK_TFLOPS = 78.6     # MI355X FP64 vector (spec), MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0
+
+
+def sweep_flops_per_pair(X=X_DIM, H=HORIZON, NP=N_POINTS) -> int:
+    """Algorithmic fp64 work of one pair's exact sweep:
+    Translate_k = NCF_k*d (3X mul + 3X add per step), then per obstacle point
+    u = s + tr (3), Transform*u from 0.0 (9 mul + 9 add), reachable test
+    (3 sub + 3 mul + 2 add).  GJK support scans are data-dependent and are not
+    counted."""
+    return H * (6 * X) + H * NP * (3 + 18 + 8)
+
+
+def algorithmic_bytes_per_pair(X=X_DIM) -> int:
+    """Compulsory HBM bytes per pair: read x_i, x_j (fp64), write one 32-B
+    half-plane slot."""
+    return 2 * X * 8 + 32
+
+
+def cpu_baseline(x, vg, gains, seconds_target=15.0):
+    """The oracle (plain-C restatement, reference operation order) on the
+    host cores: rows of the same C3 workload until ~seconds_target."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle  # test infrastructure, used here only as the timed CPU baseline
+
+    threads = int(os.environ.get("LQRO_CPU_THREADS", "16"))
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    T, NCF = pyoracle.tables(gains["A"], gains["B"], gains["L"], gains["E"], HORIZON)
+    S = pyoracle.sphere(N_POINTS)
+    # calibrate on 1 row per thread, then scale the sample to the target
+    rows = threads
+    t0 = time.perf_counter()
+    pyoracle.step(T, NCF, S, x, vg, rows=(0, rows), threads=threads, records=False)
+    dt = time.perf_counter() - t0
+    more = int(max(0, min(N_AGENTS - rows, (seconds_target - dt) / max(dt, 1e-9) * rows)))
+    more = (more // threads) * threads
+    if more > 0:
+        t0 = time.perf_counter()
+        pyoracle.step(T, NCF, S, x, vg, rows=(rows, rows + more), threads=threads, records=False)
+        dt2 = time.perf_counter() - t0
+        pairs, secs = more * (N_AGENTS - 1), dt2
+        sample = f"rows {rows}..{rows + more - 1} of the C3 step ({pairs} pairs)"
+    else:
+        pairs, secs = rows * (N_AGENTS - 1), dt
+        sample = f"rows 0..{rows - 1} of the C3 step ({pairs} pairs)"
+    return {"value": pairs / secs, "unit": "agent-pair evals/s", "cores": threads,
+            "kind": "port", "sample": sample}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import lqro
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    N = N_AGENTS
+    assert N % world == 0
+    rows = N // world
+    rb, re = rank * rows, (rank + 1) * rows
+    x, vg = lqro.synthetic_swarm(N)
+    gains = lqro.synthesize_gains()
+    ctx = lqro.Context(lqro.config(N, HORIZON, N_POINTS, device=local, row_begin=rb, row_end=re))
+    ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
+    d_x = torch.from_numpy(x).to(dev)
+    d_vg = torch.from_numpy(vg).to(dev)
+    d_newv = torch.zeros((N, 3), dtype=torch.float64, device=dev)
+    full = torch.zeros((N, 3), dtype=torch.float64, device=dev) if world > 1 else d_newv
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        ctx.step_device(d_x.data_ptr(), d_vg.data_ptr(), d_newv.data_ptr(), stream.cuda_stream)
+        if world > 1:
+            dist.all_gather_into_tensor(full, d_newv[rb:re])
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    pair_ms, step_dev_ms = [], []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        tm = ctx.timings()          # HIP events on the launch stream (waits for this step)
+        pair_ms.append(tm["pair_ms"])
+        step_dev_ms.append(tm["step_ms"])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    st = ctx.stats()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        c = torch.tensor([st["inside"], st["hull_fail"]], dtype=torch.int64, device=dev)
+        dist.all_reduce(c)
+        st["inside"], st["hull_fail"] = int(c[0]), int(c[1])
+
+    pairs_step = N * (N - 1)
+    value = pairs_step * args.steps / elapsed
+    ms_step = elapsed / args.steps * 1e3
+    # roofline of the dominant kernel (k_pair), per launch on this rank
+    pk_ms = float(np.mean(pair_ms))
+    pairs_launch = rows * (N - 1)
+    tflops = sweep_flops_per_pair() * pairs_launch / (pk_ms * 1e-3) / 1e12
+    gbs = algorithmic_bytes_per_pair() * pairs_launch / (pk_ms * 1e-3) / 1e9
+    out = {
+        "metric": "agent-pair LQR-obstacle evals/sec",
+        "value": value,
+        "unit": "agent-pair evals/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (SplitMix64 swarm, seed 0x4C51524F, constant density)",
+        "config": {
+            "workload": "C3: 1024 quadrotors, horizon 100, 100 points/ellipsoid, 16-D state; "
+                        "reference-exact fp64 pair sweep+GJK+hull+half-plane, fp32 LP",
+            "n_agents": N, "horizon": HORIZON, "n_points": N_POINTS, "x_dim": X_DIM,
+            "pairs_per_step": pairs_step,
+            "parallelism": f"rows sharded over {world} rank(s)" +
+                           (" + RCCL all-gather of newV" if world > 1 else ""),
+        },
+        "roofline": {
+            "bound": "valu-fp64",
+            "kernel": "k_pair",
+            "achieved": tflops,
+            "peak": FP64_VALU_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": tflops / FP64_VALU_PEAK_TFLOPS,
+            "traffic": None,
+            "flops_per_pair": sweep_flops_per_pair(),
+            "pairs_per_launch": pairs_launch,
+            "kernel_ms": pk_ms,
+            "hbm_algorithmic_gbs": gbs,
+            "hbm_frac": gbs / HBM_PEAK_GBS,
+        },
+        "step_device_ms": float(np.mean(step_dev_ms)),
+        "inside_hull_pairs_per_step": st["inside"],
+        "hull_failures": st["hull_fail"],
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cb = cpu_baseline(x, vg, gains)
+        out["cpu_baseline"] = cb
+        out["gpu_over_cpu"] = value / cb["value"]
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -86,7 +86,7 @@ typedef struct lqro_pair_record {
   int32_t simplex[4];     /* final GJK simplex: indices into reachablePoints */
   int32_t facet[3];       /* hull branch: arg-min facet (reachable indices)  */
   int32_t n_facets;       /* hull branch: number of hull facets              */
-  uint64_t reach_hash;    /* FNV-1a over the reachable index list            */
+  uint64_t reach_hash;    /* sum of splitmix64(q) over reachable point ids q */
   double dist;            /* distance before the *0.5 of LQRO:1416           */
   double normal[3];       /* normalVector fed to createHalfPlanes            */
   double wpt_vrel[3];     /* GJK witness on the vrel point                   */
@@ -135,6 +135,13 @@ int lqro_step(lqro_ctx* ctx, const double* x, const double* vgoal, double* newv)
  * the context's own stream) and the call returns without synchronising. */
 int lqro_step_device(lqro_ctx* ctx, const double* d_x, const double* d_vgoal,
                      double* d_newv, void* stream);
+
+/* calculateNewV (LQRO:1223-1234) for a batch of independent agents on the
+ * GPU: agent r's planes are planes[offsets[r] .. offsets[r+1]) (6 floats
+ * each: point xyz, normal xyz, in orcaPlanes_ push order), its preferred
+ * velocity vgoal[3r..3r+2]; writes newv[3r..3r+2].  Synchronous. */
+int lqro_calculate_new_v(const float* planes, const int64_t* offsets, int32_t n_agents,
+                         const double* vgoal, double vmax_lp, double* newv, int32_t device);
 
 /* Per-pair records of the last step (LQRO_FLAG_RECORDS): rows
  * [row_begin,row_end) x (n_agents-1) neighbours in j order. */

@@ -29,6 +29,7 @@
 
 #include "../../include/lqro.h"
 #include "lqro_device.hpp"
+#include "lqro_lp.hpp"
 
 using namespace lqro;
 
@@ -1043,184 +1044,58 @@ __global__ void __launch_bounds__(HULL_THREADS) k_hull(HullArgs A) {
 }
 
 // ---------------------------------------------------------------------------
-// LP kernel: one thread per row agent, fp32 RVO2-3D LP (:1001-1234)
+// LP kernel: one wavefront per row agent (lqro_lp.hpp), fp32 as the reference
 // ---------------------------------------------------------------------------
-struct v3 { float x, y, z; };
-__device__ __forceinline__ v3 V3(float x, float y, float z) { v3 r; r.x = x; r.y = y; r.z = z; return r; }
-__device__ __forceinline__ float vdot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-__device__ __forceinline__ v3 vadd(v3 a, v3 b) { return V3(a.x + b.x, a.y + b.y, a.z + b.z); }
-__device__ __forceinline__ v3 vsub(v3 a, v3 b) { return V3(a.x - b.x, a.y - b.y, a.z - b.z); }
-__device__ __forceinline__ v3 vmul(v3 a, float s) { return V3(a.x * s, a.y * s, a.z * s); }
-__device__ __forceinline__ v3 smul(float s, v3 a) { return V3(s * a.x, s * a.y, s * a.z); }
-__device__ __forceinline__ v3 vcross(v3 a, v3 b) {
-  return V3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
-}
-__device__ __forceinline__ v3 vnormalize(v3 a) {
-  float l = sqrtf(vdot(a, a));
-  const float inv = 1.0f / l;
-  return V3(a.x * inv, a.y * inv, a.z * inv);
-}
-__device__ __forceinline__ float sqrf(float s) { return s * s; }
-#define RVO_EPS 0.00001f
-
-struct LPPlane { v3 point, normal; };
-
-__device__ __forceinline__ LPPlane ld_plane(const float* p) {
-  LPPlane r;
-  r.point = V3(p[0], p[1], p[2]);
-  r.normal = V3(p[3], p[4], p[5]);
-  return r;
-}
-
-// planes: stride 8 floats
-__device__ bool d_lp1(const float* planes, int planeNo, v3 lpt, v3 ldir, float radius, v3 opt,
-                      bool dirOpt, v3& result) {
-  const float dotProduct = vdot(lpt, ldir);
-  const float disc = sqrf(dotProduct) + sqrf(radius) - vdot(lpt, lpt);
-  if (disc < 0.0f) return false;
-  const float sq = sqrtf(disc);
-  float tLeft = -dotProduct - sq;
-  float tRight = -dotProduct + sq;
-  for (int i = 0; i < planeNo; ++i) {
-    LPPlane pi = ld_plane(planes + 8 * (size_t)i);
-    const float numerator = vdot(vsub(pi.point, lpt), pi.normal);
-    const float denominator = vdot(ldir, pi.normal);
-    if (sqrf(denominator) <= RVO_EPS) {
-      if (numerator > 0.0f) return false;
-      continue;
-    }
-    const float t = numerator / denominator;
-    if (denominator >= 0.0f) tLeft = (tLeft < t) ? t : tLeft;
-    else tRight = (t < tRight) ? t : tRight;
-    if (tLeft > tRight) return false;
-  }
-  if (dirOpt) {
-    if (vdot(opt, ldir) > 0.0f) result = vadd(lpt, smul(tRight, ldir));
-    else result = vadd(lpt, smul(tLeft, ldir));
-  } else {
-    const float t = vdot(ldir, vsub(opt, lpt));
-    if (t < tLeft) result = vadd(lpt, smul(tLeft, ldir));
-    else if (t > tRight) result = vadd(lpt, smul(tRight, ldir));
-    else result = vadd(lpt, smul(t, ldir));
-  }
-  return true;
-}
-
-__device__ bool d_lp2(const float* planes, int planeNo, float radius, v3 opt, bool dirOpt, v3& result) {
-  const LPPlane pn = ld_plane(planes + 8 * (size_t)planeNo);
-  const float planeDist = vdot(pn.point, pn.normal);
-  const float planeDistSq = sqrf(planeDist);
-  const float radiusSq = sqrf(radius);
-  if (planeDistSq > radiusSq) return false;
-  const float planeRadiusSq = radiusSq - planeDistSq;
-  const v3 planeCenter = smul(planeDist, pn.normal);
-  if (dirOpt) {
-    const v3 pov = vsub(opt, smul(vdot(opt, pn.normal), pn.normal));
-    const float povSq = vdot(pov, pov);
-    if (povSq <= RVO_EPS) result = planeCenter;
-    else result = vadd(planeCenter, smul(sqrtf(planeRadiusSq / povSq), pov));
-  } else {
-    result = vadd(opt, smul(vdot(vsub(pn.point, opt), pn.normal), pn.normal));
-    if (vdot(result, result) > radiusSq) {
-      const v3 pr = vsub(result, planeCenter);
-      const float prSq = vdot(pr, pr);
-      result = vadd(planeCenter, smul(sqrtf(planeRadiusSq / prSq), pr));
-    }
-  }
-  for (int i = 0; i < planeNo; ++i) {
-    const LPPlane pi = ld_plane(planes + 8 * (size_t)i);
-    if (vdot(pi.normal, vsub(pi.point, result)) > 0.0f) {
-      v3 cp = vcross(pi.normal, pn.normal);
-      if (vdot(cp, cp) <= RVO_EPS) return false;
-      v3 ldir = vnormalize(cp);
-      const v3 lineNormal = vcross(ldir, pn.normal);
-      v3 lpt = vadd(pn.point, smul(vdot(vsub(pi.point, pn.point), pi.normal) / vdot(lineNormal, pi.normal),
-                                   lineNormal));
-      if (!d_lp1(planes, i, lpt, ldir, radius, opt, dirOpt, result)) return false;
-    }
-  }
-  return true;
-}
-
-__device__ int d_lp3(const float* planes, int m, double radius, v3 opt, bool dirOpt, v3& result) {
-  const float rf = (float)radius;
-  if (dirOpt) result = vmul(opt, rf);
-  else if (vdot(opt, opt) > sqrf(rf)) result = vmul(vnormalize(opt), rf);
-  else result = opt;
-  for (int i = 0; i < m; ++i) {
-    const LPPlane pi = ld_plane(planes + 8 * (size_t)i);
-    if (vdot(pi.normal, vsub(pi.point, result)) > 0.0f) {
-      const v3 tmp = result;
-      if (!d_lp2(planes, i, rf, opt, dirOpt, result)) { result = tmp; return i; }
-    }
-  }
-  return m;
-}
-
-__device__ void d_lp4(const float* planes, int m, int beginPlane, float radius, v3& result,
-                      float* scratch) {
-  float distance = 0.0f;
-  for (int i = beginPlane; i < m; ++i) {
-    const LPPlane pi = ld_plane(planes + 8 * (size_t)i);
-    if (vdot(pi.normal, vsub(pi.point, result)) > distance) {
-      int np = 0;
-      for (int j = 0; j < i; ++j) {
-        const LPPlane pj = ld_plane(planes + 8 * (size_t)j);
-        v3 ppt, pnm;
-        const v3 cp = vcross(pj.normal, pi.normal);
-        if (vdot(cp, cp) <= RVO_EPS) {
-          if (vdot(pi.normal, pj.normal) > 0.0f) continue;
-          ppt = smul(0.5f, vadd(pi.point, pj.point));
-        } else {
-          const v3 lineNormal = vcross(cp, pi.normal);
-          ppt = vadd(pi.point, smul(vdot(vsub(pj.point, pi.point), pj.normal) / vdot(lineNormal, pj.normal),
-                                    lineNormal));
-        }
-        pnm = vnormalize(vsub(pj.normal, pi.normal));
-        float* d = scratch + 8 * (size_t)np;
-        d[0] = ppt.x; d[1] = ppt.y; d[2] = ppt.z; d[3] = pnm.x; d[4] = pnm.y; d[5] = pnm.z;
-        np++;
-      }
-      const v3 tmp = result;
-      if (d_lp3(scratch, np, radius, pi.normal, true, result) < np) result = tmp;
-      distance = vdot(pi.normal, vsub(pi.point, result));
-    }
-  }
-}
-
 struct LpArgs {
   int npr, nrows, row_begin;
   double vmax;
-  float* planes;        // compacted in place, per row
-  float* scratch;       // per row npr*8
+  const float* slots;   // per row npr x 8 (flag in [6]: 1 = plane)
+  float* compact;       // per row npr x 8: emitted planes in j order
+  float* proj;          // per row npr x 8: linearProgram4's projected planes
   const double* vgoal;
   double* newv;
 };
 
-__global__ void __launch_bounds__(64) k_lp(LpArgs A) {
-  const int lrow = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(256) k_lp(LpArgs A) {
+  const int lane = threadIdx.x & 63;
+  const int lrow = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (lrow >= A.nrows) return;
   const int i = A.row_begin + lrow;
-  float* rowp = A.planes + (size_t)lrow * A.npr * 8;
-  // compact emitted planes in j order (orcaPlanes_ push order, :1220)
+  const float* src = A.slots + (size_t)lrow * A.npr * 8;
+  float* planes = A.compact + (size_t)lrow * A.npr * 8;
+  // orcaPlanes_ in push order (j order, LQRObstacles.cpp:1220)
   int m = 0;
-  for (int s = 0; s < A.npr; ++s) {
-    const float* src = rowp + 8 * (size_t)s;
-    if (__float_as_int(src[6]) == 1) {
-      if (m != s) {
-        float* dst = rowp + 8 * (size_t)m;
-        for (int q = 0; q < 8; ++q) dst[q] = src[q];
-      }
-      m++;
+  for (int base = 0; base < A.npr; base += 64) {
+    const int sidx = base + lane;
+    float4 a = make_float4(0, 0, 0, 0), b = make_float4(0, 0, 0, 0);
+    bool f = false;
+    if (sidx < A.npr) {
+      const float4* p = reinterpret_cast<const float4*>(src + 8 * (size_t)sidx);
+      a = p[0];
+      b = p[1];
+      f = __float_as_int(b.z) == 1;
     }
+    const unsigned long long bal = __ballot(f);
+    if (f) {
+      float4* d = reinterpret_cast<float4*>(planes + 8 * (size_t)(m + __popcll(bal & ((1ull << lane) - 1ull))));
+      d[0] = a;
+      d[1] = b;
+    }
+    m += __popcll(bal);
   }
-  v3 pref = V3((float)A.vgoal[3 * i], (float)A.vgoal[3 * i + 1], (float)A.vgoal[3 * i + 2]);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  const v3 pref = V3((float)A.vgoal[3 * i], (float)A.vgoal[3 * i + 1], (float)A.vgoal[3 * i + 2]);
   v3 nv = V3(0.0f, 0.0f, 0.0f);
-  int fail = d_lp3(rowp, m, A.vmax, pref, false, nv);
-  if (fail < m) d_lp4(rowp, m, fail, (float)A.vmax, nv, A.scratch + (size_t)lrow * A.npr * 8);
-  A.newv[3 * i] = nv.x;
-  A.newv[3 * i + 1] = nv.y;
-  A.newv[3 * i + 2] = nv.z;
+  const int fail = w_lp3(planes, m, A.vmax, pref, false, nv, lane);          // :1228
+  if (fail < m)
+    w_lp4(planes, m, fail, (float)A.vmax, nv, A.proj + (size_t)lrow * A.npr * 8, lane);  // :1230
+  if (lane == 0) {
+    A.newv[3 * i] = nv.x;
+    A.newv[3 * i + 1] = nv.y;
+    A.newv[3 * i + 2] = nv.z;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1234,7 +1109,7 @@ struct lqro_ctx {
   hipEvent_t ev[5];
   double *d_T, *d_NCF, *d_S, *d_x, *d_vgoal, *d_newv;
   double *d_A, *d_B, *d_L, *d_E;
-  float *d_planes, *d_lpscratch;
+  float *d_planes, *d_lpscratch, *d_lpcompact;
   lqro_pair_record* d_recs;
   int *d_hq, *d_hcount, *d_hnext, *d_err;
   double* d_hscratch;
@@ -1296,7 +1171,7 @@ void lqro_destroy(lqro_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->cfg.device);
   void* ps[] = {c->d_T, c->d_NCF, c->d_S, c->d_x, c->d_vgoal, c->d_newv, c->d_A, c->d_B,
-                c->d_L, c->d_E, c->d_planes, c->d_lpscratch, c->d_recs, c->d_hq, c->d_hcount,
+                c->d_L, c->d_E, c->d_planes, c->d_lpscratch, c->d_lpcompact, c->d_recs, c->d_hq, c->d_hcount,
                 c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats};
   for (void* p : ps)
     if (p) (void)hipFree(p);
@@ -1324,6 +1199,7 @@ static int ctx_alloc(lqro_ctx* c) {
   HIPCHK(hipMalloc(&c->d_NCF, sizeof(double) * N * H * 3 * X));
   HIPCHK(hipMalloc(&c->d_planes, sizeof(float) * 8 * (slots ? slots : 1)));
   HIPCHK(hipMalloc(&c->d_lpscratch, sizeof(float) * 8 * (slots ? slots : 1)));
+  HIPCHK(hipMalloc(&c->d_lpcompact, sizeof(float) * 8 * (slots ? slots : 1)));
   if (g.flags & LQRO_FLAG_RECORDS)
     HIPCHK(hipMalloc(&c->d_recs, sizeof(lqro_pair_record) * (slots ? slots : 1)));
   c->hull_cap = (int)(slots < (1u << 22) ? slots : (1u << 22));
@@ -1476,8 +1352,9 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   HIPCHK(hipEventRecord(c->ev[2], s));
   LpArgs La;
   La.npr = c->npr; La.nrows = c->nrows; La.row_begin = c->rb; La.vmax = g.vmax_lp;
-  La.planes = c->d_planes; La.scratch = c->d_lpscratch; La.vgoal = d_vgoal; La.newv = d_newv;
-  hipLaunchKernelGGL(k_lp, dim3((unsigned)((c->nrows + 63) / 64)), dim3(64), 0, s, La);
+  La.slots = c->d_planes; La.compact = c->d_lpcompact; La.proj = c->d_lpscratch;
+  La.vgoal = d_vgoal; La.newv = d_newv;
+  hipLaunchKernelGGL(k_lp, dim3((unsigned)((c->nrows + 3) / 4)), dim3(256), 0, s, La);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev[3], s));
   return LQRO_OK;
@@ -1509,6 +1386,52 @@ int lqro_step(lqro_ctx* c, const double* x, const double* vgoal, double* newv) {
   HIPCHK(hipMemcpy(&hc, c->d_hcount, sizeof(int), hipMemcpyDeviceToHost));
   if (hc > c->hull_cap) return LQRO_E_OVERFLOW;
   return LQRO_OK;
+}
+
+int lqro_calculate_new_v(const float* planes, const int64_t* offsets, int32_t n_agents,
+                         const double* vgoal, double vmax_lp, double* newv, int32_t device) {
+  if (!planes || !offsets || !vgoal || !newv || n_agents <= 0) return LQRO_E_ARG;
+  HIPCHK(hipSetDevice(device));
+  int64_t mmax = 1;
+  for (int r = 0; r < n_agents; ++r) {
+    const int64_t m = offsets[r + 1] - offsets[r];
+    if (m < 0) return LQRO_E_ARG;
+    if (m > mmax) mmax = m;
+  }
+  const size_t slots = (size_t)n_agents * (size_t)mmax;
+  std::vector<float> h(slots * 8, 0.0f);
+  for (int r = 0; r < n_agents; ++r)
+    for (int64_t k = offsets[r]; k < offsets[r + 1]; ++k) {
+      float* d = &h[((size_t)r * mmax + (size_t)(k - offsets[r])) * 8];
+      for (int q = 0; q < 6; ++q) d[q] = planes[6 * k + q];
+      int one = 1;
+      memcpy(&d[6], &one, 4);
+    }
+  float *d_slots = nullptr, *d_compact = nullptr, *d_proj = nullptr;
+  double *d_vg = nullptr, *d_nv = nullptr;
+  int rc = LQRO_OK;
+  if (hipMalloc(&d_slots, sizeof(float) * 8 * slots) != hipSuccess ||
+      hipMalloc(&d_compact, sizeof(float) * 8 * slots) != hipSuccess ||
+      hipMalloc(&d_proj, sizeof(float) * 8 * slots) != hipSuccess ||
+      hipMalloc(&d_vg, sizeof(double) * 3 * n_agents) != hipSuccess ||
+      hipMalloc(&d_nv, sizeof(double) * 3 * n_agents) != hipSuccess) {
+    rc = LQRO_E_NOMEM;
+  } else if (hipMemcpy(d_slots, h.data(), sizeof(float) * 8 * slots, hipMemcpyHostToDevice) != hipSuccess ||
+             hipMemcpy(d_vg, vgoal, sizeof(double) * 3 * n_agents, hipMemcpyHostToDevice) != hipSuccess) {
+    rc = LQRO_E_HIP;
+  } else {
+    LpArgs La;
+    La.npr = (int)mmax; La.nrows = n_agents; La.row_begin = 0; La.vmax = vmax_lp;
+    La.slots = d_slots; La.compact = d_compact; La.proj = d_proj; La.vgoal = d_vg; La.newv = d_nv;
+    hipLaunchKernelGGL(k_lp, dim3((unsigned)((n_agents + 3) / 4)), dim3(256), 0, 0, La);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(newv, d_nv, sizeof(double) * 3 * n_agents, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = LQRO_E_HIP;
+  }
+  void* ps[] = {d_slots, d_compact, d_proj, d_vg, d_nv};
+  for (void* p : ps)
+    if (p) (void)hipFree(p);
+  return rc;
 }
 
 int lqro_get_records(lqro_ctx* c, lqro_pair_record* out, int64_t cap, int64_t* n_out) {

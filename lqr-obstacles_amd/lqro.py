@@ -71,7 +71,7 @@ EXPORTS = (
     "lqro_config_default", "lqro_model_default", "lqro_synthesize_gains", "lqro_sphere",
     "lqro_create", "lqro_destroy", "lqro_set_gains", "lqro_step", "lqro_step_device",
     "lqro_get_records", "lqro_get_stats", "lqro_get_timings", "lqro_status_string",
-    "lqro_version",
+    "lqro_version", "lqro_calculate_new_v",
 )
 
 _lib = None
@@ -99,6 +99,7 @@ def lib() -> C.CDLL:
         L.lqro_get_records.argtypes = [vp, vp, i64, C.POINTER(i64)]
         L.lqro_get_stats.argtypes = [vp, vp]
         L.lqro_get_timings.argtypes = [vp, vp]
+        L.lqro_calculate_new_v.argtypes = [vp, vp, i32, vp, dbl, vp, i32]
         _lib = L
     return _lib
 
@@ -210,6 +211,25 @@ class Context:
         _check(lib().lqro_get_timings(self._h, _p(t)), "lqro_get_timings")
         return dict(pair_ms=float(t[0]), hull_ms=float(t[1]), lp_ms=float(t[2]),
                     step_ms=float(t[3]))
+
+
+def calculate_new_v(plane_lists, vgoals, vmax_lp: float = 100.0, device: int = 0) -> np.ndarray:
+    """calculateNewV (LQRO:1223-1234) for many agents at once on the GPU.
+    plane_lists: sequence of (m_r, 6) float32 arrays (point, normal) in push
+    order; vgoals: (n, 3)."""
+    n = len(plane_lists)
+    offs = np.zeros(n + 1, dtype=np.int64)
+    for r, p in enumerate(plane_lists):
+        offs[r + 1] = offs[r] + len(p)
+    flat = np.zeros((max(int(offs[-1]), 1), 6), dtype=np.float32)
+    for r, p in enumerate(plane_lists):
+        if len(p):
+            flat[offs[r]:offs[r + 1]] = np.asarray(p, dtype=np.float32).reshape(-1, 6)
+    vg = np.ascontiguousarray(vgoals, dtype=np.float64).reshape(n, 3)
+    out = np.zeros((n, 3))
+    _check(lib().lqro_calculate_new_v(_p(flat), _p(offs), n, _p(vg), vmax_lp, _p(out), device),
+           "lqro_calculate_new_v")
+    return out
 
 
 # ---------------------------------------------------------------------------
