@@ -1,0 +1,433 @@
+// lqro_pair.hpp — the pair kernel: one wavefront per ordered pair (i, j),
+// one workgroup per row agent i (its horizon tables staged in LDS).
+//
+// Reference (LQRObstacles.cpp, "LQRO"):
+//   createObstacle      :770-783  point(k,p) = T_k (s_p + Translate_k),
+//                                 Translate_k = (-C F_k)(x_i - x_j)
+//   findReachableObstacle :786-812 |point - vrel|^2/30^2 < 1, kept in k*NP+p order
+//   pointInHull / run_gjk :814-864 GJK point-to-hull distance (lqro_gjk.hpp)
+//   createHalfPlanes    :1208-1221
+//
+// Work-efficient but exact.  A horizon step k ("slice") holds NP points that
+// lie on the ellipsoid c_k + T_k diag(2r_xy, 2r_xy, 2r_z) S^2, c_k = T_k tr_k.
+// From that ellipsoid the kernel derives, per pair:
+//   * a slice class: every point certainly reachable (IN), certainly not
+//     (OUT), or MIXED — only MIXED slices run the per-point test;
+//   * for a GJK support direction d, an upper bound d.c_k + |S T_k^T d| on
+//     every point value in the slice: slices are evaluated in decreasing bound
+//     order and skipped once their bound is below the best value found.
+// Bounds carry a 1e-9 relative margin (far above fp64 rounding), and every
+// value that is compared or returned is computed exactly as the reference
+// computes it, so n_reach, the reachable list, the support points and hence
+// the GJK result are bit-identical to evaluating every point.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/lqro.h"
+#include "lqro_device.hpp"
+#include "lqro_gjk.hpp"
+
+namespace lqro {
+
+enum : int { kSliceOut = 0, kSliceIn = 1, kSliceMixed = 2 };
+constexpr int kMaxPW = 4;  // NP <= 256 (one 64-bit reachable mask per 64 points)
+
+struct PairArgs {
+  int N, H, NP, PW, min_reach;
+  int row_begin, nrows, npr;          // npr = pairs per row = N-1
+  int blocks_per_row, pairs_per_block, waves;
+  int per_agent;
+  double vmax, r2, r2_lo, r2_hi;      // reachable radius, its square, fast-test bounds
+  double rad0, rad1, rad2, umax;      // sphere semi-axes (2 r_xy, 2 r_xy, 2 r_z); max |u_p|
+  const double* T;                    // per agent H x 9
+  const double* NCF;                  // per agent H x 3 x X
+  const double* R;                    // per agent H: bound on |T_k s_p|
+  const double* TF;                   // per agent H: ||T_k||_F
+  const double* S;                    // NP x 3
+  const unsigned long long* shash;    // H: sum_p mix64(k*NP+p)
+  const double* x;                    // N x X
+  float* planes;                      // nrows*npr x 8
+  lqro_pair_record* recs;             // nullable
+  int* hull_queue;
+  int* hull_count;
+  int hull_cap;
+  unsigned long long* stats;          // 8 counters
+  // LDS layout, in doubles
+  int XP, lds_T, lds_N, lds_S, lds_R, lds_TF, lds_H, lds_wave, wave_doubles;
+};
+
+struct BlockTabs {
+  const double* T;
+  const double* N;
+  const double* S;    // SoA: x[NP], y[NP], z[NP]
+  const double* R;
+  const double* TF;
+  const unsigned long long* shash;
+};
+
+struct WaveTabs {
+  double* tr;                // H x 3
+  double* c;                 // H x 3
+  double* sc;                // H: magnitude scale for the margins
+  double* ub;                // H: support bounds of the current query
+  int* cls;                  // H
+  int* cnt;                  // H: reachable points in the slice
+  int* mixed;                // H: list of MIXED slices
+  unsigned long long* mask;  // H x PW
+};
+
+// Transform*(points[p] + Translate) (LQRO:776); Matrix::operator* accumulates
+// from 0.0 (include/matrix.h:223-227)
+__device__ __forceinline__ void exact_point(const BlockTabs& B, const WaveTabs& W, int NP, int k,
+                                            int p, double* x) {
+  const double* Tk = B.T + 9 * k;
+  const double* tk = W.tr + 3 * k;
+  const double u0 = B.S[p] + tk[0];
+  const double u1 = B.S[NP + p] + tk[1];
+  const double u2 = B.S[2 * NP + p] + tk[2];
+  x[0] = ((0.0 + Tk[0] * u0) + Tk[1] * u1) + Tk[2] * u2;
+  x[1] = ((0.0 + Tk[3] * u0) + Tk[4] * u1) + Tk[5] * u2;
+  x[2] = ((0.0 + Tk[6] * u0) + Tk[7] * u1) + Tk[8] * u2;
+}
+
+// findReachableObstacle's test (LQRO:799), pow(x,2) = x*x; decided by a
+// 1e-12-margin pre-test except near the sphere, where the reference's
+// divisions run literally.
+__device__ __forceinline__ bool reach_exact(double a, double b, double c, const PairArgs& P) {
+  const double t = a * a + b * b + c * c;
+  if (t < P.r2_lo) return true;
+  if (t > P.r2_hi) return false;
+  return (a * a) / P.r2 + (b * b) / P.r2 + (c * c) / P.r2 < 1.0;
+}
+
+__device__ __forceinline__ bool better(double v, int q, double bv, int bq) {
+  return v > bv || (v == bv && q < bq);
+}
+
+__device__ __forceinline__ void wave_argmax(double& v, int& q) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double ov = __shfl_xor(v, off);
+    const int oq = __shfl_xor(q, off);
+    if (better(ov, oq, v, q)) { v = ov; q = oq; }
+  }
+}
+
+struct SliceSupport {
+  const PairArgs& P;
+  const BlockTabs& B;
+  const WaveTabs& W;
+  int lane;
+
+  __device__ void point(int q, double* x) const {
+    const int k = q / P.NP;
+    exact_point(B, W, P.NP, k, q - k * P.NP, x);
+  }
+
+  // best (value, q) over the reachable points of slice k, merged into (bv, bq)
+  __device__ void eval_slice(int k, double d0, double d1, double d2, double& bv, int& bq) const {
+    double lv = -INFINITY;
+    int lq = INT_MAX;
+    for (int pw = 0; pw < P.PW; ++pw) {
+      const int p = pw * 64 + lane;
+      const unsigned long long bits = W.mask[k * P.PW + pw];
+      if (p < P.NP && ((bits >> lane) & 1ull)) {
+        double x[3];
+        exact_point(B, W, P.NP, k, p, x);
+        const double v = x[0] * d0 + x[1] * d1 + x[2] * d2;   // SUPPORT_DOT_PRODUCT
+        const int q = k * P.NP + p;
+        if (better(v, q, lv, lq)) { lv = v; lq = q; }
+      }
+    }
+    wave_argmax(lv, lq);
+    if (better(lv, lq, bv, bq)) { bv = lv; bq = lq; }
+  }
+
+  // support_simple semantics: lowest-index maximiser of p.d over the reachable set
+  __device__ void support(double d0, double d1, double d2, double& bv, int& bq) const {
+    const double dn = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+    for (int k = lane; k < P.H; k += 64) {
+      double ub = -INFINITY;
+      if (W.cls[k] != kSliceOut) {
+        const double* Tk = B.T + 9 * k;
+        const double w0 = Tk[0] * d0 + Tk[3] * d1 + Tk[6] * d2;
+        const double w1 = Tk[1] * d0 + Tk[4] * d1 + Tk[7] * d2;
+        const double w2 = Tk[2] * d0 + Tk[5] * d1 + Tk[8] * d2;
+        const double a0 = P.rad0 * w0, a1 = P.rad1 * w1, a2 = P.rad2 * w2;
+        const double* ck = W.c + 3 * k;
+        ub = ck[0] * d0 + ck[1] * d1 + ck[2] * d2 + sqrt(a0 * a0 + a1 * a1 + a2 * a2) * P.umax +
+             1e-9 * dn * W.sc[k];
+      }
+      W.ub[k] = ub;
+    }
+    wave_lds_sync();
+    bv = -INFINITY;
+    bq = INT_MAX;
+    for (;;) {
+      // next slice: largest bound among those that may still hold a value >= bv
+      double cu = -INFINITY;
+      int ck = INT_MAX;
+      for (int k = lane; k < P.H; k += 64) {
+        const double u = W.ub[k];
+        if (u > -INFINITY && u >= bv && (u > cu || (u == cu && k < ck))) { cu = u; ck = k; }
+      }
+      wave_argmax(cu, ck);
+      if (ck == INT_MAX) break;
+      eval_slice(ck, d0, d1, d2, bv, bq);
+      if (lane == 0) W.ub[ck] = -INFINITY;
+      wave_lds_sync();
+    }
+  }
+};
+
+// rank of point q in the reachable list (the reachablePoints index)
+__device__ inline int reach_rank(const PairArgs& P, const WaveTabs& W, int lane, int q) {
+  const int kq = q / P.NP, pq = q - kq * P.NP;
+  int cnt = 0;
+  for (int k = lane; k < kq; k += 64) cnt += W.cnt[k];
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
+  for (int pw = 0; pw < P.PW; ++pw) {
+    const unsigned long long bits = W.mask[kq * P.PW + pw];
+    const int lo = pw * 64;
+    if (lo + 64 <= pq) cnt += __popcll(bits);
+    else if (lo < pq) cnt += __popcll(bits & ((1ull << (pq - lo)) - 1ull));
+  }
+  return cnt;
+}
+
+template <int X>
+__global__ void __launch_bounds__(1024) k_pair(PairArgs P) {
+  extern __shared__ double lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int lrow = blockIdx.x / P.blocks_per_row;
+  const int chunk = blockIdx.x % P.blocks_per_row;
+  const int i = P.row_begin + lrow;
+  const int H = P.H, NP = P.NP, XP = P.XP;
+
+  // agent i's horizon tables and the sphere, staged once per workgroup
+  const size_t ag = P.per_agent ? (size_t)i : 0;
+  double* sT = lds + P.lds_T;
+  double* sN = lds + P.lds_N;
+  double* sS = lds + P.lds_S;
+  double* sR = lds + P.lds_R;
+  double* sTF = lds + P.lds_TF;
+  unsigned long long* sH = reinterpret_cast<unsigned long long*>(lds + P.lds_H);
+  {
+    const double* Ti = P.T + ag * H * 9;
+    const double* Ni = P.NCF + ag * H * 3 * X;
+    const double* Ri = P.R + ag * H;
+    const double* TFi = P.TF + ag * H;
+    for (int q = threadIdx.x; q < H * 9; q += blockDim.x) sT[q] = Ti[q];
+    for (int q = threadIdx.x; q < H * 3 * X; q += blockDim.x) sN[(q / X) * XP + (q % X)] = Ni[q];
+    for (int q = threadIdx.x; q < NP * 3; q += blockDim.x) sS[(q % 3) * NP + q / 3] = P.S[q];
+    for (int q = threadIdx.x; q < H; q += blockDim.x) {
+      sR[q] = Ri[q];
+      sTF[q] = TFi[q];
+      sH[q] = P.shash[q];
+    }
+  }
+  __syncthreads();
+
+  BlockTabs B;
+  B.T = sT; B.N = sN; B.S = sS; B.R = sR; B.TF = sTF; B.shash = sH;
+  WaveTabs W;
+  {
+    double* w = lds + P.lds_wave + (size_t)wave * P.wave_doubles;
+    W.tr = w;            w += 3 * H;
+    W.c = w;             w += 3 * H;
+    W.sc = w;            w += H;
+    W.ub = w;            w += H;
+    W.mask = reinterpret_cast<unsigned long long*>(w);  w += H * P.PW;
+    int* wi = reinterpret_cast<int*>(w);
+    W.cls = wi;          wi += H;
+    W.cnt = wi;          wi += H;
+    W.mixed = wi;
+  }
+  const double* xi = P.x + (size_t)i * X;
+  const int jj_begin = chunk * P.pairs_per_block;
+  const int jj_end = min(P.npr, jj_begin + P.pairs_per_block);
+  unsigned long long st_reach = 0, st_iters = 0, st_planes = 0, st_inside = 0, st_backup = 0;
+  SliceSupport sup{P, B, W, lane};
+
+  for (int jj = jj_begin + wave; jj < jj_end; jj += P.waves) {
+    const int j = jj < i ? jj : jj + 1;
+    const double* xj = P.x + (size_t)j * X;
+    double d[X];
+#pragma unroll
+    for (int c = 0; c < X; ++c) d[c] = xi[c] - xj[c];                       // (xInit1-xInit2)
+    const double vrel[3] = {xi[3] - xj[3], xi[4] - xj[4], xi[5] - xj[5]};    // :794-796
+    unsigned long long hsh = 0;
+
+    // 1. per slice: Translate (exact), centre, class       (lanes <-> k)
+    for (int k = lane; k < H; k += 64) {
+      const double* nc = B.N + (size_t)k * 3 * XP;
+      double t0 = 0.0, t1 = 0.0, t2 = 0.0;
+#pragma unroll
+      for (int c = 0; c < X; ++c) t0 += nc[c] * d[c];
+#pragma unroll
+      for (int c = 0; c < X; ++c) t1 += nc[XP + c] * d[c];
+#pragma unroll
+      for (int c = 0; c < X; ++c) t2 += nc[2 * XP + c] * d[c];
+      W.tr[3 * k] = t0; W.tr[3 * k + 1] = t1; W.tr[3 * k + 2] = t2;
+      const double* Tk = B.T + 9 * k;
+      const double c0 = Tk[0] * t0 + Tk[1] * t1 + Tk[2] * t2;
+      const double c1 = Tk[3] * t0 + Tk[4] * t1 + Tk[5] * t2;
+      const double c2 = Tk[6] * t0 + Tk[7] * t1 + Tk[8] * t2;
+      W.c[3 * k] = c0; W.c[3 * k + 1] = c1; W.c[3 * k + 2] = c2;
+      const double Rk = B.R[k];
+      const double sc = sqrt(c0 * c0 + c1 * c1 + c2 * c2) + Rk +
+                        B.TF[k] * sqrt(t0 * t0 + t1 * t1 + t2 * t2) + 1.0;
+      W.sc[k] = sc;
+      const double e0 = c0 - vrel[0], e1 = c1 - vrel[1], e2 = c2 - vrel[2];
+      const double dc = sqrt(e0 * e0 + e1 * e1 + e2 * e2);
+      const double slack = 1e-9 * sc;
+      int cls = kSliceMixed;
+      if (dc + Rk < P.vmax - slack) cls = kSliceIn;
+      else if (dc - Rk > P.vmax + slack) cls = kSliceOut;
+      W.cls[k] = cls;
+      for (int pw = 0; pw < P.PW; ++pw) {
+        unsigned long long m = 0;
+        if (cls == kSliceIn) {
+          const int left = NP - pw * 64;
+          m = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
+        }
+        W.mask[k * P.PW + pw] = m;
+      }
+      W.cnt[k] = cls == kSliceIn ? NP : 0;
+      if (cls == kSliceIn) hsh += B.shash[k];
+    }
+    wave_lds_sync();
+
+    // 2. MIXED slices: per-point exact test                 (lanes <-> p)
+    int nmixed = 0;
+    for (int base = 0; base < H; base += 64) {
+      const int k = base + lane;
+      const bool m = k < H && W.cls[k] == kSliceMixed;
+      const unsigned long long bal = __ballot(m);
+      if (m) W.mixed[nmixed + __popcll(bal & ((1ull << lane) - 1ull))] = k;
+      nmixed += __popcll(bal);
+    }
+    wave_lds_sync();
+    for (int mi = 0; mi < nmixed; ++mi) {
+      const int k = W.mixed[mi];
+      int cnt = 0;
+      for (int pw = 0; pw < P.PW; ++pw) {
+        const int p = pw * 64 + lane;
+        bool ok = false;
+        if (p < NP) {
+          double x[3];
+          exact_point(B, W, NP, k, p, x);
+          ok = reach_exact(x[0] - vrel[0], x[1] - vrel[1], x[2] - vrel[2], P);
+        }
+        const unsigned long long bal = __ballot(ok);
+        if (ok) hsh += mix64((uint64_t)(k * NP + p));
+        if (lane == 0) W.mask[k * P.PW + pw] = bal;
+        cnt += __popcll(bal);
+      }
+      if (lane == 0) {
+        W.cnt[k] = cnt;
+        if (cnt == 0) W.cls[k] = kSliceOut;
+      }
+    }
+    wave_lds_sync();
+
+    // n_reach and the first reachable point
+    int n = 0, qfirst = INT_MAX;
+    for (int k = lane; k < H; k += 64) {
+      n += W.cnt[k];
+      if (W.cnt[k] > 0 && qfirst == INT_MAX)
+        for (int pw = 0; pw < P.PW; ++pw) {
+          const unsigned long long bits = W.mask[k * P.PW + pw];
+          if (bits) { qfirst = k * NP + pw * 64 + __ffsll((long long)bits) - 1; break; }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      n += __shfl_xor(n, off);
+      qfirst = min(qfirst, __shfl_xor(qfirst, off));
+      hsh += __shfl_xor(hsh, off);
+    }
+    st_reach += n;
+
+    // 3. GJK and the half-plane
+    int flags = 0;
+    float pl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    double dist = 0.0, nrm[3] = {0, 0, 0};
+    GjkOut go;
+    go.iters = 0; go.backup = 0; go.sqrd = 0;
+    for (int q = 0; q < 3; ++q) { go.w1[q] = 0; go.w2[q] = 0; }
+    GjkState g;
+    g.npts = 0;
+    bool inside = false;
+    if (n > P.min_reach) {                                    // :1409
+      gjk_run(sup, qfirst, n, vrel, g, go);
+      double distance = sqrt(go.sqrd);                          // :843
+      nrm[0] = (go.w1[0] - go.w2[0]) / distance;                // :850-852
+      nrm[1] = (go.w1[1] - go.w2[1]) / distance;
+      nrm[2] = (go.w1[2] - go.w2[2]) / distance;
+      inside = (distance < 0.0001 && distance > -1 * 0.0001);  // :860
+      flags = LQRO_REC_PLANE | (inside ? LQRO_REC_INSIDE : 0) | (go.backup ? LQRO_REC_BACKUP : 0);
+      st_iters += go.iters;
+      st_backup += go.backup;
+      dist = distance;
+      if (!inside) {
+        st_planes += 1;
+        distance *= 0.5;                                        // :1416
+        const double mult = -1.0;                               // :1215
+        pl[0] = (float)(xi[3] + mult * distance * nrm[0]);      // :1217
+        pl[1] = (float)(xi[4] + mult * distance * nrm[1]);
+        pl[2] = (float)(xi[5] + mult * distance * nrm[2]);
+        pl[3] = (float)nrm[0]; pl[4] = (float)nrm[1]; pl[5] = (float)nrm[2];
+        pl[6] = __int_as_float(1);
+      } else {
+        st_inside += 1;
+        pl[6] = __int_as_float(2);                              // completed by k_hull
+      }
+    }
+    const size_t slot = (size_t)lrow * P.npr + jj;
+    int sranks[4] = {-1, -1, -1, -1};
+    if (P.recs != nullptr && g.npts > 0)
+      for (int s = 0; s < 4; ++s)
+        if (s < g.npts) sranks[s] = reach_rank(P, W, lane, g.s2[s]);
+    if (lane == 0) {
+      float4* dst = reinterpret_cast<float4*>(P.planes + slot * 8);
+      dst[0] = make_float4(pl[0], pl[1], pl[2], pl[3]);
+      dst[1] = make_float4(pl[4], pl[5], pl[6], pl[7]);
+      if (inside) {
+        const int qi = atomicAdd(P.hull_count, 1);
+        if (qi < P.hull_cap) P.hull_queue[qi] = (int)slot;
+      }
+      if (P.recs != nullptr) {
+        lqro_pair_record rec;
+        rec.i = i; rec.j = j; rec.n_reach = n; rec.flags = flags;
+        rec.gjk_iters = go.iters; rec.simplex_n = g.npts;
+        for (int s = 0; s < 4; ++s) rec.simplex[s] = sranks[s];
+        rec.facet[0] = rec.facet[1] = rec.facet[2] = -1;
+        rec.n_facets = 0;
+        rec.reach_hash = hsh;
+        rec.dist = dist;
+        for (int q = 0; q < 3; ++q) {
+          rec.normal[q] = nrm[q];
+          rec.wpt_vrel[q] = go.w1[q];
+          rec.wpt_hull[q] = go.w2[q];
+          rec.plane_point[q] = pl[q];
+          rec.plane_normal[q] = pl[3 + q];
+        }
+        P.recs[slot] = rec;
+      }
+    }
+    wave_lds_sync();
+  }
+  if (lane == 0) {
+    atomicAdd(&P.stats[1], st_planes);
+    atomicAdd(&P.stats[2], st_inside);
+    atomicAdd(&P.stats[5], st_backup);
+    atomicAdd(&P.stats[6], st_reach);
+    atomicAdd(&P.stats[7], st_iters);
+  }
+}
+
+}  // namespace lqro

@@ -19,6 +19,7 @@
 // are bit-identical to the reference's CPU path (tests/test_gpu_parity.py).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
 #include <cmath>
 #include <cstdio>
@@ -30,11 +31,11 @@
 #include "../../include/lqro.h"
 #include "lqro_device.hpp"
 #include "lqro_lp.hpp"
+#include "lqro_pair.hpp"
 
 using namespace lqro;
 
 #define LQRO_MAXX 16
-#define PAIR_WAVES 8                 // waves per pair workgroup (one row agent)
 #define HULL_THREADS 256
 #define HULL_FMAX 8192               // face slots per hull workgroup (global scratch)
 #define HULL_VMAX 2048               // visible faces per insertion
@@ -50,7 +51,11 @@ __global__ void __launch_bounds__(256) k_tables(int X, int U, int H, const doubl
                                                 const double* __restrict__ L,
                                                 const double* __restrict__ E, int per_agent,
                                                 double* __restrict__ Tout,
-                                                double* __restrict__ Nout, int* __restrict__ err) {
+                                                double* __restrict__ Nout,
+                                                double* __restrict__ Rout,
+                                                double* __restrict__ TFout, double rad0,
+                                                double rad1, double rad2, double umax,
+                                                int* __restrict__ err) {
   __shared__ double sAt[LQRO_MAXX * LQRO_MAXX], sBt[LQRO_MAXX * 3];
   __shared__ double sF[LQRO_MAXX * LQRO_MAXX], sG[LQRO_MAXX * 3];
   __shared__ double sFn[LQRO_MAXX * LQRO_MAXX], sGn[LQRO_MAXX * 3];
@@ -123,472 +128,19 @@ __global__ void __launch_bounds__(256) k_tables(int X, int U, int H, const doubl
         Ta[(size_t)k * 9 + q] = inv[q];
         if (!isfinite(inv[q])) atomicOr(err, 1);
       }
+      // slice bounds for k_pair: |T_k s_p| <= ||T_k diag(rad)||_F * max|u_p|
+      const double rad[3] = {rad0, rad1, rad2};
+      double fr = 0.0, ff = 0.0;
+      for (int rr = 0; rr < 3; ++rr)
+        for (int cc = 0; cc < 3; ++cc) {
+          const double tv = inv[rr * 3 + cc];
+          fr += (tv * rad[cc]) * (tv * rad[cc]);
+          ff += tv * tv;
+        }
+      Rout[(size_t)agent * H + k] = sqrt(fr) * umax * (1.0 + 1e-12);
+      TFout[(size_t)agent * H + k] = sqrt(ff);
     }
     __syncthreads();
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Pair kernel
-// ---------------------------------------------------------------------------
-struct PairArgs {
-  int N, X, H, NP, min_reach;
-  int row_begin, nrows, npr;        // npr = pairs per row = N-1
-  int blocks_per_row, pairs_per_block;
-  int per_agent;
-  int chunks, words;                // ceil(H*NP/64), ceil(chunks/32)
-  double r2, r2_lo, r2_hi;          // vmax_reach^2 and the fast-test bounds
-  const double* T;
-  const double* NCF;
-  const double* S;                  // NP x 3
-  const double* x;                  // N x X
-  float* planes;                    // nrows*npr x 8
-  lqro_pair_record* recs;           // nullable
-  int* hull_queue;
-  int* hull_count;
-  int hull_cap;
-  unsigned long long* stats;        // 8 counters
-  int lds_T, lds_N, lds_S, lds_wave, wave_doubles, XP;
-};
-
-struct PairLds {
-  const double* sT;    // H x 9
-  const double* sN;    // H x 3 x XP
-  const double* sS;    // 3 x NP (SoA)
-  double* tr;          // H x 3 (this wave)
-  uint32_t* mask;      // words x 64 (this wave)
-};
-
-// exact reachable test of findReachableObstacle (:799): the fast bounds
-// decide unless the point is within 1e-12 (relative) of the sphere, where the
-// reference's three divisions are evaluated literally.
-__device__ __forceinline__ bool reach_test(double a, double b, double c, const PairArgs& P) {
-  double t = a * a + b * b + c * c;
-  if (t < P.r2_lo) return true;
-  if (t > P.r2_hi) return false;
-  return (a * a) / P.r2 + (b * b) / P.r2 + (c * c) / P.r2 < 1.0;
-}
-
-// Transform*(points[p] + Translate)  (:776), accumulating from 0.0 as
-// Matrix::operator* does.
-__device__ __forceinline__ void obstacle_point(const PairLds& L, int NP, int k, int p, double& x0,
-                                               double& x1, double& x2) {
-  const double* Tk = L.sT + k * 9;
-  const double* tk = L.tr + k * 3;
-  double u0 = L.sS[p] + tk[0];
-  double u1 = L.sS[NP + p] + tk[1];
-  double u2 = L.sS[2 * NP + p] + tk[2];
-  x0 = ((0.0 + Tk[0] * u0) + Tk[1] * u1) + Tk[2] * u2;
-  x1 = ((0.0 + Tk[3] * u0) + Tk[4] * u1) + Tk[5] * u2;
-  x2 = ((0.0 + Tk[6] * u0) + Tk[7] * u1) + Tk[8] * u2;
-}
-
-// point q (k*NP + p) computed uniformly in every lane
-__device__ __forceinline__ void point_q(const PairLds& L, int NP, int q, double* pt) {
-  obstacle_point(L, NP, q / NP, q % NP, pt[0], pt[1], pt[2]);
-}
-
-// Support of the reachable set in direction d: the first (lowest index)
-// maximiser of p.d, as support_simple's strict '>' scan (gjk.cpp:770-794).
-__device__ void support_scan(const PairLds& L, const PairArgs& P, int lane, int qfirst, double d0,
-                             double d1, double d2, double& bestv, int& bestq) {
-  double bv = -INFINITY;
-  int bq = INT_MAX;
-  int k = lane / P.NP, p = lane % P.NP;
-  for (int w = 0; w < P.words; ++w) {
-    uint32_t bits = L.mask[w * kWave + lane];
-    if (__ballot(bits != 0) == 0) {
-      int adv = 32 * kWave;
-      p += adv;
-      k += p / P.NP;
-      p %= P.NP;
-      continue;
-    }
-    for (int b = 0; b < 32; ++b) {
-      if (bits & (1u << b)) {
-        double x0, x1, x2;
-        obstacle_point(L, P.NP, k, p, x0, x1, x2);
-        double v = x0 * d0 + x1 * d1 + x2 * d2;
-        if (v > bv) { bv = v; bq = (w * 32 + b) * kWave + lane; }
-      }
-      p += kWave;
-      while (p >= P.NP) { p -= P.NP; ++k; }
-    }
-  }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    double ov = __shfl_xor(bv, off);
-    int oq = __shfl_xor(bq, off);
-    if (ov > bv || (ov == bv && oq < bq)) { bv = ov; bq = oq; }
-  }
-  // sequential semantics when the first point's value is NaN: nothing beats it
-  double f[3];
-  point_q(L, P.NP, qfirst, f);
-  double vf = f[0] * d0 + f[1] * d1 + f[2] * d2;
-  if (isnan(vf) || bq == INT_MAX) { bv = vf; bq = qfirst; }
-  bestv = bv;
-  bestq = bq;
-}
-
-// rank of reachable point q in the reachable list (= reachablePoints index)
-__device__ int reach_rank(const PairLds& L, const PairArgs& P, int lane, int q) {
-  int mt = q / kWave, lt = q % kWave;
-  int cnt = 0;
-  for (int w = 0; w < P.words; ++w) {
-    uint32_t bits = L.mask[w * kWave + lane];
-    int lo = w * 32;
-    if (lo + 32 <= mt) cnt += __popc(bits);
-    else if (lo <= mt) {
-      int nb = mt - lo;               // chunks before mt in this word
-      uint32_t below = nb >= 32 ? bits : (bits & ((1u << nb) - 1u));
-      cnt += __popc(below);
-      if (lane < lt && ((bits >> nb) & 1u)) cnt += 1;
-    }
-  }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
-  return cnt;
-}
-
-// --- GJK (gjk.cpp), run uniformly by every lane of the wave -----------------
-__constant__ int g_card[16] = {0, 1, 1, 2, 1, 2, 2, 3, 1, 2, 2, 3, 2, 3, 3, 4};
-__constant__ int g_maxe[16] = {-1, 0, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 3, 3, 3, 3};
-__constant__ int g_elts[16][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {1, 0, 0, 0}, {0, 1, 0, 0},
-                                  {2, 0, 0, 0}, {0, 2, 0, 0}, {1, 2, 0, 0}, {0, 1, 2, 0},
-                                  {3, 0, 0, 0}, {0, 3, 0, 0}, {1, 3, 0, 0}, {0, 1, 3, 0},
-                                  {2, 3, 0, 0}, {0, 2, 3, 0}, {1, 2, 3, 0}, {0, 1, 2, 3}};
-__constant__ int g_nonelts[16][4] = {{0, 1, 2, 3}, {1, 2, 3, 0}, {0, 2, 3, 0}, {2, 3, 0, 0},
-                                     {0, 1, 3, 0}, {1, 3, 0, 0}, {0, 3, 0, 0}, {3, 0, 0, 0},
-                                     {0, 1, 2, 0}, {1, 2, 0, 0}, {0, 2, 0, 0}, {2, 0, 0, 0},
-                                     {0, 1, 0, 0}, {1, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
-__constant__ int g_pred[16][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {2, 1, 0, 0},
-                                  {0, 0, 0, 0}, {4, 1, 0, 0}, {4, 2, 0, 0}, {6, 5, 3, 0},
-                                  {0, 0, 0, 0}, {8, 1, 0, 0}, {8, 2, 0, 0}, {10, 9, 3, 0},
-                                  {8, 4, 0, 0}, {12, 9, 5, 0}, {12, 10, 6, 0}, {14, 13, 11, 7}};
-__constant__ int g_succ[16][4] = {{1, 2, 4, 8}, {3, 5, 9, 0}, {3, 6, 10, 0}, {7, 11, 0, 0},
-                                  {5, 6, 12, 0}, {7, 13, 0, 0}, {7, 14, 0, 0}, {15, 0, 0, 0},
-                                  {9, 10, 12, 0}, {11, 13, 0, 0}, {11, 14, 0, 0}, {15, 0, 0, 0},
-                                  {13, 14, 0, 0}, {15, 0, 0, 0}, {15, 0, 0, 0}, {0, 0, 0, 0}};
-
-struct GjkState {
-  int npts;
-  int s2[4];          // point ids (q) of the hull-side simplex vertices
-  double lambdas[4];
-  double c1[4][3], c2[4][3];
-  double dv[16][4];
-  double dp[4][4];
-  double dsum[16];
-};
-
-__device__ void gjk_subterms(GjkState& g) {
-  const int size = g.npts;
-  double csp[4][3];
-  for (int i = 0; i < size; i++)
-    for (int j = 0; j < 3; j++) csp[i][j] = g.c1[i][j] - g.c2[i][j];
-  for (int i = 0; i < size; i++)
-    for (int j = i; j < size; j++)
-      g.dp[i][j] = g.dp[j][i] = csp[i][0] * csp[j][0] + csp[i][1] * csp[j][1] + csp[i][2] * csp[j][2];
-  for (int s = 1; s < 16 && g_maxe[s] < size; s++) {
-    if (g_card[s] <= 1) { g.dv[s][g_elts[s][0]] = 1.0; continue; }
-    if (g_card[s] == 2) {
-      int e0 = g_elts[s][0], e1 = g_elts[s][1];
-      g.dv[s][e0] = g.dp[e1][e1] - g.dp[e1][e0];
-      g.dv[s][e1] = g.dp[e0][e0] - g.dp[e0][e1];
-      continue;
-    }
-    for (int j = 0; j < g_card[s]; j++) {
-      int jelt = g_elts[s][j], jsub = g_pred[s][j];
-      double sum = 0;
-      for (int i = 0; i < g_card[jsub]; i++) {
-        int ielt = g_elts[jsub][i];
-        sum += g.dv[jsub][ielt] * (g.dp[ielt][g_elts[jsub][0]] - g.dp[ielt][jelt]);
-      }
-      g.dv[s][jelt] = sum;
-    }
-  }
-}
-
-__device__ void gjk_reset(GjkState& g, int subset) {
-  for (int j = 0; j < g_card[subset]; j++) {
-    int oldpos = g_elts[subset][j];
-    if (oldpos != j) {
-      g.s2[j] = g.s2[oldpos];
-      for (int i = 0; i < 3; i++) { g.c1[j][i] = g.c1[oldpos][i]; g.c2[j][i] = g.c2[oldpos][i]; }
-    }
-    g.lambdas[j] = g.dv[subset][g_elts[subset][j]] / g.dsum[subset];
-  }
-  g.npts = g_card[subset];
-}
-
-__device__ int gjk_default(GjkState& g) {
-  int s, ok = 0, size = g.npts;
-  for (s = 1; s < 16 && g_maxe[s] < size; s++) {
-    g.dsum[s] = 0.0; ok = 1;
-    for (int j = 0; ok && j < g_card[s]; j++) {
-      if (g.dv[s][g_elts[s][j]] > 0.0) g.dsum[s] += g.dv[s][g_elts[s][j]];
-      else ok = 0;
-    }
-    for (int k = 0; ok && k < size - g_card[s]; k++)
-      if (g.dv[g_succ[s][k]][g_nonelts[s][k]] > 0) ok = 0;
-    if (ok && g.dsum[s] >= 1.0e-20) break;
-  }
-  if (ok) { gjk_reset(g, s); return 1; }
-  return 0;
-}
-
-__device__ void gjk_backup(GjkState& g) {
-  int size = g.npts, bests = 0;
-  double num[16], den[16];
-  for (int s = 1; s < 16 && g_maxe[s] < size; s++) {
-    if (g.dsum[s] <= 0.0) continue;
-    int i;
-    for (i = 0; i < g_card[s]; i++)
-      if (g.dv[s][g_elts[s][i]] <= 0.0) break;
-    if (i < g_card[s]) continue;
-    num[s] = 0.0;
-    for (int j = 0; j < g_card[s]; j++)
-      for (int k = 0; k < g_card[s]; k++)
-        num[s] += (g.dv[s][g_elts[s][j]] * g.dv[s][g_elts[s][k]]) * g.dp[g_elts[s][j]][g_elts[s][k]];
-    den[s] = g.dsum[s] * g.dsum[s];
-    if ((bests < 1) || (num[s] * den[bests] < num[bests] * den[s])) bests = s;
-  }
-  gjk_reset(g, bests);
-}
-
-__device__ __forceinline__ void gjk_point(double* pt, int len, const double (*v)[3], const double* lam) {
-  for (int d = 0; d < 3; d++) {
-    pt[d] = 0;
-    for (int i = 0; i < len; i++) pt[d] += v[i][d] * lam[i];
-  }
-}
-
-struct GjkOut {
-  double sqrd, w1[3], w2[3];
-  int iters, backup;
-};
-
-// gjk_distance (gjk.cpp:296-501) for object 1 = {vrel}, object 2 = the
-// reachable points (support by support_scan).
-__device__ void gjk_run(const PairLds& L, const PairArgs& P, int lane, int qfirst, int n,
-                        const double* vrel, GjkState& g, GjkOut& o) {
-  for (int s = 0; s < 16; ++s) {
-    g.dsum[s] = 0.0;
-    for (int k = 0; k < 4; ++k) g.dv[s][k] = 0.0;
-  }
-  int use_default = 1, first_iteration = 1, max_iterations = n;
-  double oldsqrd = 0.0, sqrd = 0.0;
-  double disp[3], rdisp[3];
-  o.iters = 0; o.backup = 0;
-  g.npts = 1; g.s2[0] = qfirst; g.lambdas[0] = 1.0;
-  {
-    double f[3];
-    point_q(L, P.NP, qfirst, f);
-    for (int d = 0; d < 3; d++) { g.c1[0][d] = vrel[d]; g.c2[0][d] = f[d]; }
-  }
-  while (max_iterations-- > 0) {
-    if (g.npts == 1) g.lambdas[0] = 1.0;
-    else {
-      gjk_subterms(g);
-      if (use_default) use_default = gjk_default(g);
-      if (!use_default) { gjk_backup(g); o.backup = 1; }
-    }
-    gjk_point(o.w1, g.npts, g.c1, g.lambdas);
-    gjk_point(o.w2, g.npts, g.c2, g.lambdas);
-    for (int d = 0; d < 3; d++) { disp[d] = o.w2[d] - o.w1[d]; rdisp[d] = -disp[d]; }
-    sqrd = disp[0] * disp[0] + disp[1] * disp[1] + disp[2] * disp[2];
-    if (sqrd < 1.0e-8) { o.sqrd = sqrd; return; }
-    double maxv = vrel[0] * disp[0] + vrel[1] * disp[1] + vrel[2] * disp[2];
-    double minus_minv;
-    int minq;
-    support_scan(L, P, lane, qfirst, rdisp[0], rdisp[1], rdisp[2], minus_minv, minq);
-    o.iters++;
-    double g_val = sqrd + maxv + minus_minv;
-    if (g_val < 0.0) g_val = 0;
-    if (g_val < 1.0e-8) { o.sqrd = sqrd; return; }
-    if ((first_iteration || (sqrd < oldsqrd)) && (g.npts <= 3)) {
-      double f[3];
-      point_q(L, P.NP, minq, f);
-      int np_ = g.npts;
-      g.s2[np_] = minq;
-      g.lambdas[np_] = 0.0;
-      for (int d = 0; d < 3; d++) { g.c1[np_][d] = vrel[d]; g.c2[np_][d] = f[d]; }
-      g.npts++;
-      oldsqrd = sqrd;
-      first_iteration = 0;
-      use_default = 1;
-      continue;
-    }
-    if (use_default) use_default = 0;
-    else { o.sqrd = sqrd; return; }
-  }
-  o.sqrd = 0.0;
-}
-
-template <int XT>
-__global__ void __launch_bounds__(PAIR_WAVES * 64) k_pair(PairArgs P) {
-  extern __shared__ double lds[];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int lrow = blockIdx.x / P.blocks_per_row;
-  const int chunk = blockIdx.x % P.blocks_per_row;
-  const int i = P.row_begin + lrow;
-  constexpr int X = XT;
-  const int H = P.H, NP = P.NP, XP = P.XP;
-
-  // stage agent i's horizon tables and the sphere into LDS
-  const double* Ti = P.T + (P.per_agent ? (size_t)i * H * 9 : 0);
-  const double* Ni = P.NCF + (P.per_agent ? (size_t)i * H * 3 * X : 0);
-  double* sT = lds + P.lds_T;
-  double* sN = lds + P.lds_N;
-  double* sS = lds + P.lds_S;
-  for (int q = threadIdx.x; q < H * 9; q += blockDim.x) sT[q] = Ti[q];
-  for (int q = threadIdx.x; q < H * 3 * X; q += blockDim.x) {
-    int kr = q / X, c = q % X;
-    sN[kr * XP + c] = Ni[q];
-  }
-  for (int q = threadIdx.x; q < NP * 3; q += blockDim.x) {
-    int p = q / 3, d = q % 3;
-    sS[d * NP + p] = P.S[q];
-  }
-  __syncthreads();
-
-  PairLds L;
-  L.sT = sT; L.sN = sN; L.sS = sS;
-  L.tr = lds + P.lds_wave + (size_t)wave * P.wave_doubles;
-  L.mask = reinterpret_cast<uint32_t*>(L.tr + 3 * H);
-
-  const double* xi = P.x + (size_t)i * X;
-  const int jj_begin = chunk * P.pairs_per_block;
-  const int jj_end = min(P.npr, jj_begin + P.pairs_per_block);
-  unsigned long long st_reach = 0, st_iters = 0, st_planes = 0, st_inside = 0, st_backup = 0;
-
-  for (int jj = jj_begin + wave; jj < jj_end; jj += PAIR_WAVES) {
-    const int j = jj < i ? jj : jj + 1;
-    const double* xj = P.x + (size_t)j * X;
-    double d[X];
-#pragma unroll
-    for (int c = 0; c < X; ++c) d[c] = xi[c] - xj[c];                        // (xInit1-xInit2)
-    const double vrel[3] = {xi[3] - xj[3], xi[4] - xj[4], xi[5] - xj[5]};     // :794-796
-
-    // Translate_k = NCF_k * d for every k (:773): item (k, r) per lane
-    for (int it = lane; it < 3 * H; it += kWave) {
-      const double* row = sN + (size_t)it * XP;
-      double s = 0.0;
-#pragma unroll
-      for (int c = 0; c < X; ++c) s += row[c] * d[c];
-      L.tr[it] = s;
-    }
-    wave_lds_sync();
-
-    // sweep + reachable filter; bit m of lane l <=> point q = 64 m + l
-    int n = 0, qfirst = INT_MAX;
-    uint64_t hsh = 0;
-    {
-      int k = lane / NP, p = lane % NP;
-      for (int w = 0; w < P.words; ++w) {
-        uint32_t bits = 0;
-        for (int b = 0; b < 32; ++b) {
-          const int m = w * 32 + b;
-          if (m >= P.chunks) break;
-          const int q = m * kWave + lane;
-          bool ok = false;
-          if (q < H * NP) {
-            double x0, x1, x2;
-            obstacle_point(L, NP, k, p, x0, x1, x2);
-            ok = reach_test(x0 - vrel[0], x1 - vrel[1], x2 - vrel[2], P);
-          }
-          if (ok) { bits |= 1u << b; hsh += mix64((uint64_t)q); }
-          const unsigned long long bal = __ballot(ok);
-          if (bal) {
-            n += __popcll(bal);
-            if (qfirst == INT_MAX) qfirst = m * kWave + __ffsll((long long)bal) - 1;
-          }
-          p += kWave;
-          while (p >= NP) { p -= NP; ++k; }
-        }
-        L.mask[w * kWave + lane] = bits;
-      }
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) hsh += __shfl_xor(hsh, off);
-    wave_lds_sync();
-    st_reach += n;
-
-    lqro_pair_record rec;
-    const bool want_rec = P.recs != nullptr;
-    int flags = 0;
-    float pl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    double dist = 0.0, nrm[3] = {0, 0, 0};
-    GjkOut go;
-    go.iters = 0; go.backup = 0; go.sqrd = 0;
-    for (int q = 0; q < 3; ++q) { go.w1[q] = 0; go.w2[q] = 0; }
-    GjkState g;
-    g.npts = 0;
-    bool inside = false;
-    if (n > P.min_reach) {                                   // :1409
-      gjk_run(L, P, lane, qfirst, n, vrel, g, go);
-      double distance = sqrt(go.sqrd);                         // :843
-      nrm[0] = (go.w1[0] - go.w2[0]) / distance;               // :850-852
-      nrm[1] = (go.w1[1] - go.w2[1]) / distance;
-      nrm[2] = (go.w1[2] - go.w2[2]) / distance;
-      inside = (distance < 0.0001 && distance > -1 * 0.0001); // :860
-      flags = LQRO_REC_PLANE | (inside ? LQRO_REC_INSIDE : 0) | (go.backup ? LQRO_REC_BACKUP : 0);
-      st_iters += go.iters;
-      st_backup += go.backup;
-      dist = distance;
-      if (!inside) {
-        st_planes += 1;
-        distance *= 0.5;                                       // :1416
-        const double mult = -1.0;                              // :1215
-        pl[0] = (float)(xi[3] + mult * distance * nrm[0]);     // :1217
-        pl[1] = (float)(xi[4] + mult * distance * nrm[1]);
-        pl[2] = (float)(xi[5] + mult * distance * nrm[2]);
-        pl[3] = (float)nrm[0]; pl[4] = (float)nrm[1]; pl[5] = (float)nrm[2];
-        pl[6] = __int_as_float(1);
-      } else {
-        st_inside += 1;
-        pl[6] = __int_as_float(2);                             // filled in by k_hull
-      }
-    }
-    const size_t slot = (size_t)lrow * P.npr + jj;
-    int sranks[4] = {-1, -1, -1, -1};
-    if (want_rec && g.npts > 0)
-      for (int s = 0; s < 4; ++s)
-        if (s < g.npts) sranks[s] = reach_rank(L, P, lane, g.s2[s]);
-    if (lane == 0) {
-      float4* dst = reinterpret_cast<float4*>(P.planes + slot * 8);
-      dst[0] = make_float4(pl[0], pl[1], pl[2], pl[3]);
-      dst[1] = make_float4(pl[4], pl[5], pl[6], pl[7]);
-      if (inside) {
-        int qi = atomicAdd(P.hull_count, 1);
-        if (qi < P.hull_cap) P.hull_queue[qi] = (int)slot;
-      }
-      if (want_rec) {
-        rec.i = i; rec.j = j; rec.n_reach = n; rec.flags = flags;
-        rec.gjk_iters = go.iters; rec.simplex_n = g.npts;
-        for (int s = 0; s < 4; ++s) rec.simplex[s] = sranks[s];
-        rec.facet[0] = rec.facet[1] = rec.facet[2] = -1;
-        rec.n_facets = 0;
-        rec.reach_hash = hsh;
-        rec.dist = dist;
-        for (int q = 0; q < 3; ++q) {
-          rec.normal[q] = nrm[q];
-          rec.wpt_vrel[q] = go.w1[q];
-          rec.wpt_hull[q] = go.w2[q];
-          rec.plane_point[q] = pl[q];
-          rec.plane_normal[q] = pl[3 + q];
-        }
-        P.recs[slot] = rec;
-      }
-    }
-    wave_lds_sync();
-  }
-  if (lane == 0) {
-    atomicAdd(&P.stats[1], st_planes);
-    atomicAdd(&P.stats[2], st_inside);
-    atomicAdd(&P.stats[5], st_backup);
-    atomicAdd(&P.stats[6], st_reach);
-    atomicAdd(&P.stats[7], st_iters);
   }
 }
 
@@ -1103,6 +655,8 @@ __global__ void __launch_bounds__(256) k_lp(LpArgs A) {
 // ---------------------------------------------------------------------------
 struct lqro_ctx {
   lqro_config cfg;
+  double *d_R, *d_TF, umax;
+  unsigned long long* d_shash;
   int rb, re, nrows, npr;
   int have_gains, per_agent;
   hipStream_t stream;
@@ -1170,7 +724,7 @@ void lqro_config_default(lqro_config* c, int32_t n, int32_t h, int32_t np) {
 void lqro_destroy(lqro_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->cfg.device);
-  void* ps[] = {c->d_T, c->d_NCF, c->d_S, c->d_x, c->d_vgoal, c->d_newv, c->d_A, c->d_B,
+  void* ps[] = {c->d_R, c->d_TF, c->d_shash, c->d_T, c->d_NCF, c->d_S, c->d_x, c->d_vgoal, c->d_newv, c->d_A, c->d_B,
                 c->d_L, c->d_E, c->d_planes, c->d_lpscratch, c->d_lpcompact, c->d_recs, c->d_hq, c->d_hcount,
                 c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats};
   for (void* p : ps)
@@ -1197,6 +751,9 @@ static int ctx_alloc(lqro_ctx* c) {
   HIPCHK(hipMalloc(&c->d_E, sizeof(double) * N * g.u_dim * 3));
   HIPCHK(hipMalloc(&c->d_T, sizeof(double) * N * H * 9));
   HIPCHK(hipMalloc(&c->d_NCF, sizeof(double) * N * H * 3 * X));
+  HIPCHK(hipMalloc(&c->d_R, sizeof(double) * N * H));
+  HIPCHK(hipMalloc(&c->d_TF, sizeof(double) * N * H));
+  HIPCHK(hipMalloc(&c->d_shash, sizeof(unsigned long long) * H));
   HIPCHK(hipMalloc(&c->d_planes, sizeof(float) * 8 * (slots ? slots : 1)));
   HIPCHK(hipMalloc(&c->d_lpscratch, sizeof(float) * 8 * (slots ? slots : 1)));
   HIPCHK(hipMalloc(&c->d_lpcompact, sizeof(float) * 8 * (slots ? slots : 1)));
@@ -1243,31 +800,63 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
   if (c->rb < 0 || c->re > g.n_agents || c->rb >= c->re) { delete c; return LQRO_E_ARG; }
   c->nrows = c->re - c->rb;
   c->npr = g.n_agents - 1;
-  // LDS layout of k_pair
+  // LDS layout of k_pair (in doubles): block tables, then one region per wave
   const int H = g.horizon, NP = g.n_points, X = g.x_dim, XP = X + 1;
-  const int chunks = (H * NP + 63) / 64;
-  const int words = (chunks + 31) / 32;
+  if (NP > 64 * kMaxPW) { delete c; return LQRO_E_ARG; }
   int off = 0;
   PairArgs& P = c->pa;
+  P.XP = XP;
+  P.PW = (NP + 63) / 64;
   P.lds_T = off; off += H * 9;
   P.lds_N = off; off += H * 3 * XP;
   P.lds_S = off; off += 3 * NP;
+  P.lds_R = off; off += H;
+  P.lds_TF = off; off += H;
+  P.lds_H = off; off += H;
   P.lds_wave = off;
-  P.wave_doubles = 3 * H + (words * 64 + 1) / 2;
-  off += PAIR_WAVES * P.wave_doubles;
-  c->lds_bytes = off * 8;
-  if (c->lds_bytes > 160 * 1024) {
-    fprintf(stderr, "liblqro: horizon %d x %d points needs %d B of LDS\n", H, NP, c->lds_bytes);
+  // tr 3H, c 3H, sc H, ub H, mask H*PW (u64), cls/cnt/mixed 3H ints
+  P.wave_doubles = 8 * H + H * P.PW + (3 * H + 1) / 2;
+  const int budget = 160 * 1024 / 8;
+  int waves = (budget - off) / P.wave_doubles;
+  if (waves > 16) waves = 16;
+  if (waves < 1) {
+    fprintf(stderr, "liblqro: horizon %d x %d points does not fit in LDS\n", H, NP);
     delete c;
     return LQRO_E_ARG;
   }
-  P.XP = XP;
-  P.chunks = chunks;
-  P.words = words;
+  P.waves = waves;
+  off += waves * P.wave_doubles;
+  c->lds_bytes = off * 8;
   int rc = ctx_alloc(c);
   if (rc) { lqro_destroy(c); return rc; }
   std::vector<double> S(3 * (size_t)NP);
   lqro_sphere(NP, g.xy_radius, g.z_radius, S.data());
+  // max |u_p| with s_p = diag(2r_xy, 2r_xy, 2r_z) u_p (createSpheres, :743-745)
+  {
+    const double rad[3] = {2 * g.xy_radius, 2 * g.xy_radius, 2 * g.z_radius};
+    double um = 0.0;
+    for (int p = 0; p < NP; ++p) {
+      double u2 = 0.0;
+      for (int d = 0; d < 3; ++d) { const double u = S[3 * p + d] / rad[d]; u2 += u * u; }
+      um = std::max(um, std::sqrt(u2));
+    }
+    c->umax = um * (1.0 + 1e-12);
+    P.rad0 = rad[0]; P.rad1 = rad[1]; P.rad2 = rad[2]; P.umax = c->umax;
+  }
+  {
+    std::vector<unsigned long long> sh(H, 0ull);
+    for (int k = 0; k < H; ++k)
+      for (int p = 0; p < NP; ++p) {
+        unsigned long long z = (unsigned long long)(k * NP + p) + 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        sh[k] += z ^ (z >> 31);
+      }
+    if (hipMemcpy(c->d_shash, sh.data(), sizeof(unsigned long long) * H, hipMemcpyHostToDevice) != hipSuccess) {
+      lqro_destroy(c);
+      return LQRO_E_HIP;
+    }
+  }
   if (hipMemcpy(c->d_S, S.data(), sizeof(double) * S.size(), hipMemcpyHostToDevice) != hipSuccess) {
     lqro_destroy(c);
     return LQRO_E_HIP;
@@ -1297,7 +886,8 @@ int lqro_set_gains(lqro_ctx* c, const double* A, const double* B, const double* 
   HIPCHK(hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream));
   hipLaunchKernelGGL(k_tables, dim3((unsigned)na), dim3(256), 0, c->stream, (int)X, (int)U,
                      g.horizon, c->d_A, c->d_B, c->d_L, c->d_E, per_agent ? 1 : 0, c->d_T,
-                     c->d_NCF, c->d_err);
+                     c->d_NCF, c->d_R, c->d_TF, c->pa.rad0, c->pa.rad1, c->pa.rad2, c->umax,
+                     c->d_err);
   HIPCHK(hipGetLastError());
   int err = 0;
   HIPCHK(hipMemcpyAsync(&err, c->d_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
@@ -1312,27 +902,29 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
                         hipStream_t s) {
   const lqro_config& g = c->cfg;
   PairArgs P = c->pa;
-  P.N = g.n_agents; P.X = g.x_dim; P.H = g.horizon; P.NP = g.n_points; P.min_reach = g.min_reach;
+  P.N = g.n_agents; P.H = g.horizon; P.NP = g.n_points; P.min_reach = g.min_reach;
   P.row_begin = c->rb; P.nrows = c->nrows; P.npr = c->npr;
   P.per_agent = c->per_agent;
+  P.vmax = g.vmax_reach;
   P.r2 = g.vmax_reach * g.vmax_reach;
   P.r2_lo = P.r2 * (1.0 - 1e-12);
   P.r2_hi = P.r2 * (1.0 + 1e-12);
-  P.T = c->d_T; P.NCF = c->d_NCF; P.S = c->d_S; P.x = d_x;
+  P.T = c->d_T; P.NCF = c->d_NCF; P.R = c->d_R; P.TF = c->d_TF; P.S = c->d_S;
+  P.shash = c->d_shash; P.x = d_x;
   P.planes = c->d_planes; P.recs = c->d_recs;
   P.hull_queue = c->d_hq; P.hull_count = c->d_hcount; P.hull_cap = c->hull_cap;
   P.stats = c->d_stats;
-  // one workgroup = PAIR_WAVES waves on one row; each wave takes several pairs
-  P.pairs_per_block = PAIR_WAVES * 4;
+  // one workgroup = P.waves wavefronts on one row; each wave takes several pairs
+  P.pairs_per_block = P.waves * 4;
   P.blocks_per_row = (c->npr + P.pairs_per_block - 1) / P.pairs_per_block;
   HIPCHK(hipMemsetAsync(c->d_hcount, 0, sizeof(int) * 2, s));
   HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * 8, s));
   HIPCHK(hipEventRecord(c->ev[0], s));
   const unsigned nblk = (unsigned)P.blocks_per_row * (unsigned)c->nrows;
   if (g.x_dim == 16)
-    hipLaunchKernelGGL(k_pair<16>, dim3(nblk), dim3(PAIR_WAVES * 64), c->lds_bytes, s, P);
+    hipLaunchKernelGGL(k_pair<16>, dim3(nblk), dim3(P.waves * 64), c->lds_bytes, s, P);
   else if (g.x_dim == 12)
-    hipLaunchKernelGGL(k_pair<12>, dim3(nblk), dim3(PAIR_WAVES * 64), c->lds_bytes, s, P);
+    hipLaunchKernelGGL(k_pair<12>, dim3(nblk), dim3(P.waves * 64), c->lds_bytes, s, P);
   else
     return LQRO_E_ARG;
   HIPCHK(hipGetLastError());
