@@ -1,44 +1,47 @@
 // lqro_gjk.hpp — gjk_distance (gjk.cpp:296-501, Cameron's Oxford GJK v2.4)
 // specialised to the call the path makes (run_gjk, LQRObstacles.cpp:814-853):
-// object 1 is the single point vrel (hill climbing on a one-vertex ring
-// returns it), object 2 is the reachable point set with a brute-force
-// support function (support_simple, gjk.cpp:770-794).
+// object 1 is the single point vrel (hill climbing on its one-vertex ring
+// returns it), object 2 is the reachable point set with a brute-force support
+// function (support_simple, gjk.cpp:770-794), no transforms, no seed.
 //
 // The simplex bookkeeping runs redundantly in every lane (all values are
-// wave-uniform); the support query is supplied by the caller and must return
-// the lowest-index maximiser, which is what support_simple's strict '>' scan
-// returns.  Johnson's sub-algorithm (compute_subterms, default_distance,
-// backup_distance, reset_simplex: gjk.cpp:527-736) and the constant subset
-// tables (gjk.cpp:86-160) are restated one-for-one.
+// wave-uniform).  Johnson's sub-algorithm — compute_subterms, default_distance,
+// backup_distance, reset_simplex (gjk.cpp:527-736) over the constant subset
+// tables (gjk.cpp:86-160) — is restated with every loop fully unrolled over
+// the 15 subsets, so all table lookups and state indices are compile-time and
+// the state stays in registers; the arithmetic and its order are unchanged.
+// Object 1's simplex coordinates are all vrel, so coords1[i] is not stored.
 #pragma once
 #include <hip/hip_runtime.h>
 
 namespace lqro {
 
-__constant__ int g_card[16] = {0, 1, 1, 2, 1, 2, 2, 3, 1, 2, 2, 3, 2, 3, 3, 4};
-__constant__ int g_maxe[16] = {-1, 0, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 3, 3, 3, 3};
-__constant__ int g_elts[16][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {1, 0, 0, 0}, {0, 1, 0, 0},
-                                  {2, 0, 0, 0}, {0, 2, 0, 0}, {1, 2, 0, 0}, {0, 1, 2, 0},
-                                  {3, 0, 0, 0}, {0, 3, 0, 0}, {1, 3, 0, 0}, {0, 1, 3, 0},
-                                  {2, 3, 0, 0}, {0, 2, 3, 0}, {1, 2, 3, 0}, {0, 1, 2, 3}};
-__constant__ int g_nonelts[16][4] = {{0, 1, 2, 3}, {1, 2, 3, 0}, {0, 2, 3, 0}, {2, 3, 0, 0},
-                                     {0, 1, 3, 0}, {1, 3, 0, 0}, {0, 3, 0, 0}, {3, 0, 0, 0},
-                                     {0, 1, 2, 0}, {1, 2, 0, 0}, {0, 2, 0, 0}, {2, 0, 0, 0},
-                                     {0, 1, 0, 0}, {1, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
-__constant__ int g_pred[16][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {2, 1, 0, 0},
-                                  {0, 0, 0, 0}, {4, 1, 0, 0}, {4, 2, 0, 0}, {6, 5, 3, 0},
-                                  {0, 0, 0, 0}, {8, 1, 0, 0}, {8, 2, 0, 0}, {10, 9, 3, 0},
-                                  {8, 4, 0, 0}, {12, 9, 5, 0}, {12, 10, 6, 0}, {14, 13, 11, 7}};
-__constant__ int g_succ[16][4] = {{1, 2, 4, 8}, {3, 5, 9, 0}, {3, 6, 10, 0}, {7, 11, 0, 0},
-                                  {5, 6, 12, 0}, {7, 13, 0, 0}, {7, 14, 0, 0}, {15, 0, 0, 0},
-                                  {9, 10, 12, 0}, {11, 13, 0, 0}, {11, 14, 0, 0}, {15, 0, 0, 0},
-                                  {13, 14, 0, 0}, {15, 0, 0, 0}, {15, 0, 0, 0}, {0, 0, 0, 0}};
+struct GjkTab {
+  static constexpr int card[16] = {0, 1, 1, 2, 1, 2, 2, 3, 1, 2, 2, 3, 2, 3, 3, 4};
+  static constexpr int maxe[16] = {-1, 0, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 3, 3, 3, 3};
+  static constexpr int elts[16][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {1, 0, 0, 0}, {0, 1, 0, 0},
+                                      {2, 0, 0, 0}, {0, 2, 0, 0}, {1, 2, 0, 0}, {0, 1, 2, 0},
+                                      {3, 0, 0, 0}, {0, 3, 0, 0}, {1, 3, 0, 0}, {0, 1, 3, 0},
+                                      {2, 3, 0, 0}, {0, 2, 3, 0}, {1, 2, 3, 0}, {0, 1, 2, 3}};
+  static constexpr int nonelts[16][4] = {{0, 1, 2, 3}, {1, 2, 3, 0}, {0, 2, 3, 0}, {2, 3, 0, 0},
+                                         {0, 1, 3, 0}, {1, 3, 0, 0}, {0, 3, 0, 0}, {3, 0, 0, 0},
+                                         {0, 1, 2, 0}, {1, 2, 0, 0}, {0, 2, 0, 0}, {2, 0, 0, 0},
+                                         {0, 1, 0, 0}, {1, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+  static constexpr int pred[16][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {2, 1, 0, 0},
+                                      {0, 0, 0, 0}, {4, 1, 0, 0}, {4, 2, 0, 0}, {6, 5, 3, 0},
+                                      {0, 0, 0, 0}, {8, 1, 0, 0}, {8, 2, 0, 0}, {10, 9, 3, 0},
+                                      {8, 4, 0, 0}, {12, 9, 5, 0}, {12, 10, 6, 0}, {14, 13, 11, 7}};
+  static constexpr int succ[16][4] = {{1, 2, 4, 8}, {3, 5, 9, 0}, {3, 6, 10, 0}, {7, 11, 0, 0},
+                                      {5, 6, 12, 0}, {7, 13, 0, 0}, {7, 14, 0, 0}, {15, 0, 0, 0},
+                                      {9, 10, 12, 0}, {11, 13, 0, 0}, {11, 14, 0, 0}, {15, 0, 0, 0},
+                                      {13, 14, 0, 0}, {15, 0, 0, 0}, {15, 0, 0, 0}, {0, 0, 0, 0}};
+};
 
 struct GjkState {
   int npts;
   int s2[4];          // point ids (q = k*NP + p) of the hull-side simplex vertices
-  double lambdas[4];
-  double c1[4][3], c2[4][3];
+  double lam[4];
+  double c2[4][3];    // coords2 (coords1 are all vrel)
   double dv[16][4];   // delta_values (gjk.cpp:163)
   double dp[4][4];    // dot_products (gjk.cpp:164)
   double dsum[16];    // delta (gjk.cpp:522)
@@ -49,85 +52,151 @@ struct GjkOut {
   int iters, backup;
 };
 
-__device__ inline void gjk_subterms(GjkState& g) {
+// compute_subterms (gjk.cpp:527-581)
+__device__ __forceinline__ void gjk_subterms(GjkState& g, const double* vrel) {
+  using T = GjkTab;
   const int size = g.npts;
   double csp[4][3];
-  for (int i = 0; i < size; i++)
-    for (int j = 0; j < 3; j++) csp[i][j] = g.c1[i][j] - g.c2[i][j];
-  for (int i = 0; i < size; i++)
-    for (int j = i; j < size; j++)
-      g.dp[i][j] = g.dp[j][i] = csp[i][0] * csp[j][0] + csp[i][1] * csp[j][1] + csp[i][2] * csp[j][2];
-  for (int s = 1; s < 16 && g_maxe[s] < size; s++) {
-    if (g_card[s] <= 1) { g.dv[s][g_elts[s][0]] = 1.0; continue; }
-    if (g_card[s] == 2) {
-      int e0 = g_elts[s][0], e1 = g_elts[s][1];
-      g.dv[s][e0] = g.dp[e1][e1] - g.dp[e1][e0];
-      g.dv[s][e1] = g.dp[e0][e0] - g.dp[e0][e1];
-      continue;
-    }
-    for (int j = 0; j < g_card[s]; j++) {
-      int jelt = g_elts[s][j], jsub = g_pred[s][j];
-      double sum = 0;
-      for (int i = 0; i < g_card[jsub]; i++) {
-        int ielt = g_elts[jsub][i];
-        sum += g.dv[jsub][ielt] * (g.dp[ielt][g_elts[jsub][0]] - g.dp[ielt][jelt]);
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++) csp[i][j] = vrel[j] - g.c2[i][j];
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int j = i; j < 4; j++)
+      if (j < size)
+        g.dp[i][j] = g.dp[j][i] = csp[i][0] * csp[j][0] + csp[i][1] * csp[j][1] + csp[i][2] * csp[j][2];
+#pragma unroll
+  for (int s = 1; s < 16; s++) {
+    if (T::maxe[s] < size) {
+      if (T::card[s] <= 1) {
+        g.dv[s][T::elts[s][0]] = 1.0;
+      } else if (T::card[s] == 2) {
+        constexpr int dummy = 0; (void)dummy;
+        const int e0 = T::elts[s][0], e1 = T::elts[s][1];
+        g.dv[s][e0] = g.dp[e1][e1] - g.dp[e1][e0];
+        g.dv[s][e1] = g.dp[e0][e0] - g.dp[e0][e1];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          if (j < T::card[s]) {
+            const int jelt = T::elts[s][j], jsub = T::pred[s][j];
+            double sum = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+              if (i < T::card[jsub]) {
+                const int ielt = T::elts[jsub][i];
+                sum += g.dv[jsub][ielt] * (g.dp[ielt][T::elts[jsub][0]] - g.dp[ielt][jelt]);
+              }
+            g.dv[s][jelt] = sum;
+          }
+        }
       }
-      g.dv[s][jelt] = sum;
     }
   }
 }
 
-__device__ inline void gjk_reset(GjkState& g, int subset) {
-  for (int j = 0; j < g_card[subset]; j++) {
-    int oldpos = g_elts[subset][j];
-    if (oldpos != j) {
-      g.s2[j] = g.s2[oldpos];
-      for (int i = 0; i < 3; i++) { g.c1[j][i] = g.c1[oldpos][i]; g.c2[j][i] = g.c2[oldpos][i]; }
+// reset_simplex (gjk.cpp:708-736) for a subset chosen at run time
+__device__ __forceinline__ void gjk_reset(GjkState& g, int subset) {
+  using T = GjkTab;
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    if (t == subset) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        if (j < T::card[t]) {
+          const int oldpos = T::elts[t][j];
+          if (oldpos != j) {
+            g.s2[j] = g.s2[oldpos];
+#pragma unroll
+            for (int i = 0; i < 3; i++) g.c2[j][i] = g.c2[oldpos][i];
+          }
+          g.lam[j] = g.dv[t][T::elts[t][j]] / g.dsum[t];
+        }
+      }
+      g.npts = T::card[t];
     }
-    g.lambdas[j] = g.dv[subset][g_elts[subset][j]] / g.dsum[subset];
   }
-  g.npts = g_card[subset];
 }
 
-__device__ inline int gjk_default(GjkState& g) {
-  int s, ok = 0, size = g.npts;
-  for (s = 1; s < 16 && g_maxe[s] < size; s++) {
-    g.dsum[s] = 0.0; ok = 1;
-    for (int j = 0; ok && j < g_card[s]; j++) {
-      if (g.dv[s][g_elts[s][j]] > 0.0) g.dsum[s] += g.dv[s][g_elts[s][j]];
-      else ok = 0;
+// default_distance (gjk.cpp:593-657)
+__device__ __forceinline__ int gjk_default(GjkState& g) {
+  using T = GjkTab;
+  const int size = g.npts;
+  int ok = 0, found = 0, sel = 0, s_end = 16;
+#pragma unroll
+  for (int s = 1; s < 16; s++) {
+    if (!found && T::maxe[s] < size) {
+      g.dsum[s] = 0.0;
+      ok = 1;
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if (j < T::card[s] && ok) {
+          const double v = g.dv[s][T::elts[s][j]];
+          if (v > 0.0) g.dsum[s] += v;
+          else ok = 0;
+        }
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (k < 4 - T::card[s] && k < size - T::card[s] && ok)
+          if (g.dv[T::succ[s][k]][T::nonelts[s][k]] > 0) ok = 0;
+      if (ok && g.dsum[s] >= 1.0e-20) { found = 1; sel = s; }
+    } else if (!found && s_end == 16) {
+      s_end = s;
     }
-    for (int k = 0; ok && k < size - g_card[s]; k++)
-      if (g.dv[g_succ[s][k]][g_nonelts[s][k]] > 0) ok = 0;
-    if (ok && g.dsum[s] >= 1.0e-20) break;
   }
-  if (ok) { gjk_reset(g, s); return 1; }
-  return 0;
+  if (!found) {
+    // loop ran out: the reference then calls reset_simplex(s) with the
+    // terminating s if the last subset tested was ok (tiny delta sum)
+    if (ok && s_end < 16) sel = s_end;
+    else return 0;
+  }
+  gjk_reset(g, sel);
+  return 1;
 }
 
-__device__ inline void gjk_backup(GjkState& g) {
-  int size = g.npts, bests = 0;
-  double num[16], den[16];
-  for (int s = 1; s < 16 && g_maxe[s] < size; s++) {
-    if (g.dsum[s] <= 0.0) continue;
-    int i;
-    for (i = 0; i < g_card[s]; i++)
-      if (g.dv[s][g_elts[s][i]] <= 0.0) break;
-    if (i < g_card[s]) continue;
-    num[s] = 0.0;
-    for (int j = 0; j < g_card[s]; j++)
-      for (int k = 0; k < g_card[s]; k++)
-        num[s] += (g.dv[s][g_elts[s][j]] * g.dv[s][g_elts[s][k]]) * g.dp[g_elts[s][j]][g_elts[s][k]];
-    den[s] = g.dsum[s] * g.dsum[s];
-    if ((bests < 1) || (num[s] * den[bests] < num[bests] * den[s])) bests = s;
+// backup_distance (gjk.cpp:663-706)
+__device__ __forceinline__ void gjk_backup(GjkState& g) {
+  using T = GjkTab;
+  const int size = g.npts;
+  int bests = 0;
+  double bnum = 0.0, bden = 0.0;
+#pragma unroll
+  for (int s = 1; s < 16; s++) {
+    if (T::maxe[s] < size && g.dsum[s] > 0.0) {
+      bool viable = true;
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        if (i < T::card[s] && g.dv[s][T::elts[s][i]] <= 0.0) viable = false;
+      if (viable) {
+        double num = 0.0;
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+#pragma unroll
+          for (int k = 0; k < 4; k++)
+            if (j < T::card[s] && k < T::card[s])
+              num += (g.dv[s][T::elts[s][j]] * g.dv[s][T::elts[s][k]]) *
+                     g.dp[T::elts[s][j]][T::elts[s][k]];
+        const double den = g.dsum[s] * g.dsum[s];
+        if ((bests < 1) || (num * bden < bnum * den)) { bests = s; bnum = num; bden = den; }
+      }
+    }
   }
   gjk_reset(g, bests);
 }
 
-__device__ __forceinline__ void gjk_point(double* pt, int len, const double (*v)[3], const double* lam) {
+// compute_point (gjk.cpp:851-862): sum_i vertices[i][d] * lambdas[i] from 0
+__device__ __forceinline__ void gjk_witnesses(const GjkState& g, const double* vrel, double* w1,
+                                              double* w2) {
+#pragma unroll
   for (int d = 0; d < 3; d++) {
-    pt[d] = 0;
-    for (int i = 0; i < len; i++) pt[d] += v[i][d] * lam[i];
+    double a = 0, b = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if (i < g.npts) { a += vrel[d] * g.lam[i]; b += g.c2[i][d] * g.lam[i]; }
+    w1[d] = a;
+    w2[d] = b;
   }
 }
 
@@ -136,29 +205,36 @@ __device__ __forceinline__ void gjk_point(double* pt, int len, const double (*v)
 //   void point(int q, double* pt)
 template <class Sup>
 __device__ void gjk_run(Sup& sup, int qfirst, int n, const double* vrel, GjkState& g, GjkOut& o) {
+#pragma unroll
   for (int s = 0; s < 16; ++s) {
     g.dsum[s] = 0.0;
+#pragma unroll
     for (int k = 0; k < 4; ++k) g.dv[s][k] = 0.0;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    g.s2[i] = -1;
+    g.lam[i] = 0.0;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) g.c2[i][d] = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) g.dp[i][j] = 0.0;
   }
   int use_default = 1, first_iteration = 1, max_iterations = n;
   double oldsqrd = 0.0, sqrd = 0.0;
   double disp[3], rdisp[3];
   o.iters = 0; o.backup = 0;
-  g.npts = 1; g.s2[0] = qfirst; g.lambdas[0] = 1.0;
-  {
-    double f[3];
-    sup.point(qfirst, f);
-    for (int d = 0; d < 3; d++) { g.c1[0][d] = vrel[d]; g.c2[0][d] = f[d]; }
-  }
+  g.npts = 1; g.s2[0] = qfirst; g.lam[0] = 1.0;
+  sup.point(qfirst, g.c2[0]);
   while (max_iterations-- > 0) {
-    if (g.npts == 1) g.lambdas[0] = 1.0;
+    if (g.npts == 1) g.lam[0] = 1.0;
     else {
-      gjk_subterms(g);
+      gjk_subterms(g, vrel);
       if (use_default) use_default = gjk_default(g);
       if (!use_default) { gjk_backup(g); o.backup = 1; }
     }
-    gjk_point(o.w1, g.npts, g.c1, g.lambdas);
-    gjk_point(o.w2, g.npts, g.c2, g.lambdas);
+    gjk_witnesses(g, vrel, o.w1, o.w2);
+#pragma unroll
     for (int d = 0; d < 3; d++) { disp[d] = o.w2[d] - o.w1[d]; rdisp[d] = -disp[d]; }
     sqrd = disp[0] * disp[0] + disp[1] * disp[1] + disp[2] * disp[2];
     if (sqrd < 1.0e-8) { o.sqrd = sqrd; return; }
@@ -173,10 +249,14 @@ __device__ void gjk_run(Sup& sup, int qfirst, int n, const double* vrel, GjkStat
     if ((first_iteration || (sqrd < oldsqrd)) && (g.npts <= 3)) {
       double f[3];
       sup.point(minq, f);
-      const int np_ = g.npts;
-      g.s2[np_] = minq;
-      g.lambdas[np_] = 0.0;
-      for (int d = 0; d < 3; d++) { g.c1[np_][d] = vrel[d]; g.c2[np_][d] = f[d]; }
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (k == g.npts) {
+          g.s2[k] = minq;
+          g.lam[k] = 0.0;
+#pragma unroll
+          for (int d = 0; d < 3; d++) g.c2[k][d] = f[d];
+        }
       g.npts++;
       oldsqrd = sqrd;
       first_iteration = 0;

@@ -31,7 +31,10 @@
 namespace lqro {
 
 enum : int { kSliceOut = 0, kSliceIn = 1, kSliceMixed = 2 };
-constexpr int kMaxPW = 4;  // NP <= 256 (one 64-bit reachable mask per 64 points)
+constexpr int kMaxPW = 4;
+#ifndef LQRO_PAIR_LB
+#define LQRO_PAIR_LB 512
+#endif  // NP <= 256 (one 64-bit reachable mask per 64 points)
 
 struct PairArgs {
   int N, H, NP, PW, min_reach;
@@ -198,7 +201,7 @@ __device__ inline int reach_rank(const PairArgs& P, const WaveTabs& W, int lane,
 }
 
 template <int X>
-__global__ void __launch_bounds__(1024) k_pair(PairArgs P) {
+__global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
   extern __shared__ double lds[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;

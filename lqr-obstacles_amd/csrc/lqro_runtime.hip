@@ -32,14 +32,11 @@
 #include "lqro_device.hpp"
 #include "lqro_lp.hpp"
 #include "lqro_pair.hpp"
+#include "lqro_hull.hpp"
 
 using namespace lqro;
 
 #define LQRO_MAXX 16
-#define HULL_THREADS 256
-#define HULL_FMAX 8192               // face slots per hull workgroup (global scratch)
-#define HULL_VMAX 2048               // visible faces per insertion
-#define HULL_HMAX 256                // horizon edges per insertion
 
 // ---------------------------------------------------------------------------
 // Horizon tables (per agent): T_k = !(C*G_k) (3x3), NCF_k = (-C)*F_k (3xX),
@@ -145,457 +142,6 @@ __global__ void __launch_bounds__(256) k_tables(int X, int U, int H, const doubl
 }
 
 // ---------------------------------------------------------------------------
-// Hull kernel: one workgroup per inside-hull pair (persistent over the queue)
-// ---------------------------------------------------------------------------
-struct HullArgs {
-  int N, X, H, NP;
-  int row_begin, npr, per_agent;
-  double r2, r2_lo, r2_hi;
-  const double* T;
-  const double* NCF;
-  const double* S;
-  const double* x;
-  float* planes;
-  lqro_pair_record* recs;
-  const int* queue;
-  const int* count;
-  int cap;
-  int* next;
-  double* scratch;                  // per block: H*NP*6 doubles (rounded, full)
-  int* iscratch;                    // per block: H*NP ints (conflict face)
-  float* fscratch;                  // per block: H*NP floats (conflict distance)
-  void* faces;                      // per block: HULL_FMAX HFace + HULL_FMAX free-list ints
-  unsigned long long* stats;
-};
-
-struct HFace {
-  int v[3];
-  int adj[3];    // adj[e] = face across edge (v[e], v[e+1])
-  double n[3];
-  int alive;
-};
-
-__device__ __forceinline__ double hface_dist(const HFace& f, const double* P, int p) {
-  const double* a = P + 3 * f.v[0];
-  const double* q = P + 3 * p;
-  return f.n[0] * (q[0] - a[0]) + f.n[1] * (q[1] - a[1]) + f.n[2] * (q[2] - a[2]);
-}
-__device__ __forceinline__ void hface_plane(HFace& f, const double* P) {
-  const double *a = P + 3 * f.v[0], *b = P + 3 * f.v[1], *c = P + 3 * f.v[2];
-  double e1[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
-  double e2[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
-  f.n[0] = e1[1] * e2[2] - e1[2] * e2[1];
-  f.n[1] = e1[2] * e2[0] - e1[0] * e2[2];
-  f.n[2] = e1[0] * e2[1] - e1[1] * e2[0];
-}
-
-// block-wide argmax of (key, idx) with lowest idx on ties
-__device__ void block_argmax(double& key, int& idx, double* sk, int* si) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    double ok = __shfl_xor(key, off);
-    int oi = __shfl_xor(idx, off);
-    if (ok > key || (ok == key && oi < idx)) { key = ok; idx = oi; }
-  }
-  if (lane == 0) { sk[wave] = key; si[wave] = idx; }
-  __syncthreads();
-  key = sk[0]; idx = si[0];
-  for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
-    if (sk[w] > key || (sk[w] == key && si[w] < idx)) { key = sk[w]; idx = si[w]; }
-  __syncthreads();
-}
-
-__global__ void __launch_bounds__(HULL_THREADS) k_hull(HullArgs A) {
-  __shared__ unsigned char vis[HULL_FMAX];
-  __shared__ int s_job, s_n, s_nf, s_fail, s_apex, s_nvis, s_nh, s_nnew;
-  __shared__ int s_nfree;
-  __shared__ int s_vis[HULL_VMAX];
-  __shared__ int h_a[HULL_HMAX], h_b[HULL_HMAX], h_out[HULL_HMAX], h_new[HULL_HMAX];
-  __shared__ double sk[HULL_THREADS / 64];
-  __shared__ int si[HULL_THREADS / 64];
-  __shared__ int s_scan[HULL_THREADS];
-  __shared__ double s_tr[3 * 256];
-  __shared__ int s_init[4];
-  __shared__ double s_eps;
-
-  const int tid = threadIdx.x;
-  const int HNP = A.H * A.NP;
-  double* Pr = A.scratch + (size_t)blockIdx.x * HNP * 6;    // rounded points
-  double* Pf = Pr + (size_t)HNP * 3;                         // full-precision points
-  int* conf = A.iscratch + (size_t)blockIdx.x * HNP;
-  float* cd = A.fscratch + (size_t)blockIdx.x * HNP;
-  HFace* F = reinterpret_cast<HFace*>(A.faces) + (size_t)blockIdx.x * HULL_FMAX;
-  int* s_free = reinterpret_cast<int*>(reinterpret_cast<HFace*>(A.faces) + (size_t)gridDim.x * HULL_FMAX) +
-               (size_t)blockIdx.x * HULL_FMAX;
-
-  for (;;) {
-    if (tid == 0) s_job = atomicAdd(A.next, 1);
-    __syncthreads();
-    const int job = s_job;
-    __syncthreads();
-    if (job >= min(*A.count, A.cap)) break;
-    const int slot = A.queue[job];
-    const int lrow = slot / A.npr, jj = slot % A.npr;
-    const int i = A.row_begin + lrow;
-    const int j = jj < i ? jj : jj + 1;
-    const double* xi = A.x + (size_t)i * A.X;
-    const double* xj = A.x + (size_t)j * A.X;
-    const double* Ti = A.T + (A.per_agent ? (size_t)i * A.H * 9 : 0);
-    const double* Ni = A.NCF + (A.per_agent ? (size_t)i * A.H * 3 * A.X : 0);
-    const double vrel[3] = {xi[3] - xj[3], xi[4] - xj[4], xi[5] - xj[5]};
-
-    // 1. reachable points in reference order (compacted), full + %g-rounded
-    if (tid == 0) { s_n = 0; s_fail = 0; }
-    __syncthreads();
-    for (int k0 = 0; k0 < A.H; k0 += 256) {
-      for (int it = tid; it < 3 * 256; it += blockDim.x) {
-        int k = k0 + it / 3, r = it % 3;
-        if (k < A.H) {
-          double d = 0.0;
-          for (int c = 0; c < A.X; ++c) d += Ni[((size_t)k * 3 + r) * A.X + c] * (xi[c] - xj[c]);
-          s_tr[it] = d;
-        }
-      }
-      __syncthreads();
-      const int kend = min(A.H, k0 + 256);
-      for (int q0 = k0 * A.NP; q0 < kend * A.NP; q0 += blockDim.x) {
-        const int q = q0 + tid;
-        bool ok = false;
-        double p0 = 0, p1 = 0, p2 = 0;
-        if (q < kend * A.NP) {
-          const int k = q / A.NP, p = q % A.NP;
-          const double* Tk = Ti + (size_t)k * 9;
-          const double* tk = s_tr + (k - k0) * 3;
-          double u0 = A.S[3 * p] + tk[0], u1 = A.S[3 * p + 1] + tk[1], u2 = A.S[3 * p + 2] + tk[2];
-          p0 = ((0.0 + Tk[0] * u0) + Tk[1] * u1) + Tk[2] * u2;
-          p1 = ((0.0 + Tk[3] * u0) + Tk[4] * u1) + Tk[5] * u2;
-          p2 = ((0.0 + Tk[6] * u0) + Tk[7] * u1) + Tk[8] * u2;
-          double a = p0 - vrel[0], b = p1 - vrel[1], c = p2 - vrel[2];
-          double t = a * a + b * b + c * c;
-          if (t < A.r2_lo) ok = true;
-          else if (t > A.r2_hi) ok = false;
-          else ok = (a * a) / A.r2 + (b * b) / A.r2 + (c * c) / A.r2 < 1.0;
-        }
-        // block exclusive scan of ok
-        s_scan[tid] = ok ? 1 : 0;
-        __syncthreads();
-        for (int off = 1; off < (int)blockDim.x; off <<= 1) {
-          int v = tid >= off ? s_scan[tid - off] : 0;
-          __syncthreads();
-          s_scan[tid] += v;
-          __syncthreads();
-        }
-        const int base = s_n;
-        const int pos = base + s_scan[tid] - (ok ? 1 : 0);
-        if (ok) {
-          int oor = 0;
-          Pf[3 * pos] = p0; Pf[3 * pos + 1] = p1; Pf[3 * pos + 2] = p2;
-          Pr[3 * pos] = round6(p0, &oor);
-          Pr[3 * pos + 1] = round6(p1, &oor);
-          Pr[3 * pos + 2] = round6(p2, &oor);
-          if (oor) s_fail = 1;
-        }
-        __syncthreads();
-        if (tid == blockDim.x - 1) s_n = base + s_scan[tid];
-        __syncthreads();
-      }
-    }
-    const int n = s_n;
-
-    // 2. scale-aware coplanarity tolerance (as the oracle's hull)
-    {
-      double mx = 0.0;
-      for (int q = tid; q < 3 * n; q += blockDim.x) mx = fmax(mx, fabs(Pr[q]));
-      int dummy = tid;
-      block_argmax(mx, dummy, sk, si);
-      if (tid == 0) s_eps = 1e-13 * (mx + 1.0);
-      __syncthreads();
-    }
-    const double eps = s_eps;
-
-    // 3. initial tetrahedron (extreme points)
-    if (n < 4) { if (tid == 0) s_fail = 1; }
-    __syncthreads();
-    if (!s_fail) {
-      double key; int idx;
-      // i0: min x
-      key = -INFINITY; idx = INT_MAX;
-      for (int q = tid; q < n; q += blockDim.x) {
-        double v = -Pr[3 * q];
-        if (v > key || (v == key && q < idx)) { key = v; idx = q; }
-      }
-      block_argmax(key, idx, sk, si);
-      const int i0 = idx;
-      key = -INFINITY; idx = INT_MAX;
-      for (int q = tid; q < n; q += blockDim.x) {
-        double dx = Pr[3 * q] - Pr[3 * i0], dy = Pr[3 * q + 1] - Pr[3 * i0 + 1], dz = Pr[3 * q + 2] - Pr[3 * i0 + 2];
-        double v = dx * dx + dy * dy + dz * dz;
-        if (v > key || (v == key && q < idx)) { key = v; idx = q; }
-      }
-      block_argmax(key, idx, sk, si);
-      const int i1 = idx;
-      key = -INFINITY; idx = INT_MAX;
-      for (int q = tid; q < n; q += blockDim.x) {
-        double e1[3] = {Pr[3 * i1] - Pr[3 * i0], Pr[3 * i1 + 1] - Pr[3 * i0 + 1], Pr[3 * i1 + 2] - Pr[3 * i0 + 2]};
-        double e2[3] = {Pr[3 * q] - Pr[3 * i0], Pr[3 * q + 1] - Pr[3 * i0 + 1], Pr[3 * q + 2] - Pr[3 * i0 + 2]};
-        double cx = e1[1] * e2[2] - e1[2] * e2[1], cy = e1[2] * e2[0] - e1[0] * e2[2], cz = e1[0] * e2[1] - e1[1] * e2[0];
-        double v = cx * cx + cy * cy + cz * cz;
-        if (v > key || (v == key && q < idx)) { key = v; idx = q; }
-      }
-      block_argmax(key, idx, sk, si);
-      const int i2 = idx;
-      HFace tf;
-      tf.v[0] = i0; tf.v[1] = i1; tf.v[2] = i2;
-      hface_plane(tf, Pr);
-      const double nn = sqrt(tf.n[0] * tf.n[0] + tf.n[1] * tf.n[1] + tf.n[2] * tf.n[2]);
-      key = -INFINITY; idx = INT_MAX;
-      for (int q = tid; q < n; q += blockDim.x) {
-        double v = fabs(hface_dist(tf, Pr, q)) / nn;
-        if (v > key || (v == key && q < idx)) { key = v; idx = q; }
-      }
-      block_argmax(key, idx, sk, si);
-      const int i3 = idx;
-      if (tid == 0) {
-        if (!(key > eps) || i0 == i1 || i1 == i2 || i2 == i3) s_fail = 1;
-        s_init[0] = i0; s_init[1] = i1; s_init[2] = i2; s_init[3] = i3;
-      }
-      __syncthreads();
-    }
-    if (!s_fail && tid == 0) {
-      const int tet[4] = {s_init[0], s_init[1], s_init[2], s_init[3]};
-      const int fv[4][3] = {{0, 1, 2}, {0, 3, 1}, {1, 3, 2}, {0, 2, 3}};
-      for (int f = 0; f < 4; ++f) {
-        HFace h;
-        h.v[0] = tet[fv[f][0]]; h.v[1] = tet[fv[f][1]]; h.v[2] = tet[fv[f][2]];
-        hface_plane(h, Pr);
-        const int other = tet[6 - fv[f][0] - fv[f][1] - fv[f][2]];
-        if (hface_dist(h, Pr, other) > 0) {
-          int t = h.v[1]; h.v[1] = h.v[2]; h.v[2] = t;
-          hface_plane(h, Pr);
-        }
-        h.alive = 1;
-        F[f] = h;
-      }
-      // adjacency by matching reversed edges
-      for (int f = 0; f < 4; ++f)
-        for (int e = 0; e < 3; ++e) {
-          int a = F[f].v[e], b = F[f].v[(e + 1) % 3];
-          F[f].adj[e] = -1;
-          for (int g = 0; g < 4; ++g)
-            for (int e2 = 0; e2 < 3; ++e2)
-              if (F[g].v[e2] == b && F[g].v[(e2 + 1) % 3] == a) F[f].adj[e] = g;
-        }
-      s_nf = 4;
-      s_nfree = 0;
-    }
-    __syncthreads();
-    if (!s_fail) {
-      // 4. initial conflict assignment
-      for (int q = tid; q < n; q += blockDim.x) {
-        int c = -1; double dd = 0.0;
-        if (q != s_init[0] && q != s_init[1] && q != s_init[2] && q != s_init[3]) {
-          for (int f = 0; f < 4; ++f) {
-            const double nl = sqrt(F[f].n[0] * F[f].n[0] + F[f].n[1] * F[f].n[1] + F[f].n[2] * F[f].n[2]);
-            const double dist = hface_dist(F[f], Pr, q);
-            if (dist > eps * nl) { c = f; dd = dist / nl; break; }
-          }
-        }
-        conf[q] = c;
-        cd[q] = (float)dd;
-      }
-      __syncthreads();
-      // 5. quickhull iterations
-      for (int iter = 0; iter < 100000; ++iter) {
-        double key = -INFINITY; int idx = INT_MAX;
-        for (int q = tid; q < n; q += blockDim.x) {
-          if (conf[q] >= 0) {
-            double v = (double)cd[q];
-            if (v > key || (v == key && q < idx)) { key = v; idx = q; }
-          }
-        }
-        block_argmax(key, idx, sk, si);
-        if (idx == INT_MAX) break;
-        const int apex = idx;
-        // visible region: BFS from the apex's conflict face (thread 0)
-        for (int f = tid; f < s_nf; f += blockDim.x) vis[f] = 0;
-        __syncthreads();
-        if (tid == 0) {
-          s_apex = apex;
-          int nv = 0, nh = 0;
-          const int f0 = conf[apex];
-          vis[f0] = 1; s_vis[nv++] = f0;
-          for (int h = 0; h < nv; ++h) {
-            const HFace& fh = F[s_vis[h]];
-            for (int e = 0; e < 3; ++e) {
-              const int nb = fh.adj[e];
-              if (nb < 0) { s_fail = 1; continue; }
-              if (vis[nb]) continue;
-              const double nl = sqrt(F[nb].n[0] * F[nb].n[0] + F[nb].n[1] * F[nb].n[1] + F[nb].n[2] * F[nb].n[2]);
-              if (hface_dist(F[nb], Pr, apex) > eps * nl) {
-                vis[nb] = 1;
-                if (nv < HULL_VMAX) s_vis[nv++] = nb; else s_fail = 1;
-              }
-            }
-          }
-          // horizon
-          for (int h = 0; h < nv; ++h) {
-            const HFace& fh = F[s_vis[h]];
-            for (int e = 0; e < 3; ++e) {
-              const int nb = fh.adj[e];
-              if (nb >= 0 && !vis[nb]) {
-                if (nh < HULL_HMAX) { h_a[nh] = fh.v[e]; h_b[nh] = fh.v[(e + 1) % 3]; h_out[nh] = nb; nh++; }
-                else s_fail = 1;
-              }
-            }
-          }
-          // retire the visible faces, make the cone (a slot retired in this
-          // round is reused only from the next round on, after the
-          // reassignment below has seen it dead)
-          for (int h = 0; h < nv; ++h) F[s_vis[h]].alive = 0;
-          for (int h = 0; h < nh && !s_fail; ++h) {
-            int slotf;
-            if (s_nfree > 0) slotf = s_free[--s_nfree];
-            else if (s_nf < HULL_FMAX) slotf = s_nf++;
-            else { s_fail = 1; break; }
-            h_new[h] = slotf;
-            HFace nf;
-            nf.v[0] = h_a[h]; nf.v[1] = h_b[h]; nf.v[2] = apex;
-            nf.alive = 1;
-            nf.adj[0] = h_out[h];
-            nf.adj[1] = -1; nf.adj[2] = -1;
-            hface_plane(nf, Pr);
-            F[slotf] = nf;
-            vis[slotf] = 0;
-            // outer neighbour: its edge (b, a) now faces the new face
-            HFace& on = F[h_out[h]];
-            for (int e = 0; e < 3; ++e)
-              if (on.v[e] == h_b[h] && on.v[(e + 1) % 3] == h_a[h]) on.adj[e] = slotf;
-          }
-          if (!s_fail)
-            for (int h = 0; h < nh; ++h) {
-              // edge (b, apex) <-> face whose horizon edge starts at b
-              // edge (apex, a) <-> face whose horizon edge ends at a
-              for (int g = 0; g < nh; ++g) {
-                if (h_a[g] == h_b[h]) F[h_new[h]].adj[1] = h_new[g];
-                if (h_b[g] == h_a[h]) F[h_new[h]].adj[2] = h_new[g];
-              }
-              if (F[h_new[h]].adj[1] < 0 || F[h_new[h]].adj[2] < 0) s_fail = 1;
-            }
-          for (int h = 0; h < nv; ++h) s_free[s_nfree++] = s_vis[h];
-          s_nvis = nv;
-          s_nh = nh;
-        }
-        __syncthreads();
-        if (s_fail) break;
-        // reassign the conflict points of the visible faces
-        const int nh = s_nh;
-        for (int q = tid; q < n; q += blockDim.x) {
-          const int c = conf[q];
-          if (c < 0) continue;
-          if (q == apex) { conf[q] = -1; continue; }
-          if (F[c].alive) continue;          // c was visible (freed) this round
-          int nc = -1; double dd = 0.0;
-          for (int h = 0; h < nh; ++h) {
-            const HFace& f = F[h_new[h]];
-            const double nl = sqrt(f.n[0] * f.n[0] + f.n[1] * f.n[1] + f.n[2] * f.n[2]);
-            const double dist = hface_dist(f, Pr, q);
-            if (dist > eps * nl) { nc = h_new[h]; dd = dist / nl; break; }
-          }
-          conf[q] = nc;
-          cd[q] = (float)dd;
-        }
-        __syncthreads();
-      }
-    }
-    __syncthreads();
-
-    // 6. arg-min facet (LQRObstacles.cpp:955-968) in canonical facet order:
-    //    normal from the rounded vertices (lowest index first), distance from
-    //    the full-precision lowest-index vertex.
-    double best = INFINITY;
-    int bt0 = INT_MAX, bt1 = INT_MAX, bt2 = INT_MAX;
-    double bn[3] = {0, 0, 0};
-    int nfac = 0;
-    if (!s_fail) {
-      for (int f = tid; f < s_nf; f += blockDim.x) {
-        if (!F[f].alive) continue;
-        nfac++;
-        int t0 = F[f].v[0], t1 = F[f].v[1], t2 = F[f].v[2];
-        while (!(t0 < t1 && t0 < t2)) { int a = t0; t0 = t1; t1 = t2; t2 = a; }
-        const double *a = Pr + 3 * t0, *b = Pr + 3 * t1, *c = Pr + 3 * t2;
-        double e1[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
-        double e2[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
-        double nv[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
-        double len = sqrt(nv[0] * nv[0] + nv[1] * nv[1] + nv[2] * nv[2]);
-        nv[0] /= len; nv[1] /= len; nv[2] /= len;
-        const double* p0 = Pf + 3 * t0;
-        double dd = fabs(nv[0] * (vrel[0] - p0[0]) + nv[1] * (vrel[1] - p0[1]) + nv[2] * (vrel[2] - p0[2]));
-        // canonical triple order key = sorted (t0, min(t1,t2), max(t1,t2))
-        int s1 = min(t1, t2), s2 = max(t1, t2);
-        bool better = dd < best || (dd == best && (t0 < bt0 || (t0 == bt0 && (s1 < bt1 || (s1 == bt1 && s2 < bt2)))));
-        if (better) {
-          best = dd; bt0 = t0; bt1 = s1; bt2 = s2;
-          bn[0] = nv[0]; bn[1] = nv[1]; bn[2] = nv[2];
-        }
-      }
-    }
-    // block reduction of (best, triple)
-    __shared__ double r_best[HULL_THREADS];
-    __shared__ int r_t[HULL_THREADS][3];
-    __shared__ double r_n[HULL_THREADS][3];
-    __shared__ int r_cnt[HULL_THREADS];
-    r_best[tid] = best; r_t[tid][0] = bt0; r_t[tid][1] = bt1; r_t[tid][2] = bt2;
-    r_n[tid][0] = bn[0]; r_n[tid][1] = bn[1]; r_n[tid][2] = bn[2];
-    r_cnt[tid] = nfac;
-    __syncthreads();
-    if (tid == 0) {
-      int fo = 0, total = 0;
-      for (int t = 0; t < (int)blockDim.x; ++t) {
-        total += r_cnt[t];
-        bool better = r_best[t] < r_best[fo] ||
-                      (r_best[t] == r_best[fo] &&
-                       (r_t[t][0] < r_t[fo][0] || (r_t[t][0] == r_t[fo][0] &&
-                        (r_t[t][1] < r_t[fo][1] || (r_t[t][1] == r_t[fo][1] && r_t[t][2] < r_t[fo][2])))));
-        if (better) fo = t;
-      }
-      const bool ok = !s_fail && total > 0 && r_t[fo][0] != INT_MAX;
-      float* pl = A.planes + (size_t)slot * 8;
-      double distance = r_best[fo];
-      double nrm[3] = {r_n[fo][0], r_n[fo][1], r_n[fo][2]};
-      if (ok) {
-        double dh = distance * 0.5;                       // :1416
-        const double mult = 1.0;                          // :1213
-        pl[0] = (float)(xi[3] + mult * dh * nrm[0]);
-        pl[1] = (float)(xi[4] + mult * dh * nrm[1]);
-        pl[2] = (float)(xi[5] + mult * dh * nrm[2]);
-        pl[3] = (float)nrm[0]; pl[4] = (float)nrm[1]; pl[5] = (float)nrm[2];
-        pl[6] = __int_as_float(1);
-        atomicAdd(&A.stats[3], 1ull);
-      } else {
-        pl[6] = __int_as_float(0);                        // no usable plane
-        atomicAdd(&A.stats[4], 1ull);
-      }
-      if (A.recs) {
-        lqro_pair_record& rec = A.recs[slot];
-        rec.flags |= ok ? LQRO_REC_HULL : LQRO_REC_HULLFAIL;
-        rec.n_facets = ok ? total : -1;
-        if (ok) {
-          rec.facet[0] = r_t[fo][0]; rec.facet[1] = r_t[fo][1]; rec.facet[2] = r_t[fo][2];
-          rec.dist = distance;
-          for (int q = 0; q < 3; ++q) {
-            rec.normal[q] = nrm[q];
-            rec.plane_point[q] = pl[q];
-            rec.plane_normal[q] = pl[3 + q];
-          }
-        }
-      }
-    }
-    __syncthreads();
-  }
-}
-
-// ---------------------------------------------------------------------------
 // LP kernel: one wavefront per row agent (lqro_lp.hpp), fp32 as the reference
 // ---------------------------------------------------------------------------
 struct LpArgs {
@@ -665,13 +211,16 @@ struct lqro_ctx {
   double *d_A, *d_B, *d_L, *d_E;
   float *d_planes, *d_lpscratch, *d_lpcompact;
   lqro_pair_record* d_recs;
-  int *d_hq, *d_hcount, *d_hnext, *d_err;
+  int *d_hq, *d_hcount, *d_hnext, *d_err, *d_rq;
+  void* d_hbig;
+  int hull_big_blocks;
   double* d_hscratch;
   int* d_hiscratch;
   float* d_hfscratch;
   void* d_hfaces;
   int hull_blocks, hull_cap;
   unsigned long long* d_stats;
+  unsigned long long* d_prof;
   int lds_bytes;
   PairArgs pa;
 };
@@ -726,7 +275,7 @@ void lqro_destroy(lqro_ctx* c) {
   (void)hipSetDevice(c->cfg.device);
   void* ps[] = {c->d_R, c->d_TF, c->d_shash, c->d_T, c->d_NCF, c->d_S, c->d_x, c->d_vgoal, c->d_newv, c->d_A, c->d_B,
                 c->d_L, c->d_E, c->d_planes, c->d_lpscratch, c->d_lpcompact, c->d_recs, c->d_hq, c->d_hcount,
-                c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats};
+                c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats, c->d_prof, c->d_rq, c->d_hbig};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (int k = 0; k < 5; ++k)
@@ -762,15 +311,20 @@ static int ctx_alloc(lqro_ctx* c) {
   c->hull_cap = (int)(slots < (1u << 22) ? slots : (1u << 22));
   if (c->hull_cap < 1) c->hull_cap = 1;
   HIPCHK(hipMalloc(&c->d_hq, sizeof(int) * c->hull_cap));
-  HIPCHK(hipMalloc(&c->d_hcount, sizeof(int) * 2));
+  HIPCHK(hipMalloc(&c->d_hcount, sizeof(int) * 4));   // count, next, retry count, retry next
   c->d_hnext = c->d_hcount + 1;
+  HIPCHK(hipMalloc(&c->d_rq, sizeof(int) * c->hull_cap));
   HIPCHK(hipMalloc(&c->d_err, sizeof(int)));
   HIPCHK(hipMalloc(&c->d_stats, sizeof(unsigned long long) * 8));
-  c->hull_blocks = 512;
+  HIPCHK(hipMalloc(&c->d_prof, sizeof(unsigned long long) * 32));
+  HIPCHK(hipMemset(c->d_prof, 0, sizeof(unsigned long long) * 32));
+  c->hull_blocks = 256;   // one 138 KB-LDS workgroup per CU, persistent over the queue
   HIPCHK(hipMalloc(&c->d_hscratch, sizeof(double) * 6 * H * NP * c->hull_blocks));
-  HIPCHK(hipMalloc(&c->d_hiscratch, sizeof(int) * H * NP * c->hull_blocks));
+  HIPCHK(hipMalloc(&c->d_hiscratch, sizeof(int) * 2 * H * NP * c->hull_blocks));
   HIPCHK(hipMalloc(&c->d_hfscratch, sizeof(float) * H * NP * c->hull_blocks));
-  HIPCHK(hipMalloc(&c->d_hfaces, (sizeof(HFace) + sizeof(int)) * HULL_FMAX * (size_t)c->hull_blocks));
+  HIPCHK(hipMalloc(&c->d_hfaces, sizeof(int) * HULL_SBMULT * H * NP * (size_t)c->hull_blocks));
+  c->hull_big_blocks = 64;
+  HIPCHK(hipMalloc(&c->d_hbig, sizeof(HullMemBig) * (size_t)c->hull_big_blocks));
   return LQRO_OK;
 }
 
@@ -818,7 +372,7 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
   P.wave_doubles = 8 * H + H * P.PW + (3 * H + 1) / 2;
   const int budget = 160 * 1024 / 8;
   int waves = (budget - off) / P.wave_doubles;
-  if (waves > 16) waves = 16;
+  if (waves > LQRO_PAIR_LB / 64) waves = LQRO_PAIR_LB / 64;
   if (waves < 1) {
     fprintf(stderr, "liblqro: horizon %d x %d points does not fit in LDS\n", H, NP);
     delete c;
@@ -917,7 +471,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   // one workgroup = P.waves wavefronts on one row; each wave takes several pairs
   P.pairs_per_block = P.waves * 4;
   P.blocks_per_row = (c->npr + P.pairs_per_block - 1) / P.pairs_per_block;
-  HIPCHK(hipMemsetAsync(c->d_hcount, 0, sizeof(int) * 2, s));
+  HIPCHK(hipMemsetAsync(c->d_hcount, 0, sizeof(int) * 4, s));
   HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * 8, s));
   HIPCHK(hipEventRecord(c->ev[0], s));
   const unsigned nblk = (unsigned)P.blocks_per_row * (unsigned)c->nrows;
@@ -937,9 +491,14 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   Hh.planes = c->d_planes; Hh.recs = c->d_recs;
   Hh.queue = c->d_hq; Hh.count = c->d_hcount; Hh.cap = c->hull_cap; Hh.next = c->d_hnext;
   Hh.scratch = c->d_hscratch; Hh.iscratch = c->d_hiscratch; Hh.fscratch = c->d_hfscratch;
-  Hh.faces = c->d_hfaces;
+  Hh.sb = reinterpret_cast<int*>(c->d_hfaces);
+  Hh.rqueue = c->d_rq; Hh.rcount = c->d_hcount + 2; Hh.rnext = c->d_hcount + 3;
+  Hh.bigmem = c->d_hbig;
   Hh.stats = c->d_stats;
+  Hh.prof = c->d_prof;
   hipLaunchKernelGGL(k_hull, dim3(c->hull_blocks), dim3(HULL_THREADS), 0, s, Hh);
+  HIPCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_hull_big, dim3(c->hull_big_blocks), dim3(HULL_THREADS), 0, s, Hh);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev[2], s));
   LpArgs La;
@@ -1046,6 +605,16 @@ int lqro_get_stats(lqro_ctx* c, int64_t* st) {
   HIPCHK(hipMemcpy(h, c->d_stats, sizeof h, hipMemcpyDeviceToHost));
   for (int k = 0; k < 8; ++k) st[k] = (int64_t)h[k];
   st[0] = (int64_t)c->nrows * c->npr;
+  return LQRO_OK;
+}
+
+/* diagnostic (not in lqro.h): accumulated k_hull phase cycles of a
+ * -DLQRO_HULL_PROFILE build */
+int lqro_debug_hull_profile(lqro_ctx* c, unsigned long long* out16) {
+  if (!c || !out16) return LQRO_E_ARG;
+  HIPCHK(hipSetDevice(c->cfg.device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipMemcpy(out16, c->d_prof, sizeof(unsigned long long) * 32, hipMemcpyDeviceToHost));
   return LQRO_OK;
 }
 
