@@ -35,11 +35,16 @@ HBM_PEAK_GBS = 8000.0
 
 
 def sweep_flops_per_pair(X=X_DIM, H=HORIZON, NP=N_POINTS) -> int:
-    """Algorithmic fp64 work of one pair's exact sweep:
-    Translate_k = NCF_k*d (3X mul + 3X add per step), then per obstacle point
-    u = s + tr (3), Transform*u from 0.0 (9 mul + 9 add), reachable test
-    (3 sub + 3 mul + 2 add).  GJK support scans are data-dependent and are not
-    counted."""
+    """SURVEY.md §8d's algorithmic work per agent-pair, the unit of the
+    metric: F_pair = X + H*(6X + 11*NP) (dx; off_t = W_t*dx; per point 3 adds
+    + 3 subs + 5 for |d|^2).  GJK and hull are data-dependent and excluded."""
+    return X + H * (6 * X + 11 * NP)
+
+
+def exact_order_flops_per_pair(X=X_DIM, H=HORIZON, NP=N_POINTS) -> int:
+    """What the reference-order sweep evaluates if no slice is pruned
+    (informational): Translate_k (6X per k), then per point u = s + tr (3),
+    Transform*u accumulated from 0.0 (18), reachable test (8)."""
     return H * (6 * X) + H * NP * (3 + 18 + 8)
 
 
@@ -47,6 +52,23 @@ def algorithmic_bytes_per_pair(X=X_DIM) -> int:
     """Compulsory HBM bytes per pair: read x_i, x_j (fp64), write one 32-B
     half-plane slot."""
     return 2 * X * 8 + 32
+
+
+def pmc_traffic(kernel: str = "k_pair"):
+    """HBM bytes per launch of `kernel` from the committed PMC passes
+    (profiles/*_pmc_traffic.json, written by scripts/pmc_traffic.py from
+    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this bench at
+    N=1, FETCH_SIZE doubled per the gfx950 correction).  None if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    k = d.get("kernels", {}).get(kernel)
+    if not k or d.get("n_agents") != N_AGENTS or d.get("horizon") != HORIZON:
+        return None
+    return k["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
 
 
 def cpu_baseline(x, vg, gains, seconds_target=15.0):
@@ -104,9 +126,8 @@ def main():
     torch.cuda.set_device(dev)
 
     N = N_AGENTS
-    assert N % world == 0
-    rows = N // world
-    rb, re = rank * rows, (rank + 1) * rows
+    rb, re = lqro.row_shard(N, rank, world)
+    rows = re - rb
     x, vg = lqro.synthetic_swarm(N)
     gains = lqro.synthesize_gains()
     ctx = lqro.Context(lqro.config(N, HORIZON, N_POINTS, device=local, row_begin=rb, row_end=re))
@@ -114,13 +135,12 @@ def main():
     d_x = torch.from_numpy(x).to(dev)
     d_vg = torch.from_numpy(vg).to(dev)
     d_newv = torch.zeros((N, 3), dtype=torch.float64, device=dev)
-    full = torch.zeros((N, 3), dtype=torch.float64, device=dev) if world > 1 else d_newv
     stream = torch.cuda.current_stream(dev)
 
     def step():
         ctx.step_device(d_x.data_ptr(), d_vg.data_ptr(), d_newv.data_ptr(), stream.cuda_stream)
         if world > 1:
-            dist.all_gather_into_tensor(full, d_newv[rb:re])
+            lqro.allgather_rows(dist, d_newv, rank, world)
 
     for _ in range(args.warmup):
         step()
@@ -157,6 +177,7 @@ def main():
     pairs_launch = rows * (N - 1)
     tflops = sweep_flops_per_pair() * pairs_launch / (pk_ms * 1e-3) / 1e12
     gbs = algorithmic_bytes_per_pair() * pairs_launch / (pk_ms * 1e-3) / 1e9
+    traffic = pmc_traffic() if world == 1 else None
     out = {
         "metric": "agent-pair LQR-obstacle evals/sec",
         "value": value,
@@ -185,8 +206,11 @@ def main():
             "peak": FP64_VALU_PEAK_TFLOPS,
             "unit": "TFLOP/s",
             "frac": tflops / FP64_VALU_PEAK_TFLOPS,
-            "traffic": None,
+            "traffic": traffic[0] if traffic else None,
+            "traffic_unit": "bytes/launch",
+            "traffic_source": traffic[1] if traffic else None,
             "flops_per_pair": sweep_flops_per_pair(),
+            "flops_per_pair_exact_order": exact_order_flops_per_pair(),
             "pairs_per_launch": pairs_launch,
             "kernel_ms": pk_ms,
             "hbm_algorithmic_gbs": gbs,

@@ -333,3 +333,39 @@ class Simulator:
         for q, v in zip(self.qlist, newv):
             q.newV = v.copy()
         return newv
+
+
+# ---------------------------------------------------------------------------
+# Multi-GPU: rows (agents i) block-sharded over ranks
+# ---------------------------------------------------------------------------
+def row_shard(n_agents: int, rank: int, world: int) -> tuple[int, int]:
+    """Rows [rb, re) owned by `rank`: balanced contiguous blocks (sizes
+    differ by at most one).  Every pair (i, j) of row i is computed by the
+    owner of i; no pair is split across ranks."""
+    if not (0 <= rank < world) or n_agents < world:
+        raise ValueError(f"cannot shard {n_agents} agents over {world} ranks")
+    return rank * n_agents // world, (rank + 1) * n_agents // world
+
+
+def allgather_rows(dist, full, rank: int, world: int, group=None):
+    """The per-step exchange: every rank holds its own rows of `full`
+    (an (N, k) tensor, rows from row_shard); afterwards every rank holds all
+    rows.  One all-gather of equal ceil(N/world)-row chunks — RCCL over xGMI
+    with the "nccl" backend, gloo on the CPU."""
+    import torch
+
+    n = full.shape[0]
+    chunk = -(-n // world)
+    rb, re = row_shard(n, rank, world)
+    send = torch.zeros((chunk,) + tuple(full.shape[1:]), dtype=full.dtype, device=full.device)
+    send[: re - rb] = full[rb:re]
+    recv = torch.empty((chunk * world,) + tuple(full.shape[1:]), dtype=full.dtype,
+                       device=full.device)
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(recv, send, group=group)
+    else:
+        dist.all_gather(list(recv.chunk(world)), send, group=group)
+    for r in range(world):
+        b, e = row_shard(n, r, world)
+        full[b:e] = recv[r * chunk: r * chunk + (e - b)]
+    return full
