@@ -5,22 +5,26 @@
 // (:869-874), runs qconvex.exe twice (:879-880) and takes
 //     min_f | n_f . (vrel - P[first vertex of f]) |   (:955-968)
 // over the hull facets, n_f from the hull of the ROUNDED points, P at full
-// precision.  Here one workgroup per inside-hull pair (persistent over the
-// queue k_pair fills):
+// precision.  One single-wave workgroup per inside-hull pair (persistent over
+// the queue k_pair fills):
 //   1. recomputes the pair's reachable points in reference order (exact, as
 //      k_pair does) and their %g round trip (lqro_device.hpp: round6);
-//   2. builds the hull of the rounded points by quickhull.  The hull's
-//      vertices (coordinates) and faces (vertex slots + adjacency) live in
-//      LDS; every insertion step — visible faces, horizon, cone, reassignment
-//      of outside points — runs across the workgroup.  Each point keeps the
-//      face it is outside of ("conflict") in global scratch, and an active
-//      list shrinks as points fall inside;
+//   2. builds the hull of the rounded points by quickhull: a LIFO stack of
+//      faces with outside points; each step inserts the furthest point of
+//      the popped face, grows its visible region over the face adjacency,
+//      links a cone over the horizon and re-distributes the region's outside
+//      points over the cone.  Topology (vertex slots, adjacency, stamps) and
+//      vertex coordinates live in LDS; outside sets, their extents and the
+//      furthest-point keys in per-block global scratch.  With one wave every
+//      step is a handful of dependent LDS round trips;
 //   3. evaluates the reference's facet formula on every facet (canonical
 //      facet order, lowest-index vertex) and writes the
 //      half-plane (createHalfPlanes, :1208-1221, inside => mult = +1).
 // A point is beyond a face iff n.(p - a) > eps |n|, n = (b-a) x (c-a),
 // eps = 1e-13 (max|coord| + 1) — the rule of the oracle's hull, so the facet
-// set (unique for points in general position) is the oracle's.
+// set (unique for points in general position) is the oracle's.  Jobs whose
+// hull outgrows the LDS capacities are re-run by k_hull_big with the same
+// code and the topology in global memory.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -30,12 +34,11 @@
 
 namespace lqro {
 
-#define HULL_THREADS 256
-#define HULL_FMAX 3072     // face slots per workgroup
-#define HULL_VTX 1400      // hull vertex slots per workgroup
-#define HULL_SBMULT 24     // outside-set segment buffer: HULL_SBMULT * H*NP entries
-#define HULL_HMAX 512      // horizon edges per insertion
-#define HULL_VMAX 1024     // visible faces per insertion
+#define HULL_THREADS 64          // one wave per hull
+#define HULL_SBMULT 24           // outside-set segment buffer: HULL_SBMULT * H*NP entries
+#define HULL_STKMULT 4           // work stack: HULL_STKMULT * H*NP faces
+#define HULL_FB_STRIDE 16384     // per-block face records in global scratch (= big faces)
+#define HULL_VG_STRIDE 8192      // per-block vertex records in global scratch (= big vertices)
 
 struct HullArgs {
   int N, X, H, NP;
@@ -55,6 +58,10 @@ struct HullArgs {
   int* iscratch;                    // per block: 2*H*NP ints (moved point, target face)
   float* fscratch;                  // per block: H*NP floats (distance beyond the target)
   int* sb;                          // per block: HULL_SBMULT*H*NP ints (outside-set segments)
+  unsigned long long* fbest;        // per block: HULL_FB_STRIDE furthest-point keys
+  int* fseg;                        // per block: 2*HULL_FB_STRIDE ints (outside-set offset, count)
+  int* vpid;                        // per block: HULL_VG_STRIDE vertex -> point ids
+  int* stack;                       // per block: HULL_STKMULT*H*NP faces
   int* rqueue;                      // pairs that overflowed the LDS variant
   int* rcount;
   int* rnext;
@@ -63,38 +70,52 @@ struct HullArgs {
   unsigned long long* prof;          // LQRO_HULL_PROFILE: per-phase cycles
 };
 
-// Hull topology and outside sets: in LDS for the common case, in global
+// Hull topology and vertex coordinates: LDS for the common case, global
 // scratch (larger capacities) for the jobs that overflow it.
 template <int FMAX, int VTX>
 struct HullMem {
   static constexpr int kFaces = FMAX, kVerts = VTX;
   unsigned short fv[FMAX][3];        // vertex slots, outward counter-clockwise
   unsigned short fa[FMAX][3];        // fa[f][e]: face across edge (fv[e], fv[e+1])
+  unsigned short vst[FMAX];          // visible-region stamp (insertion number)
+  unsigned short freel[FMAX];        // retired face slots
   unsigned char alive[FMAX];
-  unsigned char vis[FMAX];
-  unsigned short freel[FMAX];
-  int soff[FMAX], scnt[FMAX];        // outside set of face f: sb[soff .. soff+scnt)
-  unsigned long long fbest[FMAX];    // furthest outside point: (dist bits << 32) | ~q
   double vx[VTX][3];                 // hull vertex coordinates (rounded points)
-  int vpid[VTX];                     // vertex slot -> reachable-point index
+  unsigned short vmap[VTX];          // horizon: vertex slot -> edge leaving it
 };
-typedef HullMem<3072, 1400> HullMemSmall;   // ~135 KB: LDS
-typedef HullMem<16384, 8192> HullMemBig;    // ~750 KB: global scratch
+typedef HullMem<4752, 2368> HullMemSmall;   // ~141 KB: LDS
+typedef HullMem<16384, 8192> HullMemBig;    // ~480 KB: global scratch
 
-// per-workgroup control state (always LDS)
-struct HullLds {
-  int hcnt[HULL_HMAX], hoff[HULL_HMAX];
-  int vpre[HULL_VMAX + 1];
-  unsigned short vlist[HULL_VMAX];
-  unsigned short h_a[HULL_HMAX], h_b[HULL_HMAX], h_out[HULL_HMAX], h_new[HULL_HMAX];
+// per-step work lists (always LDS)
+template <int RG, int HZ>
+struct HullLdsT {
+  static constexpr int kRegion = RG, kHorizon = HZ;
+  unsigned short region[RG];                 // visible region of the apex
+  int roff[RG], rcnt[RG], rpre[RG + 1];      //   their outside sets
+  unsigned short h_a[HZ], h_b[HZ], h_out[HZ], h_new[HZ];   // horizon edges, cone faces
+  int hcnt[HZ], hoff[HZ];
+  double cn[HZ][8];                          // cone planes: n, a, |n|, eps |n|
   double tr[3 * 128];
   double rk[HULL_THREADS / 64];
   int ri[HULL_THREADS / 64];
-  int scan[HULL_THREADS];
-  int nf, nfree, nvtx, nvis, nh, fail, n, job, init[4], sbtop, fstar;
-  unsigned long long kstar;
+  int scan[HULL_THREADS / 64];
+  int nf, nfree, nvtx, fail, n, job, init[4], sbtop, sp, qh, it;
   double eps;
 };
+typedef HullLdsT<512, 128> HullLdsSmall;
+typedef HullLdsT<2048, 1024> HullLdsBig;
+
+static_assert(HULL_THREADS == 64, "the hull kernels are single-wave");
+
+// Ordering point between the lanes of the (single-wave) workgroup.  A wave
+// executes its LDS and its global memory operations in issue order, so only
+// the compiler has to be kept from moving memory operations across this
+// point; no s_waitcnt / s_barrier is needed (a workgroup fence would stall on
+// every outstanding global store).
+__device__ __forceinline__ void hl_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
 
 // n = (b-a) x (c-a) of face f
 template <class Mem>
@@ -122,7 +143,8 @@ __device__ __forceinline__ bool hl_beyond(const Mem& L, int f, const double* p, 
 }
 
 // block-wide argmax of (key, idx), lowest idx on ties; result in every thread
-__device__ __forceinline__ void hl_argmax(HullLds& L, double& key, int& idx) {
+template <class LT>
+__device__ __forceinline__ void hl_argmax(LT& L, double& key, int& idx) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
@@ -131,31 +153,62 @@ __device__ __forceinline__ void hl_argmax(HullLds& L, double& key, int& idx) {
     if (ok > key || (ok == key && oi < idx)) { key = ok; idx = oi; }
   }
   if (lane == 0) { L.rk[wave] = key; L.ri[wave] = idx; }
-  __syncthreads();
+  hl_sync();
   key = L.rk[0]; idx = L.ri[0];
   for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
     if (L.rk[w] > key || (L.rk[w] == key && L.ri[w] < idx)) { key = L.rk[w]; idx = L.ri[w]; }
-  __syncthreads();
+  hl_sync();
 }
 
 // exclusive block scan of v (0/1); total in *tot
-__device__ __forceinline__ int hl_scan(HullLds& L, int v, int* tot) {
+template <class LT>
+__device__ __forceinline__ int hl_scan(LT& L, int v, int* tot) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const unsigned long long b = __ballot(v != 0);
   const int in_wave = __popcll(b & ((1ull << lane) - 1ull));
   if (lane == 0) L.scan[wave] = __popcll(b);
-  __syncthreads();
+  hl_sync();
   int base = 0, t = 0;
   for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
     if (w < wave) base += L.scan[w];
     t += L.scan[w];
   }
   *tot = t;
-  __syncthreads();
+  hl_sync();
   return base + in_wave;
 }
 
+// exclusive block scan of v (any int); total in *tot
+template <class LT>
+__device__ __forceinline__ int hl_scan_val(LT& L, int v, int* tot) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) L.scan[wave] = x;
+  hl_sync();
+  int base = 0, t = 0;
+  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+    if (w < wave) base += L.scan[w];
+    t += L.scan[w];
+  }
+  *tot = t;
+  hl_sync();
+  return base + x - v;
+}
+
 #ifdef LQRO_HULL_PROFILE
+#define HSUB(k)                                                     \
+  do {                                                              \
+    if (tid == 0) {                                                 \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();   \
+      prof_sub[k] += t_ - prof_last;                                \
+      prof_last = t_;                                               \
+    }                                                               \
+  } while (0)
 #define HSTAMP(k)                                                   \
   do {                                                              \
     if (tid == 0) {                                                 \
@@ -166,13 +219,15 @@ __device__ __forceinline__ int hl_scan(HullLds& L, int v, int* tot) {
   } while (0)
 #else
 #define HSTAMP(k) do {} while (0)
+#define HSUB(k) do {} while (0)
 #endif
 
-template <class Mem>
-__device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, HullLds& L, bool big) {
+template <class Mem, class LT>
+__device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool big) {
   const int tid = threadIdx.x;
 #ifdef LQRO_HULL_PROFILE
   unsigned long long prof_acc[16] = {0};
+  unsigned long long prof_sub[6] = {0};
   unsigned long long prof_last = __builtin_amdgcn_s_memtime();
 #endif
   const int HNP = A.H * A.NP;
@@ -183,13 +238,20 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, HullLds& L,
   float* td = A.fscratch + (size_t)blockIdx.x * HNP;         // distance beyond it
   int* sb = A.sb + (size_t)blockIdx.x * HNP * HULL_SBMULT;
   const int sbcap = HNP * HULL_SBMULT;
+  // per face: furthest outside point (dist bits << 32) | ~q, outside-set extent
+  unsigned long long* fbest = A.fbest + (size_t)blockIdx.x * HULL_FB_STRIDE;
+  int* soff = A.fseg + (size_t)blockIdx.x * HULL_FB_STRIDE * 2;
+  int* scnt = soff + HULL_FB_STRIDE;
+  int* vpid = A.vpid + (size_t)blockIdx.x * HULL_VG_STRIDE;
+  int* stk = A.stack + (size_t)blockIdx.x * HNP * HULL_STKMULT;
+  const int stkcap = HNP * HULL_STKMULT;
 
   const int* queue = big ? A.rqueue : A.queue;
   const int* qcount = big ? A.rcount : A.count;
   int* qnext = big ? A.rnext : A.next;
   for (;;) {
     if (tid == 0) L.job = atomicAdd(qnext, 1);
-    __syncthreads();
+    hl_sync();
     const int job = L.job;
     if (job >= min(*qcount, A.cap)) break;
     const int slot = queue[job];
@@ -201,11 +263,14 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, HullLds& L,
     const double* Ti = A.T + (A.per_agent ? (size_t)i * A.H * 9 : 0);
     const double* Ni = A.NCF + (A.per_agent ? (size_t)i * A.H * 3 * A.X : 0);
     const double vrel[3] = {xi[3] - xj[3], xi[4] - xj[4], xi[5] - xj[5]};
+#ifdef LQRO_HULL_PROFILE
+    const unsigned long long job_t0 = __builtin_amdgcn_s_memtime();
+#endif
 
     HSTAMP(15);
     // 1. reachable points in reference order, full + %g-rounded
     if (tid == 0) { L.n = 0; L.fail = 0; }
-    __syncthreads();
+    hl_sync();
     for (int k0 = 0; k0 < A.H; k0 += 128) {
       for (int it = tid; it < 3 * 128; it += blockDim.x) {
         const int k = k0 + it / 3, r = it % 3;
@@ -215,7 +280,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, HullLds& L,
           L.tr[it] = d;
         }
       }
-      __syncthreads();
+      hl_sync();
       const int kend = min(A.H, k0 + 128);
       for (int q0 = k0 * A.NP; q0 < kend * A.NP; q0 += blockDim.x) {
         const int q = q0 + tid;
@@ -245,9 +310,9 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, HullLds& L,
           Pr[3 * pos + 2] = round6(p2, &oor);
           if (oor) L.fail = 7;
         }
-        __syncthreads();
+        hl_sync();
         if (tid == 0) L.n += tot;
-        __syncthreads();
+        hl_sync();
       }
     }
     const int n = L.n;
@@ -262,7 +327,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, HullLds& L,
         L.eps = 1e-13 * (mx + 1.0);
         if (n < 4) L.fail = 8;
       }
-      __syncthreads();
+      hl_sync();
     }
     const double eps = L.eps;
 
@@ -303,7 +368,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, HullLds& L,
         }
         M.fv[0][0] = 0; M.fv[0][1] = 1; M.fv[0][2] = 2;
       }
-      __syncthreads();
+      hl_sync();
       key = -INFINITY; idx = INT_MAX;
       for (int q = tid; q < n; q += blockDim.x) {
         double dd;
@@ -318,7 +383,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, HullLds& L,
         L.init[0] = i0; L.init[1] = i1; L.init[2] = i2; L.init[3] = i3;
         if (!L.fail) {
           for (int v = 0; v < 4; ++v) {
-            M.vpid[v] = L.init[v];
+            vpid[v] = L.init[v];
             for (int d = 0; d < 3; ++d) M.vx[v][d] = Pr[3 * L.init[v] + d];
           }
           L.nvtx = 4;
@@ -330,7 +395,6 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, HullLds& L,
             hl_beyond(M, f, M.vx[other], -INFINITY, &dd);
             if (dd > 0) { const unsigned short t = M.fv[f][1]; M.fv[f][1] = M.fv[f][2]; M.fv[f][2] = t; }
             M.alive[f] = 1;
-            M.vis[f] = 0;
           }
           for (int f = 0; f < 4; ++f)
             for (int e = 0; e < 3; ++e) {
@@ -343,14 +407,14 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, HullLds& L,
           L.nfree = 0;
         }
       }
-      __syncthreads();
+      hl_sync();
     }
 
     if (!L.fail) {
       // 4. outside sets of the tetrahedron's faces
-      if (tid < 4) { M.scnt[tid] = 0; M.fbest[tid] = 0ull; }
-      if (tid == 0) L.sbtop = 0;
-      __syncthreads();
+      if (tid < 4) { scnt[tid] = 0; fbest[tid] = 0ull; L.hcnt[tid] = 0; }
+      if (tid == 0) { L.sbtop = 0; L.sp = 0; L.qh = 0; L.it = 0; }
+      hl_sync();
       for (int q = tid; q < n; q += blockDim.x) {
         int c = -1;
         double dd = 0.0;
@@ -361,210 +425,353 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, HullLds& L,
         }
         th[q] = c;
         td[q] = (float)dd;
-        if (c >= 0) atomicAdd(&M.scnt[c], 1);
+        if (c >= 0) atomicAdd(&L.hcnt[c], 1);
       }
-      __syncthreads();
+      hl_sync();
       if (tid == 0) {
         int o = 0;
-        for (int f = 0; f < 4; ++f) { M.soff[f] = o; L.hcnt[f] = 0; o += M.scnt[f]; }
+        for (int f = 0; f < 4; ++f) {
+          soff[f] = o; scnt[f] = L.hcnt[f]; o += L.hcnt[f];
+          L.hoff[f] = soff[f];
+          M.vst[f] = 0;
+        }
+        for (int f = 0; f < 4; ++f)
+          if (L.hcnt[f] > 0) stk[L.sp++] = f;
         L.sbtop = o;
       }
-      __syncthreads();
+      hl_sync();
       for (int q = tid; q < n; q += blockDim.x) {
         const int c = th[q];
         if (c < 0) continue;
-        sb[M.soff[c] + atomicAdd(&L.hcnt[c], 1)] = q;
+        sb[atomicAdd(&L.hoff[c], 1)] = q;
         const unsigned long long key =
             ((unsigned long long)__float_as_uint(td[q]) << 32) | (unsigned long long)(~(unsigned)q);
-        atomicMax(&M.fbest[c], key);
+        atomicMax(&fbest[c], key);
       }
-      __syncthreads();
+      hl_sync();
 
       HSTAMP(1);
-      // 5. quickhull insertions
+      // 5. quickhull: take the oldest live face with outside points (FIFO
+      //    work queue: the hull grows evenly, which wastes fewer insertions
+      //    on points that later fall inside than depth-first order), insert
+      //    its furthest point.  One wave: every step is a few dependent LDS
+      //    round trips, no cross-wave barrier.
+      // The next queue entry's face, key and apex coordinates are fetched
+      // during the current insertion (three dependent global loads off the
+      // critical path).  They stay valid unless that face is retired (it is
+      // in the current region) or was dead when checked (its slot may be
+      // reused by a cone face of this insertion).
+      int pf_idx = -1, pf_face = 0;
+      bool pf_ok = false;
+      unsigned long long pf_key = 0ull;
+      double pf_p[3] = {0.0, 0.0, 0.0};
       for (;;) {
-        // (0) the face whose outside set holds the furthest point, and that point
-        if (tid == 0) { L.kstar = 0ull; L.fstar = -1; }
-        __syncthreads();
-        {
-          unsigned long long kb = 0ull;
-          for (int f = tid; f < L.nf; f += blockDim.x)
-            if (M.alive[f] && M.scnt[f] > 0 && M.fbest[f] > kb) kb = M.fbest[f];
-#pragma unroll
-          for (int off = 32; off >= 1; off >>= 1) {
-            const unsigned long long o = __shfl_xor(kb, off);
-            kb = o > kb ? o : kb;
-          }
-          if ((tid & 63) == 0 && kb) atomicMax(&L.kstar, kb);
-        }
-        __syncthreads();
-        if (L.kstar == 0ull) break;
-        const int apex = (int)(~(unsigned)(L.kstar & 0xFFFFFFFFull));
+        const int qh = L.qh, sp = L.sp;
+        if (qh == sp) break;
+        const bool use_pf = pf_ok && pf_idx == qh;
+        const int f = use_pf ? pf_face : stk[qh];
+        hl_sync();
+        if (tid == 0) L.qh = qh + 1;
+        // stale entries: the face was retired (its slot maybe reused by a
+        // face without outside points) after it was pushed
+        const unsigned long long key = use_pf ? pf_key : fbest[f];
+        pf_ok = false;
+        if (!M.alive[f] || key == 0ull) { hl_sync(); continue; }
+        const int apex = (int)(~(unsigned)(key & 0xFFFFFFFFull));
+        if (apex < 0 || apex >= n || L.it >= 4 * Mem::kVerts) { if (tid == 0) L.fail = 9; break; }
+        const int av = L.nvtx;
+        const unsigned short stamp = (unsigned short)(L.it + 1);
+        double p[3];
+        if (use_pf) { p[0] = pf_p[0]; p[1] = pf_p[1]; p[2] = pf_p[2]; }
+        else { p[0] = Pr[3 * apex]; p[1] = Pr[3 * apex + 1]; p[2] = Pr[3 * apex + 2]; }
+        pf_idx = qh + 1 < sp ? qh + 1 : -1;
+        if (pf_idx >= 0) pf_face = stk[pf_idx];
+        if (av >= Mem::kVerts) { if (tid == 0) L.fail = 1; break; }
         if (tid == 0) {
-          if (L.nvtx < Mem::kVerts) {
-            const int v = L.nvtx++;
-            M.vpid[v] = apex;
-            M.vx[v][0] = Pr[3 * apex]; M.vx[v][1] = Pr[3 * apex + 1]; M.vx[v][2] = Pr[3 * apex + 2];
-          } else {
-            L.fail = 1;
-          }
-          L.nvis = 0;
-          L.nh = 0;
+          M.vx[av][0] = p[0]; M.vx[av][1] = p[1]; M.vx[av][2] = p[2];
+          vpid[av] = apex;
+          L.nvtx = av + 1;
+          L.it = stamp;
+          L.region[0] = (unsigned short)f;
+          M.vst[f] = stamp;
         }
-        __syncthreads();
-        if (L.fail) break;
-        const int av = L.nvtx - 1;                   // the apex's vertex slot
+        hl_sync();
         HSTAMP(2);
-        // (a) visible faces: every live face the apex is beyond
-        for (int f = tid; f < L.nf; f += blockDim.x) {
-          if (!M.alive[f]) continue;
-          if (hl_beyond(M, f, M.vx[av], eps, nullptr)) {
-            M.vis[f] = 1;
-            const int t = atomicAdd(&L.nvis, 1);
-            if (t < HULL_VMAX) L.vlist[t] = (unsigned short)f;
-            else L.fail = 2;
+        // (a) visible region: grown over adjacency from f; lanes 0..2 test
+        //     the three neighbours of one region face at a time
+        int R = 1;
+        for (int r = 0; r < R; ++r) {
+          const int g = L.region[r];
+          int nb = -1, vis = 0;
+          if (tid < 3) {
+            nb = M.fa[g][tid];
+            vis = (M.vst[nb] != stamp) && hl_beyond(M, nb, p, eps, nullptr);
           }
+          const unsigned long long b = __ballot(vis);
+          if (vis) {
+            const int pos = R + __popcll(b & ((1ull << tid) - 1ull));
+            if (pos < LT::kRegion) { L.region[pos] = (unsigned short)nb; M.vst[nb] = stamp; }
+          }
+          R += __popcll(b);
+          if (R > LT::kRegion) break;
+          hl_sync();
         }
-        __syncthreads();
-        if (L.fail || L.nvis == 0) { if (tid == 0 && !L.fail) L.fail = 9; break; }
-        const int nvis = L.nvis;
+        if (R > LT::kRegion) { if (tid == 0) L.fail = 2; break; }
+        if (pf_idx >= 0) {
+          pf_ok = M.alive[pf_face] && M.vst[pf_face] != stamp;
+          if (pf_ok) pf_key = fbest[pf_face];
+        }
         HSTAMP(3);
-        // (b) horizon: edges of visible faces whose neighbour is not visible
-        for (int t = tid; t < nvis; t += blockDim.x) {
-          const int fh = L.vlist[t];
-          for (int e = 0; e < 3; ++e) {
-            const int nb = M.fa[fh][e];
-            if (!M.vis[nb]) {
-              const int h = atomicAdd(&L.nh, 1);
-              if (h < HULL_HMAX) {
-                L.h_a[h] = M.fv[fh][e];
-                L.h_b[h] = M.fv[fh][(e + 1) % 3];
-                L.h_out[h] = (unsigned short)nb;
-              } else {
-                L.fail = 3;
+        // (b) horizon: region edges whose neighbour is not in the region,
+        //     in (region order, edge) order
+        int nh = 0;
+        for (int b0 = 0; b0 < 3 * R; b0 += blockDim.x) {
+          const int t = b0 + tid;
+          int ha = 0, hb = 0, ho = 0, is = 0;
+          if (t < 3 * R) {
+            const int g = L.region[t / 3], e = t % 3;
+            ho = M.fa[g][e];
+            if (M.vst[ho] != stamp) { is = 1; ha = M.fv[g][e]; hb = M.fv[g][(e + 1) % 3]; }
+          }
+          int tot;
+          const int pos = nh + hl_scan(L, is, &tot);
+          if (is && pos < LT::kHorizon) {
+            L.h_a[pos] = (unsigned short)ha; L.h_b[pos] = (unsigned short)hb; L.h_out[pos] = (unsigned short)ho;
+          }
+          nh += tot;
+        }
+        if (nh > LT::kHorizon || nh < 3) { if (tid == 0) L.fail = 3; break; }
+        const int nf0 = L.nf, nfree0 = L.nfree;
+        if (nf0 + max(0, nh - nfree0) > Mem::kFaces) { if (tid == 0) L.fail = 4; break; }
+        // (c) cone face slots (retired slots first) and the vertex -> edge map
+        for (int h = tid; h < nh; h += blockDim.x) {
+          const int sf = h < nfree0 ? M.freel[nfree0 - 1 - h] : nf0 + (h - nfree0);
+          L.h_new[h] = (unsigned short)sf;
+          M.vmap[L.h_a[h]] = (unsigned short)h;
+          L.hcnt[h] = 0;
+        }
+        hl_sync();
+        HSTAMP(4);
+        // (d) cone faces (a, b, apex): adjacency, outer neighbours, planes
+        for (int h = tid; h < nh; h += blockDim.x) {
+          const int sf = L.h_new[h];
+          const int ha = L.h_a[h], hb = L.h_b[h], on = L.h_out[h];
+          const int k = M.vmap[hb];                    // edge leaving b
+          M.fv[sf][0] = (unsigned short)ha;
+          M.fv[sf][1] = (unsigned short)hb;
+          M.fv[sf][2] = (unsigned short)av;
+          M.fa[sf][0] = (unsigned short)on;
+          M.fa[sf][1] = L.h_new[k];                    // across (b, apex)
+          M.fa[L.h_new[k]][2] = (unsigned short)sf;    // k's (apex, a_k = b)
+          M.vst[sf] = 0;
+          for (int e = 0; e < 3; ++e)
+            if (M.fv[on][e] == hb && M.fv[on][(e + 1) % 3] == ha) M.fa[on][e] = (unsigned short)sf;
+          if (L.h_a[k] != hb) L.fail = 5;
+          // plane of the new face, as hl_normal / hl_beyond compute it
+          const double* a = M.vx[ha];
+          const double* bb = M.vx[hb];
+          const double e1[3] = {bb[0] - a[0], bb[1] - a[1], bb[2] - a[2]};
+          const double e2[3] = {p[0] - a[0], p[1] - a[1], p[2] - a[2]};
+          const double nx = e1[1] * e2[2] - e1[2] * e2[1];
+          const double ny = e1[2] * e2[0] - e1[0] * e2[2];
+          const double nz = e1[0] * e2[1] - e1[1] * e2[0];
+          double* cp = L.cn[h];
+          cp[0] = nx; cp[1] = ny; cp[2] = nz;
+          cp[3] = a[0]; cp[4] = a[1]; cp[5] = a[2];
+          cp[6] = sqrt(nx * nx + ny * ny + nz * nz);
+          cp[7] = eps * cp[6];
+          fbest[sf] = 0ull;
+        }
+        // retired faces' outside-set extents
+        for (int r = tid; r < R; r += blockDim.x) {
+          const int g = L.region[r];
+          L.roff[r] = soff[g];
+          L.rcnt[r] = scnt[g];
+        }
+        hl_sync();
+        if (L.fail) break;
+        {
+          int run = 0;
+          for (int r0 = 0; r0 < R; r0 += blockDim.x) {
+            const int r = r0 + tid;
+            const int v = r < R ? L.rcnt[r] : 0;
+            int tot;
+            const int pos = run + hl_scan_val(L, v, &tot);
+            if (r < R) L.rpre[r] = pos;
+            run += tot;
+          }
+          if (tid == 0) L.rpre[R] = run;
+        }
+        hl_sync();
+        HSTAMP(5);
+        // (e) the retired faces' outside points: first cone face they are beyond
+        const int total = L.rpre[R];
+        if (pf_ok) {
+          const int pa = (int)(~(unsigned)(pf_key & 0xFFFFFFFFull));
+          if (pa >= 0 && pa < n) { pf_p[0] = Pr[3 * pa]; pf_p[1] = Pr[3 * pa + 1]; pf_p[2] = Pr[3 * pa + 2]; }
+        }
+        HSUB(0);
+        if (total <= 4 * 64) {
+          // up to four points per lane, grouped by target with ballots; no
+          // scratch round trip
+          const unsigned long long lt = (1ull << tid) - 1ull;
+          int tg[4], qq[4];
+          float dv[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            tg[c] = -1; qq[c] = -1; dv[c] = 0.0f;
+            const int t = c * 64 + tid;
+            if (t < total) {
+              int lo = 0, hi = R - 1;
+              while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (L.rpre[mid] <= t) lo = mid; else hi = mid - 1;
+              }
+              qq[c] = sb[L.roff[lo] + (t - L.rpre[lo])];
+            }
+          }
+          HSUB(1);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int q = qq[c];
+            if (q >= 0 && q != apex) {
+              const double x0 = Pr[3 * q], x1 = Pr[3 * q + 1], x2 = Pr[3 * q + 2];
+              for (int h = 0; h < nh; ++h) {
+                const double* cp = L.cn[h];
+                const double d = cp[0] * (x0 - cp[3]) + cp[1] * (x1 - cp[4]) + cp[2] * (x2 - cp[5]);
+                if (d > cp[7]) { tg[c] = h; dv[c] = (float)(d / cp[6]); break; }
               }
             }
           }
-        }
-        __syncthreads();
-        if (L.fail) break;
-        const int nh = L.nh;
-        // (c) slots for the cone (faces retired in earlier rounds first);
-        //     prefix of the retired faces' outside-set sizes
-        for (int h = tid; h < nh; h += blockDim.x) {
-          int sf;
-          if (h < L.nfree) sf = M.freel[L.nfree - 1 - h];
-          else sf = L.nf + (h - L.nfree);
-          if (sf >= Mem::kFaces) { L.fail = 4; sf = 0; }
-          L.h_new[h] = (unsigned short)sf;
-          L.hcnt[h] = 0;
-        }
-        if (tid == 0) {
-          int o = 0;
-          for (int t = 0; t < nvis; ++t) { L.vpre[t] = o; o += M.scnt[L.vlist[t]]; }
-          L.vpre[nvis] = o;
-        }
-        __syncthreads();
-        if (L.fail) break;
-        HSTAMP(4);
-        // (d) cone faces (a, b, apex); patch the outer neighbours
-        for (int h = tid; h < nh; h += blockDim.x) {
-          const int sf = L.h_new[h];
-          M.fv[sf][0] = L.h_a[h];
-          M.fv[sf][1] = L.h_b[h];
-          M.fv[sf][2] = (unsigned short)av;
-          M.fa[sf][0] = L.h_out[h];
-          int n1 = -1, n2 = -1;
-          for (int g = 0; g < nh; ++g) {
-            if (L.h_a[g] == L.h_b[h]) n1 = L.h_new[g];   // edge (b, apex)
-            if (L.h_b[g] == L.h_a[h]) n2 = L.h_new[g];   // edge (apex, a)
+          HSUB(2);
+          int run = L.sbtop;
+          int mp[4] = {0, 0, 0, 0};
+          for (int h = 0; h < nh; ++h) {
+            const int base = run;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              if (c * 64 < total) {
+                const unsigned long long b = __ballot(tg[c] == h);
+                if (tg[c] == h) mp[c] = run + __popcll(b & lt);
+                run += __popcll(b);
+              }
+            }
+            if (tid == 0) { L.hcnt[h] = run - base; L.hoff[h] = base; }
           }
-          if (n1 < 0 || n2 < 0) L.fail = 5;
-          M.fa[sf][1] = (unsigned short)(n1 < 0 ? 0 : n1);
-          M.fa[sf][2] = (unsigned short)(n2 < 0 ? 0 : n2);
-          M.vis[sf] = 0;
-          M.scnt[sf] = 0;
-          M.fbest[sf] = 0ull;
-          const int on = L.h_out[h];
-          for (int e = 0; e < 3; ++e)
-            if (M.fv[on][e] == L.h_b[h] && M.fv[on][(e + 1) % 3] == L.h_a[h]) M.fa[on][e] = (unsigned short)sf;
-        }
-        __syncthreads();
-        if (L.fail) break;
-        HSTAMP(5);
-        // (e) the retired faces' outside points: which cone face (if any) now
-        const int total = L.vpre[nvis];
+          if (run > sbcap) { if (tid == 0) L.fail = 6; break; }
+          HSUB(3);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            if (tg[c] >= 0) {
+              sb[mp[c]] = qq[c];
+              const unsigned long long k2 =
+                  ((unsigned long long)__float_as_uint(dv[c]) << 32) | (unsigned long long)(~(unsigned)qq[c]);
+              atomicMax(&fbest[L.h_new[tg[c]]], k2);
+            }
+          }
+          hl_sync();
+          HSUB(4);
+          for (int h = tid; h < nh; h += blockDim.x) {
+            soff[L.h_new[h]] = L.hoff[h];
+            scnt[L.h_new[h]] = L.hcnt[h];
+          }
+          if (tid == 0) L.sbtop = run;
+          hl_sync();
+          HSUB(5);
+        } else {
         for (int t = tid; t < total; t += blockDim.x) {
-          int lo = 0, hi = nvis - 1;                 // face owning item t
+          int lo = 0, hi = R - 1;
           while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
-            if (L.vpre[mid] <= t) lo = mid; else hi = mid - 1;
+            if (L.rpre[mid] <= t) lo = mid; else hi = mid - 1;
           }
-          const int fo = L.vlist[lo];
-          const int q = sb[M.soff[fo] + (t - L.vpre[lo])];
+          const int q = sb[L.roff[lo] + (t - L.rpre[lo])];
           int tgt = -1;
-          double dd = 0.0;
+          float dd = 0.0f;
           if (q != apex) {
-            const double p[3] = {Pr[3 * q], Pr[3 * q + 1], Pr[3 * q + 2]};
-            for (int h = 0; h < nh; ++h)
-              if (hl_beyond(M, L.h_new[h], p, eps, &dd)) { tgt = h; break; }
+            const double x0 = Pr[3 * q], x1 = Pr[3 * q + 1], x2 = Pr[3 * q + 2];
+            for (int h = 0; h < nh; ++h) {
+              const double* cp = L.cn[h];
+              const double d = cp[0] * (x0 - cp[3]) + cp[1] * (x1 - cp[4]) + cp[2] * (x2 - cp[5]);
+              if (d > cp[7]) { tgt = h; dd = (float)(d / cp[6]); break; }
+            }
           }
           tq[t] = q;
           th[t] = tgt;
-          td[t] = (float)dd;
+          td[t] = dd;
           if (tgt >= 0) atomicAdd(&L.hcnt[tgt], 1);
         }
-        __syncthreads();
-        if (tid == 0) {
-          int o = L.sbtop;
-          for (int h = 0; h < nh; ++h) {
-            L.hoff[h] = o;
-            M.soff[L.h_new[h]] = o;
-            M.scnt[L.h_new[h]] = L.hcnt[h];
-            o += L.hcnt[h];
-            L.hcnt[h] = 0;
+        hl_sync();
+        {
+          int run = L.sbtop;
+          for (int h0 = 0; h0 < nh; h0 += blockDim.x) {
+            const int h = h0 + tid;
+            const int v = h < nh ? L.hcnt[h] : 0;
+            int tot;
+            const int pos = run + hl_scan_val(L, v, &tot);
+            if (h < nh) {
+              soff[L.h_new[h]] = pos;
+              scnt[L.h_new[h]] = v;
+              L.hoff[h] = pos;
+            }
+            run += tot;
           }
-          if (o > sbcap) L.fail = 6;
-          L.sbtop = o;
+          if (tid == 0) {
+            if (run > sbcap) L.fail = 6;
+            L.sbtop = run;
+          }
         }
-        __syncthreads();
+        hl_sync();
         if (L.fail) break;
         for (int t = tid; t < total; t += blockDim.x) {
           const int h = th[t];
           if (h < 0) continue;
           const int q = tq[t];
-          sb[L.hoff[h] + atomicAdd(&L.hcnt[h], 1)] = q;
-          const unsigned long long key =
+          sb[atomicAdd(&L.hoff[h], 1)] = q;
+          const unsigned long long k2 =
               ((unsigned long long)__float_as_uint(td[t]) << 32) | (unsigned long long)(~(unsigned)q);
-          atomicMax(&M.fbest[L.h_new[h]], key);
+          atomicMax(&fbest[L.h_new[h]], k2);
+        }
         }
         HSTAMP(6);
-        // (f) retire the visible faces, commit the cone
-        for (int t = tid; t < nvis; t += blockDim.x) {
-          const int f = L.vlist[t];
-          M.alive[f] = 0;
-          M.vis[f] = 0;
-          M.freel[L.nfree + t] = (unsigned short)f;
+        // (f) retire the region, commit the cone, push the cone faces that
+        //     have outside points (in horizon order; the last on top)
+        const int used = min(nh, nfree0);
+        for (int r = tid; r < R; r += blockDim.x) {
+          const int g = L.region[r];
+          M.alive[g] = 0;
+          M.freel[nfree0 - used + r] = (unsigned short)g;
         }
-        __syncthreads();
-        for (int h = tid; h < nh; h += blockDim.x) M.alive[L.h_new[h]] = 1;
+        int npush = 0;
+        for (int h0 = 0; h0 < nh; h0 += blockDim.x) {
+          const int h = h0 + tid;
+          int is = 0;
+          if (h < nh) {
+            M.alive[L.h_new[h]] = 1;
+            is = L.hcnt[h] > 0;
+          }
+          int tot;
+          const int pos = sp + npush + hl_scan(L, is, &tot);
+          if (is) {
+            if (pos < stkcap) stk[pos] = L.h_new[h];
+            else L.fail = 6;
+          }
+          npush += tot;
+        }
         if (tid == 0) {
-          // cone slots came off the top of the free list: move the retired
-          // faces (just pushed above it) down over them
-          const int used_free = min(nh, L.nfree);
-          if (used_free > 0)
-            for (int t = 0; t < nvis; ++t) M.freel[L.nfree - used_free + t] = M.freel[L.nfree + t];
-          L.nfree += nvis - used_free;
-          if (nh > used_free) L.nf += nh - used_free;
+          L.nfree = nfree0 - used + R;
+          L.nf = nf0 + (nh - used);
+          L.sp = sp + npush;
         }
-        __syncthreads();
+        hl_sync();
+        if (L.fail) break;
         HSTAMP(7);
 #ifdef LQRO_HULL_PROFILE
-        if (tid == 0) prof_acc[14] += 1;
+        if (tid == 0) { prof_acc[14] += 1; prof_acc[10] += (unsigned long long)R; prof_acc[11] += (unsigned long long)nh; prof_acc[12] += (unsigned long long)total; }
 #endif
       }
     }
-    __syncthreads();
+    hl_sync();
 
     HSTAMP(8);
     // 6. the reference's facet selection over all facets (canonical order)
@@ -575,7 +782,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, HullLds& L,
       for (int f = tid; f < L.nf; f += blockDim.x) {
         if (!M.alive[f]) continue;
         nfac++;
-        int t0 = M.vpid[M.fv[f][0]], t1 = M.vpid[M.fv[f][1]], t2 = M.vpid[M.fv[f][2]];
+        int t0 = vpid[M.fv[f][0]], t1 = vpid[M.fv[f][1]], t2 = vpid[M.fv[f][2]];
         while (!(t0 < t1 && t0 < t2)) { const int a = t0; t0 = t1; t1 = t2; t2 = a; }
         const double *a = Pr + 3 * t0, *b = Pr + 3 * t1, *c = Pr + 3 * t2;
         const double e1[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
@@ -608,7 +815,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, HullLds& L,
         s_best[wave] = best; s_t[wave][0] = bt0; s_t[wave][1] = bt1; s_t[wave][2] = bt2;
         s_n[wave][0] = bn[0]; s_n[wave][1] = bn[1]; s_n[wave][2] = bn[2]; s_cnt[wave] = nfac;
       }
-      __syncthreads();
+      hl_sync();
       if (tid == 0) {
         int fo = 0, total = 0;
         for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
@@ -662,24 +869,34 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, HullLds& L,
           }
         }
       }
-      __syncthreads();
+      hl_sync();
     }
     HSTAMP(9);
+#ifdef LQRO_HULL_PROFILE
+    if (tid == 0 && A.prof && job < 2048) {
+      const int pj = 32 + 2 * (big ? 2048 + job : job);
+      A.prof[pj] = __builtin_amdgcn_s_memtime() - job_t0;
+      A.prof[pj + 1] = (unsigned long long)L.nvtx | ((unsigned long long)n << 20) |
+                       ((unsigned long long)L.fail << 40) | ((unsigned long long)slot << 44);
+    }
+#endif
   }
 #ifdef LQRO_HULL_PROFILE
   if (tid == 0 && A.prof)
     for (int k = 0; k < 16; ++k) atomicAdd(&A.prof[k], prof_acc[k]);
+  if (tid == 0 && A.prof)
+    for (int k = 0; k < 6; ++k) atomicAdd(&A.prof[26 + k], prof_sub[k]);
 #endif
 }
 
 __global__ void __launch_bounds__(HULL_THREADS) k_hull(HullArgs A) {
-  __shared__ HullLds L;
+  __shared__ HullLdsSmall L;
   __shared__ HullMemSmall M;
   hull_body(A, M, L, false);
 }
 
 __global__ void __launch_bounds__(HULL_THREADS) k_hull_big(HullArgs A) {
-  __shared__ HullLds L;
+  __shared__ HullLdsBig L;
   HullMemBig& M = reinterpret_cast<HullMemBig*>(A.bigmem)[blockIdx.x];
   hull_body(A, M, L, true);
 }

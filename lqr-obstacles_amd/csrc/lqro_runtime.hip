@@ -34,6 +34,8 @@
 #include "lqro_pair.hpp"
 #include "lqro_hull.hpp"
 
+#define LQRO_PROF_WORDS (32 + 2 * 4096)   // hull profiling: 32 counters + 2 words per job
+
 using namespace lqro;
 
 #define LQRO_MAXX 16
@@ -217,6 +219,8 @@ struct lqro_ctx {
   double* d_hscratch;
   int* d_hiscratch;
   float* d_hfscratch;
+  unsigned long long* d_hfbest;
+  int *d_hfseg, *d_hvpid, *d_hstack;
   void* d_hfaces;
   int hull_blocks, hull_cap;
   unsigned long long* d_stats;
@@ -275,7 +279,7 @@ void lqro_destroy(lqro_ctx* c) {
   (void)hipSetDevice(c->cfg.device);
   void* ps[] = {c->d_R, c->d_TF, c->d_shash, c->d_T, c->d_NCF, c->d_S, c->d_x, c->d_vgoal, c->d_newv, c->d_A, c->d_B,
                 c->d_L, c->d_E, c->d_planes, c->d_lpscratch, c->d_lpcompact, c->d_recs, c->d_hq, c->d_hcount,
-                c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats, c->d_prof, c->d_rq, c->d_hbig};
+                c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats, c->d_prof, c->d_rq, c->d_hbig, c->d_hfbest, c->d_hfseg, c->d_hvpid, c->d_hstack};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (int k = 0; k < 5; ++k)
@@ -316,12 +320,16 @@ static int ctx_alloc(lqro_ctx* c) {
   HIPCHK(hipMalloc(&c->d_rq, sizeof(int) * c->hull_cap));
   HIPCHK(hipMalloc(&c->d_err, sizeof(int)));
   HIPCHK(hipMalloc(&c->d_stats, sizeof(unsigned long long) * 8));
-  HIPCHK(hipMalloc(&c->d_prof, sizeof(unsigned long long) * 32));
-  HIPCHK(hipMemset(c->d_prof, 0, sizeof(unsigned long long) * 32));
+  HIPCHK(hipMalloc(&c->d_prof, sizeof(unsigned long long) * LQRO_PROF_WORDS));
+  HIPCHK(hipMemset(c->d_prof, 0, sizeof(unsigned long long) * LQRO_PROF_WORDS));
   c->hull_blocks = 256;   // one 138 KB-LDS workgroup per CU, persistent over the queue
   HIPCHK(hipMalloc(&c->d_hscratch, sizeof(double) * 6 * H * NP * c->hull_blocks));
   HIPCHK(hipMalloc(&c->d_hiscratch, sizeof(int) * 2 * H * NP * c->hull_blocks));
   HIPCHK(hipMalloc(&c->d_hfscratch, sizeof(float) * H * NP * c->hull_blocks));
+  HIPCHK(hipMalloc(&c->d_hfbest, sizeof(unsigned long long) * HULL_FB_STRIDE * (size_t)c->hull_blocks));
+  HIPCHK(hipMalloc(&c->d_hfseg, sizeof(int) * 2 * HULL_FB_STRIDE * (size_t)c->hull_blocks));
+  HIPCHK(hipMalloc(&c->d_hvpid, sizeof(int) * HULL_VG_STRIDE * (size_t)c->hull_blocks));
+  HIPCHK(hipMalloc(&c->d_hstack, sizeof(int) * HULL_STKMULT * H * NP * (size_t)c->hull_blocks));
   HIPCHK(hipMalloc(&c->d_hfaces, sizeof(int) * HULL_SBMULT * H * NP * (size_t)c->hull_blocks));
   c->hull_big_blocks = 64;
   HIPCHK(hipMalloc(&c->d_hbig, sizeof(HullMemBig) * (size_t)c->hull_big_blocks));
@@ -492,6 +500,8 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   Hh.queue = c->d_hq; Hh.count = c->d_hcount; Hh.cap = c->hull_cap; Hh.next = c->d_hnext;
   Hh.scratch = c->d_hscratch; Hh.iscratch = c->d_hiscratch; Hh.fscratch = c->d_hfscratch;
   Hh.sb = reinterpret_cast<int*>(c->d_hfaces);
+  Hh.fbest = c->d_hfbest;
+  Hh.fseg = c->d_hfseg; Hh.vpid = c->d_hvpid; Hh.stack = c->d_hstack;
   Hh.rqueue = c->d_rq; Hh.rcount = c->d_hcount + 2; Hh.rnext = c->d_hcount + 3;
   Hh.bigmem = c->d_hbig;
   Hh.stats = c->d_stats;
@@ -614,7 +624,7 @@ int lqro_debug_hull_profile(lqro_ctx* c, unsigned long long* out16) {
   if (!c || !out16) return LQRO_E_ARG;
   HIPCHK(hipSetDevice(c->cfg.device));
   HIPCHK(hipStreamSynchronize(c->stream));
-  HIPCHK(hipMemcpy(out16, c->d_prof, sizeof(unsigned long long) * 32, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(out16, c->d_prof, sizeof(unsigned long long) * LQRO_PROF_WORDS, hipMemcpyDeviceToHost));
   return LQRO_OK;
 }
 
