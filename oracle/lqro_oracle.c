@@ -1116,6 +1116,10 @@ void orc_newv(int m, const float* pl, const double* vgoal, double vmax_lp, doubl
   free(planes); free(scratch);
 }
 
+/* operator! on a 3x3 / 4x4 matrix (MAT:603-671), for the tests */
+void orc_inverse3(const double* in, double* out) { minv(3, in, out); }
+void orc_inverse4(const double* in, double* out) { minv(4, in, out); }
+
 /* ------------------------------------------------------------------------ */
 /* Whole step                                                                */
 /* ------------------------------------------------------------------------ */

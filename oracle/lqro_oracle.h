@@ -101,6 +101,10 @@ int  orc_hull(int n, const double* pts, int32_t* facets, int cap);
 
 /* %g (6 significant digits) round trip of one double: what qconvex reads
  * back from pointList.txt (LQRO:871-873). */
+/* operator! (MAT:603-671) on 3x3 / 4x4 row-major matrices. */
+void orc_inverse3(const double* in, double* out);
+void orc_inverse4(const double* in, double* out);
+
 double orc_round6(double v);
 
 #ifdef __cplusplus
