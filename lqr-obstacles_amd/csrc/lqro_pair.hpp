@@ -39,7 +39,8 @@ constexpr int kMaxPW = 4;
 struct PairArgs {
   int N, H, NP, PW, min_reach;
   int row_begin, nrows, npr;          // npr = pairs per row = N-1
-  int blocks_per_row, pairs_per_block, waves;
+  int waves;
+  int* row_counter;                   // persistent row queue (zeroed per step)
   int per_agent;
   double vmax, r2, r2_lo, r2_hi;      // reachable radius, its square, fast-test bounds
   double rad0, rad1, rad2, umax;      // sphere semi-axes (2 r_xy, 2 r_xy, 2 r_z); max |u_p|
@@ -56,6 +57,7 @@ struct PairArgs {
   int* hull_count;
   int hull_cap;
   unsigned long long* stats;          // 8 counters
+  unsigned long long* prof;           // LQRO_PAIR_PROFILE: per-phase cycles (16 words)
   // LDS layout, in doubles
   int XP, lds_T, lds_N, lds_S, lds_R, lds_TF, lds_H, lds_wave, wave_doubles;
 };
@@ -71,7 +73,6 @@ struct BlockTabs {
 
 struct WaveTabs {
   double* tr;                // H x 3
-  double* c;                 // H x 3
   double* sc;                // H: magnitude scale for the margins
   double* ub;                // H: support bounds of the current query
   int* cls;                  // H
@@ -158,8 +159,10 @@ struct SliceSupport {
         const double w1 = Tk[1] * d0 + Tk[4] * d1 + Tk[7] * d2;
         const double w2 = Tk[2] * d0 + Tk[5] * d1 + Tk[8] * d2;
         const double a0 = P.rad0 * w0, a1 = P.rad1 * w1, a2 = P.rad2 * w2;
-        const double* ck = W.c + 3 * k;
-        ub = ck[0] * d0 + ck[1] * d1 + ck[2] * d2 + sqrt(a0 * a0 + a1 * a1 + a2 * a2) * P.umax +
+        // c_k.d = (T_k tr_k).d = tr_k.(T_k^T d); the reassociation error is
+        // ~1e-16 |tr| ||T|| |d|, far inside the 1e-9 dn sc margin
+        const double* tk = W.tr + 3 * k;
+        ub = tk[0] * w0 + tk[1] * w1 + tk[2] * w2 + sqrt(a0 * a0 + a1 * a1 + a2 * a2) * P.umax +
              1e-9 * dn * W.sc[k];
       }
       W.ub[k] = ub;
@@ -200,47 +203,41 @@ __device__ inline int reach_rank(const PairArgs& P, const WaveTabs& W, int lane,
   return cnt;
 }
 
+#ifdef LQRO_PAIR_PROFILE
+#define PSTAMP(k)                                                   \
+  do {                                                              \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();     \
+    pp[k] += t_ - p_last;                                           \
+    p_last = t_;                                                    \
+  } while (0)
+#else
+#define PSTAMP(k) do {} while (0)
+#endif
+
 template <int X>
 __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
+#ifdef LQRO_PAIR_PROFILE
+  unsigned long long pp[16] = {0};
+  unsigned long long p_last = __builtin_amdgcn_s_memtime();
+#endif
   extern __shared__ double lds[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int lrow = blockIdx.x / P.blocks_per_row;
-  const int chunk = blockIdx.x % P.blocks_per_row;
-  const int i = P.row_begin + lrow;
   const int H = P.H, NP = P.NP, XP = P.XP;
+  __shared__ int s_row, s_next;
 
-  // agent i's horizon tables and the sphere, staged once per workgroup
-  const size_t ag = P.per_agent ? (size_t)i : 0;
   double* sT = lds + P.lds_T;
   double* sN = lds + P.lds_N;
   double* sS = lds + P.lds_S;
   double* sR = lds + P.lds_R;
   double* sTF = lds + P.lds_TF;
   unsigned long long* sH = reinterpret_cast<unsigned long long*>(lds + P.lds_H);
-  {
-    const double* Ti = P.T + ag * H * 9;
-    const double* Ni = P.NCF + ag * H * 3 * X;
-    const double* Ri = P.R + ag * H;
-    const double* TFi = P.TF + ag * H;
-    for (int q = threadIdx.x; q < H * 9; q += blockDim.x) sT[q] = Ti[q];
-    for (int q = threadIdx.x; q < H * 3 * X; q += blockDim.x) sN[(q / X) * XP + (q % X)] = Ni[q];
-    for (int q = threadIdx.x; q < NP * 3; q += blockDim.x) sS[(q % 3) * NP + q / 3] = P.S[q];
-    for (int q = threadIdx.x; q < H; q += blockDim.x) {
-      sR[q] = Ri[q];
-      sTF[q] = TFi[q];
-      sH[q] = P.shash[q];
-    }
-  }
-  __syncthreads();
-
   BlockTabs B;
   B.T = sT; B.N = sN; B.S = sS; B.R = sR; B.TF = sTF; B.shash = sH;
   WaveTabs W;
   {
     double* w = lds + P.lds_wave + (size_t)wave * P.wave_doubles;
     W.tr = w;            w += 3 * H;
-    W.c = w;             w += 3 * H;
     W.sc = w;            w += H;
     W.ub = w;            w += H;
     W.mask = reinterpret_cast<unsigned long long*>(w);  w += H * P.PW;
@@ -249,13 +246,44 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
     W.cnt = wi;          wi += H;
     W.mixed = wi;
   }
-  const double* xi = P.x + (size_t)i * X;
-  const int jj_begin = chunk * P.pairs_per_block;
-  const int jj_end = min(P.npr, jj_begin + P.pairs_per_block);
   unsigned long long st_reach = 0, st_iters = 0, st_planes = 0, st_inside = 0, st_backup = 0;
   SliceSupport sup{P, B, W, lane};
 
-  for (int jj = jj_begin + wave; jj < jj_end; jj += P.waves) {
+  // Persistent: the workgroup takes whole rows (agent i) off a queue; its
+  // waves take the row's pairs one at a time (LDS counter), so uneven pair
+  // costs balance inside the row.  Agent i's horizon tables are staged into
+  // LDS only when they change (once per workgroup with shared gains).
+  long staged = -1;
+  for (;;) {
+    if (threadIdx.x == 0) { s_row = atomicAdd(P.row_counter, 1); s_next = 0; }
+    __syncthreads();
+    const int lrow = s_row;
+    if (lrow >= P.nrows) break;
+    const int i = P.row_begin + lrow;
+    const long ag = P.per_agent ? (long)i : 0;
+    if (ag != staged) {
+      const double* Ti = P.T + ag * H * 9;
+      const double* Ni = P.NCF + ag * H * 3 * X;
+      const double* Ri = P.R + ag * H;
+      const double* TFi = P.TF + ag * H;
+      for (int q = threadIdx.x; q < H * 9; q += blockDim.x) sT[q] = Ti[q];
+      for (int q = threadIdx.x; q < H * 3 * X; q += blockDim.x) sN[(q / X) * XP + (q % X)] = Ni[q];
+      for (int q = threadIdx.x; q < NP * 3; q += blockDim.x) sS[(q % 3) * NP + q / 3] = P.S[q];
+      for (int q = threadIdx.x; q < H; q += blockDim.x) {
+        sR[q] = Ri[q];
+        sTF[q] = TFi[q];
+        sH[q] = P.shash[q];
+      }
+      staged = ag;
+      __syncthreads();
+    }
+    PSTAMP(0);
+    const double* xi = P.x + (size_t)i * X;
+  for (;;) {
+    int jj = 0;
+    if (lane == 0) jj = atomicAdd(&s_next, 1);
+    jj = __shfl(jj, 0);
+    if (jj >= P.npr) break;
     const int j = jj < i ? jj : jj + 1;
     const double* xj = P.x + (size_t)j * X;
     double d[X];
@@ -263,6 +291,7 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
     for (int c = 0; c < X; ++c) d[c] = xi[c] - xj[c];                       // (xInit1-xInit2)
     const double vrel[3] = {xi[3] - xj[3], xi[4] - xj[4], xi[5] - xj[5]};    // :794-796
     unsigned long long hsh = 0;
+    PSTAMP(7);
 
     // 1. per slice: Translate (exact), centre, class       (lanes <-> k)
     for (int k = lane; k < H; k += 64) {
@@ -279,7 +308,6 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
       const double c0 = Tk[0] * t0 + Tk[1] * t1 + Tk[2] * t2;
       const double c1 = Tk[3] * t0 + Tk[4] * t1 + Tk[5] * t2;
       const double c2 = Tk[6] * t0 + Tk[7] * t1 + Tk[8] * t2;
-      W.c[3 * k] = c0; W.c[3 * k + 1] = c1; W.c[3 * k + 2] = c2;
       const double Rk = B.R[k];
       const double sc = sqrt(c0 * c0 + c1 * c1 + c2 * c2) + Rk +
                         B.TF[k] * sqrt(t0 * t0 + t1 * t1 + t2 * t2) + 1.0;
@@ -303,6 +331,7 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
       if (cls == kSliceIn) hsh += B.shash[k];
     }
     wave_lds_sync();
+    PSTAMP(1);
 
     // 2. MIXED slices: per-point exact test                 (lanes <-> p)
     int nmixed = 0;
@@ -336,6 +365,10 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
       }
     }
     wave_lds_sync();
+    PSTAMP(2);
+#ifdef LQRO_PAIR_PROFILE
+    pp[10] += nmixed;
+#endif
 
     // n_reach and the first reachable point
     int n = 0, qfirst = INT_MAX;
@@ -354,6 +387,7 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
       hsh += __shfl_xor(hsh, off);
     }
     st_reach += n;
+    PSTAMP(3);
 
     // 3. GJK and the half-plane
     int flags = 0;
@@ -390,6 +424,7 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
         pl[6] = __int_as_float(2);                              // completed by k_hull
       }
     }
+    PSTAMP(4);
     const size_t slot = (size_t)lrow * P.npr + jj;
     int sranks[4] = {-1, -1, -1, -1};
     if (P.recs != nullptr && g.npts > 0)
@@ -423,7 +458,17 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
       }
     }
     wave_lds_sync();
+    PSTAMP(5);
+#ifdef LQRO_PAIR_PROFILE
+    pp[11] += 1;
+#endif
   }
+    __syncthreads();   // the row is done before s_row / the tables change
+  }
+#ifdef LQRO_PAIR_PROFILE
+  if (lane == 0 && P.prof)
+    for (int k = 0; k < 16; ++k) atomicAdd(&P.prof[k], pp[k]);
+#endif
   if (lane == 0) {
     atomicAdd(&P.stats[1], st_planes);
     atomicAdd(&P.stats[2], st_inside);

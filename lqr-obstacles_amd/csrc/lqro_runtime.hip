@@ -34,7 +34,7 @@
 #include "lqro_pair.hpp"
 #include "lqro_hull.hpp"
 
-#define LQRO_PROF_WORDS (32 + 2 * 4096)   // hull profiling: 32 counters + 2 words per job
+#define LQRO_PROF_WORDS (32 + 2 * 4096 + 16)   // hull: 32 counters + 2 words per job; pair: 16
 
 using namespace lqro;
 
@@ -216,6 +216,7 @@ struct lqro_ctx {
   int *d_hq, *d_hcount, *d_hnext, *d_err, *d_rq;
   void* d_hbig;
   int hull_big_blocks;
+  int n_cu;
   double* d_hscratch;
   int* d_hiscratch;
   float* d_hfscratch;
@@ -315,7 +316,7 @@ static int ctx_alloc(lqro_ctx* c) {
   c->hull_cap = (int)(slots < (1u << 22) ? slots : (1u << 22));
   if (c->hull_cap < 1) c->hull_cap = 1;
   HIPCHK(hipMalloc(&c->d_hq, sizeof(int) * c->hull_cap));
-  HIPCHK(hipMalloc(&c->d_hcount, sizeof(int) * 4));   // count, next, retry count, retry next
+  HIPCHK(hipMalloc(&c->d_hcount, sizeof(int) * 8));   // count, next, retry count, retry next, pair rows
   c->d_hnext = c->d_hcount + 1;
   HIPCHK(hipMalloc(&c->d_rq, sizeof(int) * c->hull_cap));
   HIPCHK(hipMalloc(&c->d_err, sizeof(int)));
@@ -356,6 +357,7 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
   if (!c) return LQRO_E_NOMEM;
   memset(c, 0, sizeof *c);
   c->cfg = g;
+  c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   c->rb = g.row_begin;
   c->re = (g.row_end > g.row_begin) ? g.row_end : g.n_agents;
   if (g.row_end == 0 && g.row_begin == 0) { c->rb = 0; c->re = g.n_agents; }
@@ -376,8 +378,8 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
   P.lds_TF = off; off += H;
   P.lds_H = off; off += H;
   P.lds_wave = off;
-  // tr 3H, c 3H, sc H, ub H, mask H*PW (u64), cls/cnt/mixed 3H ints
-  P.wave_doubles = 8 * H + H * P.PW + (3 * H + 1) / 2;
+  // tr 3H, sc H, ub H, mask H*PW (u64), cls/cnt/mixed 3H ints
+  P.wave_doubles = 5 * H + H * P.PW + (3 * H + 1) / 2;
   const int budget = 160 * 1024 / 8;
   int waves = (budget - off) / P.wave_doubles;
   if (waves > LQRO_PAIR_LB / 64) waves = LQRO_PAIR_LB / 64;
@@ -476,13 +478,13 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   P.planes = c->d_planes; P.recs = c->d_recs;
   P.hull_queue = c->d_hq; P.hull_count = c->d_hcount; P.hull_cap = c->hull_cap;
   P.stats = c->d_stats;
-  // one workgroup = P.waves wavefronts on one row; each wave takes several pairs
-  P.pairs_per_block = P.waves * 4;
-  P.blocks_per_row = (c->npr + P.pairs_per_block - 1) / P.pairs_per_block;
-  HIPCHK(hipMemsetAsync(c->d_hcount, 0, sizeof(int) * 4, s));
+  P.prof = c->d_prof + 32 + 2 * 4096;
+  // persistent: one workgroup per CU (LDS-bound), rows off a queue
+  P.row_counter = c->d_hcount + 4;
+  HIPCHK(hipMemsetAsync(c->d_hcount, 0, sizeof(int) * 8, s));
   HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * 8, s));
   HIPCHK(hipEventRecord(c->ev[0], s));
-  const unsigned nblk = (unsigned)P.blocks_per_row * (unsigned)c->nrows;
+  const unsigned nblk = (unsigned)std::min(c->nrows, c->n_cu);
   if (g.x_dim == 16)
     hipLaunchKernelGGL(k_pair<16>, dim3(nblk), dim3(P.waves * 64), c->lds_bytes, s, P);
   else if (g.x_dim == 12)

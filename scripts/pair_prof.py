@@ -1,0 +1,25 @@
+"""Per-phase cycle profile of k_pair at C3 (liblqro_pprof.so, -DLQRO_PAIR_PROFILE)."""
+import sys, os, ctypes as C, numpy as np
+sys.path[:0] = [os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "lqr-obstacles_amd")]
+import lqro
+lqro.LIB_PATH = os.path.join(os.path.dirname(lqro.LIB_PATH), "liblqro_pprof.so")
+L = lqro.lib()
+N, H, NP = 1024, 100, 100
+x, vg = lqro.synthetic_swarm(N)
+g = lqro.synthesize_gains()
+c = lqro.Context(lqro.config(N, H, NP))
+c.set_gains(g["A"], g["B"], g["L"], g["E"])
+c.step(x, vg)
+print(c.timings(), c.stats())
+out = np.zeros(32 + 2 * 4096 + 16, np.uint64)
+L.lqro_debug_hull_profile(c._h, out.ctypes.data_as(C.c_void_p))
+pp = out[32 + 2 * 4096:]
+names = ["tables->LDS", "classify", "mixed", "nreach", "gjk", "write", "", "loop-top"]
+tot = pp[:8].sum()
+for k in range(8):
+    if pp[k]:
+        print(f"{names[k]:12s} {int(pp[k]):14d} {100 * pp[k] / tot:5.1f}%")
+pairs = int(pp[11])
+print("pairs", pairs, "mixed slices/pair %.2f" % (pp[10] / max(pairs, 1)),
+      "slice evals/pair %.2f" % (pp[12] / max(pairs, 1)),
+      "cycles/pair/wave %.0f" % (tot / max(pairs, 1)))
