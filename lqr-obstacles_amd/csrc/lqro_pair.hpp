@@ -41,6 +41,7 @@ struct PairArgs {
   int row_begin, nrows, npr;          // npr = pairs per row = N-1
   int waves;
   int* row_counter;                   // persistent row queue (zeroed per step)
+  int* pair_done;                     // finished workgroups (k_hull workers wait on it)
   int per_agent;
   double vmax, r2, r2_lo, r2_hi;      // reachable radius, its square, fast-test bounds
   double rad0, rad1, rad2, umax;      // sphere semi-axes (2 r_xy, 2 r_xy, 2 r_z); max |u_p|
@@ -435,8 +436,10 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
       dst[0] = make_float4(pl[0], pl[1], pl[2], pl[3]);
       dst[1] = make_float4(pl[4], pl[5], pl[6], pl[7]);
       if (inside) {
+        // published with release: k_hull workers may already be polling
         const int qi = atomicAdd(P.hull_count, 1);
-        if (qi < P.hull_cap) P.hull_queue[qi] = (int)slot;
+        if (qi < P.hull_cap)
+          __hip_atomic_store(P.hull_queue + qi, (int)slot, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       }
       if (P.recs != nullptr) {
         lqro_pair_record rec;
@@ -465,6 +468,9 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
   }
     __syncthreads();   // the row is done before s_row / the tables change
   }
+  // every queue entry of this workgroup is published: count it finished
+  if (threadIdx.x == 0)
+    __hip_atomic_fetch_add(P.pair_done, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 #ifdef LQRO_PAIR_PROFILE
   if (lane == 0 && P.prof)
     for (int k = 0; k < 16; ++k) atomicAdd(&P.prof[k], pp[k]);

@@ -209,6 +209,8 @@ struct lqro_ctx {
   int have_gains, per_agent;
   hipStream_t stream;
   hipEvent_t ev[5];
+  hipStream_t side;          // k_hull workers running beside k_pair
+  hipEvent_t xev[2];         // cross-stream ordering (no timing)
   double *d_T, *d_NCF, *d_S, *d_x, *d_vgoal, *d_newv;
   double *d_A, *d_B, *d_L, *d_E;
   float *d_planes, *d_lpscratch, *d_lpcompact;
@@ -285,6 +287,9 @@ void lqro_destroy(lqro_ctx* c) {
     if (p) (void)hipFree(p);
   for (int k = 0; k < 5; ++k)
     if (c->ev[k]) (void)hipEventDestroy(c->ev[k]);
+  for (int k = 0; k < 2; ++k)
+    if (c->xev[k]) (void)hipEventDestroy(c->xev[k]);
+  if (c->side) (void)hipStreamDestroy(c->side);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -295,6 +300,8 @@ static int ctx_alloc(lqro_ctx* c) {
   const size_t slots = (size_t)c->nrows * c->npr;
   HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   for (int k = 0; k < 5; ++k) HIPCHK(hipEventCreate(&c->ev[k]));
+  HIPCHK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+  for (int k = 0; k < 2; ++k) HIPCHK(hipEventCreateWithFlags(&c->xev[k], hipEventDisableTiming));
   HIPCHK(hipMalloc(&c->d_S, sizeof(double) * NP * 3));
   HIPCHK(hipMalloc(&c->d_x, sizeof(double) * N * X));
   HIPCHK(hipMalloc(&c->d_vgoal, sizeof(double) * N * 3));
@@ -479,20 +486,17 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   P.hull_queue = c->d_hq; P.hull_count = c->d_hcount; P.hull_cap = c->hull_cap;
   P.stats = c->d_stats;
   P.prof = c->d_prof + 32 + 2 * 4096;
-  // persistent: one workgroup per CU (LDS-bound), rows off a queue
+  // persistent: one workgroup per CU (LDS-bound), rows off a queue.  A few
+  // CUs run k_hull workers beside it (side stream) so that inside-hull pairs
+  // start as soon as k_pair finds them; the rest of the hull queue is taken by
+  // a full-width k_hull after k_pair.
   P.row_counter = c->d_hcount + 4;
+  P.pair_done = c->d_hcount + 5;
   HIPCHK(hipMemsetAsync(c->d_hcount, 0, sizeof(int) * 8, s));
   HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * 8, s));
-  HIPCHK(hipEventRecord(c->ev[0], s));
-  const unsigned nblk = (unsigned)std::min(c->nrows, c->n_cu);
-  if (g.x_dim == 16)
-    hipLaunchKernelGGL(k_pair<16>, dim3(nblk), dim3(P.waves * 64), c->lds_bytes, s, P);
-  else if (g.x_dim == 12)
-    hipLaunchKernelGGL(k_pair<12>, dim3(nblk), dim3(P.waves * 64), c->lds_bytes, s, P);
-  else
-    return LQRO_E_ARG;
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(c->ev[1], s));
+  HIPCHK(hipMemsetAsync(c->d_hq, 0xFF, sizeof(int) * (size_t)c->hull_cap, s));
+  const int nwait = (c->nrows >= 4 * c->n_cu && c->n_cu >= 64) ? c->n_cu / 8 : 0;
+  const unsigned nblk = (unsigned)std::min(c->nrows, c->n_cu - nwait);
   HullArgs Hh;
   Hh.N = g.n_agents; Hh.X = g.x_dim; Hh.H = g.horizon; Hh.NP = g.n_points;
   Hh.row_begin = c->rb; Hh.npr = c->npr; Hh.per_agent = c->per_agent;
@@ -508,8 +512,32 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   Hh.bigmem = c->d_hbig;
   Hh.stats = c->d_stats;
   Hh.prof = c->d_prof;
-  hipLaunchKernelGGL(k_hull, dim3(c->hull_blocks), dim3(HULL_THREADS), 0, s, Hh);
+  Hh.pair_done = P.pair_done;
+  Hh.pair_blocks = (int)nblk;
+  Hh.block_base = 0;
+  Hh.wait_pairs = 1;
+  if (nwait > 0) {
+    HIPCHK(hipEventRecord(c->xev[0], s));
+    HIPCHK(hipStreamWaitEvent(c->side, c->xev[0], 0));
+    hipLaunchKernelGGL(k_hull, dim3(nwait), dim3(HULL_THREADS), 0, c->side, Hh);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->xev[1], c->side));
+  }
+  HIPCHK(hipEventRecord(c->ev[0], s));
+  if (g.x_dim == 16)
+    hipLaunchKernelGGL(k_pair<16>, dim3(nblk), dim3(P.waves * 64), c->lds_bytes, s, P);
+  else if (g.x_dim == 12)
+    hipLaunchKernelGGL(k_pair<12>, dim3(nblk), dim3(P.waves * 64), c->lds_bytes, s, P);
+  else
+    return LQRO_E_ARG;
   HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->ev[1], s));
+  Hh.block_base = nwait;
+  Hh.wait_pairs = 0;
+  hipLaunchKernelGGL(k_hull, dim3(c->hull_blocks - nwait), dim3(HULL_THREADS), 0, s, Hh);
+  HIPCHK(hipGetLastError());
+  if (nwait > 0) HIPCHK(hipStreamWaitEvent(s, c->xev[1], 0));
+  Hh.block_base = 0;
   hipLaunchKernelGGL(k_hull_big, dim3(c->hull_big_blocks), dim3(HULL_THREADS), 0, s, Hh);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev[2], s));

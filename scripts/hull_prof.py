@@ -10,9 +10,9 @@ c = lqro.Context(lqro.config(N, H, NP))
 c.set_gains(g["A"], g["B"], g["L"], g["E"])
 c.step(x, vg)
 print(c.timings(), c.stats())
-out = np.zeros(32 + 2 * 4096, np.uint64)
+out = np.zeros(32 + 2 * 4096 + 16, np.uint64)
 L.lqro_debug_hull_profile(c._h, out.ctypes.data_as(C.c_void_p))
-names = ["points", "init", "candidates", "regions", "accept", "cone", "reassign", "retire", "final-prep", "final", "sum region", "sum horizon", "sum moved", "", "insertions", "wait"]
+names = ["points", "init", "candidates", "regions", "accept", "cone", "reassign", "retire", "final-prep", "final", "candidates", "rounds", "sum moved", "", "insertions", "wait"]
 tot = out[:10].sum()
 for k in range(16):
     if out[k]:
