@@ -35,7 +35,7 @@
 namespace lqro {
 
 #define HULL_THREADS 64          // one wave per hull
-#define HULL_KC 8                // apex candidates per round (claim bytes 0..7)
+#define HULL_WAVES 1
 #define HULL_SBMULT 24           // outside-set segment buffer: HULL_SBMULT * H*NP entries
 #define HULL_STKMULT 4           // work stack: HULL_STKMULT * H*NP faces
 #define HULL_FB_STRIDE 16384     // per-block face records in global scratch (= big faces)
@@ -82,10 +82,11 @@ struct HullMem {
   static constexpr int kFaces = FMAX, kVerts = VTX;
   unsigned short fv[FMAX][3];        // vertex slots, outward counter-clockwise
   unsigned short fa[FMAX][3];        // fa[f][e]: face across edge (fv[e], fv[e+1])
-  unsigned int owner[FMAX / 2];      // claim bytes of the round: region, ring (2 faces / word)
+  unsigned short vst[FMAX];          // visible-region stamp (insertion number)
   unsigned short freel[FMAX];        // retired face slots
   unsigned char alive[FMAX];
   double vx[VTX][3];                 // hull vertex coordinates (rounded points)
+  unsigned short vmap[VTX];          // horizon: vertex slot -> edge leaving it
 };
 typedef HullMem<4752, 2368> HullMemSmall;   // ~141 KB: LDS
 typedef HullMem<16384, 8192> HullMemBig;    // ~480 KB: global scratch
@@ -94,49 +95,20 @@ typedef HullMem<16384, 8192> HullMemBig;    // ~480 KB: global scratch
 template <int RG, int HZ>
 struct HullLdsT {
   static constexpr int kRegion = RG, kHorizon = HZ;
-  unsigned short region[RG];                 // visible regions (per-candidate slices)
-  unsigned short ef[RG];                     // accepted regions, flattened
-  unsigned char ec[RG];                      //   their candidate
+  unsigned short region[RG];                 // visible region of the apex
   int roff[RG], rcnt[RG], rpre[RG + 1];      //   their outside sets
   unsigned short h_a[HZ], h_b[HZ], h_out[HZ], h_new[HZ];   // horizon edges, cone faces
-  unsigned char h_c[HZ];
   int hcnt[HZ], hoff[HZ];
   double cn[HZ][8];                          // cone planes: n, a, |n|, eps |n|
-  unsigned long long ck[HULL_KC];            // candidates: furthest-point key
-  double cp[HULL_KC][3];                     //   apex coordinates
-  int ca[HULL_KC];                           //   apex point
-  unsigned short cf[HULL_KC], cvo[HULL_KC], rn[HULL_KC], chn[HULL_KC], cho[HULL_KC], ceo[HULL_KC],
-      cvx[HULL_KC];
-  unsigned char cok[HULL_KC], covf[HULL_KC];
   double tr[3 * 128];
   double rk[HULL_THREADS / 64];
   int ri[HULL_THREADS / 64];
   int scan[HULL_THREADS / 64];
-  int nf, nfree, nvtx, fail, n, job, slot, init[4], sbtop, sp, qh, it, tot_h, tot_e, nacc;
+  int nf, nfree, nvtx, fail, n, job, slot, init[4], sbtop, sp, qh, it;
   double eps;
 };
 typedef HullLdsT<512, 128> HullLdsSmall;
 typedef HullLdsT<2048, 1024> HullLdsBig;
-
-// claim face f for candidate c as part of its visible region (kind 0) or of
-// the region's one-ring (kind 1): claim byte = min(byte, c)
-template <class W>
-__device__ __forceinline__ void hl_claim(W* ow, int f, int kind, unsigned c) {
-  unsigned int* w = (unsigned int*)ow + (f >> 1);
-  const int sh = (((f & 1) << 1) + kind) * 8;
-  unsigned int old = *(volatile unsigned int*)w;
-  for (;;) {
-    if (((old >> sh) & 0xFFu) <= c) return;
-    const unsigned int nw = (old & ~(0xFFu << sh)) | (c << sh);
-    const unsigned int prev = atomicCAS(w, old, nw);
-    if (prev == old) return;
-    old = prev;
-  }
-}
-template <class W>
-__device__ __forceinline__ unsigned hl_owner(const W* ow, int f, int kind) {
-  return (((const volatile unsigned int*)ow)[f >> 1] >> ((((f & 1) << 1) + kind) * 8)) & 0xFFu;
-}
 
 static_assert(HULL_THREADS == 64, "the hull kernels are single-wave");
 
@@ -495,6 +467,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
         for (int f = 0; f < 4; ++f) {
           soff[f] = o; scnt[f] = L.hcnt[f]; o += L.hcnt[f];
           L.hoff[f] = soff[f];
+          M.vst[f] = 0;
         }
         for (int f = 0; f < 4; ++f)
           if (L.hcnt[f] > 0) stk[L.sp++] = f;
@@ -512,290 +485,268 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
       hl_sync();
 
       HSTAMP(1);
-      // 5. quickhull, batched.  Each round takes the next up-to-HULL_KC live
-      //    faces of the FIFO queue as candidates (queue order = priority).
-      //    Lanes 3c..3c+2 grow candidate c's visible region over the face
-      //    adjacency, claiming every face they touch in a per-face byte:
-      //    region claims and ring claims (neighbours outside the region),
-      //    each the minimum candidate index.  c is inserted iff no lower
-      //    candidate touched its region and none holds one of c's ring faces
-      //    in its region: accepted regions are then disjoint and separated,
-      //    so their insertions commute with sequential quickhull (rings may
-      //    overlap — they are patched on distinct edges).  Candidate 0 always
-      //    wins; rejected candidates that are still live go back on the
-      //    queue.  One wave: every phase is a few LDS round trips.
-      for (int w = tid; w < Mem::kFaces / 2; w += blockDim.x) M.owner[w] = 0xFFFFFFFFu;
-      hl_sync();
-      const unsigned long long lt = (1ull << tid) - 1ull;
+      // 5. quickhull: take the oldest live face with outside points (FIFO
+      //    work queue: the hull grows evenly, which wastes fewer insertions
+      //    on points that later fall inside than depth-first order), insert
+      //    its furthest point.  One wave: every step is a few dependent LDS
+      //    round trips, no cross-wave barrier.
+      // The next queue entry's face, key and apex coordinates are fetched
+      // during the current insertion (three dependent global loads off the
+      // critical path).  They stay valid unless that face is retired (it is
+      // in the current region) or was dead when checked (its slot may be
+      // reused by a cone face of this insertion).
+      int pf_idx = -1, pf_face = 0;
+      bool pf_ok = false;
+      unsigned long long pf_key = 0ull;
+      double pf_p[3] = {0.0, 0.0, 0.0};
       for (;;) {
-        const int qh = L.qh, qt = L.sp;
-        if (qh == qt) break;
-        // (0) candidates: the first HULL_KC live entries from the head
-        int nc = 0, consumed = qh;
-        for (int b0 = qh; b0 < qt && nc < HULL_KC; b0 += 64) {
-          const int t = b0 + tid;
-          int f = -1;
-          unsigned long long key = 0ull;
-          bool live = false;
-          if (t < qt) {
-            f = stk[t];
-            if (M.alive[f]) { key = fbest[f]; live = key != 0ull; }
-          }
-          const unsigned long long b = __ballot(live);
-          const int rk = nc + __popcll(b & lt);
-          if (live && rk < HULL_KC) { L.cf[rk] = (unsigned short)f; L.ck[rk] = key; }
-          const int got = __popcll(b);
-          if (nc + got >= HULL_KC) {
-            unsigned long long bb = b;
-            for (int k = 1; k < HULL_KC - nc; ++k) bb &= bb - 1ull;   // drop the lowest bits
-            consumed = b0 + __ffsll((long long)bb);                      // past the last taken
-            nc = HULL_KC;
-          } else {
-            nc += got;
-            consumed = min(b0 + 64, qt);
-          }
+        const int qh = L.qh, sp = L.sp;
+        if (qh == sp) break;
+        const bool use_pf = pf_ok && pf_idx == qh;
+        const int f = use_pf ? pf_face : stk[qh];
+        hl_sync();
+        if (tid == 0) L.qh = qh + 1;
+        // stale entries: the face was retired (its slot maybe reused by a
+        // face without outside points) after it was pushed
+        const unsigned long long key = use_pf ? pf_key : fbest[f];
+        pf_ok = false;
+        if (!M.alive[f] || key == 0ull) { hl_sync(); continue; }
+        const int apex = (int)(~(unsigned)(key & 0xFFFFFFFFull));
+        if (apex < 0 || apex >= n || L.it >= 4 * Mem::kVerts) { if (tid == 0) L.fail = 9; break; }
+        const int av = L.nvtx;
+        const unsigned short stamp = (unsigned short)(L.it + 1);
+        double p[3];
+        if (use_pf) { p[0] = pf_p[0]; p[1] = pf_p[1]; p[2] = pf_p[2]; }
+        else { p[0] = Pr[3 * apex]; p[1] = Pr[3 * apex + 1]; p[2] = Pr[3 * apex + 2]; }
+        pf_idx = qh + 1 < sp ? qh + 1 : -1;
+        if (pf_idx >= 0) pf_face = stk[pf_idx];
+        if (av >= Mem::kVerts) { if (tid == 0) L.fail = 1; break; }
+        if (tid == 0) {
+          M.vx[av][0] = p[0]; M.vx[av][1] = p[1]; M.vx[av][2] = p[2];
+          vpid[av] = apex;
+          L.nvtx = av + 1;
+          L.it = stamp;
+          L.region[0] = (unsigned short)f;
+          M.vst[f] = stamp;
         }
         hl_sync();
-        if (tid == 0) L.qh = consumed;
-        if (nc == 0) { hl_sync(); continue; }
-        // candidate apexes
-        if (tid < nc) {
-          const int apex = (int)(~(unsigned)(L.ck[tid] & 0xFFFFFFFFull));
-          if (apex < 0 || apex >= n) L.fail = 9;
-          else {
-            L.ca[tid] = apex;
-            L.cp[tid][0] = Pr[3 * apex]; L.cp[tid][1] = Pr[3 * apex + 1]; L.cp[tid][2] = Pr[3 * apex + 2];
-          }
-        }
-        hl_sync();
-        if (L.fail) break;
         HSTAMP(2);
-        // (a) visible regions, all candidates in lock step
-        const int rc0 = nc == 1 ? LT::kRegion : LT::kRegion / 2;
-        const int rcr = nc == 1 ? 0 : (LT::kRegion - rc0) / (nc - 1);
-        const int mc = tid / 3, me = tid - 3 * (tid / 3);
-        const bool cl = mc < nc;
-        const int myoff = mc == 0 ? 0 : rc0 + (mc - 1) * rcr;
-        const int mycap = mc == 0 ? rc0 : rcr;
-        double mp[3] = {0.0, 0.0, 0.0};
-        if (cl) { mp[0] = L.cp[mc][0]; mp[1] = L.cp[mc][1]; mp[2] = L.cp[mc][2]; }
-        if (cl && me == 0) {
-          L.cvo[mc] = (unsigned short)myoff;
-          L.region[myoff] = L.cf[mc];
-          L.rn[mc] = 1;
-          L.covf[mc] = 0;
-          hl_claim(M.owner, L.cf[mc], 0, (unsigned)mc);
-        }
-        hl_sync();
-        for (int step = 0;; ++step) {
-          const bool act = cl && step < (int)L.rn[mc] && !L.covf[mc];
-          if (__ballot(act) == 0ull) break;
-          int nb = -1;
-          bool vis = false;
-          if (act) {
-            const int g = L.region[myoff + step];
-            nb = M.fa[g][me];
-            if (hl_owner(M.owner, nb, 0) != (unsigned)mc) {
-              if (hl_beyond(M, nb, mp, eps, nullptr)) {
-                vis = true;
-                hl_claim(M.owner, nb, 0, (unsigned)mc);
-              } else {
-                hl_claim(M.owner, nb, 1, (unsigned)mc);
-              }
-            }
+        // (a) visible region: grown over adjacency from f; lanes 0..2 test
+        //     the three neighbours of one region face at a time
+        int R = 1;
+        for (int r = 0; r < R; ++r) {
+          const int g = L.region[r];
+          int nb = -1, vis = 0;
+          if (tid < 3) {
+            nb = M.fa[g][tid];
+            vis = (M.vst[nb] != stamp) && hl_beyond(M, nb, p, eps, nullptr);
           }
           const unsigned long long b = __ballot(vis);
-          const int base = cl ? (int)L.rn[mc] : 0;
           if (vis) {
-            const int pos = base + __popcll((b >> (3 * mc)) & ((1ull << me) - 1ull));
-            if (pos < mycap) L.region[myoff + pos] = (unsigned short)nb;
-            else L.covf[mc] = 1;
+            const int pos = R + __popcll(b & ((1ull << tid) - 1ull));
+            if (pos < LT::kRegion) { L.region[pos] = (unsigned short)nb; M.vst[nb] = stamp; }
           }
-          hl_sync();
-          if (cl && me == 0) L.rn[mc] = (unsigned short)min(mycap, base + (int)__popcll((b >> (3 * mc)) & 7ull));
+          R += __popcll(b);
+          if (R > LT::kRegion) break;
           hl_sync();
         }
-        if (L.covf[0]) { if (tid == 0) L.fail = 2; break; }
+        if (R > LT::kRegion) { if (tid == 0) L.fail = 2; break; }
+        if (pf_idx >= 0) {
+          pf_ok = M.alive[pf_face] && M.vst[pf_face] != stamp;
+          if (pf_ok) pf_key = fbest[pf_face];
+        }
         HSTAMP(3);
-        // (b) acceptance and horizon size (one lane per candidate)
-        if (tid < nc) {
-          const int c = tid;
-          const int R = L.rn[c];
-          const unsigned short* rg = L.region + L.cvo[c];
-          int ok = !L.covf[c], hn = 0;
-          for (int r = 0; r < R && ok; ++r) {
-            const int g = rg[r];
-            if (hl_owner(M.owner, g, 0) != (unsigned)c || hl_owner(M.owner, g, 1) < (unsigned)c) ok = 0;
-            for (int e = 0; e < 3; ++e) {
-              const int nb = M.fa[g][e];
-              const unsigned ob = hl_owner(M.owner, nb, 0);
-              if (ob != (unsigned)c) {
-                ++hn;
-                if (ob < (unsigned)c) ok = 0;
-              }
-            }
+        // (b) horizon: region edges whose neighbour is not in the region,
+        //     in (region order, edge) order
+        int nh = 0;
+        for (int b0 = 0; b0 < 3 * R; b0 += blockDim.x) {
+          const int t = b0 + tid;
+          int ha = 0, hb = 0, ho = 0, is = 0;
+          if (t < 3 * R) {
+            const int g = L.region[t / 3], e = t % 3;
+            ho = M.fa[g][e];
+            if (M.vst[ho] != stamp) { is = 1; ha = M.fv[g][e]; hb = M.fv[g][(e + 1) % 3]; }
           }
-          L.cok[c] = (unsigned char)ok;
-          L.chn[c] = (unsigned short)hn;
-        }
-        hl_sync();
-        // in candidate order, within the per-round capacities
-        if (tid == 0) {
-          int ch = 0, ce = 0, na = 0;
-          for (int c = 0; c < nc; ++c) {
-            int ok = L.cok[c];
-            if (ok && (ch + L.chn[c] > LT::kHorizon || L.chn[c] < 3)) ok = (c == 0) ? -1 : 0;
-            if (ok < 0) { L.fail = 3; break; }
-            L.cok[c] = (unsigned char)ok;
-            if (!ok) continue;
-            L.cho[c] = (unsigned short)ch;
-            L.ceo[c] = (unsigned short)ce;
-            L.cvx[c] = (unsigned short)(L.nvtx + na);
-            ch += L.chn[c];
-            ce += L.rn[c];
-            ++na;
+          int tot;
+          const int pos = nh + hl_scan(L, is, &tot);
+          if (is && pos < LT::kHorizon) {
+            L.h_a[pos] = (unsigned short)ha; L.h_b[pos] = (unsigned short)hb; L.h_out[pos] = (unsigned short)ho;
           }
-          L.tot_h = ch; L.tot_e = ce; L.nacc = na;
-          if (L.nvtx + na > Mem::kVerts) L.fail = 1;
-          if (L.nf + max(0, ch - L.nfree) > Mem::kFaces) L.fail = 4;
+          nh += tot;
         }
-        hl_sync();
-        if (L.fail) break;
-        const int tot_h = L.tot_h, tot_e = L.tot_e, nacc = L.nacc;
+        if (nh > LT::kHorizon || nh < 3) { if (tid == 0) L.fail = 3; break; }
         const int nf0 = L.nf, nfree0 = L.nfree;
-        HSTAMP(4);
-        // (c) accepted candidates: apex vertex, region entries, horizon edges
-        if (tid < nc && L.cok[tid]) {
-          const int c = tid;
-          const int v = L.cvx[c];
-          M.vx[v][0] = L.cp[c][0]; M.vx[v][1] = L.cp[c][1]; M.vx[v][2] = L.cp[c][2];
-          vpid[v] = L.ca[c];
-          const int R = L.rn[c];
-          const unsigned short* rg = L.region + L.cvo[c];
-          int h = L.cho[c];
-          const int e0 = L.ceo[c];
-          for (int r = 0; r < R; ++r) {
-            const int g = rg[r];
-            L.ef[e0 + r] = (unsigned short)g;
-            L.ec[e0 + r] = (unsigned char)c;
-            for (int e = 0; e < 3; ++e) {
-              const int nb = M.fa[g][e];
-              if (hl_owner(M.owner, nb, 0) == (unsigned)c) continue;
-              L.h_a[h] = M.fv[g][e];
-              L.h_b[h] = M.fv[g][(e + 1) % 3];
-              L.h_out[h] = (unsigned short)nb;
-              L.h_c[h] = (unsigned char)c;
-              ++h;
-            }
-          }
-        }
-        for (int t = tid; t < tot_h; t += blockDim.x) {
-          L.h_new[t] = (unsigned short)(t < nfree0 ? M.freel[nfree0 - 1 - t] : nf0 + (t - nfree0));
-          L.hcnt[t] = 0;
-        }
-        for (int e = tid; e < tot_e; e += blockDim.x) {
-          const int g = L.ef[e];
-          L.roff[e] = soff[g];
-          L.rcnt[e] = scnt[g];
+        if (nf0 + max(0, nh - nfree0) > Mem::kFaces) { if (tid == 0) L.fail = 4; break; }
+        // (c) cone face slots (retired slots first) and the vertex -> edge map
+        for (int h = tid; h < nh; h += blockDim.x) {
+          const int sf = h < nfree0 ? M.freel[nfree0 - 1 - h] : nf0 + (h - nfree0);
+          L.h_new[h] = (unsigned short)sf;
+          M.vmap[L.h_a[h]] = (unsigned short)h;
+          L.hcnt[h] = 0;
         }
         hl_sync();
-        // (d) cone faces (a, b, apex_c): adjacency, outer neighbours, planes
-        for (int t = tid; t < tot_h; t += blockDim.x) {
-          const int c = L.h_c[t];
-          const int sf = L.h_new[t];
-          const int ha = L.h_a[t], hb = L.h_b[t], on = L.h_out[t];
-          const int av = L.cvx[c];
-          int k = -1;
-          for (int s = L.cho[c], s1 = L.cho[c] + L.chn[c]; s < s1; ++s)
-            if (L.h_a[s] == hb) { k = s; break; }
-          if (k < 0) { L.fail = 5; k = t; }
+        HSTAMP(4);
+        // (d) cone faces (a, b, apex): adjacency, outer neighbours, planes
+        for (int h = tid; h < nh; h += blockDim.x) {
+          const int sf = L.h_new[h];
+          const int ha = L.h_a[h], hb = L.h_b[h], on = L.h_out[h];
+          const int k = M.vmap[hb];                    // edge leaving b
           M.fv[sf][0] = (unsigned short)ha;
           M.fv[sf][1] = (unsigned short)hb;
           M.fv[sf][2] = (unsigned short)av;
           M.fa[sf][0] = (unsigned short)on;
           M.fa[sf][1] = L.h_new[k];                    // across (b, apex)
           M.fa[L.h_new[k]][2] = (unsigned short)sf;    // k's (apex, a_k = b)
+          M.vst[sf] = 0;
           for (int e = 0; e < 3; ++e)
             if (M.fv[on][e] == hb && M.fv[on][(e + 1) % 3] == ha) M.fa[on][e] = (unsigned short)sf;
+          if (L.h_a[k] != hb) L.fail = 5;
+          // plane of the new face, as hl_normal / hl_beyond compute it
           const double* a = M.vx[ha];
           const double* bb = M.vx[hb];
-          const double* pc = L.cp[c];
           const double e1[3] = {bb[0] - a[0], bb[1] - a[1], bb[2] - a[2]};
-          const double e2[3] = {pc[0] - a[0], pc[1] - a[1], pc[2] - a[2]};
+          const double e2[3] = {p[0] - a[0], p[1] - a[1], p[2] - a[2]};
           const double nx = e1[1] * e2[2] - e1[2] * e2[1];
           const double ny = e1[2] * e2[0] - e1[0] * e2[2];
           const double nz = e1[0] * e2[1] - e1[1] * e2[0];
-          double* cp = L.cn[t];
+          double* cp = L.cn[h];
           cp[0] = nx; cp[1] = ny; cp[2] = nz;
           cp[3] = a[0]; cp[4] = a[1]; cp[5] = a[2];
           cp[6] = sqrt(nx * nx + ny * ny + nz * nz);
           cp[7] = eps * cp[6];
           fbest[sf] = 0ull;
         }
-        {
-          int run = 0;
-          for (int e0 = 0; e0 < tot_e; e0 += blockDim.x) {
-            const int e = e0 + tid;
-            const int v = e < tot_e ? L.rcnt[e] : 0;
-            int tot;
-            const int pos = run + hl_scan_val(L, v, &tot);
-            if (e < tot_e) L.rpre[e] = pos;
-            run += tot;
-          }
-          if (tid == 0) L.rpre[tot_e] = run;
+        // retired faces' outside-set extents
+        for (int r = tid; r < R; r += blockDim.x) {
+          const int g = L.region[r];
+          L.roff[r] = soff[g];
+          L.rcnt[r] = scnt[g];
         }
         hl_sync();
         if (L.fail) break;
+        {
+          int run = 0;
+          for (int r0 = 0; r0 < R; r0 += blockDim.x) {
+            const int r = r0 + tid;
+            const int v = r < R ? L.rcnt[r] : 0;
+            int tot;
+            const int pos = run + hl_scan_val(L, v, &tot);
+            if (r < R) L.rpre[r] = pos;
+            run += tot;
+          }
+          if (tid == 0) L.rpre[R] = run;
+        }
+        hl_sync();
         HSTAMP(5);
-        // (e) the retired faces' outside points: first cone face of their
-        //     candidate they are beyond; rank within that face by LDS atomic
-        const int total = L.rpre[tot_e];
-        const int nch = (total + 63) / 64;
-        int tg[4] = {-1, -1, -1, -1}, qq[4] = {-1, -1, -1, -1}, rkk[4] = {0, 0, 0, 0};
-        float dv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        for (int ch = 0; ch < nch; ++ch) {
-          const int t = ch * 64 + tid;
-          int tgt = -1, q = -1, rank = 0;
-          float dd = 0.0f;
-          if (t < total) {
-            int lo = 0, hi = tot_e - 1;
-            while (lo < hi) {
-              const int mid = (lo + hi + 1) >> 1;
-              if (L.rpre[mid] <= t) lo = mid; else hi = mid - 1;
+        // (e) the retired faces' outside points: first cone face they are beyond
+        const int total = L.rpre[R];
+        if (pf_ok) {
+          const int pa = (int)(~(unsigned)(pf_key & 0xFFFFFFFFull));
+          if (pa >= 0 && pa < n) { pf_p[0] = Pr[3 * pa]; pf_p[1] = Pr[3 * pa + 1]; pf_p[2] = Pr[3 * pa + 2]; }
+        }
+        HSUB(0);
+        if (total <= 4 * 64) {
+          // up to four points per lane, grouped by target with ballots; no
+          // scratch round trip
+          const unsigned long long lt = (1ull << tid) - 1ull;
+          int tg[4], qq[4];
+          float dv[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            tg[c] = -1; qq[c] = -1; dv[c] = 0.0f;
+            const int t = c * 64 + tid;
+            if (t < total) {
+              int lo = 0, hi = R - 1;
+              while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (L.rpre[mid] <= t) lo = mid; else hi = mid - 1;
+              }
+              qq[c] = sb[L.roff[lo] + (t - L.rpre[lo])];
             }
-            q = sb[L.roff[lo] + (t - L.rpre[lo])];
-            const int c = L.ec[lo];
-            if (q != L.ca[c]) {
+          }
+          HSUB(1);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int q = qq[c];
+            if (q >= 0 && q != apex) {
               const double x0 = Pr[3 * q], x1 = Pr[3 * q + 1], x2 = Pr[3 * q + 2];
-              for (int h = L.cho[c], h1 = L.cho[c] + L.chn[c]; h < h1; ++h) {
+              for (int h = 0; h < nh; ++h) {
                 const double* cp = L.cn[h];
                 const double d = cp[0] * (x0 - cp[3]) + cp[1] * (x1 - cp[4]) + cp[2] * (x2 - cp[5]);
-                if (d > cp[7]) { tgt = h; dd = (float)(d / cp[6]); break; }
+                if (d > cp[7]) { tg[c] = h; dv[c] = (float)(d / cp[6]); break; }
               }
             }
-            if (tgt >= 0) rank = atomicAdd(&L.hcnt[tgt], 1);
           }
-          if (ch < 4) {
+          HSUB(2);
+          int run = L.sbtop;
+          int mp[4] = {0, 0, 0, 0};
+          for (int h = 0; h < nh; ++h) {
+            const int base = run;
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-              if (k == ch) { tg[k] = tgt; qq[k] = q; rkk[k] = rank; dv[k] = dd; }
-          } else {
-            tq[t < total ? t : 0] = q;
-            if (t < total) { th[t] = tgt < 0 ? -1 : (tgt | (rank << 8)); td[t] = dd; }
+            for (int c = 0; c < 4; ++c) {
+              if (c * 64 < total) {
+                const unsigned long long b = __ballot(tg[c] == h);
+                if (tg[c] == h) mp[c] = run + __popcll(b & lt);
+                run += __popcll(b);
+              }
+            }
+            if (tid == 0) { L.hcnt[h] = run - base; L.hoff[h] = base; }
           }
+          if (run > sbcap) { if (tid == 0) L.fail = 6; break; }
+          HSUB(3);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            if (tg[c] >= 0) {
+              sb[mp[c]] = qq[c];
+              const unsigned long long k2 =
+                  ((unsigned long long)__float_as_uint(dv[c]) << 32) | (unsigned long long)(~(unsigned)qq[c]);
+              atomicMax(&fbest[L.h_new[tg[c]]], k2);
+            }
+          }
+          hl_sync();
+          HSUB(4);
+          for (int h = tid; h < nh; h += blockDim.x) {
+            soff[L.h_new[h]] = L.hoff[h];
+            scnt[L.h_new[h]] = L.hcnt[h];
+          }
+          if (tid == 0) L.sbtop = run;
+          hl_sync();
+          HSUB(5);
+        } else {
+        for (int t = tid; t < total; t += blockDim.x) {
+          int lo = 0, hi = R - 1;
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (L.rpre[mid] <= t) lo = mid; else hi = mid - 1;
+          }
+          const int q = sb[L.roff[lo] + (t - L.rpre[lo])];
+          int tgt = -1;
+          float dd = 0.0f;
+          if (q != apex) {
+            const double x0 = Pr[3 * q], x1 = Pr[3 * q + 1], x2 = Pr[3 * q + 2];
+            for (int h = 0; h < nh; ++h) {
+              const double* cp = L.cn[h];
+              const double d = cp[0] * (x0 - cp[3]) + cp[1] * (x1 - cp[4]) + cp[2] * (x2 - cp[5]);
+              if (d > cp[7]) { tgt = h; dd = (float)(d / cp[6]); break; }
+            }
+          }
+          tq[t] = q;
+          th[t] = tgt;
+          td[t] = dd;
+          if (tgt >= 0) atomicAdd(&L.hcnt[tgt], 1);
         }
         hl_sync();
         {
           int run = L.sbtop;
-          for (int h0 = 0; h0 < tot_h; h0 += blockDim.x) {
+          for (int h0 = 0; h0 < nh; h0 += blockDim.x) {
             const int h = h0 + tid;
-            const int v = h < tot_h ? L.hcnt[h] : 0;
+            const int v = h < nh ? L.hcnt[h] : 0;
             int tot;
             const int pos = run + hl_scan_val(L, v, &tot);
-            if (h < tot_h) {
-              L.hoff[h] = pos;
+            if (h < nh) {
               soff[L.h_new[h]] = pos;
               scnt[L.h_new[h]] = v;
+              L.hoff[h] = pos;
             }
             run += tot;
           }
@@ -806,70 +757,51 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
         }
         hl_sync();
         if (L.fail) break;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (tg[k] >= 0) {
-            sb[L.hoff[tg[k]] + rkk[k]] = qq[k];
-            const unsigned long long k2 =
-                ((unsigned long long)__float_as_uint(dv[k]) << 32) | (unsigned long long)(~(unsigned)qq[k]);
-            atomicMax(&fbest[L.h_new[tg[k]]], k2);
-          }
-        }
-        for (int t = 256 + tid; t < total; t += blockDim.x) {
-          const int w = th[t];
-          if (w < 0) continue;
-          const int h = w & 0xFF, rank = w >> 8;
+        for (int t = tid; t < total; t += blockDim.x) {
+          const int h = th[t];
+          if (h < 0) continue;
           const int q = tq[t];
-          sb[L.hoff[h] + rank] = q;
+          sb[atomicAdd(&L.hoff[h], 1)] = q;
           const unsigned long long k2 =
               ((unsigned long long)__float_as_uint(td[t]) << 32) | (unsigned long long)(~(unsigned)q);
           atomicMax(&fbest[L.h_new[h]], k2);
         }
-        HSTAMP(6);
-        // (f) retire the regions, commit the cones; cone slots came off the
-        //     top of the free list, the retired faces go on after what is left
-        const int used = min(tot_h, nfree0);
-        for (int e = tid; e < tot_e; e += blockDim.x) {
-          const int g = L.ef[e];
-          M.alive[g] = 0;
-          M.freel[nfree0 - used + e] = (unsigned short)g;
         }
-        hl_sync();
-        for (int t = tid; t < tot_h; t += blockDim.x) M.alive[L.h_new[t]] = 1;
-        hl_sync();
-        // queue: cone faces with outside points (horizon order), then the
-        // rejected candidates whose face is still live
+        HSTAMP(6);
+        // (f) retire the region, commit the cone, push the cone faces that
+        //     have outside points (in horizon order; the last on top)
+        const int used = min(nh, nfree0);
+        for (int r = tid; r < R; r += blockDim.x) {
+          const int g = L.region[r];
+          M.alive[g] = 0;
+          M.freel[nfree0 - used + r] = (unsigned short)g;
+        }
         int npush = 0;
-        for (int h0 = 0; h0 < tot_h + nc; h0 += blockDim.x) {
+        for (int h0 = 0; h0 < nh; h0 += blockDim.x) {
           const int h = h0 + tid;
-          int is = 0, f = 0;
-          if (h < tot_h) { is = L.hcnt[h] > 0; f = L.h_new[h]; }
-          else if (h < tot_h + nc) {
-            const int c = h - tot_h;
-            f = L.cf[c];
-            is = !L.cok[c] && M.alive[f];
+          int is = 0;
+          if (h < nh) {
+            M.alive[L.h_new[h]] = 1;
+            is = L.hcnt[h] > 0;
           }
           int tot;
-          const int pos = qt + npush + hl_scan(L, is, &tot);
+          const int pos = sp + npush + hl_scan(L, is, &tot);
           if (is) {
-            if (pos < stkcap) stk[pos] = f;
+            if (pos < stkcap) stk[pos] = L.h_new[h];
             else L.fail = 6;
           }
           npush += tot;
         }
         if (tid == 0) {
-          L.nfree = nfree0 - used + tot_e;
-          L.nf = nf0 + (tot_h - used);
-          L.nvtx += nacc;
-          L.sp = qt + npush;
+          L.nfree = nfree0 - used + R;
+          L.nf = nf0 + (nh - used);
+          L.sp = sp + npush;
         }
-        hl_sync();
-        for (int w = tid; w < (L.nf + 1) / 2; w += blockDim.x) M.owner[w] = 0xFFFFFFFFu;
         hl_sync();
         if (L.fail) break;
         HSTAMP(7);
 #ifdef LQRO_HULL_PROFILE
-        if (tid == 0) { prof_acc[14] += (unsigned long long)nacc; prof_acc[10] += (unsigned long long)nc; prof_acc[11] += 1; prof_acc[12] += (unsigned long long)total; }
+        if (tid == 0) { prof_acc[14] += 1; prof_acc[10] += (unsigned long long)R; prof_acc[11] += (unsigned long long)nh; prof_acc[12] += (unsigned long long)total; }
 #endif
       }
     }

@@ -219,6 +219,7 @@ struct lqro_ctx {
   void* d_hbig;
   int hull_big_blocks;
   int n_cu;
+  int side_cus;              // CUs running k_hull beside k_pair (LQRO_SIDE_HULL_CUS)
   double* d_hscratch;
   int* d_hiscratch;
   float* d_hfscratch;
@@ -332,8 +333,8 @@ static int ctx_alloc(lqro_ctx* c) {
   HIPCHK(hipMemset(c->d_prof, 0, sizeof(unsigned long long) * LQRO_PROF_WORDS));
   c->hull_blocks = 256;   // one 138 KB-LDS workgroup per CU, persistent over the queue
   HIPCHK(hipMalloc(&c->d_hscratch, sizeof(double) * 6 * H * NP * c->hull_blocks));
-  HIPCHK(hipMalloc(&c->d_hiscratch, sizeof(int) * 2 * H * NP * c->hull_blocks));
-  HIPCHK(hipMalloc(&c->d_hfscratch, sizeof(float) * H * NP * c->hull_blocks));
+  HIPCHK(hipMalloc(&c->d_hiscratch, sizeof(int) * 2 * H * NP * HULL_WAVES * c->hull_blocks));
+  HIPCHK(hipMalloc(&c->d_hfscratch, sizeof(float) * H * NP * HULL_WAVES * c->hull_blocks));
   HIPCHK(hipMalloc(&c->d_hfbest, sizeof(unsigned long long) * HULL_FB_STRIDE * (size_t)c->hull_blocks));
   HIPCHK(hipMalloc(&c->d_hfseg, sizeof(int) * 2 * HULL_FB_STRIDE * (size_t)c->hull_blocks));
   HIPCHK(hipMalloc(&c->d_hvpid, sizeof(int) * HULL_VG_STRIDE * (size_t)c->hull_blocks));
@@ -365,6 +366,11 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
   memset(c, 0, sizeof *c);
   c->cfg = g;
   c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  {
+    const char* e = getenv("LQRO_SIDE_HULL_CUS");
+    c->side_cus = e ? atoi(e) : 0;
+    if (c->side_cus < 0) c->side_cus = 0;
+  }
   c->rb = g.row_begin;
   c->re = (g.row_end > g.row_begin) ? g.row_end : g.n_agents;
   if (g.row_end == 0 && g.row_begin == 0) { c->rb = 0; c->re = g.n_agents; }
@@ -495,7 +501,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   HIPCHK(hipMemsetAsync(c->d_hcount, 0, sizeof(int) * 8, s));
   HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * 8, s));
   HIPCHK(hipMemsetAsync(c->d_hq, 0xFF, sizeof(int) * (size_t)c->hull_cap, s));
-  const int nwait = (c->nrows >= 4 * c->n_cu && c->n_cu >= 64) ? c->n_cu / 8 : 0;
+  const int nwait = (c->nrows >= 4 * c->n_cu && c->n_cu >= 64) ? std::min(c->side_cus, c->n_cu / 2) : 0;
   const unsigned nblk = (unsigned)std::min(c->nrows, c->n_cu - nwait);
   HullArgs Hh;
   Hh.N = g.n_agents; Hh.X = g.x_dim; Hh.H = g.horizon; Hh.NP = g.n_points;
