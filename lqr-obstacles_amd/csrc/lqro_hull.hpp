@@ -36,10 +36,17 @@ namespace lqro {
 
 #define HULL_THREADS 64          // one wave per hull
 #define HULL_WAVES 1
-#define HULL_SBMULT 24           // outside-set segment buffer: HULL_SBMULT * H*NP entries
+#define HULL_SBMULT 16           // outside-set segment buffer: HULL_SBMULT * H*NP entries
 #define HULL_STKMULT 4           // work stack: HULL_STKMULT * H*NP faces
 #define HULL_FB_STRIDE 16384     // per-block face records in global scratch (= big faces)
 #define HULL_VG_STRIDE 8192      // per-block vertex records in global scratch (= big vertices)
+
+// an outside-set entry: the point and its (rounded) coordinates, so that
+// re-distributing it needs one load
+struct HullPt {
+  double x, y, z;
+  int q, pad;
+};
 
 struct HullArgs {
   int N, X, H, NP;
@@ -58,7 +65,7 @@ struct HullArgs {
   double* scratch;                  // per block: H*NP*6 doubles (rounded, full)
   int* iscratch;                    // per block: 2*H*NP ints (moved point, target face)
   float* fscratch;                  // per block: H*NP floats (distance beyond the target)
-  int* sb;                          // per block: HULL_SBMULT*H*NP ints (outside-set segments)
+  HullPt* sb;                       // per block: HULL_SBMULT*H*NP entries (outside-set segments)
   unsigned long long* fbest;        // per block: HULL_FB_STRIDE furthest-point keys
   int* fseg;                        // per block: 2*HULL_FB_STRIDE ints (outside-set offset, count)
   int* vpid;                        // per block: HULL_VG_STRIDE vertex -> point ids
@@ -134,18 +141,20 @@ __device__ __forceinline__ void hl_normal(const Mem& L, int f, double* n) {
   n[1] = e1[2] * e2[0] - e1[0] * e2[2];
   n[2] = e1[0] * e2[1] - e1[1] * e2[0];
 }
-// is p beyond face f?  *dist = signed distance
+// is p beyond face f: d > eps |n| with d = n.(p - a), tested squared (no
+// sqrt on the hot path): d > 0 and d^2 > eps^2 (n.n).  *dist = d / |n|.
 template <class Mem>
-__device__ __forceinline__ bool hl_beyond(const Mem& L, int f, const double* p, double eps,
+__device__ __forceinline__ bool hl_beyond(const Mem& L, int f, const double* p, double eps2,
                                           double* dist) {
   double n[3];
   hl_normal(L, f, n);
   const double* a = L.vx[L.fv[f][0]];
   const double d = n[0] * (p[0] - a[0]) + n[1] * (p[1] - a[1]) + n[2] * (p[2] - a[2]);
-  const double nl = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
-  if (dist) *dist = d / nl;
-  return d > eps * nl;
+  const double nn = n[0] * n[0] + n[1] * n[1] + n[2] * n[2];
+  if (dist) *dist = d / sqrt(nn);
+  return d > 0.0 && d * d > eps2 * nn;
 }
+
 
 // block-wide argmax of (key, idx), lowest idx on ties; result in every thread
 template <class LT>
@@ -242,7 +251,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
   int* tq = A.iscratch + (size_t)hb * HNP * 2;      // moved point ids
   int* th = tq + HNP;                                        // their target cone face
   float* td = A.fscratch + (size_t)hb * HNP;         // distance beyond it
-  int* sb = A.sb + (size_t)hb * HNP * HULL_SBMULT;
+  HullPt* sb = A.sb + (size_t)hb * HNP * HULL_SBMULT;
   const int sbcap = HNP * HULL_SBMULT;
   // per face: furthest outside point (dist bits << 32) | ~q, outside-set extent
   unsigned long long* fbest = A.fbest + (size_t)hb * HULL_FB_STRIDE;
@@ -364,6 +373,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
       hl_sync();
     }
     const double eps = L.eps;
+    const double eps2 = eps * eps;
 
     HSTAMP(0);
     // 3. initial tetrahedron from extreme points
@@ -406,7 +416,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
       key = -INFINITY; idx = INT_MAX;
       for (int q = tid; q < n; q += blockDim.x) {
         double dd;
-        hl_beyond(M, 0, Pr + 3 * q, eps, &dd);
+        hl_beyond(M, 0, Pr + 3 * q, eps2, &dd);
         const double v = fabs(dd);
         if (v > key || (v == key && q < idx)) { key = v; idx = q; }
       }
@@ -426,7 +436,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
             for (int e = 0; e < 3; ++e) M.fv[f][e] = (unsigned short)fvv[f][e];
             const int other = 6 - fvv[f][0] - fvv[f][1] - fvv[f][2];
             double dd;
-            hl_beyond(M, f, M.vx[other], -INFINITY, &dd);
+            hl_beyond(M, f, M.vx[other], 0.0, &dd);
             if (dd > 0) { const unsigned short t = M.fv[f][1]; M.fv[f][1] = M.fv[f][2]; M.fv[f][2] = t; }
             M.alive[f] = 1;
           }
@@ -455,7 +465,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
         if (q != L.init[0] && q != L.init[1] && q != L.init[2] && q != L.init[3]) {
           const double p[3] = {Pr[3 * q], Pr[3 * q + 1], Pr[3 * q + 2]};
           for (int f = 0; f < 4; ++f)
-            if (hl_beyond(M, f, p, eps, &dd)) { c = f; break; }
+            if (hl_beyond(M, f, p, eps2, &dd)) { c = f; break; }
         }
         th[q] = c;
         td[q] = (float)dd;
@@ -477,7 +487,9 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
       for (int q = tid; q < n; q += blockDim.x) {
         const int c = th[q];
         if (c < 0) continue;
-        sb[atomicAdd(&L.hoff[c], 1)] = q;
+        HullPt e;
+        e.x = Pr[3 * q]; e.y = Pr[3 * q + 1]; e.z = Pr[3 * q + 2]; e.q = q; e.pad = 0;
+        sb[atomicAdd(&L.hoff[c], 1)] = e;
         const unsigned long long key =
             ((unsigned long long)__float_as_uint(td[q]) << 32) | (unsigned long long)(~(unsigned)q);
         atomicMax(&fbest[c], key);
@@ -539,7 +551,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
           int nb = -1, vis = 0;
           if (tid < 3) {
             nb = M.fa[g][tid];
-            vis = (M.vst[nb] != stamp) && hl_beyond(M, nb, p, eps, nullptr);
+            vis = (M.vst[nb] != stamp) && hl_beyond(M, nb, p, eps2, nullptr);
           }
           const unsigned long long b = __ballot(vis);
           if (vis) {
@@ -612,8 +624,9 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
           double* cp = L.cn[h];
           cp[0] = nx; cp[1] = ny; cp[2] = nz;
           cp[3] = a[0]; cp[4] = a[1]; cp[5] = a[2];
-          cp[6] = sqrt(nx * nx + ny * ny + nz * nz);
-          cp[7] = eps * cp[6];
+          const double nn = nx * nx + ny * ny + nz * nz;
+          cp[6] = 1.0 / sqrt(nn);                      // for the distance key only
+          cp[7] = eps2 * nn;
           fbest[sf] = 0ull;
         }
         // retired faces' outside-set extents
@@ -646,14 +659,14 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
         }
         HSUB(0);
         if (total <= 4 * 64) {
-          // up to four points per lane, grouped by target with ballots; no
-          // scratch round trip
-          const unsigned long long lt = (1ull << tid) - 1ull;
-          int tg[4], qq[4];
+          // up to four points per lane; each point's rank within its target
+          // cone face from an LDS atomic; no scratch round trip
+          int tg[4], rk[4];
+          HullPt pt[4];
           float dv[4];
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
-            tg[c] = -1; qq[c] = -1; dv[c] = 0.0f;
+            tg[c] = -1; rk[c] = 0; dv[c] = 0.0f; pt[c].q = -1;
             const int t = c * 64 + tid;
             if (t < total) {
               int lo = 0, hi = R - 1;
@@ -661,54 +674,55 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
                 const int mid = (lo + hi + 1) >> 1;
                 if (L.rpre[mid] <= t) lo = mid; else hi = mid - 1;
               }
-              qq[c] = sb[L.roff[lo] + (t - L.rpre[lo])];
+              pt[c] = sb[L.roff[lo] + (t - L.rpre[lo])];
             }
           }
           HSUB(1);
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
-            const int q = qq[c];
+            const int q = pt[c].q;
             if (q >= 0 && q != apex) {
-              const double x0 = Pr[3 * q], x1 = Pr[3 * q + 1], x2 = Pr[3 * q + 2];
+              const double x0 = pt[c].x, x1 = pt[c].y, x2 = pt[c].z;
               for (int h = 0; h < nh; ++h) {
                 const double* cp = L.cn[h];
                 const double d = cp[0] * (x0 - cp[3]) + cp[1] * (x1 - cp[4]) + cp[2] * (x2 - cp[5]);
-                if (d > cp[7]) { tg[c] = h; dv[c] = (float)(d / cp[6]); break; }
+                if (d > 0.0 && d * d > cp[7]) { tg[c] = h; dv[c] = (float)(d * cp[6]); break; }
               }
+              if (tg[c] >= 0) rk[c] = atomicAdd(&L.hcnt[tg[c]], 1);
             }
           }
+          hl_sync();
           HSUB(2);
           int run = L.sbtop;
-          int mp[4] = {0, 0, 0, 0};
-          for (int h = 0; h < nh; ++h) {
-            const int base = run;
+          for (int h0 = 0; h0 < nh; h0 += 64) {
+            const int h = h0 + tid;
+            const int v = h < nh ? L.hcnt[h] : 0;
+            int x = v;
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-              if (c * 64 < total) {
-                const unsigned long long b = __ballot(tg[c] == h);
-                if (tg[c] == h) mp[c] = run + __popcll(b & lt);
-                run += __popcll(b);
-              }
+            for (int off = 1; off < 64; off <<= 1) {
+              const int y = __shfl_up(x, off);
+              if (tid >= off) x += y;
             }
-            if (tid == 0) { L.hcnt[h] = run - base; L.hoff[h] = base; }
+            if (h < nh) {
+              L.hoff[h] = run + x - v;
+              soff[L.h_new[h]] = run + x - v;
+              scnt[L.h_new[h]] = v;
+            }
+            run += __shfl(x, 63);
           }
           if (run > sbcap) { if (tid == 0) L.fail = 6; break; }
+          hl_sync();
           HSUB(3);
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             if (tg[c] >= 0) {
-              sb[mp[c]] = qq[c];
+              sb[L.hoff[tg[c]] + rk[c]] = pt[c];
               const unsigned long long k2 =
-                  ((unsigned long long)__float_as_uint(dv[c]) << 32) | (unsigned long long)(~(unsigned)qq[c]);
+                  ((unsigned long long)__float_as_uint(dv[c]) << 32) | (unsigned long long)(~(unsigned)pt[c].q);
               atomicMax(&fbest[L.h_new[tg[c]]], k2);
             }
           }
-          hl_sync();
           HSUB(4);
-          for (int h = tid; h < nh; h += blockDim.x) {
-            soff[L.h_new[h]] = L.hoff[h];
-            scnt[L.h_new[h]] = L.hcnt[h];
-          }
           if (tid == 0) L.sbtop = run;
           hl_sync();
           HSUB(5);
@@ -719,15 +733,16 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
             const int mid = (lo + hi + 1) >> 1;
             if (L.rpre[mid] <= t) lo = mid; else hi = mid - 1;
           }
-          const int q = sb[L.roff[lo] + (t - L.rpre[lo])];
+          const HullPt e = sb[L.roff[lo] + (t - L.rpre[lo])];
+          const int q = e.q;
           int tgt = -1;
           float dd = 0.0f;
           if (q != apex) {
-            const double x0 = Pr[3 * q], x1 = Pr[3 * q + 1], x2 = Pr[3 * q + 2];
+            const double x0 = e.x, x1 = e.y, x2 = e.z;
             for (int h = 0; h < nh; ++h) {
               const double* cp = L.cn[h];
               const double d = cp[0] * (x0 - cp[3]) + cp[1] * (x1 - cp[4]) + cp[2] * (x2 - cp[5]);
-              if (d > cp[7]) { tgt = h; dd = (float)(d / cp[6]); break; }
+              if (d > 0.0 && d * d > cp[7]) { tgt = h; dd = (float)(d * cp[6]); break; }
             }
           }
           tq[t] = q;
@@ -761,7 +776,9 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
           const int h = th[t];
           if (h < 0) continue;
           const int q = tq[t];
-          sb[atomicAdd(&L.hoff[h], 1)] = q;
+          HullPt e;
+          e.x = Pr[3 * q]; e.y = Pr[3 * q + 1]; e.z = Pr[3 * q + 2]; e.q = q; e.pad = 0;
+          sb[atomicAdd(&L.hoff[h], 1)] = e;
           const unsigned long long k2 =
               ((unsigned long long)__float_as_uint(td[t]) << 32) | (unsigned long long)(~(unsigned)q);
           atomicMax(&fbest[L.h_new[h]], k2);

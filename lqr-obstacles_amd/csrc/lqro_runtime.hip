@@ -339,7 +339,7 @@ static int ctx_alloc(lqro_ctx* c) {
   HIPCHK(hipMalloc(&c->d_hfseg, sizeof(int) * 2 * HULL_FB_STRIDE * (size_t)c->hull_blocks));
   HIPCHK(hipMalloc(&c->d_hvpid, sizeof(int) * HULL_VG_STRIDE * (size_t)c->hull_blocks));
   HIPCHK(hipMalloc(&c->d_hstack, sizeof(int) * HULL_STKMULT * H * NP * (size_t)c->hull_blocks));
-  HIPCHK(hipMalloc(&c->d_hfaces, sizeof(int) * HULL_SBMULT * H * NP * (size_t)c->hull_blocks));
+  HIPCHK(hipMalloc(&c->d_hfaces, sizeof(HullPt) * HULL_SBMULT * H * NP * (size_t)c->hull_blocks));
   c->hull_big_blocks = 64;
   HIPCHK(hipMalloc(&c->d_hbig, sizeof(HullMemBig) * (size_t)c->hull_big_blocks));
   return LQRO_OK;
@@ -511,7 +511,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   Hh.planes = c->d_planes; Hh.recs = c->d_recs;
   Hh.queue = c->d_hq; Hh.count = c->d_hcount; Hh.cap = c->hull_cap; Hh.next = c->d_hnext;
   Hh.scratch = c->d_hscratch; Hh.iscratch = c->d_hiscratch; Hh.fscratch = c->d_hfscratch;
-  Hh.sb = reinterpret_cast<int*>(c->d_hfaces);
+  Hh.sb = reinterpret_cast<HullPt*>(c->d_hfaces);
   Hh.fbest = c->d_hfbest;
   Hh.fseg = c->d_hfseg; Hh.vpid = c->d_hvpid; Hh.stack = c->d_hstack;
   Hh.rqueue = c->d_rq; Hh.rcount = c->d_hcount + 2; Hh.rnext = c->d_hcount + 3;

@@ -765,8 +765,9 @@ int orc_hull(int n, const double* P, int32_t* out, int cap) {
     for (int f = 0; f < fn; f++) {
       visible[f] = 0;
       if (!F[f].alive) continue;
-      double nl = sqrt(GDOT(F[f].n, F[f].n));
-      if (face_dist(P, &F[f], p) > eps * nl) { visible[f] = 1; vis[nv++] = f; }
+      /* beyond: d > eps |n|, tested squared as the GPU kernel does */
+      const double d = face_dist(P, &F[f], p), nn = GDOT(F[f].n, F[f].n);
+      if (d > 0.0 && d * d > eps * eps * nn) { visible[f] = 1; vis[nv++] = f; }
     }
     if (nv == 0) continue;
     /* horizon edges */
