@@ -110,13 +110,41 @@ __device__ __forceinline__ bool better(double v, int q, double bv, int bq) {
   return v > bv || (v == bv && q < bq);
 }
 
+// DPP lane moves (VALU, a few cycles) instead of ds_bpermute shuffles (LDS
+// crossbar round trips) for the wave reductions on the pair path.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ int dpp_i(int old, int x) {
+  return __builtin_amdgcn_update_dpp(old, x, CTRL, ROWS, 0xF, false);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_d(double old, double x) {
+  const long long o = __double_as_longlong(old), v = __double_as_longlong(x);
+  const int lo = dpp_i<CTRL, ROWS>((int)o, (int)v);
+  const int hi = dpp_i<CTRL, ROWS>((int)(o >> 32), (int)(v >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void argmax_step(double& v, int& q) {
+  const double ov = dpp_d<CTRL, ROWS>(-INFINITY, v);
+  const int oq = dpp_i<CTRL, ROWS>(INT_MAX, q);
+  if (better(ov, oq, v, q)) { v = ov; q = oq; }
+}
+
+// wave arg-max of (v, q), lowest q on ties, result in every lane: row_shr
+// prefix maxima within each 16-lane row, row_bcast to combine the rows
+// (lane 63 then holds the result), readlane to broadcast
 __device__ __forceinline__ void wave_argmax(double& v, int& q) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    const double ov = __shfl_xor(v, off);
-    const int oq = __shfl_xor(q, off);
-    if (better(ov, oq, v, q)) { v = ov; q = oq; }
-  }
+  argmax_step<0x111, 0xF>(v, q);   // row_shr:1
+  argmax_step<0x112, 0xF>(v, q);   // row_shr:2
+  argmax_step<0x114, 0xF>(v, q);   // row_shr:4
+  argmax_step<0x118, 0xF>(v, q);   // row_shr:8
+  argmax_step<0x142, 0xA>(v, q);   // row_bcast:15
+  argmax_step<0x143, 0xC>(v, q);   // row_bcast:31
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, 63);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+  v = __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+  q = __builtin_amdgcn_readlane(q, 63);
 }
 
 struct SliceSupport {
