@@ -67,7 +67,6 @@ struct HullArgs {
   float* fscratch;                  // per block: H*NP floats (distance beyond the target)
   HullPt* sb;                       // per block: HULL_SBMULT*H*NP entries (outside-set segments)
   unsigned long long* fbest;        // per block: HULL_FB_STRIDE furthest-point keys
-  int* fseg;                        // per block: 2*HULL_FB_STRIDE ints (outside-set offset, count)
   int* vpid;                        // per block: HULL_VG_STRIDE vertex -> point ids
   int* stack;                       // per block: HULL_STKMULT*H*NP faces
   int* rqueue;                      // pairs that overflowed the LDS variant
@@ -75,6 +74,7 @@ struct HullArgs {
   int* rnext;
   void* bigmem;                     // per block of k_hull_big: one HullMemBig
   int block_base;                   // scratch index of this launch's block 0
+  int big_main;                     // k_hull_big takes the main queue (H*NP too large for LDS)
   int wait_pairs;                   // poll the queue until k_pair has finished
   int pair_blocks;                  //   (its workgroup count)
   const int* pair_done;
@@ -84,9 +84,10 @@ struct HullArgs {
 
 // Hull topology and vertex coordinates: LDS for the common case, global
 // scratch (larger capacities) for the jobs that overflow it.
-template <int FMAX, int VTX>
+template <int FMAX, int VTX, class SEG>
 struct HullMem {
   static constexpr int kFaces = FMAX, kVerts = VTX;
+  SEG seg[FMAX];                     // outside set of face f: sb[off .. off+cnt)
   unsigned short fv[FMAX][3];        // vertex slots, outward counter-clockwise
   unsigned short fa[FMAX][3];        // fa[f][e]: face across edge (fv[e], fv[e+1])
   unsigned short vst[FMAX];          // visible-region stamp (insertion number)
@@ -95,8 +96,9 @@ struct HullMem {
   double vx[VTX][3];                 // hull vertex coordinates (rounded points)
   unsigned short vmap[VTX];          // horizon: vertex slot -> edge leaving it
 };
-typedef HullMem<4752, 2368> HullMemSmall;   // ~141 KB: LDS
-typedef HullMem<16384, 8192> HullMemBig;    // ~480 KB: global scratch
+// LDS variant: extent packed as off << 14 | cnt (H*NP <= 16383, see runtime)
+typedef HullMem<4160, 2048, unsigned int> HullMemSmall;   // ~141 KB: LDS
+typedef HullMem<16384, 8192, unsigned long long> HullMemBig;   // ~610 KB: global scratch
 
 // per-step work lists (always LDS)
 template <int RG, int HZ>
@@ -127,6 +129,20 @@ static_assert(HULL_THREADS == 64, "the hull kernels are single-wave");
 __device__ __forceinline__ void hl_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
+}
+
+// outside-set extent of face f
+__device__ __forceinline__ void seg_get(unsigned int s, int& off, int& cnt) {
+  off = (int)(s >> 14); cnt = (int)(s & 0x3FFFu);
+}
+__device__ __forceinline__ void seg_get(unsigned long long s, int& off, int& cnt) {
+  off = (int)(s >> 32); cnt = (int)(s & 0xFFFFFFFFu);
+}
+__device__ __forceinline__ void seg_put(unsigned int& s, int off, int cnt) {
+  s = ((unsigned int)off << 14) | (unsigned int)cnt;
+}
+__device__ __forceinline__ void seg_put(unsigned long long& s, int off, int cnt) {
+  s = ((unsigned long long)(unsigned)off << 32) | (unsigned)cnt;
 }
 
 // n = (b-a) x (c-a) of face f
@@ -255,15 +271,14 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
   const int sbcap = HNP * HULL_SBMULT;
   // per face: furthest outside point (dist bits << 32) | ~q, outside-set extent
   unsigned long long* fbest = A.fbest + (size_t)hb * HULL_FB_STRIDE;
-  int* soff = A.fseg + (size_t)hb * HULL_FB_STRIDE * 2;
-  int* scnt = soff + HULL_FB_STRIDE;
   int* vpid = A.vpid + (size_t)hb * HULL_VG_STRIDE;
   int* stk = A.stack + (size_t)hb * HNP * HULL_STKMULT;
   const int stkcap = HNP * HULL_STKMULT;
 
-  const int* queue = big ? A.rqueue : A.queue;
-  const int* qcount = big ? A.rcount : A.count;
-  int* qnext = big ? A.rnext : A.next;
+  const bool retryq = big && !A.big_main;
+  const int* queue = retryq ? A.rqueue : A.queue;
+  const int* qcount = retryq ? A.rcount : A.count;
+  int* qnext = retryq ? A.rnext : A.next;
   for (;;) {
     // Take the next job.  Workers launched beside k_pair (wait_pairs) poll:
     // an entry is valid once k_pair's release-store made it non-negative,
@@ -282,7 +297,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
           slot = v;
           break;
         }
-        if (big || !A.wait_pairs) break;
+        if (retryq || !A.wait_pairs) break;
         if (__hip_atomic_load(A.pair_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= A.pair_blocks) {
           if (job < min(__hip_atomic_load(qcount, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT), A.cap))
             continue;
@@ -456,7 +471,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
 
     if (!L.fail) {
       // 4. outside sets of the tetrahedron's faces
-      if (tid < 4) { scnt[tid] = 0; fbest[tid] = 0ull; L.hcnt[tid] = 0; }
+      if (tid < 4) { fbest[tid] = 0ull; L.hcnt[tid] = 0; }
       if (tid == 0) { L.sbtop = 0; L.sp = 0; L.qh = 0; L.it = 0; }
       hl_sync();
       for (int q = tid; q < n; q += blockDim.x) {
@@ -475,8 +490,9 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
       if (tid == 0) {
         int o = 0;
         for (int f = 0; f < 4; ++f) {
-          soff[f] = o; scnt[f] = L.hcnt[f]; o += L.hcnt[f];
-          L.hoff[f] = soff[f];
+          seg_put(M.seg[f], o, L.hcnt[f]);
+          L.hoff[f] = o;
+          o += L.hcnt[f];
           M.vst[f] = 0;
         }
         for (int f = 0; f < 4; ++f)
@@ -632,8 +648,10 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
         // retired faces' outside-set extents
         for (int r = tid; r < R; r += blockDim.x) {
           const int g = L.region[r];
-          L.roff[r] = soff[g];
-          L.rcnt[r] = scnt[g];
+          int so, sc;
+          seg_get(M.seg[g], so, sc);
+          L.roff[r] = so;
+          L.rcnt[r] = sc;
         }
         hl_sync();
         if (L.fail) break;
@@ -705,8 +723,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
             }
             if (h < nh) {
               L.hoff[h] = run + x - v;
-              soff[L.h_new[h]] = run + x - v;
-              scnt[L.h_new[h]] = v;
+              seg_put(M.seg[L.h_new[h]], run + x - v, v);
             }
             run += __shfl(x, 63);
           }
@@ -759,8 +776,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
             int tot;
             const int pos = run + hl_scan_val(L, v, &tot);
             if (h < nh) {
-              soff[L.h_new[h]] = pos;
-              scnt[L.h_new[h]] = v;
+              seg_put(M.seg[L.h_new[h]], pos, v);
               L.hoff[h] = pos;
             }
             run += tot;

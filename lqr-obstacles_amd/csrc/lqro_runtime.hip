@@ -224,7 +224,7 @@ struct lqro_ctx {
   int* d_hiscratch;
   float* d_hfscratch;
   unsigned long long* d_hfbest;
-  int *d_hfseg, *d_hvpid, *d_hstack;
+  int *d_hvpid, *d_hstack;
   void* d_hfaces;
   int hull_blocks, hull_cap;
   unsigned long long* d_stats;
@@ -283,7 +283,7 @@ void lqro_destroy(lqro_ctx* c) {
   (void)hipSetDevice(c->cfg.device);
   void* ps[] = {c->d_R, c->d_TF, c->d_shash, c->d_T, c->d_NCF, c->d_S, c->d_x, c->d_vgoal, c->d_newv, c->d_A, c->d_B,
                 c->d_L, c->d_E, c->d_planes, c->d_lpscratch, c->d_lpcompact, c->d_recs, c->d_hq, c->d_hcount,
-                c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats, c->d_prof, c->d_rq, c->d_hbig, c->d_hfbest, c->d_hfseg, c->d_hvpid, c->d_hstack};
+                c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats, c->d_prof, c->d_rq, c->d_hbig, c->d_hfbest, c->d_hvpid, c->d_hstack};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (int k = 0; k < 5; ++k)
@@ -336,7 +336,6 @@ static int ctx_alloc(lqro_ctx* c) {
   HIPCHK(hipMalloc(&c->d_hiscratch, sizeof(int) * 2 * H * NP * HULL_WAVES * c->hull_blocks));
   HIPCHK(hipMalloc(&c->d_hfscratch, sizeof(float) * H * NP * HULL_WAVES * c->hull_blocks));
   HIPCHK(hipMalloc(&c->d_hfbest, sizeof(unsigned long long) * HULL_FB_STRIDE * (size_t)c->hull_blocks));
-  HIPCHK(hipMalloc(&c->d_hfseg, sizeof(int) * 2 * HULL_FB_STRIDE * (size_t)c->hull_blocks));
   HIPCHK(hipMalloc(&c->d_hvpid, sizeof(int) * HULL_VG_STRIDE * (size_t)c->hull_blocks));
   HIPCHK(hipMalloc(&c->d_hstack, sizeof(int) * HULL_STKMULT * H * NP * (size_t)c->hull_blocks));
   HIPCHK(hipMalloc(&c->d_hfaces, sizeof(HullPt) * HULL_SBMULT * H * NP * (size_t)c->hull_blocks));
@@ -501,7 +500,9 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   HIPCHK(hipMemsetAsync(c->d_hcount, 0, sizeof(int) * 8, s));
   HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * 8, s));
   HIPCHK(hipMemsetAsync(c->d_hq, 0xFF, sizeof(int) * (size_t)c->hull_cap, s));
-  const int nwait = (c->nrows >= 4 * c->n_cu && c->n_cu >= 64) ? std::min(c->side_cus, c->n_cu / 2) : 0;
+  // the LDS hull variant packs outside-set extents in 32 bits: H*NP <= 16383
+  const bool lds_ok = (size_t)g.horizon * g.n_points <= 16383;
+  const int nwait = (lds_ok && c->nrows >= 4 * c->n_cu && c->n_cu >= 64) ? std::min(c->side_cus, c->n_cu / 2) : 0;
   const unsigned nblk = (unsigned)std::min(c->nrows, c->n_cu - nwait);
   HullArgs Hh;
   Hh.N = g.n_agents; Hh.X = g.x_dim; Hh.H = g.horizon; Hh.NP = g.n_points;
@@ -513,7 +514,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   Hh.scratch = c->d_hscratch; Hh.iscratch = c->d_hiscratch; Hh.fscratch = c->d_hfscratch;
   Hh.sb = reinterpret_cast<HullPt*>(c->d_hfaces);
   Hh.fbest = c->d_hfbest;
-  Hh.fseg = c->d_hfseg; Hh.vpid = c->d_hvpid; Hh.stack = c->d_hstack;
+  Hh.vpid = c->d_hvpid; Hh.stack = c->d_hstack;
   Hh.rqueue = c->d_rq; Hh.rcount = c->d_hcount + 2; Hh.rnext = c->d_hcount + 3;
   Hh.bigmem = c->d_hbig;
   Hh.stats = c->d_stats;
@@ -522,6 +523,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   Hh.pair_blocks = (int)nblk;
   Hh.block_base = 0;
   Hh.wait_pairs = 1;
+  Hh.big_main = 0;
   if (nwait > 0) {
     HIPCHK(hipEventRecord(c->xev[0], s));
     HIPCHK(hipStreamWaitEvent(c->side, c->xev[0], 0));
@@ -540,8 +542,11 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   HIPCHK(hipEventRecord(c->ev[1], s));
   Hh.block_base = nwait;
   Hh.wait_pairs = 0;
-  hipLaunchKernelGGL(k_hull, dim3(c->hull_blocks - nwait), dim3(HULL_THREADS), 0, s, Hh);
-  HIPCHK(hipGetLastError());
+  Hh.big_main = lds_ok ? 0 : 1;
+  if (lds_ok) {
+    hipLaunchKernelGGL(k_hull, dim3(c->hull_blocks - nwait), dim3(HULL_THREADS), 0, s, Hh);
+    HIPCHK(hipGetLastError());
+  }
   if (nwait > 0) HIPCHK(hipStreamWaitEvent(s, c->xev[1], 0));
   Hh.block_base = 0;
   hipLaunchKernelGGL(k_hull_big, dim3(c->hull_big_blocks), dim3(HULL_THREADS), 0, s, Hh);

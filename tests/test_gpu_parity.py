@@ -91,3 +91,17 @@ def test_dense_swarm_inside_hull(lqro_mod, oracle, gains):
     fac_ok = np.all(recs["facet"][inside] == rrecs["facet"][inside], axis=1)
     assert fac_ok.mean() >= 0.99, fac_ok.mean()
     np.testing.assert_allclose(recs["dist"][inside][fac_ok], rrecs["dist"][inside][fac_ok], rtol=0, atol=0)
+
+
+def test_large_horizon_hull_global_variant(lqro_mod, oracle, gains):
+    """H*NP = 20000 > 16383: every hull job runs in k_hull_big (topology in
+    global memory).  Facets and distances must still match the oracle."""
+    x, vg = lqro_mod.synthetic_swarm(8, box=2.5, seed=5)
+    newv, recs, st, rv, rrecs = _run(lqro_mod, oracle, gains, x, vg, 200, 100)
+    _compare(recs, rrecs)
+    inside = (rrecs["flags"] & 2) != 0
+    assert inside.any()
+    for r, q in zip(recs[inside], rrecs[inside]):
+        assert r["flags"] & 8, "hull failed"
+        assert np.array_equal(r["facet"], q["facet"])
+        assert r["dist"] == q["dist"]
