@@ -22,6 +22,31 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+// DPP lane moves (VALU, a few cycles) instead of ds_bpermute shuffles (LDS
+// crossbar round trips) for wave reductions and scans.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ int dpp_i(int old, int x) {
+  return __builtin_amdgcn_update_dpp(old, x, CTRL, ROWS, 0xF, false);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_d(double old, double x) {
+  const long long o = __double_as_longlong(old), v = __double_as_longlong(x);
+  const int lo = dpp_i<CTRL, ROWS>((int)o, (int)v);
+  const int hi = dpp_i<CTRL, ROWS>((int)(o >> 32), (int)(v >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// inclusive prefix sum over the 64 lanes (all lanes active): row_shr steps
+// inside each 16-lane row, then row_bcast:15 / row_bcast:31 across rows
+__device__ __forceinline__ int wave_incl_scan(int x) {
+  x += dpp_i<0x111, 0xF>(0, x);
+  x += dpp_i<0x112, 0xF>(0, x);
+  x += dpp_i<0x114, 0xF>(0, x);
+  x += dpp_i<0x118, 0xF>(0, x);
+  x += dpp_i<0x142, 0xA>(0, x);
+  x += dpp_i<0x143, 0xC>(0, x);
+  return x;
+}
+
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;

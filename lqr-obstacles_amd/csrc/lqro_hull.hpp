@@ -516,54 +516,57 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
       // 5. quickhull: take the oldest live face with outside points (FIFO
       //    work queue: the hull grows evenly, which wastes fewer insertions
       //    on points that later fall inside than depth-first order), insert
-      //    its furthest point.  One wave: every step is a few dependent LDS
-      //    round trips, no cross-wave barrier.
+      //    its furthest point.  One wave, and every insertion is a chain of
+      //    dependent LDS round trips, so the loop keeps its control state in
+      //    (wave-uniform) registers, passes lists between lanes with ballots,
+      //    readlane and DPP scans, and touches LDS only for the topology.
       // The next queue entry's face, key and apex coordinates are fetched
       // during the current insertion (three dependent global loads off the
       // critical path).  They stay valid unless that face is retired (it is
       // in the current region) or was dead when checked (its slot may be
       // reused by a cone face of this insertion).
+      int qh = 0, sp = L.sp, nvtx = L.nvtx, it = 0, nf = L.nf, nfree = L.nfree, sbtop = L.sbtop;
+      int fail = 0;
+      const unsigned long long lt = (1ull << tid) - 1ull;
       int pf_idx = -1, pf_face = 0;
       bool pf_ok = false;
       unsigned long long pf_key = 0ull;
       double pf_p[3] = {0.0, 0.0, 0.0};
       for (;;) {
-        const int qh = L.qh, sp = L.sp;
         if (qh == sp) break;
         const bool use_pf = pf_ok && pf_idx == qh;
         const int f = use_pf ? pf_face : stk[qh];
-        hl_sync();
-        if (tid == 0) L.qh = qh + 1;
+        ++qh;
         // stale entries: the face was retired (its slot maybe reused by a
         // face without outside points) after it was pushed
         const unsigned long long key = use_pf ? pf_key : fbest[f];
         pf_ok = false;
-        if (!M.alive[f] || key == 0ull) { hl_sync(); continue; }
+        if (!M.alive[f] || key == 0ull) continue;
         const int apex = (int)(~(unsigned)(key & 0xFFFFFFFFull));
-        if (apex < 0 || apex >= n || L.it >= 4 * Mem::kVerts) { if (tid == 0) L.fail = 9; break; }
-        const int av = L.nvtx;
-        const unsigned short stamp = (unsigned short)(L.it + 1);
+        if (apex < 0 || apex >= n || it >= 4 * Mem::kVerts) { fail = 9; break; }
+        if (nvtx >= Mem::kVerts) { fail = 1; break; }
+        const int av = nvtx++;
+        const unsigned short stamp = (unsigned short)(++it);
         double p[3];
         if (use_pf) { p[0] = pf_p[0]; p[1] = pf_p[1]; p[2] = pf_p[2]; }
         else { p[0] = Pr[3 * apex]; p[1] = Pr[3 * apex + 1]; p[2] = Pr[3 * apex + 2]; }
-        pf_idx = qh + 1 < sp ? qh + 1 : -1;
+        pf_idx = qh < sp ? qh : -1;
         if (pf_idx >= 0) pf_face = stk[pf_idx];
-        if (av >= Mem::kVerts) { if (tid == 0) L.fail = 1; break; }
         if (tid == 0) {
           M.vx[av][0] = p[0]; M.vx[av][1] = p[1]; M.vx[av][2] = p[2];
           vpid[av] = apex;
-          L.nvtx = av + 1;
-          L.it = stamp;
-          L.region[0] = (unsigned short)f;
           M.vst[f] = stamp;
         }
         hl_sync();
         HSTAMP(2);
         // (a) visible region: grown over adjacency from f; lanes 0..2 test
-        //     the three neighbours of one region face at a time
+        //     the three neighbours of one region face at a time.  Lane r
+        //     holds region face r (LDS copy for r >= 64 and for later phases).
+        int rg = tid == 0 ? f : -1;
+        if (tid == 0) L.region[0] = (unsigned short)f;
         int R = 1;
         for (int r = 0; r < R; ++r) {
-          const int g = L.region[r];
+          const int g = r < 64 ? __builtin_amdgcn_readlane(rg, r) : (int)L.region[r];
           int nb = -1, vis = 0;
           if (tid < 3) {
             nb = M.fa[g][tid];
@@ -571,14 +574,21 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
           }
           const unsigned long long b = __ballot(vis);
           if (vis) {
-            const int pos = R + __popcll(b & ((1ull << tid) - 1ull));
+            const int pos = R + __popcll(b & lt);
             if (pos < LT::kRegion) { L.region[pos] = (unsigned short)nb; M.vst[nb] = stamp; }
           }
-          R += __popcll(b);
+          // hand the new entries to lanes R, R+1, ...
+          const int n0 = __builtin_amdgcn_readlane(nb, 0), n1 = __builtin_amdgcn_readlane(nb, 1),
+                    n2 = __builtin_amdgcn_readlane(nb, 2);
+          int k = R;
+          if (b & 1ull) { if (tid == k) rg = n0; ++k; }
+          if (b & 2ull) { if (tid == k) rg = n1; ++k; }
+          if (b & 4ull) { if (tid == k) rg = n2; ++k; }
+          R = k;
           if (R > LT::kRegion) break;
           hl_sync();
         }
-        if (R > LT::kRegion) { if (tid == 0) L.fail = 2; break; }
+        if (R > LT::kRegion) { fail = 2; break; }
         if (pf_idx >= 0) {
           pf_ok = M.alive[pf_face] && M.vst[pf_face] != stamp;
           if (pf_ok) pf_key = fbest[pf_face];
@@ -587,7 +597,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
         // (b) horizon: region edges whose neighbour is not in the region,
         //     in (region order, edge) order
         int nh = 0;
-        for (int b0 = 0; b0 < 3 * R; b0 += blockDim.x) {
+        for (int b0 = 0; b0 < 3 * R; b0 += 64) {
           const int t = b0 + tid;
           int ha = 0, hb = 0, ho = 0, is = 0;
           if (t < 3 * R) {
@@ -595,18 +605,18 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
             ho = M.fa[g][e];
             if (M.vst[ho] != stamp) { is = 1; ha = M.fv[g][e]; hb = M.fv[g][(e + 1) % 3]; }
           }
-          int tot;
-          const int pos = nh + hl_scan(L, is, &tot);
+          const unsigned long long b = __ballot(is);
+          const int pos = nh + __popcll(b & lt);
           if (is && pos < LT::kHorizon) {
             L.h_a[pos] = (unsigned short)ha; L.h_b[pos] = (unsigned short)hb; L.h_out[pos] = (unsigned short)ho;
           }
-          nh += tot;
+          nh += __popcll(b);
         }
-        if (nh > LT::kHorizon || nh < 3) { if (tid == 0) L.fail = 3; break; }
-        const int nf0 = L.nf, nfree0 = L.nfree;
-        if (nf0 + max(0, nh - nfree0) > Mem::kFaces) { if (tid == 0) L.fail = 4; break; }
+        if (nh > LT::kHorizon || nh < 3) { fail = 3; break; }
+        const int nf0 = nf, nfree0 = nfree;
+        if (nf0 + max(0, nh - nfree0) > Mem::kFaces) { fail = 4; break; }
         // (c) cone face slots (retired slots first) and the vertex -> edge map
-        for (int h = tid; h < nh; h += blockDim.x) {
+        for (int h = tid; h < nh; h += 64) {
           const int sf = h < nfree0 ? M.freel[nfree0 - 1 - h] : nf0 + (h - nfree0);
           L.h_new[h] = (unsigned short)sf;
           M.vmap[L.h_a[h]] = (unsigned short)h;
@@ -615,7 +625,8 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
         hl_sync();
         HSTAMP(4);
         // (d) cone faces (a, b, apex): adjacency, outer neighbours, planes
-        for (int h = tid; h < nh; h += blockDim.x) {
+        int bad = 0;
+        for (int h = tid; h < nh; h += 64) {
           const int sf = L.h_new[h];
           const int ha = L.h_a[h], hb = L.h_b[h], on = L.h_out[h];
           const int k = M.vmap[hb];                    // edge leaving b
@@ -628,7 +639,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
           M.vst[sf] = 0;
           for (int e = 0; e < 3; ++e)
             if (M.fv[on][e] == hb && M.fv[on][(e + 1) % 3] == ha) M.fa[on][e] = (unsigned short)sf;
-          if (L.h_a[k] != hb) L.fail = 5;
+          if (L.h_a[k] != hb) bad = 1;
           // plane of the new face, as hl_normal / hl_beyond compute it
           const double* a = M.vx[ha];
           const double* bb = M.vx[hb];
@@ -645,38 +656,24 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
           cp[7] = eps2 * nn;
           fbest[sf] = 0ull;
         }
-        // retired faces' outside-set extents
-        for (int r = tid; r < R; r += blockDim.x) {
-          const int g = L.region[r];
-          int so, sc;
-          seg_get(M.seg[g], so, sc);
-          L.roff[r] = so;
-          L.rcnt[r] = sc;
+        if (__ballot(bad)) { fail = 5; break; }
+        // retired faces' outside-set extents: lane r holds region face r's
+        // (r < 64; longer regions take the scratch path below)
+        int roff = 0, rcnt = 0;
+        if (tid < R) {
+          const int g = R <= 64 ? rg : (int)L.region[tid];
+          seg_get(M.seg[g], roff, rcnt);
         }
-        hl_sync();
-        if (L.fail) break;
-        {
-          int run = 0;
-          for (int r0 = 0; r0 < R; r0 += blockDim.x) {
-            const int r = r0 + tid;
-            const int v = r < R ? L.rcnt[r] : 0;
-            int tot;
-            const int pos = run + hl_scan_val(L, v, &tot);
-            if (r < R) L.rpre[r] = pos;
-            run += tot;
-          }
-          if (tid == 0) L.rpre[R] = run;
-        }
-        hl_sync();
+        const int rinc = wave_incl_scan(rcnt);          // prefix over region faces
+        const int total = R <= 64 ? __builtin_amdgcn_readlane(rinc, 63) : -1;
         HSTAMP(5);
-        // (e) the retired faces' outside points: first cone face they are beyond
-        const int total = L.rpre[R];
         if (pf_ok) {
           const int pa = (int)(~(unsigned)(pf_key & 0xFFFFFFFFull));
           if (pa >= 0 && pa < n) { pf_p[0] = Pr[3 * pa]; pf_p[1] = Pr[3 * pa + 1]; pf_p[2] = Pr[3 * pa + 2]; }
         }
         HSUB(0);
-        if (total <= 4 * 64) {
+        // (e) the retired faces' outside points: first cone face they are beyond
+        if (total >= 0 && total <= 4 * 64) {
           // up to four points per lane; each point's rank within its target
           // cone face from an LDS atomic; no scratch round trip
           int tg[4], rk[4];
@@ -686,13 +683,18 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
           for (int c = 0; c < 4; ++c) {
             tg[c] = -1; rk[c] = 0; dv[c] = 0.0f; pt[c].q = -1;
             const int t = c * 64 + tid;
-            if (t < total) {
-              int lo = 0, hi = R - 1;
-              while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (L.rpre[mid] <= t) lo = mid; else hi = mid - 1;
+            if (c * 64 < total) {
+              // region face holding item t: the first r with rinc[r] > t
+              int lo = 0, base = 0, off0 = __builtin_amdgcn_readlane(roff, 0);
+              for (int r = 0; r < R - 1; ++r) {
+                const int inc = __builtin_amdgcn_readlane(rinc, r);
+                if (t >= inc) { lo = r + 1; base = inc; }
               }
-              pt[c] = sb[L.roff[lo] + (t - L.rpre[lo])];
+              for (int r = 1; r < R; ++r) {
+                const int o = __builtin_amdgcn_readlane(roff, r);
+                if (r == lo) off0 = o;
+              }
+              if (t < total) pt[c] = sb[off0 + (t - base)];
             }
           }
           HSUB(1);
@@ -711,23 +713,18 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
           }
           hl_sync();
           HSUB(2);
-          int run = L.sbtop;
+          int run = sbtop;
           for (int h0 = 0; h0 < nh; h0 += 64) {
             const int h = h0 + tid;
             const int v = h < nh ? L.hcnt[h] : 0;
-            int x = v;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-              const int y = __shfl_up(x, off);
-              if (tid >= off) x += y;
-            }
+            const int x = wave_incl_scan(v);
             if (h < nh) {
               L.hoff[h] = run + x - v;
               seg_put(M.seg[L.h_new[h]], run + x - v, v);
             }
-            run += __shfl(x, 63);
+            run += __builtin_amdgcn_readlane(x, 63);
           }
-          if (run > sbcap) { if (tid == 0) L.fail = 6; break; }
+          if (run > sbcap) { fail = 6; break; }
           hl_sync();
           HSUB(3);
 #pragma unroll
@@ -740,102 +737,113 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
             }
           }
           HSUB(4);
-          if (tid == 0) L.sbtop = run;
-          hl_sync();
+          sbtop = run;
           HSUB(5);
         } else {
-        for (int t = tid; t < total; t += blockDim.x) {
-          int lo = 0, hi = R - 1;
-          while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (L.rpre[mid] <= t) lo = mid; else hi = mid - 1;
+          // long regions / many points: through LDS + scratch
+          for (int r = tid; r < R; r += 64) {
+            int so, sc;
+            seg_get(M.seg[L.region[r]], so, sc);
+            L.roff[r] = so;
+            L.rcnt[r] = sc;
           }
-          const HullPt e = sb[L.roff[lo] + (t - L.rpre[lo])];
-          const int q = e.q;
-          int tgt = -1;
-          float dd = 0.0f;
-          if (q != apex) {
-            const double x0 = e.x, x1 = e.y, x2 = e.z;
-            for (int h = 0; h < nh; ++h) {
-              const double* cp = L.cn[h];
-              const double d = cp[0] * (x0 - cp[3]) + cp[1] * (x1 - cp[4]) + cp[2] * (x2 - cp[5]);
-              if (d > 0.0 && d * d > cp[7]) { tgt = h; dd = (float)(d * cp[6]); break; }
+          hl_sync();
+          int run0 = 0;
+          for (int r0 = 0; r0 < R; r0 += 64) {
+            const int r = r0 + tid;
+            const int v = r < R ? L.rcnt[r] : 0;
+            const int x = wave_incl_scan(v);
+            if (r < R) L.rpre[r] = run0 + x - v;
+            run0 += __builtin_amdgcn_readlane(x, 63);
+          }
+          if (tid == 0) L.rpre[R] = run0;
+          hl_sync();
+          const int tot2 = run0;
+          for (int t = tid; t < tot2; t += 64) {
+            int lo = 0, hi = R - 1;
+            while (lo < hi) {
+              const int mid = (lo + hi + 1) >> 1;
+              if (L.rpre[mid] <= t) lo = mid; else hi = mid - 1;
             }
+            const HullPt e = sb[L.roff[lo] + (t - L.rpre[lo])];
+            const int q = e.q;
+            int tgt = -1;
+            float dd = 0.0f;
+            if (q != apex) {
+              const double x0 = e.x, x1 = e.y, x2 = e.z;
+              for (int h = 0; h < nh; ++h) {
+                const double* cp = L.cn[h];
+                const double d = cp[0] * (x0 - cp[3]) + cp[1] * (x1 - cp[4]) + cp[2] * (x2 - cp[5]);
+                if (d > 0.0 && d * d > cp[7]) { tgt = h; dd = (float)(d * cp[6]); break; }
+              }
+            }
+            tq[t] = q;
+            th[t] = tgt;
+            td[t] = dd;
+            if (tgt >= 0) atomicAdd(&L.hcnt[tgt], 1);
           }
-          tq[t] = q;
-          th[t] = tgt;
-          td[t] = dd;
-          if (tgt >= 0) atomicAdd(&L.hcnt[tgt], 1);
-        }
-        hl_sync();
-        {
-          int run = L.sbtop;
-          for (int h0 = 0; h0 < nh; h0 += blockDim.x) {
+          hl_sync();
+          int run = sbtop;
+          for (int h0 = 0; h0 < nh; h0 += 64) {
             const int h = h0 + tid;
             const int v = h < nh ? L.hcnt[h] : 0;
-            int tot;
-            const int pos = run + hl_scan_val(L, v, &tot);
+            const int x = wave_incl_scan(v);
             if (h < nh) {
-              seg_put(M.seg[L.h_new[h]], pos, v);
-              L.hoff[h] = pos;
+              seg_put(M.seg[L.h_new[h]], run + x - v, v);
+              L.hoff[h] = run + x - v;
             }
-            run += tot;
+            run += __builtin_amdgcn_readlane(x, 63);
           }
-          if (tid == 0) {
-            if (run > sbcap) L.fail = 6;
-            L.sbtop = run;
+          if (run > sbcap) { fail = 6; break; }
+          sbtop = run;
+          hl_sync();
+          for (int t = tid; t < tot2; t += 64) {
+            const int h = th[t];
+            if (h < 0) continue;
+            const int q = tq[t];
+            HullPt e;
+            e.x = Pr[3 * q]; e.y = Pr[3 * q + 1]; e.z = Pr[3 * q + 2]; e.q = q; e.pad = 0;
+            sb[atomicAdd(&L.hoff[h], 1)] = e;
+            const unsigned long long k2 =
+                ((unsigned long long)__float_as_uint(td[t]) << 32) | (unsigned long long)(~(unsigned)q);
+            atomicMax(&fbest[L.h_new[h]], k2);
           }
-        }
-        hl_sync();
-        if (L.fail) break;
-        for (int t = tid; t < total; t += blockDim.x) {
-          const int h = th[t];
-          if (h < 0) continue;
-          const int q = tq[t];
-          HullPt e;
-          e.x = Pr[3 * q]; e.y = Pr[3 * q + 1]; e.z = Pr[3 * q + 2]; e.q = q; e.pad = 0;
-          sb[atomicAdd(&L.hoff[h], 1)] = e;
-          const unsigned long long k2 =
-              ((unsigned long long)__float_as_uint(td[t]) << 32) | (unsigned long long)(~(unsigned)q);
-          atomicMax(&fbest[L.h_new[h]], k2);
-        }
         }
         HSTAMP(6);
         // (f) retire the region, commit the cone, push the cone faces that
-        //     have outside points (in horizon order; the last on top)
+        //     have outside points (in horizon order)
         const int used = min(nh, nfree0);
-        for (int r = tid; r < R; r += blockDim.x) {
-          const int g = L.region[r];
+        for (int r = tid; r < R; r += 64) {
+          const int g = R <= 64 ? rg : (int)L.region[r];
           M.alive[g] = 0;
           M.freel[nfree0 - used + r] = (unsigned short)g;
         }
         int npush = 0;
-        for (int h0 = 0; h0 < nh; h0 += blockDim.x) {
+        for (int h0 = 0; h0 < nh; h0 += 64) {
           const int h = h0 + tid;
           int is = 0;
           if (h < nh) {
             M.alive[L.h_new[h]] = 1;
             is = L.hcnt[h] > 0;
           }
-          int tot;
-          const int pos = sp + npush + hl_scan(L, is, &tot);
-          if (is) {
-            if (pos < stkcap) stk[pos] = L.h_new[h];
-            else L.fail = 6;
-          }
-          npush += tot;
+          const unsigned long long b = __ballot(is);
+          const int pos = sp + npush + __popcll(b & lt);
+          if (is && pos < stkcap) stk[pos] = L.h_new[h];
+          npush += __popcll(b);
         }
-        if (tid == 0) {
-          L.nfree = nfree0 - used + R;
-          L.nf = nf0 + (nh - used);
-          L.sp = sp + npush;
-        }
+        if (sp + npush > stkcap) { fail = 6; break; }
+        nfree = nfree0 - used + R;
+        nf = nf0 + (nh - used);
+        sp += npush;
         hl_sync();
-        if (L.fail) break;
         HSTAMP(7);
 #ifdef LQRO_HULL_PROFILE
-        if (tid == 0) { prof_acc[14] += 1; prof_acc[10] += (unsigned long long)R; prof_acc[11] += (unsigned long long)nh; prof_acc[12] += (unsigned long long)total; }
+        if (tid == 0) { prof_acc[14] += 1; prof_acc[10] += (unsigned long long)R; prof_acc[11] += (unsigned long long)nh; prof_acc[12] += (unsigned long long)(total > 0 ? total : 0); }
 #endif
+      }
+      if (tid == 0) {
+        L.nf = nf; L.nfree = nfree; L.nvtx = nvtx; L.sbtop = sbtop; L.sp = sp;
+        if (fail) L.fail = fail;
       }
     }
     hl_sync();

@@ -110,19 +110,6 @@ __device__ __forceinline__ bool better(double v, int q, double bv, int bq) {
   return v > bv || (v == bv && q < bq);
 }
 
-// DPP lane moves (VALU, a few cycles) instead of ds_bpermute shuffles (LDS
-// crossbar round trips) for the wave reductions on the pair path.
-template <int CTRL, int ROWS>
-__device__ __forceinline__ int dpp_i(int old, int x) {
-  return __builtin_amdgcn_update_dpp(old, x, CTRL, ROWS, 0xF, false);
-}
-template <int CTRL, int ROWS>
-__device__ __forceinline__ double dpp_d(double old, double x) {
-  const long long o = __double_as_longlong(old), v = __double_as_longlong(x);
-  const int lo = dpp_i<CTRL, ROWS>((int)o, (int)v);
-  const int hi = dpp_i<CTRL, ROWS>((int)(o >> 32), (int)(v >> 32));
-  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
 template <int CTRL, int ROWS>
 __device__ __forceinline__ void argmax_step(double& v, int& q) {
   const double ov = dpp_d<CTRL, ROWS>(-INFINITY, v);
