@@ -34,8 +34,9 @@
 
 namespace lqro {
 
-#define HULL_THREADS 64          // one wave per hull
-#define HULL_WAVES 1
+#define HULL_WAVES 4             // the points / initial hull / facet phases use 4 waves,
+#define HULL_THREADS (64 * HULL_WAVES)   // the insertions one
+
 #define HULL_SBMULT 16           // outside-set segment buffer: HULL_SBMULT * H*NP entries
 #define HULL_STKMULT 4           // work stack: HULL_STKMULT * H*NP faces
 #define HULL_FB_STRIDE 16384     // per-block face records in global scratch (= big faces)
@@ -119,9 +120,8 @@ struct HullLdsT {
 typedef HullLdsT<512, 128> HullLdsSmall;
 typedef HullLdsT<2048, 1024> HullLdsBig;
 
-static_assert(HULL_THREADS == 64, "the hull kernels are single-wave");
 
-// Ordering point between the lanes of the (single-wave) workgroup.  A wave
+// Ordering point between the lanes of one wave.  A wave
 // executes its LDS and its global memory operations in issue order, so only
 // the compiler has to be kept from moving memory operations across this
 // point; no s_waitcnt / s_barrier is needed (a workgroup fence would stall on
@@ -144,6 +144,9 @@ __device__ __forceinline__ void seg_put(unsigned int& s, int off, int cnt) {
 __device__ __forceinline__ void seg_put(unsigned long long& s, int off, int cnt) {
   s = ((unsigned long long)(unsigned)off << 32) | (unsigned)cnt;
 }
+
+// Barrier across the workgroup's waves.
+__device__ __forceinline__ void hl_bar() { __syncthreads(); }
 
 // n = (b-a) x (c-a) of face f
 template <class Mem>
@@ -183,11 +186,11 @@ __device__ __forceinline__ void hl_argmax(LT& L, double& key, int& idx) {
     if (ok > key || (ok == key && oi < idx)) { key = ok; idx = oi; }
   }
   if (lane == 0) { L.rk[wave] = key; L.ri[wave] = idx; }
-  hl_sync();
+  hl_bar();
   key = L.rk[0]; idx = L.ri[0];
   for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
     if (L.rk[w] > key || (L.rk[w] == key && L.ri[w] < idx)) { key = L.rk[w]; idx = L.ri[w]; }
-  hl_sync();
+  hl_bar();
 }
 
 // exclusive block scan of v (0/1); total in *tot
@@ -197,14 +200,14 @@ __device__ __forceinline__ int hl_scan(LT& L, int v, int* tot) {
   const unsigned long long b = __ballot(v != 0);
   const int in_wave = __popcll(b & ((1ull << lane) - 1ull));
   if (lane == 0) L.scan[wave] = __popcll(b);
-  hl_sync();
+  hl_bar();
   int base = 0, t = 0;
   for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
     if (w < wave) base += L.scan[w];
     t += L.scan[w];
   }
   *tot = t;
-  hl_sync();
+  hl_bar();
   return base + in_wave;
 }
 
@@ -219,14 +222,14 @@ __device__ __forceinline__ int hl_scan_val(LT& L, int v, int* tot) {
     if (lane >= off) x += y;
   }
   if (lane == 63) L.scan[wave] = x;
-  hl_sync();
+  hl_bar();
   int base = 0, t = 0;
   for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
     if (w < wave) base += L.scan[w];
     t += L.scan[w];
   }
   *tot = t;
-  hl_sync();
+  hl_bar();
   return base + x - v;
 }
 
@@ -255,6 +258,7 @@ __device__ __forceinline__ int hl_scan_val(LT& L, int v, int* tot) {
 template <class Mem, class LT>
 __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool big) {
   const int tid = threadIdx.x;
+  const int wave = tid >> 6;
 #ifdef LQRO_HULL_PROFILE
   unsigned long long prof_acc[16] = {0};
   unsigned long long prof_sub[6] = {0};
@@ -309,7 +313,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
       L.job = job;
       L.slot = slot;
     }
-    hl_sync();
+    hl_bar();
     const int job = L.job;
     const int slot = L.slot;
     if (slot < 0) break;
@@ -328,7 +332,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
     HSTAMP(15);
     // 1. reachable points in reference order, full + %g-rounded
     if (tid == 0) { L.n = 0; L.fail = 0; }
-    hl_sync();
+    hl_bar();
     for (int k0 = 0; k0 < A.H; k0 += 128) {
       for (int it = tid; it < 3 * 128; it += blockDim.x) {
         const int k = k0 + it / 3, r = it % 3;
@@ -338,7 +342,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
           L.tr[it] = d;
         }
       }
-      hl_sync();
+      hl_bar();
       const int kend = min(A.H, k0 + 128);
       for (int q0 = k0 * A.NP; q0 < kend * A.NP; q0 += blockDim.x) {
         const int q = q0 + tid;
@@ -368,9 +372,9 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
           Pr[3 * pos + 2] = round6(p2, &oor);
           if (oor) L.fail = 7;
         }
-        hl_sync();
+        hl_bar();
         if (tid == 0) L.n += tot;
-        hl_sync();
+        hl_bar();
       }
     }
     const int n = L.n;
@@ -385,7 +389,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
         L.eps = 1e-13 * (mx + 1.0);
         if (n < 4) L.fail = 8;
       }
-      hl_sync();
+      hl_bar();
     }
     const double eps = L.eps;
     const double eps2 = eps * eps;
@@ -427,7 +431,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
         }
         M.fv[0][0] = 0; M.fv[0][1] = 1; M.fv[0][2] = 2;
       }
-      hl_sync();
+      hl_bar();
       key = -INFINITY; idx = INT_MAX;
       for (int q = tid; q < n; q += blockDim.x) {
         double dd;
@@ -466,14 +470,14 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
           L.nfree = 0;
         }
       }
-      hl_sync();
+      hl_bar();
     }
 
     if (!L.fail) {
       // 4. outside sets of the tetrahedron's faces
       if (tid < 4) { fbest[tid] = 0ull; L.hcnt[tid] = 0; }
       if (tid == 0) { L.sbtop = 0; L.sp = 0; L.qh = 0; L.it = 0; }
-      hl_sync();
+      hl_bar();
       for (int q = tid; q < n; q += blockDim.x) {
         int c = -1;
         double dd = 0.0;
@@ -486,7 +490,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
         td[q] = (float)dd;
         if (c >= 0) atomicAdd(&L.hcnt[c], 1);
       }
-      hl_sync();
+      hl_bar();
       if (tid == 0) {
         int o = 0;
         for (int f = 0; f < 4; ++f) {
@@ -499,7 +503,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
           if (L.hcnt[f] > 0) stk[L.sp++] = f;
         L.sbtop = o;
       }
-      hl_sync();
+      hl_bar();
       for (int q = tid; q < n; q += blockDim.x) {
         const int c = th[q];
         if (c < 0) continue;
@@ -510,9 +514,12 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
             ((unsigned long long)__float_as_uint(td[q]) << 32) | (unsigned long long)(~(unsigned)q);
         atomicMax(&fbest[c], key);
       }
-      hl_sync();
+      hl_bar();
 
       HSTAMP(1);
+      // Insertions run on wave 0 alone (the other waves helped with the
+      // points and the initial hull and wait for the facet selection).
+      if (wave == 0) {
       // 5. quickhull: take the oldest live face with outside points (FIFO
       //    work queue: the hull grows evenly, which wastes fewer insertions
       //    on points that later fall inside than depth-first order), insert
@@ -845,8 +852,10 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
         L.nf = nf; L.nfree = nfree; L.nvtx = nvtx; L.sbtop = sbtop; L.sp = sp;
         if (fail) L.fail = fail;
       }
+      }
+      hl_bar();
     }
-    hl_sync();
+    hl_bar();
 
     HSTAMP(8);
     // 6. the reference's facet selection over all facets (canonical order)
@@ -890,7 +899,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
         s_best[wave] = best; s_t[wave][0] = bt0; s_t[wave][1] = bt1; s_t[wave][2] = bt2;
         s_n[wave][0] = bn[0]; s_n[wave][1] = bn[1]; s_n[wave][2] = bn[2]; s_cnt[wave] = nfac;
       }
-      hl_sync();
+      hl_bar();
       if (tid == 0) {
         int fo = 0, total = 0;
         for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
@@ -944,7 +953,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
           }
         }
       }
-      hl_sync();
+      hl_bar();
     }
     HSTAMP(9);
 #ifdef LQRO_HULL_PROFILE
