@@ -41,6 +41,7 @@ struct PairArgs {
   int row_begin, nrows, npr;          // npr = pairs per row = N-1
   int waves;
   int* row_counter;                   // persistent row queue (zeroed per step)
+  int row_split;                      // pair ranges per row
   int* pair_done;                     // finished workgroups (k_hull workers wait on it)
   int per_agent;
   double vmax, r2, r2_lo, r2_hi;      // reachable radius, its square, fast-test bounds
@@ -271,10 +272,18 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
   // LDS only when they change (once per workgroup with shared gains).
   long staged = -1;
   for (;;) {
-    if (threadIdx.x == 0) { s_row = atomicAdd(P.row_counter, 1); s_next = 0; }
+    // work unit = (row, part): a row is split into row_split pair ranges
+    // when there are fewer rows than workgroups (many GPUs / small N)
+    if (threadIdx.x == 0) {
+      const int u = atomicAdd(P.row_counter, 1);
+      s_row = u;
+      s_next = (int)((long)(u % P.row_split) * P.npr / P.row_split);
+    }
     __syncthreads();
-    const int lrow = s_row;
-    if (lrow >= P.nrows) break;
+    const int unit = s_row;
+    if (unit >= P.nrows * P.row_split) break;
+    const int lrow = unit / P.row_split;
+    const int jj_end = (int)((long)(unit % P.row_split + 1) * P.npr / P.row_split);
     const int i = P.row_begin + lrow;
     const long ag = P.per_agent ? (long)i : 0;
     if (ag != staged) {
@@ -299,7 +308,7 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
     int jj = 0;
     if (lane == 0) jj = atomicAdd(&s_next, 1);
     jj = __shfl(jj, 0);
-    if (jj >= P.npr) break;
+    if (jj >= jj_end) break;
     const int j = jj < i ? jj : jj + 1;
     const double* xj = P.x + (size_t)j * X;
     double d[X];

@@ -503,7 +503,9 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   // the LDS hull variant packs outside-set extents in 32 bits: H*NP <= 16383
   const bool lds_ok = (size_t)g.horizon * g.n_points <= 16383;
   const int nwait = (lds_ok && c->nrows >= 4 * c->n_cu && c->n_cu >= 64) ? std::min(c->side_cus, c->n_cu / 2) : 0;
-  const unsigned nblk = (unsigned)std::min(c->nrows, c->n_cu - nwait);
+  const int nwg = c->n_cu - nwait;
+  P.row_split = std::max(1, std::min(16, (2 * nwg + c->nrows - 1) / c->nrows));
+  const unsigned nblk = (unsigned)std::min(c->nrows * P.row_split, nwg);
   HullArgs Hh;
   Hh.N = g.n_agents; Hh.X = g.x_dim; Hh.H = g.horizon; Hh.NP = g.n_points;
   Hh.row_begin = c->rb; Hh.npr = c->npr; Hh.per_agent = c->per_agent;
