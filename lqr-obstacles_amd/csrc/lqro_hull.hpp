@@ -5,26 +5,33 @@
 // (:869-874), runs qconvex.exe twice (:879-880) and takes
 //     min_f | n_f . (vrel - P[first vertex of f]) |   (:955-968)
 // over the hull facets, n_f from the hull of the ROUNDED points, P at full
-// precision.  One single-wave workgroup per inside-hull pair (persistent over
-// the queue k_pair fills):
+// precision.  One workgroup per inside-hull pair (persistent over the queue
+// k_pair fills):
 //   1. recomputes the pair's reachable points in reference order (exact, as
 //      k_pair does) and their %g round trip (lqro_device.hpp: round6);
-//   2. builds the hull of the rounded points by quickhull: a LIFO stack of
-//      faces with outside points; each step inserts the furthest point of
-//      the popped face, grows its visible region over the face adjacency,
-//      links a cone over the horizon and re-distributes the region's outside
-//      points over the cone.  Topology (vertex slots, adjacency, stamps) and
-//      vertex coordinates live in LDS; outside sets, their extents and the
-//      furthest-point keys in per-block global scratch.  With one wave every
-//      step is a handful of dependent LDS round trips;
+//   2. builds the hull of the rounded points by quickhull: faces with outside
+//      points wait in work queues; an insertion takes a face, adds its
+//      furthest outside point as a vertex, grows the point's visible region
+//      over the face adjacency, links a cone over the horizon and
+//      re-distributes the region's outside points over the cone;
 //   3. evaluates the reference's facet formula on every facet (canonical
 //      facet order, lowest-index vertex) and writes the
 //      half-plane (createHalfPlanes, :1208-1221, inside => mult = +1).
 // A point is beyond a face iff n.(p - a) > eps |n|, n = (b-a) x (c-a),
 // eps = 1e-13 (max|coord| + 1) — the rule of the oracle's hull, so the facet
-// set (unique for points in general position) is the oracle's.  Jobs whose
-// hull outgrows the LDS capacities are re-run by k_hull_big with the same
-// code and the topology in global memory.
+// set (unique for points in general position) is the oracle's, whatever the
+// insertion order.
+//
+// k_hull (topology in LDS) runs the insertions on all HULL_CWAVES waves at
+// once: each wave inserts on its own, and two insertions proceed together
+// when their visible regions and the faces bordering them are disjoint.
+// Every face carries a lock word; an insertion locks its region and border
+// faces as it grows the region, and backs off (re-queueing its face) when it
+// meets a face another wave holds.  Holding every face it reads or writes
+// until it is done makes the insertions serialisable, so the result is that
+// of some sequential insertion order.  Jobs whose hull outgrows the LDS
+// capacities are re-run by k_hull_big: one inserting wave, topology in
+// global memory.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -34,13 +41,22 @@
 
 namespace lqro {
 
-#define HULL_WAVES 4             // the points / initial hull / facet phases use 4 waves,
+#define HULL_WAVES 4             // k_hull_big: the points / initial hull / facet phases use 4 waves,
 #define HULL_THREADS (64 * HULL_WAVES)   // the insertions one
+#define HULL_CWAVES 4            // k_hull: waves, all of them inserting
+#define HULL_CTHREADS (64 * HULL_CWAVES)
+#define HULL_SCR_WAVES 8         // per-block integer scratch: 2*H*NP ints per wave
 
 #define HULL_SBMULT 16           // outside-set segment buffer: HULL_SBMULT * H*NP entries
 #define HULL_STKMULT 4           // work stack: HULL_STKMULT * H*NP faces
 #define HULL_FB_STRIDE 16384     // per-block face records in global scratch (= big faces)
 #define HULL_VG_STRIDE 8192      // per-block vertex records in global scratch (= big vertices)
+
+#define HULL_QCAP 512            // k_hull: per-wave face queue (LDS ring)
+#define HULL_FLCAP 64            // k_hull: per-wave list of retired face slots
+#ifndef HULL_RETRIES
+#define HULL_RETRIES 4           // k_hull: retries of a face another wave holds before re-queueing it
+#endif
 
 // an outside-set entry: the point and its (rounded) coordinates, so that
 // re-distributing it needs one load
@@ -48,6 +64,8 @@ struct HullPt {
   double x, y, z;
   int q, pad;
 };
+
+struct HullWide;
 
 struct HullArgs {
   int N, X, H, NP;
@@ -64,7 +82,7 @@ struct HullArgs {
   int cap;
   int* next;
   double* scratch;                  // per block: H*NP*6 doubles (rounded, full)
-  int* iscratch;                    // per block: 2*H*NP ints (moved point, target face)
+  int* iscratch;                    // per block: 2*H*NP*HULL_SCR_WAVES ints
   float* fscratch;                  // per block: H*NP floats (distance beyond the target)
   HullPt* sb;                       // per block: HULL_SBMULT*H*NP entries (outside-set segments)
   unsigned long long* fbest;        // per block: HULL_FB_STRIDE furthest-point keys
@@ -74,6 +92,7 @@ struct HullArgs {
   int* rcount;
   int* rnext;
   void* bigmem;                     // per block of k_hull_big: one HullMemBig
+  HullWide* wide;                   // per block of k_hull: HULL_CWAVES wide-insertion lists
   int block_base;                   // scratch index of this launch's block 0
   int big_main;                     // k_hull_big takes the main queue (H*NP too large for LDS)
   int wait_pairs;                   // poll the queue until k_pair has finished
@@ -83,8 +102,7 @@ struct HullArgs {
   unsigned long long* prof;          // LQRO_HULL_PROFILE: per-phase cycles
 };
 
-// Hull topology and vertex coordinates: LDS for the common case, global
-// scratch (larger capacities) for the jobs that overflow it.
+// Hull topology and vertex coordinates for k_hull_big (global scratch).
 template <int FMAX, int VTX, class SEG>
 struct HullMem {
   static constexpr int kFaces = FMAX, kVerts = VTX;
@@ -97,12 +115,10 @@ struct HullMem {
   double vx[VTX][3];                 // hull vertex coordinates (rounded points)
   unsigned short vmap[VTX];          // horizon: vertex slot -> edge leaving it
 };
-// LDS variant: extent packed as off << 14 | cnt (H*NP <= 16383, see runtime)
-typedef HullMem<4160, 2048, unsigned int> HullMemSmall;   // ~141 KB: LDS
 typedef HullMem<16384, 8192, unsigned long long> HullMemBig;   // ~610 KB: global scratch
 
-// per-step work lists (always LDS)
-template <int RG, int HZ>
+// k_hull_big's per-step work lists (LDS)
+template <int RG, int HZ, int NW>
 struct HullLdsT {
   static constexpr int kRegion = RG, kHorizon = HZ;
   unsigned short region[RG];                 // visible region of the apex
@@ -111,15 +127,66 @@ struct HullLdsT {
   int hcnt[HZ], hoff[HZ];
   double cn[HZ][8];                          // cone planes: n, a, |n|, eps |n|
   double tr[3 * 128];
-  double rk[HULL_THREADS / 64];
-  int ri[HULL_THREADS / 64];
-  int scan[HULL_THREADS / 64];
+  double rk[NW];
+  int ri[NW];
+  int scan[NW];
   int nf, nfree, nvtx, fail, n, job, slot, init[4], sbtop, sp, qh, it;
   double eps;
 };
-typedef HullLdsT<512, 128> HullLdsSmall;
-typedef HullLdsT<2048, 1024> HullLdsBig;
+typedef HullLdsT<2048, 1024, HULL_WAVES> HullLdsBig;
 
+// k_hull's topology (LDS, ~129 KB).  own[f], the face's lock word:
+//   bits  0-15  its furthest outside point (HULL_NOPT: none)
+//   bits 16-23  lock, one bit per wave
+//   bits 24-31  visible-region mark, one bit per wave; all set: retired slot
+// Extents are packed as off << 14 | cnt (H*NP <= 16383, see runtime).
+#define HULL_NOPT 0xFFFFu
+#define HULL_DEAD 0xFF00FFFFu
+struct HullMemC {
+  static constexpr int kFaces = 4160, kVerts = 2048;
+  unsigned int seg[kFaces];
+  unsigned int own[kFaces];
+  unsigned short fv[kFaces][3];
+  unsigned short fa[kFaces][3];
+  double vx[kVerts][3];
+};
+
+// one inserting wave's lists for an insertion whose visible region or
+// horizon exceeds 64 faces (rare; global scratch)
+#define HULL_WIDE 1024
+struct HullWide {
+  int reg[HULL_WIDE];                       // region faces 64..R-1
+  int ha[HULL_WIDE], hb[HULL_WIDE], on[HULL_WIDE], sf[HULL_WIDE];   // horizon edges, cone faces
+  int cnt[HULL_WIDE], off[HULL_WIDE];
+  unsigned long long kmax[HULL_WIDE];
+  double cn[HULL_WIDE][8];                  // cone planes: n, a, 1/|n|, eps^2 |n|^2
+  int vnext[2048], vprev[2048];             // horizon vertex -> edge leaving / entering it
+};
+
+// one inserting wave's LDS: its face queue (a ring; the owner appends, any
+// wave takes from the head), retired slots, horizon staging, per-cone-face
+// counters
+struct HullWaveL {
+  unsigned long long kmax[64];
+  int hcnt[64];
+  unsigned short q[HULL_QCAP];
+  unsigned short freel[HULL_FLCAP];
+  unsigned short h_a[64], h_b[64], h_out[64];
+  int head, tail;
+};
+
+template <int NW>
+struct HullLdsC {
+  double tr[3 * 128];
+  double rk[NW];
+  int ri[NW];
+  int scan[NW];
+  unsigned long long kmax4[4];
+  int n, fail, job, slot, init[4], hcnt[4], hoff[4];
+  int nf, nvtx, sbtop, work;
+  double eps;
+  HullWaveL wl[NW];
+};
 
 // Ordering point between the lanes of one wave.  A wave
 // executes its LDS and its global memory operations in issue order, so only
@@ -129,6 +196,22 @@ typedef HullLdsT<2048, 1024> HullLdsBig;
 __device__ __forceinline__ void hl_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
+}
+// compiler-only ordering of memory operations (LDS executes a wave's
+// operations in issue order)
+__device__ __forceinline__ void hl_cfence() { asm volatile("" ::: "memory"); }
+
+__device__ __forceinline__ int hl_ld(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void hl_st(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ double hl_rl(double v, int k) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, k);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), k);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
 // outside-set extent of face f
@@ -211,28 +294,6 @@ __device__ __forceinline__ int hl_scan(LT& L, int v, int* tot) {
   return base + in_wave;
 }
 
-// exclusive block scan of v (any int); total in *tot
-template <class LT>
-__device__ __forceinline__ int hl_scan_val(LT& L, int v, int* tot) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  int x = v;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int y = __shfl_up(x, off);
-    if (lane >= off) x += y;
-  }
-  if (lane == 63) L.scan[wave] = x;
-  hl_bar();
-  int base = 0, t = 0;
-  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
-    if (w < wave) base += L.scan[w];
-    t += L.scan[w];
-  }
-  *tot = t;
-  hl_bar();
-  return base + x - v;
-}
-
 #ifdef LQRO_HULL_PROFILE
 #define HSUB(k)                                                     \
   do {                                                              \
@@ -255,20 +316,1048 @@ __device__ __forceinline__ int hl_scan_val(LT& L, int v, int* tot) {
 #define HSUB(k) do {} while (0)
 #endif
 
+// ---------------------------------------------------------------------------
+// Phases shared by both kernels
+// ---------------------------------------------------------------------------
+
+// Take the next job (pair slot), or -1.  Workers launched beside k_pair
+// (wait_pairs) poll: an entry is valid once k_pair's release-store made it
+// non-negative, and the queue is closed when every k_pair workgroup has
+// finished.
+template <class LT>
+__device__ __forceinline__ int hull_take_job(const HullArgs& A, LT& L, bool retryq) {
+  const int* queue = retryq ? A.rqueue : A.queue;
+  const int* qcount = retryq ? A.rcount : A.count;
+  int* qnext = retryq ? A.rnext : A.next;
+  if (threadIdx.x == 0) {
+    const int job = atomicAdd(qnext, 1);
+    int slot = -1;
+    for (long spins = 0;; ++spins) {
+      const int cnt = __hip_atomic_load(qcount, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      if (job < min(cnt, A.cap)) {
+        int v = __hip_atomic_load(queue + job, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        for (long w = 0; v < 0 && w < (1l << 26); ++w) {
+          __builtin_amdgcn_s_sleep(2);
+          v = __hip_atomic_load(queue + job, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        slot = v;
+        break;
+      }
+      if (retryq || !A.wait_pairs) break;
+      if (__hip_atomic_load(A.pair_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= A.pair_blocks) {
+        if (job < min(__hip_atomic_load(qcount, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT), A.cap))
+          continue;
+        break;
+      }
+      if (spins > (1l << 26)) { atomicAdd(&A.stats[4], 1ull); break; }   // bounded wait
+      __builtin_amdgcn_s_sleep(8);
+    }
+    L.job = job;
+    L.slot = slot;
+  }
+  hl_bar();
+  return L.slot;
+}
+
+// 1. The pair's reachable points in reference order, full precision (Pf)
+// and %g-rounded (Pr); returns their number.  2. The tolerance eps, as the
+// oracle's hull: 1e-13 (max|coord| + 1), in L.eps.
+template <class LT>
+__device__ __forceinline__ int hull_points(const HullArgs& A, LT& L, const double* Ti, const double* Ni,
+                                           const double* xi, const double* xj, const double* vrel,
+                                           double* Pr, double* Pf) {
+  const int tid = threadIdx.x;
+  if (tid == 0) { L.n = 0; L.fail = 0; }
+  hl_bar();
+  for (int k0 = 0; k0 < A.H; k0 += 128) {
+    for (int it = tid; it < 3 * 128; it += blockDim.x) {
+      const int k = k0 + it / 3, r = it % 3;
+      if (k < A.H) {
+        double d = 0.0;
+        for (int c = 0; c < A.X; ++c) d += Ni[((size_t)k * 3 + r) * A.X + c] * (xi[c] - xj[c]);
+        L.tr[it] = d;
+      }
+    }
+    hl_bar();
+    const int kend = min(A.H, k0 + 128);
+    for (int q0 = k0 * A.NP; q0 < kend * A.NP; q0 += blockDim.x) {
+      const int q = q0 + tid;
+      bool ok = false;
+      double p0 = 0, p1 = 0, p2 = 0;
+      if (q < kend * A.NP) {
+        const int k = q / A.NP, p = q % A.NP;
+        const double* Tk = Ti + (size_t)k * 9;
+        const double* tk = L.tr + (k - k0) * 3;
+        const double u0 = A.S[3 * p] + tk[0], u1 = A.S[3 * p + 1] + tk[1], u2 = A.S[3 * p + 2] + tk[2];
+        p0 = ((0.0 + Tk[0] * u0) + Tk[1] * u1) + Tk[2] * u2;
+        p1 = ((0.0 + Tk[3] * u0) + Tk[4] * u1) + Tk[5] * u2;
+        p2 = ((0.0 + Tk[6] * u0) + Tk[7] * u1) + Tk[8] * u2;
+        const double a = p0 - vrel[0], b = p1 - vrel[1], c = p2 - vrel[2];
+        const double t = a * a + b * b + c * c;
+        if (t < A.r2_lo) ok = true;
+        else if (t > A.r2_hi) ok = false;
+        else ok = (a * a) / A.r2 + (b * b) / A.r2 + (c * c) / A.r2 < 1.0;
+      }
+      int tot;
+      const int pos = L.n + hl_scan(L, ok ? 1 : 0, &tot);
+      if (ok) {
+        int oor = 0;
+        Pf[3 * pos] = p0; Pf[3 * pos + 1] = p1; Pf[3 * pos + 2] = p2;
+        Pr[3 * pos] = round6(p0, &oor);
+        Pr[3 * pos + 1] = round6(p1, &oor);
+        Pr[3 * pos + 2] = round6(p2, &oor);
+        if (oor) L.fail = 7;
+      }
+      hl_bar();
+      if (tid == 0) L.n += tot;
+      hl_bar();
+    }
+  }
+  const int n = L.n;
+  double mx = 0.0;
+  int dummy = 0;
+  for (int q = tid; q < 3 * n; q += blockDim.x) mx = fmax(mx, fabs(Pr[q]));
+  hl_argmax(L, mx, dummy);
+  if (tid == 0) {
+    L.eps = 1e-13 * (mx + 1.0);
+    if (n < 4) L.fail = 8;
+  }
+  hl_bar();
+  return n;
+}
+
+// 3. Initial tetrahedron from extreme points: vertex slots 0..3, faces 0..3
+// (outward, adjacency linked), L.init = their point ids.  Sets L.fail = 8
+// for a degenerate point set.  Thread 0 writes; callers barrier after.
+template <class Mem, class LT>
+__device__ __forceinline__ void hull_tetra(Mem& M, LT& L, const double* Pr, int n, double eps,
+                                           double eps2, int* vpid) {
+  const int tid = threadIdx.x;
+  double key; int idx;
+  key = -INFINITY; idx = INT_MAX;
+  for (int q = tid; q < n; q += blockDim.x) {
+    const double v = -Pr[3 * q];
+    if (v > key || (v == key && q < idx)) { key = v; idx = q; }
+  }
+  hl_argmax(L, key, idx);
+  const int i0 = idx;
+  const double* P0 = Pr + 3 * i0;
+  key = -INFINITY; idx = INT_MAX;
+  for (int q = tid; q < n; q += blockDim.x) {
+    const double dx = Pr[3 * q] - P0[0], dy = Pr[3 * q + 1] - P0[1], dz = Pr[3 * q + 2] - P0[2];
+    const double v = dx * dx + dy * dy + dz * dz;
+    if (v > key || (v == key && q < idx)) { key = v; idx = q; }
+  }
+  hl_argmax(L, key, idx);
+  const int i1 = idx;
+  const double* P1 = Pr + 3 * i1;
+  key = -INFINITY; idx = INT_MAX;
+  for (int q = tid; q < n; q += blockDim.x) {
+    const double e1[3] = {P1[0] - P0[0], P1[1] - P0[1], P1[2] - P0[2]};
+    const double e2[3] = {Pr[3 * q] - P0[0], Pr[3 * q + 1] - P0[1], Pr[3 * q + 2] - P0[2]};
+    const double cx = e1[1] * e2[2] - e1[2] * e2[1], cy = e1[2] * e2[0] - e1[0] * e2[2], cz = e1[0] * e2[1] - e1[1] * e2[0];
+    const double v = cx * cx + cy * cy + cz * cz;
+    if (v > key || (v == key && q < idx)) { key = v; idx = q; }
+  }
+  hl_argmax(L, key, idx);
+  const int i2 = idx;
+  if (tid == 0) {
+    for (int d = 0; d < 3; ++d) {
+      M.vx[0][d] = Pr[3 * i0 + d]; M.vx[1][d] = Pr[3 * i1 + d]; M.vx[2][d] = Pr[3 * i2 + d];
+    }
+    M.fv[0][0] = 0; M.fv[0][1] = 1; M.fv[0][2] = 2;
+  }
+  hl_bar();
+  key = -INFINITY; idx = INT_MAX;
+  for (int q = tid; q < n; q += blockDim.x) {
+    double dd;
+    hl_beyond(M, 0, Pr + 3 * q, eps2, &dd);
+    const double v = fabs(dd);
+    if (v > key || (v == key && q < idx)) { key = v; idx = q; }
+  }
+  hl_argmax(L, key, idx);
+  const int i3 = idx;
+  if (tid == 0) {
+    if (!(key > eps) || i0 == i1 || i1 == i2 || i2 == i3) L.fail = 8;
+    L.init[0] = i0; L.init[1] = i1; L.init[2] = i2; L.init[3] = i3;
+    if (!L.fail) {
+      for (int v = 0; v < 4; ++v) {
+        vpid[v] = L.init[v];
+        for (int d = 0; d < 3; ++d) M.vx[v][d] = Pr[3 * L.init[v] + d];
+      }
+      const int fvv[4][3] = {{0, 1, 2}, {0, 3, 1}, {1, 3, 2}, {0, 2, 3}};
+      for (int f = 0; f < 4; ++f) {
+        for (int e = 0; e < 3; ++e) M.fv[f][e] = (unsigned short)fvv[f][e];
+        const int other = 6 - fvv[f][0] - fvv[f][1] - fvv[f][2];
+        double dd;
+        hl_beyond(M, f, M.vx[other], 0.0, &dd);
+        if (dd > 0) { const unsigned short t = M.fv[f][1]; M.fv[f][1] = M.fv[f][2]; M.fv[f][2] = t; }
+      }
+      for (int f = 0; f < 4; ++f)
+        for (int e = 0; e < 3; ++e) {
+          const int a = M.fv[f][e], b = M.fv[f][(e + 1) % 3];
+          for (int g = 0; g < 4; ++g)
+            for (int e2 = 0; e2 < 3; ++e2)
+              if (M.fv[g][e2] == b && M.fv[g][(e2 + 1) % 3] == a) M.fa[f][e] = (unsigned short)g;
+        }
+    }
+  }
+}
+
+// 6. The reference's facet selection over all live faces f < nf (canonical
+// order, see the file comment), then the half-plane, the record, the stats.
+// A capacity failure of k_hull (fail 1-4) hands the pair to k_hull_big.
+template <class Mem, class LT, class Alive>
+__device__ __forceinline__ void hull_select(const HullArgs& A, const Mem& M, LT& L, const double* Pr,
+                                            const double* Pf, const int* vpid, int nf, Alive alive,
+                                            const double* xi, const double* vrel, int slot, bool big) {
+  const int tid = threadIdx.x;
+  double best = INFINITY;
+  int bt0 = INT_MAX, bt1 = INT_MAX, bt2 = INT_MAX, nfac = 0;
+  double bn[3] = {0, 0, 0};
+  if (!L.fail) {
+    for (int f = tid; f < nf; f += blockDim.x) {
+      if (!alive(f)) continue;
+      nfac++;
+      int t0 = vpid[M.fv[f][0]], t1 = vpid[M.fv[f][1]], t2 = vpid[M.fv[f][2]];
+      while (!(t0 < t1 && t0 < t2)) { const int a = t0; t0 = t1; t1 = t2; t2 = a; }
+      const double *a = Pr + 3 * t0, *b = Pr + 3 * t1, *c = Pr + 3 * t2;
+      const double e1[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+      const double e2[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
+      double nv[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+      const double len = sqrt(nv[0] * nv[0] + nv[1] * nv[1] + nv[2] * nv[2]);
+      nv[0] /= len; nv[1] /= len; nv[2] /= len;
+      const double* p0 = Pf + 3 * t0;
+      const double dd = fabs(nv[0] * (vrel[0] - p0[0]) + nv[1] * (vrel[1] - p0[1]) + nv[2] * (vrel[2] - p0[2]));
+      const int s1 = min(t1, t2), s2 = max(t1, t2);
+      const bool bt = dd < best || (dd == best && (t0 < bt0 || (t0 == bt0 && (s1 < bt1 || (s1 == bt1 && s2 < bt2)))));
+      if (bt) { best = dd; bt0 = t0; bt1 = s1; bt2 = s2; bn[0] = nv[0]; bn[1] = nv[1]; bn[2] = nv[2]; }
+    }
+  }
+  // block arg-min by (distance, triple): wave shuffles, then across waves
+  const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double ob = __shfl_xor(best, off);
+    const int o0 = __shfl_xor(bt0, off), o1 = __shfl_xor(bt1, off), o2 = __shfl_xor(bt2, off);
+    const double on0 = __shfl_xor(bn[0], off), on1 = __shfl_xor(bn[1], off), on2 = __shfl_xor(bn[2], off);
+    nfac += __shfl_xor(nfac, off);
+    const bool bt = ob < best || (ob == best && (o0 < bt0 || (o0 == bt0 && (o1 < bt1 || (o1 == bt1 && o2 < bt2)))));
+    if (bt) { best = ob; bt0 = o0; bt1 = o1; bt2 = o2; bn[0] = on0; bn[1] = on1; bn[2] = on2; }
+  }
+  __shared__ double s_best[8], s_n[8][3];
+  __shared__ int s_t[8][3], s_cnt[8];
+  if (lane == 0) {
+    s_best[wave] = best; s_t[wave][0] = bt0; s_t[wave][1] = bt1; s_t[wave][2] = bt2;
+    s_n[wave][0] = bn[0]; s_n[wave][1] = bn[1]; s_n[wave][2] = bn[2]; s_cnt[wave] = nfac;
+  }
+  hl_bar();
+  if (tid == 0) {
+    int fo = 0, total = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+      total += s_cnt[w];
+      const bool bt = s_best[w] < s_best[fo] ||
+                      (s_best[w] == s_best[fo] &&
+                       (s_t[w][0] < s_t[fo][0] || (s_t[w][0] == s_t[fo][0] &&
+                        (s_t[w][1] < s_t[fo][1] || (s_t[w][1] == s_t[fo][1] && s_t[w][2] < s_t[fo][2])))));
+      if (bt) fo = w;
+    }
+    const bool ok = !L.fail && total > 0 && s_t[fo][0] != INT_MAX;
+    // capacity overflow in the LDS variant: hand the pair to k_hull_big
+    const bool retry = !big && L.fail >= 1 && L.fail <= 4;
+#ifdef LQRO_HULL_PROFILE
+    if (A.prof) atomicAdd(&A.prof[16 + (L.fail & 15)], 1ull);
+#endif
+    if (retry) {
+      const int r = atomicAdd(A.rcount, 1);
+      if (r < A.cap) A.rqueue[r] = slot;
+    }
+    float* pl = A.planes + (size_t)slot * 8;
+    const double distance = s_best[fo];
+    const double nrm[3] = {s_n[fo][0], s_n[fo][1], s_n[fo][2]};
+    if (retry) {
+      // written by k_hull_big
+    } else if (ok) {
+      const double dh = distance * 0.5;                  // :1416
+      const double mult = 1.0;                           // :1213
+      pl[0] = (float)(xi[3] + mult * dh * nrm[0]);
+      pl[1] = (float)(xi[4] + mult * dh * nrm[1]);
+      pl[2] = (float)(xi[5] + mult * dh * nrm[2]);
+      pl[3] = (float)nrm[0]; pl[4] = (float)nrm[1]; pl[5] = (float)nrm[2];
+      pl[6] = __int_as_float(1);
+      atomicAdd(&A.stats[3], 1ull);
+    } else {
+      pl[6] = __int_as_float(0);                         // no usable plane
+      atomicAdd(&A.stats[4], 1ull);
+    }
+    if (A.recs && !retry) {
+      lqro_pair_record& rec = A.recs[slot];
+      rec.flags |= ok ? LQRO_REC_HULL : LQRO_REC_HULLFAIL;
+      rec.n_facets = ok ? total : -1;
+      if (ok) {
+        rec.facet[0] = s_t[fo][0]; rec.facet[1] = s_t[fo][1]; rec.facet[2] = s_t[fo][2];
+        rec.dist = distance;
+        for (int q = 0; q < 3; ++q) {
+          rec.normal[q] = nrm[q];
+          rec.plane_point[q] = pl[q];
+          rec.plane_normal[q] = pl[3 + q];
+        }
+      }
+    }
+  }
+  hl_bar();
+}
+
+// ---------------------------------------------------------------------------
+// k_hull: concurrent insertions, topology in LDS
+// ---------------------------------------------------------------------------
+
+// take the oldest entry of wave queue Q (-1: empty); lane 0
+__device__ __forceinline__ int hq_pop(HullWaveL& Q) {
+  for (int tries = 0; tries < 16; ++tries) {
+    const int h = hl_ld(&Q.head);
+    hl_cfence();
+    const int t = hl_ld(&Q.tail);
+    hl_cfence();
+    if (h >= t) return -1;
+    const int e = __hip_atomic_load(&Q.q[h % HULL_QCAP], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    hl_cfence();
+    if (atomicCAS(&Q.head, h, h + 1) == h) return e;
+  }
+  return -1;
+}
+
+// One insertion whose region (R) or horizon exceeds 64 faces: the steps of
+// hull_insert_mw, chunked over 64 lanes with the lists in per-wave global
+// scratch (WG).  The wave holds the region and the faces around it.
+// Returns 0 or a failure code; updates the free-list length and queue tail.
+template <int NW>
+__device__ __noinline__ int hull_insert_wide(HullMemC& M, HullLdsC<NW>& L, HullWaveL& W, HullWide& WG,
+                                             const double* Pr, int* vpid, HullPt* sb, int sbcap, int* sq,
+                                             int HNP, int apex, const double* p, double eps2, int R, int rg,
+                                             int& nfree, int& mytail, unsigned LK, unsigned RB) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  constexpr int kF = HullMemC::kFaces, kV = HullMemC::kVerts;
+  auto region = [&](int r0, int r) { return r0 == 0 ? rg : WG.reg[r]; };
+  // horizon, in (region order, edge) order
+  int nh = 0;
+  for (int b0 = 0; b0 < 3 * R; b0 += 64) {
+    const int t = b0 + lane;
+    const int rr = t / 3;
+    int g = __shfl(rg, min(rr, 63));
+    int ha = 0, hb = 0, ho = 0, is = 0;
+    if (t < 3 * R) {
+      if (rr >= 64) g = WG.reg[rr];
+      const int e = t % 3;
+      ho = M.fa[g][e];
+      if (!(M.own[ho] & RB)) { is = 1; ha = M.fv[g][e]; hb = M.fv[g][e == 2 ? 0 : e + 1]; }
+    }
+    const unsigned long long b = __ballot(is);
+    const int pos = nh + __popcll(b & lt);
+    if (is && pos < HULL_WIDE) { WG.ha[pos] = ha; WG.hb[pos] = hb; WG.on[pos] = ho; }
+    nh += __popcll(b);
+  }
+  if (nh > HULL_WIDE || nh < 3) return 3;
+  // cone face slots, apex vertex, horizon vertex maps
+  const int used = min(nh, nfree);
+  int sfb = 0, av = 0;
+  if (lane == 0) { sfb = atomicAdd(&L.nf, nh - used); av = atomicAdd(&L.nvtx, 1); }
+  sfb = __builtin_amdgcn_readlane(sfb, 0);
+  av = __builtin_amdgcn_readlane(av, 0);
+  if (sfb + (nh - used) > kF) return 4;
+  if (av >= kV) return 1;
+  if (lane == 0) {
+    M.vx[av][0] = p[0]; M.vx[av][1] = p[1]; M.vx[av][2] = p[2];
+    vpid[av] = apex;
+  }
+  for (int h0 = 0; h0 < nh; h0 += 64) {
+    const int h = h0 + lane;
+    if (h < nh) {
+      WG.sf[h] = h < used ? (int)W.freel[nfree - 1 - h] : sfb + (h - used);
+      WG.vnext[WG.ha[h]] = h;
+      WG.vprev[WG.hb[h]] = h;
+    }
+  }
+  hl_sync();
+  int bad = 0;
+  for (int h0 = 0; h0 < nh; h0 += 64) {
+    const int h = h0 + lane;
+    if (h >= nh) continue;
+    const int ha = WG.ha[h], hb = WG.hb[h], on = WG.on[h], sf = WG.sf[h];
+    const int kn = WG.vnext[hb], kp = WG.vprev[ha];        // edge leaving b, edge entering a
+    if (kn < 0 || kn >= nh || kp < 0 || kp >= nh || WG.ha[kn] != hb || WG.hb[kp] != ha) { bad = 1; continue; }
+    M.own[sf] = LK | HULL_NOPT;
+    M.fv[sf][0] = (unsigned short)ha;
+    M.fv[sf][1] = (unsigned short)hb;
+    M.fv[sf][2] = (unsigned short)av;
+    M.fa[sf][0] = (unsigned short)on;
+    M.fa[sf][1] = (unsigned short)WG.sf[kn];
+    M.fa[sf][2] = (unsigned short)WG.sf[kp];
+    for (int e = 0; e < 3; ++e)
+      if (M.fv[on][e] == hb && M.fv[on][e == 2 ? 0 : e + 1] == ha) M.fa[on][e] = (unsigned short)sf;
+    const double* a = M.vx[ha];
+    const double* bb = M.vx[hb];
+    const double e1[3] = {bb[0] - a[0], bb[1] - a[1], bb[2] - a[2]};
+    const double e2[3] = {p[0] - a[0], p[1] - a[1], p[2] - a[2]};
+    const double cx = e1[1] * e2[2] - e1[2] * e2[1];
+    const double cy = e1[2] * e2[0] - e1[0] * e2[2];
+    const double cz = e1[0] * e2[1] - e1[1] * e2[0];
+    const double nn = cx * cx + cy * cy + cz * cz;
+    double* cp = WG.cn[h];
+    cp[0] = cx; cp[1] = cy; cp[2] = cz; cp[3] = a[0]; cp[4] = a[1]; cp[5] = a[2];
+    cp[6] = 1.0 / sqrt(nn);
+    cp[7] = eps2 * nn;
+    WG.cnt[h] = 0;
+    WG.kmax[h] = 0ull;
+  }
+  if (__ballot(bad)) return 5;
+  hl_sync();
+  // the retired faces' outside points, one region face at a time:
+  // first cone face beyond, rank and key by global atomics, to scratch
+  int items = 0;
+  for (int r = 0; r < R; ++r) {
+    const int g = r < 64 ? __builtin_amdgcn_readlane(rg, r) : WG.reg[r];
+    int so, sc;
+    seg_get(M.seg[g], so, sc);
+    for (int c0 = 0; c0 < sc; c0 += 64) {
+      const int t = c0 + lane;
+      HullPt e;
+      e.q = -1;
+      if (t < sc) e = sb[so + t];
+      int tg = -1;
+      float dv = 0.0f;
+      bool pend = t < sc && e.q != apex;
+      for (int h = 0; h < nh; ++h) {
+        if (!__ballot(pend)) break;
+        if (pend) {
+          const double* cp = WG.cn[h];
+          const double d = cp[0] * (e.x - cp[3]) + cp[1] * (e.y - cp[4]) + cp[2] * (e.z - cp[5]);
+          if (d > 0.0 && d * d > cp[7]) { tg = h; dv = (float)(d * cp[6]); pend = false; }
+        }
+      }
+      int code = 0;
+      if (tg >= 0) {
+        const int rk = atomicAdd(&WG.cnt[tg], 1);
+        atomicMax(&WG.kmax[tg], ((unsigned long long)__float_as_uint(dv) << 32) |
+                                    (unsigned long long)(~(unsigned)e.q));
+        code = (rk << 11) | (tg + 1);
+      }
+      if (t < sc) { sq[items + t] = e.q; sq[HNP + items + t] = code; }
+    }
+    items += sc;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // the rank atomics have returned
+  int run = 0;
+  for (int h0 = 0; h0 < nh; h0 += 64) {
+    const int h = h0 + lane;
+    const int cnt = h < nh ? WG.cnt[h] : 0;
+    const int x = wave_incl_scan(cnt);
+    if (h < nh) WG.off[h] = run + x - cnt;
+    run += __builtin_amdgcn_readlane(x, 63);
+  }
+  int base = 0;
+  if (lane == 0) base = atomicAdd(&L.sbtop, run);
+  base = __builtin_amdgcn_readlane(base, 0);
+  if (base + run > sbcap) return 6;
+  for (int h0 = 0; h0 < nh; h0 += 64) {
+    const int h = h0 + lane;
+    if (h < nh) {
+      const int cnt = WG.cnt[h], sf = WG.sf[h];
+      const unsigned long long km = WG.kmax[h];
+      const int off = base + WG.off[h];
+      WG.off[h] = off;
+      seg_put(M.seg[sf], off, cnt);
+      M.own[sf] = LK | (cnt ? ((~(unsigned)km) & 0xFFFFu) : HULL_NOPT);
+    }
+  }
+  hl_sync();
+  for (int t0 = 0; t0 < items; t0 += 64) {
+    const int t = t0 + lane;
+    if (t < items) {
+      const int q = sq[t], code = sq[HNP + t];
+      if (code) {
+        HullPt e;
+        e.x = Pr[3 * q]; e.y = Pr[3 * q + 1]; e.z = Pr[3 * q + 2]; e.q = q; e.pad = 0;
+        sb[WG.off[(code & 2047) - 1] + (code >> 11)] = e;
+      }
+    }
+  }
+  // retire the region, release, queue the cone faces with outside points
+  const int keep = nfree - used;
+  for (int r0 = 0; r0 < R; r0 += 64) {
+    const int r = r0 + lane;
+    if (r < R) {
+      const int g = region(r0, r);
+      M.own[g] = HULL_DEAD;
+      if (keep + r < HULL_FLCAP) W.freel[keep + r] = (unsigned short)g;
+    }
+  }
+  nfree = min(keep + R, HULL_FLCAP);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int np = 0, full = 0;
+  for (int h0 = 0; h0 < nh; h0 += 64) {
+    const int h = h0 + lane;
+    int is = 0, sf = 0;
+    if (h < nh) {
+      sf = WG.sf[h];
+      atomicAnd(&M.own[sf], ~LK);
+      atomicAnd(&M.own[WG.on[h]], ~LK);
+      is = WG.cnt[h] > 0;
+    }
+    const unsigned long long b = __ballot(is);
+    if (mytail + np + __popcll(b) - hl_ld(&W.head) > HULL_QCAP) { full = 1; break; }
+    if (is) W.q[(mytail + np + __popcll(b & lt)) % HULL_QCAP] = (unsigned short)sf;
+    np += __popcll(b);
+  }
+  if (full) return 4;
+  mytail += np;
+  hl_sync();
+  if (lane == 0) {
+    atomicAdd(&L.work, np - 1);
+    hl_cfence();
+    hl_st(&W.tail, mytail);
+  }
+  return 0;
+}
+
+// The insertion loop of one wave.  L.work counts the queued faces plus the
+// insertions in progress; the loop returns when it reaches 0, or on a
+// failure (L.fail).  Conflicts are resolved wait-die: a wave that meets a
+// face held by a higher-numbered wave waits for it, one that meets a face
+// held by a lower-numbered wave backs off (releases everything, re-queues
+// its face).  Waits only go from lower to higher wave numbers, so they end.
+template <int NW>
+__device__ __forceinline__ void hull_insert_mw(HullMemC& M, HullLdsC<NW>& L, const double* Pr, int n,
+                                               double eps2, int* vpid, HullPt* sb, int sbcap,
+                                               int* sq, int HNP, HullWide& WG, unsigned long long* pstat) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned LK = 1u << (16 + w), RB = 1u << (24 + w);
+  const unsigned OLDER = ((1u << w) - 1u) << 16;        // lock bits of lower-numbered waves
+  HullWaveL& W = L.wl[w];
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  int nfree = 0, mytail = hl_ld(&W.tail), attempts = 0, idle = 0;
+  unsigned long long n_ins = 0, n_conf = 0, n_stale = 0, n_big = 0;
+  constexpr int kF = HullMemC::kFaces, kV = HullMemC::kVerts;
+  // re-queue face f (lane 0; the entry keeps its unit of L.work)
+  auto requeue = [&](int f) {
+    if (lane == 0) {
+      if (mytail - hl_ld(&W.head) >= HULL_QCAP) atomicMax(&L.fail, 4);
+      else {
+        W.q[mytail % HULL_QCAP] = (unsigned short)f;
+        hl_cfence();
+        hl_st(&W.tail, ++mytail);
+      }
+    }
+    mytail = __builtin_amdgcn_readlane(mytail, 0);
+  };
+  int pending = -1, retries = 0;    // a face to retry before taking a new one
+  unsigned maxr = 0;
+  for (;;) {
+    if (hl_ld(&L.fail)) break;
+    // (a) a face: the one to retry, else own queue first, then the others'
+    //     (oldest entries)
+    int f = pending;
+    pending = -1;
+    if (f < 0) {
+      retries = 0;
+      if (lane == 0) {
+        for (int k = 0; k < NW && f < 0; ++k) f = hq_pop(L.wl[(w + k) % NW]);
+        if (f >= hl_ld(&L.nf)) { atomicMax(&L.fail, 9); f = -1; }
+      }
+      f = __builtin_amdgcn_readlane(f, 0);
+    }
+    if (f < 0) {
+      int done = 0;
+      if (lane == 0) done = hl_ld(&L.work) <= 0;
+      if (__builtin_amdgcn_readlane(done, 0)) break;
+      if (++idle > (1 << 24)) { if (lane == 0) atomicMax(&L.fail, 9); break; }   // bounded wait
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    idle = 0;
+    // (b) lock it; skip retired slots and faces without outside points,
+    //     re-queue faces another wave holds
+    unsigned old = 0;
+    if (lane == 0) old = atomicOr(&M.own[f], LK);
+    old = (unsigned)__builtin_amdgcn_readlane((int)old, 0);
+    if ((old & 0x00FF0000u) || (old >> 24) == 0xFFu || (old & 0xFFFFu) == HULL_NOPT) {
+      if (lane == 0) atomicAnd(&M.own[f], ~LK);
+      if ((old & 0x00FF0000u) && (old >> 24) != 0xFFu) {
+        // held by another wave: retry it shortly, then queue it again
+        if (++retries <= HULL_RETRIES) pending = f;
+        else requeue(f);
+        if (++n_stale > (1u << 22)) { if (lane == 0) atomicMax(&L.fail, 9); break; }
+        __builtin_amdgcn_s_sleep(2);
+      } else if (lane == 0) {
+        atomicSub(&L.work, 1);
+      }
+      continue;
+    }
+    if (++attempts > 16 * kV) { if (lane == 0) atomicMax(&L.fail, 9); break; }
+    const int apex = (int)(old & 0xFFFFu);
+    if (apex >= n) { if (lane == 0) atomicMax(&L.fail, 9); break; }
+    const double p[3] = {Pr[3 * apex], Pr[3 * apex + 1], Pr[3 * apex + 2]};
+    if (lane == 0) atomicOr(&M.own[f], RB);
+    // (c) visible region, grown over adjacency from f; lanes 0..2 lock and
+    //     test the three neighbours of one region face at a time.  Lane r
+    //     holds region face r.
+    int rg = lane == 0 ? f : -1;
+    int R = 1, conflict = 0;
+    for (int r = 0; r < R; ++r) {
+      const int g = r < 64 ? __builtin_amdgcn_readlane(rg, r) : WG.reg[r];
+      int nb = -1, vis = 0, cf = 0;
+      bool need = lane < 3;
+      if (need) nb = M.fa[g][lane];
+      for (int spin = 0;; ++spin) {
+        if (need) {
+          const unsigned o = atomicOr(&M.own[nb], LK);
+          if (o & LK) {
+            need = false;                                  // in the region or around it already
+          } else if (!(o & 0x00FF0000u)) {
+            need = false;
+            vis = hl_beyond(M, nb, p, eps2, nullptr);
+            if (vis) atomicOr(&M.own[nb], RB);
+          } else {
+            atomicAnd(&M.own[nb], ~LK);
+            if (o & OLDER) { cf = 1; need = false; }       // held by a lower-numbered wave: back off
+          }
+        }
+        if (__ballot(cf) || !__ballot(need)) break;
+        if (spin > (1 << 20) || hl_ld(&L.fail)) { cf = 1; break; }
+        __builtin_amdgcn_s_sleep(1);                       // wait for a higher-numbered wave
+      }
+      if (__ballot(cf)) { conflict = 1; break; }
+      const unsigned long long b = __ballot(vis);
+      const int n0 = __builtin_amdgcn_readlane(nb, 0), n1 = __builtin_amdgcn_readlane(nb, 1),
+                n2 = __builtin_amdgcn_readlane(nb, 2);
+      int k = R;
+      const int nn3[3] = {n0, n1, n2};
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        if (b & (1ull << c)) {
+          if (k < 64) { if (lane == k) rg = nn3[c]; }
+          else if (lane == 0) WG.reg[k] = nn3[c];
+          ++k;
+        }
+      R = k;
+      if (R > HULL_WIDE - 3) break;
+    }
+    maxr = max(maxr, (unsigned)R);
+    n_big += R > 32;
+    if (R > HULL_WIDE - 3) { if (lane == 0) atomicMax(&L.fail, 2); break; }
+    if (conflict) {
+      // release the region and the faces around it, re-queue f
+      for (int r0 = 0; r0 < R; r0 += 64) {
+        const int r = r0 + lane;
+        if (r < R) {
+          const int g = r0 == 0 ? rg : WG.reg[r];
+          for (int e = 0; e < 3; ++e) atomicAnd(&M.own[M.fa[g][e]], ~(LK | RB));
+          atomicAnd(&M.own[g], ~(LK | RB));
+        }
+      }
+      hl_sync();
+      if (++retries <= HULL_RETRIES) pending = f;
+      else requeue(f);
+      ++n_conf;
+      __builtin_amdgcn_s_sleep(4);
+      continue;
+    }
+    // (d) horizon: region edges whose neighbour is not in the region, in
+    //     (region order, edge) order, staged through LDS into lanes
+    int nh = 0;
+    if (R <= 64) {
+      for (int b0 = 0; b0 < 3 * R; b0 += 64) {
+        const int t = b0 + lane;
+        const int g = __shfl(rg, min(t / 3, 63));
+        int ha = 0, hb = 0, ho = 0, is = 0;
+        if (t < 3 * R) {
+          const int e = t % 3;
+          ho = M.fa[g][e];
+          if (!(M.own[ho] & RB)) { is = 1; ha = M.fv[g][e]; hb = M.fv[g][e == 2 ? 0 : e + 1]; }
+        }
+        const unsigned long long b = __ballot(is);
+        const int pos = nh + __popcll(b & lt);
+        if (is && pos < 64) {
+          W.h_a[pos] = (unsigned short)ha; W.h_b[pos] = (unsigned short)hb; W.h_out[pos] = (unsigned short)ho;
+        }
+        nh += __popcll(b);
+      }
+    }
+    if (R > 64 || nh > 64) {
+      // ---- wide insertion: region / horizon lists in global scratch ----
+      const int rc = hull_insert_wide(M, L, W, WG, Pr, vpid, sb, sbcap, sq, HNP, apex, p, eps2, R, rg,
+                                      nfree, mytail, LK, RB);
+      if (rc) { if (lane == 0) atomicMax(&L.fail, rc); break; }
+      ++n_ins;
+      continue;
+    }
+    if (nh < 3) { if (lane == 0) atomicMax(&L.fail, 3); break; }
+    hl_sync();
+    const bool hl = lane < nh;
+    int ha = 0, hb = 0, on = 0;
+    if (hl) { ha = W.h_a[lane]; hb = W.h_b[lane]; on = W.h_out[lane]; }
+    // (e) cone face slots (own retired slots first), the apex vertex
+    const int used = min(nh, nfree);
+    int sfb = 0, av = 0;
+    if (lane == 0) { sfb = atomicAdd(&L.nf, nh - used); av = atomicAdd(&L.nvtx, 1); }
+    sfb = __builtin_amdgcn_readlane(sfb, 0);
+    av = __builtin_amdgcn_readlane(av, 0);
+    if (sfb + (nh - used) > kF) { if (lane == 0) atomicMax(&L.fail, 4); break; }
+    if (av >= kV) { if (lane == 0) atomicMax(&L.fail, 1); break; }
+    int sf = 0;
+    if (hl) sf = lane < used ? (int)W.freel[nfree - 1 - lane] : sfb + (lane - used);
+    if (lane == 0) {
+      M.vx[av][0] = p[0]; M.vx[av][1] = p[1]; M.vx[av][2] = p[2];
+      vpid[av] = apex;
+    }
+    // cone neighbours: the edge leaving b (next) and the edge entering a (prev)
+    int nx = -1, pv = -1;
+    for (int k = 0; k < nh; ++k) {
+      const int ak = __builtin_amdgcn_readlane(ha, k), bk = __builtin_amdgcn_readlane(hb, k);
+      if (ak == hb) nx = k;
+      if (bk == ha) pv = k;
+    }
+    if (__ballot(hl && (nx < 0 || pv < 0))) { if (lane == 0) atomicMax(&L.fail, 5); break; }
+    const int sfn = __shfl(sf, max(nx, 0)), sfp = __shfl(sf, max(pv, 0));
+    double cx = 0, cy = 0, cz = 0, ax = 0, ay = 0, az = 0, ci = 0, ce = 0;
+    if (hl) {
+      M.own[sf] = LK | HULL_NOPT;
+      M.fv[sf][0] = (unsigned short)ha;
+      M.fv[sf][1] = (unsigned short)hb;
+      M.fv[sf][2] = (unsigned short)av;
+      M.fa[sf][0] = (unsigned short)on;
+      M.fa[sf][1] = (unsigned short)sfn;
+      M.fa[sf][2] = (unsigned short)sfp;
+      for (int e = 0; e < 3; ++e)
+        if (M.fv[on][e] == hb && M.fv[on][e == 2 ? 0 : e + 1] == ha) M.fa[on][e] = (unsigned short)sf;
+      // plane of the new face, as hl_normal / hl_beyond compute it
+      const double* a = M.vx[ha];
+      const double* bb = M.vx[hb];
+      const double e1[3] = {bb[0] - a[0], bb[1] - a[1], bb[2] - a[2]};
+      const double e2[3] = {p[0] - a[0], p[1] - a[1], p[2] - a[2]};
+      cx = e1[1] * e2[2] - e1[2] * e2[1];
+      cy = e1[2] * e2[0] - e1[0] * e2[2];
+      cz = e1[0] * e2[1] - e1[1] * e2[0];
+      ax = a[0]; ay = a[1]; az = a[2];
+      const double nn = cx * cx + cy * cy + cz * cz;
+      ci = 1.0 / sqrt(nn);                            // for the distance key only
+      ce = eps2 * nn;
+      W.hcnt[lane] = 0;
+      W.kmax[lane] = 0ull;
+    }
+    // (f) the retired faces' outside points: first cone face they are beyond
+    int roff = 0, rcnt = 0;
+    if (lane < R) seg_get(M.seg[rg], roff, rcnt);
+    const int rinc = wave_incl_scan(rcnt);
+    const int total = __builtin_amdgcn_readlane(rinc, 63);
+    hl_sync();
+    // item t -> its region face's extent
+    auto locate = [&](int t, int& src) {
+      int base = 0, off0 = __builtin_amdgcn_readlane(roff, 0);
+      for (int r = 0; r < R - 1; ++r) {
+        const int inc = __builtin_amdgcn_readlane(rinc, r);
+        const int o = __builtin_amdgcn_readlane(roff, r + 1);
+        if (t >= inc) { base = inc; off0 = o; }
+      }
+      src = off0 + (t - base);
+    };
+    // first cone face (in horizon order) p is beyond; its key in *kd
+    auto target = [&](const HullPt& e, bool act, int& tg, float& dv) {
+      tg = -1;
+      dv = 0.0f;
+      bool pend = act && e.q != apex;
+      for (int h = 0; h < nh; ++h) {
+        if (!__ballot(pend)) break;
+        const double c0 = hl_rl(cx, h), c1 = hl_rl(cy, h), c2 = hl_rl(cz, h);
+        const double a0 = hl_rl(ax, h), a1 = hl_rl(ay, h), a2 = hl_rl(az, h), cc = hl_rl(ce, h);
+        if (pend) {
+          const double d = c0 * (e.x - a0) + c1 * (e.y - a1) + c2 * (e.z - a2);
+          if (d > 0.0 && d * d > cc) { tg = h; dv = (float)(d * hl_rl(ci, h)); pend = false; }
+        }
+      }
+    };
+    int base = 0;
+    if (total <= 4 * 64) {
+      int tg[4], rk[4];
+      HullPt pt[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        tg[c] = -1; rk[c] = 0; pt[c].q = -1;
+        const int t = c * 64 + lane;
+        if (c * 64 < total) {
+          int src;
+          locate(t, src);
+          if (t < total) pt[c] = sb[src];
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (c * 64 < total) {
+          float dv;
+          target(pt[c], c * 64 + lane < total, tg[c], dv);
+          if (tg[c] >= 0) {
+            rk[c] = atomicAdd(&W.hcnt[tg[c]], 1);
+            atomicMax(&W.kmax[tg[c]], ((unsigned long long)__float_as_uint(dv) << 32) |
+                                          (unsigned long long)(~(unsigned)pt[c].q));
+          }
+        }
+      }
+      hl_sync();
+      const int cnt = hl ? W.hcnt[lane] : 0;
+      const unsigned long long km = hl ? W.kmax[lane] : 0ull;
+      const int cinc = wave_incl_scan(cnt);
+      const int tot = __builtin_amdgcn_readlane(cinc, 63);
+      if (lane == 0) base = atomicAdd(&L.sbtop, tot);
+      base = __builtin_amdgcn_readlane(base, 0);
+      if (base + tot > sbcap) { if (lane == 0) atomicMax(&L.fail, 6); break; }
+      const int off = base + cinc - cnt;
+      if (hl) {
+        seg_put(M.seg[sf], off, cnt);
+        M.own[sf] = LK | (cnt ? ((~(unsigned)km) & 0xFFFFu) : HULL_NOPT);
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int o = __shfl(off, max(tg[c], 0));
+        if (tg[c] >= 0) sb[o + rk[c]] = pt[c];
+      }
+    } else {
+      // many points (early insertions): two passes through per-wave scratch
+      for (int t0 = 0; t0 < total; t0 += 64) {
+        const int t = t0 + lane;
+        int src;
+        locate(t, src);
+        HullPt e;
+        e.q = -1;
+        if (t < total) e = sb[src];
+        int tg;
+        float dv;
+        target(e, t < total, tg, dv);
+        int code = 0;
+        if (tg >= 0) {
+          const int rk = atomicAdd(&W.hcnt[tg], 1);
+          atomicMax(&W.kmax[tg], ((unsigned long long)__float_as_uint(dv) << 32) |
+                                     (unsigned long long)(~(unsigned)e.q));
+          code = (rk << 7) | (tg + 1);
+        }
+        if (t < total) { sq[t] = e.q; sq[HNP + t] = code; }
+      }
+      hl_sync();
+      const int cnt = hl ? W.hcnt[lane] : 0;
+      const unsigned long long km = hl ? W.kmax[lane] : 0ull;
+      const int cinc = wave_incl_scan(cnt);
+      const int tot = __builtin_amdgcn_readlane(cinc, 63);
+      if (lane == 0) base = atomicAdd(&L.sbtop, tot);
+      base = __builtin_amdgcn_readlane(base, 0);
+      if (base + tot > sbcap) { if (lane == 0) atomicMax(&L.fail, 6); break; }
+      const int off = base + cinc - cnt;
+      if (hl) {
+        seg_put(M.seg[sf], off, cnt);
+        M.own[sf] = LK | (cnt ? ((~(unsigned)km) & 0xFFFFu) : HULL_NOPT);
+      }
+      for (int t0 = 0; t0 < total; t0 += 64) {
+        const int t = t0 + lane;
+        int code = 0, q = 0;
+        if (t < total) { q = sq[t]; code = sq[HNP + t]; }
+        const int tg = (code & 127) - 1;
+        const int o = __shfl(off, max(tg, 0));
+        if (code) {
+          HullPt e;
+          e.x = Pr[3 * q]; e.y = Pr[3 * q + 1]; e.z = Pr[3 * q + 2]; e.q = q; e.pad = 0;
+          sb[o + (code >> 7)] = e;
+        }
+      }
+    }
+    const int cnt_mine = hl ? W.hcnt[lane] : 0;
+    // (g) retire the region (slots to this wave's list), then, once this
+    //     wave's global stores are done, release the cone and the faces
+    //     around it and queue the cone faces that have outside points
+    if (lane < R) M.own[rg] = HULL_DEAD;
+    {
+      const int keep = nfree - used;
+      if (lane < R && keep + lane < HULL_FLCAP) W.freel[keep + lane] = (unsigned short)rg;
+      nfree = min(keep + R, HULL_FLCAP);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (hl) {
+      atomicAnd(&M.own[sf], ~LK);
+      atomicAnd(&M.own[on], ~LK);
+    }
+    {
+      const int is = hl && cnt_mine > 0;
+      const unsigned long long b = __ballot(is);
+      const int np = __popcll(b);
+      if (mytail + np - hl_ld(&W.head) > HULL_QCAP) { if (lane == 0) atomicMax(&L.fail, 4); break; }
+      if (is) W.q[(mytail + __popcll(b & lt)) % HULL_QCAP] = (unsigned short)sf;
+      mytail += np;
+      hl_sync();
+      if (lane == 0) {
+        atomicAdd(&L.work, np - 1);                        // before the entries are visible
+        hl_cfence();
+        hl_st(&W.tail, mytail);
+      }
+    }
+    ++n_ins;
+  }
+#ifdef LQRO_HULL_PROFILE
+  if (lane == 0 && pstat) {
+    atomicAdd(&pstat[0], n_ins);
+    atomicAdd(&pstat[1], n_conf);
+    atomicAdd(&pstat[2], n_stale);
+    atomicMax(&pstat[3], (unsigned long long)maxr);
+    atomicAdd(&pstat[4], n_big);
+  }
+#else
+  (void)n_ins; (void)n_conf; (void)n_stale; (void)pstat; (void)maxr; (void)n_big;
+#endif
+}
+
+template <int NW>
+__device__ __forceinline__ void hull_body_mw(const HullArgs& A, HullMemC& M, HullLdsC<NW>& L) {
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+#ifdef LQRO_HULL_PROFILE
+  unsigned long long prof_acc[16] = {0};
+  unsigned long long prof_last = __builtin_amdgcn_s_memtime();
+#endif
+  const int HNP = A.H * A.NP;
+  const int hb = A.block_base + blockIdx.x;                   // scratch slot
+  double* Pr = A.scratch + (size_t)hb * HNP * 6;              // rounded points
+  double* Pf = Pr + (size_t)HNP * 3;                          // full-precision points
+  int* isc = A.iscratch + (size_t)hb * HNP * 2 * HULL_SCR_WAVES;
+  float* td = A.fscratch + (size_t)hb * HNP;
+  HullPt* sb = A.sb + (size_t)hb * HNP * HULL_SBMULT;
+  const int sbcap = HNP * HULL_SBMULT;
+  int* vpid = A.vpid + (size_t)hb * HULL_VG_STRIDE;
+  for (;;) {
+    const int slot = hull_take_job(A, L, false);
+    if (slot < 0) break;
+    const int lrow = slot / A.npr, jj = slot % A.npr;
+    const int i = A.row_begin + lrow;
+    const int j = jj < i ? jj : jj + 1;
+    const double* xi = A.x + (size_t)i * A.X;
+    const double* xj = A.x + (size_t)j * A.X;
+    const double* Ti = A.T + (A.per_agent ? (size_t)i * A.H * 9 : 0);
+    const double* Ni = A.NCF + (A.per_agent ? (size_t)i * A.H * 3 * A.X : 0);
+    const double vrel[3] = {xi[3] - xj[3], xi[4] - xj[4], xi[5] - xj[5]};
+#ifdef LQRO_HULL_PROFILE
+    const unsigned long long job_t0 = __builtin_amdgcn_s_memtime();
+#endif
+    HSTAMP(15);
+    const int n = hull_points(A, L, Ti, Ni, xi, xj, vrel, Pr, Pf);
+    const double eps2 = L.eps * L.eps;
+    HSTAMP(0);
+    if (!L.fail) {
+      hull_tetra(M, L, Pr, n, L.eps, eps2, vpid);
+      hl_bar();
+    }
+    if (!L.fail) {
+      // 4. outside sets of the tetrahedron's faces; the faces go to the
+      //    wave queues round-robin
+      int* th = isc;
+      if (tid < 4) { L.hcnt[tid] = 0; L.kmax4[tid] = 0ull; }
+      if (tid < NW) { L.wl[tid].head = 0; L.wl[tid].tail = 0; }
+      hl_bar();
+      for (int q = tid; q < n; q += blockDim.x) {
+        int c = -1;
+        double dd = 0.0;
+        if (q != L.init[0] && q != L.init[1] && q != L.init[2] && q != L.init[3]) {
+          const double p[3] = {Pr[3 * q], Pr[3 * q + 1], Pr[3 * q + 2]};
+          for (int f = 0; f < 4; ++f)
+            if (hl_beyond(M, f, p, eps2, &dd)) { c = f; break; }
+        }
+        th[q] = c;
+        td[q] = (float)dd;
+        if (c >= 0) atomicAdd(&L.hcnt[c], 1);
+      }
+      hl_bar();
+      if (tid == 0) {
+        int o = 0;
+        for (int f = 0; f < 4; ++f) {
+          seg_put(M.seg[f], o, L.hcnt[f]);
+          L.hoff[f] = o;
+          o += L.hcnt[f];
+        }
+        L.sbtop = o;
+        L.nf = 4;
+        L.nvtx = 4;
+        L.work = 0;
+      }
+      hl_bar();
+      for (int q = tid; q < n; q += blockDim.x) {
+        const int c = th[q];
+        if (c < 0) continue;
+        HullPt e;
+        e.x = Pr[3 * q]; e.y = Pr[3 * q + 1]; e.z = Pr[3 * q + 2]; e.q = q; e.pad = 0;
+        sb[atomicAdd(&L.hoff[c], 1)] = e;
+        const unsigned long long key =
+            ((unsigned long long)__float_as_uint(td[q]) << 32) | (unsigned long long)(~(unsigned)q);
+        atomicMax(&L.kmax4[c], key);
+      }
+      hl_bar();
+      if (tid == 0) {
+        for (int f = 0; f < 4; ++f) {
+          M.own[f] = L.hcnt[f] ? ((~(unsigned)L.kmax4[f]) & 0xFFFFu) : HULL_NOPT;
+          if (L.hcnt[f]) {
+            HullWaveL& Q = L.wl[f % NW];
+            Q.q[Q.tail++] = (unsigned short)f;
+            L.work++;
+          }
+        }
+      }
+      hl_bar();
+      HSTAMP(1);
+      // 5. quickhull, every wave inserting
+      hull_insert_mw<NW>(M, L, Pr, n, eps2, vpid, sb, sbcap, isc + (size_t)wave * 2 * HNP, HNP,
+                         A.wide[(size_t)hb * NW + wave],
+#ifdef LQRO_HULL_PROFILE
+                         A.prof ? A.prof + 10 : nullptr
+#else
+                         nullptr
+#endif
+      );
+      hl_bar();
+      HSTAMP(6);
+    }
+    hl_bar();
+    HSTAMP(8);
+    // 6. facet selection
+    const int nf = L.nf;
+    hull_select(A, M, L, Pr, Pf, vpid, nf, [&](int f) { return (M.own[f] >> 24) != 0xFFu; }, xi, vrel,
+                slot, false);
+    HSTAMP(9);
+#ifdef LQRO_HULL_PROFILE
+    if (tid == 0 && A.prof && L.job < 2048) {
+      const int pj = 32 + 2 * L.job;
+      A.prof[pj] = __builtin_amdgcn_s_memtime() - job_t0;
+      A.prof[pj + 1] = (unsigned long long)L.nvtx | ((unsigned long long)n << 20) |
+                       ((unsigned long long)L.fail << 40) | ((unsigned long long)slot << 44);
+    }
+#endif
+  }
+#ifdef LQRO_HULL_PROFILE
+  if (tid == 0 && A.prof)
+    for (int k = 0; k < 10; ++k) atomicAdd(&A.prof[k], prof_acc[k]);
+  if (tid == 0 && A.prof) atomicAdd(&A.prof[15], prof_acc[15]);
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// k_hull_big: one inserting wave, topology in global memory
+// ---------------------------------------------------------------------------
 template <class Mem, class LT>
 __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool big) {
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
 #ifdef LQRO_HULL_PROFILE
   unsigned long long prof_acc[16] = {0};
-  unsigned long long prof_sub[6] = {0};
   unsigned long long prof_last = __builtin_amdgcn_s_memtime();
 #endif
   const int HNP = A.H * A.NP;
   const int hb = A.block_base + blockIdx.x;                   // scratch slot
   double* Pr = A.scratch + (size_t)hb * HNP * 6;    // rounded points
   double* Pf = Pr + (size_t)HNP * 3;                         // full-precision points
-  int* tq = A.iscratch + (size_t)hb * HNP * 2;      // moved point ids
+  int* tq = A.iscratch + (size_t)hb * HNP * 2 * HULL_SCR_WAVES;   // moved point ids
   int* th = tq + HNP;                                        // their target cone face
   float* td = A.fscratch + (size_t)hb * HNP;         // distance beyond it
   HullPt* sb = A.sb + (size_t)hb * HNP * HULL_SBMULT;
@@ -280,42 +1369,8 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
   const int stkcap = HNP * HULL_STKMULT;
 
   const bool retryq = big && !A.big_main;
-  const int* queue = retryq ? A.rqueue : A.queue;
-  const int* qcount = retryq ? A.rcount : A.count;
-  int* qnext = retryq ? A.rnext : A.next;
   for (;;) {
-    // Take the next job.  Workers launched beside k_pair (wait_pairs) poll:
-    // an entry is valid once k_pair's release-store made it non-negative,
-    // and the queue is closed when every k_pair workgroup has finished.
-    if (tid == 0) {
-      const int job = atomicAdd(qnext, 1);
-      int slot = -1;
-      for (long spins = 0;; ++spins) {
-        const int cnt = __hip_atomic_load(qcount, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        if (job < min(cnt, A.cap)) {
-          int v = __hip_atomic_load(queue + job, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-          for (long w = 0; v < 0 && w < (1l << 26); ++w) {
-            __builtin_amdgcn_s_sleep(2);
-            v = __hip_atomic_load(queue + job, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-          }
-          slot = v;
-          break;
-        }
-        if (retryq || !A.wait_pairs) break;
-        if (__hip_atomic_load(A.pair_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= A.pair_blocks) {
-          if (job < min(__hip_atomic_load(qcount, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT), A.cap))
-            continue;
-          break;
-        }
-        if (spins > (1l << 26)) { atomicAdd(&A.stats[4], 1ull); break; }   // bounded wait
-        __builtin_amdgcn_s_sleep(8);
-      }
-      L.job = job;
-      L.slot = slot;
-    }
-    hl_bar();
-    const int job = L.job;
-    const int slot = L.slot;
+    const int slot = hull_take_job(A, L, retryq);
     if (slot < 0) break;
     const int lrow = slot / A.npr, jj = slot % A.npr;
     const int i = A.row_begin + lrow;
@@ -330,145 +1385,18 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
 #endif
 
     HSTAMP(15);
-    // 1. reachable points in reference order, full + %g-rounded
-    if (tid == 0) { L.n = 0; L.fail = 0; }
-    hl_bar();
-    for (int k0 = 0; k0 < A.H; k0 += 128) {
-      for (int it = tid; it < 3 * 128; it += blockDim.x) {
-        const int k = k0 + it / 3, r = it % 3;
-        if (k < A.H) {
-          double d = 0.0;
-          for (int c = 0; c < A.X; ++c) d += Ni[((size_t)k * 3 + r) * A.X + c] * (xi[c] - xj[c]);
-          L.tr[it] = d;
-        }
-      }
-      hl_bar();
-      const int kend = min(A.H, k0 + 128);
-      for (int q0 = k0 * A.NP; q0 < kend * A.NP; q0 += blockDim.x) {
-        const int q = q0 + tid;
-        bool ok = false;
-        double p0 = 0, p1 = 0, p2 = 0;
-        if (q < kend * A.NP) {
-          const int k = q / A.NP, p = q % A.NP;
-          const double* Tk = Ti + (size_t)k * 9;
-          const double* tk = L.tr + (k - k0) * 3;
-          const double u0 = A.S[3 * p] + tk[0], u1 = A.S[3 * p + 1] + tk[1], u2 = A.S[3 * p + 2] + tk[2];
-          p0 = ((0.0 + Tk[0] * u0) + Tk[1] * u1) + Tk[2] * u2;
-          p1 = ((0.0 + Tk[3] * u0) + Tk[4] * u1) + Tk[5] * u2;
-          p2 = ((0.0 + Tk[6] * u0) + Tk[7] * u1) + Tk[8] * u2;
-          const double a = p0 - vrel[0], b = p1 - vrel[1], c = p2 - vrel[2];
-          const double t = a * a + b * b + c * c;
-          if (t < A.r2_lo) ok = true;
-          else if (t > A.r2_hi) ok = false;
-          else ok = (a * a) / A.r2 + (b * b) / A.r2 + (c * c) / A.r2 < 1.0;
-        }
-        int tot;
-        const int pos = L.n + hl_scan(L, ok ? 1 : 0, &tot);
-        if (ok) {
-          int oor = 0;
-          Pf[3 * pos] = p0; Pf[3 * pos + 1] = p1; Pf[3 * pos + 2] = p2;
-          Pr[3 * pos] = round6(p0, &oor);
-          Pr[3 * pos + 1] = round6(p1, &oor);
-          Pr[3 * pos + 2] = round6(p2, &oor);
-          if (oor) L.fail = 7;
-        }
-        hl_bar();
-        if (tid == 0) L.n += tot;
-        hl_bar();
-      }
-    }
-    const int n = L.n;
-
-    // 2. tolerance, as the oracle's hull: 1e-13 (max|coord| + 1)
-    {
-      double mx = 0.0;
-      int dummy = 0;
-      for (int q = tid; q < 3 * n; q += blockDim.x) mx = fmax(mx, fabs(Pr[q]));
-      hl_argmax(L, mx, dummy);
-      if (tid == 0) {
-        L.eps = 1e-13 * (mx + 1.0);
-        if (n < 4) L.fail = 8;
-      }
-      hl_bar();
-    }
+    const int n = hull_points(A, L, Ti, Ni, xi, xj, vrel, Pr, Pf);
     const double eps = L.eps;
     const double eps2 = eps * eps;
 
     HSTAMP(0);
-    // 3. initial tetrahedron from extreme points
     if (!L.fail) {
-      double key; int idx;
-      key = -INFINITY; idx = INT_MAX;
-      for (int q = tid; q < n; q += blockDim.x) {
-        const double v = -Pr[3 * q];
-        if (v > key || (v == key && q < idx)) { key = v; idx = q; }
-      }
-      hl_argmax(L, key, idx);
-      const int i0 = idx;
-      const double* P0 = Pr + 3 * i0;
-      key = -INFINITY; idx = INT_MAX;
-      for (int q = tid; q < n; q += blockDim.x) {
-        const double dx = Pr[3 * q] - P0[0], dy = Pr[3 * q + 1] - P0[1], dz = Pr[3 * q + 2] - P0[2];
-        const double v = dx * dx + dy * dy + dz * dz;
-        if (v > key || (v == key && q < idx)) { key = v; idx = q; }
-      }
-      hl_argmax(L, key, idx);
-      const int i1 = idx;
-      const double* P1 = Pr + 3 * i1;
-      key = -INFINITY; idx = INT_MAX;
-      for (int q = tid; q < n; q += blockDim.x) {
-        const double e1[3] = {P1[0] - P0[0], P1[1] - P0[1], P1[2] - P0[2]};
-        const double e2[3] = {Pr[3 * q] - P0[0], Pr[3 * q + 1] - P0[1], Pr[3 * q + 2] - P0[2]};
-        const double cx = e1[1] * e2[2] - e1[2] * e2[1], cy = e1[2] * e2[0] - e1[0] * e2[2], cz = e1[0] * e2[1] - e1[1] * e2[0];
-        const double v = cx * cx + cy * cy + cz * cz;
-        if (v > key || (v == key && q < idx)) { key = v; idx = q; }
-      }
-      hl_argmax(L, key, idx);
-      const int i2 = idx;
-      if (tid == 0) {
-        for (int d = 0; d < 3; ++d) {
-          M.vx[0][d] = Pr[3 * i0 + d]; M.vx[1][d] = Pr[3 * i1 + d]; M.vx[2][d] = Pr[3 * i2 + d];
-        }
-        M.fv[0][0] = 0; M.fv[0][1] = 1; M.fv[0][2] = 2;
-      }
-      hl_bar();
-      key = -INFINITY; idx = INT_MAX;
-      for (int q = tid; q < n; q += blockDim.x) {
-        double dd;
-        hl_beyond(M, 0, Pr + 3 * q, eps2, &dd);
-        const double v = fabs(dd);
-        if (v > key || (v == key && q < idx)) { key = v; idx = q; }
-      }
-      hl_argmax(L, key, idx);
-      const int i3 = idx;
-      if (tid == 0) {
-        if (!(key > eps) || i0 == i1 || i1 == i2 || i2 == i3) L.fail = 8;
-        L.init[0] = i0; L.init[1] = i1; L.init[2] = i2; L.init[3] = i3;
-        if (!L.fail) {
-          for (int v = 0; v < 4; ++v) {
-            vpid[v] = L.init[v];
-            for (int d = 0; d < 3; ++d) M.vx[v][d] = Pr[3 * L.init[v] + d];
-          }
-          L.nvtx = 4;
-          const int fvv[4][3] = {{0, 1, 2}, {0, 3, 1}, {1, 3, 2}, {0, 2, 3}};
-          for (int f = 0; f < 4; ++f) {
-            for (int e = 0; e < 3; ++e) M.fv[f][e] = (unsigned short)fvv[f][e];
-            const int other = 6 - fvv[f][0] - fvv[f][1] - fvv[f][2];
-            double dd;
-            hl_beyond(M, f, M.vx[other], 0.0, &dd);
-            if (dd > 0) { const unsigned short t = M.fv[f][1]; M.fv[f][1] = M.fv[f][2]; M.fv[f][2] = t; }
-            M.alive[f] = 1;
-          }
-          for (int f = 0; f < 4; ++f)
-            for (int e = 0; e < 3; ++e) {
-              const int a = M.fv[f][e], b = M.fv[f][(e + 1) % 3];
-              for (int g = 0; g < 4; ++g)
-                for (int e2 = 0; e2 < 3; ++e2)
-                  if (M.fv[g][e2] == b && M.fv[g][(e2 + 1) % 3] == a) M.fa[f][e] = (unsigned short)g;
-            }
-          L.nf = 4;
-          L.nfree = 0;
-        }
+      hull_tetra(M, L, Pr, n, L.eps, eps2, vpid);
+      if (tid == 0 && !L.fail) {
+        for (int f = 0; f < 4; ++f) M.alive[f] = 1;
+        L.nvtx = 4;
+        L.nf = 4;
+        L.nfree = 0;
       }
       hl_bar();
     }
@@ -521,54 +1449,33 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
       // points and the initial hull and wait for the facet selection).
       if (wave == 0) {
       // 5. quickhull: take the oldest live face with outside points (FIFO
-      //    work queue: the hull grows evenly, which wastes fewer insertions
-      //    on points that later fall inside than depth-first order), insert
-      //    its furthest point.  One wave, and every insertion is a chain of
-      //    dependent LDS round trips, so the loop keeps its control state in
-      //    (wave-uniform) registers, passes lists between lanes with ballots,
-      //    readlane and DPP scans, and touches LDS only for the topology.
-      // The next queue entry's face, key and apex coordinates are fetched
-      // during the current insertion (three dependent global loads off the
-      // critical path).  They stay valid unless that face is retired (it is
-      // in the current region) or was dead when checked (its slot may be
-      // reused by a cone face of this insertion).
+      //    work queue), insert its furthest point.  The loop keeps its
+      //    control state in (wave-uniform) registers, passes lists between
+      //    lanes with ballots, readlane and DPP scans.
       int qh = 0, sp = L.sp, nvtx = L.nvtx, it = 0, nf = L.nf, nfree = L.nfree, sbtop = L.sbtop;
       int fail = 0;
       const unsigned long long lt = (1ull << tid) - 1ull;
-      int pf_idx = -1, pf_face = 0;
-      bool pf_ok = false;
-      unsigned long long pf_key = 0ull;
-      double pf_p[3] = {0.0, 0.0, 0.0};
       for (;;) {
         if (qh == sp) break;
-        const bool use_pf = pf_ok && pf_idx == qh;
-        const int f = use_pf ? pf_face : stk[qh];
+        const int f = stk[qh];
         ++qh;
         // stale entries: the face was retired (its slot maybe reused by a
         // face without outside points) after it was pushed
-        const unsigned long long key = use_pf ? pf_key : fbest[f];
-        pf_ok = false;
+        const unsigned long long key = fbest[f];
         if (!M.alive[f] || key == 0ull) continue;
         const int apex = (int)(~(unsigned)(key & 0xFFFFFFFFull));
         if (apex < 0 || apex >= n || it >= 4 * Mem::kVerts) { fail = 9; break; }
         if (nvtx >= Mem::kVerts) { fail = 1; break; }
         const int av = nvtx++;
         const unsigned short stamp = (unsigned short)(++it);
-        double p[3];
-        if (use_pf) { p[0] = pf_p[0]; p[1] = pf_p[1]; p[2] = pf_p[2]; }
-        else { p[0] = Pr[3 * apex]; p[1] = Pr[3 * apex + 1]; p[2] = Pr[3 * apex + 2]; }
-        pf_idx = qh < sp ? qh : -1;
-        if (pf_idx >= 0) pf_face = stk[pf_idx];
+        const double p[3] = {Pr[3 * apex], Pr[3 * apex + 1], Pr[3 * apex + 2]};
         if (tid == 0) {
           M.vx[av][0] = p[0]; M.vx[av][1] = p[1]; M.vx[av][2] = p[2];
           vpid[av] = apex;
           M.vst[f] = stamp;
         }
         hl_sync();
-        HSTAMP(2);
-        // (a) visible region: grown over adjacency from f; lanes 0..2 test
-        //     the three neighbours of one region face at a time.  Lane r
-        //     holds region face r (LDS copy for r >= 64 and for later phases).
+        // (a) visible region over adjacency from f
         int rg = tid == 0 ? f : -1;
         if (tid == 0) L.region[0] = (unsigned short)f;
         int R = 1;
@@ -584,7 +1491,6 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
             const int pos = R + __popcll(b & lt);
             if (pos < LT::kRegion) { L.region[pos] = (unsigned short)nb; M.vst[nb] = stamp; }
           }
-          // hand the new entries to lanes R, R+1, ...
           const int n0 = __builtin_amdgcn_readlane(nb, 0), n1 = __builtin_amdgcn_readlane(nb, 1),
                     n2 = __builtin_amdgcn_readlane(nb, 2);
           int k = R;
@@ -596,26 +1502,20 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
           hl_sync();
         }
         if (R > LT::kRegion) { fail = 2; break; }
-        if (pf_idx >= 0) {
-          pf_ok = M.alive[pf_face] && M.vst[pf_face] != stamp;
-          if (pf_ok) pf_key = fbest[pf_face];
-        }
-        HSTAMP(3);
-        // (b) horizon: region edges whose neighbour is not in the region,
-        //     in (region order, edge) order
+        // (b) horizon
         int nh = 0;
         for (int b0 = 0; b0 < 3 * R; b0 += 64) {
           const int t = b0 + tid;
-          int ha = 0, hb = 0, ho = 0, is = 0;
+          int ha = 0, hb2 = 0, ho = 0, is = 0;
           if (t < 3 * R) {
             const int g = L.region[t / 3], e = t % 3;
             ho = M.fa[g][e];
-            if (M.vst[ho] != stamp) { is = 1; ha = M.fv[g][e]; hb = M.fv[g][(e + 1) % 3]; }
+            if (M.vst[ho] != stamp) { is = 1; ha = M.fv[g][e]; hb2 = M.fv[g][(e + 1) % 3]; }
           }
           const unsigned long long b = __ballot(is);
           const int pos = nh + __popcll(b & lt);
           if (is && pos < LT::kHorizon) {
-            L.h_a[pos] = (unsigned short)ha; L.h_b[pos] = (unsigned short)hb; L.h_out[pos] = (unsigned short)ho;
+            L.h_a[pos] = (unsigned short)ha; L.h_b[pos] = (unsigned short)hb2; L.h_out[pos] = (unsigned short)ho;
           }
           nh += __popcll(b);
         }
@@ -630,26 +1530,24 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
           L.hcnt[h] = 0;
         }
         hl_sync();
-        HSTAMP(4);
         // (d) cone faces (a, b, apex): adjacency, outer neighbours, planes
         int bad = 0;
         for (int h = tid; h < nh; h += 64) {
           const int sf = L.h_new[h];
-          const int ha = L.h_a[h], hb = L.h_b[h], on = L.h_out[h];
-          const int k = M.vmap[hb];                    // edge leaving b
+          const int ha = L.h_a[h], hb2 = L.h_b[h], on = L.h_out[h];
+          const int k = M.vmap[hb2];                   // edge leaving b
           M.fv[sf][0] = (unsigned short)ha;
-          M.fv[sf][1] = (unsigned short)hb;
+          M.fv[sf][1] = (unsigned short)hb2;
           M.fv[sf][2] = (unsigned short)av;
           M.fa[sf][0] = (unsigned short)on;
           M.fa[sf][1] = L.h_new[k];                    // across (b, apex)
           M.fa[L.h_new[k]][2] = (unsigned short)sf;    // k's (apex, a_k = b)
           M.vst[sf] = 0;
           for (int e = 0; e < 3; ++e)
-            if (M.fv[on][e] == hb && M.fv[on][(e + 1) % 3] == ha) M.fa[on][e] = (unsigned short)sf;
-          if (L.h_a[k] != hb) bad = 1;
-          // plane of the new face, as hl_normal / hl_beyond compute it
+            if (M.fv[on][e] == hb2 && M.fv[on][(e + 1) % 3] == ha) M.fa[on][e] = (unsigned short)sf;
+          if (L.h_a[k] != hb2) bad = 1;
           const double* a = M.vx[ha];
-          const double* bb = M.vx[hb];
+          const double* bb = M.vx[hb2];
           const double e1[3] = {bb[0] - a[0], bb[1] - a[1], bb[2] - a[2]};
           const double e2[3] = {p[0] - a[0], p[1] - a[1], p[2] - a[2]};
           const double nx = e1[1] * e2[2] - e1[2] * e2[1];
@@ -664,164 +1562,79 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
           fbest[sf] = 0ull;
         }
         if (__ballot(bad)) { fail = 5; break; }
-        // retired faces' outside-set extents: lane r holds region face r's
-        // (r < 64; longer regions take the scratch path below)
-        int roff = 0, rcnt = 0;
-        if (tid < R) {
-          const int g = R <= 64 ? rg : (int)L.region[tid];
-          seg_get(M.seg[g], roff, rcnt);
+        // (e) the retired faces' outside points, through LDS + scratch
+        for (int r = tid; r < R; r += 64) {
+          int so, sc;
+          seg_get(M.seg[L.region[r]], so, sc);
+          L.roff[r] = so;
+          L.rcnt[r] = sc;
         }
-        const int rinc = wave_incl_scan(rcnt);          // prefix over region faces
-        const int total = R <= 64 ? __builtin_amdgcn_readlane(rinc, 63) : -1;
-        HSTAMP(5);
-        if (pf_ok) {
-          const int pa = (int)(~(unsigned)(pf_key & 0xFFFFFFFFull));
-          if (pa >= 0 && pa < n) { pf_p[0] = Pr[3 * pa]; pf_p[1] = Pr[3 * pa + 1]; pf_p[2] = Pr[3 * pa + 2]; }
+        hl_sync();
+        int run0 = 0;
+        for (int r0 = 0; r0 < R; r0 += 64) {
+          const int r = r0 + tid;
+          const int v = r < R ? L.rcnt[r] : 0;
+          const int x = wave_incl_scan(v);
+          if (r < R) L.rpre[r] = run0 + x - v;
+          run0 += __builtin_amdgcn_readlane(x, 63);
         }
-        HSUB(0);
-        // (e) the retired faces' outside points: first cone face they are beyond
-        if (total >= 0 && total <= 4 * 64) {
-          // up to four points per lane; each point's rank within its target
-          // cone face from an LDS atomic; no scratch round trip
-          int tg[4], rk[4];
-          HullPt pt[4];
-          float dv[4];
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            tg[c] = -1; rk[c] = 0; dv[c] = 0.0f; pt[c].q = -1;
-            const int t = c * 64 + tid;
-            if (c * 64 < total) {
-              // region face holding item t: the first r with rinc[r] > t
-              int lo = 0, base = 0, off0 = __builtin_amdgcn_readlane(roff, 0);
-              for (int r = 0; r < R - 1; ++r) {
-                const int inc = __builtin_amdgcn_readlane(rinc, r);
-                if (t >= inc) { lo = r + 1; base = inc; }
-              }
-              for (int r = 1; r < R; ++r) {
-                const int o = __builtin_amdgcn_readlane(roff, r);
-                if (r == lo) off0 = o;
-              }
-              if (t < total) pt[c] = sb[off0 + (t - base)];
+        if (tid == 0) L.rpre[R] = run0;
+        hl_sync();
+        const int tot2 = run0;
+        for (int t = tid; t < tot2; t += 64) {
+          int lo = 0, hi = R - 1;
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (L.rpre[mid] <= t) lo = mid; else hi = mid - 1;
+          }
+          const HullPt e = sb[L.roff[lo] + (t - L.rpre[lo])];
+          const int q = e.q;
+          int tgt = -1;
+          float dd = 0.0f;
+          if (q != apex) {
+            const double x0 = e.x, x1 = e.y, x2 = e.z;
+            for (int h = 0; h < nh; ++h) {
+              const double* cp = L.cn[h];
+              const double d = cp[0] * (x0 - cp[3]) + cp[1] * (x1 - cp[4]) + cp[2] * (x2 - cp[5]);
+              if (d > 0.0 && d * d > cp[7]) { tgt = h; dd = (float)(d * cp[6]); break; }
             }
           }
-          HSUB(1);
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const int q = pt[c].q;
-            if (q >= 0 && q != apex) {
-              const double x0 = pt[c].x, x1 = pt[c].y, x2 = pt[c].z;
-              for (int h = 0; h < nh; ++h) {
-                const double* cp = L.cn[h];
-                const double d = cp[0] * (x0 - cp[3]) + cp[1] * (x1 - cp[4]) + cp[2] * (x2 - cp[5]);
-                if (d > 0.0 && d * d > cp[7]) { tg[c] = h; dv[c] = (float)(d * cp[6]); break; }
-              }
-              if (tg[c] >= 0) rk[c] = atomicAdd(&L.hcnt[tg[c]], 1);
-            }
-          }
-          hl_sync();
-          HSUB(2);
-          int run = sbtop;
-          for (int h0 = 0; h0 < nh; h0 += 64) {
-            const int h = h0 + tid;
-            const int v = h < nh ? L.hcnt[h] : 0;
-            const int x = wave_incl_scan(v);
-            if (h < nh) {
-              L.hoff[h] = run + x - v;
-              seg_put(M.seg[L.h_new[h]], run + x - v, v);
-            }
-            run += __builtin_amdgcn_readlane(x, 63);
-          }
-          if (run > sbcap) { fail = 6; break; }
-          hl_sync();
-          HSUB(3);
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            if (tg[c] >= 0) {
-              sb[L.hoff[tg[c]] + rk[c]] = pt[c];
-              const unsigned long long k2 =
-                  ((unsigned long long)__float_as_uint(dv[c]) << 32) | (unsigned long long)(~(unsigned)pt[c].q);
-              atomicMax(&fbest[L.h_new[tg[c]]], k2);
-            }
-          }
-          HSUB(4);
-          sbtop = run;
-          HSUB(5);
-        } else {
-          // long regions / many points: through LDS + scratch
-          for (int r = tid; r < R; r += 64) {
-            int so, sc;
-            seg_get(M.seg[L.region[r]], so, sc);
-            L.roff[r] = so;
-            L.rcnt[r] = sc;
-          }
-          hl_sync();
-          int run0 = 0;
-          for (int r0 = 0; r0 < R; r0 += 64) {
-            const int r = r0 + tid;
-            const int v = r < R ? L.rcnt[r] : 0;
-            const int x = wave_incl_scan(v);
-            if (r < R) L.rpre[r] = run0 + x - v;
-            run0 += __builtin_amdgcn_readlane(x, 63);
-          }
-          if (tid == 0) L.rpre[R] = run0;
-          hl_sync();
-          const int tot2 = run0;
-          for (int t = tid; t < tot2; t += 64) {
-            int lo = 0, hi = R - 1;
-            while (lo < hi) {
-              const int mid = (lo + hi + 1) >> 1;
-              if (L.rpre[mid] <= t) lo = mid; else hi = mid - 1;
-            }
-            const HullPt e = sb[L.roff[lo] + (t - L.rpre[lo])];
-            const int q = e.q;
-            int tgt = -1;
-            float dd = 0.0f;
-            if (q != apex) {
-              const double x0 = e.x, x1 = e.y, x2 = e.z;
-              for (int h = 0; h < nh; ++h) {
-                const double* cp = L.cn[h];
-                const double d = cp[0] * (x0 - cp[3]) + cp[1] * (x1 - cp[4]) + cp[2] * (x2 - cp[5]);
-                if (d > 0.0 && d * d > cp[7]) { tgt = h; dd = (float)(d * cp[6]); break; }
-              }
-            }
-            tq[t] = q;
-            th[t] = tgt;
-            td[t] = dd;
-            if (tgt >= 0) atomicAdd(&L.hcnt[tgt], 1);
-          }
-          hl_sync();
-          int run = sbtop;
-          for (int h0 = 0; h0 < nh; h0 += 64) {
-            const int h = h0 + tid;
-            const int v = h < nh ? L.hcnt[h] : 0;
-            const int x = wave_incl_scan(v);
-            if (h < nh) {
-              seg_put(M.seg[L.h_new[h]], run + x - v, v);
-              L.hoff[h] = run + x - v;
-            }
-            run += __builtin_amdgcn_readlane(x, 63);
-          }
-          if (run > sbcap) { fail = 6; break; }
-          sbtop = run;
-          hl_sync();
-          for (int t = tid; t < tot2; t += 64) {
-            const int h = th[t];
-            if (h < 0) continue;
-            const int q = tq[t];
-            HullPt e;
-            e.x = Pr[3 * q]; e.y = Pr[3 * q + 1]; e.z = Pr[3 * q + 2]; e.q = q; e.pad = 0;
-            sb[atomicAdd(&L.hoff[h], 1)] = e;
-            const unsigned long long k2 =
-                ((unsigned long long)__float_as_uint(td[t]) << 32) | (unsigned long long)(~(unsigned)q);
-            atomicMax(&fbest[L.h_new[h]], k2);
-          }
+          tq[t] = q;
+          th[t] = tgt;
+          td[t] = dd;
+          if (tgt >= 0) atomicAdd(&L.hcnt[tgt], 1);
         }
-        HSTAMP(6);
+        hl_sync();
+        int run = sbtop;
+        for (int h0 = 0; h0 < nh; h0 += 64) {
+          const int h = h0 + tid;
+          const int v = h < nh ? L.hcnt[h] : 0;
+          const int x = wave_incl_scan(v);
+          if (h < nh) {
+            seg_put(M.seg[L.h_new[h]], run + x - v, v);
+            L.hoff[h] = run + x - v;
+          }
+          run += __builtin_amdgcn_readlane(x, 63);
+        }
+        if (run > sbcap) { fail = 6; break; }
+        sbtop = run;
+        hl_sync();
+        for (int t = tid; t < tot2; t += 64) {
+          const int h = th[t];
+          if (h < 0) continue;
+          const int q = tq[t];
+          HullPt e;
+          e.x = Pr[3 * q]; e.y = Pr[3 * q + 1]; e.z = Pr[3 * q + 2]; e.q = q; e.pad = 0;
+          sb[atomicAdd(&L.hoff[h], 1)] = e;
+          const unsigned long long k2 =
+              ((unsigned long long)__float_as_uint(td[t]) << 32) | (unsigned long long)(~(unsigned)q);
+          atomicMax(&fbest[L.h_new[h]], k2);
+        }
         // (f) retire the region, commit the cone, push the cone faces that
         //     have outside points (in horizon order)
         const int used = min(nh, nfree0);
         for (int r = tid; r < R; r += 64) {
-          const int g = R <= 64 ? rg : (int)L.region[r];
+          const int g = L.region[r];
           M.alive[g] = 0;
           M.freel[nfree0 - used + r] = (unsigned short)g;
         }
@@ -843,10 +1656,6 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
         nf = nf0 + (nh - used);
         sp += npush;
         hl_sync();
-        HSTAMP(7);
-#ifdef LQRO_HULL_PROFILE
-        if (tid == 0) { prof_acc[14] += 1; prof_acc[10] += (unsigned long long)R; prof_acc[11] += (unsigned long long)nh; prof_acc[12] += (unsigned long long)(total > 0 ? total : 0); }
-#endif
       }
       if (tid == 0) {
         L.nf = nf; L.nfree = nfree; L.nvtx = nvtx; L.sbtop = sbtop; L.sp = sp;
@@ -856,109 +1665,12 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
       hl_bar();
     }
     hl_bar();
-
     HSTAMP(8);
-    // 6. the reference's facet selection over all facets (canonical order)
-    double best = INFINITY;
-    int bt0 = INT_MAX, bt1 = INT_MAX, bt2 = INT_MAX, nfac = 0;
-    double bn[3] = {0, 0, 0};
-    if (!L.fail) {
-      for (int f = tid; f < L.nf; f += blockDim.x) {
-        if (!M.alive[f]) continue;
-        nfac++;
-        int t0 = vpid[M.fv[f][0]], t1 = vpid[M.fv[f][1]], t2 = vpid[M.fv[f][2]];
-        while (!(t0 < t1 && t0 < t2)) { const int a = t0; t0 = t1; t1 = t2; t2 = a; }
-        const double *a = Pr + 3 * t0, *b = Pr + 3 * t1, *c = Pr + 3 * t2;
-        const double e1[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
-        const double e2[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
-        double nv[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
-        const double len = sqrt(nv[0] * nv[0] + nv[1] * nv[1] + nv[2] * nv[2]);
-        nv[0] /= len; nv[1] /= len; nv[2] /= len;
-        const double* p0 = Pf + 3 * t0;
-        const double dd = fabs(nv[0] * (vrel[0] - p0[0]) + nv[1] * (vrel[1] - p0[1]) + nv[2] * (vrel[2] - p0[2]));
-        const int s1 = min(t1, t2), s2 = max(t1, t2);
-        const bool bt = dd < best || (dd == best && (t0 < bt0 || (t0 == bt0 && (s1 < bt1 || (s1 == bt1 && s2 < bt2)))));
-        if (bt) { best = dd; bt0 = t0; bt1 = s1; bt2 = s2; bn[0] = nv[0]; bn[1] = nv[1]; bn[2] = nv[2]; }
-      }
-    }
-    // block arg-min by (distance, triple): wave shuffles, then across waves
-    {
-      const int lane = tid & 63, wave = tid >> 6;
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) {
-        const double ob = __shfl_xor(best, off);
-        const int o0 = __shfl_xor(bt0, off), o1 = __shfl_xor(bt1, off), o2 = __shfl_xor(bt2, off);
-        const double on0 = __shfl_xor(bn[0], off), on1 = __shfl_xor(bn[1], off), on2 = __shfl_xor(bn[2], off);
-        nfac += __shfl_xor(nfac, off);
-        const bool bt = ob < best || (ob == best && (o0 < bt0 || (o0 == bt0 && (o1 < bt1 || (o1 == bt1 && o2 < bt2)))));
-        if (bt) { best = ob; bt0 = o0; bt1 = o1; bt2 = o2; bn[0] = on0; bn[1] = on1; bn[2] = on2; }
-      }
-      __shared__ double s_best[HULL_THREADS / 64], s_n[HULL_THREADS / 64][3];
-      __shared__ int s_t[HULL_THREADS / 64][3], s_cnt[HULL_THREADS / 64];
-      if (lane == 0) {
-        s_best[wave] = best; s_t[wave][0] = bt0; s_t[wave][1] = bt1; s_t[wave][2] = bt2;
-        s_n[wave][0] = bn[0]; s_n[wave][1] = bn[1]; s_n[wave][2] = bn[2]; s_cnt[wave] = nfac;
-      }
-      hl_bar();
-      if (tid == 0) {
-        int fo = 0, total = 0;
-        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
-          total += s_cnt[w];
-          const bool bt = s_best[w] < s_best[fo] ||
-                          (s_best[w] == s_best[fo] &&
-                           (s_t[w][0] < s_t[fo][0] || (s_t[w][0] == s_t[fo][0] &&
-                            (s_t[w][1] < s_t[fo][1] || (s_t[w][1] == s_t[fo][1] && s_t[w][2] < s_t[fo][2])))));
-          if (bt) fo = w;
-        }
-        const bool ok = !L.fail && total > 0 && s_t[fo][0] != INT_MAX;
-        // capacity overflow in the LDS variant: hand the pair to k_hull_big
-        const bool retry = !big && L.fail >= 1 && L.fail <= 4;
-#ifdef LQRO_HULL_PROFILE
-        if (A.prof) atomicAdd(&A.prof[16 + (L.fail & 15)], 1ull);
-#endif
-        if (retry) {
-          const int r = atomicAdd(A.rcount, 1);
-          if (r < A.cap) A.rqueue[r] = slot;
-        }
-        float* pl = A.planes + (size_t)slot * 8;
-        const double distance = s_best[fo];
-        const double nrm[3] = {s_n[fo][0], s_n[fo][1], s_n[fo][2]};
-        if (retry) {
-          // written by k_hull_big
-        } else if (ok) {
-          const double dh = distance * 0.5;                  // :1416
-          const double mult = 1.0;                           // :1213
-          pl[0] = (float)(xi[3] + mult * dh * nrm[0]);
-          pl[1] = (float)(xi[4] + mult * dh * nrm[1]);
-          pl[2] = (float)(xi[5] + mult * dh * nrm[2]);
-          pl[3] = (float)nrm[0]; pl[4] = (float)nrm[1]; pl[5] = (float)nrm[2];
-          pl[6] = __int_as_float(1);
-          atomicAdd(&A.stats[3], 1ull);
-        } else {
-          pl[6] = __int_as_float(0);                         // no usable plane
-          atomicAdd(&A.stats[4], 1ull);
-        }
-        if (A.recs && !retry) {
-          lqro_pair_record& rec = A.recs[slot];
-          rec.flags |= ok ? LQRO_REC_HULL : LQRO_REC_HULLFAIL;
-          rec.n_facets = ok ? total : -1;
-          if (ok) {
-            rec.facet[0] = s_t[fo][0]; rec.facet[1] = s_t[fo][1]; rec.facet[2] = s_t[fo][2];
-            rec.dist = distance;
-            for (int q = 0; q < 3; ++q) {
-              rec.normal[q] = nrm[q];
-              rec.plane_point[q] = pl[q];
-              rec.plane_normal[q] = pl[3 + q];
-            }
-          }
-        }
-      }
-      hl_bar();
-    }
+    hull_select(A, M, L, Pr, Pf, vpid, L.nf, [&](int f) { return M.alive[f] != 0; }, xi, vrel, slot, big);
     HSTAMP(9);
 #ifdef LQRO_HULL_PROFILE
-    if (tid == 0 && A.prof && job < 2048) {
-      const int pj = 32 + 2 * (big ? 2048 + job : job);
+    if (tid == 0 && A.prof && L.job < 2048) {
+      const int pj = 32 + 2 * (2048 + L.job);
       A.prof[pj] = __builtin_amdgcn_s_memtime() - job_t0;
       A.prof[pj + 1] = (unsigned long long)L.nvtx | ((unsigned long long)n << 20) |
                        ((unsigned long long)L.fail << 40) | ((unsigned long long)slot << 44);
@@ -967,16 +1679,15 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
   }
 #ifdef LQRO_HULL_PROFILE
   if (tid == 0 && A.prof)
-    for (int k = 0; k < 16; ++k) atomicAdd(&A.prof[k], prof_acc[k]);
-  if (tid == 0 && A.prof)
-    for (int k = 0; k < 6; ++k) atomicAdd(&A.prof[26 + k], prof_sub[k]);
+    for (int k = 0; k < 10; ++k) atomicAdd(&A.prof[k], prof_acc[k]);
 #endif
+  (void)wave;
 }
 
-__global__ void __launch_bounds__(HULL_THREADS) k_hull(HullArgs A) {
-  __shared__ HullLdsSmall L;
-  __shared__ HullMemSmall M;
-  hull_body(A, M, L, false);
+__global__ void __launch_bounds__(HULL_CTHREADS) k_hull(HullArgs A) {
+  __shared__ HullLdsC<HULL_CWAVES> L;
+  __shared__ HullMemC M;
+  hull_body_mw<HULL_CWAVES>(A, M, L);
 }
 
 __global__ void __launch_bounds__(HULL_THREADS) k_hull_big(HullArgs A) {

@@ -217,6 +217,7 @@ struct lqro_ctx {
   lqro_pair_record* d_recs;
   int *d_hq, *d_hcount, *d_hnext, *d_err, *d_rq;
   void* d_hbig;
+  HullWide* d_hwide;
   int hull_big_blocks;
   int n_cu;
   int side_cus;              // CUs running k_hull beside k_pair (LQRO_SIDE_HULL_CUS)
@@ -283,7 +284,7 @@ void lqro_destroy(lqro_ctx* c) {
   (void)hipSetDevice(c->cfg.device);
   void* ps[] = {c->d_R, c->d_TF, c->d_shash, c->d_T, c->d_NCF, c->d_S, c->d_x, c->d_vgoal, c->d_newv, c->d_A, c->d_B,
                 c->d_L, c->d_E, c->d_planes, c->d_lpscratch, c->d_lpcompact, c->d_recs, c->d_hq, c->d_hcount,
-                c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats, c->d_prof, c->d_rq, c->d_hbig, c->d_hfbest, c->d_hvpid, c->d_hstack};
+                c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats, c->d_prof, c->d_rq, c->d_hbig, c->d_hwide, c->d_hfbest, c->d_hvpid, c->d_hstack};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (int k = 0; k < 5; ++k)
@@ -333,7 +334,7 @@ static int ctx_alloc(lqro_ctx* c) {
   HIPCHK(hipMemset(c->d_prof, 0, sizeof(unsigned long long) * LQRO_PROF_WORDS));
   c->hull_blocks = 256;   // one 138 KB-LDS workgroup per CU, persistent over the queue
   HIPCHK(hipMalloc(&c->d_hscratch, sizeof(double) * 6 * H * NP * c->hull_blocks));
-  HIPCHK(hipMalloc(&c->d_hiscratch, sizeof(int) * 2 * H * NP * HULL_WAVES * c->hull_blocks));
+  HIPCHK(hipMalloc(&c->d_hiscratch, sizeof(int) * 2 * H * NP * HULL_SCR_WAVES * c->hull_blocks));
   HIPCHK(hipMalloc(&c->d_hfscratch, sizeof(float) * H * NP * HULL_WAVES * c->hull_blocks));
   HIPCHK(hipMalloc(&c->d_hfbest, sizeof(unsigned long long) * HULL_FB_STRIDE * (size_t)c->hull_blocks));
   HIPCHK(hipMalloc(&c->d_hvpid, sizeof(int) * HULL_VG_STRIDE * (size_t)c->hull_blocks));
@@ -341,6 +342,7 @@ static int ctx_alloc(lqro_ctx* c) {
   HIPCHK(hipMalloc(&c->d_hfaces, sizeof(HullPt) * HULL_SBMULT * H * NP * (size_t)c->hull_blocks));
   c->hull_big_blocks = 64;
   HIPCHK(hipMalloc(&c->d_hbig, sizeof(HullMemBig) * (size_t)c->hull_big_blocks));
+  HIPCHK(hipMalloc(&c->d_hwide, sizeof(HullWide) * HULL_CWAVES * (size_t)c->hull_blocks));
   return LQRO_OK;
 }
 
@@ -519,6 +521,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   Hh.vpid = c->d_hvpid; Hh.stack = c->d_hstack;
   Hh.rqueue = c->d_rq; Hh.rcount = c->d_hcount + 2; Hh.rnext = c->d_hcount + 3;
   Hh.bigmem = c->d_hbig;
+  Hh.wide = c->d_hwide;
   Hh.stats = c->d_stats;
   Hh.prof = c->d_prof;
   Hh.pair_done = P.pair_done;
@@ -529,7 +532,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   if (nwait > 0) {
     HIPCHK(hipEventRecord(c->xev[0], s));
     HIPCHK(hipStreamWaitEvent(c->side, c->xev[0], 0));
-    hipLaunchKernelGGL(k_hull, dim3(nwait), dim3(HULL_THREADS), 0, c->side, Hh);
+    hipLaunchKernelGGL(k_hull, dim3(nwait), dim3(HULL_CTHREADS), 0, c->side, Hh);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->xev[1], c->side));
   }
@@ -546,7 +549,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   Hh.wait_pairs = 0;
   Hh.big_main = lds_ok ? 0 : 1;
   if (lds_ok) {
-    hipLaunchKernelGGL(k_hull, dim3(c->hull_blocks - nwait), dim3(HULL_THREADS), 0, s, Hh);
+    hipLaunchKernelGGL(k_hull, dim3(c->hull_blocks - nwait), dim3(HULL_CTHREADS), 0, s, Hh);
     HIPCHK(hipGetLastError());
   }
   if (nwait > 0) HIPCHK(hipStreamWaitEvent(s, c->xev[1], 0));
