@@ -43,7 +43,9 @@ namespace lqro {
 
 #define HULL_WAVES 4             // k_hull_big: the points / initial hull / facet phases use 4 waves,
 #define HULL_THREADS (64 * HULL_WAVES)   // the insertions one
-#define HULL_CWAVES 4            // k_hull: waves, all of them inserting
+#ifndef HULL_CWAVES
+#define HULL_CWAVES 8            // k_hull: waves, all of them inserting
+#endif
 #define HULL_CTHREADS (64 * HULL_CWAVES)
 #define HULL_SCR_WAVES 8         // per-block integer scratch: 2*H*NP ints per wave
 
@@ -54,9 +56,6 @@ namespace lqro {
 
 #define HULL_QCAP 512            // k_hull: per-wave face queue (LDS ring)
 #define HULL_FLCAP 64            // k_hull: per-wave list of retired face slots
-#ifndef HULL_RETRIES
-#define HULL_RETRIES 4           // k_hull: retries of a face another wave holds before re-queueing it
-#endif
 
 // an outside-set entry: the point and its (rounded) coordinates, so that
 // re-distributing it needs one load
@@ -311,9 +310,16 @@ __device__ __forceinline__ int hl_scan(LT& L, int v, int* tot) {
       prof_last = t_;                                               \
     }                                                               \
   } while (0)
+#define WSTAMP(k)                                                   \
+  do {                                                              \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();     \
+    wacc[k] += t_ - wlast;                                          \
+    wlast = t_;                                                     \
+  } while (0)
 #else
 #define HSTAMP(k) do {} while (0)
 #define HSUB(k) do {} while (0)
+#define WSTAMP(k) do {} while (0)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -713,6 +719,15 @@ __device__ __noinline__ int hull_insert_wide(HullMemC& M, HullLdsC<NW>& L, HullW
   }
   if (__ballot(bad)) return 5;
   hl_sync();
+  // release the faces around the region, retire the region (see the fast path)
+  for (int h0 = 0; h0 < nh; h0 += 64) {
+    const int h = h0 + lane;
+    if (h < nh) atomicAnd(&M.own[WG.on[h]], ~LK);
+  }
+  for (int r0 = 0; r0 < R; r0 += 64) {
+    const int r = r0 + lane;
+    if (r < R) M.own[region(r0, r)] = HULL_DEAD;
+  }
   // the retired faces' outside points, one region face at a time:
   // first cone face beyond, rank and key by global atomics, to scratch
   int items = 0;
@@ -787,11 +802,7 @@ __device__ __noinline__ int hull_insert_wide(HullMemC& M, HullLdsC<NW>& L, HullW
   const int keep = nfree - used;
   for (int r0 = 0; r0 < R; r0 += 64) {
     const int r = r0 + lane;
-    if (r < R) {
-      const int g = region(r0, r);
-      M.own[g] = HULL_DEAD;
-      if (keep + r < HULL_FLCAP) W.freel[keep + r] = (unsigned short)g;
-    }
+    if (r < R && keep + r < HULL_FLCAP) W.freel[keep + r] = (unsigned short)region(r0, r);
   }
   nfree = min(keep + R, HULL_FLCAP);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -802,7 +813,6 @@ __device__ __noinline__ int hull_insert_wide(HullMemC& M, HullLdsC<NW>& L, HullW
     if (h < nh) {
       sf = WG.sf[h];
       atomicAnd(&M.own[sf], ~LK);
-      atomicAnd(&M.own[WG.on[h]], ~LK);
       is = WG.cnt[h] > 0;
     }
     const unsigned long long b = __ballot(is);
@@ -851,21 +861,75 @@ __device__ __forceinline__ void hull_insert_mw(HullMemC& M, HullLdsC<NW>& L, con
     }
     mytail = __builtin_amdgcn_readlane(mytail, 0);
   };
-  int pending = -1, retries = 0;    // a face to retry before taking a new one
+#ifdef LQRO_HULL_PROFILE
+  unsigned long long wacc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long wlast = __builtin_amdgcn_s_memtime();
+#endif
   unsigned maxr = 0;
+  unsigned long long n_held = 0;
+  // a batch of entries taken from the own queue at once (lanes 0..lbn-1)
+  int lb = -1, lbn = 0;
   for (;;) {
     if (hl_ld(&L.fail)) break;
-    // (a) a face: the one to retry, else own queue first, then the others'
-    //     (oldest entries)
-    int f = pending;
-    pending = -1;
-    if (f < 0) {
-      retries = 0;
-      if (lane == 0) {
-        for (int k = 0; k < NW && f < 0; ++k) f = hq_pop(L.wl[(w + k) % NW]);
-        if (f >= hl_ld(&L.nf)) { atomicMax(&L.fail, 9); f = -1; }
+    // (a) a face: from the local batch; refill it from the own queue (up to
+    //     8 entries, one CAS), else take one entry of another wave's queue
+    if (lbn == 0) {
+      for (int tries = 0; tries < 16; ++tries) {
+        int h = 0, t = 0;
+        if (lane == 0) {
+          h = hl_ld(&W.head);
+          hl_cfence();
+          t = hl_ld(&W.tail);
+        }
+        h = __builtin_amdgcn_readlane(h, 0);
+        t = __builtin_amdgcn_readlane(t, 0);
+        const int m = min(t - h, 8);
+        if (m <= 0) break;
+        int e = -1;
+        if (lane < m) e = __hip_atomic_load(&W.q[(h + lane) % HULL_QCAP], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        hl_cfence();
+        int ok = 0;
+        if (lane == 0) ok = atomicCAS(&W.head, h, h + m) == h;
+        if (__builtin_amdgcn_readlane(ok, 0)) { lb = e; lbn = m; break; }
       }
-      f = __builtin_amdgcn_readlane(f, 0);
+      if (lbn == 0) {
+        int e = -1;
+        if (lane == 0)
+          for (int k = 1; k < NW && e < 0; ++k) e = hq_pop(L.wl[(w + k) % NW]);
+        e = __builtin_amdgcn_readlane(e, 0);
+        if (e >= 0) { lb = lane == 0 ? e : -1; lbn = 1; }
+      }
+      if (lbn > 0) {
+        // drop retired faces and faces without outside points (a hint: the
+        // lock below decides)
+        int live = 0;
+        if (lane < lbn) {
+          if (lb >= hl_ld(&L.nf)) { atomicMax(&L.fail, 9); }
+          else {
+            const unsigned o = M.own[lb];
+            live = (o >> 24) != 0xFFu && (o & 0xFFFFu) != HULL_NOPT;
+          }
+        }
+        const unsigned long long b = __ballot(live);
+        const int nl = __popcll(b);
+        if (nl < lbn && lane == 0) atomicSub(&L.work, lbn - nl);
+        int nlb = -1, k = 0;
+        for (int j = 0; j < lbn; ++j)
+          if (b & (1ull << j)) {
+            const int v = __builtin_amdgcn_readlane(lb, j);
+            if (lane == k) nlb = v;
+            ++k;
+          }
+        lb = nlb;
+        lbn = nl;
+      }
+    }
+    WSTAMP(8);
+    int f = -1;
+    if (lbn > 0) {
+      f = __builtin_amdgcn_readlane(lb, 0);
+      lb = __shfl(lb, min(lane + 1, 63));
+      --lbn;
     }
     if (f < 0) {
       int done = 0;
@@ -873,25 +937,28 @@ __device__ __forceinline__ void hull_insert_mw(HullMemC& M, HullLdsC<NW>& L, con
       if (__builtin_amdgcn_readlane(done, 0)) break;
       if (++idle > (1 << 24)) { if (lane == 0) atomicMax(&L.fail, 9); break; }   // bounded wait
       __builtin_amdgcn_s_sleep(2);
+      WSTAMP(5);
       continue;
     }
     idle = 0;
-    // (b) lock it; skip retired slots and faces without outside points,
-    //     re-queue faces another wave holds
+    // (b) lock it.  Skip retired slots and faces without outside points.
+    //     A face in another wave's visible region is dropped (retired, or
+    //     re-queued by that wave if it backs off); one held around another
+    //     wave's region is re-queued.
     unsigned old = 0;
     if (lane == 0) old = atomicOr(&M.own[f], LK);
     old = (unsigned)__builtin_amdgcn_readlane((int)old, 0);
     if ((old & 0x00FF0000u) || (old >> 24) == 0xFFu || (old & 0xFFFFu) == HULL_NOPT) {
       if (lane == 0) atomicAnd(&M.own[f], ~LK);
-      if ((old & 0x00FF0000u) && (old >> 24) != 0xFFu) {
-        // held by another wave: retry it shortly, then queue it again
-        if (++retries <= HULL_RETRIES) pending = f;
-        else requeue(f);
+      if ((old & 0x00FF0000u) && (old >> 24) == 0u) {
+        ++n_held;
+        requeue(f);
         if (++n_stale > (1u << 22)) { if (lane == 0) atomicMax(&L.fail, 9); break; }
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(1);
       } else if (lane == 0) {
         atomicSub(&L.work, 1);
       }
+      WSTAMP(9);
       continue;
     }
     if (++attempts > 16 * kV) { if (lane == 0) atomicMax(&L.fail, 9); break; }
@@ -899,6 +966,9 @@ __device__ __forceinline__ void hull_insert_mw(HullMemC& M, HullLdsC<NW>& L, con
     if (apex >= n) { if (lane == 0) atomicMax(&L.fail, 9); break; }
     const double p[3] = {Pr[3 * apex], Pr[3 * apex + 1], Pr[3 * apex + 2]};
     if (lane == 0) atomicOr(&M.own[f], RB);
+    WSTAMP(0);
+    if (p[0] + p[1] + p[2] == 1e300) atomicAdd(&L.fail, 0);   // profiling: wait for the apex load
+    WSTAMP(10);
     // (c) visible region, grown over adjacency from f; lanes 0..2 lock and
     //     test the three neighbours of one region face at a time.  Lane r
     //     holds region face r.
@@ -947,22 +1017,38 @@ __device__ __forceinline__ void hull_insert_mw(HullMemC& M, HullLdsC<NW>& L, con
     n_big += R > 32;
     if (R > HULL_WIDE - 3) { if (lane == 0) atomicMax(&L.fail, 2); break; }
     if (conflict) {
-      // release the region and the faces around it, re-queue f
+      // release the region and the faces around it; re-queue the region's
+      // faces that have outside points (f with its unit of L.work, the
+      // others with a new one: a popper may have dropped their entries)
+      int nq = 0, full = 0;
       for (int r0 = 0; r0 < R; r0 += 64) {
         const int r = r0 + lane;
+        int g = -1, is = 0;
         if (r < R) {
-          const int g = r0 == 0 ? rg : WG.reg[r];
+          g = r0 == 0 ? rg : WG.reg[r];
           for (int e = 0; e < 3; ++e) atomicAnd(&M.own[M.fa[g][e]], ~(LK | RB));
-          atomicAnd(&M.own[g], ~(LK | RB));
+          const unsigned o = atomicAnd(&M.own[g], ~(LK | RB));
+          is = (o & 0xFFFFu) != HULL_NOPT;
         }
+        const unsigned long long b = __ballot(is);
+        if (mytail + nq + __popcll(b) - hl_ld(&W.head) > HULL_QCAP) { full = 1; break; }
+        if (is) W.q[(mytail + nq + __popcll(b & lt)) % HULL_QCAP] = (unsigned short)g;
+        nq += __popcll(b);
       }
+      if (full) { if (lane == 0) atomicMax(&L.fail, 4); break; }
+      mytail += nq;
       hl_sync();
-      if (++retries <= HULL_RETRIES) pending = f;
-      else requeue(f);
+      if (lane == 0) {
+        atomicAdd(&L.work, nq - 1);
+        hl_cfence();
+        hl_st(&W.tail, mytail);
+      }
       ++n_conf;
       __builtin_amdgcn_s_sleep(4);
+      WSTAMP(2);
       continue;
     }
+    WSTAMP(1);
     // (d) horizon: region edges whose neighbour is not in the region, in
     //     (region order, edge) order, staged through LDS into lanes
     int nh = 0;
@@ -990,6 +1076,7 @@ __device__ __forceinline__ void hull_insert_mw(HullMemC& M, HullLdsC<NW>& L, con
                                       nfree, mytail, LK, RB);
       if (rc) { if (lane == 0) atomicMax(&L.fail, rc); break; }
       ++n_ins;
+      WSTAMP(7);
       continue;
     }
     if (nh < 3) { if (lane == 0) atomicMax(&L.fail, 3); break; }
@@ -1046,6 +1133,14 @@ __device__ __forceinline__ void hull_insert_mw(HullMemC& M, HullLdsC<NW>& L, con
       W.hcnt[lane] = 0;
       W.kmax[lane] = 0ull;
     }
+    // the cone is linked: release the faces around the region and retire
+    // the region now (its outside sets stay readable: retired slots are
+    // reused only by this wave); the cone stays locked until its outside
+    // sets are written
+    hl_cfence();
+    if (hl) atomicAnd(&M.own[on], ~LK);
+    if (lane < R) M.own[rg] = HULL_DEAD;
+    WSTAMP(3);
     // (f) the retired faces' outside points: first cone face they are beyond
     int roff = 0, rcnt = 0;
     if (lane < R) seg_get(M.seg[rg], roff, rcnt);
@@ -1168,21 +1263,18 @@ __device__ __forceinline__ void hull_insert_mw(HullMemC& M, HullLdsC<NW>& L, con
         }
       }
     }
+    WSTAMP(4);
     const int cnt_mine = hl ? W.hcnt[lane] : 0;
     // (g) retire the region (slots to this wave's list), then, once this
     //     wave's global stores are done, release the cone and the faces
     //     around it and queue the cone faces that have outside points
-    if (lane < R) M.own[rg] = HULL_DEAD;
     {
       const int keep = nfree - used;
       if (lane < R && keep + lane < HULL_FLCAP) W.freel[keep + lane] = (unsigned short)rg;
       nfree = min(keep + R, HULL_FLCAP);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (hl) {
-      atomicAnd(&M.own[sf], ~LK);
-      atomicAnd(&M.own[on], ~LK);
-    }
+    if (hl) atomicAnd(&M.own[sf], ~LK);
     {
       const int is = hl && cnt_mine > 0;
       const unsigned long long b = __ballot(is);
@@ -1198,17 +1290,21 @@ __device__ __forceinline__ void hull_insert_mw(HullMemC& M, HullLdsC<NW>& L, con
       }
     }
     ++n_ins;
+    WSTAMP(6);
   }
 #ifdef LQRO_HULL_PROFILE
+  if (lane == 0 && pstat)
+    for (int k = 0; k < 12; ++k) atomicAdd(&pstat[32 + 2 * 4096 + 16 - 10 + k], wacc[k]);
   if (lane == 0 && pstat) {
     atomicAdd(&pstat[0], n_ins);
     atomicAdd(&pstat[1], n_conf);
     atomicAdd(&pstat[2], n_stale);
     atomicMax(&pstat[3], (unsigned long long)maxr);
     atomicAdd(&pstat[4], n_big);
+    atomicAdd(&pstat[32 + 2 * 4096 + 16 - 10 + 15], n_held);
   }
 #else
-  (void)n_ins; (void)n_conf; (void)n_stale; (void)pstat; (void)maxr; (void)n_big;
+  (void)n_ins; (void)n_conf; (void)n_stale; (void)pstat; (void)maxr; (void)n_big; (void)n_held;
 #endif
 }
 

@@ -34,7 +34,7 @@
 #include "lqro_pair.hpp"
 #include "lqro_hull.hpp"
 
-#define LQRO_PROF_WORDS (32 + 2 * 4096 + 16)   // hull: 32 counters + 2 words per job; pair: 16
+#define LQRO_PROF_WORDS (32 + 2 * 4096 + 16 + 16)   // hull: 32 counters + 2 words per job; pair: 16; hull wave phases: 16
 
 using namespace lqro;
 

@@ -17,11 +17,11 @@ c = lqro.Context(lqro.config(N, H, NP))
 c.set_gains(g["A"], g["B"], g["L"], g["E"])
 c.step(x, vg)
 print(c.timings(), c.stats())
-out = np.zeros(32 + 2 * 4096 + 16, np.uint64)
+out = np.zeros(32 + 2 * 4096 + 32, np.uint64)
 L.lqro_debug_hull_profile(c._h, out.ctypes.data_as(C.c_void_p))
 print(f"insertions {int(out[10])}  conflicts {int(out[11])}  stale {int(out[12])}")
 print('fail reasons (0=ok):', {k: int(out[16 + k]) for k in range(16) if out[16 + k]})
-jobs = out[32:].reshape(-1, 2)
+jobs = out[32:32 + 2 * 4096].reshape(-1, 2)
 for k, (cyc, w) in enumerate(jobs):
     if cyc:
         w = int(w)

@@ -13,15 +13,20 @@ c = lqro.Context(lqro.config(N, H, NP))
 c.set_gains(g["A"], g["B"], g["L"], g["E"])
 c.step(x, vg)
 print(c.timings(), c.stats())
-out = np.zeros(32 + 2 * 4096 + 16, np.uint64)
+out = np.zeros(32 + 2 * 4096 + 32, np.uint64)
 L.lqro_debug_hull_profile(c._h, out.ctypes.data_as(C.c_void_p))
 names = {0: "points", 1: "init", 6: "insertions", 8: "final-prep", 9: "final", 15: "job wait"}
 tot = sum(int(out[k]) for k in names)
 for k, nm in names.items():
     print(f"{nm:14s} {int(out[k]):14d}  {100 * int(out[k]) / max(tot, 1):5.1f}%")
-print(f"insertions {int(out[10])}  conflicts (backed off) {int(out[11])}  stale/held pops {int(out[12])}  max region {int(out[13])}  regions > 32: {int(out[14])}")
+print(f"insertions {int(out[10])}  conflicts (backed off) {int(out[11])}  stale/held pops {int(out[12])}  max region {int(out[13])}  regions > 32: {int(out[14])}  held pops {int(out[32 + 2 * 4096 + 31])}")
 print('fail reasons (0=ok):', {k: int(out[16 + k]) for k in range(16) if out[16 + k]})
-jobs = out[32:].reshape(-1, 2)
+wn = ["lock", "region", "conflict (wasted)", "horizon+cone", "reassign", "idle", "commit", "wide path", "refill", "held/dead", "apex load"]
+wv = out[32 + 2 * 4096 + 16: 32 + 2 * 4096 + 27].astype(float)
+print("wave time:", "  ".join(f"{a} {100 * b / max(wv.sum(), 1):.1f}%" for a, b in zip(wn, wv)))
+if out[10]:
+    print("wave cycles per insertion:", "  ".join(f"{a} {b / out[10]:.0f}" for a, b in zip(wn, wv)))
+jobs = out[32:32 + 2 * 4096].reshape(-1, 2)
 rows = []
 for k, (cyc, w) in enumerate(jobs):
     if cyc == 0:

@@ -5,7 +5,7 @@ import sys, os, ctypes as C, numpy as np
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path[:0] = [os.path.join(ROOT, "lqr-obstacles_amd"), os.path.join(ROOT, "oracle")]
 import lqro, pyoracle as po
-lqro.LIB_PATH = os.path.join(os.path.dirname(lqro.LIB_PATH), "liblqro_hprof.so")
+lqro.LIB_PATH = os.path.join(os.path.dirname(lqro.LIB_PATH), os.environ.get("LQRO_LIB", "liblqro_hprof.so"))
 L = lqro.lib()
 N, H, NP, K = (int(a) for a in sys.argv[1:5])
 kw = {}
@@ -20,7 +20,7 @@ inside = (rrecs["flags"] & 2) != 0
 print("inside pairs", int(inside.sum()), flush=True)
 c = lqro.Context(lqro.config(N, H, NP, flags=lqro.LQRO_FLAG_RECORDS))
 c.set_gains(g["A"], g["B"], g["L"], g["E"])
-prev = np.zeros(32 + 2 * 4096 + 16, np.uint64)
+prev = np.zeros(32 + 2 * 4096 + 32, np.uint64)
 bad_total = 0
 for t in range(K):
     c.step(x, vg)

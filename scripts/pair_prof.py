@@ -11,7 +11,7 @@ c = lqro.Context(lqro.config(N, H, NP))
 c.set_gains(g["A"], g["B"], g["L"], g["E"])
 c.step(x, vg)
 print(c.timings(), c.stats())
-out = np.zeros(32 + 2 * 4096 + 16, np.uint64)
+out = np.zeros(32 + 2 * 4096 + 32, np.uint64)
 L.lqro_debug_hull_profile(c._h, out.ctypes.data_as(C.c_void_p))
 pp = out[32 + 2 * 4096:]
 names = ["tables->LDS", "classify", "mixed", "nreach", "gjk", "write", "", "loop-top"]
