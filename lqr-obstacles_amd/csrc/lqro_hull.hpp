@@ -55,7 +55,7 @@ namespace lqro {
 #define HULL_VG_STRIDE 8192      // per-block vertex records in global scratch (= big vertices)
 
 #define HULL_QCAP 512            // k_hull: per-wave face queue (LDS ring)
-#define HULL_FLCAP 64            // k_hull: per-wave list of retired face slots
+#define HULL_FLCAP 256           // k_hull: per-wave list of retired face slots
 
 // an outside-set entry: the point and its (rounded) coordinates, so that
 // re-distributing it needs one load
@@ -512,7 +512,7 @@ __device__ __forceinline__ void hull_tetra(Mem& M, LT& L, const double* Pr, int 
 
 // 6. The reference's facet selection over all live faces f < nf (canonical
 // order, see the file comment), then the half-plane, the record, the stats.
-// A capacity failure of k_hull (fail 1-4) hands the pair to k_hull_big.
+// A capacity failure of k_hull (fail 1-4, 11) hands the pair to k_hull_big.
 template <class Mem, class LT, class Alive>
 __device__ __forceinline__ void hull_select(const HullArgs& A, const Mem& M, LT& L, const double* Pr,
                                             const double* Pf, const int* vpid, int nf, Alive alive,
@@ -570,7 +570,7 @@ __device__ __forceinline__ void hull_select(const HullArgs& A, const Mem& M, LT&
     }
     const bool ok = !L.fail && total > 0 && s_t[fo][0] != INT_MAX;
     // capacity overflow in the LDS variant: hand the pair to k_hull_big
-    const bool retry = !big && L.fail >= 1 && L.fail <= 4;
+    const bool retry = !big && ((L.fail >= 1 && L.fail <= 4) || L.fail == 11);
 #ifdef LQRO_HULL_PROFILE
     if (A.prof) atomicAdd(&A.prof[16 + (L.fail & 15)], 1ull);
 #endif
@@ -820,7 +820,7 @@ __device__ __noinline__ int hull_insert_wide(HullMemC& M, HullLdsC<NW>& L, HullW
     if (is) W.q[(mytail + np + __popcll(b & lt)) % HULL_QCAP] = (unsigned short)sf;
     np += __popcll(b);
   }
-  if (full) return 4;
+  if (full) return 11;
   mytail += np;
   hl_sync();
   if (lane == 0) {
@@ -852,7 +852,7 @@ __device__ __forceinline__ void hull_insert_mw(HullMemC& M, HullLdsC<NW>& L, con
   // re-queue face f (lane 0; the entry keeps its unit of L.work)
   auto requeue = [&](int f) {
     if (lane == 0) {
-      if (mytail - hl_ld(&W.head) >= HULL_QCAP) atomicMax(&L.fail, 4);
+      if (mytail - hl_ld(&W.head) >= HULL_QCAP) atomicMax(&L.fail, 11);
       else {
         W.q[mytail % HULL_QCAP] = (unsigned short)f;
         hl_cfence();
@@ -1035,7 +1035,7 @@ __device__ __forceinline__ void hull_insert_mw(HullMemC& M, HullLdsC<NW>& L, con
         if (is) W.q[(mytail + nq + __popcll(b & lt)) % HULL_QCAP] = (unsigned short)g;
         nq += __popcll(b);
       }
-      if (full) { if (lane == 0) atomicMax(&L.fail, 4); break; }
+      if (full) { if (lane == 0) atomicMax(&L.fail, 11); break; }
       mytail += nq;
       hl_sync();
       if (lane == 0) {
@@ -1279,7 +1279,7 @@ __device__ __forceinline__ void hull_insert_mw(HullMemC& M, HullLdsC<NW>& L, con
       const int is = hl && cnt_mine > 0;
       const unsigned long long b = __ballot(is);
       const int np = __popcll(b);
-      if (mytail + np - hl_ld(&W.head) > HULL_QCAP) { if (lane == 0) atomicMax(&L.fail, 4); break; }
+      if (mytail + np - hl_ld(&W.head) > HULL_QCAP) { if (lane == 0) atomicMax(&L.fail, 11); break; }
       if (is) W.q[(mytail + __popcll(b & lt)) % HULL_QCAP] = (unsigned short)sf;
       mytail += np;
       hl_sync();
