@@ -165,9 +165,19 @@ struct SliceSupport {
     if (better(lv, lq, bv, bq)) { bv = lv; bq = lq; }
   }
 
-  // support_simple semantics: lowest-index maximiser of p.d over the reachable set
+  // support_simple semantics: lowest-index maximiser of p.d over the reachable set.
+  // 1. an upper bound ub_k on every point value of each live slice;
+  // 2. the slice with the largest bound is evaluated exactly: its best value
+  //    bv is a lower bound on the answer;
+  // 3. every other slice with ub_k >= bv (the only ones that can hold a value
+  //    >= bv, ties included) is evaluated in one flattened pass, lanes over
+  //    (candidate, point), and one arg-max merges the lanes.
   __device__ void support(double d0, double d1, double d2, double& bv, int& bq) const {
-    const double dn = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+    // magnitudes below only scale the 1e-9 margins: the hardware square root
+    // (a few ulp) is ample there
+    const double dn = __builtin_amdgcn_sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+    double cu = -INFINITY;
+    int ck = INT_MAX;
     for (int k = lane; k < P.H; k += 64) {
       double ub = -INFINITY;
       if (W.cls[k] != kSliceOut) {
@@ -179,28 +189,49 @@ struct SliceSupport {
         // c_k.d = (T_k tr_k).d = tr_k.(T_k^T d); the reassociation error is
         // ~1e-16 |tr| ||T|| |d|, far inside the 1e-9 dn sc margin
         const double* tk = W.tr + 3 * k;
-        ub = tk[0] * w0 + tk[1] * w1 + tk[2] * w2 + sqrt(a0 * a0 + a1 * a1 + a2 * a2) * P.umax +
-             1e-9 * dn * W.sc[k];
+        ub = tk[0] * w0 + tk[1] * w1 + tk[2] * w2 +
+             __builtin_amdgcn_sqrt(a0 * a0 + a1 * a1 + a2 * a2) * P.umax + 1e-9 * dn * W.sc[k];
+        if (ub > cu) { cu = ub; ck = k; }
       }
       W.ub[k] = ub;
     }
-    wave_lds_sync();
+    wave_argmax(cu, ck);
     bv = -INFINITY;
     bq = INT_MAX;
-    for (;;) {
-      // next slice: largest bound among those that may still hold a value >= bv
-      double cu = -INFINITY;
-      int ck = INT_MAX;
-      for (int k = lane; k < P.H; k += 64) {
-        const double u = W.ub[k];
-        if (u > -INFINITY && u >= bv && (u > cu || (u == cu && k < ck))) { cu = u; ck = k; }
-      }
-      wave_argmax(cu, ck);
-      if (ck == INT_MAX) break;
-      eval_slice(ck, d0, d1, d2, bv, bq);
-      if (lane == 0) W.ub[ck] = -INFINITY;
-      wave_lds_sync();
+    if (ck == INT_MAX) return;
+    eval_slice(ck, d0, d1, d2, bv, bq);
+    // candidates: the other slices whose bound reaches bv
+    wave_lds_sync();   // the previous query's readers of W.mixed are done
+    int ncand = 0;
+    for (int base = 0; base < P.H; base += 64) {
+      const int k = base + lane;
+      const bool m = k < P.H && k != ck && W.ub[k] > -INFINITY && W.ub[k] >= bv;
+      const unsigned long long bal = __ballot(m);
+      if (m) W.mixed[ncand + __popcll(bal & ((1ull << lane) - 1ull))] = k;
+      ncand += __popcll(bal);
     }
+    if (ncand == 0) return;
+    wave_lds_sync();
+    double lv = -INFINITY;
+    int lq = INT_MAX;
+    // lane walks (c, p) = divmod(idx, NP) for idx = lane, lane+64, ...
+    int c = 0, p = lane;
+    while (p >= P.NP) { p -= P.NP; ++c; }
+    while (c < ncand) {
+      const int k = W.mixed[c];
+      const unsigned long long bits = W.mask[k * P.PW + (p >> 6)];
+      if ((bits >> (p & 63)) & 1ull) {
+        double x[3];
+        exact_point(B, W, P.NP, k, p, x);
+        const double v = x[0] * d0 + x[1] * d1 + x[2] * d2;   // SUPPORT_DOT_PRODUCT
+        const int q = k * P.NP + p;
+        if (better(v, q, lv, lq)) { lv = v; lq = q; }
+      }
+      p += 64;
+      while (p >= P.NP) { p -= P.NP; ++c; }
+    }
+    wave_argmax(lv, lq);
+    if (better(lv, lq, bv, bq)) { bv = lv; bq = lq; }
   }
 };
 
@@ -316,6 +347,8 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
     for (int c = 0; c < X; ++c) d[c] = xi[c] - xj[c];                       // (xInit1-xInit2)
     const double vrel[3] = {xi[3] - xj[3], xi[4] - xj[4], xi[5] - xj[5]};    // :794-796
     unsigned long long hsh = 0;
+    const bool want_hash = P.recs != nullptr;
+    const double vabs = fabs(vrel[0]) + fabs(vrel[1]) + fabs(vrel[2]);
     PSTAMP(7);
 
     // 1. per slice: Translate (exact), centre, class       (lanes <-> k)
@@ -334,12 +367,14 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
       const double c1 = Tk[3] * t0 + Tk[4] * t1 + Tk[5] * t2;
       const double c2 = Tk[6] * t0 + Tk[7] * t1 + Tk[8] * t2;
       const double Rk = B.R[k];
-      const double sc = sqrt(c0 * c0 + c1 * c1 + c2 * c2) + Rk +
-                        B.TF[k] * sqrt(t0 * t0 + t1 * t1 + t2 * t2) + 1.0;
+      // magnitudes for the 1e-9 relative margins: the hardware square root
+      // (error a few ulp) suffices; |vrel| covers dc's own rounding
+      const double sc = __builtin_amdgcn_sqrt(c0 * c0 + c1 * c1 + c2 * c2) + Rk +
+                        B.TF[k] * __builtin_amdgcn_sqrt(t0 * t0 + t1 * t1 + t2 * t2) + 1.0;
       W.sc[k] = sc;
       const double e0 = c0 - vrel[0], e1 = c1 - vrel[1], e2 = c2 - vrel[2];
-      const double dc = sqrt(e0 * e0 + e1 * e1 + e2 * e2);
-      const double slack = 1e-9 * sc;
+      const double dc = __builtin_amdgcn_sqrt(e0 * e0 + e1 * e1 + e2 * e2);
+      const double slack = 1e-9 * (sc + vabs);
       int cls = kSliceMixed;
       if (dc + Rk < P.vmax - slack) cls = kSliceIn;
       else if (dc - Rk > P.vmax + slack) cls = kSliceOut;
@@ -380,7 +415,7 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
           ok = reach_exact(x[0] - vrel[0], x[1] - vrel[1], x[2] - vrel[2], P);
         }
         const unsigned long long bal = __ballot(ok);
-        if (ok) hsh += mix64((uint64_t)(k * NP + p));
+        if (ok && want_hash) hsh += mix64((uint64_t)(k * NP + p));   // records only
         if (lane == 0) W.mask[k * P.PW + pw] = bal;
         cnt += __popcll(bal);
       }
