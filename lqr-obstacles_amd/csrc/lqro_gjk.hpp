@@ -14,6 +14,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "lqro_device.hpp"
+
 namespace lqro {
 
 struct GjkTab {
@@ -258,6 +260,251 @@ __device__ void gjk_run(Sup& sup, int qfirst, int n, const double* vrel, GjkStat
           for (int d = 0; d < 3; d++) g.c2[k][d] = f[d];
         }
       g.npts++;
+      oldsqrd = sqrd;
+      first_iteration = 0;
+      use_default = 1;
+      continue;
+    }
+    if (use_default) use_default = 0;
+    else { o.sqrd = sqrd; return; }
+  }
+  o.sqrd = 0.0;
+}
+
+
+// ---------------------------------------------------------------------------
+// Wave-parallel Johnson sub-algorithm (what k_pair runs).
+//
+// The same arithmetic as gjk_subterms/gjk_default/gjk_backup/gjk_reset above,
+// element by element and in the same order, but spread over the wave instead
+// of repeated in every lane: lane L = 4 s + j holds delta_values[s][elts[s][j]]
+// (subset s, its j-th element) and delta[s]; the subsets of one cardinality
+// are computed together (cardinality 2, then 3 reading 2, then 4 reading 3),
+// the first acceptable subset is found with a ballot.  The simplex (coords2,
+// lambdas, point ids) lives in a 20-word per-wave LDS block, so the
+// per-lane register state is two doubles.
+//
+// Subset s is the bit set of its elements: elts[s] are its set bits in
+// increasing order, pred[s][j] = s without elts[s][j], maxe[s] its highest
+// bit, succ[s][k] = s with its k-th missing element added (gjk.cpp:86-160).
+
+struct GjkWave {
+  double* c2;   // [4][3] coords2 of the simplex (LDS)
+  double* lam;  // [4] lambdas (LDS)
+  int* s2;      // [4] point ids (LDS)
+};
+
+__device__ __forceinline__ int gjk_nth_bit(int m, int n) {
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+    if ((m >> b) & 1) {
+      if (n == 0) return b;
+      --n;
+    }
+  return 0;
+}
+
+__device__ __forceinline__ double gjk_shfl(double v, int src) { return __shfl(v, src, 64); }
+
+// dot_products[a][b] (gjk.cpp:541-548): csp_a . csp_b, csp = coords1 - coords2;
+// symmetric exactly (each product commutes, same summation order)
+__device__ __forceinline__ double gjk_dp(const GjkWave& G, const double* vrel, int a, int b) {
+  const double* ca = G.c2 + 3 * a;
+  const double* cb = G.c2 + 3 * b;
+  const double a0 = vrel[0] - ca[0], a1 = vrel[1] - ca[1], a2 = vrel[2] - ca[2];
+  const double b0 = vrel[0] - cb[0], b1 = vrel[1] - cb[1], b2 = vrel[2] - cb[2];
+  return a0 * b0 + a1 * b1 + a2 * b2;
+}
+
+// compute_subterms (gjk.cpp:527-581) into this lane's dv
+__device__ __forceinline__ void gjkw_subterms(const GjkWave& G, const double* vrel, int size,
+                                              int lane, double& dv) {
+  const int s = lane >> 2, j = lane & 3;
+  const int card = __popc(s);
+  const bool live = s >= 1 && j < card && (s >> size) == 0;   // maxe[s] < size
+  const int e = gjk_nth_bit(s, j);
+  if (live && card == 1) dv = 1.0;
+  if (live && card == 2) {
+    const int e0 = gjk_nth_bit(s, 0), e1 = gjk_nth_bit(s, 1);
+    dv = j == 0 ? gjk_dp(G, vrel, e1, e1) - gjk_dp(G, vrel, e1, e0)
+                : gjk_dp(G, vrel, e0, e0) - gjk_dp(G, vrel, e0, e1);
+  }
+#pragma unroll
+  for (int c = 3; c <= 4; ++c) {
+    if (size < c) break;
+    const int jsub = s & ~(1 << e);
+    const int f0 = gjk_nth_bit(jsub, 0);
+    double sum = 0;
+#pragma unroll
+    for (int i = 0; i < c - 1; ++i) {
+      const int ielt = gjk_nth_bit(jsub, i);
+      const double dsub = gjk_shfl(dv, 4 * jsub + i);   // delta_values[jsub][ielt]
+      sum += dsub * (gjk_dp(G, vrel, ielt, f0) - gjk_dp(G, vrel, ielt, e));
+    }
+    if (live && card == c) dv = sum;
+  }
+}
+
+// reset_simplex (gjk.cpp:708-736) for a wave-uniform subset; returns the new size
+__device__ __forceinline__ int gjkw_reset(const GjkWave& G, int subset, double dv, double dsum,
+                                          int lane) {
+  const int card = __popc(subset);
+  const double ds = gjk_shfl(dsum, 4 * subset);
+  const double lv = gjk_shfl(dv, 4 * subset + (lane & 3));
+  // lanes 0..11 move coords2, lanes 0..3 the ids and lambdas
+  double cv = 0.0;
+  int sv = 0;
+  const int jj = lane / 3, d = lane - 3 * jj;
+  if (lane < 3 * card) cv = G.c2[3 * gjk_nth_bit(subset, jj) + d];
+  if (lane < card) sv = G.s2[gjk_nth_bit(subset, lane)];
+  wave_lds_sync();
+  if (lane < 3 * card) G.c2[lane] = cv;
+  if (lane < card) {
+    G.s2[lane] = sv;
+    G.lam[lane] = lv / ds;
+  }
+  wave_lds_sync();
+  return card;
+}
+
+// default_distance (gjk.cpp:593-657): 1 and the new size through *size, or 0
+__device__ __forceinline__ int gjkw_default(const GjkWave& G, int& size, double dv, double& dsum,
+                                            int lane) {
+  const int s = lane >> 2;
+  const int card = __popc(s);
+  const bool valid = s >= 1 && (s >> size) == 0;
+  int ok = 1;
+  double ds = 0.0;
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    const double v = gjk_shfl(dv, 4 * s + jj);
+    if (jj < card && ok) {
+      if (v > 0.0) ds += v;
+      else ok = 0;
+    }
+  }
+  int nk = 0;   // k-th element missing from s, below size
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const bool cand = ((s >> b) & 1) == 0 && b < size;
+    const int sc = s | (1 << b);
+    const int pos = __popc(sc & ((1 << b) - 1));
+    const double v = gjk_shfl(dv, 4 * (sc & 15) + pos);   // delta_values[succ][nonelt]
+    if (cand) {
+      if (ok && v > 0) ok = 0;
+      ++nk;
+    }
+  }
+  const bool found = valid && ok && ds >= 1.0e-20;
+  const unsigned long long bal = __ballot(found && (lane & 3) == 0);
+  int sel;
+  if (bal) {
+    sel = (__ffsll((long long)bal) - 1) >> 2;
+    if (valid && s <= sel) dsum = ds;
+  } else {
+    if (valid) dsum = ds;
+    // the loop ran out: reset_simplex(s) with the terminating s when the
+    // last subset tested was ok (it had a tiny delta sum)
+    const int last = (1 << size) - 1;
+    const int okl = __shfl(ok, 4 * last, 64);
+    if (!(okl && size < 4)) return 0;
+    sel = 1 << size;
+  }
+  size = gjkw_reset(G, sel, dv, dsum, lane);
+  return 1;
+}
+
+// backup_distance (gjk.cpp:663-706)
+__device__ __forceinline__ int gjkw_backup(const GjkWave& G, const double* vrel, int size, double dv,
+                                           double dsum, int lane) {
+  const int s = lane >> 2;
+  const int card = __popc(s);
+  const bool valid = s >= 1 && (s >> size) == 0;
+  double v[4];
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) v[jj] = gjk_shfl(dv, 4 * s + jj);
+  bool viable = valid && dsum > 0.0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (i < card && v[i] <= 0.0) viable = false;
+  double num = 0.0;
+  if (viable) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+        if (jj < card && kk < card)
+          num += (v[jj] * v[kk]) *
+                 gjk_dp(G, vrel, gjk_nth_bit(s, jj), gjk_nth_bit(s, kk));
+  }
+  const double den = dsum * dsum;
+  const unsigned long long vb = __ballot(viable && (lane & 3) == 0);
+  int bests = 0;
+  double bnum = 0.0, bden = 0.0;
+  for (int t = 1; t < 16; ++t) {
+    if (!((vb >> (4 * t)) & 1ull)) continue;
+    const double tn = gjk_shfl(num, 4 * t), td = gjk_shfl(den, 4 * t);
+    if ((bests < 1) || (tn * bden < bnum * td)) { bests = t; bnum = tn; bden = td; }
+  }
+  return gjkw_reset(G, bests, dv, dsum, lane);
+}
+
+// gjk_run with the wave-parallel sub-algorithm.  Sup as for gjk_run.
+template <class Sup>
+__device__ void gjkw_run(Sup& sup, const GjkWave& G, int lane, int qfirst, int n,
+                         const double* vrel, int& npts, GjkOut& o) {
+  double dv = 0.0, dsum = 0.0;            // delta_values / delta (zeroed per call)
+  int use_default = 1, first_iteration = 1, max_iterations = n;
+  double oldsqrd = 0.0, sqrd = 0.0;
+  o.iters = 0; o.backup = 0;
+  {
+    double f[3];
+    sup.point(qfirst, f);
+    if (lane < 3) G.c2[lane] = f[lane == 0 ? 0 : (lane == 1 ? 1 : 2)];
+    if (lane == 0) { G.s2[0] = qfirst; G.lam[0] = 1.0; }
+    wave_lds_sync();
+  }
+  npts = 1;
+  while (max_iterations-- > 0) {
+    if (npts == 1) {
+      if (lane == 0) G.lam[0] = 1.0;
+      wave_lds_sync();
+    } else {
+      gjkw_subterms(G, vrel, npts, lane, dv);
+      if (use_default) use_default = gjkw_default(G, npts, dv, dsum, lane);
+      if (!use_default) { npts = gjkw_backup(G, vrel, npts, dv, dsum, lane); o.backup = 1; }
+    }
+    // compute_point (gjk.cpp:851-862)
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      double a = 0, b = 0;
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        if (i < npts) { a += vrel[d] * G.lam[i]; b += G.c2[3 * i + d] * G.lam[i]; }
+      o.w1[d] = a;
+      o.w2[d] = b;
+    }
+    double disp[3], rdisp[3];
+#pragma unroll
+    for (int d = 0; d < 3; d++) { disp[d] = o.w2[d] - o.w1[d]; rdisp[d] = -disp[d]; }
+    sqrd = disp[0] * disp[0] + disp[1] * disp[1] + disp[2] * disp[2];
+    if (sqrd < 1.0e-8) { o.sqrd = sqrd; return; }
+    const double maxv = vrel[0] * disp[0] + vrel[1] * disp[1] + vrel[2] * disp[2];
+    double minus_minv;
+    int minq;
+    sup.support(rdisp[0], rdisp[1], rdisp[2], minus_minv, minq);
+    o.iters++;
+    double g_val = sqrd + maxv + minus_minv;
+    if (g_val < 0.0) g_val = 0;
+    if (g_val < 1.0e-8) { o.sqrd = sqrd; return; }
+    if ((first_iteration || (sqrd < oldsqrd)) && (npts <= 3)) {
+      double f[3];
+      sup.point(minq, f);
+      wave_lds_sync();   // every lane has read the old simplex
+      if (lane < 3) G.c2[3 * npts + lane] = f[lane == 0 ? 0 : (lane == 1 ? 1 : 2)];
+      if (lane == 0) { G.s2[npts] = minq; G.lam[npts] = 0.0; }
+      wave_lds_sync();
+      npts++;
       oldsqrd = sqrd;
       first_iteration = 0;
       use_default = 1;

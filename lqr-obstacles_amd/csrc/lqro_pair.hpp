@@ -33,8 +33,8 @@ namespace lqro {
 enum : int { kSliceOut = 0, kSliceIn = 1, kSliceMixed = 2 };
 constexpr int kMaxPW = 4;
 #ifndef LQRO_PAIR_LB
-#define LQRO_PAIR_LB 512
-#endif  // NP <= 256 (one 64-bit reachable mask per 64 points)
+#define LQRO_PAIR_LB 768
+#endif  // 12 waves (3 per SIMD: <= 168 VGPRs); NP <= 256 (one 64-bit reachable mask per 64 points)
 
 struct PairArgs {
   int N, H, NP, PW, min_reach;
@@ -81,6 +81,7 @@ struct WaveTabs {
   int* cnt;                  // H: reachable points in the slice
   int* mixed;                // H: list of MIXED slices
   unsigned long long* mask;  // H x PW
+  GjkWave gjk;               // the GJK simplex (18 doubles)
 };
 
 // Transform*(points[p] + Translate) (LQRO:776); Matrix::operator* accumulates
@@ -140,6 +141,9 @@ struct SliceSupport {
   const BlockTabs& B;
   const WaveTabs& W;
   int lane;
+#ifdef LQRO_PAIR_PROFILE
+  unsigned long long* pc;   // [0] support cycles, [1] calls, [2] candidate slices
+#endif
 
   __device__ void point(int q, double* x) const {
     const int k = q / P.NP;
@@ -173,6 +177,14 @@ struct SliceSupport {
   //    >= bv, ties included) is evaluated in one flattened pass, lanes over
   //    (candidate, point), and one arg-max merges the lanes.
   __device__ void support(double d0, double d1, double d2, double& bv, int& bq) const {
+#ifdef LQRO_PAIR_PROFILE
+    const unsigned long long t0_ = __builtin_amdgcn_s_memtime();
+    pc[1] += 1;
+    support_(d0, d1, d2, bv, bq);
+    pc[0] += __builtin_amdgcn_s_memtime() - t0_;
+  }
+  __device__ void support_(double d0, double d1, double d2, double& bv, int& bq) const {
+#endif
     // magnitudes below only scale the 1e-9 margins: the hardware square root
     // (a few ulp) is ample there
     const double dn = __builtin_amdgcn_sqrt(d0 * d0 + d1 * d1 + d2 * d2);
@@ -210,6 +222,9 @@ struct SliceSupport {
       if (m) W.mixed[ncand + __popcll(bal & ((1ull << lane) - 1ull))] = k;
       ncand += __popcll(bal);
     }
+#ifdef LQRO_PAIR_PROFILE
+    pc[2] += ncand;
+#endif
     if (ncand == 0) return;
     wave_lds_sync();
     double lv = -INFINITY;
@@ -292,10 +307,18 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
     int* wi = reinterpret_cast<int*>(w);
     W.cls = wi;          wi += H;
     W.cnt = wi;          wi += H;
-    W.mixed = wi;
+    W.mixed = wi;        wi += H + (H & 1);
+    W.gjk.c2 = reinterpret_cast<double*>(wi);
+    W.gjk.lam = W.gjk.c2 + 12;
+    W.gjk.s2 = reinterpret_cast<int*>(W.gjk.c2 + 16);
   }
   unsigned long long st_reach = 0, st_iters = 0, st_planes = 0, st_inside = 0, st_backup = 0;
+#ifdef LQRO_PAIR_PROFILE
+  unsigned long long pc[3] = {0, 0, 0};
+  SliceSupport sup{P, B, W, lane, pc};
+#else
   SliceSupport sup{P, B, W, lane};
+#endif
 
   // Persistent: the workgroup takes whole rows (agent i) off a queue; its
   // waves take the row's pairs one at a time (LDS counter), so uneven pair
@@ -456,11 +479,10 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
     GjkOut go;
     go.iters = 0; go.backup = 0; go.sqrd = 0;
     for (int q = 0; q < 3; ++q) { go.w1[q] = 0; go.w2[q] = 0; }
-    GjkState g;
-    g.npts = 0;
+    int npts = 0;
     bool inside = false;
     if (n > P.min_reach) {                                    // :1409
-      gjk_run(sup, qfirst, n, vrel, g, go);
+      gjkw_run(sup, W.gjk, lane, qfirst, n, vrel, npts, go);
       double distance = sqrt(go.sqrd);                          // :843
       nrm[0] = (go.w1[0] - go.w2[0]) / distance;                // :850-852
       nrm[1] = (go.w1[1] - go.w2[1]) / distance;
@@ -487,9 +509,9 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
     PSTAMP(4);
     const size_t slot = (size_t)lrow * P.npr + jj;
     int sranks[4] = {-1, -1, -1, -1};
-    if (P.recs != nullptr && g.npts > 0)
+    if (P.recs != nullptr && npts > 0)
       for (int s = 0; s < 4; ++s)
-        if (s < g.npts) sranks[s] = reach_rank(P, W, lane, g.s2[s]);
+        if (s < npts) sranks[s] = reach_rank(P, W, lane, W.gjk.s2[s]);
     if (lane == 0) {
       float4* dst = reinterpret_cast<float4*>(P.planes + slot * 8);
       dst[0] = make_float4(pl[0], pl[1], pl[2], pl[3]);
@@ -503,7 +525,7 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
       if (P.recs != nullptr) {
         lqro_pair_record rec;
         rec.i = i; rec.j = j; rec.n_reach = n; rec.flags = flags;
-        rec.gjk_iters = go.iters; rec.simplex_n = g.npts;
+        rec.gjk_iters = go.iters; rec.simplex_n = npts;
         for (int s = 0; s < 4; ++s) rec.simplex[s] = sranks[s];
         rec.facet[0] = rec.facet[1] = rec.facet[2] = -1;
         rec.n_facets = 0;
@@ -523,6 +545,7 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
     PSTAMP(5);
 #ifdef LQRO_PAIR_PROFILE
     pp[11] += 1;
+    pp[12] = pc[0]; pp[13] = pc[1]; pp[14] = pc[2];
 #endif
   }
     __syncthreads();   // the row is done before s_row / the tables change

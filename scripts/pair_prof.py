@@ -21,5 +21,7 @@ for k in range(8):
         print(f"{names[k]:12s} {int(pp[k]):14d} {100 * pp[k] / tot:5.1f}%")
 pairs = int(pp[11])
 print("pairs", pairs, "mixed slices/pair %.2f" % (pp[10] / max(pairs, 1)),
-      "slice evals/pair %.2f" % (pp[12] / max(pairs, 1)),
+      "supports/pair %.2f" % (pp[13] / max(pairs, 1)),
+      "support cycles/pair %.0f (%.1f%% of gjk)" % (pp[12] / max(pairs, 1), 100 * pp[12] / max(pp[4], 1)),
+      "candidates/support %.2f" % (pp[14] / max(pp[13], 1)),
       "cycles/pair/wave %.0f" % (tot / max(pairs, 1)))

@@ -105,3 +105,32 @@ def test_large_horizon_hull_global_variant(lqro_mod, oracle, gains):
         assert r["flags"] & 8, "hull failed"
         assert np.array_equal(r["facet"], q["facet"])
         assert r["dist"] == q["dist"]
+
+
+def test_c3_full_step(lqro_mod, oracle, gains):
+    """C3, the bench workload (1024 agents, H = 100, NP = 100: 1,047,552
+    pairs), against the oracle: every non-hull pair bit-exact (this size
+    reaches GJK's backup procedure), every hull pair's arg-min facet and
+    distance exact, and newV bit-exact on rows without hull pairs."""
+    N, H, NP = 1024, 100, 100
+    x, vg = lqro_mod.synthetic_swarm(N)
+    ctx = lqro_mod.Context(lqro_mod.config(N, H, NP, flags=lqro_mod.LQRO_FLAG_RECORDS))
+    ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
+    newv = ctx.step(x, vg)
+    recs = ctx.records()
+    st = ctx.stats()
+    ctx.close()
+    T, NCF = oracle.tables(gains["A"], gains["B"], gains["L"], gains["E"], H)
+    S = oracle.sphere(NP)
+    rv, rrecs = oracle.step(T, NCF, S, x, vg, threads=16)
+    _compare(recs, rrecs)
+    assert st["gjk_backups"] == int(((rrecs["flags"] & 4) != 0).sum())
+    inside = (rrecs["flags"] & 2) != 0
+    assert inside.sum() > 100
+    assert np.all(recs["flags"][inside] & 8), "hull failed"
+    assert np.array_equal(recs["facet"][inside], rrecs["facet"][inside])
+    assert np.array_equal(recs["dist"][inside], rrecs["dist"][inside])
+    rows_clean = np.ones(N, bool)
+    rows_clean[rrecs["i"][inside]] = False
+    assert np.array_equal(newv[rows_clean], rv[rows_clean])
+    np.testing.assert_allclose(newv, rv, rtol=1e-5, atol=1e-6)
