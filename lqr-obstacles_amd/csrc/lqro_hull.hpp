@@ -49,13 +49,14 @@ namespace lqro {
 #define HULL_CTHREADS (64 * HULL_CWAVES)
 #define HULL_SCR_WAVES 8         // per-block integer scratch: 2*H*NP ints per wave
 
-#define HULL_SBMULT 16           // outside-set segment buffer: HULL_SBMULT * H*NP entries
+#define HULL_SBMULT 24           // outside-set segment buffer: HULL_SBMULT * H*NP entries
 #define HULL_STKMULT 4           // work stack: HULL_STKMULT * H*NP faces
 #define HULL_FB_STRIDE 16384     // per-block face records in global scratch (= big faces)
 #define HULL_VG_STRIDE 8192      // per-block vertex records in global scratch (= big vertices)
 
 #define HULL_QCAP 512            // k_hull: per-wave face queue (LDS ring)
 #define HULL_FLCAP 256           // k_hull: per-wave list of retired face slots
+#define HULL_BAGCAP 16384        // k_hull: per-block overflow bag in global memory
 
 // an outside-set entry: the point and its (rounded) coordinates, so that
 // re-distributing it needs one load
@@ -92,6 +93,7 @@ struct HullArgs {
   int* rnext;
   void* bigmem;                     // per block of k_hull_big: one HullMemBig
   HullWide* wide;                   // per block of k_hull: HULL_CWAVES wide-insertion lists
+  int* bag;                         // per block of k_hull: HULL_BAGCAP overflow face ids (-1: empty)
   int block_base;                   // scratch index of this launch's block 0
   int big_main;                     // k_hull_big takes the main queue (H*NP too large for LDS)
   int wait_pairs;                   // poll the queue until k_pair has finished
@@ -171,6 +173,7 @@ struct HullWaveL {
   unsigned short q[HULL_QCAP];
   unsigned short freel[HULL_FLCAP];
   unsigned short h_a[64], h_b[64], h_out[64];
+  unsigned short ovf[64];                   // staging: queue overflow -> local batch
   int head, tail;
 };
 
@@ -183,6 +186,7 @@ struct HullLdsC {
   unsigned long long kmax4[4];
   int n, fail, job, slot, init[4], hcnt[4], hoff[4];
   int nf, nvtx, sbtop, work;
+  int gb_head, gb_tail;              // overflow bag (global memory) of this job
   double eps;
   HullWaveL wl[NW];
 };
@@ -570,10 +574,8 @@ __device__ __forceinline__ void hull_select(const HullArgs& A, const Mem& M, LT&
     }
     const bool ok = !L.fail && total > 0 && s_t[fo][0] != INT_MAX;
     // capacity overflow in the LDS variant: hand the pair to k_hull_big
-    const bool retry = !big && ((L.fail >= 1 && L.fail <= 4) || L.fail == 11);
-#ifdef LQRO_HULL_PROFILE
-    if (A.prof) atomicAdd(&A.prof[16 + (L.fail & 15)], 1ull);
-#endif
+    const bool retry = !big && ((L.fail >= 1 && L.fail <= 4) || L.fail == 6 || L.fail == 11);
+    if (A.prof) atomicAdd(&A.prof[16 + (L.fail & 15)], 1ull);   // outcome histogram
     if (retry) {
       const int r = atomicAdd(A.rcount, 1);
       if (r < A.cap) A.rqueue[r] = slot;
@@ -633,6 +635,69 @@ __device__ __forceinline__ int hq_pop(HullWaveL& Q) {
   return -1;
 }
 
+// Stage the faces of the lanes with `is` (ballot order) behind the own
+// queue's unpublished tail (mytail + qn).  What does not fit in the ring goes
+// to the wave's local batch (lanes lbn.., taken next by this wave), so a full
+// queue costs order, not a retry.  Returns 0, or 11 when both are full.
+// The overflow bag: faces that fit neither the ring nor the local batch
+// (global memory, filled by any wave, taken when the queues run dry).  Slots
+// hold -1 until written; the job's used prefix is cleared when it ends.
+struct HullBag {
+  int* slot;
+  int* head;   // LDS
+  int* tail;   // LDS
+};
+
+__device__ __forceinline__ int hq_stage(HullWaveL& W, int mytail, int& qn, int& lb, int& lbn, bool is,
+                                        int face, const HullBag& BG) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long b = __ballot(is);
+  const int np = __popcll(b);
+  if (np == 0) return 0;
+  const int room = max(HULL_QCAP - (mytail + qn - hl_ld(&W.head)), 0);
+  const int nq = min(np, room);
+  const int rank = __popcll(b & ((1ull << lane) - 1ull));
+  if (is && rank < nq) W.q[(mytail + qn + rank) % HULL_QCAP] = (unsigned short)face;
+  qn += nq;
+  const int nx = np - nq;
+  if (nx == 0) return 0;
+  if (lbn + nx > 64) {
+    int pos = 0;
+    if (lane == 0) pos = atomicAdd(BG.tail, nx);
+    pos = __builtin_amdgcn_readlane(pos, 0);
+    if (pos + nx > HULL_BAGCAP) return 11;
+    if (is && rank >= nq)
+      __hip_atomic_store(BG.slot + pos + rank - nq, face, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  }
+  if (is && rank >= nq) W.ovf[rank - nq] = (unsigned short)face;
+  hl_sync();
+  if (lane >= lbn && lane < lbn + nx) lb = W.ovf[lane - lbn];
+  hl_sync();
+  lbn += nx;
+  return 0;
+}
+
+// take one face from the bag (lane 0; -1: empty)
+__device__ __forceinline__ int hq_bag_take(const HullBag& BG) {
+  for (int tries = 0; tries < 16; ++tries) {
+    const int h = hl_ld(BG.head);
+    hl_cfence();
+    const int t = hl_ld(BG.tail);
+    if (h >= t || h >= HULL_BAGCAP) return -1;
+    if (atomicCAS(BG.head, h, h + 1) == h) {
+      int e;
+      for (int spin = 0;; ++spin) {   // the writer has reserved the slot; its store is in flight
+        e = __hip_atomic_load(BG.slot + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (e >= 0 || spin > (1 << 20)) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      return e;
+    }
+  }
+  return -1;
+}
+
 // One insertion whose region (R) or horizon exceeds 64 faces: the steps of
 // hull_insert_mw, chunked over 64 lanes with the lists in per-wave global
 // scratch (WG).  The wave holds the region and the faces around it.
@@ -641,7 +706,8 @@ template <int NW>
 __device__ __noinline__ int hull_insert_wide(HullMemC& M, HullLdsC<NW>& L, HullWaveL& W, HullWide& WG,
                                              const double* Pr, int* vpid, HullPt* sb, int sbcap, int* sq,
                                              int HNP, int apex, const double* p, double eps2, int R, int rg,
-                                             int& nfree, int& mytail, unsigned LK, unsigned RB) {
+                                             int& nfree, int& mytail, int& lb, int& lbn, const HullBag& BG,
+                                             unsigned LK, unsigned RB) {
   const int lane = threadIdx.x & 63;
   const unsigned long long lt = (1ull << lane) - 1ull;
   constexpr int kF = HullMemC::kFaces, kV = HullMemC::kVerts;
@@ -806,7 +872,7 @@ __device__ __noinline__ int hull_insert_wide(HullMemC& M, HullLdsC<NW>& L, HullW
   }
   nfree = min(keep + R, HULL_FLCAP);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  int np = 0, full = 0;
+  int np = 0, qn = 0;
   for (int h0 = 0; h0 < nh; h0 += 64) {
     const int h = h0 + lane;
     int is = 0, sf = 0;
@@ -815,13 +881,11 @@ __device__ __noinline__ int hull_insert_wide(HullMemC& M, HullLdsC<NW>& L, HullW
       atomicAnd(&M.own[sf], ~LK);
       is = WG.cnt[h] > 0;
     }
-    const unsigned long long b = __ballot(is);
-    if (mytail + np + __popcll(b) - hl_ld(&W.head) > HULL_QCAP) { full = 1; break; }
-    if (is) W.q[(mytail + np + __popcll(b & lt)) % HULL_QCAP] = (unsigned short)sf;
-    np += __popcll(b);
+    np += __popcll(__ballot(is));
+    const int rc = hq_stage(W, mytail, qn, lb, lbn, is, sf, BG);
+    if (rc) return rc;
   }
-  if (full) return 11;
-  mytail += np;
+  mytail += qn;
   hl_sync();
   if (lane == 0) {
     atomicAdd(&L.work, np - 1);
@@ -840,7 +904,8 @@ __device__ __noinline__ int hull_insert_wide(HullMemC& M, HullLdsC<NW>& L, HullW
 template <int NW>
 __device__ __forceinline__ void hull_insert_mw(HullMemC& M, HullLdsC<NW>& L, const double* Pr, int n,
                                                double eps2, int* vpid, HullPt* sb, int sbcap,
-                                               int* sq, int HNP, HullWide& WG, unsigned long long* pstat) {
+                                               int* sq, int HNP, HullWide& WG, const HullBag& BG,
+                                               unsigned long long* pstat) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const unsigned LK = 1u << (16 + w), RB = 1u << (24 + w);
   const unsigned OLDER = ((1u << w) - 1u) << 16;        // lock bits of lower-numbered waves
@@ -849,17 +914,20 @@ __device__ __forceinline__ void hull_insert_mw(HullMemC& M, HullLdsC<NW>& L, con
   int nfree = 0, mytail = hl_ld(&W.tail), attempts = 0, idle = 0;
   unsigned long long n_ins = 0, n_conf = 0, n_stale = 0, n_big = 0;
   constexpr int kF = HullMemC::kFaces, kV = HullMemC::kVerts;
-  // re-queue face f (lane 0; the entry keeps its unit of L.work)
+  // a batch of entries taken from the own queue at once (lanes 0..lbn-1)
+  int lb = -1, lbn = 0;
+  // re-queue face f (wave-uniform; the entry keeps its unit of L.work)
   auto requeue = [&](int f) {
-    if (lane == 0) {
-      if (mytail - hl_ld(&W.head) >= HULL_QCAP) atomicMax(&L.fail, 11);
-      else {
-        W.q[mytail % HULL_QCAP] = (unsigned short)f;
-        hl_cfence();
-        hl_st(&W.tail, ++mytail);
-      }
+    int qn = 0;
+    if (hq_stage(W, mytail, qn, lb, lbn, lane == 0, f, BG)) {
+      if (lane == 0) atomicMax(&L.fail, 11);
+      return;
     }
-    mytail = __builtin_amdgcn_readlane(mytail, 0);
+    if (qn) {
+      mytail += qn;
+      hl_sync();
+      if (lane == 0) hl_st(&W.tail, mytail);
+    }
   };
 #ifdef LQRO_HULL_PROFILE
   unsigned long long wacc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -867,8 +935,6 @@ __device__ __forceinline__ void hull_insert_mw(HullMemC& M, HullLdsC<NW>& L, con
 #endif
   unsigned maxr = 0;
   unsigned long long n_held = 0;
-  // a batch of entries taken from the own queue at once (lanes 0..lbn-1)
-  int lb = -1, lbn = 0;
   for (;;) {
     if (hl_ld(&L.fail)) break;
     // (a) a face: from the local batch; refill it from the own queue (up to
@@ -894,8 +960,10 @@ __device__ __forceinline__ void hull_insert_mw(HullMemC& M, HullLdsC<NW>& L, con
       }
       if (lbn == 0) {
         int e = -1;
-        if (lane == 0)
+        if (lane == 0) {
           for (int k = 1; k < NW && e < 0; ++k) e = hq_pop(L.wl[(w + k) % NW]);
+          if (e < 0) e = hq_bag_take(BG);
+        }
         e = __builtin_amdgcn_readlane(e, 0);
         if (e >= 0) { lb = lane == 0 ? e : -1; lbn = 1; }
       }
@@ -1020,7 +1088,7 @@ __device__ __forceinline__ void hull_insert_mw(HullMemC& M, HullLdsC<NW>& L, con
       // release the region and the faces around it; re-queue the region's
       // faces that have outside points (f with its unit of L.work, the
       // others with a new one: a popper may have dropped their entries)
-      int nq = 0, full = 0;
+      int nq = 0, qn = 0, full = 0;
       for (int r0 = 0; r0 < R; r0 += 64) {
         const int r = r0 + lane;
         int g = -1, is = 0;
@@ -1030,13 +1098,11 @@ __device__ __forceinline__ void hull_insert_mw(HullMemC& M, HullLdsC<NW>& L, con
           const unsigned o = atomicAnd(&M.own[g], ~(LK | RB));
           is = (o & 0xFFFFu) != HULL_NOPT;
         }
-        const unsigned long long b = __ballot(is);
-        if (mytail + nq + __popcll(b) - hl_ld(&W.head) > HULL_QCAP) { full = 1; break; }
-        if (is) W.q[(mytail + nq + __popcll(b & lt)) % HULL_QCAP] = (unsigned short)g;
-        nq += __popcll(b);
+        nq += __popcll(__ballot(is));
+        if (hq_stage(W, mytail, qn, lb, lbn, is, g, BG)) { full = 1; break; }
       }
       if (full) { if (lane == 0) atomicMax(&L.fail, 11); break; }
-      mytail += nq;
+      mytail += qn;
       hl_sync();
       if (lane == 0) {
         atomicAdd(&L.work, nq - 1);
@@ -1073,7 +1139,7 @@ __device__ __forceinline__ void hull_insert_mw(HullMemC& M, HullLdsC<NW>& L, con
     if (R > 64 || nh > 64) {
       // ---- wide insertion: region / horizon lists in global scratch ----
       const int rc = hull_insert_wide(M, L, W, WG, Pr, vpid, sb, sbcap, sq, HNP, apex, p, eps2, R, rg,
-                                      nfree, mytail, LK, RB);
+                                      nfree, mytail, lb, lbn, BG, LK, RB);
       if (rc) { if (lane == 0) atomicMax(&L.fail, rc); break; }
       ++n_ins;
       WSTAMP(7);
@@ -1277,11 +1343,10 @@ __device__ __forceinline__ void hull_insert_mw(HullMemC& M, HullLdsC<NW>& L, con
     if (hl) atomicAnd(&M.own[sf], ~LK);
     {
       const int is = hl && cnt_mine > 0;
-      const unsigned long long b = __ballot(is);
-      const int np = __popcll(b);
-      if (mytail + np - hl_ld(&W.head) > HULL_QCAP) { if (lane == 0) atomicMax(&L.fail, 11); break; }
-      if (is) W.q[(mytail + __popcll(b & lt)) % HULL_QCAP] = (unsigned short)sf;
-      mytail += np;
+      const int np = __popcll(__ballot(is));
+      int qn = 0;
+      if (hq_stage(W, mytail, qn, lb, lbn, is, sf, BG)) { if (lane == 0) atomicMax(&L.fail, 11); break; }
+      mytail += qn;
       hl_sync();
       if (lane == 0) {
         atomicAdd(&L.work, np - 1);                        // before the entries are visible
@@ -1325,6 +1390,8 @@ __device__ __forceinline__ void hull_body_mw(const HullArgs& A, HullMemC& M, Hul
   HullPt* sb = A.sb + (size_t)hb * HNP * HULL_SBMULT;
   const int sbcap = HNP * HULL_SBMULT;
   int* vpid = A.vpid + (size_t)hb * HULL_VG_STRIDE;
+  const HullBag BG{A.bag + (size_t)hb * HULL_BAGCAP, &L.gb_head, &L.gb_tail};
+  if (tid == 0) L.gb_tail = 0;
   for (;;) {
     const int slot = hull_take_job(A, L, false);
     if (slot < 0) break;
@@ -1353,6 +1420,7 @@ __device__ __forceinline__ void hull_body_mw(const HullArgs& A, HullMemC& M, Hul
       int* th = isc;
       if (tid < 4) { L.hcnt[tid] = 0; L.kmax4[tid] = 0ull; }
       if (tid < NW) { L.wl[tid].head = 0; L.wl[tid].tail = 0; }
+      if (tid == 0) { L.gb_head = 0; L.gb_tail = 0; }
       hl_bar();
       for (int q = tid; q < n; q += blockDim.x) {
         int c = -1;
@@ -1405,7 +1473,7 @@ __device__ __forceinline__ void hull_body_mw(const HullArgs& A, HullMemC& M, Hul
       HSTAMP(1);
       // 5. quickhull, every wave inserting
       hull_insert_mw<NW>(M, L, Pr, n, eps2, vpid, sb, sbcap, isc + (size_t)wave * 2 * HNP, HNP,
-                         A.wide[(size_t)hb * NW + wave],
+                         A.wide[(size_t)hb * NW + wave], BG,
 #ifdef LQRO_HULL_PROFILE
                          A.prof ? A.prof + 10 : nullptr
 #else
@@ -1416,6 +1484,9 @@ __device__ __forceinline__ void hull_body_mw(const HullArgs& A, HullMemC& M, Hul
       HSTAMP(6);
     }
     hl_bar();
+    // the bag's used prefix back to empty (-1) for the next job
+    for (int q = tid; q < min(L.gb_tail, HULL_BAGCAP); q += blockDim.x) BG.slot[q] = -1;
+    if (tid == 0) L.gb_tail = 0;
     HSTAMP(8);
     // 6. facet selection
     const int nf = L.nf;

@@ -218,6 +218,7 @@ struct lqro_ctx {
   int *d_hq, *d_hcount, *d_hnext, *d_err, *d_rq;
   void* d_hbig;
   HullWide* d_hwide;
+  int* d_hbag;
   int hull_big_blocks;
   int n_cu;
   int side_cus;              // CUs running k_hull beside k_pair (LQRO_SIDE_HULL_CUS)
@@ -284,7 +285,7 @@ void lqro_destroy(lqro_ctx* c) {
   (void)hipSetDevice(c->cfg.device);
   void* ps[] = {c->d_R, c->d_TF, c->d_shash, c->d_T, c->d_NCF, c->d_S, c->d_x, c->d_vgoal, c->d_newv, c->d_A, c->d_B,
                 c->d_L, c->d_E, c->d_planes, c->d_lpscratch, c->d_lpcompact, c->d_recs, c->d_hq, c->d_hcount,
-                c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats, c->d_prof, c->d_rq, c->d_hbig, c->d_hwide, c->d_hfbest, c->d_hvpid, c->d_hstack};
+                c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats, c->d_prof, c->d_rq, c->d_hbig, c->d_hwide, c->d_hbag, c->d_hfbest, c->d_hvpid, c->d_hstack};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (int k = 0; k < 5; ++k)
@@ -343,6 +344,8 @@ static int ctx_alloc(lqro_ctx* c) {
   c->hull_big_blocks = 64;
   HIPCHK(hipMalloc(&c->d_hbig, sizeof(HullMemBig) * (size_t)c->hull_big_blocks));
   HIPCHK(hipMalloc(&c->d_hwide, sizeof(HullWide) * HULL_CWAVES * (size_t)c->hull_blocks));
+  HIPCHK(hipMalloc(&c->d_hbag, sizeof(int) * HULL_BAGCAP * (size_t)c->hull_blocks));
+  HIPCHK(hipMemset(c->d_hbag, 0xFF, sizeof(int) * HULL_BAGCAP * (size_t)c->hull_blocks));
   return LQRO_OK;
 }
 
@@ -523,6 +526,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   Hh.rqueue = c->d_rq; Hh.rcount = c->d_hcount + 2; Hh.rnext = c->d_hcount + 3;
   Hh.bigmem = c->d_hbig;
   Hh.wide = c->d_hwide;
+  Hh.bag = c->d_hbag;
   Hh.stats = c->d_stats;
   Hh.prof = c->d_prof;
   Hh.pair_done = P.pair_done;
