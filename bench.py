@@ -12,7 +12,9 @@ operation order (results bit-identical to the reference CPU path).
 Multi-GPU (python -m torch.distributed.run --nproc-per-node G bench.py --gpus G):
 rows (agents i) are block-sharded over ranks, each rank runs its rows' pairs,
 then one RCCL all-gather of the new velocities (the per-step state exchange,
-SURVEY.md §8e).  Total work is fixed (strong scaling).
+SURVEY.md §8e).  Weak scaling: the swarm grows to round(1024 sqrt(G)) agents
+so that every GPU keeps C3's ~1.05 M pairs per step (the path is all-pairs,
+O(N^2)); --agents fixes N instead (e.g. --agents 4096 at G = 8 is C4).
 
 Prints ONE JSON line (rank 0).
 """
@@ -107,6 +109,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--agents", type=int, default=0,
+                    help="swarm size (default: round(1024 sqrt(world)), C3's pairs per GPU)")
+    ap.add_argument("--no-roofline-probe", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -125,7 +130,7 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    N = N_AGENTS
+    N = args.agents if args.agents > 0 else int(round(N_AGENTS * world ** 0.5))
     rb, re = lqro.row_shard(N, rank, world)
     rows = re - rb
     x, vg = lqro.synthetic_swarm(N)
@@ -172,8 +177,27 @@ def main():
     pairs_step = N * (N - 1)
     value = pairs_step * args.steps / elapsed
     ms_step = elapsed / args.steps * 1e3
-    # roofline of the dominant kernel (k_pair), per launch on this rank
-    pk_ms = float(np.mean(pair_ms))
+    sweep_ms = float(np.mean(pair_ms))
+    # Roofline of the dominant kernel, k_pair.  In the timed steps k_pair runs
+    # as two launches beside the hull (hot pairs + rows on a side stream, rows
+    # on the main stream), so its own duration is measured right after, on
+    # this rank's same rows, with the overlap off (LQRO_HOT=0: one k_pair
+    # launch over all pairs, HIP events on its launch stream).
+    pk_ms = sweep_ms
+    probe = "sweep (k_prio + k_pair launches + overlapped side hull), timed steps"
+    if not args.no_roofline_probe:
+        os.environ["LQRO_HOT"] = "0"
+        pctx = lqro.Context(lqro.config(N, HORIZON, N_POINTS, device=local, row_begin=rb, row_end=re))
+        del os.environ["LQRO_HOT"]
+        pctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
+        pk = []
+        for k in range(1 + min(args.steps, 5)):
+            pctx.step_device(d_x.data_ptr(), d_vg.data_ptr(), d_newv.data_ptr(), stream.cuda_stream)
+            if k:
+                pk.append(pctx.timings()["pair_ms"])
+        pctx.close()
+        pk_ms = float(np.mean(pk))
+        probe = f"k_pair alone (LQRO_HOT=0 probe, {len(pk)} launches after the timed steps)"
     pairs_launch = rows * (N - 1)
     tflops = sweep_flops_per_pair() * pairs_launch / (pk_ms * 1e-3) / 1e12
     gbs = algorithmic_bytes_per_pair() * pairs_launch / (pk_ms * 1e-3) / 1e9
@@ -187,12 +211,13 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_step,
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (SplitMix64 swarm, seed 0x4C51524F, constant density)",
         "config": {
-            "workload": "C3: 1024 quadrotors, horizon 100, 100 points/ellipsoid, 16-D state; "
+            "workload": (f"C3: 1024 quadrotors" if N == N_AGENTS else f"{N} quadrotors (C3 pairs per GPU)") +
+                        ", horizon 100, 100 points/ellipsoid, 16-D state; "
                         "reference-exact fp64 pair sweep+GJK+hull+half-plane, fp32 LP",
             "n_agents": N, "horizon": HORIZON, "n_points": N_POINTS, "x_dim": X_DIM,
             "pairs_per_step": pairs_step,
@@ -213,10 +238,12 @@ def main():
             "flops_per_pair_exact_order": exact_order_flops_per_pair(),
             "pairs_per_launch": pairs_launch,
             "kernel_ms": pk_ms,
+            "kernel_ms_source": probe,
             "hbm_algorithmic_gbs": gbs,
             "hbm_frac": gbs / HBM_PEAK_GBS,
         },
         "step_device_ms": float(np.mean(step_dev_ms)),
+        "sweep_ms": sweep_ms,
         "inside_hull_pairs_per_step": st["inside"],
         "hull_failures": st["hull_fail"],
     }

@@ -60,6 +60,13 @@ struct PairArgs {
   int hull_cap;
   unsigned long long* stats;          // 8 counters
   unsigned long long* prof;           // LQRO_PAIR_PROFILE: per-phase cycles (16 words)
+  // hot phase (k_prio's list of likely inside-hull pairs; null: none)
+  const int* hot_list;
+  const unsigned char* hot_mark;      // per slot: 1 = in the hot list
+  const int* hot_count;
+  int* hot_next;
+  int hot_cap;
+  int hot_only;                       // 1: this launch computes the hot list only
   // LDS layout, in doubles
   int XP, lds_T, lds_N, lds_S, lds_R, lds_TF, lds_H, lds_wave, wave_doubles;
 };
@@ -277,13 +284,14 @@ __device__ inline int reach_rank(const PairArgs& P, const WaveTabs& W, int lane,
 #define PSTAMP(k) do {} while (0)
 #endif
 
+// One workgroup's share of a k_pair launch (LDS at `lds`, laid out per
+// PairArgs; waves = blockDim.x / 64 <= P.waves).  Also the tail of k_side.
 template <int X>
-__global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
+__device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
 #ifdef LQRO_PAIR_PROFILE
   unsigned long long pp[16] = {0};
   unsigned long long p_last = __builtin_amdgcn_s_memtime();
 #endif
-  extern __shared__ double lds[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int H = P.H, NP = P.NP, XP = P.XP;
@@ -320,49 +328,9 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
   SliceSupport sup{P, B, W, lane};
 #endif
 
-  // Persistent: the workgroup takes whole rows (agent i) off a queue; its
-  // waves take the row's pairs one at a time (LDS counter), so uneven pair
-  // costs balance inside the row.  Agent i's horizon tables are staged into
-  // LDS only when they change (once per workgroup with shared gains).
-  long staged = -1;
-  for (;;) {
-    // work unit = (row, part): a row is split into row_split pair ranges
-    // when there are fewer rows than workgroups (many GPUs / small N)
-    if (threadIdx.x == 0) {
-      const int u = atomicAdd(P.row_counter, 1);
-      s_row = u;
-      s_next = (int)((long)(u % P.row_split) * P.npr / P.row_split);
-    }
-    __syncthreads();
-    const int unit = s_row;
-    if (unit >= P.nrows * P.row_split) break;
-    const int lrow = unit / P.row_split;
-    const int jj_end = (int)((long)(unit % P.row_split + 1) * P.npr / P.row_split);
-    const int i = P.row_begin + lrow;
-    const long ag = P.per_agent ? (long)i : 0;
-    if (ag != staged) {
-      const double* Ti = P.T + ag * H * 9;
-      const double* Ni = P.NCF + ag * H * 3 * X;
-      const double* Ri = P.R + ag * H;
-      const double* TFi = P.TF + ag * H;
-      for (int q = threadIdx.x; q < H * 9; q += blockDim.x) sT[q] = Ti[q];
-      for (int q = threadIdx.x; q < H * 3 * X; q += blockDim.x) sN[(q / X) * XP + (q % X)] = Ni[q];
-      for (int q = threadIdx.x; q < NP * 3; q += blockDim.x) sS[(q % 3) * NP + q / 3] = P.S[q];
-      for (int q = threadIdx.x; q < H; q += blockDim.x) {
-        sR[q] = Ri[q];
-        sTF[q] = TFi[q];
-        sH[q] = P.shash[q];
-      }
-      staged = ag;
-      __syncthreads();
-    }
-    PSTAMP(0);
+  // one ordered pair (i, j = jj-th other agent) of local row lrow
+  auto do_pair = [&](const int i, const int lrow, const int jj) {
     const double* xi = P.x + (size_t)i * X;
-  for (;;) {
-    int jj = 0;
-    if (lane == 0) jj = atomicAdd(&s_next, 1);
-    jj = __shfl(jj, 0);
-    if (jj >= jj_end) break;
     const int j = jj < i ? jj : jj + 1;
     const double* xj = P.x + (size_t)j * X;
     double d[X];
@@ -547,9 +515,80 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
     pp[11] += 1;
     pp[12] = pc[0]; pp[13] = pc[1]; pp[14] = pc[2];
 #endif
+    };
+  // Hot launch (shared gains only): the pairs k_prio marked as likely
+  // inside-hull, one per wave, so that their hulls can run on side-stream
+  // k_hull workers while the row launch sweeps the rest.  Scheduling only:
+  // every pair is computed by the same code.
+  if (P.hot_only) {
+    for (int q = threadIdx.x; q < H * 9; q += blockDim.x) sT[q] = P.T[q];
+    for (int q = threadIdx.x; q < H * 3 * X; q += blockDim.x) sN[(q / X) * XP + (q % X)] = P.NCF[q];
+    for (int q = threadIdx.x; q < NP * 3; q += blockDim.x) sS[(q % 3) * NP + q / 3] = P.S[q];
+    for (int q = threadIdx.x; q < H; q += blockDim.x) {
+      sR[q] = P.R[q];
+      sTF[q] = P.TF[q];
+      sH[q] = P.shash[q];
+    }
+    __syncthreads();
+    const int nhot = min(*P.hot_count, P.hot_cap);
+    for (;;) {
+      int h = 0;
+      if (lane == 0) h = atomicAdd(P.hot_next, 1);
+      h = __shfl(h, 0);
+      if (h >= nhot) break;
+      const int slot = P.hot_list[h];
+      const int lrow = slot / P.npr;
+      do_pair(P.row_begin + lrow, lrow, slot - lrow * P.npr);
+    }
+  } else {
+  // Persistent: the workgroup takes whole rows (agent i) off a queue; its
+  // waves take the row's pairs one at a time (LDS counter), so uneven pair
+  // costs balance inside the row.  Agent i's horizon tables are staged into
+  // LDS only when they change (once per workgroup with shared gains).
+  long staged = -1;
+  for (;;) {
+    // work unit = (row, part): a row is split into row_split pair ranges
+    // when there are fewer rows than workgroups (many GPUs / small N)
+    if (threadIdx.x == 0) {
+      const int u = atomicAdd(P.row_counter, 1);
+      s_row = u;
+      s_next = (int)((long)(u % P.row_split) * P.npr / P.row_split);
+    }
+    __syncthreads();
+    const int unit = s_row;
+    if (unit >= P.nrows * P.row_split) break;
+    const int lrow = unit / P.row_split;
+    const int jj_end = (int)((long)(unit % P.row_split + 1) * P.npr / P.row_split);
+    const int i = P.row_begin + lrow;
+    const long ag = P.per_agent ? (long)i : 0;
+    if (ag != staged) {
+      const double* Ti = P.T + ag * H * 9;
+      const double* Ni = P.NCF + ag * H * 3 * X;
+      const double* Ri = P.R + ag * H;
+      const double* TFi = P.TF + ag * H;
+      for (int q = threadIdx.x; q < H * 9; q += blockDim.x) sT[q] = Ti[q];
+      for (int q = threadIdx.x; q < H * 3 * X; q += blockDim.x) sN[(q / X) * XP + (q % X)] = Ni[q];
+      for (int q = threadIdx.x; q < NP * 3; q += blockDim.x) sS[(q % 3) * NP + q / 3] = P.S[q];
+      for (int q = threadIdx.x; q < H; q += blockDim.x) {
+        sR[q] = Ri[q];
+        sTF[q] = TFi[q];
+        sH[q] = P.shash[q];
+      }
+      staged = ag;
+      __syncthreads();
+    }
+    PSTAMP(0);
+  for (;;) {
+    int jj = 0;
+    if (lane == 0) jj = atomicAdd(&s_next, 1);
+    jj = __shfl(jj, 0);
+    if (jj >= jj_end) break;
+    if (P.hot_mark != nullptr && P.hot_mark[(size_t)lrow * P.npr + jj]) continue;   // done in the hot phase
+    do_pair(i, lrow, jj);
   }
     __syncthreads();   // the row is done before s_row / the tables change
   }
+  }   // row launch
   // every queue entry of this workgroup is published: count it finished
   if (threadIdx.x == 0)
     __hip_atomic_fetch_add(P.pair_done, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
@@ -563,6 +602,58 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
     atomicAdd(&P.stats[5], st_backup);
     atomicAdd(&P.stats[6], st_reach);
     atomicAdd(&P.stats[7], st_iters);
+  }
+}
+
+template <int X>
+__global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
+  extern __shared__ double lds[];
+  pair_block<X>(P, lds);
+}
+
+// k_prio: which pairs go first.  A pair whose relative motion brings the two
+// agents within hot_r of each other in the next t_hot seconds (closest
+// approach of p_i - p_j + t (v_i - v_j), t in [0, t_hot]) is likely to put
+// vrel inside its LQR-obstacle hull; those pairs are listed (and marked) so
+// that k_pair computes them first and their hulls overlap the rest of the
+// sweep.  A heuristic for ORDER only: a missed or extra pair changes no
+// result, only when its hull starts.
+struct PrioArgs {
+  int npr, nrows, row_begin, X;
+  const double* x;
+  double t_hot, r2_hot;
+  int* list;
+  unsigned char* mark;
+  int* count;
+  int cap;
+};
+
+__global__ void __launch_bounds__(256) k_prio(PrioArgs A) {
+  const long total = (long)A.nrows * A.npr;
+  const int lane = threadIdx.x & 63;
+  for (long base = (long)blockIdx.x * 256 + (threadIdx.x & ~63); base < total; base += (long)gridDim.x * 256) {
+    const long slot = base + lane;
+    bool hot = false;
+    if (slot < total) {
+      const int lrow = (int)(slot / A.npr), jj = (int)(slot - (long)lrow * A.npr);
+      const int i = A.row_begin + lrow, j = jj < i ? jj : jj + 1;
+      const double* xi = A.x + (size_t)i * A.X;
+      const double* xj = A.x + (size_t)j * A.X;
+      const double p0 = xi[0] - xj[0], p1 = xi[1] - xj[1], p2 = xi[2] - xj[2];
+      const double v0 = xi[3] - xj[3], v1 = xi[4] - xj[4], v2 = xi[5] - xj[5];
+      const double vv = v0 * v0 + v1 * v1 + v2 * v2;
+      double t = vv > 0.0 ? -(p0 * v0 + p1 * v1 + p2 * v2) / vv : 0.0;
+      t = fmin(fmax(t, 0.0), A.t_hot);
+      const double e0 = p0 + t * v0, e1 = p1 + t * v1, e2 = p2 + t * v2;
+      hot = e0 * e0 + e1 * e1 + e2 * e2 <= A.r2_hot;
+    }
+    const unsigned long long b = __ballot(hot);
+    int pos = 0;
+    if (lane == 0 && b) pos = atomicAdd(A.count, __popcll(b));
+    pos = __shfl(pos, 0) + __popcll(b & ((1ull << lane) - 1ull));
+    if (hot && pos >= A.cap) hot = false;
+    if (hot) A.list[pos] = (int)slot;
+    if (slot < total) A.mark[slot] = hot ? 1 : 0;
   }
 }
 

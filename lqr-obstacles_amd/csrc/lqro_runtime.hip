@@ -38,6 +38,19 @@
 
 using namespace lqro;
 
+// k_side: the side stream's hull workers (the hot pairs' hulls, topology in
+// LDS as k_hull), which turn into k_pair row workers once the hull queue is
+// drained, so the side CUs never idle while the sweep goes on.  The pair
+// tables and per-wave regions reuse the hull's LDS (host checks the fit).
+template <int X>
+__global__ void __launch_bounds__(HULL_CTHREADS) k_side(HullArgs A, PairArgs P) {
+  __shared__ HullLdsC<HULL_CWAVES> L;
+  __shared__ HullMemC M;
+  hull_body_mw<HULL_CWAVES>(A, M, L);
+  __syncthreads();
+  if (P.nrows > 0) pair_block<X>(P, reinterpret_cast<double*>(&M));
+}
+
 #define LQRO_MAXX 16
 
 // ---------------------------------------------------------------------------
@@ -219,6 +232,10 @@ struct lqro_ctx {
   void* d_hbig;
   HullWide* d_hwide;
   int* d_hbag;
+  int* d_hotlist;            // k_prio: likely inside-hull pairs (slots), computed first
+  unsigned char* d_hotmark;  // per slot: in the hot list
+  int hot_cap;
+  int hot_on;                // LQRO_HOT (default 1)
   int hull_big_blocks;
   int n_cu;
   int side_cus;              // CUs running k_hull beside k_pair (LQRO_SIDE_HULL_CUS)
@@ -285,7 +302,7 @@ void lqro_destroy(lqro_ctx* c) {
   (void)hipSetDevice(c->cfg.device);
   void* ps[] = {c->d_R, c->d_TF, c->d_shash, c->d_T, c->d_NCF, c->d_S, c->d_x, c->d_vgoal, c->d_newv, c->d_A, c->d_B,
                 c->d_L, c->d_E, c->d_planes, c->d_lpscratch, c->d_lpcompact, c->d_recs, c->d_hq, c->d_hcount,
-                c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats, c->d_prof, c->d_rq, c->d_hbig, c->d_hwide, c->d_hbag, c->d_hfbest, c->d_hvpid, c->d_hstack};
+                c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats, c->d_prof, c->d_rq, c->d_hbig, c->d_hwide, c->d_hbag, c->d_hotlist, c->d_hotmark, c->d_hfbest, c->d_hvpid, c->d_hstack};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (int k = 0; k < 5; ++k)
@@ -326,7 +343,8 @@ static int ctx_alloc(lqro_ctx* c) {
   c->hull_cap = (int)(slots < (1u << 22) ? slots : (1u << 22));
   if (c->hull_cap < 1) c->hull_cap = 1;
   HIPCHK(hipMalloc(&c->d_hq, sizeof(int) * c->hull_cap));
-  HIPCHK(hipMalloc(&c->d_hcount, sizeof(int) * 8));   // count, next, retry count, retry next, pair rows
+  // hull count, next, retry count, retry next, pair rows, pair_done, hot count, hot next, hot done
+  HIPCHK(hipMalloc(&c->d_hcount, sizeof(int) * 16));
   c->d_hnext = c->d_hcount + 1;
   HIPCHK(hipMalloc(&c->d_rq, sizeof(int) * c->hull_cap));
   HIPCHK(hipMalloc(&c->d_err, sizeof(int)));
@@ -346,6 +364,9 @@ static int ctx_alloc(lqro_ctx* c) {
   HIPCHK(hipMalloc(&c->d_hwide, sizeof(HullWide) * HULL_CWAVES * (size_t)c->hull_blocks));
   HIPCHK(hipMalloc(&c->d_hbag, sizeof(int) * HULL_BAGCAP * (size_t)c->hull_blocks));
   HIPCHK(hipMemset(c->d_hbag, 0xFF, sizeof(int) * HULL_BAGCAP * (size_t)c->hull_blocks));
+  c->hot_cap = (int)std::max<size_t>(16384, slots / 32);
+  HIPCHK(hipMalloc(&c->d_hotlist, sizeof(int) * c->hot_cap));
+  HIPCHK(hipMalloc(&c->d_hotmark, slots ? slots : 1));
   return LQRO_OK;
 }
 
@@ -371,9 +392,13 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
   c->cfg = g;
   c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   {
+    // CUs running k_hull workers beside k_pair (the hot-pair hulls); default 3/8
     const char* e = getenv("LQRO_SIDE_HULL_CUS");
-    c->side_cus = e ? atoi(e) : 0;
+    c->side_cus = e ? atoi(e) : (3 * c->n_cu) / 8;
     if (c->side_cus < 0) c->side_cus = 0;
+    if (c->side_cus > c->n_cu / 2) c->side_cus = c->n_cu / 2;
+    const char* h = getenv("LQRO_HOT");
+    c->hot_on = h ? atoi(h) != 0 : 1;
   }
   c->rb = g.row_begin;
   c->re = (g.row_end > g.row_begin) ? g.row_end : g.n_agents;
@@ -497,21 +522,46 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   P.hull_queue = c->d_hq; P.hull_count = c->d_hcount; P.hull_cap = c->hull_cap;
   P.stats = c->d_stats;
   P.prof = c->d_prof + 32 + 2 * 4096;
-  // persistent: one workgroup per CU (LDS-bound), rows off a queue.  A few
-  // CUs run k_hull workers beside it (side stream) so that inside-hull pairs
-  // start as soon as k_pair finds them; the rest of the hull queue is taken by
-  // a full-width k_hull after k_pair.
+  // persistent: one workgroup per CU (LDS-bound), rows off a queue.
+  //   main:  k_prio -> k_pair(rows, n_cu - side blocks) -> [side done] -> k_hull -> k_hull_big -> k_lp
+  //   side:  [k_prio done] -> k_pair(hot, side blocks) -> k_side(hot hulls, then rows)
+  // The hot launch computes the pairs k_prio predicts to be inside-hull, so
+  // their hulls run on the side CUs while the row launch sweeps the rest on
+  // the others; each side workgroup joins the sweep as soon as the hull
+  // queue is drained.  No kernel waits on another running kernel (streams
+  // sharing a hardware queue just serialise), and the two concurrent grids
+  // add up to one workgroup per CU.  Hull jobs the prediction missed are
+  // taken by the k_hull after the sweep.
   P.row_counter = c->d_hcount + 4;
   P.pair_done = c->d_hcount + 5;
-  HIPCHK(hipMemsetAsync(c->d_hcount, 0, sizeof(int) * 8, s));
+  HIPCHK(hipEventRecord(c->ev[0], s));
+  HIPCHK(hipMemsetAsync(c->d_hcount, 0, sizeof(int) * 16, s));
   HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * 8, s));
   HIPCHK(hipMemsetAsync(c->d_hq, 0xFF, sizeof(int) * (size_t)c->hull_cap, s));
   // the LDS hull variant packs outside-set extents in 32 bits: H*NP <= 16383
   const bool lds_ok = (size_t)g.horizon * g.n_points <= 16383;
-  const int nwait = (lds_ok && c->nrows >= 4 * c->n_cu && c->n_cu >= 64) ? std::min(c->side_cus, c->n_cu / 2) : 0;
-  const int nwg = c->n_cu - nwait;
-  P.row_split = std::max(1, std::min(16, (2 * nwg + c->nrows - 1) / c->nrows));
-  const unsigned nblk = (unsigned)std::min(c->nrows * P.row_split, nwg);
+  const long slots = (long)c->nrows * c->npr;
+  const bool side_fits = (size_t)(P.lds_wave + HULL_CWAVES * P.wave_doubles) * 8 <= sizeof(HullMemC) &&
+                         P.waves >= HULL_CWAVES;
+  const bool hot = c->hot_on && !c->per_agent && lds_ok && side_fits && c->n_cu >= 64 && slots >= 65536;
+  const int nwait = hot ? c->side_cus : 0;
+  P.row_split = std::max(1, std::min(16, (2 * c->n_cu + c->nrows - 1) / c->nrows));
+  const int units = c->nrows * P.row_split;
+  const unsigned nblk = (unsigned)std::min(units, c->n_cu - nwait);
+  const unsigned nside = (unsigned)std::max(0, std::min(units - (int)nblk, nwait));
+  P.hot_list = nullptr; P.hot_mark = nullptr; P.hot_count = nullptr;
+  P.hot_next = nullptr; P.hot_cap = 0; P.hot_only = 0;
+  if (hot) {
+    PrioArgs Q;
+    Q.npr = c->npr; Q.nrows = c->nrows; Q.row_begin = c->rb; Q.X = g.x_dim; Q.x = d_x;
+    Q.t_hot = 3.0; Q.r2_hot = 3.0 * 3.0;   // seconds, metres (scheduling heuristic)
+    Q.list = c->d_hotlist; Q.mark = c->d_hotmark; Q.count = c->d_hcount + 6; Q.cap = c->hot_cap;
+    const long nb = std::min<long>((slots + 255) / 256, 8L * c->n_cu);
+    hipLaunchKernelGGL(k_prio, dim3((unsigned)nb), dim3(256), 0, s, Q);
+    HIPCHK(hipGetLastError());
+    P.hot_list = c->d_hotlist; P.hot_mark = c->d_hotmark; P.hot_count = c->d_hcount + 6;
+    P.hot_next = c->d_hcount + 7; P.hot_cap = c->hot_cap;
+  }
   HullArgs Hh;
   Hh.N = g.n_agents; Hh.X = g.x_dim; Hh.H = g.horizon; Hh.NP = g.n_points;
   Hh.row_begin = c->rb; Hh.npr = c->npr; Hh.per_agent = c->per_agent;
@@ -530,18 +580,29 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   Hh.stats = c->d_stats;
   Hh.prof = c->d_prof;
   Hh.pair_done = P.pair_done;
-  Hh.pair_blocks = (int)nblk;
+  Hh.pair_blocks = (int)(nblk + nside);
   Hh.block_base = 0;
-  Hh.wait_pairs = 1;
+  Hh.wait_pairs = 0;
   Hh.big_main = 0;
   if (nwait > 0) {
     HIPCHK(hipEventRecord(c->xev[0], s));
     HIPCHK(hipStreamWaitEvent(c->side, c->xev[0], 0));
-    hipLaunchKernelGGL(k_hull, dim3(nwait), dim3(HULL_CTHREADS), 0, c->side, Hh);
+    PairArgs Ph = P;
+    Ph.hot_only = 1;
+    if (g.x_dim == 16)
+      hipLaunchKernelGGL(k_pair<16>, dim3(nwait), dim3(P.waves * 64), c->lds_bytes, c->side, Ph);
+    else
+      hipLaunchKernelGGL(k_pair<12>, dim3(nwait), dim3(P.waves * 64), c->lds_bytes, c->side, Ph);
+    HIPCHK(hipGetLastError());
+    PairArgs Pt = P;
+    if (nside == 0) Pt.nrows = 0;
+    if (g.x_dim == 16)
+      hipLaunchKernelGGL(k_side<16>, dim3(nwait), dim3(HULL_CTHREADS), 0, c->side, Hh, Pt);
+    else
+      hipLaunchKernelGGL(k_side<12>, dim3(nwait), dim3(HULL_CTHREADS), 0, c->side, Hh, Pt);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->xev[1], c->side));
   }
-  HIPCHK(hipEventRecord(c->ev[0], s));
   if (g.x_dim == 16)
     hipLaunchKernelGGL(k_pair<16>, dim3(nblk), dim3(P.waves * 64), c->lds_bytes, s, P);
   else if (g.x_dim == 12)
@@ -549,6 +610,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   else
     return LQRO_E_ARG;
   HIPCHK(hipGetLastError());
+  if (nwait > 0) HIPCHK(hipStreamWaitEvent(s, c->xev[1], 0));
   HIPCHK(hipEventRecord(c->ev[1], s));
   Hh.block_base = nwait;
   Hh.wait_pairs = 0;
@@ -557,7 +619,6 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
     hipLaunchKernelGGL(k_hull, dim3(c->hull_blocks - nwait), dim3(HULL_CTHREADS), 0, s, Hh);
     HIPCHK(hipGetLastError());
   }
-  if (nwait > 0) HIPCHK(hipStreamWaitEvent(s, c->xev[1], 0));
   Hh.block_base = 0;
   hipLaunchKernelGGL(k_hull_big, dim3(c->hull_big_blocks), dim3(HULL_THREADS), 0, s, Hh);
   HIPCHK(hipGetLastError());
