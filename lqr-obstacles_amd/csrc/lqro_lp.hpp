@@ -64,7 +64,7 @@ __device__ __forceinline__ int first_violated(const float* planes, int i0, int n
   return n;
 }
 
-__device__ bool w_lp1(const float* planes, int planeNo, v3 lpt, v3 ldir, float radius, v3 opt,
+__device__ __forceinline__ bool w_lp1(const float* planes, int planeNo, v3 lpt, v3 ldir, float radius, v3 opt,
                       bool dirOpt, v3& result, int lane) {
   const float dotProduct = vdot(lpt, ldir);
   const float disc = sqrf(dotProduct) + sqrf(radius) - vdot(lpt, lpt);
@@ -107,7 +107,7 @@ __device__ bool w_lp1(const float* planes, int planeNo, v3 lpt, v3 ldir, float r
   return true;
 }
 
-__device__ bool w_lp2(const float* planes, int planeNo, float radius, v3 opt, bool dirOpt,
+__device__ __forceinline__ bool w_lp2(const float* planes, int planeNo, float radius, v3 opt, bool dirOpt,
                       v3& result, int lane) {
   const LPPlane pn = ld_plane(planes, planeNo);
   const float planeDist = vdot(pn.point, pn.normal);
@@ -144,7 +144,7 @@ __device__ bool w_lp2(const float* planes, int planeNo, float radius, v3 opt, bo
   return true;
 }
 
-__device__ int w_lp3(const float* planes, int m, double radius, v3 opt, bool dirOpt, v3& result,
+__device__ __forceinline__ int w_lp3(const float* planes, int m, double radius, v3 opt, bool dirOpt, v3& result,
                      int lane) {
   const float rf = (float)radius;
   if (dirOpt) result = vmul(opt, rf);
@@ -160,8 +160,12 @@ __device__ int w_lp3(const float* planes, int m, double radius, v3 opt, bool dir
 
 // linearProgram4: the projected planes of plane i are built in parallel and
 // compacted in j order (skipped same-direction parallels keep their order).
-__device__ void w_lp4(const float* planes, int m, int beginPlane, float radius, v3& result,
-                      float* proj, int lane) {
+__device__ __forceinline__ void w_lp4(const float* planes, int m, int beginPlane, float radius, v3& result,
+                      float* proj, int lane
+#ifdef LQRO_LP_PROFILE
+                      , int& lp4_iters
+#endif
+                      ) {
   float distance = 0.0f;
   for (int i = first_violated(planes, beginPlane, m, result, distance, lane); i < m;
        i = first_violated(planes, i + 1, m, result, distance, lane)) {
@@ -201,6 +205,9 @@ __device__ void w_lp4(const float* planes, int m, int beginPlane, float radius, 
     const v3 tmp = result;
     if (w_lp3(proj, np, radius, pi.normal, true, result, lane) < np) result = tmp;
     distance = vdot(pi.normal, vsub(pi.point, result));
+#ifdef LQRO_LP_PROFILE
+    ++lp4_iters;
+#endif
   }
 }
 

@@ -167,15 +167,13 @@ struct LpArgs {
   float* proj;          // per row npr x 8: linearProgram4's projected planes
   const double* vgoal;
   double* newv;
+  unsigned long long* prof;   // LQRO_LP_PROFILE: cycles per row
 };
 
-__global__ void __launch_bounds__(256) k_lp(LpArgs A) {
-  const int lane = threadIdx.x & 63;
-  const int lrow = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (lrow >= A.nrows) return;
+// one row's LP; `planes` holds its compacted plane list (LDS or global)
+__device__ __forceinline__ void lp_row(const LpArgs& A, int lrow, float* planes, int lane) {
   const int i = A.row_begin + lrow;
   const float* src = A.slots + (size_t)lrow * A.npr * 8;
-  float* planes = A.compact + (size_t)lrow * A.npr * 8;
   // orcaPlanes_ in push order (j order, LQRObstacles.cpp:1220)
   int m = 0;
   for (int base = 0; base < A.npr; base += 64) {
@@ -202,13 +200,59 @@ __global__ void __launch_bounds__(256) k_lp(LpArgs A) {
   const v3 pref = V3((float)A.vgoal[3 * i], (float)A.vgoal[3 * i + 1], (float)A.vgoal[3 * i + 2]);
   v3 nv = V3(0.0f, 0.0f, 0.0f);
   const int fail = w_lp3(planes, m, A.vmax, pref, false, nv, lane);          // :1228
+#ifdef LQRO_LP_PROFILE
+  int lp4_iters = 0;
+  if (fail < m)
+    w_lp4(planes, m, fail, (float)A.vmax, nv, A.proj + (size_t)lrow * A.npr * 8, lane, lp4_iters);
+  if (lane == 0 && A.prof && lrow < 4096) A.prof[32 + 4096 + lrow] = ((unsigned long long)m << 40) |
+                                               ((unsigned long long)fail << 20) | (unsigned)lp4_iters;
+#else
   if (fail < m)
     w_lp4(planes, m, fail, (float)A.vmax, nv, A.proj + (size_t)lrow * A.npr * 8, lane);  // :1230
+#endif
   if (lane == 0) {
     A.newv[3 * i] = nv.x;
     A.newv[3 * i + 1] = nv.y;
     A.newv[3 * i + 2] = nv.z;
   }
+}
+
+// plane list in global scratch (rows with more planes than LDS holds)
+__global__ void __launch_bounds__(256) k_lp(LpArgs A) {
+  const int lane = threadIdx.x & 63;
+  const int lrow = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (lrow >= A.nrows) return;
+  lp_row(A, lrow, A.compact + (size_t)lrow * A.npr * 8, lane);
+}
+
+// one wave per workgroup, the row's plane list in LDS (the LP rescans it for
+// every violated plane: LDS round trips instead of L2 ones)
+__global__ void __launch_bounds__(64) k_lp_lds(LpArgs A) {
+  extern __shared__ float lp_planes[];
+  const int lrow = blockIdx.x;
+  if (lrow >= A.nrows) return;
+#ifdef LQRO_LP_PROFILE
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
+  lp_row(A, lrow, lp_planes, threadIdx.x);
+#ifdef LQRO_LP_PROFILE
+  if (threadIdx.x == 0 && lrow < 8192) A.prof[32 + lrow] = __builtin_amdgcn_s_memtime() - t0;
+#endif
+}
+
+constexpr size_t kLpLdsMax = 64 * 1024;
+
+static hipError_t launch_lp(const LpArgs& La, hipStream_t s) {
+  const size_t lds = (size_t)La.npr * 32;
+  if (lds <= kLpLdsMax) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k_lp_lds,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLpLdsMax);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_lp_lds, dim3((unsigned)La.nrows), dim3(64), lds, s, La);
+  }
+  else
+    hipLaunchKernelGGL(k_lp, dim3((unsigned)((La.nrows + 3) / 4)), dim3(256), 0, s, La);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -626,9 +670,8 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   LpArgs La;
   La.npr = c->npr; La.nrows = c->nrows; La.row_begin = c->rb; La.vmax = g.vmax_lp;
   La.slots = c->d_planes; La.compact = c->d_lpcompact; La.proj = c->d_lpscratch;
-  La.vgoal = d_vgoal; La.newv = d_newv;
-  hipLaunchKernelGGL(k_lp, dim3((unsigned)((c->nrows + 3) / 4)), dim3(256), 0, s, La);
-  HIPCHK(hipGetLastError());
+  La.vgoal = d_vgoal; La.newv = d_newv; La.prof = c->d_prof;
+  HIPCHK(launch_lp(La, s));
   HIPCHK(hipEventRecord(c->ev[3], s));
   return LQRO_OK;
 }
@@ -695,9 +738,8 @@ int lqro_calculate_new_v(const float* planes, const int64_t* offsets, int32_t n_
   } else {
     LpArgs La;
     La.npr = (int)mmax; La.nrows = n_agents; La.row_begin = 0; La.vmax = vmax_lp;
-    La.slots = d_slots; La.compact = d_compact; La.proj = d_proj; La.vgoal = d_vg; La.newv = d_nv;
-    hipLaunchKernelGGL(k_lp, dim3((unsigned)((n_agents + 3) / 4)), dim3(256), 0, 0, La);
-    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+    La.slots = d_slots; La.compact = d_compact; La.proj = d_proj; La.vgoal = d_vg; La.newv = d_nv; La.prof = nullptr;
+    if (launch_lp(La, 0) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
         hipMemcpy(newv, d_nv, sizeof(double) * 3 * n_agents, hipMemcpyDeviceToHost) != hipSuccess)
       rc = LQRO_E_HIP;
   }
