@@ -126,6 +126,53 @@ __device__ __forceinline__ void argmax_step(double& v, int& q) {
   if (better(ov, oq, v, q)) { v = ov; q = oq; }
 }
 
+#ifndef LQRO_ARGMAX_PAIRS
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void max_step(double& v) {
+  v = fmax(v, dpp_d<CTRL, ROWS>(-INFINITY, v));
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void min_step(int& q) {
+  q = min(q, dpp_i<CTRL, ROWS>(INT_MAX, q));
+}
+// wave arg-max of (v, q), lowest q on ties, result in every lane: the wave
+// maximum of v (row_shr prefix maxima in each 16-lane row, row_bcast across
+// rows: lane 63 holds it), then the wave minimum of q over the lanes holding
+// that value, and v read from that lane (so a -0.0 / +0.0 tie returns the
+// winner's own zero, as the sequential scan would)
+__device__ __forceinline__ void wave_argmax(double& v, int& q) {
+  double m = v;
+  max_step<0x111, 0xF>(m);   // row_shr:1
+  max_step<0x112, 0xF>(m);   // row_shr:2
+  max_step<0x114, 0xF>(m);   // row_shr:4
+  max_step<0x118, 0xF>(m);   // row_shr:8
+  max_step<0x142, 0xA>(m);   // row_bcast:15
+  max_step<0x143, 0xC>(m);   // row_bcast:31
+  const long long b = __double_as_longlong(m);
+  const int lo = __builtin_amdgcn_readlane((int)b, 63);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+  m = __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+  int t = v == m ? q : INT_MAX;
+  min_step<0x111, 0xF>(t);
+  min_step<0x112, 0xF>(t);
+  min_step<0x114, 0xF>(t);
+  min_step<0x118, 0xF>(t);
+  min_step<0x142, 0xA>(t);
+  min_step<0x143, 0xC>(t);
+  const int qw = __builtin_amdgcn_readlane(t, 63);
+  const unsigned long long w = __ballot(v == m && q == qw);
+  if (w) {
+    const int wl = __ffsll((long long)w) - 1;
+    const long long vb = __double_as_longlong(v);
+    const int vlo = __builtin_amdgcn_readlane((int)vb, wl);
+    const int vhi = __builtin_amdgcn_readlane((int)(vb >> 32), wl);
+    v = __longlong_as_double(((long long)vhi << 32) | (unsigned)vlo);
+  } else {
+    v = m;
+  }
+  q = qw;
+}
+#else
 // wave arg-max of (v, q), lowest q on ties, result in every lane: row_shr
 // prefix maxima within each 16-lane row, row_bcast to combine the rows
 // (lane 63 then holds the result), readlane to broadcast
@@ -142,6 +189,7 @@ __device__ __forceinline__ void wave_argmax(double& v, int& q) {
   v = __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
   q = __builtin_amdgcn_readlane(q, 63);
 }
+#endif
 
 struct SliceSupport {
   const PairArgs& P;

@@ -168,6 +168,10 @@ struct LpArgs {
   const double* vgoal;
   double* newv;
   unsigned long long* prof;   // LQRO_LP_PROFILE: cycles per row
+  // rows whose linearProgram3 fails go to k_lp4 (null: linearProgram4 inline)
+  int* lp4_list;              // 6 ints per row: lrow, fail, m, nv.xyz (float bits)
+  int* lp4_count;
+  int* lp4_next;
 };
 
 // one row's LP; `planes` holds its compacted plane list (LDS or global)
@@ -207,6 +211,20 @@ __device__ __forceinline__ void lp_row(const LpArgs& A, int lrow, float* planes,
   if (lane == 0 && A.prof && lrow < 4096) A.prof[32 + 4096 + lrow] = ((unsigned long long)m << 40) |
                                                ((unsigned long long)fail << 20) | (unsigned)lp4_iters;
 #else
+  if (fail < m && A.lp4_list != nullptr) {
+    // linearProgram4 (:1230) in k_lp4, with its projected planes in LDS too:
+    // hand over the compacted planes and linearProgram3's result
+    float* dst = A.compact + (size_t)lrow * A.npr * 8;
+    if (dst != planes)
+      for (int q = lane; q < 8 * m; q += 64) dst[q] = planes[q];
+    if (lane == 0) {
+      const int k = atomicAdd(A.lp4_count, 1);
+      int* e = A.lp4_list + 6 * (size_t)k;
+      e[0] = lrow; e[1] = fail; e[2] = m;
+      e[3] = __float_as_int(nv.x); e[4] = __float_as_int(nv.y); e[5] = __float_as_int(nv.z);
+    }
+    return;
+  }
   if (fail < m)
     w_lp4(planes, m, fail, (float)A.vmax, nv, A.proj + (size_t)lrow * A.npr * 8, lane);  // :1230
 #endif
@@ -240,18 +258,58 @@ __global__ void __launch_bounds__(64) k_lp_lds(LpArgs A) {
 #endif
 }
 
-constexpr size_t kLpLdsMax = 64 * 1024;
+// linearProgram4 for the rows k_lp_lds listed (one wave per row): the planes
+// AND the projected planes in LDS, so the O(m^2)
+// rescans of linearProgram4's inner linearProgram3 stay out of L2
+__global__ void __launch_bounds__(64) k_lp4(LpArgs A) {
+  extern __shared__ float lp4_sm[];
+  float* planes = lp4_sm;
+  float* proj = lp4_sm + (size_t)A.npr * 8;
+  const int lane = threadIdx.x;
+  {
+    // one workgroup per listed row (a persistent loop over the list around
+    // these ballot-driven loops hung on gfx950; the extra workgroups exit at once)
+    const int job = blockIdx.x;
+    if (job >= *A.lp4_count) return;
+    const int* e = A.lp4_list + 6 * (size_t)job;
+    const int lrow = e[0], fail = e[1], m = e[2];
+    v3 nv = V3(__int_as_float(e[3]), __int_as_float(e[4]), __int_as_float(e[5]));
+    const float* src = A.compact + (size_t)lrow * A.npr * 8;
+    for (int q = lane; q < 8 * m; q += 64) planes[q] = src[q];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    w_lp4(planes, m, fail, (float)A.vmax, nv, proj, lane);                 // :1230
+    if (lane == 0) {
+      const int i = A.row_begin + lrow;
+      A.newv[3 * i] = nv.x;
+      A.newv[3 * i + 1] = nv.y;
+      A.newv[3 * i + 2] = nv.z;
+    }
+  }
+}
 
-static hipError_t launch_lp(const LpArgs& La, hipStream_t s) {
+constexpr size_t kLpLdsMax = 64 * 1024;
+constexpr size_t kLp4LdsMax = 128 * 1024;
+
+// La.lp4_count / lp4_next must be zero (or lp4_list null)
+static hipError_t launch_lp(LpArgs La, hipStream_t s) {
   const size_t lds = (size_t)La.npr * 32;
   if (lds <= kLpLdsMax) {
-    const hipError_t e = hipFuncSetAttribute((const void*)k_lp_lds,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLpLdsMax);
+    hipError_t e = hipFuncSetAttribute((const void*)k_lp_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)kLpLdsMax);
     if (e != hipSuccess) return e;
+    if (2 * lds > kLp4LdsMax) La.lp4_list = nullptr;
     hipLaunchKernelGGL(k_lp_lds, dim3((unsigned)La.nrows), dim3(64), lds, s, La);
-  }
-  else
+    e = hipGetLastError();
+    if (e != hipSuccess || La.lp4_list == nullptr) return e;
+    e = hipFuncSetAttribute((const void*)k_lp4, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLp4LdsMax);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_lp4, dim3((unsigned)La.nrows), dim3(64), 2 * lds, s, La);
+  } else {
+    La.lp4_list = nullptr;
     hipLaunchKernelGGL(k_lp, dim3((unsigned)((La.nrows + 3) / 4)), dim3(256), 0, s, La);
+  }
   return hipGetLastError();
 }
 
@@ -276,6 +334,7 @@ struct lqro_ctx {
   void* d_hbig;
   HullWide* d_hwide;
   int* d_hbag;
+  int* d_lp4;                // k_lp_lds -> k_lp4 row list (6 ints per row)
   int* d_hotlist;            // k_prio: likely inside-hull pairs (slots), computed first
   unsigned char* d_hotmark;  // per slot: in the hot list
   int hot_cap;
@@ -346,7 +405,7 @@ void lqro_destroy(lqro_ctx* c) {
   (void)hipSetDevice(c->cfg.device);
   void* ps[] = {c->d_R, c->d_TF, c->d_shash, c->d_T, c->d_NCF, c->d_S, c->d_x, c->d_vgoal, c->d_newv, c->d_A, c->d_B,
                 c->d_L, c->d_E, c->d_planes, c->d_lpscratch, c->d_lpcompact, c->d_recs, c->d_hq, c->d_hcount,
-                c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats, c->d_prof, c->d_rq, c->d_hbig, c->d_hwide, c->d_hbag, c->d_hotlist, c->d_hotmark, c->d_hfbest, c->d_hvpid, c->d_hstack};
+                c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats, c->d_prof, c->d_rq, c->d_hbig, c->d_hwide, c->d_hbag, c->d_lp4, c->d_hotlist, c->d_hotmark, c->d_hfbest, c->d_hvpid, c->d_hstack};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (int k = 0; k < 5; ++k)
@@ -411,6 +470,7 @@ static int ctx_alloc(lqro_ctx* c) {
   c->hot_cap = (int)std::max<size_t>(16384, slots / 32);
   HIPCHK(hipMalloc(&c->d_hotlist, sizeof(int) * c->hot_cap));
   HIPCHK(hipMalloc(&c->d_hotmark, slots ? slots : 1));
+  HIPCHK(hipMalloc(&c->d_lp4, sizeof(int) * 6 * (size_t)std::max(1, c->nrows)));
   return LQRO_OK;
 }
 
@@ -671,6 +731,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   La.npr = c->npr; La.nrows = c->nrows; La.row_begin = c->rb; La.vmax = g.vmax_lp;
   La.slots = c->d_planes; La.compact = c->d_lpcompact; La.proj = c->d_lpscratch;
   La.vgoal = d_vgoal; La.newv = d_newv; La.prof = c->d_prof;
+  La.lp4_list = c->d_lp4; La.lp4_count = c->d_hcount + 9; La.lp4_next = c->d_hcount + 10;
   HIPCHK(launch_lp(La, s));
   HIPCHK(hipEventRecord(c->ev[3], s));
   return LQRO_OK;
@@ -725,12 +786,15 @@ int lqro_calculate_new_v(const float* planes, const int64_t* offsets, int32_t n_
     }
   float *d_slots = nullptr, *d_compact = nullptr, *d_proj = nullptr;
   double *d_vg = nullptr, *d_nv = nullptr;
+  int *d_l4 = nullptr, *d_l4c = nullptr;
   int rc = LQRO_OK;
   if (hipMalloc(&d_slots, sizeof(float) * 8 * slots) != hipSuccess ||
       hipMalloc(&d_compact, sizeof(float) * 8 * slots) != hipSuccess ||
       hipMalloc(&d_proj, sizeof(float) * 8 * slots) != hipSuccess ||
       hipMalloc(&d_vg, sizeof(double) * 3 * n_agents) != hipSuccess ||
-      hipMalloc(&d_nv, sizeof(double) * 3 * n_agents) != hipSuccess) {
+      hipMalloc(&d_nv, sizeof(double) * 3 * n_agents) != hipSuccess ||
+      hipMalloc(&d_l4, sizeof(int) * 6 * n_agents) != hipSuccess ||
+      hipMalloc(&d_l4c, sizeof(int) * 2) != hipSuccess || hipMemset(d_l4c, 0, sizeof(int) * 2) != hipSuccess) {
     rc = LQRO_E_NOMEM;
   } else if (hipMemcpy(d_slots, h.data(), sizeof(float) * 8 * slots, hipMemcpyHostToDevice) != hipSuccess ||
              hipMemcpy(d_vg, vgoal, sizeof(double) * 3 * n_agents, hipMemcpyHostToDevice) != hipSuccess) {
@@ -739,11 +803,12 @@ int lqro_calculate_new_v(const float* planes, const int64_t* offsets, int32_t n_
     LpArgs La;
     La.npr = (int)mmax; La.nrows = n_agents; La.row_begin = 0; La.vmax = vmax_lp;
     La.slots = d_slots; La.compact = d_compact; La.proj = d_proj; La.vgoal = d_vg; La.newv = d_nv; La.prof = nullptr;
+    La.lp4_list = d_l4; La.lp4_count = d_l4c; La.lp4_next = d_l4c + 1;
     if (launch_lp(La, 0) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
         hipMemcpy(newv, d_nv, sizeof(double) * 3 * n_agents, hipMemcpyDeviceToHost) != hipSuccess)
       rc = LQRO_E_HIP;
   }
-  void* ps[] = {d_slots, d_compact, d_proj, d_vg, d_nv};
+  void* ps[] = {d_slots, d_compact, d_proj, d_vg, d_nv, d_l4, d_l4c};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   return rc;

@@ -2,6 +2,7 @@
 import sys, os, ctypes as C, numpy as np
 sys.path[:0] = [os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "lqr-obstacles_amd")]
 import lqro
+os.environ.setdefault("LQRO_HOT", "0")   # time k_pair alone
 libs = sys.argv[1:]
 N, H, NP = 1024, 100, 100
 x, vg = lqro.synthetic_swarm(N)
