@@ -32,6 +32,7 @@ namespace lqro {
 
 enum : int { kSliceOut = 0, kSliceIn = 1, kSliceMixed = 2 };
 constexpr int kMaxPW = 4;
+constexpr int kMaxKS = 4;   // H <= 64 kMaxKS = 256 (per-lane slice slots)
 #ifndef LQRO_PAIR_LB
 #define LQRO_PAIR_LB 768
 #endif  // 12 waves (3 per SIMD: <= 168 VGPRs); NP <= 256 (one 64-bit reachable mask per 64 points)
@@ -83,7 +84,6 @@ struct BlockTabs {
 struct WaveTabs {
   double* tr;                // H x 3
   double* sc;                // H: magnitude scale for the margins
-  double* ub;                // H: support bounds of the current query
   int* cls;                  // H
   int* cnt;                  // H: reachable points in the slice
   int* mixed;                // H: list of MIXED slices
@@ -245,9 +245,13 @@ struct SliceSupport {
     const double dn = __builtin_amdgcn_sqrt(d0 * d0 + d1 * d1 + d2 * d2);
     double cu = -INFINITY;
     int ck = INT_MAX;
-    for (int k = lane; k < P.H; k += 64) {
+    // the bounds stay in registers: lane owns slices lane + 64 s (H <= 64 kMaxKS)
+    double ubr[kMaxKS];
+#pragma unroll
+    for (int s = 0; s < kMaxKS; ++s) {
+      const int k = lane + 64 * s;
       double ub = -INFINITY;
-      if (W.cls[k] != kSliceOut) {
+      if (k < P.H && W.cls[k] != kSliceOut) {
         const double* Tk = B.T + 9 * k;
         const double w0 = Tk[0] * d0 + Tk[3] * d1 + Tk[6] * d2;
         const double w1 = Tk[1] * d0 + Tk[4] * d1 + Tk[7] * d2;
@@ -260,27 +264,33 @@ struct SliceSupport {
              __builtin_amdgcn_sqrt(a0 * a0 + a1 * a1 + a2 * a2) * P.umax + 1e-9 * dn * W.sc[k];
         if (ub > cu) { cu = ub; ck = k; }
       }
-      W.ub[k] = ub;
+      ubr[s] = ub;
     }
     wave_argmax(cu, ck);
     bv = -INFINITY;
     bq = INT_MAX;
     if (ck == INT_MAX) return;
     eval_slice(ck, d0, d1, d2, bv, bq);
-    // candidates: the other slices whose bound reaches bv
+    // candidates: the other slices whose bound reaches bv (usually none)
+    unsigned long long cb[kMaxKS];
+    unsigned long long any = 0;
+#pragma unroll
+    for (int s = 0; s < kMaxKS; ++s) {
+      const int k = lane + 64 * s;
+      cb[s] = __ballot(k < P.H && k != ck && ubr[s] > -INFINITY && ubr[s] >= bv);
+      any |= cb[s];
+    }
+    if (!any) return;
     wave_lds_sync();   // the previous query's readers of W.mixed are done
     int ncand = 0;
-    for (int base = 0; base < P.H; base += 64) {
-      const int k = base + lane;
-      const bool m = k < P.H && k != ck && W.ub[k] > -INFINITY && W.ub[k] >= bv;
-      const unsigned long long bal = __ballot(m);
-      if (m) W.mixed[ncand + __popcll(bal & ((1ull << lane) - 1ull))] = k;
-      ncand += __popcll(bal);
+#pragma unroll
+    for (int s = 0; s < kMaxKS; ++s) {
+      if ((cb[s] >> lane) & 1ull) W.mixed[ncand + __popcll(cb[s] & ((1ull << lane) - 1ull))] = lane + 64 * s;
+      ncand += __popcll(cb[s]);
     }
 #ifdef LQRO_PAIR_PROFILE
     pc[2] += ncand;
 #endif
-    if (ncand == 0) return;
     wave_lds_sync();
     double lv = -INFINITY;
     int lq = INT_MAX;
@@ -358,7 +368,6 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
     double* w = lds + P.lds_wave + (size_t)wave * P.wave_doubles;
     W.tr = w;            w += 3 * H;
     W.sc = w;            w += H;
-    W.ub = w;            w += H;
     W.mask = reinterpret_cast<unsigned long long*>(w);  w += H * P.PW;
     int* wi = reinterpret_cast<int*>(w);
     W.cls = wi;          wi += H;

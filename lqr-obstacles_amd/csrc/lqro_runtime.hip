@@ -339,6 +339,7 @@ struct lqro_ctx {
   unsigned char* d_hotmark;  // per slot: in the hot list
   int hot_cap;
   int hot_on;                // LQRO_HOT (default 1)
+  double hot_t, hot_r;       // k_prio horizon (s) and radius (m): LQRO_HOT_T, LQRO_HOT_R
   int hull_big_blocks;
   int n_cu;
   int side_cus;              // CUs running k_hull beside k_pair (LQRO_SIDE_HULL_CUS)
@@ -503,6 +504,10 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
     if (c->side_cus > c->n_cu / 2) c->side_cus = c->n_cu / 2;
     const char* h = getenv("LQRO_HOT");
     c->hot_on = h ? atoi(h) != 0 : 1;
+    const char* ht = getenv("LQRO_HOT_T");
+    const char* hr = getenv("LQRO_HOT_R");
+    c->hot_t = ht ? atof(ht) : 3.0;
+    c->hot_r = hr ? atof(hr) : 3.0;
   }
   c->rb = g.row_begin;
   c->re = (g.row_end > g.row_begin) ? g.row_end : g.n_agents;
@@ -512,7 +517,7 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
   c->npr = g.n_agents - 1;
   // LDS layout of k_pair (in doubles): block tables, then one region per wave
   const int H = g.horizon, NP = g.n_points, X = g.x_dim, XP = X + 1;
-  if (NP > 64 * kMaxPW) { delete c; return LQRO_E_ARG; }
+  if (NP > 64 * kMaxPW || H > 64 * kMaxKS) { delete c; return LQRO_E_ARG; }
   int off = 0;
   PairArgs& P = c->pa;
   P.XP = XP;
@@ -524,9 +529,9 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
   P.lds_TF = off; off += H;
   P.lds_H = off; off += H;
   P.lds_wave = off;
-  // tr 3H, sc H, ub H, mask H*PW (u64), cls/cnt/mixed 3H ints (mixed padded
-  // to even), GJK simplex 18
-  P.wave_doubles = 5 * H + H * P.PW + H + (H + (H & 1)) / 2 + 18;
+  // tr 3H, sc H, mask H*PW (u64), cls/cnt/mixed 3H ints (mixed padded to
+  // even), GJK simplex 18
+  P.wave_doubles = 4 * H + H * P.PW + H + (H + (H & 1)) / 2 + 18;
   const int budget = 160 * 1024 / 8;
   int waves = (budget - off) / P.wave_doubles;
   if (waves > LQRO_PAIR_LB / 64) waves = LQRO_PAIR_LB / 64;
@@ -658,7 +663,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   if (hot) {
     PrioArgs Q;
     Q.npr = c->npr; Q.nrows = c->nrows; Q.row_begin = c->rb; Q.X = g.x_dim; Q.x = d_x;
-    Q.t_hot = 3.0; Q.r2_hot = 3.0 * 3.0;   // seconds, metres (scheduling heuristic)
+    Q.t_hot = c->hot_t; Q.r2_hot = c->hot_r * c->hot_r;   // seconds, metres (scheduling heuristic)
     Q.list = c->d_hotlist; Q.mark = c->d_hotmark; Q.count = c->d_hcount + 6; Q.cap = c->hot_cap;
     const long nb = std::min<long>((slots + 255) / 256, 8L * c->n_cu);
     hipLaunchKernelGGL(k_prio, dim3((unsigned)nb), dim3(256), 0, s, Q);
