@@ -96,9 +96,6 @@ struct HullArgs {
   int* bag;                         // per block of k_hull: HULL_BAGCAP overflow face ids (-1: empty)
   int block_base;                   // scratch index of this launch's block 0
   int big_main;                     // k_hull_big takes the main queue (H*NP too large for LDS)
-  int wait_pairs;                   // poll the queue until k_pair has finished
-  int pair_blocks;                  //   (its workgroup count)
-  const int* pair_done;
   unsigned long long* stats;
   unsigned long long* prof;          // LQRO_HULL_PROFILE: per-phase cycles
 };
@@ -330,37 +327,31 @@ __device__ __forceinline__ int hl_scan(LT& L, int v, int* tot) {
 // Phases shared by both kernels
 // ---------------------------------------------------------------------------
 
-// Take the next job (pair slot), or -1.  Workers launched beside k_pair
-// (wait_pairs) poll: an entry is valid once k_pair's release-store made it
-// non-negative, and the queue is closed when every k_pair workgroup has
-// finished.
+// Take the next job (pair slot), or -1 when the queue holds no untaken entry.
 template <class LT>
 __device__ __forceinline__ int hull_take_job(const HullArgs& A, LT& L, bool retryq) {
   const int* queue = retryq ? A.rqueue : A.queue;
   const int* qcount = retryq ? A.rcount : A.count;
   int* qnext = retryq ? A.rnext : A.next;
   if (threadIdx.x == 0) {
-    const int job = atomicAdd(qnext, 1);
-    int slot = -1;
-    for (long spins = 0;; ++spins) {
-      const int cnt = __hip_atomic_load(qcount, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-      if (job < min(cnt, A.cap)) {
-        int v = __hip_atomic_load(queue + job, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        for (long w = 0; v < 0 && w < (1l << 26); ++w) {
-          __builtin_amdgcn_s_sleep(2);
-          v = __hip_atomic_load(queue + job, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        slot = v;
-        break;
+    // take an entry only if it is there (CAS on the head): a workgroup that
+    // finds the queue empty consumes no index, so entries a concurrent k_pair
+    // launch appends later are still taken (by the k_hull after the sweep)
+    int job = -1, slot = -1;
+    for (;;) {
+      const int nx = __hip_atomic_load(qnext, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      const int cnt = min(__hip_atomic_load(qcount, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT), A.cap);
+      if (nx >= cnt) break;
+      if (atomicCAS(qnext, nx, nx + 1) != nx) continue;
+      job = nx;
+      // counted before published: wait for k_pair's release store
+      int v = __hip_atomic_load(queue + job, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      for (long w = 0; v < 0 && w < (1l << 26); ++w) {
+        __builtin_amdgcn_s_sleep(2);
+        v = __hip_atomic_load(queue + job, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (retryq || !A.wait_pairs) break;
-      if (__hip_atomic_load(A.pair_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= A.pair_blocks) {
-        if (job < min(__hip_atomic_load(qcount, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT), A.cap))
-          continue;
-        break;
-      }
-      if (spins > (1l << 26)) { atomicAdd(&A.stats[4], 1ull); break; }   // bounded wait
-      __builtin_amdgcn_s_sleep(8);
+      slot = v;
+      break;
     }
     L.job = job;
     L.slot = slot;

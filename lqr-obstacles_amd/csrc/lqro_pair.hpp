@@ -43,7 +43,6 @@ struct PairArgs {
   int waves;
   int* row_counter;                   // persistent row queue (zeroed per step)
   int row_split;                      // pair ranges per row
-  int* pair_done;                     // finished workgroups (k_hull workers wait on it)
   int per_agent;
   double vmax, r2, r2_lo, r2_hi;      // reachable radius, its square, fast-test bounds
   double rad0, rad1, rad2, umax;      // sphere semi-axes (2 r_xy, 2 r_xy, 2 r_z); max |u_p|
@@ -646,9 +645,6 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
     __syncthreads();   // the row is done before s_row / the tables change
   }
   }   // row launch
-  // every queue entry of this workgroup is published: count it finished
-  if (threadIdx.x == 0)
-    __hip_atomic_fetch_add(P.pair_done, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 #ifdef LQRO_PAIR_PROFILE
   if (lane == 0 && P.prof)
     for (int k = 0; k < 16; ++k) atomicAdd(&P.prof[k], pp[k]);

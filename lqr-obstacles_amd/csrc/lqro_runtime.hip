@@ -447,7 +447,7 @@ static int ctx_alloc(lqro_ctx* c) {
   c->hull_cap = (int)(slots < (1u << 22) ? slots : (1u << 22));
   if (c->hull_cap < 1) c->hull_cap = 1;
   HIPCHK(hipMalloc(&c->d_hq, sizeof(int) * c->hull_cap));
-  // hull count, next, retry count, retry next, pair rows, pair_done, hot count, hot next, hot done
+  // hull count, next, retry count, retry next, pair rows, -, hot count, hot next, -, lp4 count, lp4 next
   HIPCHK(hipMalloc(&c->d_hcount, sizeof(int) * 16));
   c->d_hnext = c->d_hcount + 1;
   HIPCHK(hipMalloc(&c->d_rq, sizeof(int) * c->hull_cap));
@@ -642,7 +642,6 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   // add up to one workgroup per CU.  Hull jobs the prediction missed are
   // taken by the k_hull after the sweep.
   P.row_counter = c->d_hcount + 4;
-  P.pair_done = c->d_hcount + 5;
   HIPCHK(hipEventRecord(c->ev[0], s));
   HIPCHK(hipMemsetAsync(c->d_hcount, 0, sizeof(int) * 16, s));
   HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * 8, s));
@@ -688,10 +687,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   Hh.bag = c->d_hbag;
   Hh.stats = c->d_stats;
   Hh.prof = c->d_prof;
-  Hh.pair_done = P.pair_done;
-  Hh.pair_blocks = (int)(nblk + nside);
   Hh.block_base = 0;
-  Hh.wait_pairs = 0;
   Hh.big_main = 0;
   if (nwait > 0) {
     HIPCHK(hipEventRecord(c->xev[0], s));
@@ -722,7 +718,6 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   if (nwait > 0) HIPCHK(hipStreamWaitEvent(s, c->xev[1], 0));
   HIPCHK(hipEventRecord(c->ev[1], s));
   Hh.block_base = nwait;
-  Hh.wait_pairs = 0;
   Hh.big_main = lds_ok ? 0 : 1;
   if (lds_ok) {
     hipLaunchKernelGGL(k_hull, dim3(c->hull_blocks - nwait), dim3(HULL_CTHREADS), 0, s, Hh);

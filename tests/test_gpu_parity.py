@@ -134,3 +134,32 @@ def test_c3_full_step(lqro_mod, oracle, gains):
     rows_clean[rrecs["i"][inside]] = False
     assert np.array_equal(newv[rows_clean], rv[rows_clean])
     np.testing.assert_allclose(newv, rv, rtol=1e-5, atol=1e-6)
+
+
+def test_overlap_schedule_identical(lqro_mod, gains, monkeypatch):
+    """The step's schedule (k_prio hot list, side-stream hulls, side width,
+    hot radius) changes only the order of work: every record and every new
+    velocity is bit-identical across schedules and repeated steps."""
+    N, H, NP = 512, 100, 100          # 261,632 pairs: the overlap path is taken
+    x, vg = lqro_mod.synthetic_swarm(N, seed=3)
+    outs = []
+    for env in ({"LQRO_HOT": "0"}, {"LQRO_HOT": "1"}, {"LQRO_HOT": "1", "LQRO_SIDE_HULL_CUS": "32"},
+                {"LQRO_HOT": "1", "LQRO_HOT_R": "0.5"}):
+        for k in ("LQRO_HOT", "LQRO_SIDE_HULL_CUS", "LQRO_HOT_R"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        ctx = lqro_mod.Context(lqro_mod.config(N, H, NP, flags=lqro_mod.LQRO_FLAG_RECORDS))
+        ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
+        v1 = ctx.step(x, vg)
+        r1 = ctx.records()
+        v2 = ctx.step(x, vg)
+        ctx.close()
+        assert np.array_equal(v1, v2)
+        outs.append((v1, r1))
+    v0, r0 = outs[0]
+    assert ((r0["flags"] & 2) != 0).sum() > 0
+    for v, r in outs[1:]:
+        assert np.array_equal(v, v0)
+        for f in ("n_reach", "reach_hash", "flags", "facet", "dist", "normal", "plane_point", "plane_normal"):
+            assert np.array_equal(r[f], r0[f]), f
