@@ -109,6 +109,15 @@ int lqro_synthesize_gains(const lqro_model* m,
                           double* L  /* U*X */, double* E  /* U*3 */,
                           double* Lh /* 3*X */, double* Eh /* 3*3 */);
 
+/* The same synthesis for a swarm of heterogeneous agents, on the GPU (one
+ * agent per lane): models[n]; outputs are n consecutive blocks of the shapes
+ * above (A n*X*X, B n*X*U, c n*X, L n*U*X, E n*U*3, Lh n*3*X, Eh n*3*3), host
+ * arrays, any may be NULL.  Bit-identical to lqro_synthesize_gains per model.
+ * Feeds lqro_set_gains(..., per_agent = 1).  Synchronous. */
+int lqro_synthesize_gains_batch(const lqro_model* models, int32_t n,
+                                double* A, double* B, double* c, double* L, double* E,
+                                double* Lh, double* Eh, int32_t device);
+
 /* Replaces createSpheres (LQRO:735-750): NP Fibonacci-sphere points. */
 int lqro_sphere(int32_t n_points, double xy_radius, double z_radius, double* out /* NP*3 */);
 

@@ -33,6 +33,7 @@
 #include "lqro_lp.hpp"
 #include "lqro_pair.hpp"
 #include "lqro_hull.hpp"
+#include "lqro_synth.hpp"
 
 #define LQRO_PROF_WORDS (32 + 2 * 4096 + 16 + 16)   // hull: 32 counters + 2 words per job; pair: 16; hull wave phases: 16
 
@@ -763,6 +764,66 @@ int lqro_step(lqro_ctx* c, const double* x, const double* vgoal, double* newv) {
   HIPCHK(hipMemcpy(&hc, c->d_hcount, sizeof(int), hipMemcpyDeviceToHost));
   if (hc > c->hull_cap) return LQRO_E_OVERFLOW;
   return LQRO_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Gain synthesis (controlMatrices, LQRO:520-582): host for one agent type,
+// device for heterogeneous swarms (one agent per lane; lqro_synth.hpp)
+// ---------------------------------------------------------------------------
+int lqro_synthesize_gains(const lqro_model* md, double* Ao, double* Bo, double* co, double* Lo,
+                          double* Eo, double* Lho, double* Eho) {
+  if (!md) return LQRO_E_ARG;
+  synth::gains(md, Ao, Bo, co, Lo, Eo, Lho, Eho);
+  return LQRO_OK;
+}
+
+// per-agent output block, in doubles: A 256, B 64, c 16, L 64, E 12, Lh 48, Eh 9
+constexpr int kSynthOut[7] = {256, 64, 16, 64, 12, 48, 9};
+constexpr int kSynthStride = 469;
+
+__global__ void __launch_bounds__(64) k_synth(const lqro_model* models, int n, double* out) {
+  const int a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= n) return;
+  double* o = out + (size_t)a * kSynthStride;
+  synth::gains(models + a, o, o + 256, o + 320, o + 336, o + 400, o + 412, o + 460);
+}
+
+int lqro_synthesize_gains_batch(const lqro_model* models, int32_t n, double* A, double* B, double* c,
+                                double* L, double* E, double* Lh, double* Eh, int32_t device) {
+  if (!models || n <= 0) return LQRO_E_ARG;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) return LQRO_E_NODEVICE;
+  if (hipSetDevice(device) != hipSuccess) return LQRO_E_HIP;
+  lqro_model* d_m = nullptr;
+  double* d_out = nullptr;
+  int rc = LQRO_OK;
+  if (hipMalloc(&d_m, sizeof(lqro_model) * (size_t)n) != hipSuccess ||
+      hipMalloc(&d_out, sizeof(double) * kSynthStride * (size_t)n) != hipSuccess) {
+    rc = LQRO_E_NOMEM;
+  } else if (hipMemcpy(d_m, models, sizeof(lqro_model) * (size_t)n, hipMemcpyHostToDevice) != hipSuccess) {
+    rc = LQRO_E_HIP;
+  } else {
+    hipLaunchKernelGGL(k_synth, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, 0, (const lqro_model*)d_m, (int)n,
+                       d_out);
+    std::vector<double> h((size_t)kSynthStride * n);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(h.data(), d_out, sizeof(double) * h.size(), hipMemcpyDeviceToHost) != hipSuccess) {
+      rc = LQRO_E_HIP;
+    } else {
+      double* outs[7] = {A, B, c, L, E, Lh, Eh};
+      int off = 0;
+      for (int k = 0; k < 7; ++k) {
+        if (outs[k])
+          for (int a = 0; a < n; ++a)
+            memcpy(outs[k] + (size_t)a * kSynthOut[k], h.data() + (size_t)a * kSynthStride + off,
+                   sizeof(double) * kSynthOut[k]);
+        off += kSynthOut[k];
+      }
+    }
+  }
+  if (d_m) (void)hipFree(d_m);
+  if (d_out) (void)hipFree(d_out);
+  return rc;
 }
 
 int lqro_calculate_new_v(const float* planes, const int64_t* offsets, int32_t n_agents,

@@ -1,230 +1,10 @@
-// lqro_synth.cpp — setup-time host code of liblqro.so: the hover linearisation
-// and the two infinite-horizon Riccati iterations that produce the gains the
-// pair loop reads.  Replaces controlMatrices (LQRObstacles.cpp:520-582),
-// linearizeDiscretize (:456-471), f (:368-397), Jacobian_fx/fu (:421-441),
-// createSpheres (:735-750) and the matrix semantics they rely on
-// (include/matrix.h: operator* :218-231, operator! :603-671, operator% :370-442,
-// exp :763-790).
-//
-// Everything here runs once per agent type on the host (the reference does it
-// once per agent in _tmain, LQRObstacles.cpp:1370-1373).  It is written so that
-// every rounding happens where the reference's rounds: compiled with
-// -ffp-contract=off, products accumulate from 0.0 in k order, expression
-// chains associate left to right.  tests/test_synth.py checks it bit-for-bit.
+// lqro_synth.cpp — setup-time host helpers of liblqro.so: the model defaults
+// (setup(), LQRObstacles.cpp:169-189, 1275-1286, 559-561) and createSpheres
+// (:735-750).  The gain synthesis itself (controlMatrices) is shared by the
+// host and the device: lqro_synth.hpp, entry points in lqro_runtime.hip.
 #include <cmath>
-#include <cstring>
 
 #include "../../include/lqro.h"
-
-namespace {
-
-template <int R, int C>
-struct Mat {
-  double e[R * C];
-  double& operator()(int r, int c) { return e[r * C + c]; }
-  double operator()(int r, int c) const { return e[r * C + c]; }
-  static Mat zero() { Mat m; for (double& v : m.e) v = 0.0; return m; }
-};
-template <int N>
-Mat<N, N> eye() {
-  Mat<N, N> m;
-  for (int i = 0; i < N; ++i)
-    for (int j = 0; j < N; ++j) m(i, j) = (i == j ? 1.0 : 0.0);
-  return m;
-}
-template <int R, int K, int C>
-Mat<R, C> operator*(const Mat<R, K>& a, const Mat<K, C>& b) {
-  Mat<R, C> m;
-  for (int i = 0; i < R; ++i)
-    for (int j = 0; j < C; ++j) {
-      double acc = 0.0;
-      for (int k = 0; k < K; ++k) acc += a(i, k) * b(k, j);
-      m(i, j) = acc;
-    }
-  return m;
-}
-template <int R, int C>
-Mat<R, C> operator+(const Mat<R, C>& a, const Mat<R, C>& b) {
-  Mat<R, C> m; for (int i = 0; i < R * C; ++i) m.e[i] = a.e[i] + b.e[i]; return m;
-}
-template <int R, int C>
-Mat<R, C> operator-(const Mat<R, C>& a, const Mat<R, C>& b) {
-  Mat<R, C> m; for (int i = 0; i < R * C; ++i) m.e[i] = a.e[i] - b.e[i]; return m;
-}
-template <int R, int C>
-Mat<R, C> operator-(const Mat<R, C>& a) {
-  Mat<R, C> m; for (int i = 0; i < R * C; ++i) m.e[i] = -a.e[i]; return m;
-}
-// matrix*scalar and scalar*matrix both evaluate elem*s in the reference
-template <int R, int C>
-Mat<R, C> operator*(const Mat<R, C>& a, double s) {
-  Mat<R, C> m; for (int i = 0; i < R * C; ++i) m.e[i] = a.e[i] * s; return m;
-}
-template <int R, int C>
-Mat<R, C> operator*(double s, const Mat<R, C>& a) { return a * s; }
-template <int R, int C>
-Mat<R, C> operator/(const Mat<R, C>& a, double s) {
-  Mat<R, C> m; for (int i = 0; i < R * C; ++i) m.e[i] = a.e[i] / s; return m;
-}
-template <int R, int C>
-Mat<C, R> tr(const Mat<R, C>& a) {
-  Mat<C, R> m;
-  for (int i = 0; i < C; ++i)
-    for (int j = 0; j < R; ++j) m(i, j) = a(j, i);
-  return m;
-}
-
-// full-pivot Gauss-Jordan, pivot = first strict maximum in (row, col) scan order
-template <int N>
-Mat<N, N> inverse(const Mat<N, N>& q) {
-  Mat<N, N> m = q, inv = eye<N>();
-  int rp[N], cp[N];
-  for (int i = 0; i < N; ++i) rp[i] = cp[i] = i;
-  for (int k = 0; k < N; ++k) {
-    double best = 0.0; int br = k, bc = k;
-    for (int i = k; i < N; ++i)
-      for (int j = k; j < N; ++j) {
-        double a = std::fabs(m(rp[i], cp[j]));
-        if (a > best) { best = a; br = i; bc = j; }
-      }
-    int t = rp[k]; rp[k] = rp[br]; rp[br] = t;
-    t = cp[k]; cp[k] = cp[bc]; cp[bc] = t;
-    for (int i = k + 1; i < N; ++i) {
-      double f = m(rp[i], cp[k]) / m(rp[k], cp[k]);
-      for (int j = k + 1; j < N; ++j) m(rp[i], cp[j]) -= f * m(rp[k], cp[j]);
-      for (int j = 0; j < k; ++j) inv(rp[i], rp[j]) -= f * inv(rp[k], rp[j]);
-      inv(rp[i], rp[k]) = -f;
-    }
-  }
-  for (int k = N - 1; k >= 0; --k) {
-    double qk = m(rp[k], cp[k]);
-    for (int j = 0; j < N; ++j) inv(rp[k], j) /= qk;
-    for (int i = 0; i < k; ++i) {
-      double f = m(rp[i], cp[k]);
-      for (int j = 0; j < N; ++j) inv(rp[i], j) -= f * inv(rp[k], j);
-    }
-  }
-  for (int i = 0; i < N; ++i)
-    for (int j = 0; j < N; ++j) m(cp[i], j) = inv(rp[i], j);
-  return m;
-}
-
-// P X = Q by full-pivot elimination with the reference's final reshuffle
-template <int N, int C>
-Mat<N, C> solve(const Mat<N, N>& p, const Mat<N, C>& q) {
-  Mat<N, N> m = p;
-  Mat<N, C> x = q;
-  int rp[N], cp[N], irp[N];
-  for (int i = 0; i < N; ++i) rp[i] = cp[i] = i;
-  for (int k = 0; k < N; ++k) {
-    double best = 0.0; int br = k, bc = k;
-    for (int i = k; i < N; ++i)
-      for (int j = k; j < N; ++j) {
-        double a = std::fabs(m(rp[i], cp[j]));
-        if (a > best) { best = a; br = i; bc = j; }
-      }
-    int t = rp[k]; rp[k] = rp[br]; rp[br] = t;
-    t = cp[k]; cp[k] = cp[bc]; cp[bc] = t;
-    for (int i = k + 1; i < N; ++i) {
-      double f = m(rp[i], cp[k]) / m(rp[k], cp[k]);
-      for (int j = k + 1; j < N; ++j) m(rp[i], cp[j]) -= f * m(rp[k], cp[j]);
-      for (int j = 0; j < C; ++j) x(rp[i], j) -= f * x(rp[k], j);
-    }
-  }
-  for (int k = N - 1; k >= 0; --k) {
-    double qk = m(rp[k], cp[k]);
-    for (int j = 0; j < C; ++j) x(rp[k], j) /= qk;
-    for (int i = 0; i < k; ++i) {
-      double f = m(rp[i], cp[k]);
-      for (int j = 0; j < C; ++j) x(rp[i], j) -= f * x(rp[k], j);
-    }
-  }
-  for (int i = 0; i < N; ++i) irp[rp[i]] = i;
-  for (int i = 0; i < N; ++i) {
-    for (int j = 0; j < C; ++j) { double t = x(cp[i], j); x(cp[i], j) = x(rp[i], j); x(rp[i], j) = t; }
-    rp[irp[cp[i]]] = rp[i];
-    irp[rp[i]] = irp[cp[i]];
-  }
-  return x;
-}
-
-template <int N>
-double norm1(const Mat<N, N>& q) {
-  double best = 0.0;
-  for (int j = 0; j < N; ++j) {
-    double s = 0.0;
-    for (int i = 0; i < N; ++i) s += std::fabs(q(i, j));
-    if (s > best) best = s;
-  }
-  return best;
-}
-
-// degree-7 Pade with scaling and squaring
-template <int N>
-Mat<N, N> expm(const Mat<N, N>& q) {
-  const double b0 = 1729728e1, b1 = 864864e1, b2 = 199584e1, b3 = 2772e2, b4 = 252e2,
-               b5 = 1512e0, b6 = 56e0, b7 = 1e0, lim = 9.504178996162932e-1;
-  Mat<N, N> A = q;
-  double c = std::ceil(std::log(norm1(A) / lim) * M_LOG2E);
-  int s = (int)(0.0 < c ? c : 0.0);
-  double p2 = std::pow(2.0, s);
-  for (double& v : A.e) v /= p2;
-  Mat<N, N> A2 = A * A, A4 = A2 * A2, A6 = A2 * A4, I = eye<N>();
-  Mat<N, N> U = A * (A6 * b7 + A4 * b5 + A2 * b3 + I * b1);
-  Mat<N, N> V = A6 * b6 + A4 * b4 + A2 * b2 + I * b0;
-  Mat<N, N> R = solve(V - U, V + U);
-  for (int i = 0; i < s; ++i) R = R * R;
-  return R;
-}
-
-typedef Mat<3, 1> Vec3;
-Mat<3, 3> skew(const Vec3& v) {
-  Mat<3, 3> m = Mat<3, 3>::zero();
-  m(0, 1) = -v.e[2]; m(0, 2) = v.e[1];
-  m(1, 0) = v.e[2];  m(1, 2) = -v.e[0];
-  m(2, 0) = -v.e[1]; m(2, 1) = v.e[0];
-  return m;
-}
-double hypot3(const Vec3& v) {
-  double X = std::fabs(v.e[0]), Y = std::fabs(v.e[1]), Z = std::fabs(v.e[2]);
-  if (X > Y && X > Z) return X * std::sqrt(1.0 + (Y / X) * (Y / X) + (Z / X) * (Z / X));
-  if (Y > Z) return Y * std::sqrt(1.0 + (X / Y) * (X / Y) + (Z / Y) * (Z / Y));
-  return Z * std::sqrt(1.0 + (X / Z) * (X / Z) + (Y / Z) * (Y / Z));
-}
-
-struct Quad {
-  double dt, g, mass, kM, lat, arm, h;
-  Mat<3, 3> J, Jinv;
-};
-
-// hover dynamics x' = f(x, R, u), 16-state quadrotor (position, velocity,
-// rotation error, body rates, rotor forces)
-Mat<16, 1> dynamics(const Quad& q, const Mat<16, 1>& x, const Mat<3, 3>& R, const Mat<4, 1>& u) {
-  Vec3 eX = Vec3::zero(), eY = Vec3::zero(), eZ = Vec3::zero();
-  eX.e[0] = 1; eY.e[1] = 1; eZ.e[2] = 1;
-  Vec3 v, r, w;
-  double F[4];
-  for (int k = 0; k < 3; ++k) { v.e[k] = x.e[3 + k]; r.e[k] = x.e[6 + k]; w.e[k] = x.e[9 + k]; }
-  for (int k = 0; k < 4; ++k) F[k] = x.e[12 + k];
-  Mat<16, 1> xd;
-  for (int k = 0; k < 3; ++k) xd.e[k] = v.e[k];
-  Vec3 acc = -q.g * eZ + R * expm(skew(r)) * ((F[0] + F[1] + F[2] + F[3]) / q.mass) * eZ;
-  for (int k = 0; k < 3; ++k) xd.e[3 + k] = acc.e[k];
-  double l = hypot3(r);
-  Vec3 rd;
-  if (0.5 * l > 0.0)
-    rd = w + 0.5 * skew(r) * w + (1.0 - 0.5 * l / std::tan(0.5 * l)) * skew(r / l) * (skew(r / l) * w);
-  else
-    rd = w + 0.5 * skew(r) * w;
-  for (int k = 0; k < 3; ++k) xd.e[6 + k] = rd.e[k];
-  Vec3 wd = q.Jinv * (q.arm * (F[1] - F[3]) * eX + q.arm * (F[2] - F[0]) * eY +
-                      (F[0] - F[1] + F[2] - F[3]) * q.kM * eZ - skew(w) * q.J * w);
-  for (int k = 0; k < 3; ++k) xd.e[9 + k] = wd.e[k];
-  for (int k = 0; k < 4; ++k) xd.e[12 + k] = (u.e[k] - F[k]) * q.lat;
-  return xd;
-}
-
-}  // namespace
 
 extern "C" void lqro_model_default(lqro_model* m) {
   m->dt = 1.0 / 30.0;
@@ -254,101 +34,5 @@ extern "C" int lqro_sphere(int32_t np, double xy_radius, double z_radius, double
     z -= dz;
     lon += dlong;
   }
-  return LQRO_OK;
-}
-
-extern "C" int lqro_synthesize_gains(const lqro_model* md, double* Ao, double* Bo, double* co,
-                                     double* Lo, double* Eo, double* Lho, double* Eho) {
-  if (!md) return LQRO_E_ARG;
-  Quad q;
-  q.dt = md->dt; q.g = md->gravity; q.mass = md->mass; q.kM = md->moment_const;
-  q.lat = md->thrust_latency; q.arm = md->length; q.h = md->j_step;
-  q.J = md->inertia * eye<3>();
-  q.Jinv = inverse(q.J);
-  const double hover = q.g * q.mass / 4;
-  Mat<4, 1> u0;
-  for (double& v : u0.e) v = hover;
-  Mat<16, 1> x0 = Mat<16, 1>::zero();
-  for (int k = 12; k < 16; ++k) x0.e[k] = hover;
-  Mat<3, 3> R0 = eye<3>();
-
-  // central-difference Jacobians, then A = e^{F dt}, B/c by Simpson's rule
-  Mat<16, 16> F;
-  Mat<16, 4> G;
-  {
-    Mat<16, 1> xr = x0, xl = x0;
-    for (int i = 0; i < 16; ++i) {
-      xr.e[i] += q.h; xl.e[i] -= q.h;
-      Mat<16, 1> col = (dynamics(q, xr, R0, u0) - dynamics(q, xl, R0, u0)) / (2 * q.h);
-      for (int k = 0; k < 16; ++k) F(k, i) = col.e[k];
-      xr.e[i] = xl.e[i] = x0.e[i];
-    }
-    Mat<4, 1> ur = u0, ul = u0;
-    for (int i = 0; i < 4; ++i) {
-      ur.e[i] += q.h; ul.e[i] -= q.h;
-      Mat<16, 1> col = (dynamics(q, x0, R0, ur) - dynamics(q, x0, R0, ul)) / (2 * q.h);
-      for (int k = 0; k < 16; ++k) G(k, i) = col.e[k];
-      ur.e[i] = ul.e[i] = u0.e[i];
-    }
-  }
-  Mat<16, 1> xdot = dynamics(q, x0, R0, u0);
-  Mat<16, 16> A = expm(q.dt * F);
-  Mat<16, 16> Int = (q.dt / 6.0) * (eye<16>() + 4.0 * expm(0.5 * q.dt * F) + A);
-  Mat<16, 4> B = Int * G;
-  Mat<16, 1> c = Int * xdot;
-
-  // velocity LQR: 300 Riccati sweeps with a velocity-tracking term
-  Mat<3, 16> Vs = Mat<3, 16>::zero(), Ps = Mat<3, 16>::zero();
-  Vs(0, 3) = Vs(1, 4) = Vs(2, 5) = 1;
-  Ps(0, 0) = Ps(1, 1) = Ps(2, 2) = 1;
-  Mat<3, 3> Qv = md->qv * eye<3>(), Qp = md->qp * eye<3>();
-  Mat<4, 4> Rw = md->r * eye<4>();
-  Mat<16, 16> Qx = Mat<16, 16>::zero();
-  Mat<16, 16> At = tr(A);
-  Mat<4, 16> Bt = tr(B);
-  Mat<16, 3> Vt = tr(Vs);
-  Mat<16, 16> S = Vt * Qv * Vs;
-  Mat<16, 3> T = -Vt * Qv;
-  for (int it = 0; it < 300; ++it) {
-    Mat<16, 4> K = At * S * B * inverse(Rw + Bt * S * B);
-    Mat<16, 3> Tn = -Vt * Qv + At * T - K * Bt * T;
-    Mat<16, 16> Sn = Vt * Qv * Vs + Qx + At * S * A - K * (Bt * S * A);
-    T = Tn;
-    S = Sn;
-  }
-  Mat<4, 4> Ri = inverse(Rw + Bt * S * B);
-  Mat<4, 16> L = -Ri * Bt * S * A;
-  Mat<4, 3> E = -Ri * Bt * T;
-
-  // position LQR on the closed velocity loop, with the cross term
-  const double wgt = md->pos_weight;
-  Mat<16, 16> Qpt = tr(Ps) * Qp * Ps + wgt * tr(L) * Rw * L;
-  Mat<3, 3> Rt = wgt * tr(E) * Rw * E;
-  Mat<3, 16> Pt = wgt * tr(E) * Rw * L;
-  Mat<16, 16> Acl = A + B * L;
-  Mat<16, 3> Bcl = B * E;
-  Mat<16, 16> Aclt = tr(Acl);
-  Mat<3, 16> Bclt = tr(Bcl);
-  Mat<16, 3> Ptt = tr(Pt);
-  Mat<16, 16> St = Qpt;
-  Mat<16, 3> Tt = -tr(Ps) * Qp;
-  for (int it = 0; it < 300; ++it) {
-    Mat<16, 3> K = (Ptt + Aclt * St * Bcl) * inverse(Rt + Bclt * St * Bcl);
-    Mat<16, 3> Ttn = -tr(Ps) * Qp + Aclt * Tt - K * Bclt * Tt;
-    Mat<16, 16> Stn = Qpt + Aclt * St * Acl - K * (Pt + Bclt * St * Acl);
-    Tt = Ttn;
-    St = Stn;
-  }
-  Mat<3, 3> RRi = inverse(Rt + Bclt * St * Bcl);
-  Mat<3, 16> Lh = -RRi * (Pt + Bclt * St * Acl);
-  Mat<3, 3> Eh = -RRi * (Bclt * Tt);
-
-  if (Ao) std::memcpy(Ao, A.e, sizeof A.e);
-  if (Bo) std::memcpy(Bo, B.e, sizeof B.e);
-  if (co) std::memcpy(co, c.e, sizeof c.e);
-  if (Lo) std::memcpy(Lo, L.e, sizeof L.e);
-  if (Eo) std::memcpy(Eo, E.e, sizeof E.e);
-  if (Lho) std::memcpy(Lho, Lh.e, sizeof Lh.e);
-  if (Eho) std::memcpy(Eho, Eh.e, sizeof Eh.e);
   return LQRO_OK;
 }

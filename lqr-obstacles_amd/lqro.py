@@ -71,7 +71,7 @@ EXPORTS = (
     "lqro_config_default", "lqro_model_default", "lqro_synthesize_gains", "lqro_sphere",
     "lqro_create", "lqro_destroy", "lqro_set_gains", "lqro_step", "lqro_step_device",
     "lqro_get_records", "lqro_get_stats", "lqro_get_timings", "lqro_status_string",
-    "lqro_version", "lqro_calculate_new_v",
+    "lqro_version", "lqro_calculate_new_v", "lqro_synthesize_gains_batch",
 )
 
 _lib = None
@@ -89,6 +89,7 @@ def lib() -> C.CDLL:
         L.lqro_config_default.argtypes = [C.POINTER(Config), i32, i32, i32]
         L.lqro_model_default.argtypes = [C.POINTER(Model)]
         L.lqro_synthesize_gains.argtypes = [C.POINTER(Model)] + [vp] * 7
+        L.lqro_synthesize_gains_batch.argtypes = [C.POINTER(Model), i32] + [vp] * 7 + [i32]
         L.lqro_sphere.argtypes = [i32, dbl, dbl, vp]
         L.lqro_create.argtypes = [C.POINTER(Config), C.POINTER(vp)]
         L.lqro_destroy.argtypes = [vp]
@@ -132,6 +133,21 @@ def synthesize_gains(model: Model | None = None) -> dict:
     _check(lib().lqro_synthesize_gains(C.byref(m), *[_p(out[k]) for k in
                                                    ("A", "B", "c", "L", "E", "Lh", "Eh")]),
            "lqro_synthesize_gains")
+    return out
+
+
+GAIN_SHAPES = dict(A=(16, 16), B=(16, 4), c=(16,), L=(4, 16), E=(4, 3), Lh=(3, 16), Eh=(3, 3))
+
+
+def synthesize_gains_batch(models, device: int = 0) -> dict:
+    """controlMatrices for heterogeneous agents, on the GPU (one agent per
+    lane): arrays with a leading agent axis, bit-identical to
+    synthesize_gains(models[k]); L and E feed Context.set_gains(per_agent=1)."""
+    n = len(models)
+    arr = (Model * n)(*models)
+    out = {k: np.zeros((n,) + s) for k, s in GAIN_SHAPES.items()}
+    _check(lib().lqro_synthesize_gains_batch(arr, n, *[_p(out[k]) for k in GAIN_SHAPES], device),
+           "lqro_synthesize_gains_batch")
     return out
 
 
