@@ -119,14 +119,21 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; more ranks than GPUs (a rehearsal on a smaller box)
+    # share them round-robin.  LQRO_BENCH_BACKEND=gloo rehearses the exchange
+    # without RCCL (the driver's runs use the default, RCCL).
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    backend = os.environ.get("LQRO_BENCH_BACKEND", "nccl")
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     dist = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -222,7 +229,8 @@ def main():
             "n_agents": N, "horizon": HORIZON, "n_points": N_POINTS, "x_dim": X_DIM,
             "pairs_per_step": pairs_step,
             "parallelism": f"rows sharded over {world} rank(s)" +
-                           (" + RCCL all-gather of newV" if world > 1 else ""),
+                           ((" + RCCL all-gather of newV" if backend == "nccl" else f" + {backend} all-gather of newV")
+                            if world > 1 else ""),
         },
         "roofline": {
             "bound": "valu-fp64",
