@@ -481,7 +481,7 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
   *out = nullptr;
   const lqro_config& g = *cfg;
   if (g.n_agents < 2 || (g.x_dim != 16 && g.x_dim != 12) || g.u_dim != 4 || g.horizon < 1 ||
-      g.n_points < 1 || g.vmax_reach <= 0)
+      g.n_points < 1 || g.vmax_reach <= 0 || g.n_points > 64 * kMaxPW || g.horizon > 64 * kMaxKS)
     return LQRO_E_ARG;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= g.device) return LQRO_E_NODEVICE;

@@ -163,3 +163,27 @@ def test_overlap_schedule_identical(lqro_mod, gains, monkeypatch):
         assert np.array_equal(v, v0)
         for f in ("n_reach", "reach_hash", "flags", "facet", "dist", "normal", "plane_point", "plane_normal"):
             assert np.array_equal(r[f], r0[f]), f
+
+
+@pytest.mark.parametrize("case", ["two_agents", "far_apart", "max_horizon"])
+def test_edge_cases(lqro_mod, oracle, gains, case):
+    """Edge sizes: a single pair each way; a swarm so sparse that no pair
+    emits a plane (every LP sees zero planes); the largest horizon the kernels
+    take (H = 256 slices, 4 per lane) with NP = 50."""
+    if case == "two_agents":
+        x, vg = lqro_mod.synthetic_swarm(2, box=1.5, seed=2)
+        H, NP = 50, 100
+    elif case == "far_apart":
+        x, vg = lqro_mod.synthetic_swarm(6, box=4000.0, seed=3)
+        H, NP = 30, 50
+    else:
+        x, vg = lqro_mod.synthetic_swarm(6, box=4.0, seed=4)
+        H, NP = 256, 50
+    newv, recs, st, rv, rrecs = _run(lqro_mod, oracle, gains, x, vg, H, NP)
+    _compare(recs, rrecs)
+    if case == "far_apart":
+        assert st["planes"] == 0 and st["inside"] == 0
+    inside = (rrecs["flags"] & 2) != 0
+    for r, q in zip(recs[inside], rrecs[inside]):
+        assert np.array_equal(r["facet"], q["facet"]) and r["dist"] == q["dist"]
+    np.testing.assert_allclose(newv, rv, rtol=1e-5, atol=1e-6)

@@ -74,6 +74,10 @@ def test_bad_config_rejected(lqro_mod):
     assert L.lqro_create(C.byref(bad), C.byref(h)) == -1
     bad = lqro_mod.config(8, 0, 100)
     assert L.lqro_create(C.byref(bad), C.byref(h)) == -1
+    bad = lqro_mod.config(8, 257, 100)             # horizon beyond the per-lane slice slots
+    assert L.lqro_create(C.byref(bad), C.byref(h)) == -1
+    bad = lqro_mod.config(8, 50, 257)              # points beyond the 4 reachable-mask words
+    assert L.lqro_create(C.byref(bad), C.byref(h)) == -1
     assert L.lqro_create(None, C.byref(h)) == -1
 
 
