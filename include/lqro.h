@@ -164,6 +164,53 @@ int lqro_get_stats(lqro_ctx* ctx, int64_t* stats8);
  * the context's stream: [0]=pair sweep+GJK, [1]=hull, [2]=LP, [3]=whole step. */
 int lqro_get_timings(lqro_ctx* ctx, float* ms4);
 
+/* ---- the per-agent step after the pair loop ------
+ * Replaces the agent loop LQRO:1437-1446: vGoal = newV; u = findU()
+ * (riccatiControllerSteady, LQRO:594-617); propagateU (propagate,
+ * LQRO:473-486) of the true state; kalmanFilter1 (LQRO:488-505); the
+ * observation z = sampleGaussian(h(xTrue, RotTrue), N) (LQRO:1442);
+ * kalmanFilter2 (LQRO:507-518); vGoal = findVGoal()
+ * (riccatiControllerSteadyPosition, LQRO:619-645).  Quadrotor::visualize
+ * (Callisto) is not part of it.  X = 16, U = 4, Z = 6.
+ * The reference draws its noise from rand() in agent order (normal(),
+ * LQRO:334-350): the caller supplies the draws, LQRO_NORMALS_PER_AGENT per
+ * agent (16 for propagate, then 6 for the observation); lqro_normals
+ * reproduces the stream. */
+#define LQRO_NORMALS_PER_AGENT 22
+
+typedef struct lqro_agents {
+  double* x;             /* n*16  Quadrotor::x: the estimate lqro_step reads     */
+  double* rot;           /* n*9   Quadrotor::Rot                                 */
+  double* x_true;        /* n*16  Quadrotor::xTrue                               */
+  double* rot_true;      /* n*9   Quadrotor::RotTrue                             */
+  double* P;             /* n*256 Quadrotor::P, state covariance                 */
+  double* vgoal;         /* n*3   in: newV (lqro_step); out: findVGoal()         */
+  double* u;             /* n*4   out: findU(); may be NULL                      */
+  const double* u_goal;  /* n*4   Quadrotor::uGoal                               */
+  const double* p_goal;  /* n*3   Quadrotor::pGoal                               */
+  const double* L;       /* U*X   gains (Quadrotor::L,E,l,Lh,Eh): one block, or  */
+  const double* E;       /* U*3     n blocks with per_agent_gains = 1            */
+  const double* l;       /* U                                                    */
+  const double* Lh;      /* 3*X                                                  */
+  const double* Eh;      /* 3*3                                                  */
+  const double* M;       /* X*X   motion noise variance (LQRO:1285)              */
+  const double* N;       /* 6*6   observation noise variance (LQRO:1286)         */
+  const double* normals; /* n*LQRO_NORMALS_PER_AGENT                             */
+} lqro_agents;
+
+/* Host arrays; synchronous.  models: n_models = 1 (shared) or n. */
+int lqro_dynamics_step(const lqro_model* models, int32_t n_models, int32_t n,
+                       int32_t per_agent_gains, const lqro_agents* agents, int32_t device);
+/* Device-resident: every pointer in *agents and `models` is a device pointer on
+ * the current device; enqueued on `stream` (hipStream_t, NULL = default),
+ * returns without synchronising.  d_x then feeds lqro_step_device directly. */
+int lqro_dynamics_step_device(const lqro_model* models, int32_t n_models, int32_t n,
+                              int32_t per_agent_gains, const lqro_agents* agents, void* stream);
+/* normal() (LQRO:340-350) over random() (LQRO:334-337) on the MSVC rand()
+ * stream (seed' = seed*214013 + 2531011, rand = (seed' >> 16) & 0x7fff; srand(s)
+ * sets seed = s).  Writes `count` draws, advances *seed. */
+int lqro_normals(uint32_t* seed, int64_t count, double* out);
+
 const char* lqro_status_string(int status);
 int lqro_version(void);
 

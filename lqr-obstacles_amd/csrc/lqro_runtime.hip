@@ -34,6 +34,7 @@
 #include "lqro_pair.hpp"
 #include "lqro_hull.hpp"
 #include "lqro_synth.hpp"
+#include "lqro_dyn.hpp"
 
 #define LQRO_PROF_WORDS (32 + 2 * 4096 + 16 + 16)   // hull: 32 counters + 2 words per job; pair: 16; hull wave phases: 16
 
@@ -823,6 +824,93 @@ int lqro_synthesize_gains_batch(const lqro_model* models, int32_t n, double* A, 
   }
   if (d_m) (void)hipFree(d_m);
   if (d_out) (void)hipFree(d_out);
+  return rc;
+}
+
+// ---- the per-agent step after the pair loop (LQRO:1437-1446) -------------
+// One agent per lane: the step is a chain of 16x16 products, exponentials and
+// a Jacobi sweep with data-dependent control flow (lqro_dyn.hpp), fp64,
+// ~10 MFLOP per agent, latency bound on per-lane scratch.
+__global__ void __launch_bounds__(64) k_dyn(const lqro_model* models, int n_models, int n, int per_agent,
+                                            lqro_agents A) {
+  const int a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= n) return;
+  const size_t g = per_agent ? (size_t)a : 0;
+  dyn::AgentParams p;
+  p.model = models + (n_models > 1 ? a : 0);
+  p.L = A.L + g * dyn::kU * dyn::kX;
+  p.E = A.E + g * dyn::kU * dyn::kV;
+  p.l = A.l + g * dyn::kU;
+  p.Lh = A.Lh + g * dyn::kV * dyn::kX;
+  p.Eh = A.Eh + g * dyn::kV * dyn::kV;
+  p.u_goal = A.u_goal + (size_t)a * dyn::kU;
+  p.p_goal = A.p_goal + (size_t)a * 3;
+  p.M = A.M;
+  p.Nz = A.N;
+  p.normals = A.normals + (size_t)a * dyn::kNormals;
+  dyn::agent_step(p, A.x + (size_t)a * dyn::kX, A.rot + (size_t)a * 9, A.x_true + (size_t)a * dyn::kX,
+                  A.rot_true + (size_t)a * 9, A.P + (size_t)a * dyn::kX * dyn::kX, A.vgoal + (size_t)a * 3,
+                  A.u ? A.u + (size_t)a * dyn::kU : nullptr);
+}
+
+static bool agents_complete(const lqro_agents* a) {
+  return a && a->x && a->rot && a->x_true && a->rot_true && a->P && a->vgoal && a->u_goal && a->p_goal &&
+         a->L && a->E && a->l && a->Lh && a->Eh && a->M && a->N && a->normals;
+}
+
+int lqro_dynamics_step_device(const lqro_model* models, int32_t n_models, int32_t n, int32_t per_agent_gains,
+                              const lqro_agents* agents, void* stream) {
+  if (!models || n <= 0 || (n_models != 1 && n_models != n) || !agents_complete(agents)) return LQRO_E_ARG;
+  hipLaunchKernelGGL(k_dyn, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream, models,
+                     (int)n_models, (int)n, (int)(per_agent_gains != 0), *agents);
+  return hipGetLastError() == hipSuccess ? LQRO_OK : LQRO_E_HIP;
+}
+
+int lqro_dynamics_step(const lqro_model* models, int32_t n_models, int32_t n, int32_t per_agent_gains,
+                       const lqro_agents* agents, int32_t device) {
+  if (!models || n <= 0 || (n_models != 1 && n_models != n) || !agents_complete(agents)) return LQRO_E_ARG;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) return LQRO_E_NODEVICE;
+  if (hipSetDevice(device) != hipSuccess) return LQRO_E_HIP;
+  const size_t G = per_agent_gains ? (size_t)n : 1, N = (size_t)n;
+  using namespace dyn;
+  // (host source, element count, written back)
+  struct Buf { const double* h; double* out; size_t cnt; double* d; };
+  Buf b[17] = {
+      {agents->x, agents->x, N * kX, nullptr},            {agents->rot, agents->rot, N * 9, nullptr},
+      {agents->x_true, agents->x_true, N * kX, nullptr},  {agents->rot_true, agents->rot_true, N * 9, nullptr},
+      {agents->P, agents->P, N * kX * kX, nullptr},       {agents->vgoal, agents->vgoal, N * 3, nullptr},
+      {nullptr, agents->u, agents->u ? N * kU : 0, nullptr},
+      {agents->u_goal, nullptr, N * kU, nullptr},         {agents->p_goal, nullptr, N * 3, nullptr},
+      {agents->L, nullptr, G * kU * kX, nullptr},         {agents->E, nullptr, G * kU * kV, nullptr},
+      {agents->l, nullptr, G * kU, nullptr},              {agents->Lh, nullptr, G * kV * kX, nullptr},
+      {agents->Eh, nullptr, G * kV * kV, nullptr},        {agents->M, nullptr, (size_t)kX * kX, nullptr},
+      {agents->N, nullptr, (size_t)kZ * kZ, nullptr},     {agents->normals, nullptr, N * kNormals, nullptr}};
+  lqro_model* d_m = nullptr;
+  int rc = LQRO_OK;
+  if (hipMalloc(&d_m, sizeof(lqro_model) * (size_t)n_models) != hipSuccess) rc = LQRO_E_NOMEM;
+  for (auto& q : b)
+    if (rc == LQRO_OK && q.cnt && hipMalloc(&q.d, sizeof(double) * q.cnt) != hipSuccess) rc = LQRO_E_NOMEM;
+  if (rc == LQRO_OK &&
+      hipMemcpy(d_m, models, sizeof(lqro_model) * (size_t)n_models, hipMemcpyHostToDevice) != hipSuccess)
+    rc = LQRO_E_HIP;
+  for (auto& q : b)
+    if (rc == LQRO_OK && q.h && hipMemcpy(q.d, q.h, sizeof(double) * q.cnt, hipMemcpyHostToDevice) != hipSuccess)
+      rc = LQRO_E_HIP;
+  if (rc == LQRO_OK) {
+    lqro_agents d;
+    d.x = b[0].d; d.rot = b[1].d; d.x_true = b[2].d; d.rot_true = b[3].d; d.P = b[4].d; d.vgoal = b[5].d;
+    d.u = b[6].d; d.u_goal = b[7].d; d.p_goal = b[8].d; d.L = b[9].d; d.E = b[10].d; d.l = b[11].d;
+    d.Lh = b[12].d; d.Eh = b[13].d; d.M = b[14].d; d.N = b[15].d; d.normals = b[16].d;
+    rc = lqro_dynamics_step_device(d_m, n_models, n, per_agent_gains, &d, nullptr);
+    if (rc == LQRO_OK && hipDeviceSynchronize() != hipSuccess) rc = LQRO_E_HIP;
+  }
+  for (auto& q : b)
+    if (rc == LQRO_OK && q.out && hipMemcpy(q.out, q.d, sizeof(double) * q.cnt, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = LQRO_E_HIP;
+  if (d_m) (void)hipFree(d_m);
+  for (auto& q : b)
+    if (q.d) (void)hipFree(q.d);
   return rc;
 }
 

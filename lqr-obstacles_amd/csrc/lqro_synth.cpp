@@ -1,6 +1,6 @@
 // lqro_synth.cpp — setup-time host helpers of liblqro.so: the model defaults
 // (setup(), LQRObstacles.cpp:169-189, 1275-1286, 559-561) and createSpheres
-// (:735-750).  The gain synthesis itself (controlMatrices) is shared by the
+// (:735-750), and the reference's noise stream (normal(), :334-350).  The gain synthesis itself (controlMatrices) is shared by the
 // host and the device: lqro_synth.hpp, entry points in lqro_runtime.hip.
 #include <cmath>
 
@@ -33,6 +33,33 @@ extern "C" int lqro_sphere(int32_t np, double xy_radius, double z_radius, double
     out[3 * i + 2] = 2 * z_radius * z;
     z -= dz;
     lon += dlong;
+  }
+  return LQRO_OK;
+}
+
+// MSVC rand(): seed = seed*214013 + 2531011, (seed >> 16) & 0x7fff (RAND_MAX 32767)
+static int msvc_rand(uint32_t* seed) {
+  *seed = *seed * 214013u + 2531011u;
+  return (int)((*seed >> 16) & 0x7fff);
+}
+
+// random() (LQRO:334-337); the two rand() calls are taken left to right
+static double ref_uniform(uint32_t* seed) {
+  const int a = msvc_rand(seed);
+  const int b = msvc_rand(seed);
+  return (double)(a * (32767 + 1) + b) / (32767 * (32767 + 2));
+}
+
+extern "C" int lqro_normals(uint32_t* seed, int64_t count, double* out) {
+  if (!seed || count < 0 || (count > 0 && !out)) return LQRO_E_ARG;
+  for (int64_t k = 0; k < count; ++k) {   // normal() (LQRO:340-350)
+    double u = 0, v = 0, s = 0;
+    while (s == 0 || s > 1) {
+      u = 2 * ref_uniform(seed) - 1;
+      v = 2 * ref_uniform(seed) - 1;
+      s = u * u + v * v;
+    }
+    out[k] = u * std::sqrt(-2 * std::log(s) / s);
   }
   return LQRO_OK;
 }

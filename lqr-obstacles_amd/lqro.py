@@ -72,7 +72,18 @@ EXPORTS = (
     "lqro_create", "lqro_destroy", "lqro_set_gains", "lqro_step", "lqro_step_device",
     "lqro_get_records", "lqro_get_stats", "lqro_get_timings", "lqro_status_string",
     "lqro_version", "lqro_calculate_new_v", "lqro_synthesize_gains_batch",
+    "lqro_dynamics_step", "lqro_dynamics_step_device", "lqro_normals",
 )
+
+NORMALS_PER_AGENT = 22   # LQRO_NORMALS_PER_AGENT: 16 propagate + 6 observation
+
+
+class Agents(C.Structure):
+    """lqro_agents: per-agent state, gains and noise of the step after the
+    pair loop (LQRO:1437-1446)."""
+    _fields_ = [(n, C.c_void_p) for n in (
+        "x", "rot", "x_true", "rot_true", "P", "vgoal", "u", "u_goal", "p_goal",
+        "L", "E", "l", "Lh", "Eh", "M", "N", "normals")]
 
 _lib = None
 
@@ -101,6 +112,9 @@ def lib() -> C.CDLL:
         L.lqro_get_stats.argtypes = [vp, vp]
         L.lqro_get_timings.argtypes = [vp, vp]
         L.lqro_calculate_new_v.argtypes = [vp, vp, i32, vp, dbl, vp, i32]
+        L.lqro_dynamics_step.argtypes = [C.POINTER(Model), i32, i32, i32, C.POINTER(Agents), i32]
+        L.lqro_dynamics_step_device.argtypes = [vp, i32, i32, i32, C.POINTER(Agents), vp]
+        L.lqro_normals.argtypes = [C.POINTER(C.c_uint32), i64, vp]
         _lib = L
     return _lib
 
@@ -298,6 +312,66 @@ def swap_scenario():
         x[i, :3] = p
         x[i, 12:16] = nominal
     return x, np.array(goal)
+
+
+# ---------------------------------------------------------------------------
+# The per-agent step after the pair loop (LQRO:1437-1446), SURVEY §8f next #1
+# ---------------------------------------------------------------------------
+AGENT_FIELDS = dict(x=(16,), rot=(3, 3), x_true=(16,), rot_true=(3, 3), P=(16, 16), vgoal=(3,),
+                    u_goal=(4,), p_goal=(3,))
+
+
+def normals(seed: int, count: int) -> tuple[np.ndarray, int]:
+    """`count` draws of the reference's normal() (LQRO:340-350) on the MSVC
+    rand() stream seeded with `seed` (srand); returns (draws, next seed)."""
+    st = C.c_uint32(seed & 0xFFFFFFFF)
+    out = np.zeros(count)
+    _check(lib().lqro_normals(C.byref(st), count, _p(out)), "lqro_normals")
+    return out, int(st.value)
+
+
+def agent_states(x, u_goal=None, p_goal=None, p0: float = 1e-9) -> dict:
+    """Host-side agent records for dynamics_step: the estimate x, Rot = I,
+    xTrue = x, RotTrue = I, P = p0 I (Pinit, LQRO:1297), vGoal = 0, uGoal =
+    hover thrust, pGoal = 0 (setupQuadrotors, LQRO:107-122, without its
+    initial noise draw)."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    n = x.shape[0]
+    hover = default_model().gravity * default_model().mass / 4
+    st = dict(x=x.copy(), rot=np.tile(np.eye(3), (n, 1, 1)), x_true=x.copy(),
+              rot_true=np.tile(np.eye(3), (n, 1, 1)), P=np.tile(p0 * np.eye(16), (n, 1, 1)),
+              vgoal=np.zeros((n, 3)),
+              u_goal=np.full((n, 4), hover) if u_goal is None else np.array(u_goal, dtype=np.float64),
+              p_goal=np.zeros((n, 3)) if p_goal is None else np.array(p_goal, dtype=np.float64))
+    return st
+
+
+def dynamics_step(st: dict, gains: dict, nrm: np.ndarray, models=None, M=None, N=None,
+                  per_agent: bool = False, device: int = 0) -> np.ndarray:
+    """lqro_dynamics_step: advances every agent of `st` in place (x, rot,
+    x_true, rot_true, P; vgoal in = newV, out = findVGoal()) and returns u.
+    gains: L, E, l, Lh, Eh (one set, or a leading agent axis with
+    per_agent=True).  nrm: n x 22 draws.  M, N default to the reference's
+    1e-9 I (LQRO:1285-1286)."""
+    n = st["x"].shape[0]
+    models = [default_model()] if models is None else list(models)
+    marr = (Model * len(models))(*models)
+    M = 1e-9 * np.eye(16) if M is None else M
+    N = 1e-9 * np.eye(6) if N is None else N
+    for k, shp in AGENT_FIELDS.items():
+        if st[k].shape != (n,) + shp or st[k].dtype != np.float64 or not st[k].flags.c_contiguous:
+            raise LqroError(f"dynamics_step: {k} must be C-contiguous float64 {(n,) + shp}")
+    keep = [np.ascontiguousarray(v, dtype=np.float64) for v in
+            (gains["L"], gains["E"], gains["l"], gains["Lh"], gains["Eh"], M, N, nrm)]
+    if keep[-1].size != n * NORMALS_PER_AGENT:
+        raise LqroError("dynamics_step: need n x 22 normals")
+    u = np.zeros((n, 4))
+    a = Agents(*[_p(st[k]).value for k in ("x", "rot", "x_true", "rot_true", "P", "vgoal")],
+               _p(u).value, _p(st["u_goal"]).value, _p(st["p_goal"]).value,
+               *[_p(v).value for v in keep])
+    _check(lib().lqro_dynamics_step(marr, len(models), n, int(per_agent), C.byref(a), device),
+           "lqro_dynamics_step")
+    return u
 
 
 # ---------------------------------------------------------------------------

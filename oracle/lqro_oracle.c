@@ -1197,3 +1197,245 @@ int orc_step_mt(int N, int X, int H, int NP, int min_reach, double vmax_reach, d
   free(th); free(args);
   return rc;
 }
+
+/* ------------------------------------------------------------------------ */
+/* The per-agent step after the pair loop (LQRO:1437-1446): findU, propagate, */
+/* kalmanFilter1, the observation draw, kalmanFilter2, findVGoal.  Noise      */
+/* draws are supplied (16 for propagate, 6 for the observation).              */
+/* ------------------------------------------------------------------------ */
+
+/* jacobi (MAT:674-759) */
+static void ojacobi(int n, const double* m, double* V, double* D) {
+  memcpy(D, m, sizeof(double) * (size_t)(n * n));
+  meye(n, V);
+  if (n <= 1) return;
+  size_t pivotRow = 0, zeroCount = 0;
+  for (;;) {
+    double maximum = 0;
+    size_t p = 0, q = 0;
+    for (size_t i = 0; i < pivotRow; ++i)
+      if (fabs(D[i * n + pivotRow]) > maximum) {
+        maximum = fabs(D[i * n + pivotRow]); p = i; q = pivotRow;
+      }
+    for (size_t j = pivotRow + 1; j < (size_t)n; ++j)
+      if (fabs(D[pivotRow * n + j]) > maximum) {
+        maximum = fabs(D[pivotRow * n + j]); p = pivotRow; q = j;
+      }
+    pivotRow = (pivotRow + 1) % (size_t)n;
+    if (maximum <= 2.220446049250313080847e-16) {   /* DBL_EPSILON */
+      ++zeroCount;
+      if (zeroCount == (size_t)n) break;
+      continue;
+    }
+    zeroCount = 0;
+    double theta = 0.5 * (D[q * n + q] - D[p * n + p]) / D[p * n + q];
+    double t = 1 / (fabs(theta) + hypot(theta, 1));
+    if (theta < 0) t = -t;
+    double c = 1 / hypot(t, 1);
+    double s = c * t;
+    double tau = s / (1 + c);
+    for (size_t r = 0; r < p; ++r) {
+      double Drp = D[r * n + p], Drq = D[r * n + q];
+      D[r * n + p] -= s * (Drq + tau * Drp);
+      D[r * n + q] += s * (Drp - tau * Drq);
+    }
+    for (size_t r = p + 1; r < q; ++r) {
+      double Drp = D[p * n + r], Drq = D[r * n + q];
+      D[p * n + r] -= s * (Drq + tau * Drp);
+      D[r * n + q] += s * (Drp - tau * Drq);
+    }
+    for (size_t r = q + 1; r < (size_t)n; ++r) {
+      double Drp = D[p * n + r], Drq = D[q * n + r];
+      D[p * n + r] -= s * (Drq + tau * Drp);
+      D[q * n + r] += s * (Drp - tau * Drq);
+    }
+    D[p * n + p] -= t * D[p * n + q];
+    D[q * n + q] += t * D[p * n + q];
+    D[p * n + q] = 0;
+    for (size_t r = 0; r < (size_t)n; ++r) {
+      double Vrp = V[r * n + p], Vrq = V[r * n + q];
+      V[r * n + p] -= s * (Vrq + tau * Vrp);
+      V[r * n + q] += s * (Vrp - tau * Vrq);
+    }
+  }
+  for (int i = 0; i < n - 1; ++i)
+    for (int j = i + 1; j < n; ++j) D[j * n + i] = D[i * n + j] = 0;
+}
+
+void orc_jacobi(int n, const double* m, double* V, double* D) { ojacobi(n, m, V, D); }
+
+/* sampleGaussian (simulator2.h:21-32) with the normals supplied */
+static void sample_gauss(int n, const double* mean, const double* var, const double* nrm,
+                         double* out) {
+  double V[MXN * MXN], D[MXN * MXN], VD[MXN * MXN], t[MXN];
+  ojacobi(n, var, V, D);
+  for (int i = 0; i < n; ++i) D[i * n + i] = sqrt(D[i * n + i]);
+  mm(n, n, n, V, D, VD);
+  mm(n, n, 1, VD, nrm, t);
+  madd(n, t, mean, out);
+}
+
+/* h (LQRO:399-419) */
+static void obs_h(const double* x, double* z) {
+  z[0] = x[9]; z[1] = x[10]; z[2] = x[11];
+  z[3] = x[0]; z[4] = x[1]; z[5] = x[2];
+}
+
+/* errFromRot (stdafx.h:35-48) */
+static void err_from_rot(const double* R, double* out) {
+  double q[3] = {R[7] - R[5], R[2] - R[6], R[3] - R[1]};
+  double r = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2]);
+  double t = R[0] + R[4] + R[8] - 1;
+  if (r == 0) { out[0] = out[1] = out[2] = 0.0; return; }
+  mscale(3, q, atan2(r, t) / r, out);
+}
+
+/* the yaw-only frame RLocal and xTilde of both controllers (LQRO:597-616) */
+static void ctrl_frame(const double* x, const double* R0, const double* uGoal, double* RL,
+                       double* xt) {
+  double z0[3] = {R0[2], R0[5], R0[8]}, ez[3] = {0, 0, 1}, S[9], axis[3];
+  skew(z0, S);
+  mm(3, 3, 1, S, ez, axis);
+  double sinangle = sqrt(axis[0] * axis[0] + axis[1] * axis[1] + axis[2] * axis[2]);
+  double angle = asin(sinangle);
+  if (sinangle != 0) mscale(3, axis, angle / sinangle, axis);
+  double Sa[9], Ea[9], RLt[9], RR[9];
+  skew(axis, Sa); mexp(3, Sa, Ea); mm(3, 3, 3, Ea, R0, RL);
+  mt(3, 3, RL, RLt);
+  mm(3, 3, 1, RLt, x, xt);          /* position */
+  mm(3, 3, 1, RLt, x + 3, xt + 3);  /* velocity */
+  mm(3, 3, 3, RLt, R0, RR);
+  err_from_rot(RR, xt + 6);
+  xt[9] = x[9]; xt[10] = x[10]; xt[11] = x[11];
+  for (int k = 0; k < 4; ++k) xt[12 + k] = x[12 + k] - uGoal[k];
+}
+
+/* riccatiControllerSteady (LQRO:594-617) */
+void orc_control_velocity(const double* x, const double* R0, const double* vGoal,
+                          const double* uGoal, const double* L, const double* E,
+                          const double* l, double* u) {
+  double RL[9], RLt[9], xt[16], vt[3], Lx[4], Ev[4];
+  ctrl_frame(x, R0, uGoal, RL, xt);
+  mt(3, 3, RL, RLt);
+  mm(3, 3, 1, RLt, vGoal, vt);
+  mm(4, 16, 1, L, xt, Lx);
+  mm(4, 3, 1, E, vt, Ev);
+  madd(4, uGoal, Lx, u); madd(4, u, Ev, u); madd(4, u, l, u);
+}
+
+/* riccatiControllerSteadyPosition (LQRO:619-645) */
+void orc_control_position(const double* x, const double* R0, const double* pGoal,
+                          const double* uGoal, const double* Lh, const double* Eh, double* v) {
+  double RL[9], RLt[9], xt[16], pt[3], a[3], b[3];
+  ctrl_frame(x, R0, uGoal, RL, xt);
+  mt(3, 3, RL, RLt);
+  mm(3, 3, 1, RLt, pGoal, pt);
+  mm(3, 16, 1, Lh, xt, a);
+  mm(3, 3, 1, Eh, pt, b);
+  madd(3, a, b, a);
+  mm(3, 3, 1, RL, a, v);
+}
+
+/* the common head of propagate and kalmanFilter1 (LQRO:474-481, 489-500) */
+static void disc_step(const phys_t* P, const double* x, const double* R, const double* u,
+                      const double* M, double* A, double* MM, double* dx) {
+  enum { X = 16 };
+  double F[X * X], xdot[X], fr[X], fl[X], xr[X], xl[X];
+  memcpy(xr, x, sizeof xr); memcpy(xl, x, sizeof xl);
+  for (int i = 0; i < X; ++i) {       /* Jacobian_fx (LQRO:421-430) */
+    xr[i] += P->jStep; xl[i] -= P->jStep;
+    fdyn(P, xr, R, u, fr); fdyn(P, xl, R, u, fl);
+    for (int k = 0; k < X; ++k) F[k * X + i] = (fr[k] - fl[k]) / (2 * P->jStep);
+    xr[i] = xl[i] = x[i];
+  }
+  fdyn(P, x, R, u, xdot);
+  double t[X * X], A2[X * X], t2[X * X], t3[X * X], At[X * X], A2t[X * X];
+  mscale(X * X, F, P->dt, t); mexp(X, t, A);
+  mscale(X * X, F, P->dt * 0.5, t); mexp(X, t, A2);
+  /* MM = (dt/6) * (M + 4*A2*M*~A2 + A*M*~A) */
+  mt(X, X, A2, A2t); mt(X, X, A, At);
+  mscale(X * X, A2, 4, t); mm(X, X, X, t, M, t2); mm(X, X, X, t2, A2t, t2);
+  madd(X * X, M, t2, t3);
+  mm(X, X, X, A, M, t2); mm(X, X, X, t2, At, t2);
+  madd(X * X, t3, t2, t3);
+  mscale(X * X, t3, P->dt / 6, MM);
+  /* dx = (dt/6)*(xDot + 4*(A2*xDot) + A*xDot) */
+  double a[X], b[X];
+  mm(X, X, 1, A2, xdot, a); mscale(X, a, 4, a);
+  madd(X, xdot, a, a);
+  mm(X, X, 1, A, xdot, b); madd(X, a, b, a);
+  mscale(X, a, P->dt / 6, dx);
+}
+
+static void rot_reset(double* x, double* R) {     /* LQRO:483-485 */
+  double S[9], E[9];
+  skew(x + 6, S); mexp(3, S, E); mm(3, 3, 3, R, E, R);
+  x[6] = 0; x[7] = 0; x[8] = 0;
+}
+
+/* propagate (LQRO:473-486) */
+void orc_propagate(const lqro_model* m, double* x, double* R, const double* u, const double* M,
+                   const double* nrm) {
+  phys_t P; phys_init(m, &P);
+  double A[256], MM[256], dx[16], zero[16] = {0}, g[16];
+  disc_step(&P, x, R, u, M, A, MM, dx);
+  sample_gauss(16, zero, MM, nrm, g);
+  madd(16, x, dx, x); madd(16, x, g, x);
+  rot_reset(x, R);
+}
+
+/* kalmanFilter1 (LQRO:488-505) */
+void orc_kalman1(const lqro_model* m, double* x, double* R, const double* u, const double* M,
+                 double* Pc) {
+  phys_t P; phys_init(m, &P);
+  double A[256], MM[256], dx[16], At[256], t[256];
+  disc_step(&P, x, R, u, M, A, MM, dx);
+  madd(16, x, dx, x);
+  mt(16, 16, A, At);
+  mm(16, 16, 16, A, Pc, t); mm(16, 16, 16, t, At, t); madd(256, t, MM, Pc);
+  rot_reset(x, R);
+}
+
+/* kalmanFilter2 (LQRO:507-518) with Jacobian_hx (LQRO:443-452) */
+void orc_kalman2(const lqro_model* m, double* x, double* R, const double* z, const double* Nz,
+                 double* Pc) {
+  enum { X = 16, Z = 6 };
+  phys_t P; phys_init(m, &P);
+  double H[Z * X], xr[X], xl[X], hr[Z], hl[Z];
+  memcpy(xr, x, sizeof xr); memcpy(xl, x, sizeof xl);
+  for (int i = 0; i < X; ++i) {
+    xr[i] += P.jStep; xl[i] -= P.jStep;
+    obs_h(xr, hr); obs_h(xl, hl);
+    for (int k = 0; k < Z; ++k) H[k * X + i] = (hr[k] - hl[k]) / (2 * P.jStep);
+    xr[i] = xl[i] = x[i];
+  }
+  double Ht[X * Z], PHt[X * Z], HP[Z * X], S[Z * Z], Si[Z * Z], K[X * Z];
+  mt(Z, X, H, Ht);
+  mm(X, X, Z, Pc, Ht, PHt);
+  mm(Z, X, X, H, Pc, HP); mm(Z, X, Z, HP, Ht, S); madd(Z * Z, S, Nz, S);
+  minv(Z, S, Si);
+  mm(X, Z, Z, PHt, Si, K);
+  double hx[Z], e[Z], Ke[X];
+  obs_h(x, hx); msub(Z, z, hx, e);
+  mm(X, Z, 1, K, e, Ke); madd(X, x, Ke, x);
+  double KH[X * X], I[X * X];
+  mm(X, Z, X, K, H, KH); meye(X, I); msub(X * X, I, KH, I);
+  mm(X, X, X, I, Pc, Pc);
+  rot_reset(x, R);
+}
+
+/* One agent through LQRO:1438-1445 (see lqro_oracle.h). */
+void orc_agent_step(const lqro_model* m, const double* L, const double* E, const double* l,
+                    const double* Lh, const double* Eh, const double* uGoal, const double* pGoal,
+                    const double* M, const double* Nz, const double* nrm, double* x, double* R,
+                    double* xTrue, double* RTrue, double* Pc, double* vgoal, double* u_out) {
+  double u[4], z[6], hz[6];
+  orc_control_velocity(x, R, vgoal, uGoal, L, E, l, u);     /* findU (vGoal = newV) */
+  orc_propagate(m, xTrue, RTrue, u, M, nrm);                /* propagateU */
+  orc_kalman1(m, x, R, u, M, Pc);
+  obs_h(xTrue, hz);
+  sample_gauss(6, hz, Nz, nrm + 16, z);                     /* LQRO:1442 */
+  orc_kalman2(m, x, R, z, Nz, Pc);
+  orc_control_position(x, R, pGoal, uGoal, Lh, Eh, vgoal);  /* findVGoal */
+  if (u_out) memcpy(u_out, u, sizeof u);
+}

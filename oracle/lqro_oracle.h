@@ -107,6 +107,32 @@ void orc_inverse4(const double* in, double* out);
 
 double orc_round6(double v);
 
+/* ---- the per-agent step after the pair loop (LQRO:1437-1446) ----------- */
+/* jacobi (MAT:674-759) on an n x n symmetric matrix (n <= 16). */
+void orc_jacobi(int n, const double* m, double* V, double* D);
+/* riccatiControllerSteady (LQRO:594-617) -> u (4). */
+void orc_control_velocity(const double* x, const double* R0, const double* vGoal,
+                          const double* uGoal, const double* L, const double* E,
+                          const double* l, double* u);
+/* riccatiControllerSteadyPosition (LQRO:619-645) -> v (3). */
+void orc_control_position(const double* x, const double* R0, const double* pGoal,
+                          const double* uGoal, const double* Lh, const double* Eh, double* v);
+/* propagate (LQRO:473-486); nrm = the 16 normal() draws of its sampleGaussian. */
+void orc_propagate(const lqro_model* m, double* x, double* R, const double* u, const double* M,
+                   const double* nrm);
+/* kalmanFilter1 (LQRO:488-505), kalmanFilter2 (LQRO:507-518). */
+void orc_kalman1(const lqro_model* m, double* x, double* R, const double* u, const double* M,
+                 double* P);
+void orc_kalman2(const lqro_model* m, double* x, double* R, const double* z, const double* N,
+                 double* P);
+/* One agent through LQRO:1438-1445: findU, propagateU, kalmanFilter1, the
+ * observation draw (LQRO:1442), kalmanFilter2, findVGoal.  nrm: 22 draws
+ * (16 propagate, 6 observation).  vgoal: in newV, out the new vGoal. */
+void orc_agent_step(const lqro_model* m, const double* L, const double* E, const double* l,
+                    const double* Lh, const double* Eh, const double* uGoal, const double* pGoal,
+                    const double* M, const double* N, const double* nrm, double* x, double* R,
+                    double* xTrue, double* RTrue, double* P, double* vgoal, double* u_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -49,6 +49,8 @@ def lib():
         _o.orc_sphere.argtypes = [C.c_int, d, d, C.c_void_p]
         _o.orc_hull_branch.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         _o.orc_hull.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int]
+        _o.orc_agent_step.argtypes = [C.c_void_p] * 17
+        _o.orc_jacobi.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
     return _o
 
 
@@ -176,3 +178,41 @@ def hull_branch(points_full: np.ndarray, vrel):
     fac = np.zeros(3, np.int32)
     k = lib().orc_hull_branch(points_full.shape[0], _p(points_full), _p(v), _p(d), _p(nrm), _p(fac))
     return k, float(d[0]), nrm, fac
+
+
+def agent_step(st: dict, gains: dict, nrm, models=None, M=None, N=None,
+               per_agent: bool = False):
+    """orc_agent_step for every agent of st (same dict layout as
+    lqro.agent_states), in place; returns u (n x 4).  models: None (the
+    default model), or a list of 1 or n models with the lqro_model fields."""
+    if models is None:
+        m0 = Model()
+        lib().orc_model_default(C.byref(m0))
+        models = [m0]
+    models = [Model(*[getattr(m, f) for f, _ in Model._fields_]) for m in models]
+    M = np.ascontiguousarray(1e-9 * np.eye(16) if M is None else M, np.float64)
+    N = np.ascontiguousarray(1e-9 * np.eye(6) if N is None else N, np.float64)
+    n = st["x"].shape[0]
+    nrm = np.ascontiguousarray(nrm, np.float64).reshape(n, 22)
+    u = np.zeros((n, 4))
+    for a in range(n):
+        g = {k: np.ascontiguousarray(gains[k][a] if per_agent else gains[k], np.float64)
+             for k in ("L", "E", "l", "Lh", "Eh")}
+        row = {k: np.ascontiguousarray(st[k][a]) for k in st}
+        m = models[a if len(models) > 1 else 0]
+        lib().orc_agent_step(C.byref(m), _p(g["L"]), _p(g["E"]), _p(g["l"]), _p(g["Lh"]),
+                             _p(g["Eh"]), _p(row["u_goal"]), _p(row["p_goal"]), _p(M), _p(N),
+                             _p(nrm[a]), _p(row["x"]), _p(row["rot"]), _p(row["x_true"]),
+                             _p(row["rot_true"]), _p(row["P"]), _p(row["vgoal"]), _p(u[a]))
+        for k in ("x", "rot", "x_true", "rot_true", "P", "vgoal"):
+            st[k][a] = row[k]
+    return u
+
+
+def jacobi(m):
+    m = np.ascontiguousarray(m, np.float64)
+    n = m.shape[0]
+    V = np.zeros((n, n))
+    D = np.zeros((n, n))
+    lib().orc_jacobi(n, _p(m), _p(V), _p(D))
+    return V, D

@@ -270,4 +270,61 @@ int ref_step(int N, int np, int H, int min_reach, double vmax_reach, const doubl
   return n_inside;
 }
 
+/* ---- the per-agent step after the pair loop (LQRO:1437-1446) ---------
+ * The reference's own controllers and filters.  propagate (LQRO:473-486) and
+ * the observation draw (LQRO:1442) call sampleGaussian (simulator2.h:21-32),
+ * whose jacobi (MAT:674-759) calls MSVC's _hypot, which this image lacks:
+ * they are not built here (the oracle's jacobi is pinned by its properties,
+ * tests/test_oracle_dyn.py).  Weights M, N are the reference's (LQRO:1285-1286). */
+
+/* l of controlMatrices (LQRO:552,557), which the pair path does not read */
+void ref_gain_l(double* l_) {
+  ref_setup_consts();
+  ref_set_weights();
+  Input uGoal;
+  uGoal[0] = uGoal[1] = uGoal[2] = uGoal[3] = nominalInput;
+  State xGoal = zeros<X_DIM>();
+  xGoal[12] = xGoal[13] = xGoal[14] = xGoal[15] = nominalInput;
+  Matrix<X_DIM, X_DIM> A; Matrix<X_DIM, U_DIM> B; Matrix<X_DIM, 1> c;
+  Matrix<U_DIM, X_DIM> L; Matrix<U_DIM, V_DIM> E; Matrix<U_DIM, 1> l;
+  Matrix<V_DIM, X_DIM> Lh; Matrix<V_DIM, V_DIM> Eh;
+  controlMatrices(uGoal, xGoal, A, B, c, L, E, l, Lh, Eh);
+  store(l, l_);
+}
+
+void ref_control_velocity(const double* x_, const double* R_, const double* vg_,
+                          const double* ug_, const double* L_, const double* E_,
+                          const double* l_, double* u_) {
+  State x; Rotation R0, RG = identity<3>(); Velocity vg; Input ug;
+  Matrix<U_DIM, X_DIM> L; Matrix<U_DIM, V_DIM> E; Matrix<U_DIM, 1> l;
+  load(x, x_); load(R0, R_); load(vg, vg_); load(ug, ug_); load(L, L_); load(E, E_); load(l, l_);
+  store(riccatiControllerSteady(x, R0, vg, RG, ug, L, E, l), u_);
+}
+
+void ref_control_position(const double* x_, const double* R_, const double* pg_,
+                          const double* ug_, const double* Lh_, const double* Eh_, double* v_) {
+  State x; Rotation R0, RG = identity<3>(); Position pg; Input ug;
+  Matrix<V_DIM, X_DIM> Lh; Matrix<V_DIM, V_DIM> Eh;
+  load(x, x_); load(R0, R_); load(pg, pg_); load(ug, ug_); load(Lh, Lh_); load(Eh, Eh_);
+  store(riccatiControllerSteadyPosition(x, R0, pg, RG, ug, Lh, Eh), v_);
+}
+
+void ref_kalman1(double* x_, double* R_, const double* u_, double* P_) {
+  ref_setup_consts();
+  ref_set_weights();
+  State x; Rotation R0; Input u; Matrix<X_DIM, X_DIM> P;
+  load(x, x_); load(R0, R_); load(u, u_); load(P, P_);
+  kalmanFilter1(x, R0, u, M, P);
+  store(x, x_); store(R0, R_); store(P, P_);
+}
+
+void ref_kalman2(double* x_, double* R_, const double* z_, double* P_) {
+  ref_setup_consts();
+  ref_set_weights();
+  State x; Rotation R0; Observation z; Matrix<X_DIM, X_DIM> P;
+  load(x, x_); load(R0, R_); load(z, z_); load(P, P_);
+  kalmanFilter2(x, R0, z, N, P);
+  store(x, x_); store(R0, R_); store(P, P_);
+}
+
 } /* extern "C" */

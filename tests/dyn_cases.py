@@ -1,0 +1,43 @@
+"""Seeded agent states for the dynamics/estimation step tests (test data
+only): positions, velocities, body rates and rotor forces around hover,
+attitudes from random axis-angle rotations, covariances SPD around Pinit."""
+from __future__ import annotations
+
+import numpy as np
+
+HOVER = 9.80665 * 0.5 / 4   # nominalInput (LQRO:188)
+
+
+def rotation(axis_angle: np.ndarray) -> np.ndarray:
+    th = float(np.linalg.norm(axis_angle))
+    if th == 0.0:
+        return np.eye(3)
+    k = axis_angle / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * (K @ K)
+
+
+def random_agent_cases(n: int, seed: int, rot_err: bool = True) -> dict:
+    rng = np.random.default_rng(seed)
+    x = np.zeros((n, 16))
+    x[:, 0:3] = rng.uniform(-3, 3, (n, 3))
+    x[:, 3:6] = rng.uniform(-1, 1, (n, 3))
+    if rot_err:   # nonzero only between a propagate and its reset; exercised anyway
+        x[: n // 2, 6:9] = rng.uniform(-0.02, 0.02, (n // 2, 3))
+    x[:, 9:12] = rng.uniform(-0.5, 0.5, (n, 3))
+    x[:, 12:16] = HOVER + rng.uniform(-0.1, 0.1, (n, 4))
+    rot = np.stack([rotation(rng.normal(size=3) * rng.uniform(0, 0.4)) for _ in range(n)])
+    rot[0] = np.eye(3)   # the sinangle == 0 branch of both controllers
+    B = rng.normal(size=(n, 16, 16))
+    P = 1e-9 * np.eye(16) + 1e-10 * np.einsum("nij,nkj->nik", B, B)
+    vgoal = rng.uniform(-1, 1, (n, 3))
+    p_goal = rng.uniform(-3, 3, (n, 3))
+    u_goal = np.full((n, 4), HOVER)
+    z = np.concatenate([x[:, 9:12], x[:, 0:3]], axis=1) + 3e-5 * rng.normal(size=(n, 6))
+    return dict(x=x, rot=rot, P=P, vgoal=vgoal, p_goal=p_goal, u_goal=u_goal, z=z)
+
+
+def trajectory_start(n: int, seed: int) -> dict:
+    """States as they stand at a step boundary (rotation error reset to 0)."""
+    cs = random_agent_cases(n, seed, rot_err=False)
+    return cs

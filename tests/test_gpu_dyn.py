@@ -1,0 +1,171 @@
+"""The per-agent step after the pair loop on the GPU (lqro_dynamics_step,
+k_dyn: findU, propagate, kalmanFilter1, the observation draw, kalmanFilter2,
+findVGoal — LQRO:1437-1446) against the oracle's C
+restatement (tests/test_oracle_dyn.py pins that to the reference).
+
+Tolerance: the step calls libm on live values (tan in f, asin in the
+controllers, atan2 in errFromRot, hypot in jacobi), where the device's and
+glibc's results may differ in the last bit, so results are compared with a
+relative tolerance of 1e-9 after one step and 1e-6 after a 30-step
+trajectory (SURVEY §8c allows 1e-5 for fp64 outputs)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from dyn_cases import trajectory_start
+
+pytestmark = pytest.mark.gpu
+
+STATE = ("x", "rot", "x_true", "rot_true", "P", "vgoal")
+
+
+def _gains(oracle, l=(0.01, -0.02, 0.03, -0.04)):
+    g = oracle.synthesize()
+    g["l"] = np.array(l, dtype=np.float64)
+    return g
+
+
+def _states(lqro_mod, n, seed):
+    cs = trajectory_start(n, seed)
+    st = lqro_mod.agent_states(cs["x"], p_goal=cs["p_goal"])
+    st["rot"][:] = cs["rot"]
+    st["rot_true"][:] = cs["rot"]
+    st["P"][:] = cs["P"]
+    st["vgoal"][:] = cs["vgoal"]
+    return st
+
+
+def _close(a, b, rtol, what):
+    scale = np.maximum(np.abs(b), 1e-3 * np.abs(b).max() + 1e-300)
+    err = (np.abs(a - b) / scale).max()
+    assert err <= rtol, f"{what}: max rel err {err:.3e}"
+
+
+def _compare(g, r, rtol):
+    for k in STATE:
+        _close(g[k], r[k], rtol, k)
+
+
+def test_one_step(lqro_mod, oracle):
+    n = 200
+    g = _gains(oracle)
+    st = _states(lqro_mod, n, seed=21)
+    ref = {k: v.copy() for k, v in st.items()}
+    nrm, _ = lqro_mod.normals(7, n * lqro_mod.NORMALS_PER_AGENT)
+    u = lqro_mod.dynamics_step(st, g, nrm)
+    ur = oracle.agent_step(ref, g, nrm)
+    _close(u, ur, 1e-9, "u")
+    _compare(st, ref, 1e-9)
+    assert np.all(st["x"][:, 6:9] == 0)     # rotation error reset into Rot
+    np.testing.assert_allclose(np.einsum("nij,nkj->nik", st["rot"], st["rot"]),
+                               np.tile(np.eye(3), (n, 1, 1)), atol=1e-12)
+
+
+def test_trajectory(lqro_mod, oracle):
+    """30 steps of the closed loop velocity -> position controller with the
+    reference's noise stream (srand(1), agent order)."""
+    n = 48
+    g = _gains(oracle)
+    st = _states(lqro_mod, n, seed=22)
+    ref = {k: v.copy() for k, v in st.items()}
+    seed = 1
+    for t in range(30):
+        nrm, seed = lqro_mod.normals(seed, n * lqro_mod.NORMALS_PER_AGENT)
+        lqro_mod.dynamics_step(st, g, nrm)
+        oracle.agent_step(ref, g, nrm)
+    _compare(st, ref, 1e-6)
+    # the agents head for their position goals
+    assert np.all(np.isfinite(st["x"]))
+
+
+def test_heterogeneous(lqro_mod, oracle):
+    """Per-agent models and gains (C5-style swarm): lqro_synthesize_gains_batch
+    feeds lqro_dynamics_step(per_agent_gains = 1)."""
+    from test_gpu_synth import perturbed_models
+    n = 64
+    models = perturbed_models(lqro_mod, n, seed=5)
+    gb = lqro_mod.synthesize_gains_batch(models)
+    gb["l"] = np.random.default_rng(3).uniform(-0.02, 0.02, (n, 4))
+    st = _states(lqro_mod, n, seed=23)
+    ref = {k: v.copy() for k, v in st.items()}
+    nrm, _ = lqro_mod.normals(99, n * lqro_mod.NORMALS_PER_AGENT)
+    u = lqro_mod.dynamics_step(st, gb, nrm, models=models, per_agent=True)
+    ur = oracle.agent_step(ref, gb, nrm, models=models, per_agent=True)
+    _close(u, ur, 1e-9, "u")
+    _compare(st, ref, 1e-9)
+
+
+class _Hip:
+    """Device buffers through the HIP runtime liblqro.so itself links
+    (libamdhip64): torch's bundled runtime is not initialised in this process."""
+
+    def __init__(self):
+        self.h = C.CDLL("libamdhip64.so")
+        self.ptrs = []
+
+    def put(self, a: np.ndarray) -> int:
+        a = np.ascontiguousarray(a)
+        p = C.c_void_p()
+        assert self.h.hipMalloc(C.byref(p), C.c_size_t(max(a.nbytes, 8))) == 0
+        self.ptrs.append(p)
+        assert self.h.hipMemcpy(p, a.ctypes.data_as(C.c_void_p), C.c_size_t(a.nbytes), 1) == 0
+        return p.value
+
+    def get(self, ptr: int, like: np.ndarray) -> np.ndarray:
+        out = np.empty_like(like)
+        assert self.h.hipMemcpy(out.ctypes.data_as(C.c_void_p), C.c_void_p(ptr),
+                                C.c_size_t(out.nbytes), 2) == 0
+        return out
+
+    def sync(self):
+        assert self.h.hipDeviceSynchronize() == 0
+
+    def free(self):
+        for p in self.ptrs:
+            self.h.hipFree(p)
+
+
+def test_device_resident_closed_loop(lqro_mod, oracle, gains):
+    """lqro_step_device -> lqro_dynamics_step_device on device buffers, the
+    state never leaving HBM: newV feeds vGoal, the new estimate x feeds the
+    next pair step (the loop LQRO:1391-1446).  Against the oracle's pair
+    step + agent step; 3 control steps."""
+    L = lqro_mod.lib()
+    n, H, NP = 12, 30, 50
+    g = _gains(oracle, l=(0.0, 0.0, 0.0, 0.0))
+    x0, vg0 = lqro_mod.synthetic_swarm(n, seed=31, box=3.0)
+    st = lqro_mod.agent_states(x0, p_goal=x0[:, :3] + 1.0)
+    st["vgoal"][:] = vg0
+    ref = {k: v.copy() for k, v in st.items()}
+    hip = _Hip()
+    try:
+        d = {k: hip.put(v) for k, v in st.items()}
+        newv_d = hip.put(np.zeros((n, 3)))
+        gd = {k: hip.put(np.ascontiguousarray(g[k], np.float64)) for k in ("L", "E", "l", "Lh", "Eh")}
+        Md, Nd = hip.put(1e-9 * np.eye(16)), hip.put(1e-9 * np.eye(6))
+        models_d = hip.put(np.frombuffer(bytes(lqro_mod.default_model()), dtype=np.uint8))
+        ctx = lqro_mod.Context(lqro_mod.config(n, H, NP))
+        ctx.set_gains(g["A"], g["B"], g["L"], g["E"])
+        T, NCF = oracle.tables(g["A"], g["B"], g["L"], g["E"], H)
+        S = oracle.sphere(NP)
+        seed = 1
+        for t in range(3):
+            nrm, seed = lqro_mod.normals(seed, n * lqro_mod.NORMALS_PER_AGENT)
+            nrm_d = hip.put(nrm)
+            assert L.lqro_step_device(ctx._h, C.c_void_p(d["x"]), C.c_void_p(d["vgoal"]),
+                                      C.c_void_p(newv_d), None) == 0
+            hip.sync()
+            assert hip.h.hipMemcpy(C.c_void_p(d["vgoal"]), C.c_void_p(newv_d),
+                                   C.c_size_t(n * 3 * 8), 3) == 0          # vGoal = newV
+            a = lqro_mod.Agents(*[d[k] for k in STATE], None, d["u_goal"], d["p_goal"],
+                                *[gd[k] for k in ("L", "E", "l", "Lh", "Eh")], Md, Nd, nrm_d)
+            assert L.lqro_dynamics_step_device(C.c_void_p(models_d), 1, n, 0, C.byref(a), None) == 0
+            hip.sync()
+            newv_r, _ = oracle.step(T, NCF, S, ref["x"], ref["vgoal"], records=False)
+            ref["vgoal"][:] = newv_r
+            oracle.agent_step(ref, g, nrm)
+            got = {k: hip.get(d[k], ref[k]) for k in STATE}
+            _compare(got, ref, 1e-7)
+    finally:
+        hip.free()
