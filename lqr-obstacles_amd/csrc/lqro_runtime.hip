@@ -35,6 +35,7 @@
 #include "lqro_hull.hpp"
 #include "lqro_synth.hpp"
 #include "lqro_dyn.hpp"
+#include "lqro_dynw.hpp"
 
 #define LQRO_PROF_WORDS (32 + 2 * 4096 + 16 + 16)   // hull: 32 counters + 2 words per job; pair: 16; hull wave phases: 16
 
@@ -853,6 +854,33 @@ __global__ void __launch_bounds__(64) k_dyn(const lqro_model* models, int n_mode
                   A.u ? A.u + (size_t)a * dyn::kU : nullptr);
 }
 
+// The same step with one wave per agent (lqro_dynw.hpp): the agent's 16x16
+// matrices in LDS, the products, exponentials, solves and Jacobi sweep over
+// the lanes.  The default; LQRO_DYN_LANE=1 selects k_dyn.
+__global__ void __launch_bounds__(64) k_dynw(const lqro_model* models, int n_models, int n, int per_agent,
+                                             lqro_agents A) {
+  __shared__ double w[dynw::kWaveDoubles];
+  const int a = blockIdx.x;
+  if (a >= n) return;
+  const int lane = threadIdx.x;
+  const size_t g = per_agent ? (size_t)a : 0;
+  dyn::AgentParams p;
+  p.model = models + (n_models > 1 ? a : 0);
+  p.L = A.L + g * dyn::kU * dyn::kX;
+  p.E = A.E + g * dyn::kU * dyn::kV;
+  p.l = A.l + g * dyn::kU;
+  p.Lh = A.Lh + g * dyn::kV * dyn::kX;
+  p.Eh = A.Eh + g * dyn::kV * dyn::kV;
+  p.u_goal = A.u_goal + (size_t)a * dyn::kU;
+  p.p_goal = A.p_goal + (size_t)a * 3;
+  p.M = A.M;
+  p.Nz = A.N;
+  p.normals = A.normals + (size_t)a * dyn::kNormals;
+  dynw::agent_step(p, A.x + (size_t)a * dyn::kX, A.rot + (size_t)a * 9, A.x_true + (size_t)a * dyn::kX,
+                   A.rot_true + (size_t)a * 9, A.P + (size_t)a * dyn::kX * dyn::kX, A.vgoal + (size_t)a * 3,
+                   A.u ? A.u + (size_t)a * dyn::kU : nullptr, w, lane);
+}
+
 static bool agents_complete(const lqro_agents* a) {
   return a && a->x && a->rot && a->x_true && a->rot_true && a->P && a->vgoal && a->u_goal && a->p_goal &&
          a->L && a->E && a->l && a->Lh && a->Eh && a->M && a->N && a->normals;
@@ -861,8 +889,13 @@ static bool agents_complete(const lqro_agents* a) {
 int lqro_dynamics_step_device(const lqro_model* models, int32_t n_models, int32_t n, int32_t per_agent_gains,
                               const lqro_agents* agents, void* stream) {
   if (!models || n <= 0 || (n_models != 1 && n_models != n) || !agents_complete(agents)) return LQRO_E_ARG;
-  hipLaunchKernelGGL(k_dyn, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream, models,
-                     (int)n_models, (int)n, (int)(per_agent_gains != 0), *agents);
+  const char* lane = getenv("LQRO_DYN_LANE");
+  if (lane && atoi(lane) == 1)
+    hipLaunchKernelGGL(k_dyn, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream, models,
+                       (int)n_models, (int)n, (int)(per_agent_gains != 0), *agents);
+  else
+    hipLaunchKernelGGL(k_dynw, dim3((unsigned)n), dim3(64), 0, (hipStream_t)stream, models, (int)n_models,
+                       (int)n, (int)(per_agent_gains != 0), *agents);
   return hipGetLastError() == hipSuccess ? LQRO_OK : LQRO_E_HIP;
 }
 

@@ -169,3 +169,20 @@ def test_device_resident_closed_loop(lqro_mod, oracle, gains):
             _compare(got, ref, 1e-7)
     finally:
         hip.free()
+
+
+def test_wave_kernel_matches_lane_kernel(lqro_mod, oracle, monkeypatch):
+    """k_dynw (one wave per agent, the default) computes every element in the
+    same operation order as k_dyn (one lane per agent): bit-identical."""
+    n = 96
+    g = _gains(oracle)
+    st = _states(lqro_mod, n, seed=24)
+    other = {k: v.copy() for k, v in st.items()}
+    nrm, _ = lqro_mod.normals(5, n * lqro_mod.NORMALS_PER_AGENT)
+    monkeypatch.setenv("LQRO_DYN_LANE", "0")
+    u0 = lqro_mod.dynamics_step(st, g, nrm)
+    monkeypatch.setenv("LQRO_DYN_LANE", "1")
+    u1 = lqro_mod.dynamics_step(other, g, nrm)
+    assert np.array_equal(u0.view(np.uint64), u1.view(np.uint64))
+    for k in STATE:
+        assert np.array_equal(st[k].view(np.uint64), other[k].view(np.uint64)), k
