@@ -378,14 +378,24 @@ def dynamics_step(st: dict, gains: dict, nrm: np.ndarray, models=None, M=None, N
 # Reference-shaped interface
 # ---------------------------------------------------------------------------
 class Quadrotor:
-    """The fields of class Quadrotor (LQRO:73-165) that the pair loop uses."""
+    """The fields of class Quadrotor (LQRO:73-165) that the pair loop and the
+    agent update (LQRO:1437-1446) use."""
 
-    def __init__(self, x, vGoal=None):
+    def __init__(self, x, vGoal=None, pGoal=None):
         self.x = np.asarray(x, dtype=np.float64).copy()
         self.vGoal = np.zeros(3) if vGoal is None else np.asarray(vGoal, dtype=np.float64).copy()
         self.newV = np.zeros(3)
+        self.pGoal = np.zeros(3) if pGoal is None else np.asarray(pGoal, dtype=np.float64).copy()
         self.L = None
         self.E = None
+        self.l = np.zeros(4)   # zero at hover (c = 0); the pair path never reads it
+        self.Lh = None
+        self.Eh = None
+        # estimation state (setupQuadrotors, LQRO:107-122, without its noise draw)
+        self.Rot = np.eye(3)
+        self.xTrue = self.x.copy()
+        self.RotTrue = np.eye(3)
+        self.P = 1e-9 * np.eye(16)
 
 
 class Simulator:
@@ -397,6 +407,7 @@ class Simulator:
         self.qlist = list(qlist)
         self.model = model or default_model()
         flags = LQRO_FLAG_RECORDS if records else 0
+        self.device = device
         self.ctx = Context(config(len(self.qlist), horizon, n_points, device=device,
                                   flags=flags))
         self.A = self.B = self.c = None
@@ -405,7 +416,7 @@ class Simulator:
         g = synthesize_gains(self.model)
         self.A, self.B, self.c = g["A"], g["B"], g["c"]
         for q in self.qlist:
-            q.L, q.E = g["L"], g["E"]
+            q.L, q.E, q.Lh, q.Eh = g["L"], g["E"], g["Lh"], g["Eh"]
         Ls = np.stack([q.L for q in self.qlist])
         Es = np.stack([q.E for q in self.qlist])
         per_agent = not all(np.array_equal(Ls[0], l) for l in Ls) or \
@@ -423,6 +434,28 @@ class Simulator:
         for q, v in zip(self.qlist, newv):
             q.newV = v.copy()
         return newv
+
+    def update(self, seed: int) -> int:
+        """The agent loop after the pair loop (LQRO:1437-1446) on the GPU:
+        vGoal = newV, findU, propagateU, kalmanFilter1, the observation draw,
+        kalmanFilter2, vGoal = findVGoal.  Noise from the reference's rand()
+        stream seeded with `seed`; returns the next seed."""
+        n = len(self.qlist)
+        nrm, seed = normals(seed, n * NORMALS_PER_AGENT)
+        hover = self.model.gravity * self.model.mass / 4
+        st = dict(x=np.stack([q.x for q in self.qlist]), rot=np.stack([q.Rot for q in self.qlist]),
+                  x_true=np.stack([q.xTrue for q in self.qlist]),
+                  rot_true=np.stack([q.RotTrue for q in self.qlist]),
+                  P=np.stack([q.P for q in self.qlist]), vgoal=np.stack([q.newV for q in self.qlist]),
+                  u_goal=np.full((n, 4), hover), p_goal=np.stack([q.pGoal for q in self.qlist]))
+        gains = {k: np.stack([getattr(q, k) for q in self.qlist]) for k in ("L", "E", "l", "Lh", "Eh")}
+        dynamics_step(st, gains, nrm, models=[self.model], per_agent=True, device=self.device)
+        for a, q in enumerate(self.qlist):
+            q.x, q.Rot, q.xTrue, q.RotTrue, q.P = (st["x"][a].copy(), st["rot"][a].copy(),
+                                                   st["x_true"][a].copy(), st["rot_true"][a].copy(),
+                                                   st["P"][a].copy())
+            q.vGoal = st["vgoal"][a].copy()
+        return seed
 
 
 # ---------------------------------------------------------------------------

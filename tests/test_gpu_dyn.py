@@ -186,3 +186,31 @@ def test_wave_kernel_matches_lane_kernel(lqro_mod, oracle, monkeypatch):
     assert np.array_equal(u0.view(np.uint64), u1.view(np.uint64))
     for k in STATE:
         assert np.array_equal(st[k].view(np.uint64), other[k].view(np.uint64)), k
+
+
+def test_simulator_loop(lqro_mod, oracle):
+    """The reference-shaped driver: Simulator.step (LQRO:1393-1436) then
+    Simulator.update (LQRO:1437-1446), two control steps, against the oracle."""
+    n, H, NP = 8, 25, 50
+    x0, vg0 = lqro_mod.synthetic_swarm(n, seed=41, box=2.5)
+    qs = [lqro_mod.Quadrotor(x0[a], vg0[a], pGoal=-x0[a, :3]) for a in range(n)]
+    sim = lqro_mod.Simulator(qs, horizon=H, n_points=NP)
+    g = sim.findMatrices()
+    g = dict(g, l=np.zeros(4))
+    ref = lqro_mod.agent_states(x0, p_goal=-x0[:, :3])
+    ref["vgoal"][:] = vg0
+    T, NCF = oracle.tables(g["A"], g["B"], g["L"], g["E"], H)
+    S = oracle.sphere(NP)
+    seed = seed_ref = 3
+    for t in range(2):
+        sim.step()
+        seed = sim.update(seed)
+        newv, _ = oracle.step(T, NCF, S, ref["x"], ref["vgoal"], records=False)
+        ref["vgoal"][:] = newv
+        nrm, seed_ref = lqro_mod.normals(seed_ref, n * lqro_mod.NORMALS_PER_AGENT)
+        oracle.agent_step(ref, g, nrm)
+    got = dict(x=np.stack([q.x for q in qs]), rot=np.stack([q.Rot for q in qs]),
+               x_true=np.stack([q.xTrue for q in qs]), rot_true=np.stack([q.RotTrue for q in qs]),
+               P=np.stack([q.P for q in qs]), vgoal=np.stack([q.vGoal for q in qs]))
+    _compare(got, ref, 1e-7)
+    assert seed == seed_ref
