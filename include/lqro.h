@@ -133,6 +133,16 @@ void lqro_destroy(lqro_ctx* ctx);
 int lqro_set_gains(lqro_ctx* ctx, const double* A, const double* B,
                    const double* L, const double* E, int32_t per_agent);
 
+/* Opt-in neighbour culling, in place of the all-pairs
+ * loop (LQRO:1396): agent i then computes only the pairs with the
+ * max_neighbors agents j != i of smallest |p_i - p_j|^2 < neighbor_dist^2
+ * (ties to the lower j), RVO2-3D's computeNeighbors / insertAgentNeighbor
+ * (Agent.cpp:74-81, 153-174) with agents visited in j order; its LP sees those
+ * planes in j order.  Culled pairs emit no plane; their records carry
+ * n_reach = -1; lqro_get_stats()[0] counts the kept pairs.  This CHANGES
+ * results against the reference.  max_neighbors <= 0 restores all pairs. */
+int lqro_set_neighbors(lqro_ctx* ctx, double neighbor_dist, int32_t max_neighbors);
+
 /* One control step: the pair loop LQRO:1393-1436 for the context's rows.
  * x: n_agents*X agent states (Quadrotor::x), vgoal: n_agents*3,
  * newv: n_agents*3 (only rows [row_begin,row_end) are written).  Host

@@ -67,6 +67,7 @@ struct PairArgs {
   int* hot_next;
   int hot_cap;
   int hot_only;                       // 1: this launch computes the hot list only
+  const unsigned char* nbr;           // per slot: 1 = neighbour pair (culling on), null = all pairs
   // LDS layout, in doubles
   int XP, lds_T, lds_N, lds_S, lds_R, lds_TF, lds_H, lds_wave, wave_doubles;
 };
@@ -388,6 +389,21 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
   auto do_pair = [&](const int i, const int lrow, const int jj) {
     const double* xi = P.x + (size_t)i * X;
     const int j = jj < i ? jj : jj + 1;
+    if (P.nbr != nullptr && !P.nbr[(size_t)lrow * P.npr + jj]) {   // culled (lqro_set_neighbors)
+      if (lane == 0) {
+        const size_t cs = (size_t)lrow * P.npr + jj;
+        float4* dst = reinterpret_cast<float4*>(P.planes + cs * 8);
+        dst[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+        dst[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (P.recs != nullptr) {
+          lqro_pair_record rec;
+          memset(&rec, 0, sizeof rec);
+          rec.i = i; rec.j = j; rec.n_reach = -1;
+          P.recs[cs] = rec;
+        }
+      }
+      return;
+    }
     const double* xj = P.x + (size_t)j * X;
     double d[X];
 #pragma unroll
@@ -662,6 +678,49 @@ template <int X>
 __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
   extern __shared__ double lds[];
   pair_block<X>(P, lds);
+}
+
+// k_nbr: opt-in neighbour culling (RVO2 computeNeighbors /
+// insertAgentNeighbor, AGT:74-81,153-174).  One wave per row: agent i keeps
+// the k agents j != i with the smallest (d2, j), d2 = |p_i - p_j|^2 < r2 —
+// the set RVO2's sorted insertion keeps when agents are visited in j order.
+// Found by k rounds of a wave arg-min above the previous key; marks the
+// row's slots and counts the kept pairs into stats[0].
+__global__ void __launch_bounds__(64) k_nbr(const double* x, int X, int N, int row_begin, int npr, double r2,
+                                            int k, unsigned char* mark, unsigned long long* stats) {
+  const int lrow = blockIdx.x, lane = threadIdx.x, i = row_begin + lrow;
+  const double* xi = x + (size_t)i * X;
+  double ld = -1.0;   // last selected key (d2, j); d2 >= 0
+  int lj = -1, taken = 0;
+  for (int it = 0; it < k; ++it) {
+    double bd = INFINITY;
+    int bj = INT_MAX;
+    for (int j = lane; j < N; j += 64) {
+      if (j == i) continue;
+      const double* xj = x + (size_t)j * X;
+      const double dx = xi[0] - xj[0], dy = xi[1] - xj[1], dz = xi[2] - xj[2];
+      const double d2 = dx * dx + dy * dy + dz * dz;
+      if (!(d2 < r2)) continue;
+      if (d2 < ld || (d2 == ld && j <= lj)) continue;   // already taken
+      if (d2 < bd || (d2 == bd && j < bj)) { bd = d2; bj = j; }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const double od = __shfl_xor(bd, off);
+      const int oj = __shfl_xor(bj, off);
+      if (od < bd || (od == bd && oj < bj)) { bd = od; bj = oj; }
+    }
+    if (bj == INT_MAX) break;
+    ld = bd; lj = bj; ++taken;
+  }
+  for (int jj = lane; jj < npr; jj += 64) {
+    const int j = jj < i ? jj : jj + 1;
+    const double* xj = x + (size_t)j * X;
+    const double dx = xi[0] - xj[0], dy = xi[1] - xj[1], dz = xi[2] - xj[2];
+    const double d2 = dx * dx + dy * dy + dz * dz;
+    mark[(size_t)lrow * npr + jj] = (taken > 0 && d2 < r2 && (d2 < ld || (d2 == ld && j <= lj))) ? 1 : 0;
+  }
+  if (lane == 0) atomicAdd(&stats[0], (unsigned long long)taken);
 }
 
 // k_prio: which pairs go first.  A pair whose relative motion brings the two

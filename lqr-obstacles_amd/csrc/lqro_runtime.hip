@@ -340,6 +340,9 @@ struct lqro_ctx {
   int* d_lp4;                // k_lp_lds -> k_lp4 row list (6 ints per row)
   int* d_hotlist;            // k_prio: likely inside-hull pairs (slots), computed first
   unsigned char* d_hotmark;  // per slot: in the hot list
+  unsigned char* d_nbr;      // per slot: neighbour pair (lqro_set_neighbors), null = all pairs
+  double nbr_r2;
+  int nbr_k;
   int hot_cap;
   int hot_on;                // LQRO_HOT (default 1)
   double hot_t, hot_r;       // k_prio horizon (s) and radius (m): LQRO_HOT_T, LQRO_HOT_R
@@ -409,7 +412,7 @@ void lqro_destroy(lqro_ctx* c) {
   (void)hipSetDevice(c->cfg.device);
   void* ps[] = {c->d_R, c->d_TF, c->d_shash, c->d_T, c->d_NCF, c->d_S, c->d_x, c->d_vgoal, c->d_newv, c->d_A, c->d_B,
                 c->d_L, c->d_E, c->d_planes, c->d_lpscratch, c->d_lpcompact, c->d_recs, c->d_hq, c->d_hcount,
-                c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats, c->d_prof, c->d_rq, c->d_hbig, c->d_hwide, c->d_hbag, c->d_lp4, c->d_hotlist, c->d_hotmark, c->d_hfbest, c->d_hvpid, c->d_hstack};
+                c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats, c->d_prof, c->d_rq, c->d_hbig, c->d_hwide, c->d_hbag, c->d_lp4, c->d_hotlist, c->d_hotmark, c->d_nbr, c->d_hfbest, c->d_hvpid, c->d_hstack};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (int k = 0; k < 5; ++k)
@@ -591,6 +594,20 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
   return LQRO_OK;
 }
 
+int lqro_set_neighbors(lqro_ctx* c, double neighbor_dist, int32_t max_neighbors) {
+  if (!c) return LQRO_E_ARG;
+  if (max_neighbors <= 0) { c->nbr_k = 0; return LQRO_OK; }
+  if (!(neighbor_dist > 0)) return LQRO_E_ARG;
+  HIPCHK(hipSetDevice(c->cfg.device));
+  if (!c->d_nbr) {
+    const size_t slots = (size_t)c->nrows * c->npr;
+    if (hipMalloc(&c->d_nbr, slots ? slots : 1) != hipSuccess) return LQRO_E_NOMEM;
+  }
+  c->nbr_r2 = neighbor_dist * neighbor_dist;
+  c->nbr_k = max_neighbors;
+  return LQRO_OK;
+}
+
 int lqro_set_gains(lqro_ctx* c, const double* A, const double* B, const double* L,
                    const double* E, int32_t per_agent) {
   if (!c || !A || !B || !L || !E) return LQRO_E_ARG;
@@ -649,6 +666,13 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   HIPCHK(hipMemsetAsync(c->d_hcount, 0, sizeof(int) * 16, s));
   HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * 8, s));
   HIPCHK(hipMemsetAsync(c->d_hq, 0xFF, sizeof(int) * (size_t)c->hull_cap, s));
+  P.nbr = nullptr;
+  if (c->nbr_k > 0) {
+    hipLaunchKernelGGL(k_nbr, dim3((unsigned)c->nrows), dim3(64), 0, s, d_x, g.x_dim, g.n_agents, c->rb, c->npr,
+                       c->nbr_r2, c->nbr_k, c->d_nbr, c->d_stats);
+    HIPCHK(hipGetLastError());
+    P.nbr = c->d_nbr;
+  }
   // the LDS hull variant packs outside-set extents in 32 bits: H*NP <= 16383
   const bool lds_ok = (size_t)g.horizon * g.n_points <= 16383;
   const long slots = (long)c->nrows * c->npr;
@@ -1015,7 +1039,7 @@ int lqro_get_stats(lqro_ctx* c, int64_t* st) {
   unsigned long long h[8];
   HIPCHK(hipMemcpy(h, c->d_stats, sizeof h, hipMemcpyDeviceToHost));
   for (int k = 0; k < 8; ++k) st[k] = (int64_t)h[k];
-  st[0] = (int64_t)c->nrows * c->npr;
+  if (c->nbr_k <= 0) st[0] = (int64_t)c->nrows * c->npr;   // else k_nbr counted the kept pairs
   return LQRO_OK;
 }
 

@@ -72,7 +72,7 @@ EXPORTS = (
     "lqro_create", "lqro_destroy", "lqro_set_gains", "lqro_step", "lqro_step_device",
     "lqro_get_records", "lqro_get_stats", "lqro_get_timings", "lqro_status_string",
     "lqro_version", "lqro_calculate_new_v", "lqro_synthesize_gains_batch",
-    "lqro_dynamics_step", "lqro_dynamics_step_device", "lqro_normals",
+    "lqro_dynamics_step", "lqro_dynamics_step_device", "lqro_normals", "lqro_set_neighbors",
 )
 
 NORMALS_PER_AGENT = 22   # LQRO_NORMALS_PER_AGENT: 16 propagate + 6 observation
@@ -115,6 +115,7 @@ def lib() -> C.CDLL:
         L.lqro_dynamics_step.argtypes = [C.POINTER(Model), i32, i32, i32, C.POINTER(Agents), i32]
         L.lqro_dynamics_step_device.argtypes = [vp, i32, i32, i32, C.POINTER(Agents), vp]
         L.lqro_normals.argtypes = [C.POINTER(C.c_uint32), i64, vp]
+        L.lqro_set_neighbors.argtypes = [vp, dbl, i32]
         _lib = L
     return _lib
 
@@ -203,6 +204,12 @@ class Context:
             self.close()
         except Exception:
             pass
+
+    def set_neighbors(self, neighbor_dist: float, max_neighbors: int):
+        """Opt-in neighbour culling (lqro_set_neighbors; RVO2 computeNeighbors,
+        AGT:74-81,153-174).  Changes results; max_neighbors <= 0 = all pairs."""
+        _check(lib().lqro_set_neighbors(self._h, float(neighbor_dist), int(max_neighbors)),
+               "lqro_set_neighbors")
 
     def set_gains(self, A, B, L, E, per_agent: bool = False):
         A, B, L, E = (np.ascontiguousarray(v, dtype=np.float64) for v in (A, B, L, E))

@@ -1124,10 +1124,53 @@ void orc_inverse4(const double* in, double* out) { minv(4, in, out); }
 /* ------------------------------------------------------------------------ */
 /* Whole step                                                                */
 /* ------------------------------------------------------------------------ */
+/* Opt-in neighbour culling (SURVEY §8f next #3, RVO2 computeNeighbors /
+ * insertAgentNeighbor, AGT:74-81,153-174): agent i keeps the max_nbr agents
+ * j != i with the smallest d2 = |p_i - p_j|^2 < nbr_dist^2, ties to the lower
+ * j (RVO2 keeps the earlier-visited one).  Only their pairs are computed, and
+ * the LP sees their planes in j order.  0 neighbours = all pairs (the
+ * reference's loop). */
+static double g_nbr_r2 = 0.0;
+static int g_nbr_k = 0;
+
+void orc_set_neighbors(double nbr_dist, int max_nbr) {
+  g_nbr_r2 = nbr_dist * nbr_dist;
+  g_nbr_k = max_nbr;
+}
+
+static double nbr_d2(const double* x, int X, int i, int j) {
+  const double dx = x[(size_t)i * X] - x[(size_t)j * X];
+  const double dy = x[(size_t)i * X + 1] - x[(size_t)j * X + 1];
+  const double dz = x[(size_t)i * X + 2] - x[(size_t)j * X + 2];
+  return dx * dx + dy * dy + dz * dz;
+}
+
+/* sel[j] = 1 for agent i's neighbours (RVO2's sorted insertion, restated) */
+void orc_neighbors(int N, int X, const double* x, int i, double r2, int k, unsigned char* sel) {
+  double* kd = (double*)malloc(sizeof(double) * (size_t)(k > 0 ? k : 1));
+  int* kj = (int*)malloc(sizeof(int) * (size_t)(k > 0 ? k : 1));
+  int n = 0;
+  double range = r2;
+  for (int j = 0; j < N; ++j) {
+    sel[j] = 0;
+    if (j == i) continue;
+    const double d2 = nbr_d2(x, X, i, j);
+    if (!(d2 < range)) continue;
+    if (n < k) n++;
+    int p = n - 1;
+    while (p != 0 && d2 < kd[p - 1]) { kd[p] = kd[p - 1]; kj[p] = kj[p - 1]; --p; }
+    kd[p] = d2; kj[p] = j;
+    if (n == k) range = kd[n - 1];
+  }
+  for (int q = 0; q < n; ++q) sel[kj[q]] = 1;
+  free(kd); free(kj);
+}
+
 int orc_step(int N, int X, int H, int NP, int min_reach, double vmax_reach, double vmax_lp,
              int per_agent, const double* T, const double* NCF, const double* S,
              const double* x, const double* vgoal, int r0, int r1, double* newv,
              lqro_pair_record* recs) {
+  unsigned char* sel = (unsigned char*)malloc((size_t)N);
   double* pts = (double*)malloc(sizeof(double) * 3 * (size_t)H * (size_t)NP);
   float* planes = (float*)malloc(sizeof(float) * 6 * (size_t)(N > 1 ? N - 1 : 1));
   lqro_pair_record rec;
@@ -1136,8 +1179,17 @@ int orc_step(int N, int X, int H, int NP, int min_reach, double vmax_reach, doub
     const double* Ti = per_agent ? T + (size_t)i * H * 9 : T;
     const double* Ni = per_agent ? NCF + (size_t)i * H * 3 * X : NCF;
     int m = 0;
+    if (g_nbr_k > 0) orc_neighbors(N, X, x, i, g_nbr_r2, g_nbr_k, sel);
     for (int j = 0; j < N; ++j) {
       if (j == i) continue;
+      if (g_nbr_k > 0 && !sel[j]) {   /* culled: no pair, no plane */
+        if (recs) {
+          lqro_pair_record* r = &recs[(size_t)(i - r0) * (N - 1) + (j < i ? j : j - 1)];
+          memset(r, 0, sizeof *r);
+          r->i = i; r->j = j; r->n_reach = -1;
+        }
+        continue;
+      }
       rc = orc_pair(X, H, NP, min_reach, vmax_reach, Ti, Ni, S, x + (size_t)i * X,
                     x + (size_t)j * X, i, j, &rec, NULL, pts);
       if (rc) goto out;
@@ -1153,7 +1205,7 @@ int orc_step(int N, int X, int H, int NP, int min_reach, double vmax_reach, doub
     orc_newv(m, planes, vgoal + (size_t)i * 3, vmax_lp, newv + (size_t)i * 3);  /* LQRO:1435 */
   }
 out:
-  free(pts); free(planes);
+  free(pts); free(planes); free(sel);
   return rc;
 }
 

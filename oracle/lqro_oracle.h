@@ -72,6 +72,13 @@ int  orc_step(int N, int X, int H, int NP, int min_reach, double vmax_reach,
               const double* S, const double* x, const double* vgoal,
               int r0, int r1, double* newv, lqro_pair_record* recs);
 
+/* Opt-in neighbour culling for orc_step / orc_step_mt (RVO2 computeNeighbors,
+ * AGT:74-81,153-174): max_nbr <= 0 restores all pairs.  Culled pairs get a
+ * record with n_reach = -1 and no plane.  orc_neighbors: agent i's selection
+ * (sel[j] = 1), RVO2's sorted insertion with a shrinking range. */
+void orc_set_neighbors(double nbr_dist, int max_nbr);
+void orc_neighbors(int N, int X, const double* x, int i, double r2, int k, unsigned char* sel);
+
 /* Same as orc_step, rows split over `threads` POSIX threads (private
  * scratch per thread; the reference itself is single-threaded). */
 int  orc_step_mt(int N, int X, int H, int NP, int min_reach, double vmax_reach,

@@ -51,6 +51,9 @@ def lib():
         _o.orc_hull.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int]
         _o.orc_agent_step.argtypes = [C.c_void_p] * 17
         _o.orc_jacobi.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        _o.orc_set_neighbors.argtypes = [C.c_double, C.c_int]
+        _o.orc_neighbors.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_double, C.c_int,
+                                     C.c_void_p]
     return _o
 
 
@@ -216,3 +219,15 @@ def jacobi(m):
     D = np.zeros((n, n))
     lib().orc_jacobi(n, _p(m), _p(V), _p(D))
     return V, D
+
+
+def set_neighbors(nbr_dist: float, max_nbr: int):
+    """Neighbour culling for step() (0 = all pairs; process-wide)."""
+    lib().orc_set_neighbors(float(nbr_dist), int(max_nbr))
+
+
+def neighbors(x, i: int, nbr_dist: float, max_nbr: int) -> np.ndarray:
+    x = np.ascontiguousarray(x, np.float64)
+    sel = np.zeros(x.shape[0], np.uint8)
+    lib().orc_neighbors(x.shape[0], x.shape[1], _p(x), i, nbr_dist * nbr_dist, max_nbr, _p(sel))
+    return sel

@@ -1,0 +1,65 @@
+"""Opt-in neighbour culling (RVO2 computeNeighbors /
+insertAgentNeighbor, AGT:74-81,153-174).  The oracle's selection against a
+brute-force restatement (CPU), then the GPU step with culling against the
+oracle step with culling (bit-exact records and newV)."""
+import numpy as np
+import pytest
+
+
+def _brute(x, i, r, k):
+    d = x[i, :3] - x[:, :3]   # the kernels' op order: dx*dx + dy*dy + dz*dz
+    d2 = d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1] + d[:, 2] * d[:, 2]
+    cand = [(d2[j], j) for j in range(len(x)) if j != i and d2[j] < r * r]
+    keep = sorted(cand)[:k]
+    sel = np.zeros(len(x), np.uint8)
+    for _, j in keep:
+        sel[j] = 1
+    return sel
+
+
+@pytest.mark.parametrize("seed,k,r", [(1, 4, 2.0), (2, 10, 3.0), (3, 100, 1.5), (4, 3, 50.0)])
+def test_oracle_selection(oracle, lqro_mod, seed, k, r):
+    x, _ = lqro_mod.synthetic_swarm(40, seed=seed, box=4.0)
+    for i in range(0, 40, 7):
+        assert np.array_equal(oracle.neighbors(x, i, r, k), _brute(x, i, r, k))
+
+
+def test_oracle_selection_ties(oracle):
+    """Equal distances: the lower j is kept (RVO2 keeps the earlier-visited)."""
+    x = np.zeros((7, 16))
+    for j, p in enumerate([(0, 0, 0), (1, 0, 0), (0, 1, 0), (0, 0, 1), (-1, 0, 0), (2, 0, 0), (0, -1, 0)]):
+        x[j, :3] = p
+    sel = oracle.neighbors(x, 0, 10.0, 3)
+    assert sel.tolist() == [0, 1, 1, 1, 0, 0, 0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,r", [(6, 2.5), (1, 1.0), (500, 1000.0)])
+def test_gpu_step_with_culling(lqro_mod, oracle, gains, k, r):
+    N, H, NP = 48, 40, 50
+    x, vg = lqro_mod.synthetic_swarm(N, seed=17, box=3.0)
+    T, NCF = oracle.tables(gains["A"], gains["B"], gains["L"], gains["E"], H)
+    S = oracle.sphere(NP)
+    oracle.set_neighbors(r, k)
+    try:
+        rv, rrecs = oracle.step(T, NCF, S, x, vg)
+    finally:
+        oracle.set_neighbors(0.0, 0)
+    ctx = lqro_mod.Context(lqro_mod.config(N, H, NP, flags=lqro_mod.LQRO_FLAG_RECORDS))
+    ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
+    ctx.set_neighbors(r, k)
+    newv = ctx.step(x, vg)
+    recs = ctx.records()
+    kept = rrecs["n_reach"] >= 0
+    assert np.array_equal(recs["n_reach"], rrecs["n_reach"])
+    assert ctx.stats()["pairs"] == int(kept.sum())
+    assert int(kept.sum()) == sum(min(k, int(oracle.neighbors(x, i, r, k).sum())) for i in range(N))
+    for f in ("flags", "gjk_iters", "simplex_n", "reach_hash"):
+        assert np.array_equal(recs[f], rrecs[f]), f
+    for f in ("plane_point", "plane_normal"):
+        assert np.array_equal(recs[f].view(np.uint32), rrecs[f].view(np.uint32)), f
+    np.testing.assert_array_equal(newv, rv)
+    # all pairs again
+    ctx.set_neighbors(0.0, 0)
+    ctx.step(x, vg)
+    assert ctx.stats()["pairs"] == N * (N - 1)
