@@ -138,8 +138,10 @@ int lqro_set_gains(lqro_ctx* ctx, const double* A, const double* B,
  * max_neighbors agents j != i of smallest |p_i - p_j|^2 < neighbor_dist^2
  * (ties to the lower j), RVO2-3D's computeNeighbors / insertAgentNeighbor
  * (Agent.cpp:74-81, 153-174) with agents visited in j order; its LP sees those
- * planes in j order.  Culled pairs emit no plane; their records carry
- * n_reach = -1; lqro_get_stats()[0] counts the kept pairs.  This CHANGES
+ * planes in j order.  A row then has K = min(max_neighbors, n_agents-1) slots
+ * instead of n_agents-1: lqro_get_records returns rows x K records, the q-th
+ * the row's q-th neighbour in ascending j; unused slots have j = -1 and
+ * n_reach = -1.  lqro_get_stats()[0] counts the kept pairs.  This CHANGES
  * results against the reference.  max_neighbors <= 0 restores all pairs. */
 int lqro_set_neighbors(lqro_ctx* ctx, double neighbor_dist, int32_t max_neighbors);
 

@@ -70,6 +70,7 @@ struct HullWide;
 struct HullArgs {
   int N, X, H, NP;
   int row_begin, npr, per_agent;
+  const int* nbr_list;   // culling on: slot -> neighbour jj (see PairArgs), else null
   double r2, r2_lo, r2_hi;
   const double* T;
   const double* NCF;
@@ -1386,7 +1387,7 @@ __device__ __forceinline__ void hull_body_mw(const HullArgs& A, HullMemC& M, Hul
   for (;;) {
     const int slot = hull_take_job(A, L, false);
     if (slot < 0) break;
-    const int lrow = slot / A.npr, jj = slot % A.npr;
+    const int lrow = slot / A.npr, jj = A.nbr_list ? A.nbr_list[slot] : slot % A.npr;
     const int i = A.row_begin + lrow;
     const int j = jj < i ? jj : jj + 1;
     const double* xi = A.x + (size_t)i * A.X;
@@ -1530,7 +1531,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
   for (;;) {
     const int slot = hull_take_job(A, L, retryq);
     if (slot < 0) break;
-    const int lrow = slot / A.npr, jj = slot % A.npr;
+    const int lrow = slot / A.npr, jj = A.nbr_list ? A.nbr_list[slot] : slot % A.npr;
     const int i = A.row_begin + lrow;
     const int j = jj < i ? jj : jj + 1;
     const double* xi = A.x + (size_t)i * A.X;

@@ -67,7 +67,7 @@ struct PairArgs {
   int* hot_next;
   int hot_cap;
   int hot_only;                       // 1: this launch computes the hot list only
-  const unsigned char* nbr;           // per slot: 1 = neighbour pair (culling on), null = all pairs
+  const int* nbr_list;                // culling on: per row npr (= K) neighbour jj, ascending, -1 = none
   // LDS layout, in doubles
   int XP, lds_T, lds_N, lds_S, lds_R, lds_TF, lds_H, lds_wave, wave_doubles;
 };
@@ -388,8 +388,9 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
   // one ordered pair (i, j = jj-th other agent) of local row lrow
   auto do_pair = [&](const int i, const int lrow, const int jj) {
     const double* xi = P.x + (size_t)i * X;
-    const int j = jj < i ? jj : jj + 1;
-    if (P.nbr != nullptr && !P.nbr[(size_t)lrow * P.npr + jj]) {   // culled (lqro_set_neighbors)
+    // culling on (lqro_set_neighbors): slot q of the row holds its q-th neighbour
+    const int jq = P.nbr_list != nullptr ? P.nbr_list[(size_t)lrow * P.npr + jj] : jj;
+    if (jq < 0) {   // fewer neighbours than slots
       if (lane == 0) {
         const size_t cs = (size_t)lrow * P.npr + jj;
         float4* dst = reinterpret_cast<float4*>(P.planes + cs * 8);
@@ -398,12 +399,13 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
         if (P.recs != nullptr) {
           lqro_pair_record rec;
           memset(&rec, 0, sizeof rec);
-          rec.i = i; rec.j = j; rec.n_reach = -1;
+          rec.i = i; rec.j = -1; rec.n_reach = -1;
           P.recs[cs] = rec;
         }
       }
       return;
     }
+    const int j = jq < i ? jq : jq + 1;
     const double* xj = P.x + (size_t)j * X;
     double d[X];
 #pragma unroll
@@ -684,10 +686,11 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
 // insertAgentNeighbor, AGT:74-81,153-174).  One wave per row: agent i keeps
 // the k agents j != i with the smallest (d2, j), d2 = |p_i - p_j|^2 < r2 —
 // the set RVO2's sorted insertion keeps when agents are visited in j order.
-// Found by k rounds of a wave arg-min above the previous key; marks the
-// row's slots and counts the kept pairs into stats[0].
+// Found by k rounds of a wave arg-min above the previous key; writes the
+// row's list of K = min(k, npr) slots (neighbour jj ascending, -1 padded)
+// and counts the kept pairs into stats[0].
 __global__ void __launch_bounds__(64) k_nbr(const double* x, int X, int N, int row_begin, int npr, double r2,
-                                            int k, unsigned char* mark, unsigned long long* stats) {
+                                            int k, int K, int* list, unsigned long long* stats) {
   const int lrow = blockIdx.x, lane = threadIdx.x, i = row_begin + lrow;
   const double* xi = x + (size_t)i * X;
   double ld = -1.0;   // last selected key (d2, j); d2 >= 0
@@ -713,13 +716,23 @@ __global__ void __launch_bounds__(64) k_nbr(const double* x, int X, int N, int r
     if (bj == INT_MAX) break;
     ld = bd; lj = bj; ++taken;
   }
-  for (int jj = lane; jj < npr; jj += 64) {
-    const int j = jj < i ? jj : jj + 1;
-    const double* xj = x + (size_t)j * X;
-    const double dx = xi[0] - xj[0], dy = xi[1] - xj[1], dz = xi[2] - xj[2];
-    const double d2 = dx * dx + dy * dy + dz * dz;
-    mark[(size_t)lrow * npr + jj] = (taken > 0 && d2 < r2 && (d2 < ld || (d2 == ld && j <= lj))) ? 1 : 0;
+  int* row = list + (size_t)lrow * K;
+  int cnt = 0;
+  for (int base = 0; base < npr; base += 64) {
+    const int jj = base + lane;
+    bool sel = false;
+    if (jj < npr && taken > 0) {
+      const int j = jj < i ? jj : jj + 1;
+      const double* xj = x + (size_t)j * X;
+      const double dx = xi[0] - xj[0], dy = xi[1] - xj[1], dz = xi[2] - xj[2];
+      const double d2 = dx * dx + dy * dy + dz * dz;
+      sel = d2 < r2 && (d2 < ld || (d2 == ld && j <= lj));
+    }
+    const unsigned long long bal = __ballot(sel);
+    if (sel) row[cnt + __popcll(bal & ((1ull << lane) - 1ull))] = jj;
+    cnt += __popcll(bal);
   }
+  for (int q = cnt + lane; q < K; q += 64) row[q] = -1;
   if (lane == 0) atomicAdd(&stats[0], (unsigned long long)taken);
 }
 

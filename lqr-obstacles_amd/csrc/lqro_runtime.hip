@@ -340,9 +340,9 @@ struct lqro_ctx {
   int* d_lp4;                // k_lp_lds -> k_lp4 row list (6 ints per row)
   int* d_hotlist;            // k_prio: likely inside-hull pairs (slots), computed first
   unsigned char* d_hotmark;  // per slot: in the hot list
-  unsigned char* d_nbr;      // per slot: neighbour pair (lqro_set_neighbors), null = all pairs
+  int* d_nbrlist;            // culling on: per row K neighbour slots (lqro_set_neighbors)
   double nbr_r2;
-  int nbr_k;
+  int nbr_k, nbr_cap;         // k; rows x nbr_cap ints allocated
   int hot_cap;
   int hot_on;                // LQRO_HOT (default 1)
   double hot_t, hot_r;       // k_prio horizon (s) and radius (m): LQRO_HOT_T, LQRO_HOT_R
@@ -412,7 +412,7 @@ void lqro_destroy(lqro_ctx* c) {
   (void)hipSetDevice(c->cfg.device);
   void* ps[] = {c->d_R, c->d_TF, c->d_shash, c->d_T, c->d_NCF, c->d_S, c->d_x, c->d_vgoal, c->d_newv, c->d_A, c->d_B,
                 c->d_L, c->d_E, c->d_planes, c->d_lpscratch, c->d_lpcompact, c->d_recs, c->d_hq, c->d_hcount,
-                c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats, c->d_prof, c->d_rq, c->d_hbig, c->d_hwide, c->d_hbag, c->d_lp4, c->d_hotlist, c->d_hotmark, c->d_nbr, c->d_hfbest, c->d_hvpid, c->d_hstack};
+                c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats, c->d_prof, c->d_rq, c->d_hbig, c->d_hwide, c->d_hbag, c->d_lp4, c->d_hotlist, c->d_hotmark, c->d_nbrlist, c->d_hfbest, c->d_hvpid, c->d_hstack};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (int k = 0; k < 5; ++k)
@@ -599,9 +599,13 @@ int lqro_set_neighbors(lqro_ctx* c, double neighbor_dist, int32_t max_neighbors)
   if (max_neighbors <= 0) { c->nbr_k = 0; return LQRO_OK; }
   if (!(neighbor_dist > 0)) return LQRO_E_ARG;
   HIPCHK(hipSetDevice(c->cfg.device));
-  if (!c->d_nbr) {
-    const size_t slots = (size_t)c->nrows * c->npr;
-    if (hipMalloc(&c->d_nbr, slots ? slots : 1) != hipSuccess) return LQRO_E_NOMEM;
+  const int K = std::min<int>(max_neighbors, c->npr);
+  if (K > c->nbr_cap) {
+    if (c->d_nbrlist) (void)hipFree(c->d_nbrlist);
+    c->d_nbrlist = nullptr;
+    c->nbr_cap = 0;
+    if (hipMalloc(&c->d_nbrlist, sizeof(int) * (size_t)c->nrows * K + 4) != hipSuccess) return LQRO_E_NOMEM;
+    c->nbr_cap = K;
   }
   c->nbr_r2 = neighbor_dist * neighbor_dist;
   c->nbr_k = max_neighbors;
@@ -639,7 +643,9 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   const lqro_config& g = c->cfg;
   PairArgs P = c->pa;
   P.N = g.n_agents; P.H = g.horizon; P.NP = g.n_points; P.min_reach = g.min_reach;
-  P.row_begin = c->rb; P.nrows = c->nrows; P.npr = c->npr;
+  // culling on: each row's slots are its K neighbours (k_nbr), not its N-1 pairs
+  const int npr = c->nbr_k > 0 ? std::min(c->nbr_k, c->npr) : c->npr;
+  P.row_begin = c->rb; P.nrows = c->nrows; P.npr = npr;
   P.per_agent = c->per_agent;
   P.vmax = g.vmax_reach;
   P.r2 = g.vmax_reach * g.vmax_reach;
@@ -666,19 +672,20 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   HIPCHK(hipMemsetAsync(c->d_hcount, 0, sizeof(int) * 16, s));
   HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * 8, s));
   HIPCHK(hipMemsetAsync(c->d_hq, 0xFF, sizeof(int) * (size_t)c->hull_cap, s));
-  P.nbr = nullptr;
+  P.nbr_list = nullptr;
   if (c->nbr_k > 0) {
     hipLaunchKernelGGL(k_nbr, dim3((unsigned)c->nrows), dim3(64), 0, s, d_x, g.x_dim, g.n_agents, c->rb, c->npr,
-                       c->nbr_r2, c->nbr_k, c->d_nbr, c->d_stats);
+                       c->nbr_r2, c->nbr_k, npr, c->d_nbrlist, c->d_stats);
     HIPCHK(hipGetLastError());
-    P.nbr = c->d_nbr;
+    P.nbr_list = c->d_nbrlist;
   }
   // the LDS hull variant packs outside-set extents in 32 bits: H*NP <= 16383
   const bool lds_ok = (size_t)g.horizon * g.n_points <= 16383;
-  const long slots = (long)c->nrows * c->npr;
+  const long slots = (long)c->nrows * npr;
   const bool side_fits = (size_t)(P.lds_wave + HULL_CWAVES * P.wave_doubles) * 8 <= sizeof(HullMemC) &&
                          P.waves >= HULL_CWAVES;
-  const bool hot = c->hot_on && !c->per_agent && lds_ok && side_fits && c->n_cu >= 64 && slots >= 65536;
+  const bool hot = c->hot_on && !c->per_agent && lds_ok && side_fits && c->n_cu >= 64 && slots >= 65536 &&
+                   c->nbr_k <= 0;
   const int nwait = hot ? c->side_cus : 0;
   P.row_split = std::max(1, std::min(16, (2 * c->n_cu + c->nrows - 1) / c->nrows));
   const int units = c->nrows * P.row_split;
@@ -699,7 +706,8 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   }
   HullArgs Hh;
   Hh.N = g.n_agents; Hh.X = g.x_dim; Hh.H = g.horizon; Hh.NP = g.n_points;
-  Hh.row_begin = c->rb; Hh.npr = c->npr; Hh.per_agent = c->per_agent;
+  Hh.row_begin = c->rb; Hh.npr = npr; Hh.per_agent = c->per_agent;
+  Hh.nbr_list = P.nbr_list;
   Hh.r2 = P.r2; Hh.r2_lo = P.r2_lo; Hh.r2_hi = P.r2_hi;
   Hh.T = c->d_T; Hh.NCF = c->d_NCF; Hh.S = c->d_S; Hh.x = d_x;
   Hh.planes = c->d_planes; Hh.recs = c->d_recs;
@@ -755,7 +763,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev[2], s));
   LpArgs La;
-  La.npr = c->npr; La.nrows = c->nrows; La.row_begin = c->rb; La.vmax = g.vmax_lp;
+  La.npr = npr; La.nrows = c->nrows; La.row_begin = c->rb; La.vmax = g.vmax_lp;
   La.slots = c->d_planes; La.compact = c->d_lpcompact; La.proj = c->d_lpscratch;
   La.vgoal = d_vgoal; La.newv = d_newv; La.prof = c->d_prof;
   La.lp4_list = c->d_lp4; La.lp4_count = c->d_hcount + 9; La.lp4_next = c->d_hcount + 10;
@@ -1023,7 +1031,7 @@ int lqro_calculate_new_v(const float* planes, const int64_t* offsets, int32_t n_
 int lqro_get_records(lqro_ctx* c, lqro_pair_record* out, int64_t cap, int64_t* n_out) {
   if (!c || !out) return LQRO_E_ARG;
   if (!c->d_recs) return LQRO_E_STATE;
-  const int64_t n = (int64_t)c->nrows * c->npr;
+  const int64_t n = (int64_t)c->nrows * (c->nbr_k > 0 ? std::min(c->nbr_k, c->npr) : c->npr);
   if (cap < n) return LQRO_E_ARG;
   HIPCHK(hipSetDevice(c->cfg.device));
   HIPCHK(hipStreamSynchronize(c->stream));

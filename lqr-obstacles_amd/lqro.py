@@ -234,7 +234,7 @@ class Context:
         out = np.zeros(n, dtype=RECORD_DTYPE)
         got = C.c_int64()
         _check(lib().lqro_get_records(self._h, _p(out), n, C.byref(got)), "lqro_get_records")
-        return out
+        return out[:got.value]   # rows x K with neighbour culling on
 
     def stats(self) -> dict:
         s = np.zeros(8, dtype=np.int64)

@@ -34,10 +34,12 @@ def test_oracle_selection_ties(oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k,r", [(6, 2.5), (1, 1.0), (500, 1000.0)])
-def test_gpu_step_with_culling(lqro_mod, oracle, gains, k, r):
+@pytest.mark.parametrize("k,r,box", [(6, 2.5, 3.0), (1, 1.0, 3.0), (500, 1000.0, 3.0), (8, 3.0, 1.6)])
+def test_gpu_step_with_culling(lqro_mod, oracle, gains, k, r, box):
+    """box 1.6: a dense swarm, so neighbour pairs reach the in-kernel hull
+    (slot -> neighbour mapping in k_hull)."""
     N, H, NP = 48, 40, 50
-    x, vg = lqro_mod.synthetic_swarm(N, seed=17, box=3.0)
+    x, vg = lqro_mod.synthetic_swarm(N, seed=17, box=box)
     T, NCF = oracle.tables(gains["A"], gains["B"], gains["L"], gains["E"], H)
     S = oracle.sphere(NP)
     oracle.set_neighbors(r, k)
@@ -50,14 +52,25 @@ def test_gpu_step_with_culling(lqro_mod, oracle, gains, k, r):
     ctx.set_neighbors(r, k)
     newv = ctx.step(x, vg)
     recs = ctx.records()
+    K = min(k, N - 1)
+    assert recs.shape[0] == N * K
     kept = rrecs["n_reach"] >= 0
-    assert np.array_equal(recs["n_reach"], rrecs["n_reach"])
     assert ctx.stats()["pairs"] == int(kept.sum())
-    assert int(kept.sum()) == sum(min(k, int(oracle.neighbors(x, i, r, k).sum())) for i in range(N))
-    for f in ("flags", "gjk_iters", "simplex_n", "reach_hash"):
-        assert np.array_equal(recs[f], rrecs[f]), f
-    for f in ("plane_point", "plane_normal"):
-        assert np.array_equal(recs[f].view(np.uint32), rrecs[f].view(np.uint32)), f
+    rr = rrecs.reshape(N, N - 1)
+    gr = recs.reshape(N, K)
+    for i in range(N):   # row i: its neighbours in ascending j, then empty slots
+        ref_row = rr[i][rr[i]["n_reach"] >= 0]
+        c = len(ref_row)
+        assert c <= K and np.all(gr[i][c:]["n_reach"] == -1) and np.all(gr[i][c:]["j"] == -1)
+        g = gr[i][:c]
+        for f in ("i", "j", "n_reach", "flags", "gjk_iters", "simplex_n", "reach_hash"):
+            assert np.array_equal(g[f], ref_row[f]), (i, f)
+        for f in ("plane_point", "plane_normal"):
+            assert np.array_equal(g[f].view(np.uint32), ref_row[f].view(np.uint32)), (i, f)
+        ins = (g["flags"] & lqro_mod.REC_INSIDE) != 0
+        assert np.array_equal(g["facet"][ins], ref_row["facet"][ins]), i
+    if box < 2:
+        assert int(((recs["flags"] & lqro_mod.REC_INSIDE) != 0).sum()) > 0
     np.testing.assert_array_equal(newv, rv)
     # all pairs again
     ctx.set_neighbors(0.0, 0)
