@@ -691,21 +691,51 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
 // and counts the kept pairs into stats[0].
 __global__ void __launch_bounds__(64) k_nbr(const double* x, int X, int N, int row_begin, int npr, double r2,
                                             int k, int K, int* list, unsigned long long* stats) {
+  constexpr int kCap = 1024;   // candidates within r held in LDS
+  __shared__ double cd[kCap];
+  __shared__ int cj[kCap];
   const int lrow = blockIdx.x, lane = threadIdx.x, i = row_begin + lrow;
   const double* xi = x + (size_t)i * X;
+  // one scan: the agents within r (ascending j), usually a few dozen
+  int ncand = 0;
+  for (int base = 0; base < N; base += 64) {
+    const int j = base + lane;
+    double d2 = INFINITY;
+    if (j < N && j != i) {
+      const double* xj = x + (size_t)j * X;
+      const double dx = xi[0] - xj[0], dy = xi[1] - xj[1], dz = xi[2] - xj[2];
+      d2 = dx * dx + dy * dy + dz * dz;
+    }
+    const bool c = d2 < r2;
+    const unsigned long long bal = __ballot(c);
+    const int pos = ncand + __popcll(bal & ((1ull << lane) - 1ull));
+    if (c && pos < kCap) { cd[pos] = d2; cj[pos] = j; }
+    ncand += __popcll(bal);
+  }
+  wave_lds_sync();
+  const bool in_lds = ncand <= kCap;
   double ld = -1.0;   // last selected key (d2, j); d2 >= 0
   int lj = -1, taken = 0;
   for (int it = 0; it < k; ++it) {
     double bd = INFINITY;
     int bj = INT_MAX;
-    for (int j = lane; j < N; j += 64) {
-      if (j == i) continue;
-      const double* xj = x + (size_t)j * X;
-      const double dx = xi[0] - xj[0], dy = xi[1] - xj[1], dz = xi[2] - xj[2];
-      const double d2 = dx * dx + dy * dy + dz * dz;
-      if (!(d2 < r2)) continue;
-      if (d2 < ld || (d2 == ld && j <= lj)) continue;   // already taken
-      if (d2 < bd || (d2 == bd && j < bj)) { bd = d2; bj = j; }
+    if (in_lds) {
+      for (int q = lane; q < ncand; q += 64) {
+        const double d2 = cd[q];
+        const int j = cj[q];
+        if (d2 < ld || (d2 == ld && j <= lj)) continue;   // already taken
+        if (d2 < bd || (d2 == bd && j < bj)) { bd = d2; bj = j; }
+      }
+    } else {
+      for (int j = lane; j < N; j += 64) {
+        if (j == i) continue;
+        const double* xj = x + (size_t)j * X;
+        const double dx = xi[0] - xj[0], dy = xi[1] - xj[1], dz = xi[2] - xj[2];
+        const double d2 = dx * dx + dy * dy + dz * dz;
+        if (!(d2 < r2)) continue;
+        if (d2 < ld || (d2 == ld && j <= lj)) continue;
+        if (d2 < bd || (d2 == bd && j < bj)) { bd = d2; bj = j; }
+      }
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
@@ -718,6 +748,22 @@ __global__ void __launch_bounds__(64) k_nbr(const double* x, int X, int N, int r
   }
   int* row = list + (size_t)lrow * K;
   int cnt = 0;
+  if (in_lds) {   // candidates are in ascending j: keep those at or below the last key
+    for (int base = 0; base < ncand; base += 64) {
+      const int q = base + lane;
+      bool sel = false;
+      int jj = 0;
+      if (q < ncand && taken > 0) {
+        const double d2 = cd[q];
+        const int j = cj[q];
+        jj = j < i ? j : j - 1;
+        sel = d2 < ld || (d2 == ld && j <= lj);
+      }
+      const unsigned long long bal = __ballot(sel);
+      if (sel) row[cnt + __popcll(bal & ((1ull << lane) - 1ull))] = jj;
+      cnt += __popcll(bal);
+    }
+  } else
   for (int base = 0; base < npr; base += 64) {
     const int jj = base + lane;
     bool sel = false;

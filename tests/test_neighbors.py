@@ -76,3 +76,31 @@ def test_gpu_step_with_culling(lqro_mod, oracle, gains, k, r, box):
     ctx.set_neighbors(0.0, 0)
     ctx.step(x, vg)
     assert ctx.stats()["pairs"] == N * (N - 1)
+
+
+@pytest.mark.gpu
+def test_gpu_culling_many_candidates(lqro_mod, oracle, gains):
+    """More agents within the radius than k_nbr's LDS candidate list holds
+    (1,024): the selection falls back to scanning global memory per round."""
+    N, H, NP, k, r = 1100, 20, 50, 3, 1.0e4
+    x, vg = lqro_mod.synthetic_swarm(N, seed=19)
+    T, NCF = oracle.tables(gains["A"], gains["B"], gains["L"], gains["E"], H)
+    S = oracle.sphere(NP)
+    oracle.set_neighbors(r, k)
+    try:
+        rv, rrecs = oracle.step(T, NCF, S, x, vg, rows=(0, 24))
+    finally:
+        oracle.set_neighbors(0.0, 0)
+    ctx = lqro_mod.Context(lqro_mod.config(N, H, NP, flags=lqro_mod.LQRO_FLAG_RECORDS,
+                                           row_begin=0, row_end=24))
+    ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
+    ctx.set_neighbors(r, k)
+    newv = ctx.step(x, vg)
+    gr = ctx.records().reshape(24, k)
+    rr = rrecs.reshape(24, N - 1)
+    for i in range(24):
+        ref_row = rr[i][rr[i]["n_reach"] >= 0]
+        assert len(ref_row) == k
+        for f in ("j", "n_reach", "flags", "reach_hash"):
+            assert np.array_equal(gr[i][f], ref_row[f]), (i, f)
+    np.testing.assert_array_equal(newv[:24], rv[:24])
