@@ -183,7 +183,8 @@ int lqro_get_timings(lqro_ctx* ctx, float* ms4);
  * observation z = sampleGaussian(h(xTrue, RotTrue), N) (LQRO:1442);
  * kalmanFilter2 (LQRO:507-518); vGoal = findVGoal()
  * (riccatiControllerSteadyPosition, LQRO:619-645).  Quadrotor::visualize
- * (Callisto) is not part of it.  X = 16, U = 4, Z = 6.
+ * (LQRO:1444) becomes a keyframe record instead of Callisto calls
+ * (SURVEY §8f next #4).  X = 16, U = 4, Z = 6.
  * The reference draws its noise from rand() in agent order (normal(),
  * LQRO:334-350): the caller supplies the draws, LQRO_NORMALS_PER_AGENT per
  * agent (16 for propagate, then 6 for the observation); lqro_normals
@@ -208,6 +209,10 @@ typedef struct lqro_agents {
   const double* M;       /* X*X   motion noise variance (LQRO:1285)              */
   const double* N;       /* 6*6   observation noise variance (LQRO:1286)         */
   const double* normals; /* n*LQRO_NORMALS_PER_AGENT                             */
+  float* keyframes;      /* n*8 out, may be NULL: Quadrotor::visualize's keyframe */
+                         /*   (LQRO:128-133): time, (float) xTrue[0..2],          */
+                         /*   (float) quatFromRot(RotTrue) (stdafx.h:24-33)       */
+  double time;           /* t*dt, the keyframe time (LQRO:1444)                   */
 } lqro_agents;
 
 /* Host arrays; synchronous.  models: n_models = 1 (shared) or n. */

@@ -250,6 +250,29 @@ LQRO_HD Vec3 control_position(const Mat<kX, 1>& x, const Mat<3, 3>& R0, const Ve
   return RL * (Lh * xt + Eh * pt);
 }
 
+// std::max(a, 0.0)
+LQRO_HD double max0(double a) { return (a < 0.0) ? 0.0 : a; }
+
+// quatFromRot (stdafx.h:24-33)
+LQRO_HD Mat<4, 1> quat_from_rot(const Mat<3, 3>& R) {
+  Mat<4, 1> q;
+  q.e[0] = 0.5 * sqrt(max0(1 + R(0, 0) - R(1, 1) - R(2, 2))) * (R(2, 1) - R(1, 2) >= 0 ? 1 : -1);
+  q.e[1] = 0.5 * sqrt(max0(1 - R(0, 0) + R(1, 1) - R(2, 2))) * (R(0, 2) - R(2, 0) >= 0 ? 1 : -1);
+  q.e[2] = 0.5 * sqrt(max0(1 - R(0, 0) - R(1, 1) + R(2, 2))) * (R(1, 0) - R(0, 1) >= 0 ? 1 : -1);
+  q.e[3] = 0.5 * sqrt(max0(1 + R(0, 0) + R(1, 1) + R(2, 2)));
+  return q;
+}
+
+// Quadrotor::visualize's keyframe (LQRO:128-133): (float) time, position of
+// xTrue, quatFromRot(RotTrue), as handed to CAL_AddGroupKeyState
+LQRO_HD void keyframe(float* out, double time, const Mat<kX, 1>& xtrue, const Mat<3, 3>& Rtrue) {
+  if (!out) return;
+  const Mat<4, 1> q = quat_from_rot(Rtrue);
+  out[0] = (float)time;
+  for (int k = 0; k < 3; ++k) out[1 + k] = (float)xtrue.e[k];
+  for (int k = 0; k < 4; ++k) out[4 + k] = (float)q.e[k];
+}
+
 template <int R, int C>
 LQRO_HD Mat<R, C> get(const double* p) {
   Mat<R, C> m;
@@ -264,6 +287,8 @@ struct AgentParams {
   const double *u_goal, *p_goal;       // U, V
   const double *M, *Nz;                // X*X, Z*Z
   const double* normals;               // kNormals
+  float* keyframe;                     // 8 floats or null
+  double time;
 };
 
 // One agent through LQRO:1438-1445.  vgoal: in newV, out findVGoal(); u_out
@@ -290,6 +315,7 @@ LQRO_HD void agent_step(const AgentParams& a, double* x_, double* rot_, double* 
   synth::put(xt_, xtrue); synth::put(rott_, Rtrue);
   synth::put(P_, P); synth::put(vgoal_, vn);
   synth::put(u_out, u);
+  keyframe(a.keyframe, a.time, xtrue, Rtrue);                            // visualize
 }
 
 }  // namespace dyn

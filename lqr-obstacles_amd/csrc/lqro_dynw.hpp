@@ -489,6 +489,7 @@ __device__ void agent_step(const dyn::AgentParams& a, double* x_, double* rot_, 
     synth::put(xt_, xtrue); synth::put(rott_, Rtrue);
     synth::put(vgoal_, vn);
     synth::put(u_out, u);
+    dyn::keyframe(a.keyframe, a.time, xtrue, Rtrue);                                  // visualize
   }
 }
 

@@ -881,6 +881,8 @@ __global__ void __launch_bounds__(64) k_dyn(const lqro_model* models, int n_mode
   p.M = A.M;
   p.Nz = A.N;
   p.normals = A.normals + (size_t)a * dyn::kNormals;
+  p.keyframe = A.keyframes ? A.keyframes + (size_t)a * 8 : nullptr;
+  p.time = A.time;
   dyn::agent_step(p, A.x + (size_t)a * dyn::kX, A.rot + (size_t)a * 9, A.x_true + (size_t)a * dyn::kX,
                   A.rot_true + (size_t)a * 9, A.P + (size_t)a * dyn::kX * dyn::kX, A.vgoal + (size_t)a * 3,
                   A.u ? A.u + (size_t)a * dyn::kU : nullptr);
@@ -908,6 +910,8 @@ __global__ void __launch_bounds__(64) k_dynw(const lqro_model* models, int n_mod
   p.M = A.M;
   p.Nz = A.N;
   p.normals = A.normals + (size_t)a * dyn::kNormals;
+  p.keyframe = A.keyframes ? A.keyframes + (size_t)a * 8 : nullptr;
+  p.time = A.time;
   dynw::agent_step(p, A.x + (size_t)a * dyn::kX, A.rot + (size_t)a * 9, A.x_true + (size_t)a * dyn::kX,
                    A.rot_true + (size_t)a * 9, A.P + (size_t)a * dyn::kX * dyn::kX, A.vgoal + (size_t)a * 3,
                    A.u ? A.u + (size_t)a * dyn::kU : nullptr, w, lane);
@@ -952,8 +956,11 @@ int lqro_dynamics_step(const lqro_model* models, int32_t n_models, int32_t n, in
       {agents->Eh, nullptr, G * kV * kV, nullptr},        {agents->M, nullptr, (size_t)kX * kX, nullptr},
       {agents->N, nullptr, (size_t)kZ * kZ, nullptr},     {agents->normals, nullptr, N * kNormals, nullptr}};
   lqro_model* d_m = nullptr;
+  float* d_kf = nullptr;
   int rc = LQRO_OK;
   if (hipMalloc(&d_m, sizeof(lqro_model) * (size_t)n_models) != hipSuccess) rc = LQRO_E_NOMEM;
+  if (rc == LQRO_OK && agents->keyframes && hipMalloc(&d_kf, sizeof(float) * 8 * N) != hipSuccess)
+    rc = LQRO_E_NOMEM;
   for (auto& q : b)
     if (rc == LQRO_OK && q.cnt && hipMalloc(&q.d, sizeof(double) * q.cnt) != hipSuccess) rc = LQRO_E_NOMEM;
   if (rc == LQRO_OK &&
@@ -967,13 +974,18 @@ int lqro_dynamics_step(const lqro_model* models, int32_t n_models, int32_t n, in
     d.x = b[0].d; d.rot = b[1].d; d.x_true = b[2].d; d.rot_true = b[3].d; d.P = b[4].d; d.vgoal = b[5].d;
     d.u = b[6].d; d.u_goal = b[7].d; d.p_goal = b[8].d; d.L = b[9].d; d.E = b[10].d; d.l = b[11].d;
     d.Lh = b[12].d; d.Eh = b[13].d; d.M = b[14].d; d.N = b[15].d; d.normals = b[16].d;
+    d.keyframes = d_kf; d.time = agents->time;
     rc = lqro_dynamics_step_device(d_m, n_models, n, per_agent_gains, &d, nullptr);
     if (rc == LQRO_OK && hipDeviceSynchronize() != hipSuccess) rc = LQRO_E_HIP;
   }
   for (auto& q : b)
     if (rc == LQRO_OK && q.out && hipMemcpy(q.out, q.d, sizeof(double) * q.cnt, hipMemcpyDeviceToHost) != hipSuccess)
       rc = LQRO_E_HIP;
+  if (rc == LQRO_OK && d_kf &&
+      hipMemcpy(agents->keyframes, d_kf, sizeof(float) * 8 * N, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = LQRO_E_HIP;
   if (d_m) (void)hipFree(d_m);
+  if (d_kf) (void)hipFree(d_kf);
   for (auto& q : b)
     if (q.d) (void)hipFree(q.d);
   return rc;

@@ -83,7 +83,7 @@ class Agents(C.Structure):
     pair loop (LQRO:1437-1446)."""
     _fields_ = [(n, C.c_void_p) for n in (
         "x", "rot", "x_true", "rot_true", "P", "vgoal", "u", "u_goal", "p_goal",
-        "L", "E", "l", "Lh", "Eh", "M", "N", "normals")]
+        "L", "E", "l", "Lh", "Eh", "M", "N", "normals", "keyframes")] + [("time", C.c_double)]
 
 _lib = None
 
@@ -354,9 +354,12 @@ def agent_states(x, u_goal=None, p_goal=None, p0: float = 1e-9) -> dict:
 
 
 def dynamics_step(st: dict, gains: dict, nrm: np.ndarray, models=None, M=None, N=None,
-                  per_agent: bool = False, device: int = 0) -> np.ndarray:
+                  per_agent: bool = False, device: int = 0, keyframes: np.ndarray | None = None,
+                  time: float = 0.0) -> np.ndarray:
     """lqro_dynamics_step: advances every agent of `st` in place (x, rot,
     x_true, rot_true, P; vgoal in = newV, out = findVGoal()) and returns u.
+    keyframes: optional n x 8 float32 array that receives visualize's
+    keyframe (time, xTrue position, quatFromRot(RotTrue)) at `time`.
     gains: L, E, l, Lh, Eh (one set, or a leading agent axis with
     per_agent=True).  nrm: n x 22 draws.  M, N default to the reference's
     1e-9 I (LQRO:1285-1286)."""
@@ -376,6 +379,11 @@ def dynamics_step(st: dict, gains: dict, nrm: np.ndarray, models=None, M=None, N
     a = Agents(*[_p(st[k]).value for k in ("x", "rot", "x_true", "rot_true", "P", "vgoal")],
                _p(u).value, _p(st["u_goal"]).value, _p(st["p_goal"]).value,
                *[_p(v).value for v in keep])
+    if keyframes is not None:
+        if keyframes.shape != (n, 8) or keyframes.dtype != np.float32 or not keyframes.flags.c_contiguous:
+            raise LqroError("dynamics_step: keyframes must be C-contiguous float32 (n, 8)")
+        a.keyframes = _p(keyframes).value
+    a.time = float(time)
     _check(lib().lqro_dynamics_step(marr, len(models), n, int(per_agent), C.byref(a), device),
            "lqro_dynamics_step")
     return u
@@ -415,6 +423,8 @@ class Simulator:
         self.model = model or default_model()
         flags = LQRO_FLAG_RECORDS if records else 0
         self.device = device
+        self.t = 0                 # control steps taken (LQRO:1392)
+        self.trajectory = []       # keyframes per step (update())
         self.ctx = Context(config(len(self.qlist), horizon, n_points, device=device,
                                   flags=flags))
         self.A = self.B = self.c = None
@@ -442,6 +452,15 @@ class Simulator:
             q.newV = v.copy()
         return newv
 
+    def save_trajectory(self, path: str):
+        """The keyframes update() recorded (Quadrotor::visualize's Callisto
+        keys, LQRO:128-133): an .npz with `keyframes` (steps x agents x 8:
+        time, xTrue position, quaternion) for offline diffing/plotting."""
+        kf = np.stack(self.trajectory) if self.trajectory else np.zeros((0, len(self.qlist), 8),
+                                                                        np.float32)
+        np.savez_compressed(path, keyframes=kf, fields=np.array(
+            ["time", "px", "py", "pz", "qx", "qy", "qz", "qw"]))
+
     def update(self, seed: int) -> int:
         """The agent loop after the pair loop (LQRO:1437-1446) on the GPU:
         vGoal = newV, findU, propagateU, kalmanFilter1, the observation draw,
@@ -456,7 +475,11 @@ class Simulator:
                   P=np.stack([q.P for q in self.qlist]), vgoal=np.stack([q.newV for q in self.qlist]),
                   u_goal=np.full((n, 4), hover), p_goal=np.stack([q.pGoal for q in self.qlist]))
         gains = {k: np.stack([getattr(q, k) for q in self.qlist]) for k in ("L", "E", "l", "Lh", "Eh")}
-        dynamics_step(st, gains, nrm, models=[self.model], per_agent=True, device=self.device)
+        kf = np.zeros((n, 8), np.float32)
+        dynamics_step(st, gains, nrm, models=[self.model], per_agent=True, device=self.device,
+                      keyframes=kf, time=self.t * self.model.dt)
+        self.trajectory.append(kf)
+        self.t += 1
         for a, q in enumerate(self.qlist):
             q.x, q.Rot, q.xTrue, q.RotTrue, q.P = (st["x"][a].copy(), st["rot"][a].copy(),
                                                    st["x_true"][a].copy(), st["rot_true"][a].copy(),

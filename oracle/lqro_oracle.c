@@ -1491,3 +1491,21 @@ void orc_agent_step(const lqro_model* m, const double* L, const double* E, const
   orc_control_position(x, R, pGoal, uGoal, Lh, Eh, vgoal);  /* findVGoal */
   if (u_out) memcpy(u_out, u, sizeof u);
 }
+
+/* quatFromRot (stdafx.h:24-33) and Quadrotor::visualize's keyframe
+ * (LQRO:128-133): (float) t, (float) xTrue[0..2], (float) quat */
+void orc_quat_from_rot(const double* R, double* q) {
+  double a;
+  a = 1 + R[0] - R[4] - R[8]; q[0] = 0.5 * sqrt(a < 0.0 ? 0.0 : a) * (R[7] - R[5] >= 0 ? 1 : -1);
+  a = 1 - R[0] + R[4] - R[8]; q[1] = 0.5 * sqrt(a < 0.0 ? 0.0 : a) * (R[2] - R[6] >= 0 ? 1 : -1);
+  a = 1 - R[0] - R[4] + R[8]; q[2] = 0.5 * sqrt(a < 0.0 ? 0.0 : a) * (R[3] - R[1] >= 0 ? 1 : -1);
+  a = 1 + R[0] + R[4] + R[8]; q[3] = 0.5 * sqrt(a < 0.0 ? 0.0 : a);
+}
+
+void orc_keyframe(double t, const double* xTrue, const double* RTrue, float* out) {
+  double q[4];
+  orc_quat_from_rot(RTrue, q);
+  out[0] = (float)t;
+  for (int k = 0; k < 3; ++k) out[1 + k] = (float)xTrue[k];
+  for (int k = 0; k < 4; ++k) out[4 + k] = (float)q[k];
+}

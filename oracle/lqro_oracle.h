@@ -114,6 +114,11 @@ void orc_inverse4(const double* in, double* out);
 
 double orc_round6(double v);
 
+/* quatFromRot (stdafx.h:24-33); Quadrotor::visualize's keyframe (LQRO:128-133):
+ * out[8] = (float) t, (float) xTrue[0..2], (float) quatFromRot(RotTrue). */
+void orc_quat_from_rot(const double* R, double* q);
+void orc_keyframe(double t, const double* xTrue, const double* RTrue, float* out);
+
 /* ---- the per-agent step after the pair loop (LQRO:1437-1446) ----------- */
 /* jacobi (MAT:674-759) on an n x n symmetric matrix (n <= 16). */
 void orc_jacobi(int n, const double* m, double* V, double* D);

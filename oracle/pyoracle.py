@@ -52,6 +52,8 @@ def lib():
         _o.orc_agent_step.argtypes = [C.c_void_p] * 17
         _o.orc_jacobi.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         _o.orc_set_neighbors.argtypes = [C.c_double, C.c_int]
+        _o.orc_keyframe.argtypes = [C.c_double, C.c_void_p, C.c_void_p, C.c_void_p]
+        _o.orc_quat_from_rot.argtypes = [C.c_void_p, C.c_void_p]
         _o.orc_neighbors.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_double, C.c_int,
                                      C.c_void_p]
     return _o
@@ -231,3 +233,14 @@ def neighbors(x, i: int, nbr_dist: float, max_nbr: int) -> np.ndarray:
     sel = np.zeros(x.shape[0], np.uint8)
     lib().orc_neighbors(x.shape[0], x.shape[1], _p(x), i, nbr_dist * nbr_dist, max_nbr, _p(sel))
     return sel
+
+
+def keyframes(t: float, x_true, rot_true) -> np.ndarray:
+    """orc_keyframe per agent: n x 8 float32 (time, position, quaternion)."""
+    x_true = np.ascontiguousarray(x_true, np.float64)
+    rot_true = np.ascontiguousarray(rot_true, np.float64)
+    n = x_true.shape[0]
+    out = np.zeros((n, 8), np.float32)
+    for a in range(n):
+        lib().orc_keyframe(float(t), _p(x_true[a]), _p(rot_true[a]), _p(out[a]))
+    return out

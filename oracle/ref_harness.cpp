@@ -327,4 +327,10 @@ void ref_kalman2(double* x_, double* R_, const double* z_, double* P_) {
   store(x, x_); store(R0, R_); store(P, P_);
 }
 
+/* quatFromRot (stdafx.h:24-33), which Quadrotor::visualize keys Callisto with */
+void ref_quat_from_rot(const double* R_, double* q_) {
+  Rotation R; load(R, R_);
+  store(quatFromRot(R), q_);
+}
+
 } /* extern "C" */

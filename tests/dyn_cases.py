@@ -41,3 +41,18 @@ def trajectory_start(n: int, seed: int) -> dict:
     """States as they stand at a step boundary (rotation error reset to 0)."""
     cs = random_agent_cases(n, seed, rot_err=False)
     return cs
+
+
+def quat_cases() -> np.ndarray:
+    """Rotations for quatFromRot: random ones, the identity, half turns about
+    each axis and near-half turns (where 1 + trace terms reach 0 and the
+    std::max(., 0) clamp and the sign tests matter)."""
+    rng = np.random.default_rng(0x5154)
+    rs = [rotation(rng.normal(size=3) * rng.uniform(0, 3.1)) for _ in range(40)]
+    rs.append(np.eye(3))
+    for ax in np.eye(3):
+        rs.append(rotation(ax * np.pi))
+        rs.append(rotation(ax * (np.pi - 1e-9)))
+        rs.append(rotation(-ax * (np.pi - 1e-9)))
+    rs.append(rotation(np.array([1.0, 1.0, 0.0]) / np.sqrt(2) * np.pi))
+    return np.stack(rs)

@@ -10,6 +10,8 @@ inputs and the reference's outputs of the per-agent step after the pair loop:
                         riccatiControllerSteadyPosition (LQRO:619-645)
   k1_*                  kalmanFilter1 (LQRO:488-505)
   k2_*                  kalmanFilter2 (LQRO:507-518)
+  quat_*                quatFromRot (stdafx.h:24-33), Quadrotor::visualize's
+                        keyframe orientation (LQRO:128-133)
 
 propagate (LQRO:473-486) and the observation draw call sampleGaussian, whose
 jacobi needs MSVC's _hypot (not in this image): they have no fixture; the
@@ -30,7 +32,7 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path[:0] = [os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")]
 
 import pyoracle  # noqa: E402
-from dyn_cases import random_agent_cases  # noqa: E402
+from dyn_cases import quat_cases, random_agent_cases  # noqa: E402
 
 
 def _p(a):
@@ -57,7 +59,11 @@ def main():
                                _p(cs["u_goal"][a]), _p(g["Lh"]), _p(g["Eh"]), _p(v[a]))
         r.ref_kalman1(_p(k1["x"][a]), _p(k1["rot"][a]), _p(u[a]), _p(k1["P"][a]))
         r.ref_kalman2(_p(k2["x"][a]), _p(k2["rot"][a]), _p(cs["z"][a]), _p(k2["P"][a]))
-    out = dict(l=l, u=u, v=v, **{"in_" + k: val for k, val in cs.items()},
+    qin = quat_cases()
+    qout = np.zeros((qin.shape[0], 4))
+    for a in range(qin.shape[0]):
+        r.ref_quat_from_rot(_p(qin[a]), _p(qout[a]))
+    out = dict(l=l, u=u, v=v, quat_in=qin, quat_out=qout, **{"in_" + k: val for k, val in cs.items()},
                **{"k1_" + k: val for k, val in k1.items()},
                **{"k2_" + k: val for k, val in k2.items()})
     np.savez_compressed(os.path.join(HERE, "dyn.npz"), **out)

@@ -53,8 +53,12 @@ def test_one_step(lqro_mod, oracle):
     st = _states(lqro_mod, n, seed=21)
     ref = {k: v.copy() for k, v in st.items()}
     nrm, _ = lqro_mod.normals(7, n * lqro_mod.NORMALS_PER_AGENT)
-    u = lqro_mod.dynamics_step(st, g, nrm)
+    kf = np.zeros((n, 8), np.float32)
+    u = lqro_mod.dynamics_step(st, g, nrm, keyframes=kf, time=1.25)
     ur = oracle.agent_step(ref, g, nrm)
+    # visualize's keyframe from the step's own xTrue / RotTrue, bit for bit
+    assert np.array_equal(kf.view(np.uint32),
+                          oracle.keyframes(1.25, st["x_true"], st["rot_true"]).view(np.uint32))
     _close(u, ur, 1e-9, "u")
     _compare(st, ref, 1e-9)
     assert np.all(st["x"][:, 6:9] == 0)     # rotation error reset into Rot
@@ -188,7 +192,7 @@ def test_wave_kernel_matches_lane_kernel(lqro_mod, oracle, monkeypatch):
         assert np.array_equal(st[k].view(np.uint64), other[k].view(np.uint64)), k
 
 
-def test_simulator_loop(lqro_mod, oracle):
+def test_simulator_loop(lqro_mod, oracle, tmp_path):
     """The reference-shaped driver: Simulator.step (LQRO:1393-1436) then
     Simulator.update (LQRO:1437-1446), two control steps, against the oracle."""
     n, H, NP = 8, 25, 50
@@ -214,3 +218,8 @@ def test_simulator_loop(lqro_mod, oracle):
                P=np.stack([q.P for q in qs]), vgoal=np.stack([q.vGoal for q in qs]))
     _compare(got, ref, 1e-7)
     assert seed == seed_ref
+    sim.save_trajectory(str(tmp_path / "traj.npz"))
+    kf = np.load(tmp_path / "traj.npz")["keyframes"]
+    assert kf.shape == (2, n, 8)
+    np.testing.assert_array_equal(kf[1, :, 0], np.float32(1 * sim.model.dt))
+    np.testing.assert_allclose(kf[1, :, 1:4], got["x_true"][:, :3], rtol=1e-6)

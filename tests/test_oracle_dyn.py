@@ -155,3 +155,24 @@ def test_msvc_normals_known_answer(lqro_mod):
     assert abs(draws.mean()) < 0.03 and abs(draws.std() - 1) < 0.03
     d2, _ = lqro_mod.normals(1, 20000)
     assert np.array_equal(draws, d2) and nxt != 1
+
+
+def test_quat_from_rot(oracle, gold):
+    """quatFromRot (stdafx.h:24-33), the orientation of visualize's keyframe:
+    against the golden fixture and, where available, the live reference."""
+    o = oracle.lib()
+    qin = gold["quat_in"]
+    got = np.zeros((qin.shape[0], 4))
+    for a in range(qin.shape[0]):
+        o.orc_quat_from_rot(_p(np.ascontiguousarray(qin[a])), _p(got[a]))
+    _same(got, gold["quat_out"])
+    r = oracle.reflib()
+    if r is not None:
+        rng = np.random.default_rng(5)
+        from dyn_cases import rotation
+        for _ in range(50):
+            R = rotation(rng.normal(size=3) * rng.uniform(0, 3.14))
+            q1, q2 = np.zeros(4), np.zeros(4)
+            o.orc_quat_from_rot(_p(R), _p(q1))
+            r.ref_quat_from_rot(_p(R), _p(q2))
+            _same(q1, q2)
