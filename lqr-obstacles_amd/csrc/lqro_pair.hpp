@@ -344,7 +344,7 @@ __device__ inline int reach_rank(const PairArgs& P, const WaveTabs& W, int lane,
 
 // One workgroup's share of a k_pair launch (LDS at `lds`, laid out per
 // PairArgs; waves = blockDim.x / 64 <= P.waves).  Also the tail of k_side.
-template <int X>
+template <int X, bool RECS>
 __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
 #ifdef LQRO_PAIR_PROFILE
   unsigned long long pp[16] = {0};
@@ -396,7 +396,7 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
         float4* dst = reinterpret_cast<float4*>(P.planes + cs * 8);
         dst[0] = make_float4(0.f, 0.f, 0.f, 0.f);
         dst[1] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (P.recs != nullptr) {
+        if (RECS) {
           lqro_pair_record rec;
           memset(&rec, 0, sizeof rec);
           rec.i = i; rec.j = -1; rec.n_reach = -1;
@@ -412,7 +412,7 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
     for (int c = 0; c < X; ++c) d[c] = xi[c] - xj[c];                       // (xInit1-xInit2)
     const double vrel[3] = {xi[3] - xj[3], xi[4] - xj[4], xi[5] - xj[5]};    // :794-796
     unsigned long long hsh = 0;
-    const bool want_hash = P.recs != nullptr;
+    constexpr bool want_hash = RECS;
     const double vabs = fabs(vrel[0]) + fabs(vrel[1]) + fabs(vrel[2]);
     PSTAMP(7);
 
@@ -551,7 +551,7 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
     PSTAMP(4);
     const size_t slot = (size_t)lrow * P.npr + jj;
     int sranks[4] = {-1, -1, -1, -1};
-    if (P.recs != nullptr && npts > 0)
+    if (RECS && npts > 0)
       for (int s = 0; s < 4; ++s)
         if (s < npts) sranks[s] = reach_rank(P, W, lane, W.gjk.s2[s]);
     if (lane == 0) {
@@ -564,7 +564,7 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
         if (qi < P.hull_cap)
           __hip_atomic_store(P.hull_queue + qi, (int)slot, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (P.recs != nullptr) {
+      if (RECS) {
         lqro_pair_record rec;
         rec.i = i; rec.j = j; rec.n_reach = n; rec.flags = flags;
         rec.gjk_iters = go.iters; rec.simplex_n = npts;
@@ -676,10 +676,12 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
   }
 }
 
-template <int X>
+// RECS: per-pair records on (LQRO_FLAG_RECORDS); the bench path compiles
+// without the record code and its registers
+template <int X, bool RECS>
 __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
   extern __shared__ double lds[];
-  pair_block<X>(P, lds);
+  pair_block<X, RECS>(P, lds);
 }
 
 // k_nbr: opt-in neighbour culling (RVO2 computeNeighbors /

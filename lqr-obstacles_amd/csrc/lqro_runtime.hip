@@ -45,13 +45,35 @@ using namespace lqro;
 // LDS as k_hull), which turn into k_pair row workers once the hull queue is
 // drained, so the side CUs never idle while the sweep goes on.  The pair
 // tables and per-wave regions reuse the hull's LDS (host checks the fit).
-template <int X>
+template <int X, bool RECS>
 __global__ void __launch_bounds__(HULL_CTHREADS) k_side(HullArgs A, PairArgs P) {
   __shared__ HullLdsC<HULL_CWAVES> L;
   __shared__ HullMemC M;
   hull_body_mw<HULL_CWAVES>(A, M, L);
   __syncthreads();
-  if (P.nrows > 0) pair_block<X>(P, reinterpret_cast<double*>(&M));
+  if (P.nrows > 0) pair_block<X, RECS>(P, reinterpret_cast<double*>(&M));
+}
+
+// k_pair / k_side for the context's state width and record mode
+static void launch_pair(int x_dim, dim3 grid, dim3 block, size_t lds, hipStream_t s, const PairArgs& P) {
+  const bool r = P.recs != nullptr;
+  if (x_dim == 16) {
+    if (r) hipLaunchKernelGGL((k_pair<16, true>), grid, block, lds, s, P);
+    else hipLaunchKernelGGL((k_pair<16, false>), grid, block, lds, s, P);
+  } else {
+    if (r) hipLaunchKernelGGL((k_pair<12, true>), grid, block, lds, s, P);
+    else hipLaunchKernelGGL((k_pair<12, false>), grid, block, lds, s, P);
+  }
+}
+static void launch_side(int x_dim, dim3 grid, dim3 block, hipStream_t s, const HullArgs& H, const PairArgs& P) {
+  const bool r = P.recs != nullptr;
+  if (x_dim == 16) {
+    if (r) hipLaunchKernelGGL((k_side<16, true>), grid, block, 0, s, H, P);
+    else hipLaunchKernelGGL((k_side<16, false>), grid, block, 0, s, H, P);
+  } else {
+    if (r) hipLaunchKernelGGL((k_side<12, true>), grid, block, 0, s, H, P);
+    else hipLaunchKernelGGL((k_side<12, false>), grid, block, 0, s, H, P);
+  }
 }
 
 #define LQRO_MAXX 16
@@ -583,10 +605,12 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
     lqro_destroy(c);
     return LQRO_E_HIP;
   }
-  if (hipFuncSetAttribute((const void*)k_pair<16>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          c->lds_bytes) != hipSuccess ||
-      hipFuncSetAttribute((const void*)k_pair<12>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          c->lds_bytes) != hipSuccess) {
+  const void* pair_kernels[4] = {(const void*)k_pair<16, false>, (const void*)k_pair<16, true>,
+                                 (const void*)k_pair<12, false>, (const void*)k_pair<12, true>};
+  bool attr_ok = true;
+  for (const void* k : pair_kernels)
+    attr_ok = attr_ok && hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, c->lds_bytes) == hipSuccess;
+  if (!attr_ok) {
     lqro_destroy(c);
     return LQRO_E_HIP;
   }
@@ -729,26 +753,16 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
     HIPCHK(hipStreamWaitEvent(c->side, c->xev[0], 0));
     PairArgs Ph = P;
     Ph.hot_only = 1;
-    if (g.x_dim == 16)
-      hipLaunchKernelGGL(k_pair<16>, dim3(nwait), dim3(P.waves * 64), c->lds_bytes, c->side, Ph);
-    else
-      hipLaunchKernelGGL(k_pair<12>, dim3(nwait), dim3(P.waves * 64), c->lds_bytes, c->side, Ph);
+    launch_pair(g.x_dim, dim3(nwait), dim3(P.waves * 64), c->lds_bytes, c->side, Ph);
     HIPCHK(hipGetLastError());
     PairArgs Pt = P;
     if (nside == 0) Pt.nrows = 0;
-    if (g.x_dim == 16)
-      hipLaunchKernelGGL(k_side<16>, dim3(nwait), dim3(HULL_CTHREADS), 0, c->side, Hh, Pt);
-    else
-      hipLaunchKernelGGL(k_side<12>, dim3(nwait), dim3(HULL_CTHREADS), 0, c->side, Hh, Pt);
+    launch_side(g.x_dim, dim3(nwait), dim3(HULL_CTHREADS), c->side, Hh, Pt);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->xev[1], c->side));
   }
-  if (g.x_dim == 16)
-    hipLaunchKernelGGL(k_pair<16>, dim3(nblk), dim3(P.waves * 64), c->lds_bytes, s, P);
-  else if (g.x_dim == 12)
-    hipLaunchKernelGGL(k_pair<12>, dim3(nblk), dim3(P.waves * 64), c->lds_bytes, s, P);
-  else
-    return LQRO_E_ARG;
+  if (g.x_dim != 16 && g.x_dim != 12) return LQRO_E_ARG;
+  launch_pair(g.x_dim, dim3(nblk), dim3(P.waves * 64), c->lds_bytes, s, P);
   HIPCHK(hipGetLastError());
   if (nwait > 0) HIPCHK(hipStreamWaitEvent(s, c->xev[1], 0));
   HIPCHK(hipEventRecord(c->ev[1], s));
