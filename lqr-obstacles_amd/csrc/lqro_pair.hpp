@@ -344,7 +344,7 @@ __device__ inline int reach_rank(const PairArgs& P, const WaveTabs& W, int lane,
 
 // One workgroup's share of a k_pair launch (LDS at `lds`, laid out per
 // PairArgs; waves = blockDim.x / 64 <= P.waves).  Also the tail of k_side.
-template <int X, bool RECS>
+template <int X, bool RECS, bool HOT>
 __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
 #ifdef LQRO_PAIR_PROFILE
   unsigned long long pp[16] = {0};
@@ -594,7 +594,7 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
   // inside-hull, one per wave, so that their hulls can run on side-stream
   // k_hull workers while the row launch sweeps the rest.  Scheduling only:
   // every pair is computed by the same code.
-  if (P.hot_only) {
+  if constexpr (HOT) {
     for (int q = threadIdx.x; q < H * 9; q += blockDim.x) sT[q] = P.T[q];
     for (int q = threadIdx.x; q < H * 3 * X; q += blockDim.x) sN[(q / X) * XP + (q % X)] = P.NCF[q];
     for (int q = threadIdx.x; q < NP * 3; q += blockDim.x) sS[(q % 3) * NP + q / 3] = P.S[q];
@@ -677,11 +677,13 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
 }
 
 // RECS: per-pair records on (LQRO_FLAG_RECORDS); the bench path compiles
-// without the record code and its registers
-template <int X, bool RECS>
+// without the record code and its registers.  HOT: the hot launch (P.hot_only)
+// and the row launch are separate instantiations, so neither carries the
+// other's loop around do_pair.
+template <int X, bool RECS, bool HOT>
 __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
   extern __shared__ double lds[];
-  pair_block<X, RECS>(P, lds);
+  pair_block<X, RECS, HOT>(P, lds);
 }
 
 // k_nbr: opt-in neighbour culling (RVO2 computeNeighbors /

@@ -51,19 +51,21 @@ __global__ void __launch_bounds__(HULL_CTHREADS) k_side(HullArgs A, PairArgs P) 
   __shared__ HullMemC M;
   hull_body_mw<HULL_CWAVES>(A, M, L);
   __syncthreads();
-  if (P.nrows > 0) pair_block<X, RECS>(P, reinterpret_cast<double*>(&M));
+  if (P.nrows > 0) pair_block<X, RECS, false>(P, reinterpret_cast<double*>(&M));
 }
 
 // k_pair / k_side for the context's state width and record mode
+template <int X>
+static void launch_pair_x(dim3 grid, dim3 block, size_t lds, hipStream_t s, const PairArgs& P) {
+  const bool r = P.recs != nullptr, h = P.hot_only != 0;
+  if (r && h) hipLaunchKernelGGL((k_pair<X, true, true>), grid, block, lds, s, P);
+  else if (r) hipLaunchKernelGGL((k_pair<X, true, false>), grid, block, lds, s, P);
+  else if (h) hipLaunchKernelGGL((k_pair<X, false, true>), grid, block, lds, s, P);
+  else hipLaunchKernelGGL((k_pair<X, false, false>), grid, block, lds, s, P);
+}
 static void launch_pair(int x_dim, dim3 grid, dim3 block, size_t lds, hipStream_t s, const PairArgs& P) {
-  const bool r = P.recs != nullptr;
-  if (x_dim == 16) {
-    if (r) hipLaunchKernelGGL((k_pair<16, true>), grid, block, lds, s, P);
-    else hipLaunchKernelGGL((k_pair<16, false>), grid, block, lds, s, P);
-  } else {
-    if (r) hipLaunchKernelGGL((k_pair<12, true>), grid, block, lds, s, P);
-    else hipLaunchKernelGGL((k_pair<12, false>), grid, block, lds, s, P);
-  }
+  if (x_dim == 16) launch_pair_x<16>(grid, block, lds, s, P);
+  else launch_pair_x<12>(grid, block, lds, s, P);
 }
 static void launch_side(int x_dim, dim3 grid, dim3 block, hipStream_t s, const HullArgs& H, const PairArgs& P) {
   const bool r = P.recs != nullptr;
@@ -605,8 +607,11 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
     lqro_destroy(c);
     return LQRO_E_HIP;
   }
-  const void* pair_kernels[4] = {(const void*)k_pair<16, false>, (const void*)k_pair<16, true>,
-                                 (const void*)k_pair<12, false>, (const void*)k_pair<12, true>};
+  const void* pair_kernels[8] = {
+      (const void*)k_pair<16, false, false>, (const void*)k_pair<16, true, false>,
+      (const void*)k_pair<12, false, false>, (const void*)k_pair<12, true, false>,
+      (const void*)k_pair<16, false, true>,  (const void*)k_pair<16, true, true>,
+      (const void*)k_pair<12, false, true>,  (const void*)k_pair<12, true, true>};
   bool attr_ok = true;
   for (const void* k : pair_kernels)
     attr_ok = attr_ok && hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, c->lds_bytes) == hipSuccess;
