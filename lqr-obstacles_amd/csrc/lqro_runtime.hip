@@ -753,8 +753,15 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   Hh.prof = c->d_prof;
   Hh.block_base = 0;
   Hh.big_main = 0;
+  if (g.x_dim != 16 && g.x_dim != 12) return LQRO_E_ARG;
+  // the row launch is submitted before the side stream's work: should the two
+  // streams land on one hardware queue (a second context in the process), the
+  // main grid still runs first on its CUs instead of k_side's row tail
+  // sweeping every row on the side CUs alone
+  if (nwait > 0) HIPCHK(hipEventRecord(c->xev[0], s));
+  launch_pair(g.x_dim, dim3(nblk), dim3(P.waves * 64), c->lds_bytes, s, P);
+  HIPCHK(hipGetLastError());
   if (nwait > 0) {
-    HIPCHK(hipEventRecord(c->xev[0], s));
     HIPCHK(hipStreamWaitEvent(c->side, c->xev[0], 0));
     PairArgs Ph = P;
     Ph.hot_only = 1;
@@ -765,11 +772,8 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
     launch_side(g.x_dim, dim3(nwait), dim3(HULL_CTHREADS), c->side, Hh, Pt);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->xev[1], c->side));
+    HIPCHK(hipStreamWaitEvent(s, c->xev[1], 0));
   }
-  if (g.x_dim != 16 && g.x_dim != 12) return LQRO_E_ARG;
-  launch_pair(g.x_dim, dim3(nblk), dim3(P.waves * 64), c->lds_bytes, s, P);
-  HIPCHK(hipGetLastError());
-  if (nwait > 0) HIPCHK(hipStreamWaitEvent(s, c->xev[1], 0));
   HIPCHK(hipEventRecord(c->ev[1], s));
   Hh.block_base = nwait;
   Hh.big_main = lds_ok ? 0 : 1;
