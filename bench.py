@@ -103,6 +103,80 @@ def cpu_baseline(x, vg, gains, seconds_target=15.0):
             "kind": "port", "sample": sample}
 
 
+def closed_loop(lqro, torch, dev, stream, ctx, d_x, d_vg, gains, rb, rows, reps, world=1, dist=None, rank=0):
+    """The whole control step on the GPU, measured after the timed steps: the
+    pair step, then the agent loop LQRO:1437-1446 (k_dynw: findU, propagate,
+    kalmanFilter1/2, findVGoal) on this rank's rows, device-resident (x and
+    vGoal never leave HBM).  Reported beside the headline, not in `value`.
+    Runs on copies of the swarm, so the roofline probe after it sees the same
+    inputs as the timed steps (the loop moves the agents)."""
+    import ctypes as C
+    f64 = dict(dtype=torch.float64, device=dev)
+    n = rows
+    d_x = d_x.clone()
+    d_vg = d_vg.clone()
+    d_newv = torch.zeros_like(d_vg)
+
+    def step():
+        ctx.step_device(d_x.data_ptr(), d_vg.data_ptr(), d_newv.data_ptr(), stream.cuda_stream)
+        if world > 1:
+            lqro.allgather_rows(dist, d_newv, rank, world)
+    eye3 = torch.eye(3, **f64).repeat(n, 1, 1).contiguous()
+    hover = lqro.default_model().gravity * lqro.default_model().mass / 4
+    xs = d_x[rb:rb + n]
+    st = dict(rot=eye3.clone(), x_true=xs.clone(), rot_true=eye3.clone(),
+              P=(1e-9 * torch.eye(16, **f64)).repeat(n, 1, 1).contiguous(),
+              u_goal=torch.full((n, 4), hover, **f64), p_goal=torch.zeros((n, 3), **f64))
+    g = {k: torch.from_numpy(gains[k]).to(dev) for k in ("L", "E", "Lh", "Eh")}
+    g["l"] = torch.zeros(4, **f64)
+    M = 1e-9 * torch.eye(16, **f64)
+    Nz = 1e-9 * torch.eye(6, **f64)
+    nrm = torch.from_numpy(lqro.normals(1, n * lqro.NORMALS_PER_AGENT)[0]).to(dev)
+    mb = torch.frombuffer(bytearray(bytes(lqro.default_model())), dtype=torch.uint8).to(dev)
+    a = lqro.Agents(xs.data_ptr(), st["rot"].data_ptr(), st["x_true"].data_ptr(),
+                    st["rot_true"].data_ptr(), st["P"].data_ptr(), d_newv[rb:rb + n].data_ptr(), None,
+                    st["u_goal"].data_ptr(), st["p_goal"].data_ptr(), g["L"].data_ptr(),
+                    g["E"].data_ptr(), g["l"].data_ptr(), g["Lh"].data_ptr(), g["Eh"].data_ptr(),
+                    M.data_ptr(), Nz.data_ptr(), nrm.data_ptr())
+    L = lqro.lib()
+
+    def dyn():
+        rc = L.lqro_dynamics_step_device(C.c_void_p(mb.data_ptr()), 1, n, 0, C.byref(a),
+                                         C.c_void_p(stream.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"lqro_dynamics_step_device: {rc}")
+
+    dyn()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    dms = []
+    for _ in range(reps):
+        e0.record(stream)
+        dyn()
+        e1.record(stream)
+        e1.synchronize()
+        dms.append(e0.elapsed_time(e1))
+    torch.cuda.synchronize(dev)
+    it_ms, its = [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        step()     # the pair step on the current estimates
+        tm = ctx.timings()
+        its.append({"pair_ms": round(tm["pair_ms"], 3), "hull_ms": round(tm["hull_ms"], 3),
+                    "lp_ms": round(tm["lp_ms"], 3), "inside": ctx.stats()["inside"]})
+        dyn()      # newV -> vGoal, estimates advanced in place
+        with torch.cuda.stream(stream):
+            d_vg.copy_(d_newv)   # this vGoal feeds the next pair step
+            if world > 1:        # every rank advanced its own rows of x
+                lqro.allgather_rows(dist, d_x, rank, world)
+        torch.cuda.synchronize(dev)
+        it_ms.append((time.perf_counter() - t0) * 1e3)
+    return {"kernel": "k_dynw", "agents": n, "dynamics_ms": float(np.mean(dms)),
+            "pair_step_plus_dynamics_ms": float(np.mean(it_ms)),
+            "iteration_ms": [round(t, 3) for t in it_ms], "iterations": its,
+            "note": "closed loop LQRO:1391-1446 on device buffers; dynamics_ms from HIP events"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -190,6 +264,10 @@ def main():
     # on the main stream), so its own duration is measured right after, on
     # this rank's same rows, with the overlap off (LQRO_HOT=0: one k_pair
     # launch over all pairs, HIP events on its launch stream).
+    # the closed loop runs before the probe creates a second context (whose
+    # stream can share a hardware queue with this context's side stream)
+    closed = closed_loop(lqro, torch, dev, stream, ctx, d_x, d_vg, gains, rb, rows,
+                         min(args.steps, 5), world, dist, rank)
     pk_ms = sweep_ms
     probe = "sweep (k_prio + k_pair launches + overlapped side hull), timed steps"
     if not args.no_roofline_probe:
@@ -252,6 +330,7 @@ def main():
         },
         "step_device_ms": float(np.mean(step_dev_ms)),
         "sweep_ms": sweep_ms,
+        "closed_loop": closed,
         "inside_hull_pairs_per_step": st["inside"],
         "hull_failures": st["hull_fail"],
     }
