@@ -146,6 +146,10 @@ def closed_loop(lqro, torch, dev, stream, ctx, d_x, d_vg, gains, rb, rows, reps,
         if rc != 0:
             raise RuntimeError(f"lqro_dynamics_step_device: {rc}")
 
+    # the dynamics-only timing below moves the agents: it runs from a snapshot
+    # that is restored before the loop, so the loop starts at the bench's swarm
+    live = [d_x, d_newv] + list(st.values())
+    snap = [t.clone() for t in live]
     dyn()
     torch.cuda.synchronize(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -156,6 +160,8 @@ def closed_loop(lqro, torch, dev, stream, ctx, d_x, d_vg, gains, rb, rows, reps,
         e1.record(stream)
         e1.synchronize()
         dms.append(e0.elapsed_time(e1))
+    for t, c in zip(live, snap):
+        t.copy_(c)
     torch.cuda.synchronize(dev)
     it_ms, its = [], []
     for _ in range(reps):
