@@ -1,6 +1,8 @@
 #!/bin/sh
-# Build-time extraction of the reference's own per-pair path functions into
-# oracle/_ref/ (git-ignored, never committed).  Used only to compile the
+# Build-time extraction of the reference's own per-pair path functions into a
+# scratch directory OUTSIDE the repository (default /tmp/lqro_ref_extract, see
+# Makefile), so that no reference source sits in the tree that is pushed to
+# the GPU box.  Used only to compile the
 # reference itself as an oracle (oracle/_ref/libref.so, see Makefile).
 #
 # The reference's translation unit (LQRObstacles.cpp) cannot be compiled as a
