@@ -56,21 +56,30 @@ def algorithmic_bytes_per_pair(X=X_DIM) -> int:
     return 2 * X * 8 + 32
 
 
+def lib_sha256() -> str:
+    import hashlib
+    with open(os.path.join(ROOT, "lqr-obstacles_amd", "liblqro.so"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
 def pmc_traffic(kernel: str = "k_pair"):
     """HBM bytes per launch of `kernel` from the committed PMC passes
     (profiles/*_pmc_traffic.json, written by scripts/pmc_traffic.py from
     separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this bench at
-    N=1, FETCH_SIZE doubled per the gfx950 correction).  None if absent."""
+    N=1, FETCH_SIZE doubled per the gfx950 correction).  Only a file whose
+    build stamp is the liblqro.so this bench runs is cited; None otherwise."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
-    if not files:
-        return None
-    with open(files[-1]) as f:
-        d = json.load(f)
-    k = d.get("kernels", {}).get(kernel)
-    if not k or d.get("n_agents") != N_AGENTS or d.get("horizon") != HORIZON:
-        return None
-    return k["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+    sha = lib_sha256()
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), reverse=True):
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("build", {}).get("lib_sha256") != sha:
+            continue
+        k = d.get("kernels", {}).get(kernel)
+        if not k or d.get("n_agents") != N_AGENTS or d.get("horizon") != HORIZON:
+            continue
+        return k["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None
 
 
 def cpu_baseline(x, vg, gains, seconds_target=15.0):
@@ -103,84 +112,39 @@ def cpu_baseline(x, vg, gains, seconds_target=15.0):
             "kind": "port", "sample": sample}
 
 
-def closed_loop(lqro, torch, dev, stream, ctx, d_x, d_vg, gains, rb, rows, reps, world=1, dist=None, rank=0):
-    """The whole control step on the GPU, measured after the timed steps: the
-    pair step, then the agent loop LQRO:1437-1446 (k_dynw: findU, propagate,
-    kalmanFilter1/2, findVGoal) on this rank's rows, device-resident (x and
-    vGoal never leave HBM).  Reported beside the headline, not in `value`.
-    Runs on copies of the swarm, so the roofline probe after it sees the same
-    inputs as the timed steps (the loop moves the agents)."""
-    import ctypes as C
-    f64 = dict(dtype=torch.float64, device=dev)
-    n = rows
-    d_x = d_x.clone()
-    d_vg = d_vg.clone()
-    d_newv = torch.zeros_like(d_vg)
-
-    def step():
-        ctx.step_device(d_x.data_ptr(), d_vg.data_ptr(), d_newv.data_ptr(), stream.cuda_stream)
-        if world > 1:
-            lqro.allgather_rows(dist, d_newv, rank, world)
-    eye3 = torch.eye(3, **f64).repeat(n, 1, 1).contiguous()
-    hover = lqro.default_model().gravity * lqro.default_model().mass / 4
-    xs = d_x[rb:rb + n]
-    st = dict(rot=eye3.clone(), x_true=xs.clone(), rot_true=eye3.clone(),
-              P=(1e-9 * torch.eye(16, **f64)).repeat(n, 1, 1).contiguous(),
-              u_goal=torch.full((n, 4), hover, **f64), p_goal=torch.zeros((n, 3), **f64))
-    g = {k: torch.from_numpy(gains[k]).to(dev) for k in ("L", "E", "Lh", "Eh")}
-    g["l"] = torch.zeros(4, **f64)
-    M = 1e-9 * torch.eye(16, **f64)
-    Nz = 1e-9 * torch.eye(6, **f64)
-    nrm = torch.from_numpy(lqro.normals(1, n * lqro.NORMALS_PER_AGENT)[0]).to(dev)
-    mb = torch.frombuffer(bytearray(bytes(lqro.default_model())), dtype=torch.uint8).to(dev)
-    a = lqro.Agents(xs.data_ptr(), st["rot"].data_ptr(), st["x_true"].data_ptr(),
-                    st["rot_true"].data_ptr(), st["P"].data_ptr(), d_newv[rb:rb + n].data_ptr(), None,
-                    st["u_goal"].data_ptr(), st["p_goal"].data_ptr(), g["L"].data_ptr(),
-                    g["E"].data_ptr(), g["l"].data_ptr(), g["Lh"].data_ptr(), g["Eh"].data_ptr(),
-                    M.data_ptr(), Nz.data_ptr(), nrm.data_ptr())
-    L = lqro.lib()
-
-    def dyn():
-        rc = L.lqro_dynamics_step_device(C.c_void_p(mb.data_ptr()), 1, n, 0, C.byref(a),
-                                         C.c_void_p(stream.cuda_stream))
-        if rc != 0:
-            raise RuntimeError(f"lqro_dynamics_step_device: {rc}")
-
-    # the dynamics-only timing below moves the agents: it runs from a snapshot
-    # that is restored before the loop, so the loop starts at the bench's swarm
-    live = [d_x, d_newv] + list(st.values())
-    snap = [t.clone() for t in live]
-    dyn()
-    torch.cuda.synchronize(dev)
+def closed_loop(lqro, torch, dev, x, vg, gains, reps, world=1, dist=None, rank=0):
+    """The whole control step on the GPU, measured after the timed steps:
+    lqro.DeviceLoop — the pair step, then the agent loop LQRO:1437-1446
+    (k_dynw: findU, propagate, kalmanFilter1/2, findVGoal) on this rank's
+    rows, then the one all-gather of x (N > 1), all on torch's current stream
+    with no synchronisation between the calls (x and vGoal never leave HBM).
+    Reported beside the headline, not in `value`.  Its own context and
+    buffers start from the bench's swarm, so the roofline probe after it sees
+    the timed steps' inputs."""
+    loop = lqro.DeviceLoop(x, vg, dict(gains, l=np.zeros(4)), HORIZON, N_POINTS,
+                           rank=rank, world=world, dist=dist, device=dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    dms = []
+    it_ms, its, dms = [], [], []
     for _ in range(reps):
-        e0.record(stream)
-        dyn()
-        e1.record(stream)
-        e1.synchronize()
-        dms.append(e0.elapsed_time(e1))
-    for t, c in zip(live, snap):
-        t.copy_(c)
-    torch.cuda.synchronize(dev)
-    it_ms, its = [], []
-    for _ in range(reps):
+        torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        step()     # the pair step on the current estimates
-        tm = ctx.timings()
-        its.append({"pair_ms": round(tm["pair_ms"], 3), "hull_ms": round(tm["hull_ms"], 3),
-                    "lp_ms": round(tm["lp_ms"], 3), "inside": ctx.stats()["inside"]})
-        dyn()      # newV -> vGoal, estimates advanced in place
-        with torch.cuda.stream(stream):
-            d_vg.copy_(d_newv)   # this vGoal feeds the next pair step
-            if world > 1:        # every rank advanced its own rows of x
-                lqro.allgather_rows(dist, d_x, rank, world)
+        loop.step()
+        tm = loop.ctx.timings()
+        e0.record(loop.stream)
+        loop.update()
+        e1.record(loop.stream)
         torch.cuda.synchronize(dev)
         it_ms.append((time.perf_counter() - t0) * 1e3)
-    return {"kernel": "k_dynw", "agents": n, "dynamics_ms": float(np.mean(dms)),
+        dms.append(e0.elapsed_time(e1))
+        its.append({"pair_ms": round(tm["pair_ms"], 3), "hull_ms": round(tm["hull_ms"], 3),
+                    "lp_ms": round(tm["lp_ms"], 3), "inside": loop.ctx.stats()["inside"]})
+    loop.close()
+    return {"kernel": "k_dynw", "agents": loop.re - loop.rb,
+            "dynamics_plus_gather_ms": float(np.mean(dms)),
             "pair_step_plus_dynamics_ms": float(np.mean(it_ms)),
             "iteration_ms": [round(t, 3) for t in it_ms], "iterations": its,
-            "note": "closed loop LQRO:1391-1446 on device buffers; dynamics_ms from HIP events"}
+            "note": "closed loop LQRO:1391-1446 on device buffers (lqro.DeviceLoop); "
+                    "dynamics_plus_gather_ms from events on the launch stream"}
 
 
 def main():
@@ -272,8 +236,8 @@ def main():
     # launch over all pairs, HIP events on its launch stream).
     # the closed loop runs before the probe creates a second context (whose
     # stream can share a hardware queue with this context's side stream)
-    closed = closed_loop(lqro, torch, dev, stream, ctx, d_x, d_vg, gains, rb, rows,
-                         min(args.steps, 5), world, dist, rank)
+    ctx.close()   # one context at a time: a second one's streams can share hardware queues
+    closed = closed_loop(lqro, torch, dev, x, vg, gains, min(args.steps, 5), world, dist, rank)
     pk_ms = sweep_ms
     probe = "sweep (k_prio + k_pair launches + overlapped side hull), timed steps"
     if not args.no_roofline_probe:
@@ -346,7 +310,6 @@ def main():
         out["gpu_over_cpu"] = value / cb["value"]
     if rank == 0:
         print(json.dumps(out), flush=True)
-    ctx.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -152,8 +152,12 @@ int lqro_set_neighbors(lqro_ctx* ctx, double neighbor_dist, int32_t max_neighbor
 int lqro_step(lqro_ctx* ctx, const double* x, const double* vgoal, double* newv);
 
 /* Same, device-resident: d_x, d_vgoal, d_newv are device pointers on the
- * context's device; the work is enqueued on `stream` (hipStream_t, NULL =
- * the context's own stream) and the call returns without synchronising. */
+ * context's device; the work is enqueued on `stream` (hipStream_t; NULL = the
+ * default null stream, as in lqro_dynamics_step_device) behind whatever the
+ * caller queued there before, and the call returns without synchronising.
+ * lqro_get_stats / lqro_get_records / lqro_get_timings wait for the last
+ * enqueued step on the stream it was enqueued on.  The hull queue holds one
+ * entry per pair slot, so a step cannot overflow it. */
 int lqro_step_device(lqro_ctx* ctx, const double* d_x, const double* d_vgoal,
                      double* d_newv, void* stream);
 

@@ -383,8 +383,17 @@ struct lqro_ctx {
   unsigned long long* d_stats;
   unsigned long long* d_prof;
   int lds_bytes;
+  int stepped;               // a step was enqueued (ev[3] recorded)
   PairArgs pa;
 };
+
+// the last step's final event was recorded on whichever stream it was
+// enqueued on (the caller's for lqro_step_device): wait on that, not on
+// c->stream; a context that never stepped has nothing to wait for
+static hipError_t wait_last_step(lqro_ctx* c) {
+  if (!c->stepped) return hipStreamSynchronize(c->stream);
+  return hipEventSynchronize(c->ev[3]);
+}
 
 #define HIPCHK(x)                                                                        \
   do {                                                                                   \
@@ -474,8 +483,9 @@ static int ctx_alloc(lqro_ctx* c) {
   HIPCHK(hipMalloc(&c->d_lpcompact, sizeof(float) * 8 * (slots ? slots : 1)));
   if (g.flags & LQRO_FLAG_RECORDS)
     HIPCHK(hipMalloc(&c->d_recs, sizeof(lqro_pair_record) * (slots ? slots : 1)));
-  c->hull_cap = (int)(slots < (1u << 22) ? slots : (1u << 22));
-  if (c->hull_cap < 1) c->hull_cap = 1;
+  // one entry per slot: a pair enqueues at most one hull job per step, so the
+  // queue cannot overflow (C5's 2048 x 16383-slot shard: 134 MB, of 288 GB)
+  c->hull_cap = (int)(slots > 0 ? slots : 1);
   HIPCHK(hipMalloc(&c->d_hq, sizeof(int) * c->hull_cap));
   // hull count, next, retry count, retry next, pair rows, -, hot count, hot next, -, lp4 count, lp4 next
   HIPCHK(hipMalloc(&c->d_hcount, sizeof(int) * 16));
@@ -792,16 +802,19 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   La.lp4_list = c->d_lp4; La.lp4_count = c->d_hcount + 9; La.lp4_next = c->d_hcount + 10;
   HIPCHK(launch_lp(La, s));
   HIPCHK(hipEventRecord(c->ev[3], s));
+  c->stepped = 1;
   return LQRO_OK;
 }
 
+// `stream` is the caller's HIP stream; NULL is the default (null) stream, as
+// in lqro_dynamics_step_device, so the step is ordered with the work the
+// caller (e.g. torch's default stream, RCCL's waits on it) has on it.
 int lqro_step_device(lqro_ctx* c, const double* d_x, const double* d_vgoal, double* d_newv,
                      void* stream) {
   if (!c || !d_x || !d_vgoal || !d_newv) return LQRO_E_ARG;
   if (!c->have_gains) return LQRO_E_STATE;
   HIPCHK(hipSetDevice(c->cfg.device));
-  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-  return enqueue_step(c, d_x, d_vgoal, d_newv, s);
+  return enqueue_step(c, d_x, d_vgoal, d_newv, (hipStream_t)stream);
 }
 
 int lqro_step(lqro_ctx* c, const double* x, const double* vgoal, double* newv) {
@@ -1069,7 +1082,7 @@ int lqro_get_records(lqro_ctx* c, lqro_pair_record* out, int64_t cap, int64_t* n
   const int64_t n = (int64_t)c->nrows * (c->nbr_k > 0 ? std::min(c->nbr_k, c->npr) : c->npr);
   if (cap < n) return LQRO_E_ARG;
   HIPCHK(hipSetDevice(c->cfg.device));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(wait_last_step(c));
   HIPCHK(hipMemcpy(out, c->d_recs, sizeof(lqro_pair_record) * (size_t)n, hipMemcpyDeviceToHost));
   if (n_out) *n_out = n;
   return LQRO_OK;
@@ -1078,7 +1091,7 @@ int lqro_get_records(lqro_ctx* c, lqro_pair_record* out, int64_t cap, int64_t* n
 int lqro_get_stats(lqro_ctx* c, int64_t* st) {
   if (!c || !st) return LQRO_E_ARG;
   HIPCHK(hipSetDevice(c->cfg.device));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(wait_last_step(c));
   unsigned long long h[8];
   HIPCHK(hipMemcpy(h, c->d_stats, sizeof h, hipMemcpyDeviceToHost));
   for (int k = 0; k < 8; ++k) st[k] = (int64_t)h[k];
@@ -1091,7 +1104,7 @@ int lqro_get_stats(lqro_ctx* c, int64_t* st) {
 int lqro_debug_hull_profile(lqro_ctx* c, unsigned long long* out16) {
   if (!c || !out16) return LQRO_E_ARG;
   HIPCHK(hipSetDevice(c->cfg.device));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(wait_last_step(c));
   HIPCHK(hipMemcpy(out16, c->d_prof, sizeof(unsigned long long) * LQRO_PROF_WORDS, hipMemcpyDeviceToHost));
   return LQRO_OK;
 }

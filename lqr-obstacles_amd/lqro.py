@@ -213,18 +213,32 @@ class Context:
 
     def set_gains(self, A, B, L, E, per_agent: bool = False):
         A, B, L, E = (np.ascontiguousarray(v, dtype=np.float64) for v in (A, B, L, E))
+        X, U, n = self.cfg.x_dim, self.cfg.u_dim, self.cfg.n_agents
+        lead = (n,) if per_agent else ()
+        for name, v, shp in (("A", A, (X, X)), ("B", B, (X, U)), ("L", L, lead + (U, X)),
+                             ("E", E, lead + (U, 3))):
+            if v.shape != shp and not (per_agent is False and v.shape == (1,) + shp):
+                raise LqroError(f"set_gains: {name} has shape {v.shape}, expected {shp}")
         _check(lib().lqro_set_gains(self._h, _p(A), _p(B), _p(L), _p(E), int(per_agent)),
                "lqro_set_gains")
 
     def step(self, x: np.ndarray, vgoal: np.ndarray) -> np.ndarray:
         x = np.ascontiguousarray(x, dtype=np.float64)
         vgoal = np.ascontiguousarray(vgoal, dtype=np.float64)
+        n = self.cfg.n_agents
+        if x.shape != (n, self.cfg.x_dim):
+            raise LqroError(f"step: x has shape {x.shape}, expected {(n, self.cfg.x_dim)}")
+        if vgoal.shape != (n, 3):
+            raise LqroError(f"step: vgoal has shape {vgoal.shape}, expected {(n, 3)}")
         newv = np.zeros((self.cfg.n_agents, 3))
         _check(lib().lqro_step(self._h, _p(x), _p(vgoal), _p(newv)), "lqro_step")
         return newv
 
     def step_device(self, d_x: int, d_vgoal: int, d_newv: int, stream: int = 0):
-        """Device pointers (e.g. torch tensor .data_ptr()) on the context's device."""
+        """Device pointers (e.g. torch tensor .data_ptr()) on the context's
+        device, enqueued on `stream` (a hipStream_t handle such as
+        torch.cuda.current_stream().cuda_stream; 0 = the null stream, which is
+        torch's default stream), so it is ordered with the caller's work."""
         _check(lib().lqro_step_device(self._h, C.c_void_p(d_x), C.c_void_p(d_vgoal),
                                       C.c_void_p(d_newv), C.c_void_p(stream or None)),
                "lqro_step_device")
@@ -522,3 +536,94 @@ def allgather_rows(dist, full, rank: int, world: int, group=None):
         b, e = row_shard(n, r, world)
         full[b:e] = recv[r * chunk: r * chunk + (e - b)]
     return full
+
+
+class DeviceLoop:
+    """The whole control loop LQRO:1391-1446 on device buffers, for the rows
+    [rb, re) this rank owns: ``step()`` is the pair loop (lqro_step_device),
+    ``update()`` the agent loop after it (vGoal = newV, lqro_dynamics_step_device
+    on the own rows), then the single exchange per step: an all-gather of the
+    new estimates x.  Every launch goes on `stream` (default:
+    torch's current stream), so RCCL's stream waits order the exchange against
+    the kernels and no device synchronisation is needed between the calls.
+
+    The noise of step t is the reference's rand() stream for all N agents in
+    agent order (LQRO:1437-1446 draws per agent in turn); each rank uses its
+    own rows' draws, so a sharded run equals the single-context run bit for
+    bit."""
+
+    def __init__(self, x0, vgoal0, gains: dict, horizon: int, n_points: int = 100, *,
+                 p_goal=None, rank: int = 0, world: int = 1, dist=None, device=None,
+                 model: Model | None = None, seed: int = 1, stream=None):
+        import torch
+        self.torch = torch
+        self.dev = torch.device("cuda", torch.cuda.current_device()) if device is None else device
+        self.stream = stream if stream is not None else torch.cuda.current_stream(self.dev)
+        n = x0.shape[0]
+        self.n, self.rank, self.world, self.dist = n, rank, world, dist
+        self.rb, self.re = row_shard(n, rank, world)
+        rows = self.re - self.rb
+        self.model = model or default_model()
+        self.seed = seed
+        f64 = dict(dtype=torch.float64, device=self.dev)
+        self.ctx = Context(config(n, horizon, n_points, device=self.dev.index,
+                                  row_begin=self.rb, row_end=self.re))
+        self.ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
+        self.x = torch.from_numpy(np.ascontiguousarray(x0, np.float64)).to(self.dev)
+        self.vgoal = torch.from_numpy(np.ascontiguousarray(vgoal0, np.float64)).to(self.dev)
+        self.newv = torch.zeros((n, 3), **f64)
+        eye3 = torch.eye(3, **f64).repeat(rows, 1, 1).contiguous()
+        hover = self.model.gravity * self.model.mass / 4
+        pg = np.zeros((n, 3)) if p_goal is None else np.asarray(p_goal, np.float64)
+        self.own = dict(rot=eye3.clone(), x_true=self.x[self.rb:self.re].clone(), rot_true=eye3.clone(),
+                        P=(1e-9 * torch.eye(16, **f64)).repeat(rows, 1, 1).contiguous(),
+                        u_goal=torch.full((rows, 4), hover, **f64),
+                        p_goal=torch.from_numpy(np.ascontiguousarray(pg[self.rb:self.re])).to(self.dev))
+        self.g = {k: torch.from_numpy(np.ascontiguousarray(gains[k], np.float64)).to(self.dev)
+                  for k in ("L", "E", "Lh", "Eh")}
+        self.g["l"] = torch.from_numpy(np.ascontiguousarray(gains.get("l", np.zeros(4)), np.float64)).to(self.dev)
+        self.M = 1e-9 * torch.eye(16, **f64)
+        self.Nz = 1e-9 * torch.eye(6, **f64)
+        self.model_d = torch.frombuffer(bytearray(bytes(self.model)), dtype=torch.uint8).to(self.dev)
+        self.nrm = None
+        self.t = 0
+
+    def _sid(self):
+        return self.stream.cuda_stream
+
+    def step(self, gather: bool = False):
+        """The pair loop for the own rows; newV of the own rows on the device
+        (all rows with gather=True: one all-gather of newV)."""
+        self.ctx.step_device(self.x.data_ptr(), self.vgoal.data_ptr(), self.newv.data_ptr(), self._sid())
+        if gather and self.world > 1:
+            with self.torch.cuda.stream(self.stream):
+                allgather_rows(self.dist, self.newv, self.rank, self.world)
+        return self.newv
+
+    def update(self):
+        """LQRO:1437-1446 for the own rows, then the all-gather of x."""
+        torch = self.torch
+        rb, re = self.rb, self.re
+        nrm, self.seed = normals(self.seed, self.n * NORMALS_PER_AGENT)
+        with torch.cuda.stream(self.stream):
+            # pinned + non-blocking: no host wait on the stream's earlier work
+            host = torch.from_numpy(np.ascontiguousarray(nrm.reshape(self.n, NORMALS_PER_AGENT)[rb:re]))
+            self.nrm = host.pin_memory().to(self.dev, non_blocking=True)
+            self.vgoal[rb:re].copy_(self.newv[rb:re])          # vGoal = newV (LQRO:1438)
+        xs, vs = self.x[rb:re], self.vgoal[rb:re]
+        o, g = self.own, self.g
+        a = Agents(xs.data_ptr(), o["rot"].data_ptr(), o["x_true"].data_ptr(), o["rot_true"].data_ptr(),
+                   o["P"].data_ptr(), vs.data_ptr(), None, o["u_goal"].data_ptr(), o["p_goal"].data_ptr(),
+                   g["L"].data_ptr(), g["E"].data_ptr(), g["l"].data_ptr(), g["Lh"].data_ptr(),
+                   g["Eh"].data_ptr(), self.M.data_ptr(), self.Nz.data_ptr(), self.nrm.data_ptr())
+        a.time = self.t * self.model.dt
+        _check(lib().lqro_dynamics_step_device(C.c_void_p(self.model_d.data_ptr()), 1, re - rb, 0,
+                                               C.byref(a), C.c_void_p(self._sid() or None)),
+               "lqro_dynamics_step_device")
+        if self.world > 1:
+            with torch.cuda.stream(self.stream):
+                allgather_rows(self.dist, self.x, self.rank, self.world)
+        self.t += 1
+
+    def close(self):
+        self.ctx.close()

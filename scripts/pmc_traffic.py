@@ -43,6 +43,14 @@ def per_kernel(d, counter):
     return {k: sum(v) / len(v) for k, v in acc.items()}, {k: len(v) for k, v in acc.items()}
 
 
+def lib_stamp():
+    """The stamp of the liblqro.so these passes measured (written by
+    __graft_entry__.build_lib): bench.py cites the file only for that build."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "lqr-obstacles_amd", "liblqro.stamp.json")) as f:
+        return json.load(f)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch_dir")
@@ -65,7 +73,8 @@ def main():
     out = {"n_agents": a.n_agents, "horizon": a.horizon,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
                      "KiB -> bytes; FETCH_SIZE x2 (gfx950 correction, MI355X_MICROARCH.md)",
-           "kernels": ks}
+           "kernels": ks,
+           "build": lib_stamp()}
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
