@@ -118,6 +118,19 @@ int lqro_synthesize_gains_batch(const lqro_model* models, int32_t n,
                                 double* A, double* B, double* c, double* L, double* E,
                                 double* Lh, double* Eh, int32_t device);
 
+/* The same two syntheses for a state width x_dim: 16 (the reference's
+ * quadrotor, identical to the two calls above) or 12, the reduced model of
+ * BASELINE config 5: the 4 rotor-force states of X_DIM = 16
+ * (simulator2.h:4) dropped, rotor forces = the command (no thrust lag), every
+ * other term of f (LQRO:368-397) unchanged, linearised at the same hover
+ * point.  Shapes as above with X = x_dim. */
+int lqro_synthesize_gains_x(const lqro_model* m, int32_t x_dim,
+                            double* A, double* B, double* c, double* L, double* E,
+                            double* Lh, double* Eh);
+int lqro_synthesize_gains_batch_x(const lqro_model* models, int32_t n, int32_t x_dim,
+                                  double* A, double* B, double* c, double* L, double* E,
+                                  double* Lh, double* Eh, int32_t device);
+
 /* Replaces createSpheres (LQRO:735-750): NP Fibonacci-sphere points. */
 int lqro_sphere(int32_t n_points, double xy_radius, double z_radius, double* out /* NP*3 */);
 

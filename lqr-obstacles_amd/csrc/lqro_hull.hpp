@@ -138,7 +138,8 @@ typedef HullLdsT<2048, 1024, HULL_WAVES> HullLdsBig;
 //   bits  0-15  its furthest outside point (HULL_NOPT: none)
 //   bits 16-23  lock, one bit per wave
 //   bits 24-31  visible-region mark, one bit per wave; all set: retired slot
-// Extents are packed as off << 14 | cnt (H*NP <= 16383, see runtime).
+// Extents are packed as (off / 4) << 15 | cnt: k_hull's segments start at
+// multiples of 4 entries (seg_round), so H*NP <= kHullLdsMaxHNP (see runtime).
 #define HULL_NOPT 0xFFFFu
 #define HULL_DEAD 0xFF00FFFFu
 struct HullMemC {
@@ -217,14 +218,16 @@ __device__ __forceinline__ double hl_rl(double v, int k) {
 
 // outside-set extent of face f
 __device__ __forceinline__ void seg_get(unsigned int s, int& off, int& cnt) {
-  off = (int)(s >> 14); cnt = (int)(s & 0x3FFFu);
+  off = (int)((s >> 15) << 2); cnt = (int)(s & 0x7FFFu);
 }
 __device__ __forceinline__ void seg_get(unsigned long long s, int& off, int& cnt) {
   off = (int)(s >> 32); cnt = (int)(s & 0xFFFFFFFFu);
 }
 __device__ __forceinline__ void seg_put(unsigned int& s, int off, int cnt) {
-  s = ((unsigned int)off << 14) | (unsigned int)cnt;
+  s = (((unsigned int)off >> 2) << 15) | (unsigned int)cnt;
 }
+// room a segment of cnt entries takes in k_hull's buffer (starts stay 4-aligned)
+__device__ __forceinline__ int seg_round(int cnt) { return (cnt + 3) & ~3; }
 __device__ __forceinline__ void seg_put(unsigned long long& s, int off, int cnt) {
   s = ((unsigned long long)(unsigned)off << 32) | (unsigned)cnt;
 }
@@ -825,8 +828,8 @@ __device__ __noinline__ int hull_insert_wide(HullMemC& M, HullLdsC<NW>& L, HullW
   for (int h0 = 0; h0 < nh; h0 += 64) {
     const int h = h0 + lane;
     const int cnt = h < nh ? WG.cnt[h] : 0;
-    const int x = wave_incl_scan(cnt);
-    if (h < nh) WG.off[h] = run + x - cnt;
+    const int x = wave_incl_scan(seg_round(cnt));
+    if (h < nh) WG.off[h] = run + x - seg_round(cnt);
     run += __builtin_amdgcn_readlane(x, 63);
   }
   int base = 0;
@@ -1259,12 +1262,12 @@ __device__ __forceinline__ void hull_insert_mw(HullMemC& M, HullLdsC<NW>& L, con
       hl_sync();
       const int cnt = hl ? W.hcnt[lane] : 0;
       const unsigned long long km = hl ? W.kmax[lane] : 0ull;
-      const int cinc = wave_incl_scan(cnt);
+      const int cinc = wave_incl_scan(seg_round(cnt));
       const int tot = __builtin_amdgcn_readlane(cinc, 63);
       if (lane == 0) base = atomicAdd(&L.sbtop, tot);
       base = __builtin_amdgcn_readlane(base, 0);
       if (base + tot > sbcap) { if (lane == 0) atomicMax(&L.fail, 6); break; }
-      const int off = base + cinc - cnt;
+      const int off = base + cinc - seg_round(cnt);
       if (hl) {
         seg_put(M.seg[sf], off, cnt);
         M.own[sf] = LK | (cnt ? ((~(unsigned)km) & 0xFFFFu) : HULL_NOPT);
@@ -1298,12 +1301,12 @@ __device__ __forceinline__ void hull_insert_mw(HullMemC& M, HullLdsC<NW>& L, con
       hl_sync();
       const int cnt = hl ? W.hcnt[lane] : 0;
       const unsigned long long km = hl ? W.kmax[lane] : 0ull;
-      const int cinc = wave_incl_scan(cnt);
+      const int cinc = wave_incl_scan(seg_round(cnt));
       const int tot = __builtin_amdgcn_readlane(cinc, 63);
       if (lane == 0) base = atomicAdd(&L.sbtop, tot);
       base = __builtin_amdgcn_readlane(base, 0);
       if (base + tot > sbcap) { if (lane == 0) atomicMax(&L.fail, 6); break; }
-      const int off = base + cinc - cnt;
+      const int off = base + cinc - seg_round(cnt);
       if (hl) {
         seg_put(M.seg[sf], off, cnt);
         M.own[sf] = LK | (cnt ? ((~(unsigned)km) & 0xFFFFu) : HULL_NOPT);
@@ -1432,7 +1435,7 @@ __device__ __forceinline__ void hull_body_mw(const HullArgs& A, HullMemC& M, Hul
         for (int f = 0; f < 4; ++f) {
           seg_put(M.seg[f], o, L.hcnt[f]);
           L.hoff[f] = o;
-          o += L.hcnt[f];
+          o += seg_round(L.hcnt[f]);
         }
         L.sbtop = o;
         L.nf = 4;

@@ -79,6 +79,7 @@ static void launch_side(int x_dim, dim3 grid, dim3 block, hipStream_t s, const H
 }
 
 #define LQRO_MAXX 16
+constexpr size_t kHullLdsMaxHNP = (size_t)(1 << 19) / HULL_SBMULT;   // 21,845 (C5: H*NP = 20,000)
 
 // ---------------------------------------------------------------------------
 // Horizon tables (per agent): T_k = !(C*G_k) (3x3), NCF_k = (-C)*F_k (3xX),
@@ -405,6 +406,19 @@ static hipError_t wait_last_step(lqro_ctx* c) {
     }                                                                                    \
   } while (0)
 
+template <int X>
+__global__ void __launch_bounds__(64) k_synth(const lqro_model* models, int n, double* out) {
+  const int a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= n) return;
+  constexpr int S = X * X + 12 * X + 21;
+  double* o = out + (size_t)a * S;
+  double* p[7];
+  p[0] = o;
+  p[1] = p[0] + X * X; p[2] = p[1] + X * 4; p[3] = p[2] + X; p[4] = p[3] + 4 * X; p[5] = p[4] + 12;
+  p[6] = p[5] + 3 * X;
+  synth::gains_x<X>(models + a, p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
+}
+
 extern "C" {
 
 int lqro_version(void) { return 1; }
@@ -718,8 +732,9 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
     HIPCHK(hipGetLastError());
     P.nbr_list = c->d_nbrlist;
   }
-  // the LDS hull variant packs outside-set extents in 32 bits: H*NP <= 16383
-  const bool lds_ok = (size_t)g.horizon * g.n_points <= 16383;
+  // the LDS hull variant packs outside-set extents in 32 bits (lqro_hull.hpp
+  // seg_put: 15-bit count, 17-bit offset / 4 into HULL_SBMULT * H*NP entries)
+  const bool lds_ok = (size_t)g.horizon * g.n_points <= kHullLdsMaxHNP;
   const long slots = (long)c->nrows * npr;
   const bool side_fits = (size_t)(P.lds_wave + HULL_CWAVES * P.wave_doubles) * 8 <= sizeof(HullMemC) &&
                          P.waves >= HULL_CWAVES;
@@ -847,35 +862,46 @@ int lqro_synthesize_gains(const lqro_model* md, double* Ao, double* Bo, double* 
   return LQRO_OK;
 }
 
-// per-agent output block, in doubles: A 256, B 64, c 16, L 64, E 12, Lh 48, Eh 9
-constexpr int kSynthOut[7] = {256, 64, 16, 64, 12, 48, 9};
-constexpr int kSynthStride = 469;
-
-__global__ void __launch_bounds__(64) k_synth(const lqro_model* models, int n, double* out) {
-  const int a = blockIdx.x * blockDim.x + threadIdx.x;
-  if (a >= n) return;
-  double* o = out + (size_t)a * kSynthStride;
-  synth::gains(models + a, o, o + 256, o + 320, o + 336, o + 400, o + 412, o + 460);
+int lqro_synthesize_gains_x(const lqro_model* md, int32_t x_dim, double* Ao, double* Bo, double* co,
+                            double* Lo, double* Eo, double* Lho, double* Eho) {
+  if (!md) return LQRO_E_ARG;
+  if (x_dim == 16) synth::gains_x<16>(md, Ao, Bo, co, Lo, Eo, Lho, Eho);
+  else if (x_dim == 12) synth::gains_x<12>(md, Ao, Bo, co, Lo, Eo, Lho, Eho);
+  else return LQRO_E_ARG;
+  return LQRO_OK;
 }
 
-int lqro_synthesize_gains_batch(const lqro_model* models, int32_t n, double* A, double* B, double* c,
-                                double* L, double* E, double* Lh, double* Eh, int32_t device) {
-  if (!models || n <= 0) return LQRO_E_ARG;
+// per-agent output block, in doubles: A X*X, B X*4, c X, L 4*X, E 12, Lh 3*X, Eh 9
+static void synth_sizes(int X, int* sz) {
+  sz[0] = X * X; sz[1] = X * 4; sz[2] = X; sz[3] = 4 * X; sz[4] = 12; sz[5] = 3 * X; sz[6] = 9;
+}
+static int synth_stride(int X) { return X * X + 12 * X + 21; }
+
+int lqro_synthesize_gains_batch_x(const lqro_model* models, int32_t n, int32_t x_dim, double* A, double* B,
+                                  double* c, double* L, double* E, double* Lh, double* Eh, int32_t device) {
+  if (!models || n <= 0 || (x_dim != 16 && x_dim != 12)) return LQRO_E_ARG;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) return LQRO_E_NODEVICE;
   if (hipSetDevice(device) != hipSuccess) return LQRO_E_HIP;
+  const int stride = synth_stride(x_dim);
+  int sz[7];
+  synth_sizes(x_dim, sz);
   lqro_model* d_m = nullptr;
   double* d_out = nullptr;
   int rc = LQRO_OK;
   if (hipMalloc(&d_m, sizeof(lqro_model) * (size_t)n) != hipSuccess ||
-      hipMalloc(&d_out, sizeof(double) * kSynthStride * (size_t)n) != hipSuccess) {
+      hipMalloc(&d_out, sizeof(double) * stride * (size_t)n) != hipSuccess) {
     rc = LQRO_E_NOMEM;
   } else if (hipMemcpy(d_m, models, sizeof(lqro_model) * (size_t)n, hipMemcpyHostToDevice) != hipSuccess) {
     rc = LQRO_E_HIP;
   } else {
-    hipLaunchKernelGGL(k_synth, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, 0, (const lqro_model*)d_m, (int)n,
-                       d_out);
-    std::vector<double> h((size_t)kSynthStride * n);
+    if (x_dim == 16)
+      hipLaunchKernelGGL(k_synth<16>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, 0, (const lqro_model*)d_m,
+                         (int)n, d_out);
+    else
+      hipLaunchKernelGGL(k_synth<12>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, 0, (const lqro_model*)d_m,
+                         (int)n, d_out);
+    std::vector<double> h((size_t)stride * n);
     if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
         hipMemcpy(h.data(), d_out, sizeof(double) * h.size(), hipMemcpyDeviceToHost) != hipSuccess) {
       rc = LQRO_E_HIP;
@@ -885,15 +911,19 @@ int lqro_synthesize_gains_batch(const lqro_model* models, int32_t n, double* A, 
       for (int k = 0; k < 7; ++k) {
         if (outs[k])
           for (int a = 0; a < n; ++a)
-            memcpy(outs[k] + (size_t)a * kSynthOut[k], h.data() + (size_t)a * kSynthStride + off,
-                   sizeof(double) * kSynthOut[k]);
-        off += kSynthOut[k];
+            memcpy(outs[k] + (size_t)a * sz[k], h.data() + (size_t)a * stride + off, sizeof(double) * sz[k]);
+        off += sz[k];
       }
     }
   }
   if (d_m) (void)hipFree(d_m);
   if (d_out) (void)hipFree(d_out);
   return rc;
+}
+
+int lqro_synthesize_gains_batch(const lqro_model* models, int32_t n, double* A, double* B, double* c,
+                                double* L, double* E, double* Lh, double* Eh, int32_t device) {
+  return lqro_synthesize_gains_batch_x(models, n, 16, A, B, c, L, E, Lh, Eh, device);
 }
 
 // ---- the per-agent step after the pair loop (LQRO:1437-1446) -------------

@@ -222,16 +222,21 @@ struct Quad {
   Mat<3, 3> J, Jinv;
 };
 
-// hover dynamics x' = f(x, R, u), 16-state quadrotor (position, velocity,
-// rotation error, body rates, rotor forces)
-LQRO_HD Mat<16, 1> dynamics(const Quad& q, const Mat<16, 1>& x, const Mat<3, 3>& R, const Mat<4, 1>& u) {
+// hover dynamics x' = f(x, R, u) (LQRO:368-397).  X = 16: the reference's
+// quadrotor (position, velocity, rotation error, body rates, rotor forces
+// with first-order lag (u - F) * thrust_latency).  X = 12: the reduced model
+// of BASELINE config 5 — the 4 rotor-force states dropped, the
+// rotors follow their command at once (F = u); every other term as X = 16.
+template <int X>
+LQRO_HD Mat<X, 1> dynamics(const Quad& q, const Mat<X, 1>& x, const Mat<3, 3>& R, const Mat<4, 1>& u) {
+  static_assert(X == 16 || X == 12, "x_dim is 16 or 12");
   Vec3 eX = Vec3::zero(), eY = Vec3::zero(), eZ = Vec3::zero();
   eX.e[0] = 1; eY.e[1] = 1; eZ.e[2] = 1;
   Vec3 v, r, w;
   double F[4];
   for (int k = 0; k < 3; ++k) { v.e[k] = x.e[3 + k]; r.e[k] = x.e[6 + k]; w.e[k] = x.e[9 + k]; }
-  for (int k = 0; k < 4; ++k) F[k] = x.e[12 + k];
-  Mat<16, 1> xd;
+  for (int k = 0; k < 4; ++k) F[k] = X == 16 ? x.e[(12 + k) % X] : u.e[k];
+  Mat<X, 1> xd;
   for (int k = 0; k < 3; ++k) xd.e[k] = v.e[k];
   Vec3 acc = -q.g * eZ + R * expm(skew(r)) * ((F[0] + F[1] + F[2] + F[3]) / q.mass) * eZ;
   for (int k = 0; k < 3; ++k) xd.e[3 + k] = acc.e[k];
@@ -245,7 +250,8 @@ LQRO_HD Mat<16, 1> dynamics(const Quad& q, const Mat<16, 1>& x, const Mat<3, 3>&
   Vec3 wd = q.Jinv * (q.arm * (F[1] - F[3]) * eX + q.arm * (F[2] - F[0]) * eY +
                       (F[0] - F[1] + F[2] - F[3]) * q.kM * eZ - skew(w) * q.J * w);
   for (int k = 0; k < 3; ++k) xd.e[9 + k] = wd.e[k];
-  for (int k = 0; k < 4; ++k) xd.e[12 + k] = (u.e[k] - F[k]) * q.lat;
+  if (X == 16)
+    for (int k = 0; k < 4; ++k) xd.e[(12 + k) % X] = (u.e[k] - F[k]) * q.lat;
   return xd;
 }
 
@@ -256,9 +262,11 @@ LQRO_HD void put(double* out, const Mat<R, C>& m) {
 }
 
 // controlMatrices for one agent's model: A (X*X), B (X*U), c (X), L (U*X),
-// E (U*3), Lh (3*X), Eh (3*3); any output may be null
-LQRO_HD void gains(const lqro_model* md, double* Ao, double* Bo, double* co, double* Lo, double* Eo,
-                   double* Lho, double* Eho) {
+// E (U*3), Lh (3*X), Eh (3*3); any output may be null.  X = 12: the reduced
+// model above, linearised at the same hover point.
+template <int X>
+LQRO_HD void gains_x(const lqro_model* md, double* Ao, double* Bo, double* co, double* Lo, double* Eo,
+                     double* Lho, double* Eho) {
   Quad q;
   q.dt = md->dt; q.g = md->gravity; q.mass = md->mass; q.kM = md->moment_const;
   q.lat = md->thrust_latency; q.arm = md->length; q.h = md->j_step;
@@ -267,82 +275,87 @@ LQRO_HD void gains(const lqro_model* md, double* Ao, double* Bo, double* co, dou
   const double hover = q.g * q.mass / 4;
   Mat<4, 1> u0;
   for (int k = 0; k < 4; ++k) u0.e[k] = hover;
-  Mat<16, 1> x0 = Mat<16, 1>::zero();
-  for (int k = 12; k < 16; ++k) x0.e[k] = hover;
+  Mat<X, 1> x0 = Mat<X, 1>::zero();
+  for (int k = 12; k < X; ++k) x0.e[k] = hover;
   Mat<3, 3> R0 = eye<3>();
 
   // central-difference Jacobians, then A = e^{F dt}, B/c by Simpson's rule
-  Mat<16, 16> F;
-  Mat<16, 4> G;
+  Mat<X, X> F;
+  Mat<X, 4> G;
   {
-    Mat<16, 1> xr = x0, xl = x0;
-    for (int i = 0; i < 16; ++i) {
+    Mat<X, 1> xr = x0, xl = x0;
+    for (int i = 0; i < X; ++i) {
       xr.e[i] += q.h; xl.e[i] -= q.h;
-      Mat<16, 1> col = (dynamics(q, xr, R0, u0) - dynamics(q, xl, R0, u0)) / (2 * q.h);
-      for (int k = 0; k < 16; ++k) F(k, i) = col.e[k];
+      Mat<X, 1> col = (dynamics<X>(q, xr, R0, u0) - dynamics<X>(q, xl, R0, u0)) / (2 * q.h);
+      for (int k = 0; k < X; ++k) F(k, i) = col.e[k];
       xr.e[i] = xl.e[i] = x0.e[i];
     }
     Mat<4, 1> ur = u0, ul = u0;
     for (int i = 0; i < 4; ++i) {
       ur.e[i] += q.h; ul.e[i] -= q.h;
-      Mat<16, 1> col = (dynamics(q, x0, R0, ur) - dynamics(q, x0, R0, ul)) / (2 * q.h);
-      for (int k = 0; k < 16; ++k) G(k, i) = col.e[k];
+      Mat<X, 1> col = (dynamics<X>(q, x0, R0, ur) - dynamics<X>(q, x0, R0, ul)) / (2 * q.h);
+      for (int k = 0; k < X; ++k) G(k, i) = col.e[k];
       ur.e[i] = ul.e[i] = u0.e[i];
     }
   }
-  Mat<16, 1> xdot = dynamics(q, x0, R0, u0);
-  Mat<16, 16> A = expm(q.dt * F);
-  Mat<16, 16> Int = (q.dt / 6.0) * (eye<16>() + 4.0 * expm(0.5 * q.dt * F) + A);
-  Mat<16, 4> B = Int * G;
-  Mat<16, 1> c = Int * xdot;
+  Mat<X, 1> xdot = dynamics<X>(q, x0, R0, u0);
+  Mat<X, X> A = expm(q.dt * F);
+  Mat<X, X> Int = (q.dt / 6.0) * (eye<X>() + 4.0 * expm(0.5 * q.dt * F) + A);
+  Mat<X, 4> B = Int * G;
+  Mat<X, 1> c = Int * xdot;
 
   // velocity LQR: 300 Riccati sweeps with a velocity-tracking term
-  Mat<3, 16> Vs = Mat<3, 16>::zero(), Ps = Mat<3, 16>::zero();
+  Mat<3, X> Vs = Mat<3, X>::zero(), Ps = Mat<3, X>::zero();
   Vs(0, 3) = Vs(1, 4) = Vs(2, 5) = 1;
   Ps(0, 0) = Ps(1, 1) = Ps(2, 2) = 1;
   Mat<3, 3> Qv = md->qv * eye<3>(), Qp = md->qp * eye<3>();
   Mat<4, 4> Rw = md->r * eye<4>();
-  Mat<16, 16> Qx = Mat<16, 16>::zero();
-  Mat<16, 16> At = tr(A);
-  Mat<4, 16> Bt = tr(B);
-  Mat<16, 3> Vt = tr(Vs);
-  Mat<16, 16> S = Vt * Qv * Vs;
-  Mat<16, 3> T = -Vt * Qv;
+  Mat<X, X> Qx = Mat<X, X>::zero();
+  Mat<X, X> At = tr(A);
+  Mat<4, X> Bt = tr(B);
+  Mat<X, 3> Vt = tr(Vs);
+  Mat<X, X> S = Vt * Qv * Vs;
+  Mat<X, 3> T = -Vt * Qv;
   for (int it = 0; it < 300; ++it) {
-    Mat<16, 4> K = At * S * B * inverse(Rw + Bt * S * B);
-    Mat<16, 3> Tn = -Vt * Qv + At * T - K * Bt * T;
-    Mat<16, 16> Sn = Vt * Qv * Vs + Qx + At * S * A - K * (Bt * S * A);
+    Mat<X, 4> K = At * S * B * inverse(Rw + Bt * S * B);
+    Mat<X, 3> Tn = -Vt * Qv + At * T - K * Bt * T;
+    Mat<X, X> Sn = Vt * Qv * Vs + Qx + At * S * A - K * (Bt * S * A);
     T = Tn;
     S = Sn;
   }
   Mat<4, 4> Ri = inverse(Rw + Bt * S * B);
-  Mat<4, 16> L = -Ri * Bt * S * A;
+  Mat<4, X> L = -Ri * Bt * S * A;
   Mat<4, 3> E = -Ri * Bt * T;
 
   // position LQR on the closed velocity loop, with the cross term
   const double wgt = md->pos_weight;
-  Mat<16, 16> Qpt = tr(Ps) * Qp * Ps + wgt * tr(L) * Rw * L;
+  Mat<X, X> Qpt = tr(Ps) * Qp * Ps + wgt * tr(L) * Rw * L;
   Mat<3, 3> Rt = wgt * tr(E) * Rw * E;
-  Mat<3, 16> Pt = wgt * tr(E) * Rw * L;
-  Mat<16, 16> Acl = A + B * L;
-  Mat<16, 3> Bcl = B * E;
-  Mat<16, 16> Aclt = tr(Acl);
-  Mat<3, 16> Bclt = tr(Bcl);
-  Mat<16, 3> Ptt = tr(Pt);
-  Mat<16, 16> St = Qpt;
-  Mat<16, 3> Tt = -tr(Ps) * Qp;
+  Mat<3, X> Pt = wgt * tr(E) * Rw * L;
+  Mat<X, X> Acl = A + B * L;
+  Mat<X, 3> Bcl = B * E;
+  Mat<X, X> Aclt = tr(Acl);
+  Mat<3, X> Bclt = tr(Bcl);
+  Mat<X, 3> Ptt = tr(Pt);
+  Mat<X, X> St = Qpt;
+  Mat<X, 3> Tt = -tr(Ps) * Qp;
   for (int it = 0; it < 300; ++it) {
-    Mat<16, 3> K = (Ptt + Aclt * St * Bcl) * inverse(Rt + Bclt * St * Bcl);
-    Mat<16, 3> Ttn = -tr(Ps) * Qp + Aclt * Tt - K * Bclt * Tt;
-    Mat<16, 16> Stn = Qpt + Aclt * St * Acl - K * (Pt + Bclt * St * Acl);
+    Mat<X, 3> K = (Ptt + Aclt * St * Bcl) * inverse(Rt + Bclt * St * Bcl);
+    Mat<X, 3> Ttn = -tr(Ps) * Qp + Aclt * Tt - K * Bclt * Tt;
+    Mat<X, X> Stn = Qpt + Aclt * St * Acl - K * (Pt + Bclt * St * Acl);
     Tt = Ttn;
     St = Stn;
   }
   Mat<3, 3> RRi = inverse(Rt + Bclt * St * Bcl);
-  Mat<3, 16> Lh = -RRi * (Pt + Bclt * St * Acl);
+  Mat<3, X> Lh = -RRi * (Pt + Bclt * St * Acl);
   Mat<3, 3> Eh = -RRi * (Bclt * Tt);
 
   put(Ao, A); put(Bo, B); put(co, c); put(Lo, L); put(Eo, E); put(Lho, Lh); put(Eho, Eh);
+}
+
+LQRO_HD void gains(const lqro_model* md, double* Ao, double* Bo, double* co, double* Lo, double* Eo,
+                   double* Lho, double* Eho) {
+  gains_x<16>(md, Ao, Bo, co, Lo, Eo, Lho, Eho);
 }
 
 }  // namespace synth

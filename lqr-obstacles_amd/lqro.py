@@ -73,6 +73,7 @@ EXPORTS = (
     "lqro_get_records", "lqro_get_stats", "lqro_get_timings", "lqro_status_string",
     "lqro_version", "lqro_calculate_new_v", "lqro_synthesize_gains_batch",
     "lqro_dynamics_step", "lqro_dynamics_step_device", "lqro_normals", "lqro_set_neighbors",
+    "lqro_synthesize_gains_x", "lqro_synthesize_gains_batch_x",
 )
 
 NORMALS_PER_AGENT = 22   # LQRO_NORMALS_PER_AGENT: 16 propagate + 6 observation
@@ -101,6 +102,8 @@ def lib() -> C.CDLL:
         L.lqro_model_default.argtypes = [C.POINTER(Model)]
         L.lqro_synthesize_gains.argtypes = [C.POINTER(Model)] + [vp] * 7
         L.lqro_synthesize_gains_batch.argtypes = [C.POINTER(Model), i32] + [vp] * 7 + [i32]
+        L.lqro_synthesize_gains_x.argtypes = [C.POINTER(Model), i32] + [vp] * 7
+        L.lqro_synthesize_gains_batch_x.argtypes = [C.POINTER(Model), i32, i32] + [vp] * 7 + [i32]
         L.lqro_sphere.argtypes = [i32, dbl, dbl, vp]
         L.lqro_create.argtypes = [C.POINTER(Config), C.POINTER(vp)]
         L.lqro_destroy.argtypes = [vp]
@@ -140,29 +143,53 @@ def default_model() -> Model:
     return m
 
 
-def synthesize_gains(model: Model | None = None) -> dict:
-    """controlMatrices at hover (LQRO:520-582): A, B, c, L, E, Lh, Eh."""
+def gain_shapes(x_dim: int = 16) -> dict:
+    X = x_dim
+    return dict(A=(X, X), B=(X, 4), c=(X,), L=(4, X), E=(4, 3), Lh=(3, X), Eh=(3, 3))
+
+
+GAIN_SHAPES = gain_shapes(16)
+
+
+def synthesize_gains(model: Model | None = None, x_dim: int = 16) -> dict:
+    """controlMatrices at hover (LQRO:520-582): A, B, c, L, E, Lh, Eh.
+    x_dim = 12: BASELINE config 5's reduced model (rotor-force states
+    dropped, F = u; lqro_synthesize_gains_x)."""
     m = model or default_model()
-    out = dict(A=np.zeros((16, 16)), B=np.zeros((16, 4)), c=np.zeros(16), L=np.zeros((4, 16)),
-               E=np.zeros((4, 3)), Lh=np.zeros((3, 16)), Eh=np.zeros((3, 3)))
-    _check(lib().lqro_synthesize_gains(C.byref(m), *[_p(out[k]) for k in
-                                                   ("A", "B", "c", "L", "E", "Lh", "Eh")]),
-           "lqro_synthesize_gains")
+    out = {k: np.zeros(s) for k, s in gain_shapes(x_dim).items()}
+    _check(lib().lqro_synthesize_gains_x(C.byref(m), x_dim, *[_p(out[k]) for k in
+                                                            ("A", "B", "c", "L", "E", "Lh", "Eh")]),
+           "lqro_synthesize_gains_x")
     return out
 
 
-GAIN_SHAPES = dict(A=(16, 16), B=(16, 4), c=(16,), L=(4, 16), E=(4, 3), Lh=(3, 16), Eh=(3, 3))
-
-
-def synthesize_gains_batch(models, device: int = 0) -> dict:
+def synthesize_gains_batch(models, device: int = 0, x_dim: int = 16) -> dict:
     """controlMatrices for heterogeneous agents, on the GPU (one agent per
     lane): arrays with a leading agent axis, bit-identical to
-    synthesize_gains(models[k]); L and E feed Context.set_gains(per_agent=1)."""
+    synthesize_gains(models[k], x_dim); L and E feed
+    Context.set_gains(per_agent=1)."""
     n = len(models)
     arr = (Model * n)(*models)
-    out = {k: np.zeros((n,) + s) for k, s in GAIN_SHAPES.items()}
-    _check(lib().lqro_synthesize_gains_batch(arr, n, *[_p(out[k]) for k in GAIN_SHAPES], device),
-           "lqro_synthesize_gains_batch")
+    shp = gain_shapes(x_dim)
+    out = {k: np.zeros((n,) + s) for k, s in shp.items()}
+    _check(lib().lqro_synthesize_gains_batch_x(arr, n, x_dim, *[_p(out[k]) for k in shp], device),
+           "lqro_synthesize_gains_batch_x")
+    return out
+
+
+def perturbed_models(n: int, rel: float = 0.01, seed: int | None = None) -> list:
+    """n agent models with mass, inertia, arm length, moment constant, thrust
+    latency and the cost weights qv, qp, r each scaled by a factor in
+    [1 - rel, 1 + rel] (SplitMix64, seeded): the heterogeneous swarm of
+    BASELINE config 5."""
+    g = _splitmix(SEED_MODELS if seed is None else seed)
+    base = default_model()
+    out = []
+    for _ in range(n):
+        m = Model.from_buffer_copy(base)
+        for f in ("mass", "inertia", "length", "moment_const", "thrust_latency", "qv", "qp", "r"):
+            setattr(m, f, getattr(base, f) * (1.0 + rel * (2.0 * next(g) - 1.0)))
+        out.append(m)
     return out
 
 
@@ -287,6 +314,7 @@ def calculate_new_v(plane_lists, vgoals, vmax_lp: float = 100.0, device: int = 0
 # Synthetic swarms: SplitMix64, seed "LQRO"
 # ---------------------------------------------------------------------------
 SEED = 0x4C51524F
+SEED_MODELS = 0x4D4F444C   # "MODL"
 _M64 = 0xFFFFFFFFFFFFFFFF
 
 

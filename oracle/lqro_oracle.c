@@ -235,11 +235,18 @@ static void phys_init(const lqro_model* m, phys_t* p) {
   minv(3, p->inertia, p->invInertia);         /* LQRO:187 */
 }
 
-/* f (LQRO:368-397), X=16 */
+/* f (LQRO:368-397).  X=16: the reference.  X=12: BASELINE config 5's reduced
+ * model — no rotor-force states, F = u (not in the reference;
+ * its restatement here pins the GPU's lqro_synthesize_gains_batch_x). */
+static void fdyn_x(int X, const phys_t* P, const double* x, const double* R, const double* u, double* xdot);
 static void fdyn(const phys_t* P, const double* x, const double* R, const double* u, double* xdot) {
+  fdyn_x(16, P, x, R, u, xdot);
+}
+static void fdyn_x(int X, const phys_t* P, const double* x, const double* R, const double* u, double* xdot) {
   const double eX[3] = {1, 0, 0}, eY[3] = {0, 1, 0}, eZ[3] = {0, 0, 1};
   double v[3] = {x[3], x[4], x[5]}, r[3] = {x[6], x[7], x[8]}, w[3] = {x[9], x[10], x[11]};
-  double F[4] = {x[12], x[13], x[14], x[15]};
+  double F[4];
+  for (int i = 0; i < 4; ++i) F[i] = X == 16 ? x[12 + i] : u[i];
   double t3[3], t3b[3], S[9], E[9], RE[9];
   /* p_dot = v */
   xdot[0] = v[0]; xdot[1] = v[1]; xdot[2] = v[2];
@@ -277,31 +284,32 @@ static void fdyn(const phys_t* P, const double* x, const double* R, const double
   mm(3, 3, 1, P->invInertia, t3b, t3);
   xdot[9] = t3[0]; xdot[10] = t3[1]; xdot[11] = t3[2];
   /* f_dot = latency*(u - F) */
-  for (int i = 0; i < 4; ++i) xdot[12 + i] = (u[i] - F[i]) * P->thrust_latency;
+  if (X == 16)
+    for (int i = 0; i < 4; ++i) xdot[12 + i] = (u[i] - F[i]) * P->thrust_latency;
 }
 
 /* linearizeDiscretize (LQRO:456-471) with Jacobian_fx/fu (LQRO:421-441) */
-static void linearize(const phys_t* P, const double* x, const double* R, const double* u,
+static void linearize(int X, const phys_t* P, const double* x, const double* R, const double* u,
                       double* A, double* B, double* c) {
-  enum { X = 16, U = 4 };
-  double F[X * X], G[X * U], xdot[X], fr[X], fl[X];
-  double xr[X], xl[X], ur[U], ul[U];
-  memcpy(xr, x, sizeof xr); memcpy(xl, x, sizeof xl);
+  enum { XM = 16, U = 4 };
+  double F[XM * XM], G[XM * U], xdot[XM], fr[XM], fl[XM];
+  double xr[XM], xl[XM], ur[U], ul[U];
+  memcpy(xr, x, sizeof(double) * X); memcpy(xl, x, sizeof(double) * X);
   for (int i = 0; i < X; ++i) {
     xr[i] += P->jStep; xl[i] -= P->jStep;
-    fdyn(P, xr, R, u, fr); fdyn(P, xl, R, u, fl);
+    fdyn_x(X, P, xr, R, u, fr); fdyn_x(X, P, xl, R, u, fl);
     for (int k = 0; k < X; ++k) F[k * X + i] = (fr[k] - fl[k]) / (2 * P->jStep);
     xr[i] = xl[i] = x[i];
   }
   memcpy(ur, u, sizeof ur); memcpy(ul, u, sizeof ul);
   for (int i = 0; i < U; ++i) {
     ur[i] += P->jStep; ul[i] -= P->jStep;
-    fdyn(P, x, R, ur, fr); fdyn(P, x, R, ul, fl);
+    fdyn_x(X, P, x, R, ur, fr); fdyn_x(X, P, x, R, ul, fl);
     for (int k = 0; k < X; ++k) G[k * U + i] = (fr[k] - fl[k]) / (2 * P->jStep);
     ur[i] = ul[i] = u[i];
   }
-  fdyn(P, x, R, u, xdot);
-  double dtF[X * X], hF[X * X], E2[X * X], Int[X * X], I[X * X];
+  fdyn_x(X, P, x, R, u, xdot);
+  double dtF[XM * XM], hF[XM * XM], E2[XM * XM], Int[XM * XM], I[XM * XM];
   mscale(X * X, F, P->dt, dtF);
   mexp(X, dtF, A);
   mscale(X * X, F, 0.5 * P->dt, hF);
@@ -317,33 +325,42 @@ static void linearize(const phys_t* P, const double* x, const double* R, const d
 
 int orc_synthesize(const lqro_model* m, double* Aout, double* Bout, double* cout,
                    double* Lout, double* Eout, double* Lhout, double* Ehout) {
-  enum { X = 16, U = 4, V = 3 };
+  return orc_synthesize_x(m, 16, Aout, Bout, cout, Lout, Eout, Lhout, Ehout);
+}
+
+/* controlMatrices (LQRO:520-582) for X = 16, or X = 12 (the reduced model of
+ * fdyn_x).  Arrays are sized for X = 16 and used with stride X. */
+int orc_synthesize_x(const lqro_model* m, int X, double* Aout, double* Bout, double* cout,
+                     double* Lout, double* Eout, double* Lhout, double* Ehout) {
+  enum { XM = 16, U = 4, V = 3 };
+  if (X != 16 && X != 12) return -1;
   phys_t P; phys_init(m, &P);
   double nominal = P.gravity * P.mass / 4;   /* LQRO:188 */
   double uGoal[U] = {nominal, nominal, nominal, nominal};
-  double xHat[X] = {0}; xHat[12] = xHat[13] = xHat[14] = xHat[15] = nominal;
+  double xHat[XM] = {0};
+  for (int k = 12; k < X; ++k) xHat[k] = nominal;
   double RHat[9]; meye(3, RHat);
-  double A[X * X], B[X * U], c[X];
-  linearize(&P, xHat, RHat, uGoal, A, B, c);
+  double A[XM * XM], B[XM * U], c[XM];
+  linearize(X, &P, xHat, RHat, uGoal, A, B, c);
 
-  double Vm[V * X] = {0}; Vm[0 * X + 3] = Vm[1 * X + 4] = Vm[2 * X + 5] = 1;
-  double Pm[V * X] = {0}; Pm[0 * X + 0] = Pm[1 * X + 1] = Pm[2 * X + 2] = 1;
+  double Vm[V * XM] = {0}; Vm[0 * X + 3] = Vm[1 * X + 4] = Vm[2 * X + 5] = 1;
+  double Pm[V * XM] = {0}; Pm[0 * X + 0] = Pm[1 * X + 1] = Pm[2 * X + 2] = 1;
   double Qv[9], Qp[9], R[16], I3[9], I4[16];
   meye(3, I3); meye(4, I4);
   mscale(9, I3, m->qv, Qv); mscale(9, I3, m->qp, Qp); mscale(16, I4, m->r, R); /* 5*identity */
-  double Qx[X * X] = {0};
+  double Qx[XM * XM] = {0};
 
-  double Vt[X * V], At[X * X], Bt[U * X];
+  double Vt[XM * V], At[XM * XM], Bt[U * XM];
   mt(V, X, Vm, Vt); mt(X, X, A, At); mt(X, U, B, Bt);
-  double VtQv[X * V], VtQvV[X * X], nVt[X * V], nVtQv[X * V];
+  double VtQv[XM * V], VtQvV[XM * XM], nVt[XM * V], nVtQv[XM * V];
   mm(X, V, V, Vt, Qv, VtQv); mm(X, V, X, VtQv, Vm, VtQvV);
   mneg(X * V, Vt, nVt); mm(X, V, V, nVt, Qv, nVtQv);
 
-  double S[X * X], T[X * V];
-  memcpy(S, VtQvV, sizeof S);   /* S = ~V*Qv*V */
-  memcpy(T, nVtQv, sizeof T);   /* T = -~V*Qv  */
-  double AtS[X * X], AtSB[X * U], BtS[U * X], BtSB[U * U], RB[U * U], Ri[U * U];
-  double t1[X * U], t2[X * X], t3[X * V], AtT[X * V], BtSA[U * X], tmp[X * X];
+  double S[XM * XM], T[XM * V];
+  memcpy(S, VtQvV, sizeof(double) * X * X);   /* S = ~V*Qv*V */
+  memcpy(T, nVtQv, sizeof(double) * X * V);   /* T = -~V*Qv  */
+  double AtS[XM * XM], AtSB[XM * U], BtS[U * XM], BtSB[U * U], RB[U * U], Ri[U * U];
+  double t1[XM * U], t2[XM * XM], t3[XM * V], AtT[XM * V], BtSA[U * XM], tmp[XM * XM];
   for (int it = 0; it < 300; ++it) {
     /* common: ~A*S*B*!(R + ~B*S*B) with the OLD S */
     mm(X, X, X, At, S, AtS); mm(X, X, U, AtS, B, AtSB);
@@ -351,21 +368,21 @@ int orc_synthesize(const lqro_model* m, double* Aout, double* Bout, double* cout
     madd(U * U, R, BtSB, RB); minv(U, RB, Ri);
     mm(X, U, U, AtSB, Ri, t1);
     /* T = -~V*Qv + ~A*T - ~A*S*B*!(..)*~B*T */
-    double t1Bt[X * X];
+    double t1Bt[XM * XM];
     mm(X, U, X, t1, Bt, t1Bt); mm(X, X, V, t1Bt, T, t3);
     mm(X, X, V, At, T, AtT);
-    double Tn[X * V];
+    double Tn[XM * V];
     madd(X * V, nVtQv, AtT, Tn); msub(X * V, Tn, t3, Tn);
     /* S = ~V*Qv*V + Qx + ~A*S*A - ~A*S*B*!(..)*(~B*S*A) */
     mm(U, X, X, BtS, A, BtSA);
     mm(X, U, X, t1, BtSA, t2);
-    double Sn[X * X];
+    double Sn[XM * XM];
     madd(X * X, VtQvV, Qx, Sn); mm(X, X, X, AtS, A, tmp); madd(X * X, Sn, tmp, Sn);
     msub(X * X, Sn, t2, Sn);
-    memcpy(T, Tn, sizeof T); memcpy(S, Sn, sizeof S);
+    memcpy(T, Tn, sizeof(double) * X * V); memcpy(S, Sn, sizeof(double) * X * X);
   }
   /* L = -!(R + ~B*S*B)*~B*S*A ; E = -!(R + ~B*S*B)*~B*T  (LQRO:555-556) */
-  double L[U * X], E[U * V], nRi[U * U], tUX[U * X], tUX2[U * X];
+  double L[U * XM], E[U * V], nRi[U * U], tUX[U * XM], tUX2[U * XM];
   mm(U, X, X, Bt, S, BtS); mm(U, X, U, BtS, B, BtSB);
   madd(U * U, R, BtSB, RB); minv(U, RB, Ri); mneg(U * U, Ri, nRi);
   mm(U, U, X, nRi, Bt, tUX); mm(U, X, X, tUX, S, tUX2); mm(U, X, X, tUX2, A, L);
@@ -373,27 +390,27 @@ int orc_synthesize(const lqro_model* m, double* Aout, double* Bout, double* cout
 
   /* position LQR (LQRO:559-581) */
   const double w = m->pos_weight;
-  double Pt[X * V], Lt[X * U], Et[V * U];
+  double Pt[XM * V], Lt[XM * U], Et[V * U];
   mt(V, X, Pm, Pt); mt(U, X, L, Lt); mt(U, V, E, Et);
-  double Qpt[X * X], a1[X * V], a2[X * X], wLt[X * U], wLtR[X * U];
+  double Qpt[XM * XM], a1[XM * V], a2[XM * XM], wLt[XM * U], wLtR[XM * U];
   mm(X, V, V, Pt, Qp, a1); mm(X, V, X, a1, Pm, a2);
   mscale(X * U, Lt, w, wLt); mm(X, U, U, wLt, R, wLtR); mm(X, U, X, wLtR, L, tmp);
   madd(X * X, a2, tmp, Qpt);
-  double wEt[V * U], wEtR[V * U], Rtl[V * V], Ptl[V * X];
+  double wEt[V * U], wEtR[V * U], Rtl[V * V], Ptl[V * XM];
   mscale(V * U, Et, w, wEt); mm(V, U, U, wEt, R, wEtR);
   mm(V, U, V, wEtR, E, Rtl); mm(V, U, X, wEtR, L, Ptl);
-  double Atl[X * X], Btl[X * V], BL[X * X];
+  double Atl[XM * XM], Btl[XM * V], BL[XM * XM];
   mm(X, U, X, B, L, BL); madd(X * X, A, BL, Atl);
   mm(X, U, V, B, E, Btl);
 
-  double St[X * X], Tt[X * V], nPt[X * V], nPtQp[X * V];
-  memcpy(St, Qpt, sizeof St);
+  double St[XM * XM], Tt[XM * V], nPt[XM * V], nPtQp[XM * V];
+  memcpy(St, Qpt, sizeof(double) * X * X);
   mneg(X * V, Pt, nPt); mm(X, V, V, nPt, Qp, nPtQp);
-  memcpy(Tt, nPtQp, sizeof Tt);
-  double Atlt[X * X], Btlt[V * X], Ptlt[X * V];
+  memcpy(Tt, nPtQp, sizeof(double) * X * V);
+  double Atlt[XM * XM], Btlt[V * XM], Ptlt[XM * V];
   mt(X, X, Atl, Atlt); mt(X, V, Btl, Btlt); mt(V, X, Ptl, Ptlt);
-  double AS[X * X], ASB[X * V], BS[V * X], BSB[V * V], RR[V * V], RRi[V * V];
-  double K1[X * V], K2[X * V], BSA[V * X], PB[V * X];
+  double AS[XM * XM], ASB[XM * V], BS[V * XM], BSB[V * V], RR[V * V], RRi[V * V];
+  double K1[XM * V], K2[XM * V], BSA[V * XM], PB[V * XM];
   for (int it = 0; it < 300; ++it) {
     mm(X, X, X, Atlt, St, AS); mm(X, X, V, AS, Btl, ASB);
     madd(X * V, Ptlt, ASB, K1);                          /* (~Ptilde + ~At*St*Bt) */
@@ -401,31 +418,31 @@ int orc_synthesize(const lqro_model* m, double* Aout, double* Bout, double* cout
     madd(V * V, Rtl, BSB, RR); minv(V, RR, RRi);
     mm(X, V, V, K1, RRi, K2);                            /* (..)*!(..) */
     /* Ttilde = -~P*Qp + ~At*Tt - K2*~Bt*Tt */
-    double K2Bt[X * X], c3[X * V], AT[X * V], Ttn[X * V];
+    double K2Bt[XM * XM], c3[XM * V], AT[XM * V], Ttn[XM * V];
     mm(X, V, X, K2, Btlt, K2Bt); mm(X, X, V, K2Bt, Tt, c3);
     mm(X, X, V, Atlt, Tt, AT);
     madd(X * V, nPtQp, AT, Ttn); msub(X * V, Ttn, c3, Ttn);
     /* Stilde = Qpt + ~At*St*At - K2*(Ptilde + ~Bt*St*At) */
-    double Stn[X * X], c4[X * X];
+    double Stn[XM * XM], c4[XM * XM];
     mm(V, X, X, BS, Atl, BSA); madd(V * X, Ptl, BSA, PB);
     mm(X, V, X, K2, PB, c4);
     mm(X, X, X, AS, Atl, tmp); madd(X * X, Qpt, tmp, Stn); msub(X * X, Stn, c4, Stn);
-    memcpy(Tt, Ttn, sizeof Tt); memcpy(St, Stn, sizeof St);
+    memcpy(Tt, Ttn, sizeof(double) * X * V); memcpy(St, Stn, sizeof(double) * X * X);
   }
-  double Lh[V * X], Eh[V * V], nRRi[V * V], BtT[V * V];
+  double Lh[V * XM], Eh[V * V], nRRi[V * V], BtT[V * V];
   mm(V, X, X, Btlt, St, BS); mm(V, X, V, BS, Btl, BSB);
   madd(V * V, Rtl, BSB, RR); minv(V, RR, RRi); mneg(V * V, RRi, nRRi);
   mm(V, X, X, BS, Atl, BSA); madd(V * X, Ptl, BSA, PB);
   mm(V, V, X, nRRi, PB, Lh);
   mm(V, X, V, Btlt, Tt, BtT); mm(V, V, V, nRRi, BtT, Eh);
 
-  if (Aout) memcpy(Aout, A, sizeof A);
-  if (Bout) memcpy(Bout, B, sizeof B);
-  if (cout) memcpy(cout, c, sizeof c);
-  if (Lout) memcpy(Lout, L, sizeof L);
-  if (Eout) memcpy(Eout, E, sizeof E);
-  if (Lhout) memcpy(Lhout, Lh, sizeof Lh);
-  if (Ehout) memcpy(Ehout, Eh, sizeof Eh);
+  if (Aout) memcpy(Aout, A, sizeof(double) * X * X);
+  if (Bout) memcpy(Bout, B, sizeof(double) * X * U);
+  if (cout) memcpy(cout, c, sizeof(double) * X);
+  if (Lout) memcpy(Lout, L, sizeof(double) * U * X);
+  if (Eout) memcpy(Eout, E, sizeof(double) * U * V);
+  if (Lhout) memcpy(Lhout, Lh, sizeof(double) * V * X);
+  if (Ehout) memcpy(Ehout, Eh, sizeof(double) * V * V);
   return 0;
 }
 

@@ -88,14 +88,18 @@ class Model(C.Structure):
         "j_step", "qv", "qp", "r", "pos_weight")]
 
 
-def synthesize(model: Model | None = None) -> dict:
+def synthesize(model: Model | None = None, x_dim: int = 16) -> dict:
+    """controlMatrices (LQRO:520-582); x_dim 12 = config 5's reduced model."""
     m = model
     if m is None:
         m = Model()
         lib().orc_model_default(C.byref(m))
-    out = dict(A=np.zeros((16, 16)), B=np.zeros((16, 4)), c=np.zeros(16), L=np.zeros((4, 16)),
-               E=np.zeros((4, 3)), Lh=np.zeros((3, 16)), Eh=np.zeros((3, 3)))
-    lib().orc_synthesize(C.byref(m), *[_p(out[k]) for k in ("A", "B", "c", "L", "E", "Lh", "Eh")])
+    X = x_dim
+    out = dict(A=np.zeros((X, X)), B=np.zeros((X, 4)), c=np.zeros(X), L=np.zeros((4, X)),
+               E=np.zeros((4, 3)), Lh=np.zeros((3, X)), Eh=np.zeros((3, 3)))
+    rc = lib().orc_synthesize_x(C.byref(m), X, *[_p(out[k]) for k in ("A", "B", "c", "L", "E", "Lh", "Eh")])
+    if rc != 0:
+        raise ValueError(f"orc_synthesize_x: x_dim {X}")
     return out
 
 

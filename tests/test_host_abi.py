@@ -60,6 +60,25 @@ def test_host_gains_bit_exact(lqro_mod):
         assert np.array_equal(got[k].view(np.uint64), ref[k].view(np.uint64)), k
 
 
+
+def test_host_reduced_model_gains_bit_exact(lqro_mod, oracle):
+    """lqro_synthesize_gains_x(x_dim = 12), config 5's reduced model (host
+    C++), == the oracle's restatement, for the default and a perturbed model;
+    x_dim = 16 is the reference's synthesis."""
+    for m in (lqro_mod.default_model(), lqro_mod.perturbed_models(3)[2]):
+        om = oracle.Model(*[getattr(m, f) for f, _ in m._fields_])
+        for X in (12, 16):
+            got = lqro_mod.synthesize_gains(m, x_dim=X)
+            ref = oracle.synthesize(om, x_dim=X)
+            for k in ref:
+                assert got[k].shape == ref[k].shape
+                assert np.array_equal(got[k].view(np.uint64), ref[k].view(np.uint64)), (X, k)
+    with pytest.raises(lqro_mod.LqroError):
+        lqro_mod.synthesize_gains(x_dim=13)
+    with pytest.raises(ValueError):
+        oracle.synthesize(x_dim=13)
+
+
 @pytest.mark.parametrize("np_", [100, 50])
 def test_host_sphere_bit_exact(lqro_mod, np_):
     ref = np.load(os.path.join(GOLDEN, "gains.npz"))[f"sphere{np_}"]
