@@ -31,6 +31,10 @@
 namespace lqro {
 
 enum : int { kSliceOut = 0, kSliceIn = 1, kSliceMixed = 2 };
+// k_pair launch kinds: the row launch (rows off a queue, row tables staged in
+// LDS), the hot launch with shared tables (staged once), the hot launch with
+// per-agent tables (read from global memory, pairs of any row)
+enum : int { kRowLaunch = 0, kHotShared = 1, kHotPerAgent = 2 };
 constexpr int kMaxPW = 4;
 constexpr int kMaxKS = 4;   // H <= 64 kMaxKS = 256 (per-lane slice slots)
 #ifndef LQRO_PAIR_LB
@@ -41,6 +45,7 @@ struct PairArgs {
   int N, H, NP, PW, min_reach;
   int row_begin, nrows, npr;          // npr = pairs per row = N-1
   int waves;
+  int max_waves;                      // waves of a workgroup that take pairs (k_side's LDS fits fewer)
   int* row_counter;                   // persistent row queue (zeroed per step)
   int row_split;                      // pair ranges per row
   int per_agent;
@@ -74,7 +79,8 @@ struct PairArgs {
 
 struct BlockTabs {
   const double* T;
-  const double* N;
+  const double* N;    // H x 3 rows of pitch `pitch` (X + 1 in LDS, X in global memory)
+  int pitch;
   const double* S;    // SoA: x[NP], y[NP], z[NP]
   const double* R;
   const double* TF;
@@ -344,7 +350,7 @@ __device__ inline int reach_rank(const PairArgs& P, const WaveTabs& W, int lane,
 
 // One workgroup's share of a k_pair launch (LDS at `lds`, laid out per
 // PairArgs; waves = blockDim.x / 64 <= P.waves).  Also the tail of k_side.
-template <int X, bool RECS, bool HOT>
+template <int X, bool RECS, int HOT>
 __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
 #ifdef LQRO_PAIR_PROFILE
   unsigned long long pp[16] = {0};
@@ -362,7 +368,7 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
   double* sTF = lds + P.lds_TF;
   unsigned long long* sH = reinterpret_cast<unsigned long long*>(lds + P.lds_H);
   BlockTabs B;
-  B.T = sT; B.N = sN; B.S = sS; B.R = sR; B.TF = sTF; B.shash = sH;
+  B.T = sT; B.N = sN; B.S = sS; B.R = sR; B.TF = sTF; B.shash = sH; B.pitch = XP;
   WaveTabs W;
   {
     double* w = lds + P.lds_wave + (size_t)wave * P.wave_doubles;
@@ -418,14 +424,15 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
 
     // 1. per slice: Translate (exact), centre, class       (lanes <-> k)
     for (int k = lane; k < H; k += 64) {
-      const double* nc = B.N + (size_t)k * 3 * XP;
+      const int np = HOT == kHotPerAgent ? B.pitch : XP;
+      const double* nc = B.N + (size_t)k * 3 * np;
       double t0 = 0.0, t1 = 0.0, t2 = 0.0;
 #pragma unroll
       for (int c = 0; c < X; ++c) t0 += nc[c] * d[c];
 #pragma unroll
-      for (int c = 0; c < X; ++c) t1 += nc[XP + c] * d[c];
+      for (int c = 0; c < X; ++c) t1 += nc[np + c] * d[c];
 #pragma unroll
-      for (int c = 0; c < X; ++c) t2 += nc[2 * XP + c] * d[c];
+      for (int c = 0; c < X; ++c) t2 += nc[2 * np + c] * d[c];
       W.tr[3 * k] = t0; W.tr[3 * k + 1] = t1; W.tr[3 * k + 2] = t2;
       const double* Tk = B.T + 9 * k;
       const double c0 = Tk[0] * t0 + Tk[1] * t1 + Tk[2] * t2;
@@ -594,15 +601,17 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
   // inside-hull, one per wave, so that their hulls can run on side-stream
   // k_hull workers while the row launch sweeps the rest.  Scheduling only:
   // every pair is computed by the same code.
-  if constexpr (HOT) {
-    for (int q = threadIdx.x; q < H * 9; q += blockDim.x) sT[q] = P.T[q];
-    for (int q = threadIdx.x; q < H * 3 * X; q += blockDim.x) sN[(q / X) * XP + (q % X)] = P.NCF[q];
-    for (int q = threadIdx.x; q < NP * 3; q += blockDim.x) sS[(q % 3) * NP + q / 3] = P.S[q];
-    for (int q = threadIdx.x; q < H; q += blockDim.x) {
-      sR[q] = P.R[q];
-      sTF[q] = P.TF[q];
-      sH[q] = P.shash[q];
+  if constexpr (HOT != kRowLaunch) {
+    if constexpr (HOT == kHotShared) {
+      for (int q = threadIdx.x; q < H * 9; q += blockDim.x) sT[q] = P.T[q];
+      for (int q = threadIdx.x; q < H * 3 * X; q += blockDim.x) sN[(q / X) * XP + (q % X)] = P.NCF[q];
+      for (int q = threadIdx.x; q < H; q += blockDim.x) {
+        sR[q] = P.R[q];
+        sTF[q] = P.TF[q];
+      }
     }
+    for (int q = threadIdx.x; q < NP * 3; q += blockDim.x) sS[(q % 3) * NP + q / 3] = P.S[q];
+    for (int q = threadIdx.x; q < H; q += blockDim.x) sH[q] = P.shash[q];
     __syncthreads();
     const int nhot = min(*P.hot_count, P.hot_cap);
     for (;;) {
@@ -612,6 +621,16 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
       if (h >= nhot) break;
       const int slot = P.hot_list[h];
       const int lrow = slot / P.npr;
+      if constexpr (HOT == kHotPerAgent) {
+        // per-agent gains: the row agent's tables straight from global memory
+        // (the workgroup's waves work on pairs of different rows)
+        const size_t i = (size_t)(P.row_begin + lrow);
+        B.T = P.T + i * H * 9;
+        B.N = P.NCF + i * H * 3 * X;
+        B.pitch = X;
+        B.R = P.R + i * H;
+        B.TF = P.TF + i * H;
+      }
       do_pair(P.row_begin + lrow, lrow, slot - lrow * P.npr);
     }
   } else {
@@ -653,6 +672,7 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
     }
     PSTAMP(0);
   for (;;) {
+    if (wave >= P.max_waves) break;    // k_side: no LDS region for this wave
     int jj = 0;
     if (lane == 0) jj = atomicAdd(&s_next, 1);
     jj = __shfl(jj, 0);
@@ -680,7 +700,7 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
 // without the record code and its registers.  HOT: the hot launch (P.hot_only)
 // and the row launch are separate instantiations, so neither carries the
 // other's loop around do_pair.
-template <int X, bool RECS, bool HOT>
+template <int X, bool RECS, int HOT>
 __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
   extern __shared__ double lds[];
   pair_block<X, RECS, HOT>(P, lds);

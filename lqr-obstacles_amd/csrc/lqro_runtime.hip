@@ -51,17 +51,24 @@ __global__ void __launch_bounds__(HULL_CTHREADS) k_side(HullArgs A, PairArgs P) 
   __shared__ HullMemC M;
   hull_body_mw<HULL_CWAVES>(A, M, L);
   __syncthreads();
-  if (P.nrows > 0) pair_block<X, RECS, false>(P, reinterpret_cast<double*>(&M));
+  if (P.nrows > 0) pair_block<X, RECS, kRowLaunch>(P, reinterpret_cast<double*>(&M));
 }
 
 // k_pair / k_side for the context's state width and record mode
 template <int X>
 static void launch_pair_x(dim3 grid, dim3 block, size_t lds, hipStream_t s, const PairArgs& P) {
-  const bool r = P.recs != nullptr, h = P.hot_only != 0;
-  if (r && h) hipLaunchKernelGGL((k_pair<X, true, true>), grid, block, lds, s, P);
-  else if (r) hipLaunchKernelGGL((k_pair<X, true, false>), grid, block, lds, s, P);
-  else if (h) hipLaunchKernelGGL((k_pair<X, false, true>), grid, block, lds, s, P);
-  else hipLaunchKernelGGL((k_pair<X, false, false>), grid, block, lds, s, P);
+  const bool r = P.recs != nullptr;
+  const int h = P.hot_only == 0 ? kRowLaunch : (P.per_agent ? kHotPerAgent : kHotShared);
+  if (h == kRowLaunch) {
+    if (r) hipLaunchKernelGGL((k_pair<X, true, kRowLaunch>), grid, block, lds, s, P);
+    else hipLaunchKernelGGL((k_pair<X, false, kRowLaunch>), grid, block, lds, s, P);
+  } else if (h == kHotShared) {
+    if (r) hipLaunchKernelGGL((k_pair<X, true, kHotShared>), grid, block, lds, s, P);
+    else hipLaunchKernelGGL((k_pair<X, false, kHotShared>), grid, block, lds, s, P);
+  } else {
+    if (r) hipLaunchKernelGGL((k_pair<X, true, kHotPerAgent>), grid, block, lds, s, P);
+    else hipLaunchKernelGGL((k_pair<X, false, kHotPerAgent>), grid, block, lds, s, P);
+  }
 }
 static void launch_pair(int x_dim, dim3 grid, dim3 block, size_t lds, hipStream_t s, const PairArgs& P) {
   if (x_dim == 16) launch_pair_x<16>(grid, block, lds, s, P);
@@ -595,6 +602,7 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
     return LQRO_E_ARG;
   }
   P.waves = waves;
+  P.max_waves = waves;
   off += waves * P.wave_doubles;
   c->lds_bytes = off * 8;
   int rc = ctx_alloc(c);
@@ -631,11 +639,13 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
     lqro_destroy(c);
     return LQRO_E_HIP;
   }
-  const void* pair_kernels[8] = {
-      (const void*)k_pair<16, false, false>, (const void*)k_pair<16, true, false>,
-      (const void*)k_pair<12, false, false>, (const void*)k_pair<12, true, false>,
-      (const void*)k_pair<16, false, true>,  (const void*)k_pair<16, true, true>,
-      (const void*)k_pair<12, false, true>,  (const void*)k_pair<12, true, true>};
+  const void* pair_kernels[12] = {
+      (const void*)k_pair<16, false, kRowLaunch>,   (const void*)k_pair<16, true, kRowLaunch>,
+      (const void*)k_pair<12, false, kRowLaunch>,   (const void*)k_pair<12, true, kRowLaunch>,
+      (const void*)k_pair<16, false, kHotShared>,   (const void*)k_pair<16, true, kHotShared>,
+      (const void*)k_pair<12, false, kHotShared>,   (const void*)k_pair<12, true, kHotShared>,
+      (const void*)k_pair<16, false, kHotPerAgent>, (const void*)k_pair<16, true, kHotPerAgent>,
+      (const void*)k_pair<12, false, kHotPerAgent>, (const void*)k_pair<12, true, kHotPerAgent>};
   bool attr_ok = true;
   for (const void* k : pair_kernels)
     attr_ok = attr_ok && hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, c->lds_bytes) == hipSuccess;
@@ -736,9 +746,12 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   // seg_put: 15-bit count, 17-bit offset / 4 into HULL_SBMULT * H*NP entries)
   const bool lds_ok = (size_t)g.horizon * g.n_points <= kHullLdsMaxHNP;
   const long slots = (long)c->nrows * npr;
-  const bool side_fits = (size_t)(P.lds_wave + HULL_CWAVES * P.wave_doubles) * 8 <= sizeof(HullMemC) &&
-                         P.waves >= HULL_CWAVES;
-  const bool hot = c->hot_on && !c->per_agent && lds_ok && side_fits && c->n_cu >= 64 && slots >= 65536 &&
+  // k_side sweeps rows in the hull's LDS (HullMemC) after its hulls: as many
+  // of its waves take pairs as per-wave regions fit beside the row tables
+  const long side_room = (long)(sizeof(HullMemC) / 8) - P.lds_wave;
+  const int side_waves = side_room > 0 ? (int)std::min<long>(std::min(HULL_CWAVES, P.waves),
+                                                              side_room / P.wave_doubles) : 0;
+  const bool hot = c->hot_on && lds_ok && side_waves >= 1 && c->n_cu >= 64 && slots >= 65536 &&
                    c->nbr_k <= 0;
   const int nwait = hot ? c->side_cus : 0;
   P.row_split = std::max(1, std::min(16, (2 * c->n_cu + c->nrows - 1) / c->nrows));
@@ -793,6 +806,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
     launch_pair(g.x_dim, dim3(nwait), dim3(P.waves * 64), c->lds_bytes, c->side, Ph);
     HIPCHK(hipGetLastError());
     PairArgs Pt = P;
+    Pt.max_waves = side_waves;
     if (nside == 0) Pt.nrows = 0;
     launch_side(g.x_dim, dim3(nwait), dim3(HULL_CTHREADS), c->side, Hh, Pt);
     HIPCHK(hipGetLastError());

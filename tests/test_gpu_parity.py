@@ -139,12 +139,22 @@ def test_c3_full_step(lqro_mod, oracle, gains):
     np.testing.assert_allclose(newv, rv, rtol=1e-5, atol=1e-6)
 
 
-def test_overlap_schedule_identical(lqro_mod, gains, monkeypatch):
+@pytest.mark.parametrize("kind", ["shared", "per_agent", "per_agent_x12_h200"])
+def test_overlap_schedule_identical(lqro_mod, gains, monkeypatch, kind):
     """The step's schedule (k_prio hot list, side-stream hulls, side width,
     hot radius) changes only the order of work: every record and every new
-    velocity is bit-identical across schedules and repeated steps."""
-    N, H, NP = 512, 100, 100          # 261,632 pairs: the overlap path is taken
-    x, vg = lqro_mod.synthetic_swarm(N, seed=3)
+    velocity is bit-identical across schedules and repeated steps — with
+    shared gains (hot pairs on staged tables), per-agent gains (hot pairs read
+    their row's tables from global memory) and C5's shape (X = 12, H = 200:
+    k_side sweeps rows with the waves whose LDS regions fit)."""
+    N, H, NP, X = 512, 100, 100, 16   # 261,632 pairs: the overlap path is taken
+    per_agent = kind != "shared"
+    if kind == "per_agent_x12_h200":
+        H, X = 200, 12
+    x, vg = lqro_mod.synthetic_swarm(N, seed=3, x_dim=X)
+    if per_agent:
+        g = lqro_mod.synthesize_gains_batch(lqro_mod.perturbed_models(N, seed=17), x_dim=X)
+        gains = dict(A=g["A"][0], B=g["B"][0], L=g["L"], E=g["E"])
     outs = []
     for env in ({"LQRO_HOT": "0"}, {"LQRO_HOT": "1"}, {"LQRO_HOT": "1", "LQRO_SIDE_HULL_CUS": "32"},
                 {"LQRO_HOT": "1", "LQRO_HOT_R": "0.5"}):
@@ -152,8 +162,8 @@ def test_overlap_schedule_identical(lqro_mod, gains, monkeypatch):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
-        ctx = lqro_mod.Context(lqro_mod.config(N, H, NP, flags=lqro_mod.LQRO_FLAG_RECORDS))
-        ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
+        ctx = lqro_mod.Context(lqro_mod.config(N, H, NP, x_dim=X, flags=lqro_mod.LQRO_FLAG_RECORDS))
+        ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"], per_agent=per_agent)
         v1 = ctx.step(x, vg)
         r1 = ctx.records()
         v2 = ctx.step(x, vg)
