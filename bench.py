@@ -147,6 +147,59 @@ def closed_loop(lqro, torch, dev, x, vg, gains, reps, world=1, dist=None, rank=0
                     "dynamics_plus_gather_ms from events on the launch stream"}
 
 
+def config_runs(lqro, torch, dev, local, world, rank, dist, steps):
+    """BASELINE configs 4 and 5 beside the headline (never in `value`):
+    strong scaling — the whole swarm's rows sharded over the ranks, the
+    per-step exchange as in the headline; max over ranks of the time for
+    `steps` steps.  C4: 4096 quadrotors, H = 100, shared gains.  C5: 16384
+    agents of the 12-DoF reduced model, per-agent gains of ±1 %-perturbed
+    models (synthesised on the GPU), H = 200."""
+    out = {}
+    for name, N, H, X in (("c4", 4096, 100, 16), ("c5", 16384, 200, 12)):
+        rb, re = lqro.row_shard(N, rank, world)
+        x, vg = lqro.synthetic_swarm(N, x_dim=X)
+        if name == "c5":
+            g = lqro.synthesize_gains_batch(lqro.perturbed_models(N), device=local, x_dim=X)
+            g0 = lqro.synthesize_gains(x_dim=X)      # the shared linearisation (LQRO:1265-1266)
+            gains, per_agent = dict(A=g0["A"], B=g0["B"], L=g["L"], E=g["E"]), True
+        else:
+            gains, per_agent = lqro.synthesize_gains(), False
+        ctx = lqro.Context(lqro.config(N, H, N_POINTS, x_dim=X, device=local, row_begin=rb, row_end=re))
+        ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"], per_agent=per_agent)
+        d_x = torch.from_numpy(x).to(dev)
+        d_vg = torch.from_numpy(vg).to(dev)
+        d_newv = torch.zeros((N, 3), dtype=torch.float64, device=dev)
+
+        def step():
+            ctx.step_device(d_x.data_ptr(), d_vg.data_ptr(), d_newv.data_ptr(), 0)
+            if world > 1:
+                lqro.allgather_rows(dist, d_newv, rank, world)
+        step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        st = ctx.stats()
+        ctx.close()
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        out[name] = {"n_agents": N, "horizon": H, "x_dim": X, "per_agent_gains": per_agent,
+                     "pairs_per_step": N * (N - 1), "steps": steps, "ms_per_step": el / steps * 1e3,
+                     "evals_per_s": N * (N - 1) * steps / el, "scaling": "strong",
+                     "rank0_inside_hull": st["inside"], "rank0_hull_failures": st["hull_fail"]}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -156,6 +209,7 @@ def main():
     ap.add_argument("--agents", type=int, default=0,
                     help="swarm size (default: round(1024 sqrt(world)), C3's pairs per GPU)")
     ap.add_argument("--no-roofline-probe", action="store_true")
+    ap.add_argument("--no-configs", action="store_true", help="skip the C4 / C5 strong-scaling runs")
     args = ap.parse_args()
 
     import torch
@@ -304,6 +358,8 @@ def main():
         "inside_hull_pairs_per_step": st["inside"],
         "hull_failures": st["hull_fail"],
     }
+    if not args.no_configs:
+        out["configs"] = config_runs(lqro, torch, dev, local, world, rank, dist, 2)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(x, vg, gains)
         out["cpu_baseline"] = cb

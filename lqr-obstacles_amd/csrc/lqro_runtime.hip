@@ -377,6 +377,7 @@ struct lqro_ctx {
   int nbr_k, nbr_cap;         // k; rows x nbr_cap ints allocated
   int hot_cap;
   int hot_on;                // LQRO_HOT (default 1)
+  int hull_big_only;         // LQRO_HULL_BIG: skip the LDS hull (A/B)
   double hot_t, hot_r;       // k_prio horizon (s) and radius (m): LQRO_HOT_T, LQRO_HOT_R
   int hull_big_blocks;
   int n_cu;
@@ -524,7 +525,7 @@ static int ctx_alloc(lqro_ctx* c) {
   HIPCHK(hipMalloc(&c->d_hvpid, sizeof(int) * HULL_VG_STRIDE * (size_t)c->hull_blocks));
   HIPCHK(hipMalloc(&c->d_hstack, sizeof(int) * HULL_STKMULT * H * NP * (size_t)c->hull_blocks));
   HIPCHK(hipMalloc(&c->d_hfaces, sizeof(HullPt) * HULL_SBMULT * H * NP * (size_t)c->hull_blocks));
-  c->hull_big_blocks = 64;
+  c->hull_big_blocks = c->n_cu;   // one 1-inserting-wave hull per CU (topology in global memory)
   HIPCHK(hipMalloc(&c->d_hbig, sizeof(HullMemBig) * (size_t)c->hull_big_blocks));
   HIPCHK(hipMalloc(&c->d_hwide, sizeof(HullWide) * HULL_CWAVES * (size_t)c->hull_blocks));
   HIPCHK(hipMalloc(&c->d_hbag, sizeof(int) * HULL_BAGCAP * (size_t)c->hull_blocks));
@@ -563,6 +564,8 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
     c->side_cus = e ? atoi(e) : (3 * c->n_cu) / 8;
     if (c->side_cus < 0) c->side_cus = 0;
     if (c->side_cus > c->n_cu / 2) c->side_cus = c->n_cu / 2;
+    const char* hb = getenv("LQRO_HULL_BIG");   // every hull job in k_hull_big (A/B runs)
+    c->hull_big_only = hb ? atoi(hb) != 0 : 0;
     const char* h = getenv("LQRO_HOT");
     c->hot_on = h ? atoi(h) != 0 : 1;
     const char* ht = getenv("LQRO_HOT_T");
@@ -744,15 +747,19 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   }
   // the LDS hull variant packs outside-set extents in 32 bits (lqro_hull.hpp
   // seg_put: 15-bit count, 17-bit offset / 4 into HULL_SBMULT * H*NP entries)
-  const bool lds_ok = (size_t)g.horizon * g.n_points <= kHullLdsMaxHNP;
+  const bool lds_ok = (size_t)g.horizon * g.n_points <= kHullLdsMaxHNP && !c->hull_big_only;
   const long slots = (long)c->nrows * npr;
   // k_side sweeps rows in the hull's LDS (HullMemC) after its hulls: as many
   // of its waves take pairs as per-wave regions fit beside the row tables
   const long side_room = (long)(sizeof(HullMemC) / 8) - P.lds_wave;
   const int side_waves = side_room > 0 ? (int)std::min<long>(std::min(HULL_CWAVES, P.waves),
                                                               side_room / P.wave_doubles) : 0;
-  const bool hot = c->hot_on && lds_ok && side_waves >= 1 && c->n_cu >= 64 && slots >= 65536 &&
-                   c->nbr_k <= 0;
+  // the overlap pays where the hot pairs' hulls fit k_side's LDS topology
+  // (C3: 177 hulls of <= 1,700 vertices); at H*NP > 16,383 (C5: 40 % of the
+  // hulls outgrow its 2,048 vertices and retry in k_hull_big) the plain
+  // schedule is faster (516 vs 1,150 ms per C5 shard step, scripts/c5_once.py)
+  const bool hot = c->hot_on && lds_ok && (size_t)g.horizon * g.n_points <= 16383 && side_waves >= 1 &&
+                   c->n_cu >= 64 && slots >= 65536 && c->nbr_k <= 0;
   const int nwait = hot ? c->side_cus : 0;
   P.row_split = std::max(1, std::min(16, (2 * c->n_cu + c->nrows - 1) / c->nrows));
   const int units = c->nrows * P.row_split;
