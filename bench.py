@@ -82,34 +82,54 @@ def pmc_traffic(kernel: str = "k_pair"):
     return None
 
 
-def cpu_baseline(x, vg, gains, seconds_target=15.0):
-    """The oracle (plain-C restatement, reference operation order) on the
-    host cores: rows of the same C3 workload until ~seconds_target."""
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(x, vg, gains, seconds_target=10.0):
+    """The reference-faithful CPU restatement (oracle/, orc_step_faithful_mt:
+    the reference's per-pair findFG recursion, LQRO:1401-1406, and its two
+    GJK runs per outside pair, LQRO:1410/1414; calibrated against the
+    reference's own code compiled in the build container) on the
+    host cores: rows of the same C3 step, on 1 core and on all the cores this
+    box gives the process (16), each for ~seconds_target."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle  # test infrastructure, used here only as the timed CPU baseline
 
-    threads = int(os.environ.get("LQRO_CPU_THREADS", "16"))
-    threads = max(1, min(threads, os.cpu_count() or 1))
-    T, NCF = pyoracle.tables(gains["A"], gains["B"], gains["L"], gains["E"], HORIZON)
+    cores = max(1, min(int(os.environ.get("LQRO_CPU_THREADS", "16")), os.cpu_count() or 1))
     S = pyoracle.sphere(N_POINTS)
-    # calibrate on 1 row per thread, then scale the sample to the target
-    rows = threads
-    t0 = time.perf_counter()
-    pyoracle.step(T, NCF, S, x, vg, rows=(0, rows), threads=threads, records=False)
-    dt = time.perf_counter() - t0
-    more = int(max(0, min(N_AGENTS - rows, (seconds_target - dt) / max(dt, 1e-9) * rows)))
-    more = (more // threads) * threads
-    if more > 0:
+
+    def rate(threads, row0):
+        # calibrate on one row per thread, then scale the sample to the target
         t0 = time.perf_counter()
-        pyoracle.step(T, NCF, S, x, vg, rows=(rows, rows + more), threads=threads, records=False)
-        dt2 = time.perf_counter() - t0
-        pairs, secs = more * (N_AGENTS - 1), dt2
-        sample = f"rows {rows}..{rows + more - 1} of the C3 step ({pairs} pairs)"
-    else:
-        pairs, secs = rows * (N_AGENTS - 1), dt
-        sample = f"rows 0..{rows - 1} of the C3 step ({pairs} pairs)"
-    return {"value": pairs / secs, "unit": "agent-pair evals/s", "cores": threads,
-            "kind": "port", "sample": sample}
+        pyoracle.step_faithful(gains["A"], gains["B"], gains["L"], gains["E"], S, x, vg, HORIZON,
+                               rows=(row0, row0 + threads), threads=threads, records=False)
+        dt = time.perf_counter() - t0
+        more = int(max(0, min(N_AGENTS - row0 - threads, (seconds_target - dt) / max(dt, 1e-9) * threads)))
+        more = (more // threads) * threads
+        rows, secs = threads, dt
+        if more > 0:
+            t0 = time.perf_counter()
+            pyoracle.step_faithful(gains["A"], gains["B"], gains["L"], gains["E"], S, x, vg, HORIZON,
+                                   rows=(row0 + threads, row0 + threads + more), threads=threads,
+                                   records=False)
+            rows, secs = more, time.perf_counter() - t0
+        return rows * (N_AGENTS - 1) / secs, rows
+
+    one, rows1 = rate(1, 0)
+    allc, rows_all = rate(cores, 64)
+    return {"value": allc, "unit": "agent-pair evals/s", "cores": cores, "kind": "port",
+            "mode": "reference-faithful (per-pair findFG, GJK twice per outside pair; bit-identical results)",
+            "cores_1": one, "cores_all": allc, "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
+            "sample": f"C3 step rows: {rows1} rows on 1 core, {rows_all} rows on {cores} threads "
+                      f"({N_AGENTS - 1} pairs per row)"}
 
 
 def closed_loop(lqro, torch, dev, x, vg, gains, reps, world=1, dist=None, rank=0):

@@ -1183,18 +1183,27 @@ void orc_neighbors(int N, int X, const double* x, int i, double r2, int k, unsig
   free(kd); free(kj);
 }
 
-int orc_step(int N, int X, int H, int NP, int min_reach, double vmax_reach, double vmax_lp,
-             int per_agent, const double* T, const double* NCF, const double* S,
-             const double* x, const double* vgoal, int r0, int r1, double* newv,
-             lqro_pair_record* recs) {
+/* The gains of the reference-faithful mode (orc_step_faithful): A, B shared,
+ * L, E one block or per agent. */
+typedef struct {
+  const double *A, *B, *L, *E;
+} faith_t;
+
+static int step_rows(int N, int X, int H, int NP, int min_reach, double vmax_reach, double vmax_lp,
+                     int per_agent, const double* T, const double* NCF, const double* S,
+                     const double* x, const double* vgoal, int r0, int r1, double* newv,
+                     lqro_pair_record* recs, const faith_t* fa) {
   unsigned char* sel = (unsigned char*)malloc((size_t)N);
   double* pts = (double*)malloc(sizeof(double) * 3 * (size_t)H * (size_t)NP);
   float* planes = (float*)malloc(sizeof(float) * 6 * (size_t)(N > 1 ? N - 1 : 1));
+  double* Tf = fa ? (double*)malloc(sizeof(double) * 9 * (size_t)H) : NULL;
+  double* Nf = fa ? (double*)malloc(sizeof(double) * 3 * (size_t)X * (size_t)H) : NULL;
   lqro_pair_record rec;
   int rc = 0;
   for (int i = r0; i < r1; ++i) {
     const double* Ti = per_agent ? T + (size_t)i * H * 9 : T;
     const double* Ni = per_agent ? NCF + (size_t)i * H * 3 * X : NCF;
+    if (fa) { Ti = Tf; Ni = Nf; }
     int m = 0;
     if (g_nbr_k > 0) orc_neighbors(N, X, x, i, g_nbr_r2, g_nbr_k, sel);
     for (int j = 0; j < N; ++j) {
@@ -1207,9 +1216,27 @@ int orc_step(int N, int X, int H, int NP, int min_reach, double vmax_reach, doub
         }
         continue;
       }
+      if (fa) {
+        /* per pair, as LQRO:1401-1406: F = I, G = 0, then H x (findFG +
+         * createObstacle's Transform = !(C*G), -C*F) — orc_tables is that
+         * recursion (Atilde, Btilde recomputed every k, LQRO:723-732) */
+        const double* Li = fa->L + (per_agent ? (size_t)i * 4 * X : 0);
+        const double* Ei = fa->E + (per_agent ? (size_t)i * 4 * 3 : 0);
+        rc = orc_tables(X, 4, H, fa->A, fa->B, Li, Ei, Tf, Nf);
+        if (rc) goto out;
+      }
       rc = orc_pair(X, H, NP, min_reach, vmax_reach, Ti, Ni, S, x + (size_t)i * X,
                     x + (size_t)j * X, i, j, &rec, NULL, pts);
       if (rc) goto out;
+      if (fa && (rec.flags & LQRO_REC_PLANE) && !(rec.flags & LQRO_REC_INSIDE)) {
+        /* run_gjk (LQRO:1414) repeats pointInHull's GJK (LQRO:1410) */
+        const double* xi = x + (size_t)i * X;
+        const double* xj = x + (size_t)j * X;
+        double vrel[3] = {xi[3] - xj[3], xi[4] - xj[4], xi[5] - xj[5]}, w1[3], w2[3];
+        int it2, sn2, bk2, simp[4];
+        volatile double sq2 = orc_gjk(vrel, rec.n_reach, pts, w1, w2, &it2, &sn2, simp, &bk2);
+        (void)sq2;
+      }
       if (recs) recs[(size_t)(i - r0) * (N - 1) + (j < i ? j : j - 1)] = rec;
       if (rec.flags & LQRO_REC_PLANE) {
         for (int k = 0; k < 3; k++) {
@@ -1222,8 +1249,16 @@ int orc_step(int N, int X, int H, int NP, int min_reach, double vmax_reach, doub
     orc_newv(m, planes, vgoal + (size_t)i * 3, vmax_lp, newv + (size_t)i * 3);  /* LQRO:1435 */
   }
 out:
-  free(pts); free(planes); free(sel);
+  free(pts); free(planes); free(sel); free(Tf); free(Nf);
   return rc;
+}
+
+int orc_step(int N, int X, int H, int NP, int min_reach, double vmax_reach, double vmax_lp,
+             int per_agent, const double* T, const double* NCF, const double* S,
+             const double* x, const double* vgoal, int r0, int r1, double* newv,
+             lqro_pair_record* recs) {
+  return step_rows(N, X, H, NP, min_reach, vmax_reach, vmax_lp, per_agent, T, NCF, S, x, vgoal, r0,
+                   r1, newv, recs, NULL);
 }
 
 typedef struct {
@@ -1233,22 +1268,50 @@ typedef struct {
   double* newv;
   lqro_pair_record* recs;
   int rbase;
+  const faith_t* fa;
 } mt_arg;
 
 static void* mt_body(void* p) {
   mt_arg* a = (mt_arg*)p;
-  a->rc = orc_step(a->N, a->X, a->H, a->NP, a->min_reach, a->vmax_reach, a->vmax_lp, a->per_agent,
-                   a->T, a->NCF, a->S, a->x, a->vgoal, a->r0, a->r1, a->newv,
-                   a->recs ? a->recs + (size_t)(a->r0 - a->rbase) * (a->N - 1) : NULL);
+  a->rc = step_rows(a->N, a->X, a->H, a->NP, a->min_reach, a->vmax_reach, a->vmax_lp, a->per_agent,
+                    a->T, a->NCF, a->S, a->x, a->vgoal, a->r0, a->r1, a->newv,
+                    a->recs ? a->recs + (size_t)(a->r0 - a->rbase) * (a->N - 1) : NULL, a->fa);
   return NULL;
 }
+
+static int step_mt(int N, int X, int H, int NP, int min_reach, double vmax_reach, double vmax_lp,
+                   int per_agent, const double* T, const double* NCF, const double* S,
+                   const double* x, const double* vgoal, int r0, int r1, double* newv,
+                   lqro_pair_record* recs, int threads, const faith_t* fa);
 
 int orc_step_mt(int N, int X, int H, int NP, int min_reach, double vmax_reach, double vmax_lp,
                 int per_agent, const double* T, const double* NCF, const double* S,
                 const double* x, const double* vgoal, int r0, int r1, double* newv,
                 lqro_pair_record* recs, int threads) {
-  if (threads <= 1) return orc_step(N, X, H, NP, min_reach, vmax_reach, vmax_lp, per_agent, T, NCF,
-                                    S, x, vgoal, r0, r1, newv, recs);
+  return step_mt(N, X, H, NP, min_reach, vmax_reach, vmax_lp, per_agent, T, NCF, S, x, vgoal, r0, r1,
+                 newv, recs, threads, NULL);
+}
+
+/* The reference-faithful step: the pair loop with the reference's per-pair
+ * cost structure (findFG recursion per pair, LQRO:1401-1406; GJK twice for
+ * an outside pair, LQRO:1410/1414); results bit-identical to orc_step_mt.
+ * The CPU baseline bench.py times. */
+int orc_step_faithful_mt(int N, int X, int H, int NP, int min_reach, double vmax_reach,
+                         double vmax_lp, int per_agent, const double* A, const double* B,
+                         const double* L, const double* E, const double* S, const double* x,
+                         const double* vgoal, int r0, int r1, double* newv,
+                         lqro_pair_record* recs, int threads) {
+  faith_t fa = {A, B, L, E};
+  return step_mt(N, X, H, NP, min_reach, vmax_reach, vmax_lp, per_agent, NULL, NULL, S, x, vgoal, r0,
+                 r1, newv, recs, threads, &fa);
+}
+
+static int step_mt(int N, int X, int H, int NP, int min_reach, double vmax_reach, double vmax_lp,
+                   int per_agent, const double* T, const double* NCF, const double* S,
+                   const double* x, const double* vgoal, int r0, int r1, double* newv,
+                   lqro_pair_record* recs, int threads, const faith_t* fa) {
+  if (threads <= 1) return step_rows(N, X, H, NP, min_reach, vmax_reach, vmax_lp, per_agent, T, NCF,
+                                     S, x, vgoal, r0, r1, newv, recs, fa);
   pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)threads);
   mt_arg* args = (mt_arg*)malloc(sizeof(mt_arg) * (size_t)threads);
   int rows = r1 - r0, rc = 0;
@@ -1256,7 +1319,7 @@ int orc_step_mt(int N, int X, int H, int NP, int min_reach, double vmax_reach, d
     mt_arg* a = &args[t];
     a->N = N; a->X = X; a->H = H; a->NP = NP; a->min_reach = min_reach; a->per_agent = per_agent;
     a->vmax_reach = vmax_reach; a->vmax_lp = vmax_lp; a->T = T; a->NCF = NCF; a->S = S; a->x = x;
-    a->vgoal = vgoal; a->newv = newv; a->recs = recs; a->rbase = r0;
+    a->vgoal = vgoal; a->newv = newv; a->recs = recs; a->rbase = r0; a->fa = fa;
     a->r0 = r0 + (int)((long long)rows * t / threads);
     a->r1 = r0 + (int)((long long)rows * (t + 1) / threads);
     a->rc = 0;

@@ -89,6 +89,15 @@ int  orc_step_mt(int N, int X, int H, int NP, int min_reach, double vmax_reach,
                  double vmax_lp, int per_agent, const double* T, const double* NCF,
                  const double* S, const double* x, const double* vgoal,
                  int r0, int r1, double* newv, lqro_pair_record* recs, int threads);
+/* orc_step_mt with the reference's per-pair cost structure: F, G, Transform
+ * and -C*F recomputed per pair from A, B, L, E (LQRO:1401-1406, 723-732,
+ * 770-773) and GJK run twice for an outside pair (LQRO:1410, 1414).  Results
+ * are bit-identical to orc_step_mt; bench.py times it as the CPU baseline. */
+int  orc_step_faithful_mt(int N, int X, int H, int NP, int min_reach, double vmax_reach,
+                          double vmax_lp, int per_agent, const double* A, const double* B,
+                          const double* L, const double* E, const double* S, const double* x,
+                          const double* vgoal, int r0, int r1, double* newv,
+                          lqro_pair_record* recs, int threads);
 
 /* GJK restatement (GJK:296-501) for the path's call run_gjk (LQRO:814-853):
  * object 1 = the single point vrel, object 2 = pts[n][3].  Returns dist^2;

@@ -45,6 +45,8 @@ def lib():
         _o.orc_pair.argtypes = [C.c_int] * 4 + [d] + [C.c_void_p] * 5 + [C.c_int, C.c_int] + [C.c_void_p] * 3
         _o.orc_step.argtypes = [C.c_int] * 5 + [d, d, C.c_int] + [C.c_void_p] * 5 + [C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         _o.orc_step_mt.argtypes = _o.orc_step.argtypes + [C.c_int]
+        _o.orc_step_faithful_mt.argtypes = _o.orc_step_mt.argtypes[:8] + [C.c_void_p] * 2 + \
+            _o.orc_step_mt.argtypes[8:]
         _o.orc_newv.argtypes = [C.c_int, C.c_void_p, C.c_void_p, d, C.c_void_p]
         _o.orc_sphere.argtypes = [C.c_int, d, d, C.c_void_p]
         _o.orc_hull_branch.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
@@ -153,6 +155,25 @@ def step(T, NCF, S, x, vgoal, min_reach=4, vmax_reach=30.0, vmax_lp=100.0, rows=
                            _p(recs) if recs is not None else None, threads)
     if rc:
         raise RuntimeError(f"orc_step: {rc}")
+    return newv, recs
+
+
+def step_faithful(A, B, L, E, S, x, vgoal, H, min_reach=4, vmax_reach=30.0, vmax_lp=100.0, rows=None,
+                  per_agent=False, threads=1, records=True):
+    """orc_step_faithful_mt: the step with the reference's per-pair cost
+    (findFG per pair, LQRO:1401-1406; GJK twice for outside pairs,
+    LQRO:1410/1414); results bit-identical to step().  The CPU baseline."""
+    N, X = x.shape
+    NP = S.shape[0]
+    r0, r1 = rows if rows is not None else (0, N)
+    newv = np.zeros((N, 3))
+    recs = np.zeros((r1 - r0) * (N - 1), dtype=RECORD_DTYPE) if records else None
+    A, B, L, E, x, vgoal = (np.ascontiguousarray(v, np.float64) for v in (A, B, L, E, x, vgoal))
+    rc = lib().orc_step_faithful_mt(N, X, H, NP, min_reach, vmax_reach, vmax_lp, int(per_agent),
+                                    _p(A), _p(B), _p(L), _p(E), _p(S), _p(x), _p(vgoal), r0, r1,
+                                    _p(newv), _p(recs) if recs is not None else None, threads)
+    if rc:
+        raise RuntimeError(f"orc_step_faithful: {rc}")
     return newv, recs
 
 
