@@ -200,3 +200,21 @@ def test_edge_cases(lqro_mod, oracle, gains, case):
     for r, q in zip(recs[inside], rrecs[inside]):
         assert np.array_equal(r["facet"], q["facet"]) and r["dist"] == q["dist"]
     np.testing.assert_allclose(newv, rv, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("scenario", ["swap", "c2", "dense"])
+def test_reference_driver_one_call(lqro_mod, gains, scenario):
+    """lqro_step against the reference's whole pair loop over all rows in one
+    call (tests/golden/driver.npz, LQRO:1391-1436 with its loop-carried
+    state): every row the reference harness completes, bit for bit."""
+    import os
+    from conftest import GOLDEN
+    d = np.load(os.path.join(GOLDEN, "driver.npz"))
+    H = int(d[f"{scenario}_H"])
+    x, vg = d[f"{scenario}_x"], d[f"{scenario}_vgoal"]
+    ctx = lqro_mod.Context(lqro_mod.config(x.shape[0], H, 100))
+    ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
+    newv = ctx.step(x, vg)
+    ctx.close()
+    ok = d[f"{scenario}_ok"].astype(bool)
+    assert np.array_equal(newv[ok].view(np.uint64), d[f"{scenario}_newv"][ok].view(np.uint64))

@@ -109,17 +109,32 @@ def test_row_newv_bit_exact(oracle, scenario):
 
 
 def test_reference_accumulates_planes(oracle):
-    """Documented deviation: the reference's driver never clears orcaPlanes_
-    (declared once, LQRO:1389), so agent i's LP also sees every earlier row's
-    planes.  The build follows the per-agent semantics of RVO2-3D
-    (Agent::computeNewVelocity clears orcaPlanes_, AGT:84-151).  Row 0 of the
-    literal driver is identical by construction; on the sparse C2 swarm the
-    accumulated far planes are inactive, so rows 1..3 coincide too."""
+    """Rows 0..3 of C2 through the reference's driver in ONE call equal the
+    per-row results: calculateNewV empties orcaPlanes_ after each row's LP
+    (LQRO:1233), so no plane carries over to the next row."""
     d = _load("steps.npz")
     acc = d["c2_accum_newv"]
     per = d["c2_newv"]
-    assert _same_bits(acc[0], per[0])
-    assert np.allclose(acc[:4], per[:4], rtol=1e-6)
+    for i in range(4):
+        assert _same_bits(acc[i], per[i]), i
+
+
+@pytest.mark.parametrize("scenario", ["swap", "c2", "dense"])
+def test_reference_driver_one_call(oracle, scenario):
+    """The whole pair loop (LQRO:1391-1436) of the reference over all rows in
+    one call (tests/golden/driver.npz: its loop-carried distance /
+    normalVector / insideHull and per-row orcaPlanes_), against the oracle's
+    step: every row without an inside-hull pair bit for bit (the reference
+    harness stops inside pairs before qconvex.exe)."""
+    d = _load("driver.npz")
+    g = oracle.synthesize()
+    H = int(d[f"{scenario}_H"])
+    x, vg = d[f"{scenario}_x"], d[f"{scenario}_vgoal"]
+    T, NCF = oracle.tables(g["A"], g["B"], g["L"], g["E"], H)
+    newv, _ = oracle.step(T, NCF, oracle.sphere(100), x, vg, records=False, threads=4)
+    ok = d[f"{scenario}_ok"].astype(bool)
+    assert ok.sum() >= {"swap": 4, "c2": 62, "dense": 2}[scenario]
+    assert np.array_equal(newv[ok].view(np.uint64), d[f"{scenario}_newv"][ok].view(np.uint64))
 
 
 def _qhull_fixture():
