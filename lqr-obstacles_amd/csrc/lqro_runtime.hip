@@ -36,6 +36,7 @@
 #include "lqro_synth.hpp"
 #include "lqro_dyn.hpp"
 #include "lqro_dynw.hpp"
+#include "lqro_synthw.hpp"
 
 #define LQRO_PROF_WORDS (32 + 2 * 4096 + 16 + 16)   // hull: 32 counters + 2 words per job; pair: 16; hull wave phases: 16
 
@@ -425,6 +426,23 @@ __global__ void __launch_bounds__(64) k_synth(const lqro_model* models, int n, d
   p[1] = p[0] + X * X; p[2] = p[1] + X * 4; p[3] = p[2] + X; p[4] = p[3] + 4 * X; p[5] = p[4] + 12;
   p[6] = p[5] + 3 * X;
   synth::gains_x<X>(models + a, p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
+}
+
+// The same synthesis with one wave per agent (lqro_synthw.hpp): the agent's
+// matrices in LDS, products and sums over the lanes in the reference's order.
+// The default; LQRO_SYNTH_LANE=1 selects k_synth.
+template <int X>
+__global__ void __launch_bounds__(64) k_synthw(const lqro_model* models, int n, double* out) {
+  extern __shared__ double sw[];
+  const int a = blockIdx.x;
+  if (a >= n) return;
+  constexpr int S = X * X + 12 * X + 21;
+  double* o = out + (size_t)a * S;
+  double* p[7];
+  p[0] = o;
+  p[1] = p[0] + X * X; p[2] = p[1] + X * 4; p[3] = p[2] + X; p[4] = p[3] + 4 * X; p[5] = p[4] + 12;
+  p[6] = p[5] + 3 * X;
+  synthw::gains<X>(models + a, p[0], p[1], p[2], p[3], p[4], p[5], p[6], sw, threadIdx.x);
 }
 
 extern "C" {
@@ -916,12 +934,20 @@ int lqro_synthesize_gains_batch_x(const lqro_model* models, int32_t n, int32_t x
   } else if (hipMemcpy(d_m, models, sizeof(lqro_model) * (size_t)n, hipMemcpyHostToDevice) != hipSuccess) {
     rc = LQRO_E_HIP;
   } else {
-    if (x_dim == 16)
+    const char* lane_env = getenv("LQRO_SYNTH_LANE");
+    const bool lane = lane_env && atoi(lane_env) == 1;
+    if (lane && x_dim == 16)
       hipLaunchKernelGGL(k_synth<16>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, 0, (const lqro_model*)d_m,
                          (int)n, d_out);
-    else
+    else if (lane)
       hipLaunchKernelGGL(k_synth<12>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, 0, (const lqro_model*)d_m,
                          (int)n, d_out);
+    else if (x_dim == 16)
+      hipLaunchKernelGGL(k_synthw<16>, dim3((unsigned)n), dim3(64), sizeof(double) * synthw::Lay<16>::Total, 0,
+                         (const lqro_model*)d_m, (int)n, d_out);
+    else
+      hipLaunchKernelGGL(k_synthw<12>, dim3((unsigned)n), dim3(64), sizeof(double) * synthw::Lay<12>::Total, 0,
+                         (const lqro_model*)d_m, (int)n, d_out);
     std::vector<double> h((size_t)stride * n);
     if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
         hipMemcpy(h.data(), d_out, sizeof(double) * h.size(), hipMemcpyDeviceToHost) != hipSuccess) {
