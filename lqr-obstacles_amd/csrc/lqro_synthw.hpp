@@ -25,15 +25,32 @@ using synth::Quad;
 
 __device__ __forceinline__ void sync() { wave_lds_sync(); }
 
-// C (R x Cc) = A (R x K) * B (K x Cc); C distinct from A, B
+// C (R x Cc) = A (R x K) * B (K x Cc); C distinct from A, B.  Each element
+// is one dot product from 0.0 in k order; large products give each lane a
+// 2 x 2 block (every loaded A and B value feeds two products).
 template <int R, int K, int Cc>
 __device__ __forceinline__ void mm(const double* A, const double* B, double* C, int lane) {
-  for (int e = lane; e < R * Cc; e += 64) {
-    const int i = e / Cc, j = e - i * Cc;
-    double acc = 0.0;
+  if constexpr (R % 2 == 0 && Cc % 2 == 0 && R * Cc >= 128) {
+    constexpr int BC = Cc / 2;
+    for (int e = lane; e < (R / 2) * BC; e += 64) {
+      const int i = 2 * (e / BC), j = 2 * (e - (e / BC) * BC);
+      double c00 = 0.0, c01 = 0.0, c10 = 0.0, c11 = 0.0;
 #pragma unroll
-    for (int k = 0; k < K; ++k) acc += A[i * K + k] * B[k * Cc + j];
-    C[e] = acc;
+      for (int k = 0; k < K; ++k) {
+        const double a0 = A[i * K + k], a1 = A[(i + 1) * K + k];
+        const double b0 = B[k * Cc + j], b1 = B[k * Cc + j + 1];
+        c00 += a0 * b0; c01 += a0 * b1; c10 += a1 * b0; c11 += a1 * b1;
+      }
+      C[i * Cc + j] = c00; C[i * Cc + j + 1] = c01; C[(i + 1) * Cc + j] = c10; C[(i + 1) * Cc + j + 1] = c11;
+    }
+  } else {
+    for (int e = lane; e < R * Cc; e += 64) {
+      const int i = e / Cc, j = e - i * Cc;
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) acc += A[i * K + k] * B[k * Cc + j];
+      C[e] = acc;
+    }
   }
   sync();
 }
@@ -46,24 +63,6 @@ __device__ __forceinline__ void tr(const double* A, double* D, int lane) {
   }
   sync();
 }
-// the inverse of an N x N matrix in LDS (N <= 4), redundantly in every lane
-template <int N>
-__device__ __forceinline__ void inv_small(const double* M, double* D, int lane) {
-  Mat<N, N> m;
-#pragma unroll
-  for (int e = 0; e < N * N; ++e) m.e[e] = M[e];
-  const Mat<N, N> r = synth::inverse(m);
-  sync();   // every lane has read M (D may alias it)
-  if (lane < N * N) {
-    double v = 0.0;
-#pragma unroll
-    for (int e = 0; e < N * N; ++e)
-      if (e == lane) v = r.e[e];
-    D[lane] = v;
-  }
-  sync();
-}
-
 // first strict maximum of |m| in (row, col) scan order over the trailing
 // (N-k)^2 block of the permuted matrix (synth::solve's pivot)
 template <int N>
@@ -148,6 +147,23 @@ __device__ void solve(double* m, double* x, int* ip, int lane) {
   }
 }
 
+// D = !M (N x N, N <= 4) as solve(M, I): the same operations on the same
+// values as synth::inverse's in-place Gauss-Jordan (the identity's columns
+// beyond the pivot step are still zero when it skips them), over the lanes
+// instead of redundantly in every lane (whose dynamic pivot indexing spills
+// to scratch).  wm, wx: 16 doubles each; D may alias M.
+template <int N>
+__device__ __forceinline__ void inv_small(const double* M, double* D, double* wm, double* wx, int* ip, int lane) {
+  if (lane < N * N) {
+    wm[lane] = M[lane];
+    wx[lane] = (lane / N == lane % N) ? 1.0 : 0.0;
+  }
+  sync();
+  solve<N>(wm, wx, ip, lane);
+  if (lane < N * N) D[lane] = wx[lane];
+  sync();
+}
+
 // out = exp(q) (N x N, Padé 7 with scaling and squaring, = synth::expm);
 // w: 6 N x N work matrices, ip: 48 ints
 template <int N>
@@ -197,19 +213,29 @@ __device__ void expm(const double* q, double* out, double* w, int* ip, int lane)
   sync();
 }
 
-// per-wave LDS block (doubles), X <= 16
+// per-wave LDS block (doubles), X <= 16: A, B, L, E (and the solve's pivot
+// ints) live throughout; the linearisation's, the velocity LQR's and the
+// position LQR's work matrices overlay one region, each phase's set laid out
+// on its own (a phase starts after the previous one's last sync)
 template <int X>
 struct Lay {
-  static constexpr int XX = X * X;
+  static constexpr int XX = X * X, X3 = X * 3, X4 = X * 4;
   enum : int {
-    A = 0, At = A + XX, B = At + XX, Bt = B + X * 4, S = Bt + 4 * X, T = S + XX, AtS = T + X * 3,
-    AtSB = AtS + XX, BtS = AtSB + X * 4, BtSB = BtS + 4 * X, Ri = BtSB + 16, K = Ri + 16, AtT = K + X * 4,
-    KBt = AtT + X * 3, KBtT = KBt + XX, AtSA = KBtT + X * 3, BtSA = AtSA + XX, KBtSA = BtSA + 4 * X,
-    C1 = KBtSA + XX, C2 = C1 + X * 3, L = C2 + XX, E = L + 4 * X, Wk = E + 12,
-    // linearisation scratch inside Wk: f rows, F, G, Int, c, 6 expm work matrices
-    Fr = Wk, F = Fr + (2 * X + 9) * X, G = F + XX, Int = G + X * 4, Cv = Int + XX, Ex = Cv + X,
-    Ip = Ex + 6 * XX,                   // 48 ints (24 doubles)
-    Total = Ip + 24
+    A = 0, B = A + XX, L = B + X4, E = L + X4, Ip = E + 12, Wm = Ip + 24, Wx = Wm + 16, V0 = Wx + 16,
+    // linearisation
+    Fr = V0, F = Fr + (2 * X + 9) * X, G = F + XX, Int = G + X4, Cv = Int + XX, E2 = Cv + X, Ex = E2 + XX,
+    LinEnd = Ex + 6 * XX,
+    // velocity LQR
+    At = V0, Bt = At + XX, S = Bt + X4, T = S + XX, AtS = T + X3, AtSB = AtS + XX, BtS = AtSB + X4,
+    BtSB = BtS + X4, Ri = BtSB + 16, K = Ri + 16, AtT = K + X4, KBt = AtT + X3, KBtT = KBt + XX,
+    AtSA = KBtT + X3, BtSA = AtSA + XX, KBtSA = BtSA + X4, C1 = KBtSA + XX, C2 = C1 + X3, VelEnd = C2 + XX,
+    // position LQR
+    Qpt = V0, Acl = Qpt + XX, Aclt = Acl + XX, St = Aclt + XX, AS = St + XX, K2Bt = AS + XX, ASA = K2Bt + XX,
+    Stn = ASA + XX, TXX = Stn + XX, Bcl = TXX + XX, Tt = Bcl + X3, CPs = Tt + X3, Ptt = CPs + X3,
+    K1 = Ptt + X3, K2 = K1 + X3, C3 = K2 + X3, AT = C3 + X3, Ttn = AT + X3, Bclt = Ttn + X3, Pt = Bclt + X3,
+    BS = Pt + X3, BSA = BS + X3, PB = BSA + X3, WLt = PB + X3, WLtR = WLt + X4, Rt = WLtR + X4, RR = Rt + 9,
+    BSB = RR + 9, WEtR = BSB + 18, PosEnd = WEtR + 12,
+    Total = (LinEnd > VelEnd ? (LinEnd > PosEnd ? LinEnd : PosEnd) : (VelEnd > PosEnd ? VelEnd : PosEnd))
   };
 };
 constexpr int kSynthWaveDoubles = Lay<16>::Total;
@@ -264,7 +290,7 @@ __device__ void gains(const lqro_model* md, double* Ao, double* Bo, double* co, 
     expm<X>(tmp, w + Y::A, w + Y::Ex, ip, lane);
     for (int e = lane; e < XX; e += 64) tmp[e] = 0.5 * q.dt * w[Y::F + e];
     sync();
-    double* E2 = w + Y::S;   // exp((dt/2) F), until S is set
+    double* E2 = w + Y::E2;   // exp((dt/2) F)
     expm<X>(tmp, E2, w + Y::Ex, ip, lane);
     // Int = (dt/6) (I + 4 exp(dt F / 2) + A)
     for (int e = lane; e < XX; e += 64) {
@@ -314,7 +340,7 @@ __device__ void gains(const lqro_model* md, double* Ao, double* Bo, double* co, 
     mm<4, X, 4>(w + Y::BtS, w + Y::B, w + Y::BtSB, lane);
     for (int e = lane; e < 16; e += 64) w[Y::BtSB + e] = ((e >> 2) == (e & 3) ? r : 0.0) + w[Y::BtSB + e];
     sync();
-    inv_small<4>(w + Y::BtSB, w + Y::Ri, lane);
+    inv_small<4>(w + Y::BtSB, w + Y::Ri, w + Y::Wm, w + Y::Wx, ip, lane);
     mm<X, 4, 4>(w + Y::AtSB, w + Y::Ri, w + Y::K, lane);          // K = At S B !(R + Bt S B)
     mm<X, X, 3>(w + Y::At, w + Y::T, w + Y::AtT, lane);
     mm<X, 4, X>(w + Y::K, w + Y::Bt, w + Y::KBt, lane);
@@ -333,7 +359,7 @@ __device__ void gains(const lqro_model* md, double* Ao, double* Bo, double* co, 
   mm<4, X, 4>(w + Y::BtS, w + Y::B, w + Y::BtSB, lane);
   for (int e = lane; e < 16; e += 64) w[Y::BtSB + e] = ((e >> 2) == (e & 3) ? r : 0.0) + w[Y::BtSB + e];
   sync();
-  inv_small<4>(w + Y::BtSB, w + Y::Ri, lane);
+  inv_small<4>(w + Y::BtSB, w + Y::Ri, w + Y::Wm, w + Y::Wx, ip, lane);
   for (int e = lane; e < 16; e += 64) w[Y::Ri + e] = -w[Y::Ri + e];
   sync();
   mm<4, 4, X>(w + Y::Ri, w + Y::Bt, w + Y::BtS, lane);        // (-Ri) Bt
@@ -344,36 +370,35 @@ __device__ void gains(const lqro_model* md, double* Ao, double* Bo, double* co, 
   // position LQR with the cross term (LQRO:559-581); the velocity phase's
   // buffers are reused (A, B, L, E stay)
   const double wgt = md->pos_weight, qp = md->qp;
-  double* Ex = w + Y::Ex;
-  double* Qpt = w + Y::At;
-  double* Acl = w + Y::S;
-  double* Aclt = w + Y::AtS;
-  double* St = w + Y::AtSA;
-  double* AS = w + Y::KBt;
-  double* K2Bt = w + Y::KBtSA;
-  double* ASA = w + Y::C2;
-  double* Stn = w + Y::Fr;
-  double* Bcl = w + Y::T;
-  double* Tt = w + Y::AtT;
-  double* cPs = w + Y::C1;
-  double* Ptt = w + Y::KBtT;
-  double* K1 = w + Y::K;
-  double* K2 = w + Y::AtSB;
-  double* c3 = w + Y::F;
-  double* AT = w + Y::G;
-  double* Ttn = w + Y::Int;
-  double* Bclt = w + Y::Bt;
-  double* Pt = w + Y::BtSA;
-  double* BS = w + Y::BtS;
-  double* BSA = Ex;
-  double* PB = Ex + XX;
-  double* Rt = w + Y::BtSB;
-  double* RR = w + Y::Ri;
-  double* BSB = Ex + 2 * XX;
-  double* wEtR = Ex + 2 * XX + 16;
-  double* wLt = Ex + 3 * XX;
-  double* wLtR = Ex + 4 * XX;
-  double* tXX = Ex + 5 * XX;
+  double* Qpt = w + Y::Qpt;
+  double* Acl = w + Y::Acl;
+  double* Aclt = w + Y::Aclt;
+  double* St = w + Y::St;
+  double* AS = w + Y::AS;
+  double* K2Bt = w + Y::K2Bt;
+  double* ASA = w + Y::ASA;
+  double* Stn = w + Y::Stn;
+  double* tXX = w + Y::TXX;
+  double* Bcl = w + Y::Bcl;
+  double* Tt = w + Y::Tt;
+  double* cPs = w + Y::CPs;
+  double* Ptt = w + Y::Ptt;
+  double* K1 = w + Y::K1;
+  double* K2 = w + Y::K2;
+  double* c3 = w + Y::C3;
+  double* AT = w + Y::AT;
+  double* Ttn = w + Y::Ttn;
+  double* Bclt = w + Y::Bclt;
+  double* Pt = w + Y::Pt;
+  double* BS = w + Y::BS;
+  double* BSA = w + Y::BSA;
+  double* PB = w + Y::PB;
+  double* Rt = w + Y::Rt;
+  double* RR = w + Y::RR;
+  double* BSB = w + Y::BSB;
+  double* wEtR = w + Y::WEtR;
+  double* wLt = w + Y::WLt;
+  double* wLtR = w + Y::WLtR;
   // Qpt = ((Ps^T Qp) Ps) + (((wgt L^T) Rw) L)
   tr<4, X>(w + Y::L, wLt, lane);
   for (int e = lane; e < X * 4; e += 64) wLt[e] = wgt * wLt[e];
@@ -430,7 +455,7 @@ __device__ void gains(const lqro_model* md, double* Ao, double* Bo, double* co, 
     mm<3, X, 3>(BS, Bcl, BSB, lane);
     for (int e = lane; e < 9; e += 64) RR[e] = Rt[e] + BSB[e];
     sync();
-    inv_small<3>(RR, RR, lane);
+    inv_small<3>(RR, RR, w + Y::Wm, w + Y::Wx, ip, lane);
     mm<X, 3, 3>(K1, RR, K2, lane);                                          // K
     mm<X, 3, X>(K2, Bclt, K2Bt, lane);
     mm<X, X, 3>(K2Bt, Tt, c3, lane);
@@ -452,7 +477,7 @@ __device__ void gains(const lqro_model* md, double* Ao, double* Bo, double* co, 
   mm<3, X, 3>(BS, Bcl, BSB, lane);
   for (int e = lane; e < 9; e += 64) RR[e] = Rt[e] + BSB[e];
   sync();
-  inv_small<3>(RR, RR, lane);
+  inv_small<3>(RR, RR, w + Y::Wm, w + Y::Wx, ip, lane);
   for (int e = lane; e < 9; e += 64) RR[e] = -RR[e];
   sync();
   mm<3, X, X>(BS, Acl, BSA, lane);
