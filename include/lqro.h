@@ -123,13 +123,16 @@ int lqro_synthesize_gains_batch(const lqro_model* models, int32_t n,
  * BASELINE config 5: the 4 rotor-force states of X_DIM = 16
  * (simulator2.h:4) dropped, rotor forces = the command (no thrust lag), every
  * other term of f (LQRO:368-397) unchanged, linearised at the same hover
- * point.  Shapes as above with X = x_dim. */
+ * point.  Shapes as above with X = x_dim.  Both also return l (U), the
+ * feedforward of controlMatrices (LQRO:552-557: pseudoInverse over jacobi2,
+ * MAT:450-477, 887-1037), 0 at the reference's hover point (c = 0). */
 int lqro_synthesize_gains_x(const lqro_model* m, int32_t x_dim,
                             double* A, double* B, double* c, double* L, double* E,
+                            double* l /* U: the feedforward term, LQRO:552-557 */,
                             double* Lh, double* Eh);
 int lqro_synthesize_gains_batch_x(const lqro_model* models, int32_t n, int32_t x_dim,
                                   double* A, double* B, double* c, double* L, double* E,
-                                  double* Lh, double* Eh, int32_t device);
+                                  double* l /* n*U */, double* Lh, double* Eh, int32_t device);
 
 /* Replaces createSpheres (LQRO:735-750): NP Fibonacci-sphere points. */
 int lqro_sphere(int32_t n_points, double xy_radius, double z_radius, double* out /* NP*3 */);

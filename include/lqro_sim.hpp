@@ -93,12 +93,11 @@ class Simulator {
   // pair loop's findFG (LQRO:1265-1266).
   void findMatrices() {
     std::vector<double> c(kX);
-    check(lqro_synthesize_gains(&model_, A_.data(), B_.data(), c.data(), q_[0].L.data(), q_[0].E.data(),
-                                q_[0].Lh.data(), q_[0].Eh.data()),
-          "lqro_synthesize_gains");
+    check(lqro_synthesize_gains_x(&model_, kX, A_.data(), B_.data(), c.data(), q_[0].L.data(), q_[0].E.data(),
+                                  q_[0].l.data(), q_[0].Lh.data(), q_[0].Eh.data()),
+          "lqro_synthesize_gains_x");
     for (auto& q : q_) {
-      q.L = q_[0].L; q.E = q_[0].E; q.Lh = q_[0].Lh; q.Eh = q_[0].Eh;
-      q.l.fill(0.0);   // l (LQRO:557) is exactly 0 at hover: c = 0
+      q.L = q_[0].L; q.E = q_[0].E; q.l = q_[0].l; q.Lh = q_[0].Lh; q.Eh = q_[0].Eh;
     }
     check(lqro_set_gains(ctx_, A_.data(), B_.data(), q_[0].L.data(), q_[0].E.data(), 0), "lqro_set_gains");
   }

@@ -419,13 +419,13 @@ template <int X>
 __global__ void __launch_bounds__(64) k_synth(const lqro_model* models, int n, double* out) {
   const int a = blockIdx.x * blockDim.x + threadIdx.x;
   if (a >= n) return;
-  constexpr int S = X * X + 12 * X + 21;
+  constexpr int S = X * X + 12 * X + 25;
   double* o = out + (size_t)a * S;
-  double* p[7];
+  double* p[8];
   p[0] = o;
   p[1] = p[0] + X * X; p[2] = p[1] + X * 4; p[3] = p[2] + X; p[4] = p[3] + 4 * X; p[5] = p[4] + 12;
-  p[6] = p[5] + 3 * X;
-  synth::gains_x<X>(models + a, p[0], p[1], p[2], p[3], p[4], p[5], p[6]);
+  p[6] = p[5] + 4; p[7] = p[6] + 3 * X;
+  synth::gains_x<X>(models + a, p[0], p[1], p[2], p[3], p[4], p[6], p[7], p[5]);
 }
 
 // The same synthesis with one wave per agent (lqro_synthw.hpp): the agent's
@@ -436,13 +436,13 @@ __global__ void __launch_bounds__(64) k_synthw(const lqro_model* models, int n, 
   extern __shared__ double sw[];
   const int a = blockIdx.x;
   if (a >= n) return;
-  constexpr int S = X * X + 12 * X + 21;
+  constexpr int S = X * X + 12 * X + 25;
   double* o = out + (size_t)a * S;
-  double* p[7];
+  double* p[8];
   p[0] = o;
   p[1] = p[0] + X * X; p[2] = p[1] + X * 4; p[3] = p[2] + X; p[4] = p[3] + 4 * X; p[5] = p[4] + 12;
-  p[6] = p[5] + 3 * X;
-  synthw::gains<X>(models + a, p[0], p[1], p[2], p[3], p[4], p[5], p[6], sw, threadIdx.x);
+  p[6] = p[5] + 4; p[7] = p[6] + 3 * X;
+  synthw::gains<X>(models + a, p[0], p[1], p[2], p[3], p[4], p[6], p[7], p[5], sw, threadIdx.x);
 }
 
 extern "C" {
@@ -902,28 +902,29 @@ int lqro_synthesize_gains(const lqro_model* md, double* Ao, double* Bo, double* 
 }
 
 int lqro_synthesize_gains_x(const lqro_model* md, int32_t x_dim, double* Ao, double* Bo, double* co,
-                            double* Lo, double* Eo, double* Lho, double* Eho) {
+                            double* Lo, double* Eo, double* lo, double* Lho, double* Eho) {
   if (!md) return LQRO_E_ARG;
-  if (x_dim == 16) synth::gains_x<16>(md, Ao, Bo, co, Lo, Eo, Lho, Eho);
-  else if (x_dim == 12) synth::gains_x<12>(md, Ao, Bo, co, Lo, Eo, Lho, Eho);
+  if (x_dim == 16) synth::gains_x<16>(md, Ao, Bo, co, Lo, Eo, Lho, Eho, lo);
+  else if (x_dim == 12) synth::gains_x<12>(md, Ao, Bo, co, Lo, Eo, Lho, Eho, lo);
   else return LQRO_E_ARG;
   return LQRO_OK;
 }
 
-// per-agent output block, in doubles: A X*X, B X*4, c X, L 4*X, E 12, Lh 3*X, Eh 9
+// per-agent output block, in doubles: A X*X, B X*4, c X, L 4*X, E 12, l 4, Lh 3*X, Eh 9
 static void synth_sizes(int X, int* sz) {
-  sz[0] = X * X; sz[1] = X * 4; sz[2] = X; sz[3] = 4 * X; sz[4] = 12; sz[5] = 3 * X; sz[6] = 9;
+  sz[0] = X * X; sz[1] = X * 4; sz[2] = X; sz[3] = 4 * X; sz[4] = 12; sz[5] = 4; sz[6] = 3 * X; sz[7] = 9;
 }
-static int synth_stride(int X) { return X * X + 12 * X + 21; }
+static int synth_stride(int X) { return X * X + 12 * X + 25; }
 
 int lqro_synthesize_gains_batch_x(const lqro_model* models, int32_t n, int32_t x_dim, double* A, double* B,
-                                  double* c, double* L, double* E, double* Lh, double* Eh, int32_t device) {
+                                  double* c, double* L, double* E, double* l, double* Lh, double* Eh,
+                                  int32_t device) {
   if (!models || n <= 0 || (x_dim != 16 && x_dim != 12)) return LQRO_E_ARG;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) return LQRO_E_NODEVICE;
   if (hipSetDevice(device) != hipSuccess) return LQRO_E_HIP;
   const int stride = synth_stride(x_dim);
-  int sz[7];
+  int sz[8];
   synth_sizes(x_dim, sz);
   lqro_model* d_m = nullptr;
   double* d_out = nullptr;
@@ -953,9 +954,9 @@ int lqro_synthesize_gains_batch_x(const lqro_model* models, int32_t n, int32_t x
         hipMemcpy(h.data(), d_out, sizeof(double) * h.size(), hipMemcpyDeviceToHost) != hipSuccess) {
       rc = LQRO_E_HIP;
     } else {
-      double* outs[7] = {A, B, c, L, E, Lh, Eh};
+      double* outs[8] = {A, B, c, L, E, l, Lh, Eh};
       int off = 0;
-      for (int k = 0; k < 7; ++k) {
+      for (int k = 0; k < 8; ++k) {
         if (outs[k])
           for (int a = 0; a < n; ++a)
             memcpy(outs[k] + (size_t)a * sz[k], h.data() + (size_t)a * stride + off, sizeof(double) * sz[k]);
@@ -970,7 +971,7 @@ int lqro_synthesize_gains_batch_x(const lqro_model* models, int32_t n, int32_t x
 
 int lqro_synthesize_gains_batch(const lqro_model* models, int32_t n, double* A, double* B, double* c,
                                 double* L, double* E, double* Lh, double* Eh, int32_t device) {
-  return lqro_synthesize_gains_batch_x(models, n, 16, A, B, c, L, E, Lh, Eh, device);
+  return lqro_synthesize_gains_batch_x(models, n, 16, A, B, c, L, E, nullptr, Lh, Eh, device);
 }
 
 // ---- the per-agent step after the pair loop (LQRO:1437-1446) -------------

@@ -13,6 +13,7 @@
 // f is reached at a rotation error of j_step where it multiplies a zero body
 // rate.  So host and device agree bit for bit (tests/test_gpu_synth.py).
 #pragma once
+#include <cfloat>
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -202,6 +203,134 @@ LQRO_HD Mat<N, N> expm(const Mat<N, N>& q) {
   return R;
 }
 
+// jacobi2 (MAT:887-1037): Householder tridiagonalisation + QL iteration, the
+// reference's eigen-decomposition of a symmetric matrix (Numerical Recipes;
+// no eigenvalue sort).  z = eigenvectors (columns), D = diag(eigenvalues).
+template <int N>
+LQRO_HD void jacobi2(const Mat<N, N>& q, Mat<N, N>& z, Mat<N, N>& D) {
+  z = q;
+  double d[N], e[N];
+  for (int i = 0; i < N; ++i) d[i] = e[i] = 0.0;
+  int l, k, j, i, m, iter;
+  double scale, hh, h, g, f, s, r, p, dd, c, b, absf, absg, pfg;
+  for (i = N - 1; i > 0; i--) {
+    l = i - 1;
+    h = scale = 0.0;
+    if (l > 0) {
+      for (k = 0; k < i; k++) scale += fabs(z(i, k));
+      if (scale == 0.0)
+        e[i] = z(i, l);
+      else {
+        for (k = 0; k < i; k++) {
+          z(i, k) /= scale;
+          h += z(i, k) * z(i, k);
+        }
+        f = z(i, l);
+        g = (f >= 0.0 ? -sqrt(h) : sqrt(h));
+        e[i] = scale * g;
+        h -= f * g;
+        z(i, l) = f - g;
+        f = 0.0;
+        for (j = 0; j < i; j++) {
+          z(j, i) = z(i, j) / h;
+          g = 0.0;
+          for (k = 0; k < j + 1; k++) g += z(j, k) * z(i, k);
+          for (k = j + 1; k < i; k++) g += z(k, j) * z(i, k);
+          e[j] = g / h;
+          f += e[j] * z(i, j);
+        }
+        hh = f / (h + h);
+        for (j = 0; j < i; j++) {
+          f = z(i, j);
+          e[j] = g = e[j] - hh * f;
+          for (k = 0; k < j + 1; k++) z(j, k) -= (f * e[k] + g * z(i, k));
+        }
+      }
+    } else {
+      e[i] = z(i, l);
+    }
+    d[i] = h;
+  }
+  d[0] = 0.0;
+  e[0] = 0.0;
+  for (i = 0; i < N; i++) {
+    if (d[i] != 0.0) {
+      for (j = 0; j < i; j++) {
+        g = 0.0;
+        for (k = 0; k < i; k++) g += z(i, k) * z(k, j);
+        for (k = 0; k < i; k++) z(k, j) -= g * z(k, i);
+      }
+    }
+    d[i] = z(i, i);
+    z(i, i) = 1.0;
+    for (j = 0; j < i; j++) z(j, i) = z(i, j) = 0.0;
+  }
+  for (i = 1; i < N; i++) e[i - 1] = e[i];
+  e[N - 1] = 0.0;
+  for (l = 0; l < N; l++) {
+    iter = 0;
+    do {
+      for (m = l; m < N - 1; m++) {
+        dd = fabs(d[m]) + fabs(d[m + 1]);
+        if (fabs(e[m]) <= DBL_EPSILON * dd) break;
+      }
+      if (m != l) {
+        if (iter++ == 30) break;   // the reference prints "Too many iterations" and exits
+        g = (d[l + 1] - d[l]) / (2.0 * e[l]);
+        absg = fabs(g);
+        r = ((absg > 1.0) ? absg * sqrt(1.0 + (1.0 / absg) * (1.0 / absg)) : sqrt(1.0 + absg * absg));
+        g = d[m] - d[l] + e[l] / (g + ((g >= 0.0) ? fabs(r) : -fabs(r)));
+        s = c = 1.0;
+        p = 0.0;
+        for (i = m - 1; i >= l; i--) {
+          f = s * e[i];
+          b = c * e[i];
+          absf = fabs(f);
+          absg = fabs(g);
+          pfg = (absf > absg ? absf * sqrt(1.0 + (absg / absf) * (absg / absf))
+                             : (absg == 0.0 ? 0.0 : absg * sqrt(1.0 + (absf / absg) * (absf / absg))));
+          e[i + 1] = (r = pfg);
+          if (r == 0.0) {
+            d[i + 1] -= p;
+            e[m] = 0.0;
+            break;
+          }
+          s = f / r;
+          c = g / r;
+          g = d[i + 1] - p;
+          r = (d[i] - g) * s + 2.0 * c * b;
+          d[i + 1] = g + (p = s * r);
+          g = c * r - b;
+          for (k = 0; k < N; k++) {
+            f = z(k, i + 1);
+            z(k, i + 1) = s * z(k, i) + c * f;
+            z(k, i) = c * z(k, i) - s * f;
+          }
+        }
+        if (r == 0.0 && i >= l) continue;
+        d[l] -= p;
+        e[l] = g;
+        e[m] = 0.0;
+      }
+    } while (m != l);
+  }
+  D = Mat<N, N>::zero();
+  for (i = 0; i < N; ++i) D(i, i) = d[i];
+}
+
+// pseudoInverse (MAT:450-477) of a square matrix (the _numColumns <=
+// _numRows branch): (Vec Val^+ Vec^T) q^T with jacobi2(q^T q)
+template <int N>
+LQRO_HD Mat<N, N> pseudo_inverse(const Mat<N, N>& q) {
+  Mat<N, N> Vec, Val;
+  jacobi2<N>(tr(q) * q, Vec, Val);
+  for (int i = 0; i < N; ++i) {
+    if (fabs(Val(i, i)) <= sqrt(DBL_EPSILON)) Val(i, i) = 0.0;
+    else Val(i, i) = 1.0 / Val(i, i);
+  }
+  return (Vec * Val * tr(Vec)) * tr(q);
+}
+
 typedef Mat<3, 1> Vec3;
 LQRO_HD Mat<3, 3> skew(const Vec3& v) {
   Mat<3, 3> m = Mat<3, 3>::zero();
@@ -261,12 +390,29 @@ LQRO_HD void put(double* out, const Mat<R, C>& m) {
     for (int i = 0; i < R * C; ++i) out[i] = m.e[i];
 }
 
+// l of controlMatrices (LQRO:552, 557), with S the converged velocity-LQR
+// Riccati matrix and xstar = xGoal (hover; Qx = 0 makes Qx*xstar zero):
+//   a = pseudoInverse(~A - ~A*S*B*!(R+~B*S*B)*~B - I)
+//         * (Qx*xstar - ~A*S*c + ~A*S*B*!(R+~B*S*B)*~B*S*c)
+//   l = -!(R+~B*S*B) * (~B*S*c + ~B*a)
+// (exactly 0 for the reference's model, whose hover point has c = 0)
+template <int X>
+LQRO_HD Mat<4, 1> ell(const Mat<X, X>& A, const Mat<X, 4>& B, const Mat<X, 1>& c, const Mat<X, X>& S,
+                      const Mat<4, 4>& Rw, const Mat<X, 1>& xstar) {
+  const Mat<X, X> At = tr(A), Qx = Mat<X, X>::zero();
+  const Mat<4, X> Bt = tr(B);
+  const Mat<X, X> M1 = At - At * S * B * inverse(Rw + Bt * S * B) * Bt - eye<X>();
+  const Mat<X, 1> v1 = Qx * xstar - At * S * c + At * S * B * inverse(Rw + Bt * S * B) * Bt * S * c;
+  const Mat<X, 1> a = pseudo_inverse<X>(M1) * v1;
+  return -inverse(Rw + Bt * S * B) * (Bt * S * c + Bt * a);
+}
+
 // controlMatrices for one agent's model: A (X*X), B (X*U), c (X), L (U*X),
 // E (U*3), Lh (3*X), Eh (3*3); any output may be null.  X = 12: the reduced
 // model above, linearised at the same hover point.
 template <int X>
 LQRO_HD void gains_x(const lqro_model* md, double* Ao, double* Bo, double* co, double* Lo, double* Eo,
-                     double* Lho, double* Eho) {
+                     double* Lho, double* Eho, double* lo = nullptr) {
   Quad q;
   q.dt = md->dt; q.g = md->gravity; q.mass = md->mass; q.kM = md->moment_const;
   q.lat = md->thrust_latency; q.arm = md->length; q.h = md->j_step;
@@ -326,6 +472,7 @@ LQRO_HD void gains_x(const lqro_model* md, double* Ao, double* Bo, double* co, d
   Mat<4, 4> Ri = inverse(Rw + Bt * S * B);
   Mat<4, X> L = -Ri * Bt * S * A;
   Mat<4, 3> E = -Ri * Bt * T;
+  if (lo) put(lo, ell<X>(A, B, c, S, Rw, x0));
 
   // position LQR on the closed velocity loop, with the cross term
   const double wgt = md->pos_weight;

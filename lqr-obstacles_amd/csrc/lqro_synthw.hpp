@@ -221,7 +221,8 @@ template <int X>
 struct Lay {
   static constexpr int XX = X * X, X3 = X * 3, X4 = X * 4;
   enum : int {
-    A = 0, B = A + XX, L = B + X4, E = L + X4, Ip = E + 12, Wm = Ip + 24, Wx = Wm + 16, V0 = Wx + 16,
+    A = 0, B = A + XX, L = B + X4, E = L + X4, Cp = E + 12, Ip = Cp + X, Wm = Ip + 24, Wx = Wm + 16,
+    V0 = Wx + 16,
     // linearisation
     Fr = V0, F = Fr + (2 * X + 9) * X, G = F + XX, Int = G + X4, Cv = Int + XX, E2 = Cv + X, Ex = E2 + XX,
     LinEnd = Ex + 6 * XX,
@@ -243,7 +244,7 @@ constexpr int kSynthWaveDoubles = Lay<16>::Total;
 // controlMatrices for agent model md, outputs as synth::gains_x (any null)
 template <int X>
 __device__ void gains(const lqro_model* md, double* Ao, double* Bo, double* co, double* Lo, double* Eo,
-                      double* Lho, double* Eho, double* w, int lane) {
+                      double* Lho, double* Eho, double* lo, double* w, int lane) {
   using Y = Lay<X>;
   constexpr int XX = X * X;
   Quad q;
@@ -300,8 +301,10 @@ __device__ void gains(const lqro_model* md, double* Ao, double* Bo, double* co, 
     sync();
     mm<X, X, 4>(w + Y::Int, w + Y::G, w + Y::B, lane);                 // B = Int G
     mm<X, X, 1>(w + Y::Int, w + Y::Fr + 2 * X * X, w + Y::Cv, lane);  // c = Int xdot
-    if (co)
-      for (int e = lane; e < X; e += 64) co[e] = w[Y::Cv + e];
+    for (int e = lane; e < X; e += 64) {
+      w[Y::Cp + e] = w[Y::Cv + e];   // kept for l
+      if (co) co[e] = w[Y::Cv + e];
+    }
   }
 
   // velocity LQR (LQRO:541-557): Vs selects x[3..5]; Qx = 0
@@ -366,6 +369,19 @@ __device__ void gains(const lqro_model* md, double* Ao, double* Bo, double* co, 
   mm<4, X, X>(w + Y::BtS, w + Y::S, w + Y::BtSA, lane);       // ((-Ri) Bt) S
   mm<4, X, X>(w + Y::BtSA, w + Y::A, w + Y::L, lane);         // L
   mm<4, X, 3>(w + Y::BtS, w + Y::T, w + Y::E, lane);          // E
+  if (lo && lane == 0) {
+    // l (LQRO:552, 557): once per agent, one lane, on synth::ell
+    Mat<X, X> Am, Sm;
+    Mat<X, 4> Bm;
+    Mat<X, 1> cm, xs = Mat<X, 1>::zero();
+    for (int e = 0; e < XX; ++e) { Am.e[e] = w[Y::A + e]; Sm.e[e] = w[Y::S + e]; }
+    for (int e = 0; e < X * 4; ++e) Bm.e[e] = w[Y::B + e];
+    for (int e = 0; e < X; ++e) cm.e[e] = w[Y::Cp + e];
+    for (int k = 12; k < X; ++k) xs.e[k] = hover;
+    const Mat<4, 1> lv = synth::ell<X>(Am, Bm, cm, Sm, r * synth::eye<4>(), xs);
+    for (int k = 0; k < 4; ++k) lo[k] = lv.e[k];
+  }
+  sync();
 
   // position LQR with the cross term (LQRO:559-581); the velocity phase's
   // buffers are reused (A, B, L, E stay)

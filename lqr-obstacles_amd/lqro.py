@@ -102,8 +102,8 @@ def lib() -> C.CDLL:
         L.lqro_model_default.argtypes = [C.POINTER(Model)]
         L.lqro_synthesize_gains.argtypes = [C.POINTER(Model)] + [vp] * 7
         L.lqro_synthesize_gains_batch.argtypes = [C.POINTER(Model), i32] + [vp] * 7 + [i32]
-        L.lqro_synthesize_gains_x.argtypes = [C.POINTER(Model), i32] + [vp] * 7
-        L.lqro_synthesize_gains_batch_x.argtypes = [C.POINTER(Model), i32, i32] + [vp] * 7 + [i32]
+        L.lqro_synthesize_gains_x.argtypes = [C.POINTER(Model), i32] + [vp] * 8
+        L.lqro_synthesize_gains_batch_x.argtypes = [C.POINTER(Model), i32, i32] + [vp] * 8 + [i32]
         L.lqro_sphere.argtypes = [i32, dbl, dbl, vp]
         L.lqro_create.argtypes = [C.POINTER(Config), C.POINTER(vp)]
         L.lqro_destroy.argtypes = [vp]
@@ -144,21 +144,22 @@ def default_model() -> Model:
 
 
 def gain_shapes(x_dim: int = 16) -> dict:
+    """controlMatrices' outputs in the reference's argument order (LQRO:520)."""
     X = x_dim
-    return dict(A=(X, X), B=(X, 4), c=(X,), L=(4, X), E=(4, 3), Lh=(3, X), Eh=(3, 3))
+    return dict(A=(X, X), B=(X, 4), c=(X,), L=(4, X), E=(4, 3), l=(4,), Lh=(3, X), Eh=(3, 3))
 
 
 GAIN_SHAPES = gain_shapes(16)
 
 
 def synthesize_gains(model: Model | None = None, x_dim: int = 16) -> dict:
-    """controlMatrices at hover (LQRO:520-582): A, B, c, L, E, Lh, Eh.
+    """controlMatrices at hover (LQRO:520-582): A, B, c, L, E, l, Lh, Eh.
     x_dim = 12: BASELINE config 5's reduced model (rotor-force states
     dropped, F = u; lqro_synthesize_gains_x)."""
     m = model or default_model()
-    out = {k: np.zeros(s) for k, s in gain_shapes(x_dim).items()}
-    _check(lib().lqro_synthesize_gains_x(C.byref(m), x_dim, *[_p(out[k]) for k in
-                                                            ("A", "B", "c", "L", "E", "Lh", "Eh")]),
+    shp = gain_shapes(x_dim)
+    out = {k: np.zeros(s) for k, s in shp.items()}
+    _check(lib().lqro_synthesize_gains_x(C.byref(m), x_dim, *[_p(out[k]) for k in shp]),
            "lqro_synthesize_gains_x")
     return out
 
@@ -445,7 +446,7 @@ class Quadrotor:
         self.pGoal = np.zeros(3) if pGoal is None else np.asarray(pGoal, dtype=np.float64).copy()
         self.L = None
         self.E = None
-        self.l = np.zeros(4)   # zero at hover (c = 0); the pair path never reads it
+        self.l = np.zeros(4)   # feedforward (LQRO:557), set by findMatrices; the pair path never reads it
         self.Lh = None
         self.Eh = None
         # estimation state (setupQuadrotors, LQRO:107-122, without its noise draw)
@@ -475,7 +476,7 @@ class Simulator:
         g = synthesize_gains(self.model)
         self.A, self.B, self.c = g["A"], g["B"], g["c"]
         for q in self.qlist:
-            q.L, q.E, q.Lh, q.Eh = g["L"], g["E"], g["Lh"], g["Eh"]
+            q.L, q.E, q.l, q.Lh, q.Eh = g["L"], g["E"], g["l"], g["Lh"], g["Eh"]
         Ls = np.stack([q.L for q in self.qlist])
         Es = np.stack([q.E for q in self.qlist])
         per_agent = not all(np.array_equal(Ls[0], l) for l in Ls) or \

@@ -10,6 +10,7 @@
  */
 #include "lqro_oracle.h"
 
+#include <float.h>
 #include <math.h>
 #include <pthread.h>
 #include <stdio.h>
@@ -325,13 +326,141 @@ static void linearize(int X, const phys_t* P, const double* x, const double* R, 
 
 int orc_synthesize(const lqro_model* m, double* Aout, double* Bout, double* cout,
                    double* Lout, double* Eout, double* Lhout, double* Ehout) {
-  return orc_synthesize_x(m, 16, Aout, Bout, cout, Lout, Eout, Lhout, Ehout);
+  return orc_synthesize_x(m, 16, Aout, Bout, cout, Lout, Eout, NULL, Lhout, Ehout);
 }
+
+/* jacobi2 (MAT:887-1037): Householder tridiagonalisation + QL iteration
+ * (Numerical Recipes, no eigenvalue sort); z = eigenvectors (columns), D =
+ * diag(eigenvalues), n x n row-major. */
+static void jacobi2(int n, const double* q, double* z, double* D) {
+  double d[MXN], e[MXN];
+  memcpy(z, q, sizeof(double) * n * n);
+  for (int i = 0; i < n; ++i) d[i] = e[i] = 0.0;
+  int l, k, j, i, m, iter;
+  double scale, hh, h, g, f, s, r = 0.0, p, dd, c, b, absf, absg, pfg;
+#define Z(a, bb) z[(a) * n + (bb)]
+  for (i = n - 1; i > 0; i--) {
+    l = i - 1;
+    h = scale = 0.0;
+    if (l > 0) {
+      for (k = 0; k < i; k++) scale += fabs(Z(i, k));
+      if (scale == 0.0) e[i] = Z(i, l);
+      else {
+        for (k = 0; k < i; k++) { Z(i, k) /= scale; h += Z(i, k) * Z(i, k); }
+        f = Z(i, l);
+        g = (f >= 0.0 ? -sqrt(h) : sqrt(h));
+        e[i] = scale * g;
+        h -= f * g;
+        Z(i, l) = f - g;
+        f = 0.0;
+        for (j = 0; j < i; j++) {
+          Z(j, i) = Z(i, j) / h;
+          g = 0.0;
+          for (k = 0; k < j + 1; k++) g += Z(j, k) * Z(i, k);
+          for (k = j + 1; k < i; k++) g += Z(k, j) * Z(i, k);
+          e[j] = g / h;
+          f += e[j] * Z(i, j);
+        }
+        hh = f / (h + h);
+        for (j = 0; j < i; j++) {
+          f = Z(i, j);
+          e[j] = g = e[j] - hh * f;
+          for (k = 0; k < j + 1; k++) Z(j, k) -= (f * e[k] + g * Z(i, k));
+        }
+      }
+    } else {
+      e[i] = Z(i, l);
+    }
+    d[i] = h;
+  }
+  d[0] = 0.0;
+  e[0] = 0.0;
+  for (i = 0; i < n; i++) {
+    if (d[i] != 0.0) {
+      for (j = 0; j < i; j++) {
+        g = 0.0;
+        for (k = 0; k < i; k++) g += Z(i, k) * Z(k, j);
+        for (k = 0; k < i; k++) Z(k, j) -= g * Z(k, i);
+      }
+    }
+    d[i] = Z(i, i);
+    Z(i, i) = 1.0;
+    for (j = 0; j < i; j++) Z(j, i) = Z(i, j) = 0.0;
+  }
+  for (i = 1; i < n; i++) e[i - 1] = e[i];
+  e[n - 1] = 0.0;
+  for (l = 0; l < n; l++) {
+    iter = 0;
+    do {
+      for (m = l; m < n - 1; m++) {
+        dd = fabs(d[m]) + fabs(d[m + 1]);
+        if (fabs(e[m]) <= DBL_EPSILON * dd) break;
+      }
+      if (m != l) {
+        if (iter++ == 30) break;   /* the reference exits the program here */
+        g = (d[l + 1] - d[l]) / (2.0 * e[l]);
+        absg = fabs(g);
+        r = ((absg > 1.0) ? absg * sqrt(1.0 + (1.0 / absg) * (1.0 / absg)) : sqrt(1.0 + absg * absg));
+        g = d[m] - d[l] + e[l] / (g + ((g >= 0.0) ? fabs(r) : -fabs(r)));
+        s = c = 1.0;
+        p = 0.0;
+        for (i = m - 1; i >= l; i--) {
+          f = s * e[i];
+          b = c * e[i];
+          absf = fabs(f);
+          absg = fabs(g);
+          pfg = (absf > absg ? absf * sqrt(1.0 + (absg / absf) * (absg / absf))
+                             : (absg == 0.0 ? 0.0 : absg * sqrt(1.0 + (absf / absg) * (absf / absg))));
+          e[i + 1] = (r = pfg);
+          if (r == 0.0) { d[i + 1] -= p; e[m] = 0.0; break; }
+          s = f / r;
+          c = g / r;
+          g = d[i + 1] - p;
+          r = (d[i] - g) * s + 2.0 * c * b;
+          d[i + 1] = g + (p = s * r);
+          g = c * r - b;
+          for (k = 0; k < n; k++) {
+            f = Z(k, i + 1);
+            Z(k, i + 1) = s * Z(k, i) + c * f;
+            Z(k, i) = c * Z(k, i) - s * f;
+          }
+        }
+        if (r == 0.0 && i >= l) continue;
+        d[l] -= p;
+        e[l] = g;
+        e[m] = 0.0;
+      }
+    } while (m != l);
+  }
+#undef Z
+  for (i = 0; i < n * n; ++i) D[i] = 0.0;
+  for (i = 0; i < n; ++i) D[i * n + i] = d[i];
+}
+
+/* pseudoInverse (MAT:450-477) of a square n x n matrix: (Vec Val^+ Vec^T) q^T
+ * with jacobi2(q^T q); Val^+ zeroes |eigenvalues| <= sqrt(DBL_EPSILON) */
+static void pinv(int n, const double* q, double* out) {
+  double qt[MXN * MXN], qtq[MXN * MXN], V[MXN * MXN], D[MXN * MXN], VD[MXN * MXN], Vt[MXN * MXN], VDV[MXN * MXN];
+  mt(n, n, q, qt);
+  mm(n, n, n, qt, q, qtq);
+  jacobi2(n, qtq, V, D);
+  for (int i = 0; i < n; ++i) {
+    double* v = &D[i * n + i];
+    if (fabs(*v) <= sqrt(DBL_EPSILON)) *v = 0.0;
+    else *v = 1.0 / *v;
+  }
+  mm(n, n, n, V, D, VD);
+  mt(n, n, V, Vt);
+  mm(n, n, n, VD, Vt, VDV);
+  mm(n, n, n, VDV, qt, out);
+}
+
+void orc_pinv(int n, const double* q, double* out) { pinv(n, q, out); }
 
 /* controlMatrices (LQRO:520-582) for X = 16, or X = 12 (the reduced model of
  * fdyn_x).  Arrays are sized for X = 16 and used with stride X. */
 int orc_synthesize_x(const lqro_model* m, int X, double* Aout, double* Bout, double* cout,
-                     double* Lout, double* Eout, double* Lhout, double* Ehout) {
+                     double* Lout, double* Eout, double* lout, double* Lhout, double* Ehout) {
   enum { XM = 16, U = 4, V = 3 };
   if (X != 16 && X != 12) return -1;
   phys_t P; phys_init(m, &P);
@@ -387,6 +516,28 @@ int orc_synthesize_x(const lqro_model* m, int X, double* Aout, double* Bout, dou
   madd(U * U, R, BtSB, RB); minv(U, RB, Ri); mneg(U * U, Ri, nRi);
   mm(U, U, X, nRi, Bt, tUX); mm(U, X, X, tUX, S, tUX2); mm(U, X, X, tUX2, A, L);
   mm(U, X, V, tUX, T, E);
+  if (lout) {
+    /* l (LQRO:552, 557), xstar = xHat (Qx*xstar = 0):
+     *   a = pseudoInverse(~A - ~A*S*B*!(R+~B*S*B)*~B - I)
+     *         * (Qx*xstar - ~A*S*c + ~A*S*B*!(R+~B*S*B)*~B*S*c)
+     *   l = -!(R+~B*S*B) * (~B*S*c + ~B*a)                                  */
+    double KB[XM * XM], M1[XM * XM], I[XM * XM], Pi[XM * XM], q1[XM], q2[XM], q3[XM], v1[XM], av[XM];
+    double KBS[XM * XM], u1[U], u2[U], u3[U];
+    mm(X, X, X, At, S, AtS); mm(X, X, U, AtS, B, AtSB);          /* ~A*S*B with the final S */
+    mm(U, X, X, Bt, S, BtS); mm(U, X, U, BtS, B, BtSB);
+    madd(U * U, R, BtSB, RB); minv(U, RB, Ri);
+    mm(X, U, U, AtSB, Ri, t1);                                    /* ~A*S*B*!(..) */
+    mm(X, U, X, t1, Bt, KB);                                      /* .. *~B */
+    msub(X * X, At, KB, M1); meye(X, I); msub(X * X, M1, I, M1);
+    mm(X, X, 1, Qx, xHat, q1);                                    /* Qx*xstar */
+    mm(X, X, 1, AtS, c, q2);                                      /* ~A*S*c */
+    mm(X, X, X, KB, S, KBS); mm(X, X, 1, KBS, c, q3);             /* ..*~B*S*c */
+    msub(X, q1, q2, v1); madd(X, v1, q3, v1);
+    pinv(X, M1, Pi);
+    mm(X, X, 1, Pi, v1, av);
+    mm(U, X, 1, BtS, c, u1); mm(U, X, 1, Bt, av, u2); madd(U, u1, u2, u3);
+    mm(U, U, 1, nRi, u3, lout);
+  }
 
   /* position LQR (LQRO:559-581) */
   const double w = m->pos_weight;

@@ -39,8 +39,10 @@ int  orc_synthesize(const lqro_model* m, double* A, double* B, double* c,
                     double* L, double* E, double* Lh, double* Eh);
 /* the same for x_dim 16 or 12 (BASELINE config 5's reduced model: no
  * rotor-force states, F = u); not in the reference (SURVEY §7 hazard 7) */
+/* pseudoInverse (MAT:450-477) of a square n x n matrix, n <= 16 */
+void orc_pinv(int n, const double* q, double* out);
 int  orc_synthesize_x(const lqro_model* m, int x_dim, double* A, double* B, double* c,
-                      double* L, double* E, double* Lh, double* Eh);
+                      double* L, double* E, double* l, double* Lh, double* Eh);
 
 /* createSpheres (LQRO:735-750). */
 void orc_sphere(int np, double xy_radius, double z_radius, double* s);

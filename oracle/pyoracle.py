@@ -49,6 +49,7 @@ def lib():
             _o.orc_step_mt.argtypes[8:]
         _o.orc_newv.argtypes = [C.c_int, C.c_void_p, C.c_void_p, d, C.c_void_p]
         _o.orc_sphere.argtypes = [C.c_int, d, d, C.c_void_p]
+        _o.orc_pinv.argtypes = [C.c_int, C.c_void_p, C.c_void_p]
         _o.orc_hull_branch.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         _o.orc_hull.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int]
         _o.orc_agent_step.argtypes = [C.c_void_p] * 17
@@ -98,10 +99,18 @@ def synthesize(model: Model | None = None, x_dim: int = 16) -> dict:
         lib().orc_model_default(C.byref(m))
     X = x_dim
     out = dict(A=np.zeros((X, X)), B=np.zeros((X, 4)), c=np.zeros(X), L=np.zeros((4, X)),
-               E=np.zeros((4, 3)), Lh=np.zeros((3, X)), Eh=np.zeros((3, 3)))
-    rc = lib().orc_synthesize_x(C.byref(m), X, *[_p(out[k]) for k in ("A", "B", "c", "L", "E", "Lh", "Eh")])
+               E=np.zeros((4, 3)), l=np.zeros(4), Lh=np.zeros((3, X)), Eh=np.zeros((3, 3)))
+    rc = lib().orc_synthesize_x(C.byref(m), X, *[_p(out[k]) for k in ("A", "B", "c", "L", "E", "l", "Lh", "Eh")])
     if rc != 0:
         raise ValueError(f"orc_synthesize_x: x_dim {X}")
+    return out
+
+
+def pinv(q: np.ndarray) -> np.ndarray:
+    """pseudoInverse (MAT:450-477) of a square matrix."""
+    q = np.ascontiguousarray(q, np.float64)
+    out = np.zeros_like(q)
+    lib().orc_pinv(q.shape[0], _p(q), _p(out))
     return out
 
 

@@ -277,6 +277,14 @@ int ref_step(int N, int np, int H, int min_reach, double vmax_reach, const doubl
  * they are not built here (the oracle's jacobi is pinned by its properties,
  * tests/test_oracle_dyn.py).  Weights M, N are the reference's (LQRO:1285-1286). */
 
+/* pseudoInverse (MAT:450-477, over jacobi2 MAT:887-1037) of a 16 x 16 matrix,
+ * the form controlMatrices applies it in (LQRO:552) */
+void ref_pinv16(const double* in, double* out) {
+  Matrix<16, 16> q;
+  load(q, in);
+  store(pseudoInverse(q), out);
+}
+
 /* l of controlMatrices (LQRO:552,557), which the pair path does not read */
 void ref_gain_l(double* l_) {
   ref_setup_consts();

@@ -22,7 +22,7 @@ from test_gpu_parity import _compare
 
 pytestmark = pytest.mark.gpu
 
-KEYS = ("A", "B", "c", "L", "E", "Lh", "Eh")
+KEYS = ("A", "B", "c", "L", "E", "l", "Lh", "Eh")
 
 
 def _oracle_model(oracle, m):

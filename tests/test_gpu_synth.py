@@ -11,7 +11,7 @@ from conftest import GOLDEN
 
 pytestmark = pytest.mark.gpu
 
-KEYS = ("A", "B", "c", "L", "E", "Lh", "Eh")
+KEYS = ("A", "B", "c", "L", "E", "l", "Lh", "Eh")
 
 
 def perturbed_models(lqro_mod, n, seed=9, rel=0.01):

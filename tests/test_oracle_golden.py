@@ -223,3 +223,22 @@ def test_hull_cases_match_scipy_qhull(oracle):
         ours = sorted(tuple(sorted(int(v) for v in t)) for t in oracle.hull(pts))
         ref = sorted(tuple(sorted(int(v) for v in s)) for s in spatial.ConvexHull(pts).simplices)
         assert ours == ref, h
+
+
+def test_pseudo_inverse_matches_reference(oracle):
+    """pseudoInverse over jacobi2 (MAT:450-477, 887-1037), the kernel of l in
+    controlMatrices (LQRO:552), against the reference build
+    (tests/golden/pinv.npz: full rank, rank 4, symmetric, near-singular and
+    the closed loop of the reference's own model), bit for bit."""
+    d = _load("pinv.npz")
+    for q, ref in zip(d["inputs"], d["outputs"]):
+        got = oracle.pinv(q)
+        assert np.array_equal(got.view(np.uint64), ref.view(np.uint64))
+
+
+def test_feedforward_l_matches_reference(oracle):
+    """l of controlMatrices (LQRO:552-557) for the reference's model equals the
+    reference's (tests/golden/dyn.npz, ref_gain_l), sign of zero included."""
+    d = _load("dyn.npz")
+    got = oracle.synthesize()["l"]
+    assert np.array_equal(got.view(np.uint64), d["l"].view(np.uint64))
