@@ -37,25 +37,50 @@ __device__ __forceinline__ float stdmax(float a, float b) { return (a < b) ? b :
 __device__ __forceinline__ float stdmin(float a, float b) { return (b < a) ? b : a; }
 constexpr float kRvoEps = 0.00001f;
 
-// plane slot: {point.xyz, normal.xyz, flag, pad} (32 B)
+// A plane list holds {point.xyz, normal.xyz} per plane with a stride of PS
+// floats: PS = 8 is the 32-B slot k_pair writes ({.., flag, pad}, 16-B
+// aligned loads, global memory); PS = 6 packs the LDS copies (24 B a plane,
+// so a 4,095-plane row of C4 fits one CU's LDS).
 struct LPPlane { v3 point, normal; };
+template <int PS>
 __device__ __forceinline__ LPPlane ld_plane(const float* base, int i) {
-  const float4* p = reinterpret_cast<const float4*>(base + 8 * (size_t)i);
-  float4 a = p[0], b = p[1];
   LPPlane r;
-  r.point = V3(a.x, a.y, a.z);
-  r.normal = V3(a.w, b.x, b.y);
+  if constexpr (PS == 8) {
+    const float4* p = reinterpret_cast<const float4*>(base + 8 * (size_t)i);
+    float4 a = p[0], b = p[1];
+    r.point = V3(a.x, a.y, a.z);
+    r.normal = V3(a.w, b.x, b.y);
+  } else {
+    const float2* p = reinterpret_cast<const float2*>(base + 6 * (size_t)i);
+    float2 a = p[0], b = p[1], c = p[2];
+    r.point = V3(a.x, a.y, b.x);
+    r.normal = V3(b.y, c.x, c.y);
+  }
   return r;
+}
+template <int PS>
+__device__ __forceinline__ void st_plane(float* base, int i, v3 pt, v3 nm) {
+  if constexpr (PS == 8) {
+    float4* d = reinterpret_cast<float4*>(base + 8 * (size_t)i);
+    d[0] = make_float4(pt.x, pt.y, pt.z, nm.x);
+    d[1] = make_float4(nm.y, nm.z, 0.0f, 0.0f);
+  } else {
+    float2* d = reinterpret_cast<float2*>(base + 6 * (size_t)i);
+    d[0] = make_float2(pt.x, pt.y);
+    d[1] = make_float2(pt.z, nm.x);
+    d[2] = make_float2(nm.y, nm.z);
+  }
 }
 
 // first plane index in [i0, n) with normal.(point - r) > thresh, or n
+template <int PS>
 __device__ __forceinline__ int first_violated(const float* planes, int i0, int n, v3 r, float thresh,
                                               int lane) {
   for (int base = i0; base < n; base += 64) {
     const int i = base + lane;
     bool v = false;
     if (i < n) {
-      LPPlane p = ld_plane(planes, i);
+      LPPlane p = ld_plane<PS>(planes, i);
       v = vdot(p.normal, vsub(p.point, r)) > thresh;
     }
     unsigned long long b = __ballot(v);
@@ -64,6 +89,7 @@ __device__ __forceinline__ int first_violated(const float* planes, int i0, int n
   return n;
 }
 
+template <int PS>
 __device__ __forceinline__ bool w_lp1(const float* planes, int planeNo, v3 lpt, v3 ldir, float radius, v3 opt,
                       bool dirOpt, v3& result, int lane) {
   const float dotProduct = vdot(lpt, ldir);
@@ -75,7 +101,7 @@ __device__ __forceinline__ bool w_lp1(const float* planes, int planeNo, v3 lpt, 
   float lmax = -INFINITY, lmin = INFINITY;
   bool reject = false;
   for (int i = lane; i < planeNo; i += 64) {
-    LPPlane pi = ld_plane(planes, i);
+    LPPlane pi = ld_plane<PS>(planes, i);
     const float numerator = vdot(vsub(pi.point, lpt), pi.normal);
     const float denominator = vdot(ldir, pi.normal);
     if (sqrf(denominator) <= kRvoEps) {
@@ -107,9 +133,10 @@ __device__ __forceinline__ bool w_lp1(const float* planes, int planeNo, v3 lpt, 
   return true;
 }
 
+template <int PS>
 __device__ __forceinline__ bool w_lp2(const float* planes, int planeNo, float radius, v3 opt, bool dirOpt,
                       v3& result, int lane) {
-  const LPPlane pn = ld_plane(planes, planeNo);
+  const LPPlane pn = ld_plane<PS>(planes, planeNo);
   const float planeDist = vdot(pn.point, pn.normal);
   const float planeDistSq = sqrf(planeDist);
   const float radiusSq = sqrf(radius);
@@ -129,9 +156,9 @@ __device__ __forceinline__ bool w_lp2(const float* planes, int planeNo, float ra
       result = vadd(planeCenter, smul(sqrtf(planeRadiusSq / prSq), pr));
     }
   }
-  for (int i = first_violated(planes, 0, planeNo, result, 0.0f, lane); i < planeNo;
-       i = first_violated(planes, i + 1, planeNo, result, 0.0f, lane)) {
-    const LPPlane pi = ld_plane(planes, i);
+  for (int i = first_violated<PS>(planes, 0, planeNo, result, 0.0f, lane); i < planeNo;
+       i = first_violated<PS>(planes, i + 1, planeNo, result, 0.0f, lane)) {
+    const LPPlane pi = ld_plane<PS>(planes, i);
     v3 cp = vcross(pi.normal, pn.normal);
     if (vdot(cp, cp) <= kRvoEps) return false;
     const v3 ldir = vnormalize(cp);
@@ -139,27 +166,29 @@ __device__ __forceinline__ bool w_lp2(const float* planes, int planeNo, float ra
     const v3 lpt = vadd(pn.point, smul(vdot(vsub(pi.point, pn.point), pi.normal) /
                                            vdot(lineNormal, pi.normal),
                                        lineNormal));
-    if (!w_lp1(planes, i, lpt, ldir, radius, opt, dirOpt, result, lane)) return false;
+    if (!w_lp1<PS>(planes, i, lpt, ldir, radius, opt, dirOpt, result, lane)) return false;
   }
   return true;
 }
 
+template <int PS>
 __device__ __forceinline__ int w_lp3(const float* planes, int m, double radius, v3 opt, bool dirOpt, v3& result,
                      int lane) {
   const float rf = (float)radius;
   if (dirOpt) result = vmul(opt, rf);
   else if (vdot(opt, opt) > sqrf(rf)) result = vmul(vnormalize(opt), rf);
   else result = opt;
-  for (int i = first_violated(planes, 0, m, result, 0.0f, lane); i < m;
-       i = first_violated(planes, i + 1, m, result, 0.0f, lane)) {
+  for (int i = first_violated<PS>(planes, 0, m, result, 0.0f, lane); i < m;
+       i = first_violated<PS>(planes, i + 1, m, result, 0.0f, lane)) {
     const v3 tmp = result;
-    if (!w_lp2(planes, i, rf, opt, dirOpt, result, lane)) { result = tmp; return i; }
+    if (!w_lp2<PS>(planes, i, rf, opt, dirOpt, result, lane)) { result = tmp; return i; }
   }
   return m;
 }
 
 // linearProgram4: the projected planes of plane i are built in parallel and
 // compacted in j order (skipped same-direction parallels keep their order).
+template <int PS>
 __device__ __forceinline__ void w_lp4(const float* planes, int m, int beginPlane, float radius, v3& result,
                       float* proj, int lane
 #ifdef LQRO_LP_PROFILE
@@ -167,16 +196,16 @@ __device__ __forceinline__ void w_lp4(const float* planes, int m, int beginPlane
 #endif
                       ) {
   float distance = 0.0f;
-  for (int i = first_violated(planes, beginPlane, m, result, distance, lane); i < m;
-       i = first_violated(planes, i + 1, m, result, distance, lane)) {
-    const LPPlane pi = ld_plane(planes, i);
+  for (int i = first_violated<PS>(planes, beginPlane, m, result, distance, lane); i < m;
+       i = first_violated<PS>(planes, i + 1, m, result, distance, lane)) {
+    const LPPlane pi = ld_plane<PS>(planes, i);
     int np = 0;
     for (int base = 0; base < i; base += 64) {
       const int j = base + lane;
       bool keep = false;
       v3 ppt = V3(0, 0, 0), pnm = V3(0, 0, 0);
       if (j < i) {
-        const LPPlane pj = ld_plane(planes, j);
+        const LPPlane pj = ld_plane<PS>(planes, j);
         const v3 cp = vcross(pj.normal, pi.normal);
         keep = true;
         if (vdot(cp, cp) <= kRvoEps) {
@@ -191,19 +220,14 @@ __device__ __forceinline__ void w_lp4(const float* planes, int m, int beginPlane
         if (keep) pnm = vnormalize(vsub(pj.normal, pi.normal));
       }
       const unsigned long long b = __ballot(keep);
-      if (keep) {
-        const int pos = np + __popcll(b & ((1ull << lane) - 1ull));
-        float4* d = reinterpret_cast<float4*>(proj + 8 * (size_t)pos);
-        d[0] = make_float4(ppt.x, ppt.y, ppt.z, pnm.x);
-        d[1] = make_float4(pnm.y, pnm.z, 0.0f, 0.0f);
-      }
+      if (keep) st_plane<PS>(proj, np + __popcll(b & ((1ull << lane) - 1ull)), ppt, pnm);
       np += __popcll(b);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     const v3 tmp = result;
-    if (w_lp3(proj, np, radius, pi.normal, true, result, lane) < np) result = tmp;
+    if (w_lp3<PS>(proj, np, radius, pi.normal, true, result, lane) < np) result = tmp;
     distance = vdot(pi.normal, vsub(pi.point, result));
 #ifdef LQRO_LP_PROFILE
     ++lp4_iters;

@@ -210,7 +210,9 @@ struct LpArgs {
   int* lp4_next;
 };
 
-// one row's LP; `planes` holds its compacted plane list (LDS or global)
+// one row's LP; `planes` holds its compacted plane list (stride PS floats:
+// 6 in LDS, 8 in global memory)
+template <int PS>
 __device__ __forceinline__ void lp_row(const LpArgs& A, int lrow, float* planes, int lane) {
   const int i = A.row_begin + lrow;
   const float* src = A.slots + (size_t)lrow * A.npr * 8;
@@ -227,11 +229,8 @@ __device__ __forceinline__ void lp_row(const LpArgs& A, int lrow, float* planes,
       f = __float_as_int(b.z) == 1;
     }
     const unsigned long long bal = __ballot(f);
-    if (f) {
-      float4* d = reinterpret_cast<float4*>(planes + 8 * (size_t)(m + __popcll(bal & ((1ull << lane) - 1ull))));
-      d[0] = a;
-      d[1] = b;
-    }
+    if (f)
+      st_plane<PS>(planes, m + __popcll(bal & ((1ull << lane) - 1ull)), V3(a.x, a.y, a.z), V3(a.w, b.x, b.y));
     m += __popcll(bal);
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -239,20 +238,20 @@ __device__ __forceinline__ void lp_row(const LpArgs& A, int lrow, float* planes,
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   const v3 pref = V3((float)A.vgoal[3 * i], (float)A.vgoal[3 * i + 1], (float)A.vgoal[3 * i + 2]);
   v3 nv = V3(0.0f, 0.0f, 0.0f);
-  const int fail = w_lp3(planes, m, A.vmax, pref, false, nv, lane);          // :1228
+  const int fail = w_lp3<PS>(planes, m, A.vmax, pref, false, nv, lane);          // :1228
 #ifdef LQRO_LP_PROFILE
   int lp4_iters = 0;
   if (fail < m)
-    w_lp4(planes, m, fail, (float)A.vmax, nv, A.proj + (size_t)lrow * A.npr * 8, lane, lp4_iters);
+    w_lp4<PS>(planes, m, fail, (float)A.vmax, nv, A.proj + (size_t)lrow * A.npr * PS, lane, lp4_iters);
   if (lane == 0 && A.prof && lrow < 4096) A.prof[32 + 4096 + lrow] = ((unsigned long long)m << 40) |
                                                ((unsigned long long)fail << 20) | (unsigned)lp4_iters;
 #else
   if (fail < m && A.lp4_list != nullptr) {
     // linearProgram4 (:1230) in k_lp4, with its projected planes in LDS too:
-    // hand over the compacted planes and linearProgram3's result
+    // hand over the compacted planes (stride PS) and linearProgram3's result
     float* dst = A.compact + (size_t)lrow * A.npr * 8;
     if (dst != planes)
-      for (int q = lane; q < 8 * m; q += 64) dst[q] = planes[q];
+      for (int q = lane; q < PS * m; q += 64) dst[q] = planes[q];
     if (lane == 0) {
       const int k = atomicAdd(A.lp4_count, 1);
       int* e = A.lp4_list + 6 * (size_t)k;
@@ -262,7 +261,7 @@ __device__ __forceinline__ void lp_row(const LpArgs& A, int lrow, float* planes,
     return;
   }
   if (fail < m)
-    w_lp4(planes, m, fail, (float)A.vmax, nv, A.proj + (size_t)lrow * A.npr * 8, lane);  // :1230
+    w_lp4<PS>(planes, m, fail, (float)A.vmax, nv, A.proj + (size_t)lrow * A.npr * PS, lane);  // :1230
 #endif
   if (lane == 0) {
     A.newv[3 * i] = nv.x;
@@ -276,11 +275,11 @@ __global__ void __launch_bounds__(256) k_lp(LpArgs A) {
   const int lane = threadIdx.x & 63;
   const int lrow = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (lrow >= A.nrows) return;
-  lp_row(A, lrow, A.compact + (size_t)lrow * A.npr * 8, lane);
+  lp_row<8>(A, lrow, A.compact + (size_t)lrow * A.npr * 8, lane);
 }
 
-// one wave per workgroup, the row's plane list in LDS (the LP rescans it for
-// every violated plane: LDS round trips instead of L2 ones)
+// one wave per workgroup, the row's plane list in LDS at 24 B a plane (the LP
+// rescans it for every violated plane: LDS round trips instead of L2 ones)
 __global__ void __launch_bounds__(64) k_lp_lds(LpArgs A) {
   extern __shared__ float lp_planes[];
   const int lrow = blockIdx.x;
@@ -288,19 +287,19 @@ __global__ void __launch_bounds__(64) k_lp_lds(LpArgs A) {
 #ifdef LQRO_LP_PROFILE
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
-  lp_row(A, lrow, lp_planes, threadIdx.x);
+  lp_row<6>(A, lrow, lp_planes, threadIdx.x);
 #ifdef LQRO_LP_PROFILE
   if (threadIdx.x == 0 && lrow < 8192) A.prof[32 + lrow] = __builtin_amdgcn_s_memtime() - t0;
 #endif
 }
 
 // linearProgram4 for the rows k_lp_lds listed (one wave per row): the planes
-// AND the projected planes in LDS, so the O(m^2)
-// rescans of linearProgram4's inner linearProgram3 stay out of L2
-__global__ void __launch_bounds__(64) k_lp4(LpArgs A) {
+// in LDS, and their projections too when both fit (else the projections in
+// global memory), so the O(m^2) rescans of linearProgram4's inner
+// linearProgram3 stay out of L2
+__global__ void __launch_bounds__(64) k_lp4(LpArgs A, int proj_in_lds) {
   extern __shared__ float lp4_sm[];
   float* planes = lp4_sm;
-  float* proj = lp4_sm + (size_t)A.npr * 8;
   const int lane = threadIdx.x;
   {
     // one workgroup per listed row (a persistent loop over the list around
@@ -309,13 +308,14 @@ __global__ void __launch_bounds__(64) k_lp4(LpArgs A) {
     if (job >= *A.lp4_count) return;
     const int* e = A.lp4_list + 6 * (size_t)job;
     const int lrow = e[0], fail = e[1], m = e[2];
+    float* proj = proj_in_lds ? lp4_sm + (size_t)A.npr * 6 : A.proj + (size_t)lrow * A.npr * 6;
     v3 nv = V3(__int_as_float(e[3]), __int_as_float(e[4]), __int_as_float(e[5]));
     const float* src = A.compact + (size_t)lrow * A.npr * 8;
-    for (int q = lane; q < 8 * m; q += 64) planes[q] = src[q];
+    for (int q = lane; q < 6 * m; q += 64) planes[q] = src[q];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    w_lp4(planes, m, fail, (float)A.vmax, nv, proj, lane);                 // :1230
+    w_lp4<6>(planes, m, fail, (float)A.vmax, nv, proj, lane);               // :1230
     if (lane == 0) {
       const int i = A.row_begin + lrow;
       A.newv[3 * i] = nv.x;
@@ -325,23 +325,22 @@ __global__ void __launch_bounds__(64) k_lp4(LpArgs A) {
   }
 }
 
-constexpr size_t kLpLdsMax = 64 * 1024;
-constexpr size_t kLp4LdsMax = 128 * 1024;
+constexpr size_t kLpLdsMax = 160 * 1024;   // one CU's LDS
 
 // La.lp4_count / lp4_next must be zero (or lp4_list null)
 static hipError_t launch_lp(LpArgs La, hipStream_t s) {
-  const size_t lds = (size_t)La.npr * 32;
+  const size_t lds = (size_t)La.npr * 24;   // 6 floats a plane
   if (lds <= kLpLdsMax) {
     hipError_t e = hipFuncSetAttribute((const void*)k_lp_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)kLpLdsMax);
     if (e != hipSuccess) return e;
-    if (2 * lds > kLp4LdsMax) La.lp4_list = nullptr;
     hipLaunchKernelGGL(k_lp_lds, dim3((unsigned)La.nrows), dim3(64), lds, s, La);
     e = hipGetLastError();
     if (e != hipSuccess || La.lp4_list == nullptr) return e;
-    e = hipFuncSetAttribute((const void*)k_lp4, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLp4LdsMax);
+    e = hipFuncSetAttribute((const void*)k_lp4, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLpLdsMax);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_lp4, dim3((unsigned)La.nrows), dim3(64), 2 * lds, s, La);
+    const int proj_in_lds = 2 * lds <= kLpLdsMax;
+    hipLaunchKernelGGL(k_lp4, dim3((unsigned)La.nrows), dim3(64), proj_in_lds ? 2 * lds : lds, s, La, proj_in_lds);
   } else {
     La.lp4_list = nullptr;
     hipLaunchKernelGGL(k_lp, dim3((unsigned)((La.nrows + 3) / 4)), dim3(256), 0, s, La);

@@ -40,7 +40,8 @@ def test_batch_synthesis_bit_exact(lqro_mod, oracle):
 
 
 def test_batch_default_model_is_golden(lqro_mod):
-    ref = np.load(os.path.join(GOLDEN, "gains.npz"))
+    ref = dict(np.load(os.path.join(GOLDEN, "gains.npz")))
+    ref["l"] = np.load(os.path.join(GOLDEN, "dyn.npz"))["l"]      # ref_gain_l (LQRO:552-557)
     got = lqro_mod.synthesize_gains_batch([lqro_mod.default_model()] * 3)
     for key in KEYS:
         for k in range(3):
