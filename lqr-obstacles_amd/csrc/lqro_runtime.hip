@@ -278,8 +278,10 @@ __global__ void __launch_bounds__(256) k_lp(LpArgs A) {
   lp_row<8>(A, lrow, A.compact + (size_t)lrow * A.npr * 8, lane);
 }
 
-// one wave per workgroup, the row's plane list in LDS at 24 B a plane (the LP
-// rescans it for every violated plane: LDS round trips instead of L2 ones)
+// one wave per workgroup, the row's plane list in LDS (the LP rescans it for
+// every violated plane: LDS round trips instead of L2 ones), 32 B a plane
+// (16-B aligned loads) up to 2,048 planes, 24 B beyond (C4: 4,095)
+template <int PS>
 __global__ void __launch_bounds__(64) k_lp_lds(LpArgs A) {
   extern __shared__ float lp_planes[];
   const int lrow = blockIdx.x;
@@ -287,7 +289,7 @@ __global__ void __launch_bounds__(64) k_lp_lds(LpArgs A) {
 #ifdef LQRO_LP_PROFILE
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
-  lp_row<6>(A, lrow, lp_planes, threadIdx.x);
+  lp_row<PS>(A, lrow, lp_planes, threadIdx.x);
 #ifdef LQRO_LP_PROFILE
   if (threadIdx.x == 0 && lrow < 8192) A.prof[32 + lrow] = __builtin_amdgcn_s_memtime() - t0;
 #endif
@@ -297,6 +299,7 @@ __global__ void __launch_bounds__(64) k_lp_lds(LpArgs A) {
 // in LDS, and their projections too when both fit (else the projections in
 // global memory), so the O(m^2) rescans of linearProgram4's inner
 // linearProgram3 stay out of L2
+template <int PS>
 __global__ void __launch_bounds__(64) k_lp4(LpArgs A, int proj_in_lds) {
   extern __shared__ float lp4_sm[];
   float* planes = lp4_sm;
@@ -308,14 +311,14 @@ __global__ void __launch_bounds__(64) k_lp4(LpArgs A, int proj_in_lds) {
     if (job >= *A.lp4_count) return;
     const int* e = A.lp4_list + 6 * (size_t)job;
     const int lrow = e[0], fail = e[1], m = e[2];
-    float* proj = proj_in_lds ? lp4_sm + (size_t)A.npr * 6 : A.proj + (size_t)lrow * A.npr * 6;
+    float* proj = proj_in_lds ? lp4_sm + (size_t)A.npr * PS : A.proj + (size_t)lrow * A.npr * PS;
     v3 nv = V3(__int_as_float(e[3]), __int_as_float(e[4]), __int_as_float(e[5]));
     const float* src = A.compact + (size_t)lrow * A.npr * 8;
-    for (int q = lane; q < 6 * m; q += 64) planes[q] = src[q];
+    for (int q = lane; q < PS * m; q += 64) planes[q] = src[q];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    w_lp4<6>(planes, m, fail, (float)A.vmax, nv, proj, lane);               // :1230
+    w_lp4<PS>(planes, m, fail, (float)A.vmax, nv, proj, lane);              // :1230
     if (lane == 0) {
       const int i = A.row_begin + lrow;
       A.newv[3 * i] = nv.x;
@@ -327,24 +330,29 @@ __global__ void __launch_bounds__(64) k_lp4(LpArgs A, int proj_in_lds) {
 
 constexpr size_t kLpLdsMax = 160 * 1024;   // one CU's LDS
 
+template <int PS>
+static hipError_t launch_lp_lds(LpArgs La, hipStream_t s) {
+  const size_t lds = (size_t)La.npr * 4 * PS;
+  hipError_t e = hipFuncSetAttribute((const void*)k_lp_lds<PS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)kLpLdsMax);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_lp_lds<PS>, dim3((unsigned)La.nrows), dim3(64), lds, s, La);
+  e = hipGetLastError();
+  if (e != hipSuccess || La.lp4_list == nullptr) return e;
+  e = hipFuncSetAttribute((const void*)k_lp4<PS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLpLdsMax);
+  if (e != hipSuccess) return e;
+  const int proj_in_lds = 2 * lds <= kLpLdsMax;
+  hipLaunchKernelGGL(k_lp4<PS>, dim3((unsigned)La.nrows), dim3(64), proj_in_lds ? 2 * lds : lds, s, La,
+                     proj_in_lds);
+  return hipGetLastError();
+}
+
 // La.lp4_count / lp4_next must be zero (or lp4_list null)
 static hipError_t launch_lp(LpArgs La, hipStream_t s) {
-  const size_t lds = (size_t)La.npr * 24;   // 6 floats a plane
-  if (lds <= kLpLdsMax) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_lp_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)kLpLdsMax);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_lp_lds, dim3((unsigned)La.nrows), dim3(64), lds, s, La);
-    e = hipGetLastError();
-    if (e != hipSuccess || La.lp4_list == nullptr) return e;
-    e = hipFuncSetAttribute((const void*)k_lp4, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLpLdsMax);
-    if (e != hipSuccess) return e;
-    const int proj_in_lds = 2 * lds <= kLpLdsMax;
-    hipLaunchKernelGGL(k_lp4, dim3((unsigned)La.nrows), dim3(64), proj_in_lds ? 2 * lds : lds, s, La, proj_in_lds);
-  } else {
-    La.lp4_list = nullptr;
-    hipLaunchKernelGGL(k_lp, dim3((unsigned)((La.nrows + 3) / 4)), dim3(256), 0, s, La);
-  }
+  if ((size_t)La.npr * 32 <= 64 * 1024) return launch_lp_lds<8>(La, s);
+  if ((size_t)La.npr * 24 <= kLpLdsMax) return launch_lp_lds<6>(La, s);
+  La.lp4_list = nullptr;
+  hipLaunchKernelGGL(k_lp, dim3((unsigned)((La.nrows + 3) / 4)), dim3(256), 0, s, La);
   return hipGetLastError();
 }
 
