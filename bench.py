@@ -132,7 +132,7 @@ def cpu_baseline(x, vg, gains, seconds_target=10.0):
                       f"({N_AGENTS - 1} pairs per row)"}
 
 
-def closed_loop(lqro, torch, dev, x, vg, gains, reps, world=1, dist=None, rank=0):
+def closed_loop(lqro, torch, dev, x, vg, gains, reps, world=1, dist=None, rank=0, mode="block"):
     """The whole control step on the GPU, measured after the timed steps:
     lqro.DeviceLoop — the pair step, then the agent loop LQRO:1437-1446
     (k_dynw: findU, propagate, kalmanFilter1/2, findVGoal) on this rank's
@@ -142,7 +142,7 @@ def closed_loop(lqro, torch, dev, x, vg, gains, reps, world=1, dist=None, rank=0
     buffers start from the bench's swarm, so the roofline probe after it sees
     the timed steps' inputs."""
     loop = lqro.DeviceLoop(x, vg, dict(gains, l=np.zeros(4)), HORIZON, N_POINTS,
-                           rank=rank, world=world, dist=dist, device=dev)
+                           rank=rank, world=world, dist=dist, device=dev, rows=mode)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     it_ms, its, dms = [], [], []
     for _ in range(reps):
@@ -159,7 +159,7 @@ def closed_loop(lqro, torch, dev, x, vg, gains, reps, world=1, dist=None, rank=0
         its.append({"pair_ms": round(tm["pair_ms"], 3), "hull_ms": round(tm["hull_ms"], 3),
                     "lp_ms": round(tm["lp_ms"], 3), "inside": loop.ctx.stats()["inside"]})
     loop.close()
-    return {"kernel": "k_dynw", "agents": loop.re - loop.rb,
+    return {"kernel": "k_dynw", "agents": len(loop.ids_h),
             "dynamics_plus_gather_ms": float(np.mean(dms)),
             "pair_step_plus_dynamics_ms": float(np.mean(it_ms)),
             "iteration_ms": [round(t, 3) for t in it_ms], "iterations": its,
@@ -167,7 +167,7 @@ def closed_loop(lqro, torch, dev, x, vg, gains, reps, world=1, dist=None, rank=0
                     "dynamics_plus_gather_ms from events on the launch stream"}
 
 
-def config_runs(lqro, torch, dev, local, world, rank, dist, steps):
+def config_runs(lqro, torch, dev, local, world, rank, dist, steps, mode="block"):
     """BASELINE configs 4 and 5 beside the headline (never in `value`):
     strong scaling — the whole swarm's rows sharded over the ranks, the
     per-step exchange as in the headline; max over ranks of the time for
@@ -176,7 +176,7 @@ def config_runs(lqro, torch, dev, local, world, rank, dist, steps):
     models (synthesised on the GPU), H = 200."""
     out = {}
     for name, N, H, X in (("c4", 4096, 100, 16), ("c5", 16384, 200, 12)):
-        rb, re = lqro.row_shard(N, rank, world)
+        sh = lqro.shard_rows(N, rank, world, mode)
         x, vg = lqro.synthetic_swarm(N, x_dim=X)
         if name == "c5":
             g = lqro.synthesize_gains_batch(lqro.perturbed_models(N), device=local, x_dim=X)
@@ -184,7 +184,7 @@ def config_runs(lqro, torch, dev, local, world, rank, dist, steps):
             gains, per_agent = dict(A=g0["A"], B=g0["B"], L=g["L"], E=g["E"]), True
         else:
             gains, per_agent = lqro.synthesize_gains(), False
-        ctx = lqro.Context(lqro.config(N, H, N_POINTS, x_dim=X, device=local, row_begin=rb, row_end=re))
+        ctx = lqro.Context(lqro.config(N, H, N_POINTS, x_dim=X, device=local, **sh))
         ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"], per_agent=per_agent)
         d_x = torch.from_numpy(x).to(dev)
         d_vg = torch.from_numpy(vg).to(dev)
@@ -193,7 +193,7 @@ def config_runs(lqro, torch, dev, local, world, rank, dist, steps):
         def step():
             ctx.step_device(d_x.data_ptr(), d_vg.data_ptr(), d_newv.data_ptr(), 0)
             if world > 1:
-                lqro.allgather_rows(dist, d_newv, rank, world)
+                lqro.allgather_rows(dist, d_newv, rank, world, mode=mode)
         step()
         torch.cuda.synchronize(dev)
         if world > 1:
@@ -230,6 +230,8 @@ def main():
                     help="swarm size (default: round(1024 sqrt(world)), C3's pairs per GPU)")
     ap.add_argument("--no-roofline-probe", action="store_true")
     ap.add_argument("--no-configs", action="store_true", help="skip the C4 / C5 strong-scaling runs")
+    ap.add_argument("--rows", choices=("block", "cyclic"), default=os.environ.get("LQRO_ROWS", "block"),
+                    help="row sharding over ranks: contiguous blocks or cyclic (row_stride = world)")
     args = ap.parse_args()
 
     import torch
@@ -256,11 +258,11 @@ def main():
     torch.cuda.set_device(dev)
 
     N = args.agents if args.agents > 0 else int(round(N_AGENTS * world ** 0.5))
-    rb, re = lqro.row_shard(N, rank, world)
-    rows = re - rb
+    sh = lqro.shard_rows(N, rank, world, args.rows)
+    rows = len(lqro.shard_row_ids(N, rank, world, args.rows))
     x, vg = lqro.synthetic_swarm(N)
     gains = lqro.synthesize_gains()
-    ctx = lqro.Context(lqro.config(N, HORIZON, N_POINTS, device=local, row_begin=rb, row_end=re))
+    ctx = lqro.Context(lqro.config(N, HORIZON, N_POINTS, device=local, **sh))
     ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
     d_x = torch.from_numpy(x).to(dev)
     d_vg = torch.from_numpy(vg).to(dev)
@@ -270,7 +272,7 @@ def main():
     def step():
         ctx.step_device(d_x.data_ptr(), d_vg.data_ptr(), d_newv.data_ptr(), stream.cuda_stream)
         if world > 1:
-            lqro.allgather_rows(dist, d_newv, rank, world)
+            lqro.allgather_rows(dist, d_newv, rank, world, mode=args.rows)
 
     for _ in range(args.warmup):
         step()
@@ -311,12 +313,12 @@ def main():
     # the closed loop runs before the probe creates a second context (whose
     # stream can share a hardware queue with this context's side stream)
     ctx.close()   # one context at a time: a second one's streams can share hardware queues
-    closed = closed_loop(lqro, torch, dev, x, vg, gains, min(args.steps, 5), world, dist, rank)
+    closed = closed_loop(lqro, torch, dev, x, vg, gains, min(args.steps, 5), world, dist, rank, args.rows)
     pk_ms = sweep_ms
     probe = "sweep (k_prio + k_pair launches + overlapped side hull), timed steps"
     if not args.no_roofline_probe:
         os.environ["LQRO_HOT"] = "0"
-        pctx = lqro.Context(lqro.config(N, HORIZON, N_POINTS, device=local, row_begin=rb, row_end=re))
+        pctx = lqro.Context(lqro.config(N, HORIZON, N_POINTS, device=local, **sh))
         del os.environ["LQRO_HOT"]
         pctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
         pk = []
@@ -350,7 +352,7 @@ def main():
                         "reference-exact fp64 pair sweep+GJK+hull+half-plane, fp32 LP",
             "n_agents": N, "horizon": HORIZON, "n_points": N_POINTS, "x_dim": X_DIM,
             "pairs_per_step": pairs_step,
-            "parallelism": f"rows sharded over {world} rank(s)" +
+            "parallelism": f"rows sharded ({args.rows}) over {world} rank(s)" +
                            ((" + RCCL all-gather of newV" if backend == "nccl" else f" + {backend} all-gather of newV")
                             if world > 1 else ""),
         },
@@ -379,7 +381,7 @@ def main():
         "hull_failures": st["hull_fail"],
     }
     if not args.no_configs:
-        out["configs"] = config_runs(lqro, torch, dev, local, world, rank, dist, 2)
+        out["configs"] = config_runs(lqro, torch, dev, local, world, rank, dist, 2, args.rows)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(x, vg, gains)
         out["cpu_baseline"] = cb

@@ -64,6 +64,9 @@ typedef struct lqro_config {
   int32_t row_end;       /*   (multi-GPU sharding; 0,0 = all rows)                 */
   int32_t device;        /* HIP device ordinal                                    */
   int32_t flags;         /* LQRO_FLAG_*                                           */
+  int32_t row_stride;    /* 0/1: rows row_begin..row_end-1; s > 1: rows row_begin,  */
+                         /*   row_begin+s, ... < row_end (cyclic sharding: rank,  */
+                         /*   world); records, newv rows and the LP follow it      */
 } lqro_config;
 
 /* Physical model + cost weights: the globals set by setup() and _tmain

@@ -70,6 +70,7 @@ struct HullWide;
 struct HullArgs {
   int N, X, H, NP;
   int row_begin, npr, per_agent;
+  int row_stride;                   // local row r is agent row_begin + r * row_stride
   const int* nbr_list;   // culling on: slot -> neighbour jj (see PairArgs), else null
   double r2, r2_lo, r2_hi;
   const double* T;
@@ -1391,7 +1392,7 @@ __device__ __forceinline__ void hull_body_mw(const HullArgs& A, HullMemC& M, Hul
     const int slot = hull_take_job(A, L, false);
     if (slot < 0) break;
     const int lrow = slot / A.npr, jj = A.nbr_list ? A.nbr_list[slot] : slot % A.npr;
-    const int i = A.row_begin + lrow;
+    const int i = A.row_begin + lrow * A.row_stride;
     const int j = jj < i ? jj : jj + 1;
     const double* xi = A.x + (size_t)i * A.X;
     const double* xj = A.x + (size_t)j * A.X;
@@ -1535,7 +1536,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
     const int slot = hull_take_job(A, L, retryq);
     if (slot < 0) break;
     const int lrow = slot / A.npr, jj = A.nbr_list ? A.nbr_list[slot] : slot % A.npr;
-    const int i = A.row_begin + lrow;
+    const int i = A.row_begin + lrow * A.row_stride;
     const int j = jj < i ? jj : jj + 1;
     const double* xi = A.x + (size_t)i * A.X;
     const double* xj = A.x + (size_t)j * A.X;

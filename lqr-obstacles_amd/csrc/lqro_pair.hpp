@@ -44,6 +44,7 @@ constexpr int kMaxKS = 4;   // H <= 64 kMaxKS = 256 (per-lane slice slots)
 struct PairArgs {
   int N, H, NP, PW, min_reach;
   int row_begin, nrows, npr;          // npr = pairs per row = N-1
+  int row_stride;                     // local row r is agent row_begin + r * row_stride
   int waves;
   int max_waves;                      // waves of a workgroup that take pairs (k_side's LDS fits fewer)
   int* row_counter;                   // persistent row queue (zeroed per step)
@@ -624,14 +625,14 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
       if constexpr (HOT == kHotPerAgent) {
         // per-agent gains: the row agent's tables straight from global memory
         // (the workgroup's waves work on pairs of different rows)
-        const size_t i = (size_t)(P.row_begin + lrow);
+        const size_t i = (size_t)P.row_begin + (size_t)lrow * P.row_stride;
         B.T = P.T + i * H * 9;
         B.N = P.NCF + i * H * 3 * X;
         B.pitch = X;
         B.R = P.R + i * H;
         B.TF = P.TF + i * H;
       }
-      do_pair(P.row_begin + lrow, lrow, slot - lrow * P.npr);
+      do_pair(P.row_begin + lrow * P.row_stride, lrow, slot - lrow * P.npr);
     }
   } else {
   // Persistent: the workgroup takes whole rows (agent i) off a queue; its
@@ -652,7 +653,7 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
     if (unit >= P.nrows * P.row_split) break;
     const int lrow = unit / P.row_split;
     const int jj_end = (int)((long)(unit % P.row_split + 1) * P.npr / P.row_split);
-    const int i = P.row_begin + lrow;
+    const int i = P.row_begin + lrow * P.row_stride;
     const long ag = P.per_agent ? (long)i : 0;
     if (ag != staged) {
       const double* Ti = P.T + ag * H * 9;
@@ -713,12 +714,13 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
 // Found by k rounds of a wave arg-min above the previous key; writes the
 // row's list of K = min(k, npr) slots (neighbour jj ascending, -1 padded)
 // and counts the kept pairs into stats[0].
-__global__ void __launch_bounds__(64) k_nbr(const double* x, int X, int N, int row_begin, int npr, double r2,
+__global__ void __launch_bounds__(64) k_nbr(const double* x, int X, int N, int row_begin, int row_stride, int npr,
+                                            double r2,
                                             int k, int K, int* list, unsigned long long* stats) {
   constexpr int kCap = 1024;   // candidates within r held in LDS
   __shared__ double cd[kCap];
   __shared__ int cj[kCap];
-  const int lrow = blockIdx.x, lane = threadIdx.x, i = row_begin + lrow;
+  const int lrow = blockIdx.x, lane = threadIdx.x, i = row_begin + lrow * row_stride;
   const double* xi = x + (size_t)i * X;
   // one scan: the agents within r (ascending j), usually a few dozen
   int ncand = 0;
@@ -814,7 +816,7 @@ __global__ void __launch_bounds__(64) k_nbr(const double* x, int X, int N, int r
 // sweep.  A heuristic for ORDER only: a missed or extra pair changes no
 // result, only when its hull starts.
 struct PrioArgs {
-  int npr, nrows, row_begin, X;
+  int npr, nrows, row_begin, row_stride, X;
   const double* x;
   double t_hot, r2_hot;
   int* list;
@@ -831,7 +833,7 @@ __global__ void __launch_bounds__(256) k_prio(PrioArgs A) {
     bool hot = false;
     if (slot < total) {
       const int lrow = (int)(slot / A.npr), jj = (int)(slot - (long)lrow * A.npr);
-      const int i = A.row_begin + lrow, j = jj < i ? jj : jj + 1;
+      const int i = A.row_begin + lrow * A.row_stride, j = jj < i ? jj : jj + 1;
       const double* xi = A.x + (size_t)i * A.X;
       const double* xj = A.x + (size_t)j * A.X;
       const double p0 = xi[0] - xj[0], p1 = xi[1] - xj[1], p2 = xi[2] - xj[2];

@@ -196,7 +196,7 @@ __global__ void __launch_bounds__(256) k_tables(int X, int U, int H, const doubl
 // LP kernel: one wavefront per row agent (lqro_lp.hpp), fp32 as the reference
 // ---------------------------------------------------------------------------
 struct LpArgs {
-  int npr, nrows, row_begin;
+  int npr, nrows, row_begin, row_stride;
   double vmax;
   const float* slots;   // per row npr x 8 (flag in [6]: 1 = plane)
   float* compact;       // per row npr x 8: emitted planes in j order
@@ -214,7 +214,7 @@ struct LpArgs {
 // 6 in LDS, 8 in global memory)
 template <int PS>
 __device__ __forceinline__ void lp_row(const LpArgs& A, int lrow, float* planes, int lane) {
-  const int i = A.row_begin + lrow;
+  const int i = A.row_begin + lrow * A.row_stride;
   const float* src = A.slots + (size_t)lrow * A.npr * 8;
   // orcaPlanes_ in push order (j order, LQRObstacles.cpp:1220)
   int m = 0;
@@ -320,7 +320,7 @@ __global__ void __launch_bounds__(64) k_lp4(LpArgs A, int proj_in_lds) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     w_lp4<PS>(planes, m, fail, (float)A.vmax, nv, proj, lane);              // :1230
     if (lane == 0) {
-      const int i = A.row_begin + lrow;
+      const int i = A.row_begin + lrow * A.row_stride;
       A.newv[3 * i] = nv.x;
       A.newv[3 * i + 1] = nv.y;
       A.newv[3 * i + 2] = nv.z;
@@ -363,7 +363,7 @@ struct lqro_ctx {
   lqro_config cfg;
   double *d_R, *d_TF, umax;
   unsigned long long* d_shash;
-  int rb, re, nrows, npr;
+  int rb, re, rs, nrows, npr;   // rows rb, rb + rs, ... < re
   int have_gains, per_agent;
   hipStream_t stream;
   hipEvent_t ev[5];
@@ -483,6 +483,7 @@ void lqro_config_default(lqro_config* c, int32_t n, int32_t h, int32_t np) {
   c->vmax_lp = 100.0;
   c->row_begin = 0;
   c->row_end = 0;
+  c->row_stride = 0;
   c->device = 0;
   c->flags = 0;
 }
@@ -601,8 +602,9 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
   c->rb = g.row_begin;
   c->re = (g.row_end > g.row_begin) ? g.row_end : g.n_agents;
   if (g.row_end == 0 && g.row_begin == 0) { c->rb = 0; c->re = g.n_agents; }
-  if (c->rb < 0 || c->re > g.n_agents || c->rb >= c->re) { delete c; return LQRO_E_ARG; }
-  c->nrows = c->re - c->rb;
+  c->rs = g.row_stride > 1 ? g.row_stride : 1;
+  if (c->rb < 0 || c->re > g.n_agents || c->rb >= c->re || g.row_stride < 0) { delete c; return LQRO_E_ARG; }
+  c->nrows = (c->re - c->rb + c->rs - 1) / c->rs;
   c->npr = g.n_agents - 1;
   // LDS layout of k_pair (in doubles): block tables, then one region per wave
   const int H = g.horizon, NP = g.n_points, X = g.x_dim, XP = X + 1;
@@ -736,7 +738,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   P.N = g.n_agents; P.H = g.horizon; P.NP = g.n_points; P.min_reach = g.min_reach;
   // culling on: each row's slots are its K neighbours (k_nbr), not its N-1 pairs
   const int npr = c->nbr_k > 0 ? std::min(c->nbr_k, c->npr) : c->npr;
-  P.row_begin = c->rb; P.nrows = c->nrows; P.npr = npr;
+  P.row_begin = c->rb; P.row_stride = c->rs; P.nrows = c->nrows; P.npr = npr;
   P.per_agent = c->per_agent;
   P.vmax = g.vmax_reach;
   P.r2 = g.vmax_reach * g.vmax_reach;
@@ -765,7 +767,8 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   HIPCHK(hipMemsetAsync(c->d_hq, 0xFF, sizeof(int) * (size_t)c->hull_cap, s));
   P.nbr_list = nullptr;
   if (c->nbr_k > 0) {
-    hipLaunchKernelGGL(k_nbr, dim3((unsigned)c->nrows), dim3(64), 0, s, d_x, g.x_dim, g.n_agents, c->rb, c->npr,
+    hipLaunchKernelGGL(k_nbr, dim3((unsigned)c->nrows), dim3(64), 0, s, d_x, g.x_dim, g.n_agents, c->rb, c->rs,
+                       c->npr,
                        c->nbr_r2, c->nbr_k, npr, c->d_nbrlist, c->d_stats);
     HIPCHK(hipGetLastError());
     P.nbr_list = c->d_nbrlist;
@@ -794,7 +797,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   P.hot_next = nullptr; P.hot_cap = 0; P.hot_only = 0;
   if (hot) {
     PrioArgs Q;
-    Q.npr = c->npr; Q.nrows = c->nrows; Q.row_begin = c->rb; Q.X = g.x_dim; Q.x = d_x;
+    Q.npr = c->npr; Q.nrows = c->nrows; Q.row_begin = c->rb; Q.row_stride = c->rs; Q.X = g.x_dim; Q.x = d_x;
     Q.t_hot = c->hot_t; Q.r2_hot = c->hot_r * c->hot_r;   // seconds, metres (scheduling heuristic)
     Q.list = c->d_hotlist; Q.mark = c->d_hotmark; Q.count = c->d_hcount + 6; Q.cap = c->hot_cap;
     const long nb = std::min<long>((slots + 255) / 256, 8L * c->n_cu);
@@ -805,7 +808,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   }
   HullArgs Hh;
   Hh.N = g.n_agents; Hh.X = g.x_dim; Hh.H = g.horizon; Hh.NP = g.n_points;
-  Hh.row_begin = c->rb; Hh.npr = npr; Hh.per_agent = c->per_agent;
+  Hh.row_begin = c->rb; Hh.row_stride = c->rs; Hh.npr = npr; Hh.per_agent = c->per_agent;
   Hh.nbr_list = P.nbr_list;
   Hh.r2 = P.r2; Hh.r2_lo = P.r2_lo; Hh.r2_hi = P.r2_hi;
   Hh.T = c->d_T; Hh.NCF = c->d_NCF; Hh.S = c->d_S; Hh.x = d_x;
@@ -857,7 +860,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev[2], s));
   LpArgs La;
-  La.npr = npr; La.nrows = c->nrows; La.row_begin = c->rb; La.vmax = g.vmax_lp;
+  La.npr = npr; La.nrows = c->nrows; La.row_begin = c->rb; La.row_stride = c->rs; La.vmax = g.vmax_lp;
   La.slots = c->d_planes; La.compact = c->d_lpcompact; La.proj = c->d_lpscratch;
   La.vgoal = d_vgoal; La.newv = d_newv; La.prof = c->d_prof;
   La.lp4_list = c->d_lp4; La.lp4_count = c->d_hcount + 9; La.lp4_next = c->d_hcount + 10;
@@ -888,9 +891,19 @@ int lqro_step(lqro_ctx* c, const double* x, const double* vgoal, double* newv) {
   HIPCHK(hipMemcpyAsync(c->d_vgoal, vgoal, sizeof(double) * N * 3, hipMemcpyHostToDevice, c->stream));
   int rc = enqueue_step(c, c->d_x, c->d_vgoal, c->d_newv, c->stream);
   if (rc) return rc;
-  HIPCHK(hipMemcpyAsync(newv + (size_t)c->rb * 3, c->d_newv + (size_t)c->rb * 3,
-                        sizeof(double) * 3 * c->nrows, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  if (c->rs == 1) {
+    HIPCHK(hipMemcpyAsync(newv + (size_t)c->rb * 3, c->d_newv + (size_t)c->rb * 3,
+                          sizeof(double) * 3 * c->nrows, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+  } else {   // cyclic rows: the whole array, then this context's rows
+    std::vector<double> all(N * 3);
+    HIPCHK(hipMemcpyAsync(all.data(), c->d_newv, sizeof(double) * 3 * N, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (int r = 0; r < c->nrows; ++r) {
+      const size_t i = (size_t)c->rb + (size_t)r * c->rs;
+      for (int q = 0; q < 3; ++q) newv[3 * i + q] = all[3 * i + q];
+    }
+  }
   int hc = 0;
   HIPCHK(hipMemcpy(&hc, c->d_hcount, sizeof(int), hipMemcpyDeviceToHost));
   if (hc > c->hull_cap) return LQRO_E_OVERFLOW;
@@ -1148,7 +1161,7 @@ int lqro_calculate_new_v(const float* planes, const int64_t* offsets, int32_t n_
     rc = LQRO_E_HIP;
   } else {
     LpArgs La;
-    La.npr = (int)mmax; La.nrows = n_agents; La.row_begin = 0; La.vmax = vmax_lp;
+    La.npr = (int)mmax; La.nrows = n_agents; La.row_begin = 0; La.row_stride = 1; La.vmax = vmax_lp;
     La.slots = d_slots; La.compact = d_compact; La.proj = d_proj; La.vgoal = d_vg; La.newv = d_nv; La.prof = nullptr;
     La.lp4_list = d_l4; La.lp4_count = d_l4c; La.lp4_next = d_l4c + 1;
     if (launch_lp(La, 0) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||

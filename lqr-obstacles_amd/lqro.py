@@ -36,7 +36,7 @@ class Config(C.Structure):
         ("xy_radius", C.c_double), ("z_radius", C.c_double),
         ("vmax_reach", C.c_double), ("vmax_lp", C.c_double),
         ("row_begin", C.c_int32), ("row_end", C.c_int32),
-        ("device", C.c_int32), ("flags", C.c_int32),
+        ("device", C.c_int32), ("flags", C.c_int32), ("row_stride", C.c_int32),
     ]
 
 
@@ -221,6 +221,7 @@ class Context:
         if rb == 0 and re == 0:
             re = cfg.n_agents
         self.rows = (rb, re)
+        self.row_ids = np.arange(rb, re, max(cfg.row_stride, 1))   # the agents whose rows this computes
 
     def close(self):
         if self._h:
@@ -272,7 +273,7 @@ class Context:
                "lqro_step_device")
 
     def records(self) -> np.ndarray:
-        n = (self.rows[1] - self.rows[0]) * (self.cfg.n_agents - 1)
+        n = len(self.row_ids) * (self.cfg.n_agents - 1)
         out = np.zeros(n, dtype=RECORD_DTYPE)
         got = C.c_int64()
         _check(lib().lqro_get_records(self._h, _p(out), n, C.byref(got)), "lqro_get_records")
@@ -534,6 +535,9 @@ class Simulator:
 # ---------------------------------------------------------------------------
 # Multi-GPU: rows (agents i) block-sharded over ranks
 # ---------------------------------------------------------------------------
+ROW_MODES = ("block", "cyclic")
+
+
 def row_shard(n_agents: int, rank: int, world: int) -> tuple[int, int]:
     """Rows [rb, re) owned by `rank`: balanced contiguous blocks (sizes
     differ by at most one).  Every pair (i, j) of row i is computed by the
@@ -543,18 +547,48 @@ def row_shard(n_agents: int, rank: int, world: int) -> tuple[int, int]:
     return rank * n_agents // world, (rank + 1) * n_agents // world
 
 
-def allgather_rows(dist, full, rank: int, world: int, group=None):
+def shard_rows(n_agents: int, rank: int, world: int, mode: str = "block") -> dict:
+    """The lqro_config fields of `rank`'s shard.  "block": row_shard's
+    contiguous rows.  "cyclic": rows rank, rank + world, ... (row_stride =
+    world) — agents that crowd into one region of the index space (a
+    formation, the hull-heavy rows of SURVEY §8e) spread over every rank
+    instead of loading one."""
+    if mode not in ROW_MODES:
+        raise ValueError(f"row mode {mode!r} not in {ROW_MODES}")
+    if mode == "block":
+        rb, re = row_shard(n_agents, rank, world)
+        return dict(row_begin=rb, row_end=re, row_stride=0)
+    if not (0 <= rank < world) or n_agents < world:
+        raise ValueError(f"cannot shard {n_agents} agents over {world} ranks")
+    return dict(row_begin=rank, row_end=n_agents, row_stride=world if world > 1 else 0)
+
+
+def shard_row_ids(n_agents: int, rank: int, world: int, mode: str = "block") -> np.ndarray:
+    f = shard_rows(n_agents, rank, world, mode)
+    return np.arange(f["row_begin"], f["row_end"], max(f["row_stride"], 1))
+
+
+def allgather_rows(dist, full, rank: int, world: int, group=None, mode: str = "block"):
     """The per-step exchange: every rank holds its own rows of `full`
-    (an (N, k) tensor, rows from row_shard); afterwards every rank holds all
-    rows.  One all-gather of equal ceil(N/world)-row chunks — RCCL over xGMI
-    with the "nccl" backend, gloo on the CPU."""
+    (an (N, k) tensor, rows from shard_rows(mode)); afterwards every rank
+    holds all rows.  One all-gather of equal ceil(N/world)-row chunks — RCCL
+    over xGMI with the "nccl" backend, gloo on the CPU."""
     import torch
 
     n = full.shape[0]
     chunk = -(-n // world)
-    rb, re = row_shard(n, rank, world)
+
+    def own(r):
+        if mode == "cyclic":
+            return full[r::world]
+        b, e = row_shard(n, r, world)
+        return full[b:e]
+
+    if mode not in ROW_MODES:
+        raise ValueError(f"row mode {mode!r} not in {ROW_MODES}")
+    mine = own(rank)
     send = torch.zeros((chunk,) + tuple(full.shape[1:]), dtype=full.dtype, device=full.device)
-    send[: re - rb] = full[rb:re]
+    send[: mine.shape[0]] = mine
     recv = torch.empty((chunk * world,) + tuple(full.shape[1:]), dtype=full.dtype,
                        device=full.device)
     if dist.get_backend(group) == "nccl":
@@ -562,14 +596,15 @@ def allgather_rows(dist, full, rank: int, world: int, group=None):
     else:
         dist.all_gather(list(recv.chunk(world)), send, group=group)
     for r in range(world):
-        b, e = row_shard(n, r, world)
-        full[b:e] = recv[r * chunk: r * chunk + (e - b)]
+        dst = own(r)
+        dst.copy_(recv[r * chunk: r * chunk + dst.shape[0]])
     return full
 
 
 class DeviceLoop:
     """The whole control loop LQRO:1391-1446 on device buffers, for the rows
-    [rb, re) this rank owns: ``step()`` is the pair loop (lqro_step_device),
+    this rank owns (rows="block": [rb, re); "cyclic": rank, rank + world, ...,
+    gathered into contiguous copies around the dynamics): ``step()`` is the pair loop (lqro_step_device),
     ``update()`` the agent loop after it (vGoal = newV, lqro_dynamics_step_device
     on the own rows), then the single exchange per step: an all-gather of the
     new estimates x.  Every launch goes on `stream` (default:
@@ -583,20 +618,24 @@ class DeviceLoop:
 
     def __init__(self, x0, vgoal0, gains: dict, horizon: int, n_points: int = 100, *,
                  p_goal=None, rank: int = 0, world: int = 1, dist=None, device=None,
-                 model: Model | None = None, seed: int = 1, stream=None):
+                 model: Model | None = None, seed: int = 1, stream=None, rows: str = "block"):
         import torch
         self.torch = torch
         self.dev = torch.device("cuda", torch.cuda.current_device()) if device is None else device
         self.stream = stream if stream is not None else torch.cuda.current_stream(self.dev)
         n = x0.shape[0]
         self.n, self.rank, self.world, self.dist = n, rank, world, dist
-        self.rb, self.re = row_shard(n, rank, world)
-        rows = self.re - self.rb
+        self.mode = rows
+        sh = shard_rows(n, rank, world, rows)
+        ids = shard_row_ids(n, rank, world, rows)
+        self.rb, self.re = int(ids[0]), int(ids[-1]) + 1     # block mode: the own rows [rb, re)
+        rows = len(ids)
         self.model = model or default_model()
         self.seed = seed
         f64 = dict(dtype=torch.float64, device=self.dev)
-        self.ctx = Context(config(n, horizon, n_points, device=self.dev.index,
-                                  row_begin=self.rb, row_end=self.re))
+        self.ctx = Context(config(n, horizon, n_points, device=self.dev.index, **sh))
+        self.ids_h = ids
+        self.ids = torch.from_numpy(ids.astype(np.int64)).to(self.dev)
         self.ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
         self.x = torch.from_numpy(np.ascontiguousarray(x0, np.float64)).to(self.dev)
         self.vgoal = torch.from_numpy(np.ascontiguousarray(vgoal0, np.float64)).to(self.dev)
@@ -604,10 +643,10 @@ class DeviceLoop:
         eye3 = torch.eye(3, **f64).repeat(rows, 1, 1).contiguous()
         hover = self.model.gravity * self.model.mass / 4
         pg = np.zeros((n, 3)) if p_goal is None else np.asarray(p_goal, np.float64)
-        self.own = dict(rot=eye3.clone(), x_true=self.x[self.rb:self.re].clone(), rot_true=eye3.clone(),
+        self.own = dict(rot=eye3.clone(), x_true=self.x[self.ids].clone(), rot_true=eye3.clone(),
                         P=(1e-9 * torch.eye(16, **f64)).repeat(rows, 1, 1).contiguous(),
                         u_goal=torch.full((rows, 4), hover, **f64),
-                        p_goal=torch.from_numpy(np.ascontiguousarray(pg[self.rb:self.re])).to(self.dev))
+                        p_goal=torch.from_numpy(np.ascontiguousarray(pg[ids])).to(self.dev))
         self.g = {k: torch.from_numpy(np.ascontiguousarray(gains[k], np.float64)).to(self.dev)
                   for k in ("L", "E", "Lh", "Eh")}
         self.g["l"] = torch.from_numpy(np.ascontiguousarray(gains.get("l", np.zeros(4)), np.float64)).to(self.dev)
@@ -626,32 +665,44 @@ class DeviceLoop:
         self.ctx.step_device(self.x.data_ptr(), self.vgoal.data_ptr(), self.newv.data_ptr(), self._sid())
         if gather and self.world > 1:
             with self.torch.cuda.stream(self.stream):
-                allgather_rows(self.dist, self.newv, self.rank, self.world)
+                allgather_rows(self.dist, self.newv, self.rank, self.world, mode=self.mode)
         return self.newv
+
+    def own_rows(self, t):
+        """The own rows of an (N, k) tensor, in row order."""
+        return t[self.rb:self.re] if self.mode == "block" else t[self.ids]
 
     def update(self):
         """LQRO:1437-1446 for the own rows, then the all-gather of x."""
         torch = self.torch
         rb, re = self.rb, self.re
+        block = self.mode == "block"
         nrm, self.seed = normals(self.seed, self.n * NORMALS_PER_AGENT)
         with torch.cuda.stream(self.stream):
             # pinned + non-blocking: no host wait on the stream's earlier work
-            host = torch.from_numpy(np.ascontiguousarray(nrm.reshape(self.n, NORMALS_PER_AGENT)[rb:re]))
+            host = torch.from_numpy(np.ascontiguousarray(nrm.reshape(self.n, NORMALS_PER_AGENT)[self.ids_h]))
             self.nrm = host.pin_memory().to(self.dev, non_blocking=True)
-            self.vgoal[rb:re].copy_(self.newv[rb:re])          # vGoal = newV (LQRO:1438)
-        xs, vs = self.x[rb:re], self.vgoal[rb:re]
+            if block:
+                self.vgoal[rb:re].copy_(self.newv[rb:re])      # vGoal = newV (LQRO:1438)
+                xs, vs = self.x[rb:re], self.vgoal[rb:re]
+            else:                                              # cyclic rows: contiguous copies
+                xs = self.x.index_select(0, self.ids)
+                vs = self.newv.index_select(0, self.ids)
         o, g = self.own, self.g
         a = Agents(xs.data_ptr(), o["rot"].data_ptr(), o["x_true"].data_ptr(), o["rot_true"].data_ptr(),
                    o["P"].data_ptr(), vs.data_ptr(), None, o["u_goal"].data_ptr(), o["p_goal"].data_ptr(),
                    g["L"].data_ptr(), g["E"].data_ptr(), g["l"].data_ptr(), g["Lh"].data_ptr(),
                    g["Eh"].data_ptr(), self.M.data_ptr(), self.Nz.data_ptr(), self.nrm.data_ptr())
         a.time = self.t * self.model.dt
-        _check(lib().lqro_dynamics_step_device(C.c_void_p(self.model_d.data_ptr()), 1, re - rb, 0,
+        _check(lib().lqro_dynamics_step_device(C.c_void_p(self.model_d.data_ptr()), 1, len(self.ids_h), 0,
                                                C.byref(a), C.c_void_p(self._sid() or None)),
                "lqro_dynamics_step_device")
-        if self.world > 1:
-            with torch.cuda.stream(self.stream):
-                allgather_rows(self.dist, self.x, self.rank, self.world)
+        with torch.cuda.stream(self.stream):
+            if not block:
+                self.x.index_copy_(0, self.ids, xs)
+                self.vgoal.index_copy_(0, self.ids, vs)
+            if self.world > 1:
+                allgather_rows(self.dist, self.x, self.rank, self.world, mode=self.mode)
         self.t += 1
 
     def close(self):

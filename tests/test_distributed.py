@@ -1,5 +1,5 @@
-"""The multi-rank path on the CPU (gloo, world_size 2): rows block-sharded
-with lqro.row_shard, each rank computes its rows, one all-gather
+"""The multi-rank path on the CPU (gloo, world_size 2): rows sharded with
+lqro.shard_rows (contiguous blocks, or cyclic: row_stride = world), each rank computes its rows, one all-gather
 (lqro.allgather_rows) assembles newV on every rank; the result equals the
 single-process step.  The per-rank compute here is the oracle (no GPU in this
 container); the GPU ranks run the same sharding/gather code in bench.py."""
@@ -19,7 +19,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, N, H, NP, out_path):
+def _worker(rank, world, port, N, H, NP, out_path, mode):
     import sys
     import torch
     import torch.distributed as dist
@@ -35,21 +35,22 @@ def _worker(rank, world, port, N, H, NP, out_path):
     g = pyoracle.synthesize()
     T, NCF = pyoracle.tables(g["A"], g["B"], g["L"], g["E"], H)
     S = pyoracle.sphere(NP)
-    rb, re = lqro.row_shard(N, rank, world)
-    newv, _ = pyoracle.step(T, NCF, S, x, vg, rows=(rb, re), records=False)
     full = torch.zeros((N, 3), dtype=torch.float64)
-    full[rb:re] = torch.from_numpy(newv[rb:re])
-    lqro.allgather_rows(dist, full, rank, world)
+    for i in lqro.shard_row_ids(N, rank, world, mode):
+        newv, _ = pyoracle.step(T, NCF, S, x, vg, rows=(int(i), int(i) + 1), records=False)
+        full[i] = torch.from_numpy(newv[i])
+    lqro.allgather_rows(dist, full, rank, world, mode=mode)
     np.save(f"{out_path}.{rank}.npy", full.numpy())
     dist.barrier()
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("mode", ["block", "cyclic"])
 @pytest.mark.parametrize("N", [12, 13])
-def test_gloo_two_ranks_match_single(tmp_path, N):
+def test_gloo_two_ranks_match_single(tmp_path, N, mode):
     world, H, NP = 2, 20, 40
     out = str(tmp_path / "newv")
-    mp.spawn(_worker, args=(world, _free_port(), N, H, NP, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), N, H, NP, out, mode), nprocs=world, join=True)
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path[:0] = [os.path.join(os.path.dirname(here), "lqr-obstacles_amd")]

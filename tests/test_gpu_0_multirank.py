@@ -1,5 +1,5 @@
 """The multi-rank HIP path on one GPU: 2 gloo ranks share
-cuda:0, each owns a block of rows with its own liblqro context and runs the
+cuda:0, each owns a block of rows (or every other row: cyclic sharding) with its own liblqro context and runs the
 device-resident closed loop (lqro.DeviceLoop: lqro_step_device ->
 lqro_dynamics_step_device on its rows -> all-gather of x) on torch's default
 stream with NO device synchronisation between the calls.  The gathered x and
@@ -26,21 +26,22 @@ def _free_port():
     return p
 
 
-def _run(lqro, x0, vg0, g, rank=0, world=1, dist=None):
+def _run(lqro, x0, vg0, g, rank=0, world=1, dist=None, mode="block"):
     import torch
-    loop = lqro.DeviceLoop(x0, vg0, g, H, NP, p_goal=-x0[:, :3], rank=rank, world=world, dist=dist, seed=11)
+    loop = lqro.DeviceLoop(x0, vg0, g, H, NP, p_goal=-x0[:, :3], rank=rank, world=world, dist=dist, seed=11,
+                           rows=mode)
     newv = []
     for _ in range(ITERS):
         loop.step()
-        newv.append(loop.newv[loop.rb:loop.re].clone())
+        newv.append(loop.own_rows(loop.newv).clone())
         loop.update()
     torch.cuda.synchronize()
-    out = loop.x.cpu().numpy(), torch.stack(newv).cpu().numpy(), (loop.rb, loop.re)
+    out = loop.x.cpu().numpy(), torch.stack(newv).cpu().numpy(), loop.ids_h
     loop.close()
     return out
 
 
-def _worker(rank, world, port, out_path):
+def _worker(rank, world, port, out_path, mode):
     import sys
     import torch
     import torch.distributed as dist
@@ -53,22 +54,24 @@ def _worker(rank, world, port, out_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     x0, vg0 = lqro.synthetic_swarm(N, seed=77, box=5.0)
     g = lqro.synthesize_gains()
-    x, nv, (rb, re) = _run(lqro, x0, vg0, g, rank, world, dist)
-    np.savez(f"{out_path}.{rank}.npz", x=x, newv=nv, rows=np.array([rb, re]))
+    x, nv, ids = _run(lqro, x0, vg0, g, rank, world, dist, mode)
+    np.savez(f"{out_path}.{rank}.npz", x=x, newv=nv, rows=ids)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_two_ranks_closed_loop_match_single_context(tmp_path, lqro_mod):
+@pytest.mark.parametrize("mode", ["block", "cyclic"])
+def test_two_ranks_closed_loop_match_single_context(tmp_path, lqro_mod, mode):
     world = 2
     out = str(tmp_path / "loop")
-    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), out, mode), nprocs=world, join=True)
     x0, vg0 = lqro_mod.synthetic_swarm(N, seed=77, box=5.0)
     g = lqro_mod.synthesize_gains()
     x_ref, nv_ref, _ = _run(lqro_mod, x0, vg0, g)
     assert not np.array_equal(x_ref, x0), "the loop did not move the agents"
     for r in range(world):
         d = np.load(f"{out}.{r}.npz")
-        rb, re = d["rows"]
+        ids = d["rows"]
+        assert np.array_equal(ids, lqro_mod.shard_row_ids(N, r, world, mode))
         assert np.array_equal(d["x"].view(np.uint64), x_ref.view(np.uint64)), f"rank {r}: gathered x"
-        assert np.array_equal(d["newv"].view(np.uint64), nv_ref[:, rb:re].view(np.uint64)), f"rank {r}: newV"
+        assert np.array_equal(d["newv"].view(np.uint64), nv_ref[:, ids].view(np.uint64)), f"rank {r}: newV"

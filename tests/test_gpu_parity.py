@@ -81,6 +81,42 @@ def test_row_shards_partition(lqro_mod, oracle, gains):
     assert np.array_equal(newv[8:20], rv[8:20])
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_cyclic_row_shards(lqro_mod, gains, world):
+    """Cyclic sharding (row_stride = world): each rank's records and newV
+    rows equal the same rows of the unsharded GPU step, on a dense swarm so
+    the hull queue, the hot schedule and the LP all see strided rows."""
+    N, H, NP = 30, 45, 100
+    x, vg = lqro_mod.synthetic_swarm(N, box=3.0, seed=11)
+
+    def run(**kw):
+        ctx = lqro_mod.Context(lqro_mod.config(N, H, NP, flags=lqro_mod.LQRO_FLAG_RECORDS, **kw))
+        ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
+        nv = ctx.step(x, vg)
+        out = nv, ctx.records(), ctx.stats(), ctx.row_ids
+        ctx.close()
+        return out
+
+    full_v, full_r, full_st, _ = run()
+    assert full_st["inside"] > 0
+    seen = 0
+    for r in range(world):
+        nv, rec, st, ids = run(**lqro_mod.shard_rows(N, r, world, "cyclic"))
+        assert np.array_equal(ids, np.arange(r, N, world))
+        sel = np.isin(full_r["i"], ids)
+        ref = full_r[sel]
+        _compare(rec, ref)
+        inside = (ref["flags"] & 2) != 0
+        assert np.all(rec["flags"][inside] & 8)
+        assert np.array_equal(rec["facet"][inside], ref["facet"][inside])
+        assert np.array_equal(rec["dist"].view(np.uint64), ref["dist"].view(np.uint64))
+        assert np.array_equal(nv[ids], full_v[ids])
+        others = np.setdiff1d(np.arange(N), ids)
+        assert not nv[others].any()
+        seen += st["pairs"]
+    assert seen == N * (N - 1)
+
+
 def test_dense_swarm_inside_hull(lqro_mod, oracle, gains):
     """A tight swarm (collision courses) exercises the in-kernel hull."""
     x, vg = lqro_mod.synthetic_swarm(32, box=3.0, seed=11)

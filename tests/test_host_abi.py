@@ -132,6 +132,22 @@ def test_row_shard_partition(lqro_mod):
         lqro_mod.row_shard(3, 0, 4)
 
 
+@pytest.mark.parametrize("mode", ["block", "cyclic"])
+def test_shard_rows_partition(lqro_mod, mode):
+    """Every agent's row belongs to exactly one rank, in either mode; the
+    config fields are what the C-ABI reads (row_stride 0 = contiguous)."""
+    for n, w in ((1024, 8), (1000, 8), (64, 2), (9, 4), (4096, 8), (5, 5), (7, 1)):
+        ids = [lqro_mod.shard_row_ids(n, r, w, mode) for r in range(w)]
+        assert np.array_equal(np.sort(np.concatenate(ids)), np.arange(n))
+        assert max(len(i) for i in ids) - min(len(i) for i in ids) <= 1
+        for r in range(w):
+            f = lqro_mod.shard_rows(n, r, w, mode)
+            cfg = lqro_mod.config(n, 10, 10, **f)
+            assert cfg.row_stride == f["row_stride"]
+    with pytest.raises(ValueError):
+        lqro_mod.shard_rows(8, 0, 2, "striped")
+
+
 def test_swarm_generator_is_stable(lqro_mod):
     """The synthetic swarm is part of the bench contract."""
     x, vg = lqro_mod.synthetic_swarm(4)
