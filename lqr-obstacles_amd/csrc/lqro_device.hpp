@@ -16,6 +16,14 @@ constexpr int kWave = 64;
 // Workgroup-scope fence pair: orders this wave's LDS writes before other
 // lanes' later reads (LDS executes a wave's instructions in order; this keeps
 // the compiler from reordering and waits for lgkmcnt).
+// x, opaque to the optimiser: values derived from it are recomputed after
+// this point instead of being hoisted out of loops (each hoisted lane
+// constant holds a VGPR for the whole kernel)
+__device__ __forceinline__ int opaque(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_wave_barrier();

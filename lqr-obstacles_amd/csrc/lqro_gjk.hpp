@@ -319,6 +319,7 @@ __device__ __forceinline__ double gjk_dp(const GjkWave& G, const double* vrel, i
 // compute_subterms (gjk.cpp:527-581) into this lane's dv
 __device__ __forceinline__ void gjkw_subterms(const GjkWave& G, const double* vrel, int size,
                                               int lane, double& dv) {
+  lane = opaque(lane);
   const int s = lane >> 2, j = lane & 3;
   const int card = __popc(s);
   const bool live = s >= 1 && j < card && (s >> size) == 0;   // maxe[s] < size
@@ -348,6 +349,7 @@ __device__ __forceinline__ void gjkw_subterms(const GjkWave& G, const double* vr
 // reset_simplex (gjk.cpp:708-736) for a wave-uniform subset; returns the new size
 __device__ __forceinline__ int gjkw_reset(const GjkWave& G, int subset, double dv, double dsum,
                                           int lane) {
+  lane = opaque(lane);
   const int card = __popc(subset);
   const double ds = gjk_shfl(dsum, 4 * subset);
   const double lv = gjk_shfl(dv, 4 * subset + (lane & 3));
@@ -370,6 +372,7 @@ __device__ __forceinline__ int gjkw_reset(const GjkWave& G, int subset, double d
 // default_distance (gjk.cpp:593-657): 1 and the new size through *size, or 0
 __device__ __forceinline__ int gjkw_default(const GjkWave& G, int& size, double dv, double& dsum,
                                             int lane) {
+  lane = opaque(lane);
   const int s = lane >> 2;
   const int card = __popc(s);
   const bool valid = s >= 1 && (s >> size) == 0;
@@ -417,6 +420,7 @@ __device__ __forceinline__ int gjkw_default(const GjkWave& G, int& size, double 
 // backup_distance (gjk.cpp:663-706)
 __device__ __forceinline__ int gjkw_backup(const GjkWave& G, const double* vrel, int size, double dv,
                                            double dsum, int lane) {
+  lane = opaque(lane);
   const int s = lane >> 2;
   const int card = __popc(s);
   const bool valid = s >= 1 && (s >> size) == 0;
@@ -465,6 +469,17 @@ __device__ void gjkw_run(Sup& sup, const GjkWave& G, int lane, int qfirst, int n
     wave_lds_sync();
   }
   npts = 1;
+#ifdef LQRO_PAIR_PROFILE
+  unsigned long long t_ = __builtin_amdgcn_s_memtime();
+#define GJK_STAMP(k)                                          \
+  do {                                                        \
+    const unsigned long long u_ = __builtin_amdgcn_s_memtime(); \
+    sup.pc[k] += u_ - t_;                                     \
+    t_ = u_;                                                  \
+  } while (0)
+#else
+#define GJK_STAMP(k) do {} while (0)
+#endif
   while (max_iterations-- > 0) {
     if (npts == 1) {
       if (lane == 0) G.lam[0] = 1.0;
@@ -474,6 +489,7 @@ __device__ void gjkw_run(Sup& sup, const GjkWave& G, int lane, int qfirst, int n
       if (use_default) use_default = gjkw_default(G, npts, dv, dsum, lane);
       if (!use_default) { npts = gjkw_backup(G, vrel, npts, dv, dsum, lane); o.backup = 1; }
     }
+    GJK_STAMP(3);
     // compute_point (gjk.cpp:851-862)
 #pragma unroll
     for (int d = 0; d < 3; d++) {
@@ -488,11 +504,15 @@ __device__ void gjkw_run(Sup& sup, const GjkWave& G, int lane, int qfirst, int n
 #pragma unroll
     for (int d = 0; d < 3; d++) { disp[d] = o.w2[d] - o.w1[d]; rdisp[d] = -disp[d]; }
     sqrd = disp[0] * disp[0] + disp[1] * disp[1] + disp[2] * disp[2];
+    GJK_STAMP(4);
     if (sqrd < 1.0e-8) { o.sqrd = sqrd; return; }
     const double maxv = vrel[0] * disp[0] + vrel[1] * disp[1] + vrel[2] * disp[2];
     double minus_minv;
     int minq;
     sup.support(rdisp[0], rdisp[1], rdisp[2], minus_minv, minq);
+#ifdef LQRO_PAIR_PROFILE
+    t_ = __builtin_amdgcn_s_memtime();
+#endif
     o.iters++;
     double g_val = sqrd + maxv + minus_minv;
     if (g_val < 0.0) g_val = 0;
@@ -504,6 +524,7 @@ __device__ void gjkw_run(Sup& sup, const GjkWave& G, int lane, int qfirst, int n
       if (lane < 3) G.c2[3 * npts + lane] = f[lane == 0 ? 0 : (lane == 1 ? 1 : 2)];
       if (lane == 0) { G.s2[npts] = minq; G.lam[npts] = 0.0; }
       wave_lds_sync();
+      GJK_STAMP(5);
       npts++;
       oldsqrd = sqrd;
       first_iteration = 0;
@@ -515,5 +536,6 @@ __device__ void gjkw_run(Sup& sup, const GjkWave& G, int lane, int qfirst, int n
   }
   o.sqrd = 0.0;
 }
+#undef GJK_STAMP
 
 }  // namespace lqro

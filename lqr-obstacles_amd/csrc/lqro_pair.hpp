@@ -38,8 +38,8 @@ enum : int { kRowLaunch = 0, kHotShared = 1, kHotPerAgent = 2 };
 constexpr int kMaxPW = 4;
 constexpr int kMaxKS = 4;   // H <= 64 kMaxKS = 256 (per-lane slice slots)
 #ifndef LQRO_PAIR_LB
-#define LQRO_PAIR_LB 768
-#endif  // 12 waves (3 per SIMD: <= 168 VGPRs); NP <= 256 (one 64-bit reachable mask per 64 points)
+#define LQRO_PAIR_LB 1024
+#endif  // 16 waves (4 per SIMD: <= 128 VGPRs); NP <= 256 (one 64-bit reachable mask per 64 points)
 
 struct PairArgs {
   int N, H, NP, PW, min_reach;
@@ -204,7 +204,7 @@ struct SliceSupport {
   const WaveTabs& W;
   int lane;
 #ifdef LQRO_PAIR_PROFILE
-  unsigned long long* pc;   // [0] support cycles, [1] calls, [2] candidate slices
+  unsigned long long* pc;   // [0] support cycles, [1] calls, [2] candidate slices, [3] Johnson, [4] witness, [5] point
 #endif
 
   __device__ void point(int q, double* x) const {
@@ -358,7 +358,7 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
   unsigned long long p_last = __builtin_amdgcn_s_memtime();
 #endif
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: SGPR
   const int H = P.H, NP = P.NP, XP = P.XP;
   __shared__ int s_row, s_next;
 
@@ -386,7 +386,7 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
   }
   unsigned long long st_reach = 0, st_iters = 0, st_planes = 0, st_inside = 0, st_backup = 0;
 #ifdef LQRO_PAIR_PROFILE
-  unsigned long long pc[3] = {0, 0, 0};
+  unsigned long long pc[6] = {0, 0, 0, 0, 0, 0};
   SliceSupport sup{P, B, W, lane, pc};
 #else
   SliceSupport sup{P, B, W, lane};
@@ -394,11 +394,19 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
 
   // one ordered pair (i, j = jj-th other agent) of local row lrow
   auto do_pair = [&](const int i, const int lrow, const int jj) {
+    // the lane id, opaque per pair: lane-derived constants are rebuilt here
+    // rather than hoisted into registers held across the persistent loop
+    const int ln = opaque(lane);
+#ifdef LQRO_PAIR_PROFILE
+    SliceSupport sp{P, B, W, ln, pc};
+#else
+    SliceSupport sp{P, B, W, ln};
+#endif
     const double* xi = P.x + (size_t)i * X;
     // culling on (lqro_set_neighbors): slot q of the row holds its q-th neighbour
     const int jq = P.nbr_list != nullptr ? P.nbr_list[(size_t)lrow * P.npr + jj] : jj;
     if (jq < 0) {   // fewer neighbours than slots
-      if (lane == 0) {
+      if (ln == 0) {
         const size_t cs = (size_t)lrow * P.npr + jj;
         float4* dst = reinterpret_cast<float4*>(P.planes + cs * 8);
         dst[0] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -424,7 +432,7 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
     PSTAMP(7);
 
     // 1. per slice: Translate (exact), centre, class       (lanes <-> k)
-    for (int k = lane; k < H; k += 64) {
+    for (int k = ln; k < H; k += 64) {
       const int np = HOT == kHotPerAgent ? B.pitch : XP;
       const double* nc = B.N + (size_t)k * 3 * np;
       double t0 = 0.0, t1 = 0.0, t2 = 0.0;
@@ -467,20 +475,25 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
     PSTAMP(1);
 
     // 2. MIXED slices: per-point exact test                 (lanes <-> p)
-    int nmixed = 0;
+    // n_reach and the first reachable point come out of the same ballots,
+    // wave-uniform: IN slices count NP each, MIXED ones their ballot bits
+    int nmixed = 0, n = 0, qfirst = INT_MAX;
     for (int base = 0; base < H; base += 64) {
-      const int k = base + lane;
-      const bool m = k < H && W.cls[k] == kSliceMixed;
-      const unsigned long long bal = __ballot(m);
-      if (m) W.mixed[nmixed + __popcll(bal & ((1ull << lane) - 1ull))] = k;
+      const int k = base + ln;
+      const int c = k < H ? W.cls[k] : kSliceOut;
+      const unsigned long long bal = __ballot(c == kSliceMixed);
+      const unsigned long long bin = __ballot(c == kSliceIn);
+      if (c == kSliceMixed) W.mixed[nmixed + __popcll(bal & ((1ull << ln) - 1ull))] = k;
       nmixed += __popcll(bal);
+      n += NP * __popcll(bin);
+      if (bin && qfirst == INT_MAX) qfirst = (base + __ffsll((long long)bin) - 1) * NP;
     }
     wave_lds_sync();
     for (int mi = 0; mi < nmixed; ++mi) {
       const int k = W.mixed[mi];
       int cnt = 0;
       for (int pw = 0; pw < P.PW; ++pw) {
-        const int p = pw * 64 + lane;
+        const int p = pw * 64 + ln;
         bool ok = false;
         if (p < NP) {
           double x[3];
@@ -489,10 +502,14 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
         }
         const unsigned long long bal = __ballot(ok);
         if (ok && want_hash) hsh += mix64((uint64_t)(k * NP + p));   // records only
-        if (lane == 0) W.mask[k * P.PW + pw] = bal;
+        if (ln == 0) W.mask[k * P.PW + pw] = bal;
+        // mixed slices come in increasing k: the first set bit seen is the
+        // first reachable point of the MIXED slices
+        if (bal && cnt == 0 && k * NP < qfirst) qfirst = k * NP + pw * 64 + __ffsll((long long)bal) - 1;
         cnt += __popcll(bal);
       }
-      if (lane == 0) {
+      n += cnt;
+      if (ln == 0) {
         W.cnt[k] = cnt;
         if (cnt == 0) W.cls[k] = kSliceOut;
       }
@@ -502,22 +519,9 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
 #ifdef LQRO_PAIR_PROFILE
     pp[10] += nmixed;
 #endif
-
-    // n_reach and the first reachable point
-    int n = 0, qfirst = INT_MAX;
-    for (int k = lane; k < H; k += 64) {
-      n += W.cnt[k];
-      if (W.cnt[k] > 0 && qfirst == INT_MAX)
-        for (int pw = 0; pw < P.PW; ++pw) {
-          const unsigned long long bits = W.mask[k * P.PW + pw];
-          if (bits) { qfirst = k * NP + pw * 64 + __ffsll((long long)bits) - 1; break; }
-        }
-    }
+    if (want_hash) {
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      n += __shfl_xor(n, off);
-      qfirst = min(qfirst, __shfl_xor(qfirst, off));
-      hsh += __shfl_xor(hsh, off);
+      for (int off = 32; off >= 1; off >>= 1) hsh += __shfl_xor(hsh, off);
     }
     st_reach += n;
     PSTAMP(3);
@@ -532,7 +536,7 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
     int npts = 0;
     bool inside = false;
     if (n > P.min_reach) {                                    // :1409
-      gjkw_run(sup, W.gjk, lane, qfirst, n, vrel, npts, go);
+      gjkw_run(sp, W.gjk, ln, qfirst, n, vrel, npts, go);
       double distance = sqrt(go.sqrd);                          // :843
       nrm[0] = (go.w1[0] - go.w2[0]) / distance;                // :850-852
       nrm[1] = (go.w1[1] - go.w2[1]) / distance;
@@ -561,8 +565,8 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
     int sranks[4] = {-1, -1, -1, -1};
     if (RECS && npts > 0)
       for (int s = 0; s < 4; ++s)
-        if (s < npts) sranks[s] = reach_rank(P, W, lane, W.gjk.s2[s]);
-    if (lane == 0) {
+        if (s < npts) sranks[s] = reach_rank(P, W, ln, W.gjk.s2[s]);
+    if (ln == 0) {
       float4* dst = reinterpret_cast<float4*>(P.planes + slot * 8);
       dst[0] = make_float4(pl[0], pl[1], pl[2], pl[3]);
       dst[1] = make_float4(pl[4], pl[5], pl[6], pl[7]);
@@ -596,6 +600,7 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
 #ifdef LQRO_PAIR_PROFILE
     pp[11] += 1;
     pp[12] = pc[0]; pp[13] = pc[1]; pp[14] = pc[2];
+    pp[6] = pc[3]; pp[8] = pc[4]; pp[9] = pc[5];
 #endif
     };
   // Hot launch (shared gains only): the pairs k_prio marked as likely

@@ -25,3 +25,5 @@ print("pairs", pairs, "mixed slices/pair %.2f" % (pp[10] / max(pairs, 1)),
       "support cycles/pair %.0f (%.1f%% of gjk)" % (pp[12] / max(pairs, 1), 100 * pp[12] / max(pp[4], 1)),
       "candidates/support %.2f" % (pp[14] / max(pp[13], 1)),
       "cycles/pair/wave %.0f" % (tot / max(pairs, 1)))
+print("gjk cycles/pair: johnson %.0f witness %.0f support %.0f point %.0f" %
+      tuple(v / max(pairs, 1) for v in (pp[6], pp[8], pp[12], pp[9])))
