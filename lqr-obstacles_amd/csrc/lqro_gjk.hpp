@@ -203,7 +203,7 @@ __device__ __forceinline__ void gjk_witnesses(const GjkState& g, const double* v
 }
 
 // Sup must provide:
-//   void support(double d0, double d1, double d2, double& value, int& q)
+//   void support(double d0, double d1, double d2, double& value, int& q[, double* pt])
 //   void point(int q, double* pt)
 template <class Sup>
 __device__ void gjk_run(Sup& sup, int qfirst, int n, const double* vrel, GjkState& g, GjkOut& o) {
@@ -509,7 +509,8 @@ __device__ void gjkw_run(Sup& sup, const GjkWave& G, int lane, int qfirst, int n
     const double maxv = vrel[0] * disp[0] + vrel[1] * disp[1] + vrel[2] * disp[2];
     double minus_minv;
     int minq;
-    sup.support(rdisp[0], rdisp[1], rdisp[2], minus_minv, minq);
+    double f[3];   // the support point (== sup.point(minq))
+    sup.support(rdisp[0], rdisp[1], rdisp[2], minus_minv, minq, f);
 #ifdef LQRO_PAIR_PROFILE
     t_ = __builtin_amdgcn_s_memtime();
 #endif
@@ -518,8 +519,6 @@ __device__ void gjkw_run(Sup& sup, const GjkWave& G, int lane, int qfirst, int n
     if (g_val < 0.0) g_val = 0;
     if (g_val < 1.0e-8) { o.sqrd = sqrd; return; }
     if ((first_iteration || (sqrd < oldsqrd)) && (npts <= 3)) {
-      double f[3];
-      sup.point(minq, f);
       wave_lds_sync();   // every lane has read the old simplex
       if (lane < 3) G.c2[3 * npts + lane] = f[lane == 0 ? 0 : (lane == 1 ? 1 : 2)];
       if (lane == 0) { G.s2[npts] = minq; G.lam[npts] = 0.0; }

@@ -212,10 +212,26 @@ struct SliceSupport {
     exact_point(B, W, P.NP, k, q - k * P.NP, x);
   }
 
-  // best (value, q) over the reachable points of slice k, merged into (bv, bq)
-  __device__ void eval_slice(int k, double d0, double d1, double d2, double& bv, int& bq) const {
+  // the winner of a wave arg-max: every lane gets the point coordinates the
+  // winning lane computed (lanes' q are distinct; none won: unchanged)
+  __device__ __forceinline__ static void take_point(int myq, int qw, const double* mx, double* bx) {
+    const unsigned long long w = __ballot(myq == qw && qw != INT_MAX);
+    if (!w) return;
+    const int wl = __ffsll((long long)w) - 1;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const long long b = __double_as_longlong(mx[c]);
+      const int lo = __builtin_amdgcn_readlane((int)b, wl);
+      const int hi = __builtin_amdgcn_readlane((int)(b >> 32), wl);
+      bx[c] = __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+    }
+  }
+
+  // best (value, q, point) over the reachable points of slice k, merged into (bv, bq, bx)
+  __device__ void eval_slice(int k, double d0, double d1, double d2, double& bv, int& bq, double* bx) const {
     double lv = -INFINITY;
     int lq = INT_MAX;
+    double lx[3] = {0.0, 0.0, 0.0};
     for (int pw = 0; pw < P.PW; ++pw) {
       const int p = pw * 64 + lane;
       const unsigned long long bits = W.mask[k * P.PW + pw];
@@ -224,11 +240,12 @@ struct SliceSupport {
         exact_point(B, W, P.NP, k, p, x);
         const double v = x[0] * d0 + x[1] * d1 + x[2] * d2;   // SUPPORT_DOT_PRODUCT
         const int q = k * P.NP + p;
-        if (better(v, q, lv, lq)) { lv = v; lq = q; }
+        if (better(v, q, lv, lq)) { lv = v; lq = q; lx[0] = x[0]; lx[1] = x[1]; lx[2] = x[2]; }
       }
     }
+    const int myq = lq;
     wave_argmax(lv, lq);
-    if (better(lv, lq, bv, bq)) { bv = lv; bq = lq; }
+    if (better(lv, lq, bv, bq)) { bv = lv; bq = lq; take_point(myq, lq, lx, bx); }
   }
 
   // support_simple semantics: lowest-index maximiser of p.d over the reachable set.
@@ -238,14 +255,16 @@ struct SliceSupport {
   // 3. every other slice with ub_k >= bv (the only ones that can hold a value
   //    >= bv, ties included) is evaluated in one flattened pass, lanes over
   //    (candidate, point), and one arg-max merges the lanes.
-  __device__ void support(double d0, double d1, double d2, double& bv, int& bq) const {
+  // bx: the support point itself (the coordinates the winning lane computed,
+  // exactly what point(bq) recomputes)
+  __device__ void support(double d0, double d1, double d2, double& bv, int& bq, double* bx) const {
 #ifdef LQRO_PAIR_PROFILE
     const unsigned long long t0_ = __builtin_amdgcn_s_memtime();
     pc[1] += 1;
-    support_(d0, d1, d2, bv, bq);
+    support_(d0, d1, d2, bv, bq, bx);
     pc[0] += __builtin_amdgcn_s_memtime() - t0_;
   }
-  __device__ void support_(double d0, double d1, double d2, double& bv, int& bq) const {
+  __device__ void support_(double d0, double d1, double d2, double& bv, int& bq, double* bx) const {
 #endif
     // magnitudes below only scale the 1e-9 margins: the hardware square root
     // (a few ulp) is ample there
@@ -277,7 +296,7 @@ struct SliceSupport {
     bv = -INFINITY;
     bq = INT_MAX;
     if (ck == INT_MAX) return;
-    eval_slice(ck, d0, d1, d2, bv, bq);
+    eval_slice(ck, d0, d1, d2, bv, bq, bx);
     // candidates: the other slices whose bound reaches bv (usually none)
     unsigned long long cb[kMaxKS];
     unsigned long long any = 0;
@@ -301,6 +320,7 @@ struct SliceSupport {
     wave_lds_sync();
     double lv = -INFINITY;
     int lq = INT_MAX;
+    double lx[3] = {0.0, 0.0, 0.0};
     // lane walks (c, p) = divmod(idx, NP) for idx = lane, lane+64, ...
     int c = 0, p = lane;
     while (p >= P.NP) { p -= P.NP; ++c; }
@@ -312,13 +332,14 @@ struct SliceSupport {
         exact_point(B, W, P.NP, k, p, x);
         const double v = x[0] * d0 + x[1] * d1 + x[2] * d2;   // SUPPORT_DOT_PRODUCT
         const int q = k * P.NP + p;
-        if (better(v, q, lv, lq)) { lv = v; lq = q; }
+        if (better(v, q, lv, lq)) { lv = v; lq = q; lx[0] = x[0]; lx[1] = x[1]; lx[2] = x[2]; }
       }
       p += 64;
       while (p >= P.NP) { p -= P.NP; ++c; }
     }
+    const int myq = lq;
     wave_argmax(lv, lq);
-    if (better(lv, lq, bv, bq)) { bv = lv; bq = lq; }
+    if (better(lv, lq, bv, bq)) { bv = lv; bq = lq; take_point(myq, lq, lx, bx); }
   }
 };
 
