@@ -1847,6 +1847,7 @@ __device__ __forceinline__ void hull_body(const HullArgs& A, Mem& M, LT& L, bool
   (void)wave;
 }
 
+#ifdef LQRO_HULL_TU   // defined once, in lqro_kern_hull.hip
 __global__ void __launch_bounds__(HULL_CTHREADS) k_hull(HullArgs A) {
   __shared__ HullLdsC<HULL_CWAVES> L;
   __shared__ HullMemC M;
@@ -1858,5 +1859,6 @@ __global__ void __launch_bounds__(HULL_THREADS) k_hull_big(HullArgs A) {
   HullMemBig& M = reinterpret_cast<HullMemBig*>(A.bigmem)[blockIdx.x];
   hull_body(A, M, L, true);
 }
+#endif
 
 }  // namespace lqro

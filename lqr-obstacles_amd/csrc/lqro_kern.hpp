@@ -1,0 +1,21 @@
+// lqro_kern.hpp — launch functions of the kernels compiled in their own
+// objects (lqro_kern_hull.hip, lqro_kern_synth.hip, lqro_kern_dyn.hip), so
+// that liblqro.so's large kernels compile in parallel.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/lqro.h"
+
+namespace lqro {
+struct HullArgs;
+// k_hull: grid x 8 waves, topology in LDS
+void launch_hull(dim3 grid, hipStream_t s, const HullArgs& A);
+// k_hull_big: one inserting wave, topology in global memory
+void launch_hull_big(dim3 grid, hipStream_t s, const HullArgs& A);
+// controlMatrices for n models into out (stride X*X + 12X + 25 doubles):
+// k_synthw (one wave per agent) or, lane = true, k_synth (one agent per lane)
+void launch_synth(int x_dim, bool lane, const lqro_model* d_models, int n, double* d_out);
+// the agent loop LQRO:1437-1446: k_dynw or, lane = true, k_dyn
+void launch_dyn(bool lane, const lqro_model* models, int n_models, int n, int per_agent, const lqro_agents& A,
+                hipStream_t s);
+}  // namespace lqro

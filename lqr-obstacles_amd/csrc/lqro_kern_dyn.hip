@@ -1,0 +1,76 @@
+// lqro_kern_dyn.hip — the per-agent dynamics / estimation kernels (the agent
+// loop LQRObstacles.cpp:1437-1446) and their launch function (lqro_kern.hpp).
+#include <hip/hip_runtime.h>
+
+#include "lqro_dyn.hpp"
+#include "lqro_dynw.hpp"
+#include "lqro_kern.hpp"
+
+namespace lqro {
+
+// ---- the per-agent step after the pair loop (LQRO:1437-1446) -------------
+// One agent per lane: the step is a chain of 16x16 products, exponentials and
+// a Jacobi sweep with data-dependent control flow (lqro_dyn.hpp), fp64,
+// ~10 MFLOP per agent, latency bound on per-lane scratch.
+__global__ void __launch_bounds__(64) k_dyn(const lqro_model* models, int n_models, int n, int per_agent,
+                                            lqro_agents A) {
+  const int a = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= n) return;
+  const size_t g = per_agent ? (size_t)a : 0;
+  dyn::AgentParams p;
+  p.model = models + (n_models > 1 ? a : 0);
+  p.L = A.L + g * dyn::kU * dyn::kX;
+  p.E = A.E + g * dyn::kU * dyn::kV;
+  p.l = A.l + g * dyn::kU;
+  p.Lh = A.Lh + g * dyn::kV * dyn::kX;
+  p.Eh = A.Eh + g * dyn::kV * dyn::kV;
+  p.u_goal = A.u_goal + (size_t)a * dyn::kU;
+  p.p_goal = A.p_goal + (size_t)a * 3;
+  p.M = A.M;
+  p.Nz = A.N;
+  p.normals = A.normals + (size_t)a * dyn::kNormals;
+  p.keyframe = A.keyframes ? A.keyframes + (size_t)a * 8 : nullptr;
+  p.time = A.time;
+  dyn::agent_step(p, A.x + (size_t)a * dyn::kX, A.rot + (size_t)a * 9, A.x_true + (size_t)a * dyn::kX,
+                  A.rot_true + (size_t)a * 9, A.P + (size_t)a * dyn::kX * dyn::kX, A.vgoal + (size_t)a * 3,
+                  A.u ? A.u + (size_t)a * dyn::kU : nullptr);
+}
+
+// The same step with one wave per agent (lqro_dynw.hpp): the agent's 16x16
+// matrices in LDS, the products, exponentials, solves and Jacobi sweep over
+// the lanes.  The default; LQRO_DYN_LANE=1 selects k_dyn.
+__global__ void __launch_bounds__(64) k_dynw(const lqro_model* models, int n_models, int n, int per_agent,
+                                             lqro_agents A) {
+  __shared__ double w[dynw::kWaveDoubles];
+  const int a = blockIdx.x;
+  if (a >= n) return;
+  const int lane = threadIdx.x;
+  const size_t g = per_agent ? (size_t)a : 0;
+  dyn::AgentParams p;
+  p.model = models + (n_models > 1 ? a : 0);
+  p.L = A.L + g * dyn::kU * dyn::kX;
+  p.E = A.E + g * dyn::kU * dyn::kV;
+  p.l = A.l + g * dyn::kU;
+  p.Lh = A.Lh + g * dyn::kV * dyn::kX;
+  p.Eh = A.Eh + g * dyn::kV * dyn::kV;
+  p.u_goal = A.u_goal + (size_t)a * dyn::kU;
+  p.p_goal = A.p_goal + (size_t)a * 3;
+  p.M = A.M;
+  p.Nz = A.N;
+  p.normals = A.normals + (size_t)a * dyn::kNormals;
+  p.keyframe = A.keyframes ? A.keyframes + (size_t)a * 8 : nullptr;
+  p.time = A.time;
+  dynw::agent_step(p, A.x + (size_t)a * dyn::kX, A.rot + (size_t)a * 9, A.x_true + (size_t)a * dyn::kX,
+                   A.rot_true + (size_t)a * 9, A.P + (size_t)a * dyn::kX * dyn::kX, A.vgoal + (size_t)a * 3,
+                   A.u ? A.u + (size_t)a * dyn::kU : nullptr, w, lane);
+}
+
+void launch_dyn(bool lane, const lqro_model* models, int n_models, int n, int per_agent, const lqro_agents& A,
+                hipStream_t s) {
+  if (lane)
+    hipLaunchKernelGGL(k_dyn, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, models, n_models, n, per_agent, A);
+  else
+    hipLaunchKernelGGL(k_dynw, dim3((unsigned)n), dim3(64), 0, s, models, n_models, n, per_agent, A);
+}
+
+}  // namespace lqro

@@ -733,6 +733,7 @@ __global__ void __launch_bounds__(LQRO_PAIR_LB) k_pair(PairArgs P) {
   pair_block<X, RECS, HOT>(P, lds);
 }
 
+#ifndef LQRO_PAIR_TU   // the non-template kernels: defined once, in lqro_runtime.hip
 // k_nbr: opt-in neighbour culling (RVO2 computeNeighbors /
 // insertAgentNeighbor, AGT:74-81,153-174).  One wave per row: agent i keeps
 // the k agents j != i with the smallest (d2, j), d2 = |p_i - p_j|^2 < r2 —
@@ -879,5 +880,6 @@ __global__ void __launch_bounds__(256) k_prio(PrioArgs A) {
     if (slot < total) A.mark[slot] = hot ? 1 : 0;
   }
 }
+#endif  // LQRO_PAIR_TU
 
 }  // namespace lqro

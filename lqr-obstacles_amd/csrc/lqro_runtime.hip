@@ -31,58 +31,36 @@
 #include "../../include/lqro.h"
 #include "lqro_device.hpp"
 #include "lqro_lp.hpp"
-#include "lqro_pair.hpp"
+#include "lqro_pair_launch.hpp"
 #include "lqro_hull.hpp"
 #include "lqro_synth.hpp"
 #include "lqro_dyn.hpp"
-#include "lqro_dynw.hpp"
-#include "lqro_synthw.hpp"
+#include "lqro_kern.hpp"
 
 #define LQRO_PROF_WORDS (32 + 2 * 4096 + 16 + 16)   // hull: 32 counters + 2 words per job; pair: 16; hull wave phases: 16
 
 using namespace lqro;
 
-// k_side: the side stream's hull workers (the hot pairs' hulls, topology in
-// LDS as k_hull), which turn into k_pair row workers once the hull queue is
-// drained, so the side CUs never idle while the sweep goes on.  The pair
-// tables and per-wave regions reuse the hull's LDS (host checks the fit).
-template <int X, bool RECS>
-__global__ void __launch_bounds__(HULL_CTHREADS) k_side(HullArgs A, PairArgs P) {
-  __shared__ HullLdsC<HULL_CWAVES> L;
-  __shared__ HullMemC M;
-  hull_body_mw<HULL_CWAVES>(A, M, L);
-  __syncthreads();
-  if (P.nrows > 0) pair_block<X, RECS, kRowLaunch>(P, reinterpret_cast<double*>(&M));
-}
-
-// k_pair / k_side for the context's state width and record mode
-template <int X>
-static void launch_pair_x(dim3 grid, dim3 block, size_t lds, hipStream_t s, const PairArgs& P) {
-  const bool r = P.recs != nullptr;
-  const int h = P.hot_only == 0 ? kRowLaunch : (P.per_agent ? kHotPerAgent : kHotShared);
-  if (h == kRowLaunch) {
-    if (r) hipLaunchKernelGGL((k_pair<X, true, kRowLaunch>), grid, block, lds, s, P);
-    else hipLaunchKernelGGL((k_pair<X, false, kRowLaunch>), grid, block, lds, s, P);
-  } else if (h == kHotShared) {
-    if (r) hipLaunchKernelGGL((k_pair<X, true, kHotShared>), grid, block, lds, s, P);
-    else hipLaunchKernelGGL((k_pair<X, false, kHotShared>), grid, block, lds, s, P);
-  } else {
-    if (r) hipLaunchKernelGGL((k_pair<X, true, kHotPerAgent>), grid, block, lds, s, P);
-    else hipLaunchKernelGGL((k_pair<X, false, kHotPerAgent>), grid, block, lds, s, P);
-  }
-}
+// k_pair / k_side for the context's state width and record mode (the
+// instantiations live in lqro_pair_inst.hip, one object per combination)
 static void launch_pair(int x_dim, dim3 grid, dim3 block, size_t lds, hipStream_t s, const PairArgs& P) {
-  if (x_dim == 16) launch_pair_x<16>(grid, block, lds, s, P);
-  else launch_pair_x<12>(grid, block, lds, s, P);
+  const bool r = P.recs != nullptr;
+  if (x_dim == 16) {
+    if (r) launch_pair_t<16, true>(grid, block, lds, s, P);
+    else launch_pair_t<16, false>(grid, block, lds, s, P);
+  } else {
+    if (r) launch_pair_t<12, true>(grid, block, lds, s, P);
+    else launch_pair_t<12, false>(grid, block, lds, s, P);
+  }
 }
 static void launch_side(int x_dim, dim3 grid, dim3 block, hipStream_t s, const HullArgs& H, const PairArgs& P) {
   const bool r = P.recs != nullptr;
   if (x_dim == 16) {
-    if (r) hipLaunchKernelGGL((k_side<16, true>), grid, block, 0, s, H, P);
-    else hipLaunchKernelGGL((k_side<16, false>), grid, block, 0, s, H, P);
+    if (r) launch_side_t<16, true>(grid, block, s, H, P);
+    else launch_side_t<16, false>(grid, block, s, H, P);
   } else {
-    if (r) hipLaunchKernelGGL((k_side<12, true>), grid, block, 0, s, H, P);
-    else hipLaunchKernelGGL((k_side<12, false>), grid, block, 0, s, H, P);
+    if (r) launch_side_t<12, true>(grid, block, s, H, P);
+    else launch_side_t<12, false>(grid, block, s, H, P);
   }
 }
 
@@ -422,36 +400,6 @@ static hipError_t wait_last_step(lqro_ctx* c) {
     }                                                                                    \
   } while (0)
 
-template <int X>
-__global__ void __launch_bounds__(64) k_synth(const lqro_model* models, int n, double* out) {
-  const int a = blockIdx.x * blockDim.x + threadIdx.x;
-  if (a >= n) return;
-  constexpr int S = X * X + 12 * X + 25;
-  double* o = out + (size_t)a * S;
-  double* p[8];
-  p[0] = o;
-  p[1] = p[0] + X * X; p[2] = p[1] + X * 4; p[3] = p[2] + X; p[4] = p[3] + 4 * X; p[5] = p[4] + 12;
-  p[6] = p[5] + 4; p[7] = p[6] + 3 * X;
-  synth::gains_x<X>(models + a, p[0], p[1], p[2], p[3], p[4], p[6], p[7], p[5]);
-}
-
-// The same synthesis with one wave per agent (lqro_synthw.hpp): the agent's
-// matrices in LDS, products and sums over the lanes in the reference's order.
-// The default; LQRO_SYNTH_LANE=1 selects k_synth.
-template <int X>
-__global__ void __launch_bounds__(64) k_synthw(const lqro_model* models, int n, double* out) {
-  extern __shared__ double sw[];
-  const int a = blockIdx.x;
-  if (a >= n) return;
-  constexpr int S = X * X + 12 * X + 25;
-  double* o = out + (size_t)a * S;
-  double* p[8];
-  p[0] = o;
-  p[1] = p[0] + X * X; p[2] = p[1] + X * 4; p[3] = p[2] + X; p[4] = p[3] + 4 * X; p[5] = p[4] + 12;
-  p[6] = p[5] + 4; p[7] = p[6] + 3 * X;
-  synthw::gains<X>(models + a, p[0], p[1], p[2], p[3], p[4], p[6], p[7], p[5], sw, threadIdx.x);
-}
-
 extern "C" {
 
 int lqro_version(void) { return 1; }
@@ -669,16 +617,8 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
     lqro_destroy(c);
     return LQRO_E_HIP;
   }
-  const void* pair_kernels[12] = {
-      (const void*)k_pair<16, false, kRowLaunch>,   (const void*)k_pair<16, true, kRowLaunch>,
-      (const void*)k_pair<12, false, kRowLaunch>,   (const void*)k_pair<12, true, kRowLaunch>,
-      (const void*)k_pair<16, false, kHotShared>,   (const void*)k_pair<16, true, kHotShared>,
-      (const void*)k_pair<12, false, kHotShared>,   (const void*)k_pair<12, true, kHotShared>,
-      (const void*)k_pair<16, false, kHotPerAgent>, (const void*)k_pair<16, true, kHotPerAgent>,
-      (const void*)k_pair<12, false, kHotPerAgent>, (const void*)k_pair<12, true, kHotPerAgent>};
-  bool attr_ok = true;
-  for (const void* k : pair_kernels)
-    attr_ok = attr_ok && hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, c->lds_bytes) == hipSuccess;
+  const bool attr_ok = pair_set_lds_t<16, false>(c->lds_bytes) && pair_set_lds_t<16, true>(c->lds_bytes) &&
+                       pair_set_lds_t<12, false>(c->lds_bytes) && pair_set_lds_t<12, true>(c->lds_bytes);
   if (!attr_ok) {
     lqro_destroy(c);
     return LQRO_E_HIP;
@@ -852,11 +792,11 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   Hh.block_base = nwait;
   Hh.big_main = lds_ok ? 0 : 1;
   if (lds_ok) {
-    hipLaunchKernelGGL(k_hull, dim3(c->hull_blocks - nwait), dim3(HULL_CTHREADS), 0, s, Hh);
+    launch_hull(dim3(c->hull_blocks - nwait), s, Hh);
     HIPCHK(hipGetLastError());
   }
   Hh.block_base = 0;
-  hipLaunchKernelGGL(k_hull_big, dim3(c->hull_big_blocks), dim3(HULL_THREADS), 0, s, Hh);
+  launch_hull_big(dim3(c->hull_big_blocks), s, Hh);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev[2], s));
   LpArgs La;
@@ -956,19 +896,7 @@ int lqro_synthesize_gains_batch_x(const lqro_model* models, int32_t n, int32_t x
     rc = LQRO_E_HIP;
   } else {
     const char* lane_env = getenv("LQRO_SYNTH_LANE");
-    const bool lane = lane_env && atoi(lane_env) == 1;
-    if (lane && x_dim == 16)
-      hipLaunchKernelGGL(k_synth<16>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, 0, (const lqro_model*)d_m,
-                         (int)n, d_out);
-    else if (lane)
-      hipLaunchKernelGGL(k_synth<12>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, 0, (const lqro_model*)d_m,
-                         (int)n, d_out);
-    else if (x_dim == 16)
-      hipLaunchKernelGGL(k_synthw<16>, dim3((unsigned)n), dim3(64), sizeof(double) * synthw::Lay<16>::Total, 0,
-                         (const lqro_model*)d_m, (int)n, d_out);
-    else
-      hipLaunchKernelGGL(k_synthw<12>, dim3((unsigned)n), dim3(64), sizeof(double) * synthw::Lay<12>::Total, 0,
-                         (const lqro_model*)d_m, (int)n, d_out);
+    launch_synth(x_dim, lane_env && atoi(lane_env) == 1, d_m, (int)n, d_out);
     std::vector<double> h((size_t)stride * n);
     if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
         hipMemcpy(h.data(), d_out, sizeof(double) * h.size(), hipMemcpyDeviceToHost) != hipSuccess) {
@@ -994,63 +922,6 @@ int lqro_synthesize_gains_batch(const lqro_model* models, int32_t n, double* A, 
   return lqro_synthesize_gains_batch_x(models, n, 16, A, B, c, L, E, nullptr, Lh, Eh, device);
 }
 
-// ---- the per-agent step after the pair loop (LQRO:1437-1446) -------------
-// One agent per lane: the step is a chain of 16x16 products, exponentials and
-// a Jacobi sweep with data-dependent control flow (lqro_dyn.hpp), fp64,
-// ~10 MFLOP per agent, latency bound on per-lane scratch.
-__global__ void __launch_bounds__(64) k_dyn(const lqro_model* models, int n_models, int n, int per_agent,
-                                            lqro_agents A) {
-  const int a = blockIdx.x * blockDim.x + threadIdx.x;
-  if (a >= n) return;
-  const size_t g = per_agent ? (size_t)a : 0;
-  dyn::AgentParams p;
-  p.model = models + (n_models > 1 ? a : 0);
-  p.L = A.L + g * dyn::kU * dyn::kX;
-  p.E = A.E + g * dyn::kU * dyn::kV;
-  p.l = A.l + g * dyn::kU;
-  p.Lh = A.Lh + g * dyn::kV * dyn::kX;
-  p.Eh = A.Eh + g * dyn::kV * dyn::kV;
-  p.u_goal = A.u_goal + (size_t)a * dyn::kU;
-  p.p_goal = A.p_goal + (size_t)a * 3;
-  p.M = A.M;
-  p.Nz = A.N;
-  p.normals = A.normals + (size_t)a * dyn::kNormals;
-  p.keyframe = A.keyframes ? A.keyframes + (size_t)a * 8 : nullptr;
-  p.time = A.time;
-  dyn::agent_step(p, A.x + (size_t)a * dyn::kX, A.rot + (size_t)a * 9, A.x_true + (size_t)a * dyn::kX,
-                  A.rot_true + (size_t)a * 9, A.P + (size_t)a * dyn::kX * dyn::kX, A.vgoal + (size_t)a * 3,
-                  A.u ? A.u + (size_t)a * dyn::kU : nullptr);
-}
-
-// The same step with one wave per agent (lqro_dynw.hpp): the agent's 16x16
-// matrices in LDS, the products, exponentials, solves and Jacobi sweep over
-// the lanes.  The default; LQRO_DYN_LANE=1 selects k_dyn.
-__global__ void __launch_bounds__(64) k_dynw(const lqro_model* models, int n_models, int n, int per_agent,
-                                             lqro_agents A) {
-  __shared__ double w[dynw::kWaveDoubles];
-  const int a = blockIdx.x;
-  if (a >= n) return;
-  const int lane = threadIdx.x;
-  const size_t g = per_agent ? (size_t)a : 0;
-  dyn::AgentParams p;
-  p.model = models + (n_models > 1 ? a : 0);
-  p.L = A.L + g * dyn::kU * dyn::kX;
-  p.E = A.E + g * dyn::kU * dyn::kV;
-  p.l = A.l + g * dyn::kU;
-  p.Lh = A.Lh + g * dyn::kV * dyn::kX;
-  p.Eh = A.Eh + g * dyn::kV * dyn::kV;
-  p.u_goal = A.u_goal + (size_t)a * dyn::kU;
-  p.p_goal = A.p_goal + (size_t)a * 3;
-  p.M = A.M;
-  p.Nz = A.N;
-  p.normals = A.normals + (size_t)a * dyn::kNormals;
-  p.keyframe = A.keyframes ? A.keyframes + (size_t)a * 8 : nullptr;
-  p.time = A.time;
-  dynw::agent_step(p, A.x + (size_t)a * dyn::kX, A.rot + (size_t)a * 9, A.x_true + (size_t)a * dyn::kX,
-                   A.rot_true + (size_t)a * 9, A.P + (size_t)a * dyn::kX * dyn::kX, A.vgoal + (size_t)a * 3,
-                   A.u ? A.u + (size_t)a * dyn::kU : nullptr, w, lane);
-}
-
 static bool agents_complete(const lqro_agents* a) {
   return a && a->x && a->rot && a->x_true && a->rot_true && a->P && a->vgoal && a->u_goal && a->p_goal &&
          a->L && a->E && a->l && a->Lh && a->Eh && a->M && a->N && a->normals;
@@ -1060,12 +931,8 @@ int lqro_dynamics_step_device(const lqro_model* models, int32_t n_models, int32_
                               const lqro_agents* agents, void* stream) {
   if (!models || n <= 0 || (n_models != 1 && n_models != n) || !agents_complete(agents)) return LQRO_E_ARG;
   const char* lane = getenv("LQRO_DYN_LANE");
-  if (lane && atoi(lane) == 1)
-    hipLaunchKernelGGL(k_dyn, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream, models,
-                       (int)n_models, (int)n, (int)(per_agent_gains != 0), *agents);
-  else
-    hipLaunchKernelGGL(k_dynw, dim3((unsigned)n), dim3(64), 0, (hipStream_t)stream, models, (int)n_models,
-                       (int)n, (int)(per_agent_gains != 0), *agents);
+  launch_dyn(lane && atoi(lane) == 1, models, (int)n_models, (int)n, (int)(per_agent_gains != 0), *agents,
+             (hipStream_t)stream);
   return hipGetLastError() == hipSuccess ? LQRO_OK : LQRO_E_HIP;
 }
 

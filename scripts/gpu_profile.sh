@@ -19,6 +19,6 @@ timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/prof_wr
 python3 scripts/pmc_traffic.py $O/prof_fetch $O/prof_write $O/${TAG}_pmc_traffic.json > /dev/null
 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $O/prof_sq1 -o run -- $B > $O/prof_sq1.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_SALU --output-format csv -d $O/prof_sq2 -o run -- $B > $O/prof_sq2.log 2>&1
-KMS=$(python3 -c "import json;d=json.load(open('$O/${TAG}_kernel_breakdown.json'));print(max((r for r in d if r['kernel'].startswith('k_pair')), key=lambda r: r['workgroups'])['avg_ms'])")
+KMS=$(python3 -c "import json;d=json.load(open('$O/${TAG}_kernel_breakdown.json'));print(max((r for r in d if r['kernel'].startswith('k_pair<16')), key=lambda r: r['workgroups'])['avg_ms'])")
 python3 scripts/pmc_sq.py $O/${TAG}_pmc_sq.json $O/prof_sq1 $O/prof_sq2 --kernel-ms $KMS > /dev/null
 echo profile $TAG done
