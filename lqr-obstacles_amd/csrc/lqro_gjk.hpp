@@ -304,7 +304,21 @@ __device__ __forceinline__ int gjk_nth_bit(int m, int n) {
   return 0;
 }
 
-__device__ __forceinline__ double gjk_shfl(double v, int src) { return __shfl(v, src, 64); }
+// v of lane src (0..63, per lane): ds_bpermute on both halves, no width
+// arithmetic on the lane id
+__device__ __forceinline__ double gjk_shfl(double v, int src) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_ds_bpermute(src << 2, (int)b);
+  const int hi = __builtin_amdgcn_ds_bpermute(src << 2, (int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// v of a wave-uniform lane: two v_readlane (no LDS round trip)
+__device__ __forceinline__ double gjk_rdl(double v, int src) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, src);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
 
 // dot_products[a][b] (gjk.cpp:541-548): csp_a . csp_b, csp = coords1 - coords2;
 // symmetric exactly (each product commutes, same summation order)
@@ -351,7 +365,7 @@ __device__ __forceinline__ int gjkw_reset(const GjkWave& G, int subset, double d
                                           int lane) {
   lane = opaque(lane);
   const int card = __popc(subset);
-  const double ds = gjk_shfl(dsum, 4 * subset);
+  const double ds = gjk_rdl(dsum, 4 * subset);
   const double lv = gjk_shfl(dv, 4 * subset + (lane & 3));
   // lanes 0..11 move coords2, lanes 0..3 the ids and lambdas
   double cv = 0.0;
@@ -409,7 +423,7 @@ __device__ __forceinline__ int gjkw_default(const GjkWave& G, int& size, double 
     // the loop ran out: reset_simplex(s) with the terminating s when the
     // last subset tested was ok (it had a tiny delta sum)
     const int last = (1 << size) - 1;
-    const int okl = __shfl(ok, 4 * last, 64);
+    const int okl = __builtin_amdgcn_readlane(ok, 4 * last);
     if (!(okl && size < 4)) return 0;
     sel = 1 << size;
   }
@@ -447,7 +461,7 @@ __device__ __forceinline__ int gjkw_backup(const GjkWave& G, const double* vrel,
   double bnum = 0.0, bden = 0.0;
   for (int t = 1; t < 16; ++t) {
     if (!((vb >> (4 * t)) & 1ull)) continue;
-    const double tn = gjk_shfl(num, 4 * t), td = gjk_shfl(den, 4 * t);
+    const double tn = gjk_rdl(num, 4 * t), td = gjk_rdl(den, 4 * t);
     if ((bests < 1) || (tn * bden < bnum * td)) { bests = t; bnum = tn; bden = td; }
   }
   return gjkw_reset(G, bests, dv, dsum, lane);

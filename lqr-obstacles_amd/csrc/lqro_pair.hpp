@@ -96,7 +96,13 @@ struct WaveTabs {
   int* mixed;                // H: list of MIXED slices
   unsigned long long* mask;  // H x PW
   GjkWave gjk;               // the GJK simplex (18 doubles)
+  unsigned long long* st;    // 5 counters (reach, iters, planes, inside, backup), lane 0 adds
 };
+
+// a wave-private LDS counter: ds_add_u64 with no return, so nothing waits on it
+__device__ __forceinline__ void lds_count(unsigned long long* c, unsigned long long v) {
+  __hip_atomic_fetch_add(c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 // Transform*(points[p] + Translate) (LQRO:776); Matrix::operator* accumulates
 // from 0.0 (include/matrix.h:223-227)
@@ -404,8 +410,12 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
     W.gjk.c2 = reinterpret_cast<double*>(wi);
     W.gjk.lam = W.gjk.c2 + 12;
     W.gjk.s2 = reinterpret_cast<int*>(W.gjk.c2 + 16);
+    W.st = reinterpret_cast<unsigned long long*>(W.gjk.c2 + 18);
   }
-  unsigned long long st_reach = 0, st_iters = 0, st_planes = 0, st_inside = 0, st_backup = 0;
+  // per-wave statistics live in the wave's LDS region (registers held across
+  // the persistent loop were spilled to scratch and reloaded every pair)
+  const bool has_region = wave < P.max_waves;
+  if (has_region && lane < 5) W.st[lane] = 0;
 #ifdef LQRO_PAIR_PROFILE
   unsigned long long pc[6] = {0, 0, 0, 0, 0, 0};
   SliceSupport sup{P, B, W, lane, pc};
@@ -544,7 +554,6 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) hsh += __shfl_xor(hsh, off);
     }
-    st_reach += n;
     PSTAMP(3);
 
     // 3. GJK and the half-plane
@@ -564,11 +573,8 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
       nrm[2] = (go.w1[2] - go.w2[2]) / distance;
       inside = (distance < 0.0001 && distance > -1 * 0.0001);  // :860
       flags = LQRO_REC_PLANE | (inside ? LQRO_REC_INSIDE : 0) | (go.backup ? LQRO_REC_BACKUP : 0);
-      st_iters += go.iters;
-      st_backup += go.backup;
       dist = distance;
       if (!inside) {
-        st_planes += 1;
         distance *= 0.5;                                        // :1416
         const double mult = -1.0;                               // :1215
         pl[0] = (float)(xi[3] + mult * distance * nrm[0]);      // :1217
@@ -577,7 +583,6 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
         pl[3] = (float)nrm[0]; pl[4] = (float)nrm[1]; pl[5] = (float)nrm[2];
         pl[6] = __int_as_float(1);
       } else {
-        st_inside += 1;
         pl[6] = __int_as_float(2);                              // completed by k_hull
       }
     }
@@ -591,6 +596,12 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
       float4* dst = reinterpret_cast<float4*>(P.planes + slot * 8);
       dst[0] = make_float4(pl[0], pl[1], pl[2], pl[3]);
       dst[1] = make_float4(pl[4], pl[5], pl[6], pl[7]);
+      lds_count(&W.st[0], (unsigned long long)n);
+      if (flags) {
+        lds_count(&W.st[1], (unsigned long long)go.iters);
+        lds_count(&W.st[inside ? 3 : 2], 1ull);
+        if (go.backup) lds_count(&W.st[4], 1ull);
+      }
       if (inside) {
         // published with release: k_hull workers may already be polling
         const int qi = atomicAdd(P.hull_count, 1);
@@ -702,7 +713,7 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
     if (wave >= P.max_waves) break;    // k_side: no LDS region for this wave
     int jj = 0;
     if (lane == 0) jj = atomicAdd(&s_next, 1);
-    jj = __shfl(jj, 0);
+    jj = __builtin_amdgcn_readlane(jj, 0);
     if (jj >= jj_end) break;
     if (P.hot_mark != nullptr && P.hot_mark[(size_t)lrow * P.npr + jj]) continue;   // done in the hot phase
     do_pair(i, lrow, jj);
@@ -714,12 +725,13 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
   if (lane == 0 && P.prof)
     for (int k = 0; k < 16; ++k) atomicAdd(&P.prof[k], pp[k]);
 #endif
-  if (lane == 0) {
-    atomicAdd(&P.stats[1], st_planes);
-    atomicAdd(&P.stats[2], st_inside);
-    atomicAdd(&P.stats[5], st_backup);
-    atomicAdd(&P.stats[6], st_reach);
-    atomicAdd(&P.stats[7], st_iters);
+  wave_lds_sync();
+  if (has_region && lane == 0) {
+    atomicAdd(&P.stats[6], W.st[0]);
+    atomicAdd(&P.stats[7], W.st[1]);
+    atomicAdd(&P.stats[1], W.st[2]);
+    atomicAdd(&P.stats[2], W.st[3]);
+    atomicAdd(&P.stats[5], W.st[4]);
   }
 }
 

@@ -569,8 +569,8 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
   P.lds_H = off; off += H;
   P.lds_wave = off;
   // tr 3H, sc H, mask H*PW (u64), cls/cnt/mixed 3H ints (mixed padded to
-  // even), GJK simplex 18
-  P.wave_doubles = 4 * H + H * P.PW + H + (H + (H & 1)) / 2 + 18;
+  // even), GJK simplex 18, statistics 5
+  P.wave_doubles = 4 * H + H * P.PW + H + (H + (H & 1)) / 2 + 18 + 5;
   const int budget = 160 * 1024 / 8;
   int waves = (budget - off) / P.wave_doubles;
   if (waves > LQRO_PAIR_LB / 64) waves = LQRO_PAIR_LB / 64;
