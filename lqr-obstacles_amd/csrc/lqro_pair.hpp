@@ -139,11 +139,23 @@ __device__ __forceinline__ void argmax_step(double& v, int& q) {
   if (better(ov, oq, v, q)) { v = ov; q = oq; }
 }
 
-#ifndef LQRO_ARGMAX_PAIRS
 template <int CTRL, int ROWS>
 __device__ __forceinline__ void max_step(double& v) {
   v = fmax(v, dpp_d<CTRL, ROWS>(-INFINITY, v));
 }
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void max_step_f(float& v) {
+  v = fmaxf(v, __int_as_float(dpp_i<CTRL, ROWS>(__float_as_int(-INFINITY), __float_as_int(v))));
+}
+// v of a wave-uniform lane (two v_readlane)
+__device__ __forceinline__ double rdl_d(double v, int src) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, src);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+#ifndef LQRO_ARGMAX_PAIRS
 template <int CTRL, int ROWS>
 __device__ __forceinline__ void min_step(int& q) {
   q = min(q, dpp_i<CTRL, ROWS>(INT_MAX, q));
@@ -233,25 +245,63 @@ struct SliceSupport {
     }
   }
 
-  // best (value, q, point) over the reachable points of slice k, merged into (bv, bq, bx)
+  // best (value, q, point) over the reachable points of slice k, merged into
+  // (bv, bq, bx).  Lane L holds points p = L + 64 pw, in increasing p, so a
+  // strict > keeps each lane's first maximiser; the slice's first maximiser
+  // is then the lowest lane of the lowest pw group among the lanes holding
+  // the wave maximum (ballots, no index reduction).
   __device__ void eval_slice(int k, double d0, double d1, double d2, double& bv, int& bq, double* bx) const {
+    const double* Tk = B.T + 9 * k;
+    const double* tk = W.tr + 3 * k;
+    double T[9];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) T[e] = Tk[e];
+    const double t0 = tk[0], t1 = tk[1], t2 = tk[2];
     double lv = -INFINITY;
-    int lq = INT_MAX;
+    int lp = INT_MAX;
     double lx[3] = {0.0, 0.0, 0.0};
-    for (int pw = 0; pw < P.PW; ++pw) {
+#pragma unroll
+    for (int pw = 0; pw < kMaxPW; ++pw) {
+      if (pw >= P.PW) break;
       const int p = pw * 64 + lane;
       const unsigned long long bits = W.mask[k * P.PW + pw];
       if (p < P.NP && ((bits >> lane) & 1ull)) {
-        double x[3];
-        exact_point(B, W, P.NP, k, p, x);
-        const double v = x[0] * d0 + x[1] * d1 + x[2] * d2;   // SUPPORT_DOT_PRODUCT
-        const int q = k * P.NP + p;
-        if (better(v, q, lv, lq)) { lv = v; lq = q; lx[0] = x[0]; lx[1] = x[1]; lx[2] = x[2]; }
+        // exact_point (LQRO:776, matrix.h:223-227)
+        const double u0 = B.S[p] + t0;
+        const double u1 = B.S[P.NP + p] + t1;
+        const double u2 = B.S[2 * P.NP + p] + t2;
+        const double x0 = ((0.0 + T[0] * u0) + T[1] * u1) + T[2] * u2;
+        const double x1 = ((0.0 + T[3] * u0) + T[4] * u1) + T[5] * u2;
+        const double x2 = ((0.0 + T[6] * u0) + T[7] * u1) + T[8] * u2;
+        const double v = x0 * d0 + x1 * d1 + x2 * d2;   // SUPPORT_DOT_PRODUCT
+        if (v > lv) { lv = v; lp = p; lx[0] = x0; lx[1] = x1; lx[2] = x2; }
       }
     }
-    const int myq = lq;
-    wave_argmax(lv, lq);
-    if (better(lv, lq, bv, bq)) { bv = lv; bq = lq; take_point(myq, lq, lx, bx); }
+    double m = lv;
+    max_step<0x111, 0xF>(m);   // row_shr:1
+    max_step<0x112, 0xF>(m);   // row_shr:2
+    max_step<0x114, 0xF>(m);   // row_shr:4
+    max_step<0x118, 0xF>(m);   // row_shr:8
+    max_step<0x142, 0xA>(m);   // row_bcast:15
+    max_step<0x143, 0xC>(m);   // row_bcast:31
+    m = rdl_d(m, 63);
+    unsigned long long w = 0;
+#pragma unroll
+    for (int pw = 0; pw < kMaxPW; ++pw) {
+      if (pw >= P.PW) break;
+      w = __ballot(lv == m && (lp >> 6) == pw);
+      if (w) break;
+    }
+    if (!w) return;
+    const int wl = __ffsll((long long)w) - 1;
+    const double v = rdl_d(lv, wl);
+    const int q = k * P.NP + __builtin_amdgcn_readlane(lp, wl);
+    if (better(v, q, bv, bq)) {
+      bv = v;
+      bq = q;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) bx[c] = rdl_d(lx[c], wl);
+    }
   }
 
   // support_simple semantics: lowest-index maximiser of p.d over the reachable set.
@@ -274,6 +324,9 @@ struct SliceSupport {
 #endif
     // magnitudes below only scale the 1e-9 margins: the hardware square root
     // (a few ulp) is ample there
+#ifdef LQRO_PAIR_PROFILE
+    const unsigned long long t0s_ = __builtin_amdgcn_s_memtime();
+#endif
     const double dn = __builtin_amdgcn_sqrt(d0 * d0 + d1 * d1 + d2 * d2);
     double cu = -INFINITY;
     int ck = INT_MAX;
@@ -298,11 +351,33 @@ struct SliceSupport {
       }
       ubr[s] = ub;
     }
-    wave_argmax(cu, ck);
+    // the slice evaluated first only needs a (near-)largest bound — any
+    // choice gives the same result, the candidate pass covers the rest — so
+    // the maximum is taken in fp32 and its lowest lane wins
+    {
+      float mf = (float)cu;
+      const float cf = mf;
+      max_step_f<0x111, 0xF>(mf);
+      max_step_f<0x112, 0xF>(mf);
+      max_step_f<0x114, 0xF>(mf);
+      max_step_f<0x118, 0xF>(mf);
+      max_step_f<0x142, 0xA>(mf);
+      max_step_f<0x143, 0xC>(mf);
+      mf = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mf), 63));
+      const unsigned long long w = __ballot(ck != INT_MAX && cf == mf);
+      ck = w ? __builtin_amdgcn_readlane(ck, __ffsll((long long)w) - 1) : INT_MAX;
+    }
+#ifdef LQRO_PAIR_PROFILE
+    const unsigned long long t1_ = __builtin_amdgcn_s_memtime();
+    pc[6] += t1_ - t0s_;
+#endif
     bv = -INFINITY;
     bq = INT_MAX;
     if (ck == INT_MAX) return;
     eval_slice(ck, d0, d1, d2, bv, bq, bx);
+#ifdef LQRO_PAIR_PROFILE
+    pc[7] += __builtin_amdgcn_s_memtime() - t1_;
+#endif
     // candidates: the other slices whose bound reaches bv (usually none)
     unsigned long long cb[kMaxKS];
     unsigned long long any = 0;
@@ -417,7 +492,7 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
   const bool has_region = wave < P.max_waves;
   if (has_region && lane < 5) W.st[lane] = 0;
 #ifdef LQRO_PAIR_PROFILE
-  unsigned long long pc[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long pc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   SliceSupport sup{P, B, W, lane, pc};
 #else
   SliceSupport sup{P, B, W, lane};
@@ -554,7 +629,7 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
 #pragma unroll
       for (int off = 32; off >= 1; off >>= 1) hsh += __shfl_xor(hsh, off);
     }
-    PSTAMP(3);
+    PSTAMP(2);
 
     // 3. GJK and the half-plane
     int flags = 0;
@@ -632,7 +707,7 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
 #ifdef LQRO_PAIR_PROFILE
     pp[11] += 1;
     pp[12] = pc[0]; pp[13] = pc[1]; pp[14] = pc[2];
-    pp[6] = pc[3]; pp[8] = pc[4]; pp[9] = pc[5];
+    pp[6] = pc[3]; pp[8] = pc[4]; pp[9] = pc[5]; pp[15] = pc[6]; pp[3] = pc[7];
 #endif
     };
   // Hot launch (shared gains only): the pairs k_prio marked as likely
