@@ -582,42 +582,68 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
 
     // 2. MIXED slices: per-point exact test                 (lanes <-> p)
     // n_reach and the first reachable point come out of the same ballots,
-    // wave-uniform: IN slices count NP each, MIXED ones their ballot bits
+    // wave-uniform: IN slices count NP each, MIXED ones their ballot bits.
+    // The MIXED slices are walked as the set bits of their class ballots
+    // (increasing k), each slice's T_k / Translate_k read once for its pw
+    // groups.
     int nmixed = 0, n = 0, qfirst = INT_MAX;
-    for (int base = 0; base < H; base += 64) {
-      const int k = base + ln;
+    unsigned long long mmask[kMaxKS];
+#pragma unroll
+    for (int s = 0; s < kMaxKS; ++s) {
+      const int k = 64 * s + ln;
       const int c = k < H ? W.cls[k] : kSliceOut;
       const unsigned long long bal = __ballot(c == kSliceMixed);
       const unsigned long long bin = __ballot(c == kSliceIn);
-      if (c == kSliceMixed) W.mixed[nmixed + __popcll(bal & ((1ull << ln) - 1ull))] = k;
+      mmask[s] = bal;
       nmixed += __popcll(bal);
       n += NP * __popcll(bin);
-      if (bin && qfirst == INT_MAX) qfirst = (base + __ffsll((long long)bin) - 1) * NP;
+      if (bin && qfirst == INT_MAX) qfirst = (64 * s + __ffsll((long long)bin) - 1) * NP;
     }
-    wave_lds_sync();
-    for (int mi = 0; mi < nmixed; ++mi) {
-      const int k = W.mixed[mi];
-      int cnt = 0;
-      for (int pw = 0; pw < P.PW; ++pw) {
-        const int p = pw * 64 + ln;
-        bool ok = false;
-        if (p < NP) {
-          double x[3];
-          exact_point(B, W, NP, k, p, x);
-          ok = reach_exact(x[0] - vrel[0], x[1] - vrel[1], x[2] - vrel[2], P);
+#pragma unroll
+    for (int s = 0; s < kMaxKS; ++s) {
+      unsigned long long mm = mmask[s];
+      while (mm) {
+        const int k = 64 * s + __ffsll((long long)mm) - 1;
+        mm &= mm - 1ull;
+        const double* Tk = B.T + 9 * k;
+        const double* tk = W.tr + 3 * k;
+        double T[9];
+#pragma unroll
+        for (int e = 0; e < 9; ++e) T[e] = Tk[e];
+        const double t0 = tk[0], t1 = tk[1], t2 = tk[2];
+        bool ok[kMaxPW];
+#pragma unroll
+        for (int pw = 0; pw < kMaxPW; ++pw) {
+          const int p = pw * 64 + ln;
+          ok[pw] = false;
+          if (pw < P.PW && p < NP) {
+            // exact_point (LQRO:776, matrix.h:223-227)
+            const double u0 = B.S[p] + t0;
+            const double u1 = B.S[NP + p] + t1;
+            const double u2 = B.S[2 * NP + p] + t2;
+            const double x0 = ((0.0 + T[0] * u0) + T[1] * u1) + T[2] * u2;
+            const double x1 = ((0.0 + T[3] * u0) + T[4] * u1) + T[5] * u2;
+            const double x2 = ((0.0 + T[6] * u0) + T[7] * u1) + T[8] * u2;
+            ok[pw] = reach_exact(x0 - vrel[0], x1 - vrel[1], x2 - vrel[2], P);
+          }
         }
-        const unsigned long long bal = __ballot(ok);
-        if (ok && want_hash) hsh += mix64((uint64_t)(k * NP + p));   // records only
-        if (ln == 0) W.mask[k * P.PW + pw] = bal;
-        // mixed slices come in increasing k: the first set bit seen is the
-        // first reachable point of the MIXED slices
-        if (bal && cnt == 0 && k * NP < qfirst) qfirst = k * NP + pw * 64 + __ffsll((long long)bal) - 1;
-        cnt += __popcll(bal);
-      }
-      n += cnt;
-      if (ln == 0) {
-        W.cnt[k] = cnt;
-        if (cnt == 0) W.cls[k] = kSliceOut;
+        int cnt = 0;
+#pragma unroll
+        for (int pw = 0; pw < kMaxPW; ++pw) {
+          if (pw >= P.PW) break;
+          const unsigned long long bal = __ballot(ok[pw]);
+          if (ok[pw] && want_hash) hsh += mix64((uint64_t)(k * NP + pw * 64 + ln));   // records only
+          if (ln == 0) W.mask[k * P.PW + pw] = bal;
+          // mixed slices come in increasing k: the first set bit seen is the
+          // first reachable point of the MIXED slices
+          if (bal && cnt == 0 && k * NP < qfirst) qfirst = k * NP + pw * 64 + __ffsll((long long)bal) - 1;
+          cnt += __popcll(bal);
+        }
+        n += cnt;
+        if (ln == 0) {
+          W.cnt[k] = cnt;
+          if (cnt == 0) W.cls[k] = kSliceOut;
+        }
       }
     }
     wave_lds_sync();
