@@ -296,7 +296,12 @@ __global__ void __launch_bounds__(64) k_lp4(LpArgs A, int proj_in_lds) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#ifdef LQRO_LP_PROFILE
+    int lp4_iters = 0;
+    w_lp4<PS>(planes, m, fail, (float)A.vmax, nv, proj, lane, lp4_iters);  // :1230
+#else
     w_lp4<PS>(planes, m, fail, (float)A.vmax, nv, proj, lane);              // :1230
+#endif
     if (lane == 0) {
       const int i = A.row_begin + lrow * A.row_stride;
       A.newv[3 * i] = nv.x;
