@@ -294,14 +294,30 @@ struct GjkWave {
   int* s2;      // [4] point ids (LDS)
 };
 
-__device__ __forceinline__ int gjk_nth_bit(int m, int n) {
-#pragma unroll
+// position of the n-th set bit of the 4-bit mask m (0 when m has fewer), as
+// a 2-bit entry of a 128-bit constant table indexed by 4 m + n: branch-free
+// (a per-lane loop here became exec-mask branching in the wave-parallel code)
+constexpr int gjk_nth_bit_ref(int m, int n) {
   for (int b = 0; b < 4; ++b)
     if ((m >> b) & 1) {
       if (n == 0) return b;
       --n;
     }
   return 0;
+}
+constexpr unsigned long long gjk_nth_tab(int half) {
+  unsigned long long t = 0;
+  for (int idx = 0; idx < 32; ++idx) {
+    const int g = 32 * half + idx;
+    t |= (unsigned long long)gjk_nth_bit_ref(g >> 2, g & 3) << (2 * idx);
+  }
+  return t;
+}
+__device__ __forceinline__ int gjk_nth_bit(int m, int n) {
+  constexpr unsigned long long lo = gjk_nth_tab(0), hi = gjk_nth_tab(1);
+  const int idx = ((m & 15) << 2) | (n & 3);
+  const unsigned long long t = idx < 32 ? lo : hi;
+  return (int)((t >> (2 * (idx & 31))) & 3ull);
 }
 
 // v of lane src (0..63, per lane): ds_bpermute on both halves, no width
