@@ -336,6 +336,13 @@ __device__ __forceinline__ double gjk_rdl(double v, int src) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
+// dv of lane 4 (lane / 4) + J: a quad_perm DPP broadcast inside each group of
+// four lanes (VALU) instead of a ds_bpermute round trip
+template <int J>
+__device__ __forceinline__ double gjk_quad(double v) {
+  return dpp_d<J * 0x55, 0xF>(0.0, v);
+}
+
 // dot_products[a][b] (gjk.cpp:541-548): csp_a . csp_b, csp = coords1 - coords2;
 // symmetric exactly (each product commutes, same summation order)
 __device__ __forceinline__ double gjk_dp(const GjkWave& G, const double* vrel, int a, int b) {
@@ -356,9 +363,10 @@ __device__ __forceinline__ void gjkw_subterms(const GjkWave& G, const double* vr
   const int e = gjk_nth_bit(s, j);
   if (live && card == 1) dv = 1.0;
   if (live && card == 2) {
+    // j = 0: dp[e1][e1] - dp[e1][e0];  j = 1: dp[e0][e0] - dp[e0][e1]
     const int e0 = gjk_nth_bit(s, 0), e1 = gjk_nth_bit(s, 1);
-    dv = j == 0 ? gjk_dp(G, vrel, e1, e1) - gjk_dp(G, vrel, e1, e0)
-                : gjk_dp(G, vrel, e0, e0) - gjk_dp(G, vrel, e0, e1);
+    const int a = j == 0 ? e1 : e0, b = j == 0 ? e0 : e1;
+    dv = gjk_dp(G, vrel, a, a) - gjk_dp(G, vrel, a, b);
   }
 #pragma unroll
   for (int c = 3; c <= 4; ++c) {
@@ -408,9 +416,10 @@ __device__ __forceinline__ int gjkw_default(const GjkWave& G, int& size, double 
   const bool valid = s >= 1 && (s >> size) == 0;
   int ok = 1;
   double ds = 0.0;
+  const double q[4] = {gjk_quad<0>(dv), gjk_quad<1>(dv), gjk_quad<2>(dv), gjk_quad<3>(dv)};
 #pragma unroll
   for (int jj = 0; jj < 4; ++jj) {
-    const double v = gjk_shfl(dv, 4 * s + jj);
+    const double v = q[jj];   // delta_values[s][elts[s][jj]]
     if (jj < card && ok) {
       if (v > 0.0) ds += v;
       else ok = 0;
@@ -454,9 +463,7 @@ __device__ __forceinline__ int gjkw_backup(const GjkWave& G, const double* vrel,
   const int s = lane >> 2;
   const int card = __popc(s);
   const bool valid = s >= 1 && (s >> size) == 0;
-  double v[4];
-#pragma unroll
-  for (int jj = 0; jj < 4; ++jj) v[jj] = gjk_shfl(dv, 4 * s + jj);
+  const double v[4] = {gjk_quad<0>(dv), gjk_quad<1>(dv), gjk_quad<2>(dv), gjk_quad<3>(dv)};
   bool viable = valid && dsum > 0.0;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
