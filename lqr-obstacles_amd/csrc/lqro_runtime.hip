@@ -370,6 +370,12 @@ struct lqro_ctx {
   int hot_on;                // LQRO_HOT (default 1)
   int hull_big_only;         // LQRO_HULL_BIG: skip the LDS hull (A/B)
   double hot_t, hot_r;       // k_prio horizon (s) and radius (m): LQRO_HOT_T, LQRO_HOT_R
+  // inside-hull pairs of an earlier step (pinned, copied at the end of each
+  // step; ~0 = none yet): above hot_max_inside the side CUs cannot keep up
+  // with the hulls and the plain schedule (every CU on the hulls after the
+  // sweep) is faster (scripts/crowded.py)
+  unsigned long long* h_inside;
+  long hot_max_inside;       // LQRO_HOT_MAX_INSIDE (default 2 x side CUs)
   int hull_big_blocks;
   int n_cu;
   int side_cus;              // CUs running k_hull beside k_pair (LQRO_SIDE_HULL_CUS)
@@ -453,6 +459,7 @@ void lqro_destroy(lqro_ctx* c) {
     if (c->ev[k]) (void)hipEventDestroy(c->ev[k]);
   for (int k = 0; k < 2; ++k)
     if (c->xev[k]) (void)hipEventDestroy(c->xev[k]);
+  if (c->h_inside) (void)hipHostFree(c->h_inside);
   if (c->side) (void)hipStreamDestroy(c->side);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -494,6 +501,8 @@ static int ctx_alloc(lqro_ctx* c) {
   HIPCHK(hipMalloc(&c->d_rq, sizeof(int) * c->hull_cap));
   HIPCHK(hipMalloc(&c->d_err, sizeof(int)));
   HIPCHK(hipMalloc(&c->d_stats, sizeof(unsigned long long) * 8));
+  HIPCHK(hipHostMalloc((void**)&c->h_inside, sizeof(unsigned long long), hipHostMallocDefault));
+  *c->h_inside = ~0ull;
   HIPCHK(hipMalloc(&c->d_prof, sizeof(unsigned long long) * LQRO_PROF_WORDS));
   HIPCHK(hipMemset(c->d_prof, 0, sizeof(unsigned long long) * LQRO_PROF_WORDS));
   c->hull_blocks = 256;   // one 138 KB-LDS workgroup per CU, persistent over the queue
@@ -551,6 +560,8 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
     const char* hr = getenv("LQRO_HOT_R");
     c->hot_t = ht ? atof(ht) : 3.0;
     c->hot_r = hr ? atof(hr) : 3.0;
+    const char* hm = getenv("LQRO_HOT_MAX_INSIDE");
+    c->hot_max_inside = hm ? atol(hm) : 2L * c->side_cus;
   }
   c->rb = g.row_begin;
   c->re = (g.row_end > g.row_begin) ? g.row_end : g.n_agents;
@@ -731,8 +742,13 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   // (C3: 177 hulls of <= 1,700 vertices); at H*NP > 16,383 (C5: 40 % of the
   // hulls outgrow its 2,048 vertices and retry in k_hull_big) the plain
   // schedule is faster (516 vs 1,150 ms per C5 shard step, scripts/c5_once.py)
+  // crowded swarms (many inside-hull pairs in an earlier step: the value is
+  // read without waiting for the copy, it only picks the schedule, and every
+  // schedule gives bit-identical results) take the plain schedule
+  const unsigned long long inside_prev = *(volatile unsigned long long*)c->h_inside;
+  const bool crowded = inside_prev != ~0ull && inside_prev > (unsigned long long)std::max(0L, c->hot_max_inside);
   const bool hot = c->hot_on && lds_ok && (size_t)g.horizon * g.n_points <= 16383 && side_waves >= 1 &&
-                   c->n_cu >= 64 && slots >= 65536 && c->nbr_k <= 0;
+                   c->n_cu >= 64 && slots >= 65536 && c->nbr_k <= 0 && !crowded;
   const int nwait = hot ? c->side_cus : 0;
   P.row_split = std::max(1, std::min(16, (2 * c->n_cu + c->nrows - 1) / c->nrows));
   const int units = c->nrows * P.row_split;
@@ -810,6 +826,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   La.vgoal = d_vgoal; La.newv = d_newv; La.prof = c->d_prof;
   La.lp4_list = c->d_lp4; La.lp4_count = c->d_hcount + 9; La.lp4_next = c->d_hcount + 10;
   HIPCHK(launch_lp(La, s));
+  HIPCHK(hipMemcpyAsync(c->h_inside, c->d_stats + 2, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
   HIPCHK(hipEventRecord(c->ev[3], s));
   c->stepped = 1;
   return LQRO_OK;
