@@ -371,11 +371,12 @@ struct lqro_ctx {
   int hull_big_only;         // LQRO_HULL_BIG: skip the LDS hull (A/B)
   double hot_t, hot_r;       // k_prio horizon (s) and radius (m): LQRO_HOT_T, LQRO_HOT_R
   // inside-hull pairs of an earlier step (pinned, copied at the end of each
-  // step; ~0 = none yet): above hot_max_inside the side CUs cannot keep up
-  // with the hulls and the plain schedule (every CU on the hulls after the
-  // sweep) is faster (scripts/crowded.py)
+  // step; ~0 = none yet) size the side stream: beyond 2 per side CU it widens
+  // by a third (at most half the CUs), beyond 4 per (widened) side CU the
+  // side CUs cannot keep up with the hulls and the plain schedule (every CU
+  // on the hulls after the sweep) is faster (scripts/crowded.py)
   unsigned long long* h_inside;
-  long hot_max_inside;       // LQRO_HOT_MAX_INSIDE (default 2 x side CUs)
+  long hot_max_inside;       // LQRO_HOT_MAX_INSIDE (-1: 4 x the side CUs)
   int hull_big_blocks;
   int n_cu;
   int side_cus;              // CUs running k_hull beside k_pair (LQRO_SIDE_HULL_CUS)
@@ -561,7 +562,7 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
     c->hot_t = ht ? atof(ht) : 3.0;
     c->hot_r = hr ? atof(hr) : 3.0;
     const char* hm = getenv("LQRO_HOT_MAX_INSIDE");
-    c->hot_max_inside = hm ? atol(hm) : 2L * c->side_cus;
+    c->hot_max_inside = hm ? atol(hm) : -1L;
   }
   c->rb = g.row_begin;
   c->re = (g.row_end > g.row_begin) ? g.row_end : g.n_agents;
@@ -746,10 +747,14 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   // read without waiting for the copy, it only picks the schedule, and every
   // schedule gives bit-identical results) take the plain schedule
   const unsigned long long inside_prev = *(volatile unsigned long long*)c->h_inside;
-  const bool crowded = inside_prev != ~0ull && inside_prev > (unsigned long long)std::max(0L, c->hot_max_inside);
+  const bool known = inside_prev != ~0ull;
+  int side = c->side_cus;
+  if (known && inside_prev > 2ull * (unsigned long long)side) side = std::min(c->n_cu / 2, (4 * side) / 3);
+  const long max_inside = c->hot_max_inside >= 0 ? c->hot_max_inside : 4L * side;
+  const bool crowded = known && inside_prev > (unsigned long long)max_inside;
   const bool hot = c->hot_on && lds_ok && (size_t)g.horizon * g.n_points <= 16383 && side_waves >= 1 &&
                    c->n_cu >= 64 && slots >= 65536 && c->nbr_k <= 0 && !crowded;
-  const int nwait = hot ? c->side_cus : 0;
+  const int nwait = hot ? side : 0;
   P.row_split = std::max(1, std::min(16, (2 * c->n_cu + c->nrows - 1) / c->nrows));
   const int units = c->nrows * P.row_split;
   const unsigned nblk = (unsigned)std::min(units, c->n_cu - nwait);
