@@ -566,15 +566,14 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
       if (dc + Rk < P.vmax - slack) cls = kSliceIn;
       else if (dc - Rk > P.vmax + slack) cls = kSliceOut;
       W.cls[k] = cls;
-      for (int pw = 0; pw < P.PW; ++pw) {
-        unsigned long long m = 0;
-        if (cls == kSliceIn) {
+      // masks are read for live slices only (MIXED ones are written by the
+      // per-point test); counts only by the records' simplex ranks
+      if (cls == kSliceIn)
+        for (int pw = 0; pw < P.PW; ++pw) {
           const int left = NP - pw * 64;
-          m = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
+          W.mask[k * P.PW + pw] = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
         }
-        W.mask[k * P.PW + pw] = m;
-      }
-      W.cnt[k] = cls == kSliceIn ? NP : 0;
+      if (RECS) W.cnt[k] = cls == kSliceIn ? NP : 0;
       if (cls == kSliceIn) hsh += B.shash[k];
     }
     wave_lds_sync();
@@ -641,7 +640,7 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
         }
         n += cnt;
         if (ln == 0) {
-          W.cnt[k] = cnt;
+          if (RECS) W.cnt[k] = cnt;
           if (cnt == 0) W.cls[k] = kSliceOut;
         }
       }
