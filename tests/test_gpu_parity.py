@@ -214,6 +214,40 @@ def test_overlap_schedule_identical(lqro_mod, gains, monkeypatch, kind):
             assert np.array_equal(r[f], r0[f]), f
 
 
+def test_adaptive_schedule_identical(lqro_mod, gains, monkeypatch):
+    """The schedule adapts to the inside-hull count of an earlier step: a
+    crowded swarm (1024 agents in a 22 m box, ~1,100 inside-hull pairs) takes
+    the plain schedule from its second step on, a moderately dense one (30 m,
+    ~420) a widened side stream.  Records and new velocities of those steps
+    equal the plain schedule's and the forced overlap's bit for bit."""
+    N, H, NP = 1024, 100, 100
+    for box in (22.0, 30.0):
+        x, vg = lqro_mod.synthetic_swarm(N, box=box, seed=7)
+        outs = []
+        for env in ({"LQRO_HOT": "0"}, {}, {"LQRO_HOT_MAX_INSIDE": "1000000"}):
+            for k in ("LQRO_HOT", "LQRO_SIDE_HULL_CUS", "LQRO_HOT_R", "LQRO_HOT_MAX_INSIDE"):
+                monkeypatch.delenv(k, raising=False)
+            for k, v in env.items():
+                monkeypatch.setenv(k, v)
+            ctx = lqro_mod.Context(lqro_mod.config(N, H, NP, flags=lqro_mod.LQRO_FLAG_RECORDS))
+            ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
+            ctx.step(x, vg)                  # the count the next steps are scheduled by
+            v = ctx.step(x, vg)
+            r = ctx.records()
+            v3 = ctx.step(x, vg)
+            st = ctx.stats()
+            ctx.close()
+            assert np.array_equal(v, v3)
+            assert st["hull_fail"] == 0
+            outs.append((v, r, st["inside"]))
+        v0, r0, n_in = outs[0]
+        assert n_in > (300 if box == 30.0 else 800)
+        for v, r, _ in outs[1:]:
+            assert np.array_equal(v, v0)
+            for f in ("n_reach", "reach_hash", "flags", "facet", "dist", "normal", "plane_point", "plane_normal"):
+                assert np.array_equal(r[f], r0[f]), f
+
+
 @pytest.mark.parametrize("case", ["two_agents", "far_apart", "max_horizon"])
 def test_edge_cases(lqro_mod, oracle, gains, case):
     """Edge sizes: a single pair each way; a swarm so sparse that no pair
