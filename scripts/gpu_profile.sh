@@ -9,7 +9,10 @@ TAG=${1:-rX}
 export TMPDIR=/tmp
 O=gpurun_out
 mkdir -p $O
-B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline"
+# the profiled command runs C3 only (--no-configs): C4 / C5 steps can take the
+# plain schedule, whose full-grid k_pair launches would otherwise be averaged
+# with the C3 roofline probe's (same grid)
+B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-configs"
 # the traffic passes first: their summary (stamped with this liblqro.so) goes
 # into profiles/ so that the bench line below cites it as roofline.traffic
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/prof_fetch -o run -- $B > $O/prof_fetch.log 2>&1
