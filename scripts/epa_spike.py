@@ -1,13 +1,20 @@
 """Research spike (CPU, not product): can the inside-hull branch find the
 canonical facet from a LOCAL hull around vrel instead of the full hull?
 
-EPA-style expansion: Q = hull of a few support points (26 directions); repeat:
-every Q-facet whose plane distance from vrel (rounded vertex) is within
-V* + delta of the best certified rule value V* is either certified (no point
-of the pair's rounded set beyond it, the oracle's eps rule) or expanded (its
-furthest point joins Q).  delta = max |P_full - P_rounded| bounds the gap
-between a facet's plane distance and the reference rule's value (which uses
-the full-precision vertex), so no facet beyond the window can win.
+EPA-style expansion: Q = hull of a few support points (26 directions),
+grown until vrel is strictly inside it; then every Q-facet whose plane
+distance from vrel is within V* + delta of the best certified rule value V*,
+and every Q-facet sharing a vertex with one of those, is either certified (no
+point of the pair's rounded set beyond it, the oracle's eps rule: a facet of
+the full hull) or expanded (its furthest point joins Q).  delta = max
+|P_full - P_rounded| bounds the gap between a facet's plane distance and the
+rule's value (which uses the full-precision vertex).  Why the window is then
+complete: D(u) = h(u) - u.vrel is positive and concave along
+great-circle arcs inside a vertex's normal cone, so any direction with
+D_Q <= W lies in the normal cone of a vertex of a window facet; those
+vertices have only certified (full-hull) facets around them, so Q and the
+full hull share their normal cones, and every full-hull facet with plane
+distance <= W is a certified facet of Q.
 Compared with the oracle's full-hull result (pyoracle.hull_branch) on the
 inside pairs of tests/golden/hull_rule.npz (dense swarm, C3).
 usage: epa_spike.py [dense|c3|both]"""
@@ -39,39 +46,72 @@ def rule_value(R, P, v, t):
     return abs(n[0] * (v[0] - p0[0]) + n[1] * (v[1] - p0[1]) + n[2] * (v[2] - p0[2])), n
 
 
-def local(R, P, v):
+def local(R, P, v, ring=True):
+    """Returns (value, canonical triple, |V|, support queries), or None when
+    vrel is not strictly inside the local hull (the full hull decides then).
+    ring: also certify every facet sharing a vertex with a window facet — with
+    vrel inside Q that makes the window complete."""
     scale = np.abs(R).max()
     eps = 1e-13 * (scale + 1.0)
     delta = np.sqrt(((P - R) ** 2).sum(1)).max() * (1 + 1e-9) + 1e-12
     V = sorted(set(int(np.argmax(R @ d)) for d in DIRS))
     queries = 0
+    cert = {}                      # triple (as produced) -> rule value; P-facets
     while True:
-        F = pyoracle.hull(R[V])
-        cand = []
-        for f in F:
-            t = tuple(V[k] for k in f)
+        F = [tuple(V[k] for k in f) for f in pyoracle.hull(R[V])]
+        info = {}
+        for t in F:
             a, b, c = R[t[0]], R[t[1]], R[t[2]]
             n = np.cross(b - a, c - a)
-            nn = np.sqrt(n @ n)
-            cand.append((abs(n @ (v - a)) / nn, t, n))
-        cand.sort(key=lambda z: z[0])
-        best, best_t, added, cert = np.inf, None, False, 0
-        for pd, t, n in cand:
-            if pd > best + delta:
-                break
+            info[t] = (n @ (v - a) / np.sqrt(n @ n), n)   # signed: < 0 inside (outward normals)
+        # vrel strictly inside Q first
+        out = [t for t in F if info[t][0] >= 0]
+        added = False
+        for t in out:
             queries += 1
+            n = info[t][1]
             d = (R - R[t[0]]) @ n
             k = int(np.argmax(d))
             if d[k] > 0 and d[k] * d[k] > eps * eps * (n @ n):
-                V = sorted(set(V) | {k})
-                added = True
+                V = sorted(set(V) | {k}); added = True; break
+            return None            # a P-facet with vrel on or outside it
+        if added:
+            continue
+        order = sorted(F, key=lambda t: -info[t][0])
+        best = min(cert.values()) if cert else np.inf
+        for t in order:            # certify the nearest facets until the window closes
+            if -info[t][0] > best + delta:
                 break
-            cert += 1
-            val, _ = rule_value(R, P, v, canon(t))
-            if val < best or (val == best and canon(t) < best_t):
-                best, best_t = val, canon(t)
-        if not added:
-            return best, best_t, len(V), queries
+            if t in cert:
+                continue
+            queries += 1
+            n = info[t][1]
+            d = (R - R[t[0]]) @ n
+            k = int(np.argmax(d))
+            if d[k] > 0 and d[k] * d[k] > eps * eps * (n @ n):
+                V = sorted(set(V) | {k}); added = True; break
+            cert[t] = rule_value(R, P, v, canon(t))[0]
+            best = min(best, cert[t])
+        if added:
+            continue
+        if ring:
+            win = [t for t in F if -info[t][0] <= best + delta]
+            wv = {u for t in win for u in t}
+            for t in F:
+                if t in cert or not (set(t) & wv):
+                    continue
+                queries += 1
+                n = info[t][1]
+                d = (R - R[t[0]]) @ n
+                k = int(np.argmax(d))
+                if d[k] > 0 and d[k] * d[k] > eps * eps * (n @ n):
+                    V = sorted(set(V) | {k}); added = True; break
+                cert[t] = rule_value(R, P, v, canon(t))[0]
+            if added:
+                continue
+        fin = [(val, canon(t)) for t, val in cert.items() if t in info]
+        val, tb = min(fin)
+        return val, tb, len(V), queries
 
 
 def run(name, N, H, box, seed):
@@ -90,8 +130,12 @@ def run(name, N, H, box, seed):
         t0 = time.time()
         k, d_full, n_full, fac = pyoracle.hull_branch(P, v)
         t1 = time.time()
-        d_loc, t_best, nverts, q = local(R, P, v)
+        res = local(R, P, v)
         t2 = time.time()
+        if res is None:
+            print(f"  {name} ({i},{j}): vrel not inside the local hull -> full hull")
+            res = (d_full, tuple(fac.tolist()), 0, 0)
+        d_loc, t_best, nverts, q = res
         t_full += t1 - t0
         t_loc += t2 - t1
         same = d_loc == d_full and sorted(t_best) == sorted(fac.tolist())
