@@ -46,6 +46,7 @@ enum {
 #define LQRO_REC_BACKUP   0x04  /* GJK took its backup procedure (GJK:663-706)          */
 #define LQRO_REC_HULL     0x08  /* the in-kernel hull produced the plane (LQRO:867-969) */
 #define LQRO_REC_HULLFAIL 0x10  /* hull degenerate / capacity exceeded                  */
+#define LQRO_REC_LOCAL    0x20  /* the plane came from the local hull (k_lhull)          */
 
 /* Static configuration.  The names follow the reference's compile-time
  * macros (LQRO:9-14) and the constants of its driver (LQRO:1387, 1224). */

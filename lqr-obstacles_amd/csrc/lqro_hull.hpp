@@ -98,6 +98,11 @@ struct HullArgs {
   int* bag;                         // per block of k_hull: HULL_BAGCAP overflow face ids (-1: empty)
   int block_base;                   // scratch index of this launch's block 0
   int big_main;                     // k_hull_big takes the main queue (H*NP too large for LDS)
+  int* lqueue;                      // k_lhull: pairs the local hull hands to the full hull
+  int* lcount;
+  int* ldone;                       // k_lhull: pairs it decided
+  unsigned long long* lfail;        // k_lhull: hand-over reasons (16 counters, cumulative)
+  unsigned long long* ljobs;        // k_lhull: per job (< 4096) 4 words: point / loop ticks (100 MHz), counts
   unsigned long long* stats;
   unsigned long long* prof;          // LQRO_HULL_PROFILE: per-phase cycles
 };

@@ -12,6 +12,9 @@ struct HullArgs;
 void launch_hull(dim3 grid, hipStream_t s, const HullArgs& A);
 // k_hull_big: one inserting wave, topology in global memory
 void launch_hull_big(dim3 grid, hipStream_t s, const HullArgs& A);
+// k_lhull: grid x 4 waves, one inside-hull pair at a time from a local hull
+// around vrel; the pairs it cannot decide go to A.lqueue (for k_hull)
+void launch_lhull(dim3 grid, hipStream_t s, const HullArgs& A);
 // controlMatrices for n models into out (stride X*X + 12X + 25 doubles):
 // k_synthw (one wave per agent) or, lane = true, k_synth (one agent per lane)
 void launch_synth(int x_dim, bool lane, const lqro_model* d_models, int n, double* d_out);

@@ -1,0 +1,452 @@
+// lqro_lhull.hpp — the inside-hull branch from a LOCAL hull around vrel.
+//
+// convexHull (LQRObstacles.cpp:867-969) needs only the hull facets near
+// vrel: the rule takes the facet minimising
+//     | n_f . (vrel - P[t0(f)]) |
+// n_f from the rounded points, P at full precision.  k_lhull (one 4-wave
+// workgroup per inside-hull pair, persistent over the queue k_pair fills)
+// grows a small hull Q of the pair's rounded points EPA-style instead of the
+// whole hull (~800 vertices at C3):
+//   1. the pair's points (hull_points) and the initial tetrahedron
+//      (hull_tetra), as k_hull does;
+//   2. until vrel is strictly inside Q, the facet vrel is on or beyond takes
+//      its furthest point;
+//   3. every Q-facet whose plane distance from vrel is within W = V* + delta
+//      is CERTIFIED (a scan over all points finds none beyond it by the
+//      hull's eps rule: it is a facet of the full hull) or takes its furthest
+//      point; V* = the smallest rule value of a certified facet, delta
+//      bounds | P - P_rounded | (rule value vs plane distance);
+//   4. so is every Q-facet sharing a vertex with such a window facet.
+// Why the window is then complete: D(u) = h(u) - u.vrel is
+// positive and concave along great-circle arcs inside a vertex's normal cone,
+// so any direction with D_Q(u) <= W lies in the normal cone of a vertex of a
+// window facet; those vertices have only certified facets around them, so Q
+// and the full hull share their normal cones there, and every full-hull facet
+// with plane distance <= W — the only ones whose rule value can reach V* — is
+// a certified facet of Q.  The selection (hull_select over the certified
+// facets) is then the full hull's, bit for bit.
+// The full hull (k_hull) decides instead whenever the argument's premises are
+// not met by a margin: vrel on or outside a facet of the full hull (GJK's
+// inside test has a tolerance), a point within 64 eps of a facet's plane or
+// of a new vertex's horizon (64 eps: near-coplanar input, where the facet set
+// depends on the hull's tie rules), capacity (LH_VMAX vertices, LH_FMAX
+// faces), a degenerate point set.  Those pairs go to k_hull's queue.
+#pragma once
+#include "lqro_hull.hpp"
+
+namespace lqro {
+
+#define LH_THREADS 512
+#define LH_DIRS 32                // initial support directions (Fibonacci sphere)
+#define LH_VMAX 256
+#define LH_FMAX 512
+#define LH_EMAX 1536
+#define LH_ITERS 2048
+#define LH_LCAP 3072              // live points kept in LDS once compaction gets them this few
+
+struct LHullL {
+  // hull_points / hull_tetra / hl_argmax / hl_scan / hull_take_job
+  double tr[3 * 128];
+  double rk[LH_THREADS / 64];
+  int ri[LH_THREADS / 64];
+  int scan[LH_THREADS / 64];
+  int n, fail, job, slot, init[4];
+  double eps;
+  // the local hull Q
+  double vx[LH_VMAX][3];             // vertex coordinates (rounded points)
+  int vpid[LH_VMAX];                 // vertex -> point id
+  unsigned short fv[LH_FMAX][3];     // outward counter-clockwise
+  unsigned short fa[LH_FMAX][3];     // written by hull_tetra, unused
+  double fn[LH_FMAX][4];             // n = (b-a) x (c-a), n.n
+  double sd[LH_FMAX];                // n.(vrel - a) / |n|  (< 0: vrel inside)
+  unsigned char alive[LH_FMAX], cert[LH_FMAX];
+  unsigned short freel[LH_FMAX];     // retired face slots (a stack)
+  unsigned short ea[LH_EMAX], eb[LH_EMAX];   // edges of the visible region
+  unsigned int vmark[LH_VMAX / 32];
+  int nf, nfree, nv, ne, nh, task, tface;
+  int nc, cb, ncompact, inlds;       // live points, their global buffer, next compaction at nv, in lp
+  double4 lp[LH_LCAP];               // the live points when nc <= LH_LCAP
+  double dir[LH_DIRS][3];
+  int sup[LH_DIRS];
+  double best, delta;
+};
+
+// face f's plane and vrel's signed distance from it (one thread)
+__device__ __forceinline__ void lh_face(LHullL& L, int f, const double* vrel) {
+  double n[3];
+  hl_normal(L, f, n);
+  const double* a = L.vx[L.fv[f][0]];
+  const double nn = n[0] * n[0] + n[1] * n[1] + n[2] * n[2];
+  L.fn[f][0] = n[0]; L.fn[f][1] = n[1]; L.fn[f][2] = n[2]; L.fn[f][3] = nn;
+  L.sd[f] = (n[0] * (vrel[0] - a[0]) + n[1] * (vrel[1] - a[1]) + n[2] * (vrel[2] - a[2])) / sqrt(nn);
+  L.alive[f] = 1;
+  L.cert[f] = 0;
+}
+
+// the rule value of face f (hull_select's arithmetic: canonical rotation,
+// normal from the rounded points, distance from the full-precision vertex)
+__device__ __forceinline__ double lh_rule(const LHullL& L, int f, const double* Pr, const double* Pf,
+                                          const double* vrel) {
+  int t0 = L.vpid[L.fv[f][0]], t1 = L.vpid[L.fv[f][1]], t2 = L.vpid[L.fv[f][2]];
+  while (!(t0 < t1 && t0 < t2)) { const int a = t0; t0 = t1; t1 = t2; t2 = a; }
+  const double *a = Pr + 3 * t0, *b = Pr + 3 * t1, *c = Pr + 3 * t2;
+  const double e1[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+  const double e2[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
+  double nv[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+  const double len = sqrt(nv[0] * nv[0] + nv[1] * nv[1] + nv[2] * nv[2]);
+  nv[0] /= len; nv[1] /= len; nv[2] /= len;
+  const double* p0 = Pf + 3 * t0;
+  return fabs(nv[0] * (vrel[0] - p0[0]) + nv[1] * (vrel[1] - p0[1]) + nv[2] * (vrel[2] - p0[2]));
+}
+
+__device__ __forceinline__ int lh_wmin(int v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = min(v, __shfl_xor(v, off));
+  return v;
+}
+
+// wave 0: the next face to scan.  task 1: vrel on or beyond it (within
+// margin); 2: uncertified, in the window, nearest first; 3: uncertified,
+// sharing a vertex with a window face; 0: done.
+__device__ __forceinline__ void lh_choose(LHullL& L, int lane, double margin) {
+  const int nf = L.nf;
+  int t = INT_MAX;
+  for (int f = lane; f < nf; f += 64)
+    if (L.alive[f] && L.sd[f] >= -margin) t = min(t, f);
+  t = lh_wmin(t);
+  if (t != INT_MAX) {
+    if (lane == 0) { L.task = 1; L.tface = t; }
+    return;
+  }
+  const double W = L.best + L.delta;
+  double kb = INFINITY;
+  int fb = INT_MAX;
+  for (int f = lane; f < nf; f += 64)
+    if (L.alive[f] && !L.cert[f] && -L.sd[f] <= W && (-L.sd[f] < kb || (-L.sd[f] == kb && f < fb))) {
+      kb = -L.sd[f]; fb = f;
+    }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double ok = __shfl_xor(kb, off);
+    const int of = __shfl_xor(fb, off);
+    if (ok < kb || (ok == kb && of < fb)) { kb = ok; fb = of; }
+  }
+  if (fb != INT_MAX) {
+    if (lane == 0) { L.task = 2; L.tface = fb; }
+    return;
+  }
+  for (int w = lane; w < LH_VMAX / 32; w += 64) L.vmark[w] = 0u;
+  hl_sync();
+  for (int f = lane; f < nf; f += 64)
+    if (L.alive[f] && -L.sd[f] <= W)
+      for (int k = 0; k < 3; ++k) atomicOr(&L.vmark[L.fv[f][k] >> 5], 1u << (L.fv[f][k] & 31));
+  hl_sync();
+  t = INT_MAX;
+  for (int f = lane; f < nf; f += 64) {
+    if (!L.alive[f] || L.cert[f]) continue;
+    bool touch = false;
+    for (int k = 0; k < 3; ++k) touch |= ((L.vmark[L.fv[f][k] >> 5] >> (L.fv[f][k] & 31)) & 1u) != 0;
+    if (touch) t = min(t, f);
+  }
+  t = lh_wmin(t);
+  if (lane == 0) { L.task = t != INT_MAX ? 3 : 0; L.tface = t; }
+}
+
+// insert point q (beyond at least one face) into Q: the visible faces go,
+// a cone joins the horizon to the new vertex.  Workgroup-wide.
+__device__ __forceinline__ void lh_insert(LHullL& L, const double* Pr, int q, double eps2, double band2,
+                                          const double* vrel) {
+  const int tid = threadIdx.x;
+  const double p0 = Pr[3 * q], p1 = Pr[3 * q + 1], p2 = Pr[3 * q + 2];
+  if (tid == 0) {
+    if (L.nv >= LH_VMAX) L.fail = 24;
+    else {
+      L.vx[L.nv][0] = p0; L.vx[L.nv][1] = p1; L.vx[L.nv][2] = p2;
+      L.vpid[L.nv] = q;
+    }
+    L.ne = 0;
+    L.nh = 0;
+  }
+  hl_bar();
+  if (L.fail) return;
+  const int v = L.nv, nf = L.nf;
+  for (int f = tid; f < nf; f += blockDim.x) {
+    if (!L.alive[f]) continue;
+    const double* a = L.vx[L.fv[f][0]];
+    const double d = L.fn[f][0] * (p0 - a[0]) + L.fn[f][1] * (p1 - a[1]) + L.fn[f][2] * (p2 - a[2]);
+    const double nn = L.fn[f][3];
+    if (d > 0.0 && d * d > eps2 * nn) {
+      if (L.cert[f]) { L.fail = 25; continue; }      // cannot happen: nothing is beyond a certified face
+      const int e = atomicAdd(&L.ne, 3);
+      if (e + 3 > LH_EMAX) { L.fail = 26; continue; }
+      for (int k = 0; k < 3; ++k) { L.ea[e + k] = L.fv[f][k]; L.eb[e + k] = L.fv[f][(k + 1) % 3]; }
+      L.alive[f] = 0;
+      L.freel[atomicAdd(&L.nfree, 1)] = (unsigned short)f;
+    } else if (d > 0.0 || d * d <= band2 * nn) {
+      L.fail = 27;                                     // near-coplanar with the new vertex
+    }
+  }
+  hl_bar();
+  if (L.fail || L.ne == 0) return;   // nothing visible: q is inside Q
+  const int ne = L.ne, nfree = L.nfree;
+  for (int e = tid; e < ne; e += blockDim.x) {
+    const int a = L.ea[e], b = L.eb[e];
+    bool hz = true;
+    for (int e2 = 0; e2 < ne; ++e2)
+      if (L.ea[e2] == b && L.eb[e2] == a) { hz = false; break; }
+    if (!hz) continue;
+    const int k = atomicAdd(&L.nh, 1);
+    const int f = k < nfree ? L.freel[nfree - 1 - k] : nf + (k - nfree);
+    if (f >= LH_FMAX) { L.fail = 28; continue; }
+    L.fv[f][0] = (unsigned short)a; L.fv[f][1] = (unsigned short)b; L.fv[f][2] = (unsigned short)v;
+    lh_face(L, f, vrel);
+  }
+  hl_bar();
+  if (tid == 0 && !L.fail) {
+    const int nh = L.nh;
+    if (nh < 3) L.fail = 29;
+    if (nh <= nfree) L.nfree = nfree - nh;
+    else { L.nf = nf + (nh - nfree); L.nfree = 0; }
+    L.nv = v + 1;
+  }
+  hl_bar();
+}
+
+// the support points of directions D0 .. D0+ND-1 (lowest id on ties) -> L.sup
+template <int D0, int ND>
+__device__ __forceinline__ void lh_support(LHullL& L, const double* Pr, int n) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  double bk[ND];
+  int bi[ND];
+#pragma unroll
+  for (int d = 0; d < ND; ++d) { bk[d] = -INFINITY; bi[d] = INT_MAX; }
+  for (int q = tid; q < n; q += blockDim.x) {
+    const double x = Pr[3 * q], y = Pr[3 * q + 1], z = Pr[3 * q + 2];
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+      const double v = L.dir[D0 + d][0] * x + L.dir[D0 + d][1] * y + L.dir[D0 + d][2] * z;
+      if (v > bk[d]) { bk[d] = v; bi[d] = q; }   // q ascends per thread: first max = lowest id
+    }
+  }
+  double* sk = reinterpret_cast<double*>(L.lp);                 // scratch: lp is not in use yet
+  int* si = reinterpret_cast<int*>(sk + ND * (LH_THREADS / 64));
+#pragma unroll
+  for (int d = 0; d < ND; ++d) {
+    double k = bk[d];
+    int i = bi[d];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const double ok = __shfl_xor(k, off);
+      const int oi = __shfl_xor(i, off);
+      if (ok > k || (ok == k && oi < i)) { k = ok; i = oi; }
+    }
+    if (lane == 0) { sk[d * nw + wave] = k; si[d * nw + wave] = i; }
+  }
+  hl_bar();
+  if (tid < ND) {
+    double k = sk[tid * nw];
+    int i = si[tid * nw];
+    for (int w = 1; w < nw; ++w) {
+      const double ok = sk[tid * nw + w];
+      const int oi = si[tid * nw + w];
+      if (ok > k || (ok == k && oi < i)) { k = ok; i = oi; }
+    }
+    L.sup[D0 + tid] = i;
+  }
+  hl_bar();
+}
+
+// Drop the live points that are inside Q by more than band from every face
+// plane: Q only grows, so such a point is never beyond a later face nor
+// within band of one.  Workgroup-wide; the survivors go to the other buffer.
+__device__ __forceinline__ void lh_compact(LHullL& L, double4* C0, double4* C1, double band2) {
+  const int tid = threadIdx.x;
+  const double4* src = L.inlds ? L.lp : (L.cb ? C1 : C0);
+  double4* dst = L.cb ? C0 : C1;
+  const int nc = L.nc, nf = L.nf;
+  int base = 0;
+  for (int k0 = 0; k0 < nc; k0 += blockDim.x) {
+    const int k = k0 + tid;
+    bool keep = false;
+    double4 c;
+    if (k < nc) {
+      c = src[k];
+      for (int f = 0; f < nf && !keep; ++f) {
+        if (!L.alive[f]) continue;
+        const double* a = L.vx[L.fv[f][0]];
+        const double d = L.fn[f][0] * (c.x - a[0]) + L.fn[f][1] * (c.y - a[1]) + L.fn[f][2] * (c.z - a[2]);
+        keep = d >= 0.0 || d * d <= band2 * L.fn[f][3];
+      }
+    }
+    int tot;
+    const int pos = hl_scan(L, keep ? 1 : 0, &tot);
+    if (keep) dst[base + pos] = c;
+    base += tot;
+  }
+  const bool lds = base <= LH_LCAP;
+  if (lds) {
+    hl_bar();   // every lp read above is done; dst's stores are this block's own
+    for (int k = tid; k < base; k += blockDim.x) L.lp[k] = dst[k];
+  }
+  hl_bar();
+  if (tid == 0) { L.nc = base; L.cb ^= 1; L.ncompact = 2 * L.nv; L.inlds = lds ? 1 : 0; }
+  hl_bar();
+}
+
+// arg-max of n.(c - a) over the live points (ids x0, x1, x2 excluded), lowest
+// id on ties; per thread (the caller reduces over the workgroup)
+template <int U, class P>
+__device__ __forceinline__ void lh_scan_pts(const P* C, int nc, double n0, double n1, double n2, double a0, double a1,
+                                            double a2, int x0, int x1, int x2, double& key, int& idx) {
+  const int tid = threadIdx.x, bd = blockDim.x;
+  for (int k0 = tid; k0 < nc; k0 += U * bd) {
+    double4 c[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + u * bd;
+      if (k < nc) c[u] = C[k];
+      else c[u] = make_double4(0.0, 0.0, 0.0, -1.0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = (int)c[u].w;
+      const double d = n0 * (c[u].x - a0) + n1 * (c[u].y - a1) + n2 * (c[u].z - a2);
+      if (q >= 0 && q != x0 && q != x1 && q != x2 && (d > key || (d == key && q < idx))) { key = d; idx = q; }
+    }
+  }
+}
+
+__device__ __forceinline__ void lhull_body(const HullArgs& A, LHullL& L) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int HNP = A.H * A.NP;
+  double* Pr = A.scratch + (size_t)blockIdx.x * HNP * 6;   // rounded points
+  double* Pf = Pr + (size_t)HNP * 3;                        // full-precision points
+  // live points {x, y, z, id} (rounded), two buffers of H*NP
+  double4* C0 = reinterpret_cast<double4*>(A.iscratch + (size_t)blockIdx.x * HNP * 2 * HULL_SCR_WAVES);
+  double4* C1 = C0 + HNP;
+  for (;;) {
+    const int slot = hull_take_job(A, L, false);
+    if (slot < 0) break;
+    const int lrow = slot / A.npr, jj = A.nbr_list ? A.nbr_list[slot] : slot % A.npr;
+    const int i = A.row_begin + lrow * A.row_stride;
+    const int j = jj < i ? jj : jj + 1;
+    const double* xi = A.x + (size_t)i * A.X;
+    const double* xj = A.x + (size_t)j * A.X;
+    const double* Ti = A.T + (A.per_agent ? (size_t)i * A.H * 9 : 0);
+    const double* Ni = A.NCF + (A.per_agent ? (size_t)i * A.H * 3 * A.X : 0);
+    const double vrel[3] = {xi[3] - xj[3], xi[4] - xj[4], xi[5] - xj[5]};
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    const int n = hull_points(A, L, Ti, Ni, xi, xj, vrel, Pr, Pf);
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    int iters = 0, nscan = 0;
+    const double eps = L.eps, eps2 = eps * eps;
+    const double band = 64.0 * eps, band2 = band * band;
+    {
+      // delta = max |P - P_rounded|, with room for the rule's rounding
+      double m = 0.0;
+      int dmy = 0;
+      for (int q = tid; q < n; q += blockDim.x) {
+        const double dx = Pf[3 * q] - Pr[3 * q], dy = Pf[3 * q + 1] - Pr[3 * q + 1], dz = Pf[3 * q + 2] - Pr[3 * q + 2];
+        m = fmax(m, dx * dx + dy * dy + dz * dz);
+        C0[q] = make_double4(Pr[3 * q], Pr[3 * q + 1], Pr[3 * q + 2], (double)q);
+      }
+      hl_argmax(L, m, dmy);
+      if (tid == 0) L.delta = sqrt(m) * (1.0 + 1e-6) + band;
+    }
+    if (!L.fail) {
+      hull_tetra(L, L, Pr, n, eps, eps2, L.vpid);
+      hl_bar();
+    }
+    if (!L.fail) {
+      if (tid < 4) lh_face(L, tid, vrel);
+      if (tid == 0) { L.nf = 4; L.nv = 4; L.nfree = 0; L.best = INFINITY; L.nc = n; L.cb = 0; L.inlds = 0; }
+      hl_bar();
+      // a first Q from the support points of LH_DIRS directions (no scans
+      // per insertion), then the first compaction
+      lh_support<0, 8>(L, Pr, n);
+      lh_support<8, 8>(L, Pr, n);
+      lh_support<16, 8>(L, Pr, n);
+      lh_support<24, 8>(L, Pr, n);
+      for (int d = 0; d < LH_DIRS && !L.fail; ++d) {
+        const int q = L.sup[d];
+        bool dup = false;
+        for (int v = 0; v < L.nv; ++v) dup |= L.vpid[v] == q;
+        if (!dup) lh_insert(L, Pr, q, eps2, band2, vrel);
+      }
+      if (tid == 0) L.ncompact = L.nv;
+      hl_bar();
+      for (int it = 0;; ++it) {
+        if (L.nv >= L.ncompact) lh_compact(L, C0, C1, band2);
+        if (wave == 0) lh_choose(L, lane, band);
+        hl_bar();
+        const int task = L.task, f = L.tface;
+        iters = it;
+        if (task == 0) break;
+        if (it >= LH_ITERS) {
+          if (tid == 0) L.fail = 21;
+          break;
+        }
+        // the furthest point beyond face f (its own vertices excluded)
+        const double n0 = L.fn[f][0], n1 = L.fn[f][1], n2 = L.fn[f][2], nn = L.fn[f][3];
+        const double* av = L.vx[L.fv[f][0]];
+        const double a0 = av[0], a1 = av[1], a2 = av[2];
+        const int x0 = L.vpid[L.fv[f][0]], x1 = L.vpid[L.fv[f][1]], x2 = L.vpid[L.fv[f][2]];
+        double key = -INFINITY;
+        int idx = INT_MAX;
+        if (L.inlds) lh_scan_pts<2>(L.lp, L.nc, n0, n1, n2, a0, a1, a2, x0, x1, x2, key, idx);
+        else lh_scan_pts<8>(L.cb ? C1 : C0, L.nc, n0, n1, n2, a0, a1, a2, x0, x1, x2, key, idx);
+        hl_argmax(L, key, idx);
+        if (key > 0.0 && key * key > eps2 * nn) {
+          lh_insert(L, Pr, idx, eps2, band2, vrel);
+          if (L.fail) break;
+        } else if (key > 0.0 || key * key <= band2 * nn) {
+          if (tid == 0) L.fail = 22;                     // a point near the facet's plane
+          break;
+        } else if (task == 1) {
+          if (tid == 0) L.fail = 23;                     // vrel on or beyond a full-hull facet
+          break;
+        } else {
+          if (tid == 0) {
+            L.cert[f] = 1;
+            L.best = fmin(L.best, lh_rule(L, f, Pr, Pf, vrel));
+          }
+          hl_bar();
+        }
+      }
+    }
+    hl_bar();
+    const unsigned long long t2 = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0 && A.ljobs && L.job < 4096) {
+      unsigned long long* J = A.ljobs + 4 * (size_t)L.job;
+      J[0] = t1 - t0;
+      J[1] = t2 - t1;
+      J[2] = (unsigned long long)iters | ((unsigned long long)L.nv << 16) | ((unsigned long long)L.nc << 32);
+      J[3] = (unsigned long long)n | ((unsigned long long)L.fail << 32) | ((unsigned long long)L.nf << 40);
+    }
+    (void)nscan;
+    if (!L.fail) {
+      hull_select(A, L, L, Pr, Pf, L.vpid, L.nf, [&](int g) { return L.alive[g] && L.cert[g]; }, xi, vrel, slot,
+                  true);
+      if (tid == 0) {
+        if (A.recs) A.recs[slot].flags |= LQRO_REC_LOCAL;
+        atomicAdd(A.ldone, 1);
+      }
+    } else if (tid == 0) {
+      A.lqueue[atomicAdd(A.lcount, 1)] = slot;             // the full hull decides
+      if (A.lfail) atomicAdd(&A.lfail[L.fail >= 21 && L.fail <= 35 ? L.fail - 20 : 0], 1ull);
+    }
+    hl_bar();
+  }
+}
+
+__global__ void __launch_bounds__(LH_THREADS) k_lhull(HullArgs A) {
+  __shared__ LHullL L;
+  if (threadIdx.x < LH_DIRS) {
+    const int d = threadIdx.x;
+    const double z = 1.0 - (2.0 * d + 1.0) / LH_DIRS, r = sqrt(1.0 - z * z), ph = 2.399963229728653 * d;
+    L.dir[d][0] = r * cos(ph); L.dir[d][1] = r * sin(ph); L.dir[d][2] = z;
+  }
+  lhull_body(A, L);
+}
+
+}  // namespace lqro

@@ -37,7 +37,7 @@
 #include "lqro_dyn.hpp"
 #include "lqro_kern.hpp"
 
-#define LQRO_PROF_WORDS (32 + 2 * 4096 + 16 + 16)   // hull: 32 counters + 2 words per job; pair: 16; hull wave phases: 16
+#define LQRO_PROF_WORDS (32 + 2 * 4096 + 16 + 16 + 16 + 4 * 4096)   // hull: 32 counters + 2 words per job; pair: 16; hull wave phases: 16; local hull hand-overs: 16
 
 using namespace lqro;
 
@@ -369,6 +369,8 @@ struct lqro_ctx {
   int hot_cap;
   int hot_on;                // LQRO_HOT (default 1)
   int hull_big_only;         // LQRO_HULL_BIG: skip the LDS hull (A/B)
+  int local_hull;            // LQRO_LOCAL_HULL (default 0 until it beats the overlap): k_lhull first, k_hull for what it hands over
+  int* d_lq;                 // k_lhull -> k_hull queue
   double hot_t, hot_r;       // k_prio horizon (s) and radius (m): LQRO_HOT_T, LQRO_HOT_R
   // inside-hull pairs of an earlier step (pinned, copied at the end of each
   // step; ~0 = none yet) size the side stream: beyond 2 per side CU it widens
@@ -453,7 +455,7 @@ void lqro_destroy(lqro_ctx* c) {
   (void)hipSetDevice(c->cfg.device);
   void* ps[] = {c->d_R, c->d_TF, c->d_shash, c->d_T, c->d_NCF, c->d_S, c->d_x, c->d_vgoal, c->d_newv, c->d_A, c->d_B,
                 c->d_L, c->d_E, c->d_planes, c->d_lpscratch, c->d_lpcompact, c->d_recs, c->d_hq, c->d_hcount,
-                c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats, c->d_prof, c->d_rq, c->d_hbig, c->d_hwide, c->d_hbag, c->d_lp4, c->d_hotlist, c->d_hotmark, c->d_nbrlist, c->d_hfbest, c->d_hvpid, c->d_hstack};
+                c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats, c->d_prof, c->d_rq, c->d_hbig, c->d_hwide, c->d_hbag, c->d_lp4, c->d_hotlist, c->d_hotmark, c->d_nbrlist, c->d_hfbest, c->d_hvpid, c->d_hstack, c->d_lq};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (int k = 0; k < 5; ++k)
@@ -496,10 +498,12 @@ static int ctx_alloc(lqro_ctx* c) {
   // queue cannot overflow (C5's 2048 x 16383-slot shard: 134 MB, of 288 GB)
   c->hull_cap = (int)(slots > 0 ? slots : 1);
   HIPCHK(hipMalloc(&c->d_hq, sizeof(int) * c->hull_cap));
-  // hull count, next, retry count, retry next, pair rows, -, hot count, hot next, -, lp4 count, lp4 next
+  // hull count, next, retry count, retry next, pair rows, -, hot count, hot next, -, lp4 count, lp4 next,
+  // local-hull hand-over count, its next, local-hull decided
   HIPCHK(hipMalloc(&c->d_hcount, sizeof(int) * 16));
   c->d_hnext = c->d_hcount + 1;
   HIPCHK(hipMalloc(&c->d_rq, sizeof(int) * c->hull_cap));
+  HIPCHK(hipMalloc(&c->d_lq, sizeof(int) * c->hull_cap));
   HIPCHK(hipMalloc(&c->d_err, sizeof(int)));
   HIPCHK(hipMalloc(&c->d_stats, sizeof(unsigned long long) * 8));
   HIPCHK(hipHostMalloc((void**)&c->h_inside, sizeof(unsigned long long), hipHostMallocDefault));
@@ -555,6 +559,8 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
     if (c->side_cus > c->n_cu / 2) c->side_cus = c->n_cu / 2;
     const char* hb = getenv("LQRO_HULL_BIG");   // every hull job in k_hull_big (A/B runs)
     c->hull_big_only = hb ? atoi(hb) != 0 : 0;
+    const char* lh = getenv("LQRO_LOCAL_HULL");
+    c->local_hull = lh ? atoi(lh) != 0 : 0;
     const char* h = getenv("LQRO_HOT");
     c->hot_on = h ? atoi(h) != 0 : 1;
     const char* ht = getenv("LQRO_HOT_T");
@@ -752,7 +758,9 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   if (known && inside_prev > 2ull * (unsigned long long)side) side = std::min(c->n_cu / 2, (4 * side) / 3);
   const long max_inside = c->hot_max_inside >= 0 ? c->hot_max_inside : 4L * side;
   const bool crowded = known && inside_prev > (unsigned long long)max_inside;
-  const bool hot = c->hot_on && lds_ok && (size_t)g.horizon * g.n_points <= 16383 && side_waves >= 1 &&
+  // the local hull decides nearly every inside pair in ~1/10 of a full
+  // hull's time, so the hulls no longer need the side CUs: plain schedule
+  const bool hot = !c->local_hull && c->hot_on && lds_ok && (size_t)g.horizon * g.n_points <= 16383 && side_waves >= 1 &&
                    c->n_cu >= 64 && slots >= 65536 && c->nbr_k <= 0 && !crowded;
   const int nwait = hot ? side : 0;
   P.row_split = std::max(1, std::min(16, (2 * c->n_cu + c->nrows - 1) / c->nrows));
@@ -792,6 +800,9 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   Hh.prof = c->d_prof;
   Hh.block_base = 0;
   Hh.big_main = 0;
+  Hh.lqueue = c->d_lq; Hh.lcount = c->d_hcount + 11; Hh.ldone = c->d_hcount + 13;
+  Hh.lfail = c->d_prof + 32 + 2 * 4096 + 32;
+  Hh.ljobs = c->d_prof + 32 + 2 * 4096 + 48;
   if (g.x_dim != 16 && g.x_dim != 12) return LQRO_E_ARG;
   // the row launch is submitted before the side stream's work: should the two
   // streams land on one hardware queue (a second context in the process), the
@@ -815,6 +826,13 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
     HIPCHK(hipStreamWaitEvent(s, c->xev[1], 0));
   }
   HIPCHK(hipEventRecord(c->ev[1], s));
+  if (c->local_hull) {
+    // k_lhull takes the queue k_pair filled; k_hull / k_hull_big then take
+    // the pairs it handed over (scratch: hull_blocks blocks of 6 H*NP doubles)
+    launch_lhull(dim3(c->hull_blocks), s, Hh);
+    HIPCHK(hipGetLastError());
+    Hh.queue = c->d_lq; Hh.count = c->d_hcount + 11; Hh.next = c->d_hcount + 12;
+  }
   Hh.block_base = nwait;
   Hh.big_main = lds_ok ? 0 : 1;
   if (lds_ok) {
@@ -1088,6 +1106,35 @@ int lqro_get_stats(lqro_ctx* c, int64_t* st) {
   HIPCHK(hipMemcpy(h, c->d_stats, sizeof h, hipMemcpyDeviceToHost));
   for (int k = 0; k < 8; ++k) st[k] = (int64_t)h[k];
   if (c->nbr_k <= 0) st[0] = (int64_t)c->nrows * c->npr;   // else k_nbr counted the kept pairs
+  return LQRO_OK;
+}
+
+/* diagnostic (not in lqro.h): inside-hull pairs of the last step decided by
+ * the local hull (out[0]) and handed to the full hull (out[1]); out[2..17]:
+ * hand-over reasons since the context was created (k_lhull's fail code - 20;
+ * 0: the point set / initial tetrahedron) */
+int lqro_debug_local_hull(lqro_ctx* c, long long* out) {
+  if (!c || !out) return LQRO_E_ARG;
+  HIPCHK(hipSetDevice(c->cfg.device));
+  HIPCHK(wait_last_step(c));
+  int h[16];
+  HIPCHK(hipMemcpy(h, c->d_hcount, sizeof h, hipMemcpyDeviceToHost));
+  unsigned long long r[16];
+  HIPCHK(hipMemcpy(r, c->d_prof + 32 + 2 * 4096 + 32, sizeof r, hipMemcpyDeviceToHost));
+  out[0] = h[13];
+  out[1] = h[11];
+  for (int k = 0; k < 16; ++k) out[2 + k] = (long long)r[k];
+  return LQRO_OK;
+}
+
+/* diagnostic (not in lqro.h): k_lhull's per-job words of the last step
+ * (4 x 4096: point ticks, loop ticks at 100 MHz, iterations | nv << 16 |
+ * live points << 32, n | fail << 32 | faces << 40) */
+int lqro_debug_local_hull_jobs(lqro_ctx* c, unsigned long long* out) {
+  if (!c || !out) return LQRO_E_ARG;
+  HIPCHK(hipSetDevice(c->cfg.device));
+  HIPCHK(wait_last_step(c));
+  HIPCHK(hipMemcpy(out, c->d_prof + 32 + 2 * 4096 + 48, sizeof(unsigned long long) * 4 * 4096, hipMemcpyDeviceToHost));
   return LQRO_OK;
 }
 

@@ -26,7 +26,7 @@ LIB_PATH = os.path.join(_HERE, "liblqro.so")
 
 LQRO_OK = 0
 LQRO_FLAG_RECORDS = 0x1
-REC_PLANE, REC_INSIDE, REC_BACKUP, REC_HULL, REC_HULLFAIL = 0x01, 0x02, 0x04, 0x08, 0x10
+REC_PLANE, REC_INSIDE, REC_BACKUP, REC_HULL, REC_HULLFAIL, REC_LOCAL = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20
 
 
 class Config(C.Structure):

@@ -196,6 +196,7 @@ def test_overlap_schedule_identical(lqro_mod, gains, monkeypatch, kind):
                 {"LQRO_HOT": "1", "LQRO_HOT_R": "0.5"}):
         for k in ("LQRO_HOT", "LQRO_SIDE_HULL_CUS", "LQRO_HOT_R"):
             monkeypatch.delenv(k, raising=False)
+        monkeypatch.setenv("LQRO_LOCAL_HULL", "0")   # the overlap runs with the full hull only
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         ctx = lqro_mod.Context(lqro_mod.config(N, H, NP, x_dim=X, flags=lqro_mod.LQRO_FLAG_RECORDS))
@@ -227,6 +228,7 @@ def test_adaptive_schedule_identical(lqro_mod, gains, monkeypatch):
         for env in ({"LQRO_HOT": "0"}, {}, {"LQRO_HOT_MAX_INSIDE": "1000000"}):
             for k in ("LQRO_HOT", "LQRO_SIDE_HULL_CUS", "LQRO_HOT_R", "LQRO_HOT_MAX_INSIDE"):
                 monkeypatch.delenv(k, raising=False)
+            monkeypatch.setenv("LQRO_LOCAL_HULL", "0")
             for k, v in env.items():
                 monkeypatch.setenv(k, v)
             ctx = lqro_mod.Context(lqro_mod.config(N, H, NP, flags=lqro_mod.LQRO_FLAG_RECORDS))
@@ -288,3 +290,58 @@ def test_reference_driver_one_call(lqro_mod, gains, scenario):
     ctx.close()
     ok = d[f"{scenario}_ok"].astype(bool)
     assert np.array_equal(newv[ok].view(np.uint64), d[f"{scenario}_newv"][ok].view(np.uint64))
+
+
+@pytest.mark.parametrize("case", ["dense", "c3", "crowded", "x12_h200"])
+def test_local_hull_identical(lqro_mod, gains, monkeypatch, case):
+    """k_lhull (the inside-hull branch from a local hull around vrel,
+    lqro_lhull.hpp) against the full hull (LQRO_LOCAL_HULL=0): every record
+    (facet, distance, normal, half-plane) and every new velocity bit for bit,
+    on a dense swarm, the C3 bench swarm, a crowded C3-sized swarm (22 m box,
+    ~1,100 inside-hull pairs) and C5's shape (X = 12, H = 200, per-agent
+    gains); the local hull decides nearly every inside pair (the rest are
+    handed to k_hull)."""
+    import ctypes as C
+    N, H, NP, X, box, seed, per_agent = 1024, 100, 100, 16, None, None, False
+    if case == "dense":
+        N, H, box, seed = 32, 45, 3.0, 11
+    elif case == "crowded":
+        box, seed = 22.0, 7
+    elif case == "x12_h200":
+        N, H, X, box, seed, per_agent = 256, 200, 12, 12.0, 5, True
+    kw = {} if box is None else dict(box=box, seed=seed)
+    lqro_mod.lib().lqro_debug_local_hull.argtypes = [C.c_void_p, C.c_void_p]
+    x, vg = lqro_mod.synthetic_swarm(N, x_dim=X, **kw)
+    g = gains
+    if per_agent:
+        gb = lqro_mod.synthesize_gains_batch(lqro_mod.perturbed_models(N, seed=17), x_dim=X)
+        g = dict(A=gb["A"][0], B=gb["B"][0], L=gb["L"], E=gb["E"])
+    outs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("LQRO_LOCAL_HULL", flag)
+        ctx = lqro_mod.Context(lqro_mod.config(N, H, NP, x_dim=X, flags=lqro_mod.LQRO_FLAG_RECORDS))
+        ctx.set_gains(g["A"], g["B"], g["L"], g["E"], per_agent=per_agent)
+        v = ctx.step(x, vg)
+        r = ctx.records()
+        st = ctx.stats()
+        out = (C.c_longlong * 18)()
+        assert lqro_mod.lib().lqro_debug_local_hull(ctx._h, out) == 0
+        ctx.close()
+        outs.append((v, r, st, tuple(out)))
+    (v0, r0, st0, _), (v1, r1, st1, out) = outs
+    done, handed, reasons = out[0], out[1], out[2:]
+    inside = (r0["flags"] & 2) != 0
+    assert inside.sum() > 0 and st0["hull_fail"] == 0 and st1["hull_fail"] == 0
+    local = (r1["flags"] & lqro_mod.REC_LOCAL) != 0
+    assert local.sum() == done and done + handed == inside.sum()
+    print(f"{case}: {inside.sum()} inside pairs, local hull decided {done}, handed over {handed} "
+          f"(reasons {dict((k + 20, c) for k, c in enumerate(reasons) if c)})")
+    assert np.array_equal(r1["flags"] & ~lqro_mod.REC_LOCAL, r0["flags"])
+    for f in ("n_reach", "reach_hash", "facet", "dist", "normal", "plane_point", "plane_normal"):
+        a, b = r1[f][inside], r0[f][inside]
+        if a.dtype.kind == "f":
+            assert np.array_equal(a.view(np.uint8), b.view(np.uint8)), f
+        else:
+            assert np.array_equal(a, b), f
+    assert np.array_equal(v1.view(np.uint64), v0.view(np.uint64))
+    assert done >= 0.8 * inside.sum()
