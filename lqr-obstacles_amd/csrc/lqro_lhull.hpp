@@ -42,7 +42,8 @@ namespace lqro {
 #define LH_FMAX 512
 #define LH_EMAX 1536
 #define LH_ITERS 2048
-#define LH_LCAP 3072              // live points kept in LDS once compaction gets them this few
+#define LH_BATCH 8                // faces scanned together
+#define LH_LCAP 2560              // live points kept in LDS once compaction gets them this few
 
 struct LHullL {
   // hull_points / hull_tetra / hl_argmax / hl_scan / hull_take_job
@@ -63,9 +64,16 @@ struct LHullL {
   unsigned short freel[LH_FMAX];     // retired face slots (a stack)
   unsigned short ea[LH_EMAX], eb[LH_EMAX];   // edges of the visible region
   unsigned int vmark[LH_VMAX / 32];
-  int nf, nfree, nv, ne, nh, task, tface;
-  int nc, cb, ncompact, inlds;       // live points, their global buffer, next compaction at nv, in lp
+  int nf, nfree, nv, ne, nh, task, tface, nb;
+  int bf[LH_BATCH];                  // this iteration's faces
+  double bkey[LH_BATCH];             // their furthest point: n.(p - a), id
+  int bidx[LH_BATCH];
+  unsigned short bt[LH_BATCH][3];    // their vertices (a slot may be reused by an insertion)
+  double sk[LH_BATCH * (LH_THREADS / 64)];
+  int si[LH_BATCH * (LH_THREADS / 64)];
+  int nc, cb, ncompact, inlds, npk;       // live points, their global buffer, next compaction at nv, in lp
   double4 lp[LH_LCAP];               // the live points when nc <= LH_LCAP
+  double4 pk[LH_FMAX];               // compaction: alive faces {n, n.a - band |n| / 2}
   double dir[LH_DIRS][3];
   int sup[LH_DIRS];
   double best, delta;
@@ -105,34 +113,50 @@ __device__ __forceinline__ int lh_wmin(int v) {
   return v;
 }
 
-// wave 0: the next face to scan.  task 1: vrel on or beyond it (within
-// margin); 2: uncertified, in the window, nearest first; 3: uncertified,
-// sharing a vertex with a window face; 0: done.
+// wave 0: this iteration's faces (L.bf, L.nb).  task 1: vrel on or beyond
+// them (within margin); 2: the LH_BATCH nearest uncertified window faces;
+// 3: uncertified faces sharing a vertex with a window face; 0: done.
 __device__ __forceinline__ void lh_choose(LHullL& L, int lane, double margin) {
   const int nf = L.nf;
-  int t = INT_MAX;
-  for (int f = lane; f < nf; f += 64)
-    if (L.alive[f] && L.sd[f] >= -margin) t = min(t, f);
-  t = lh_wmin(t);
-  if (t != INT_MAX) {
-    if (lane == 0) { L.task = 1; L.tface = t; }
+  int nb = 0;
+  for (int f0 = 0; f0 < nf && nb < LH_BATCH; f0 += 64) {
+    const int f = f0 + lane;
+    unsigned long long m = __ballot(f < nf && L.alive[f] && L.sd[f] >= -margin);
+    while (m && nb < LH_BATCH) {
+      if (lane == 0) L.bf[nb] = f0 + __builtin_ctzll(m);
+      m &= m - 1;
+      nb++;
+    }
+  }
+  if (nb) {
+    if (lane == 0) { L.task = 1; L.nb = nb; }
     return;
   }
   const double W = L.best + L.delta;
-  double kb = INFINITY;
-  int fb = INT_MAX;
-  for (int f = lane; f < nf; f += 64)
-    if (L.alive[f] && !L.cert[f] && -L.sd[f] <= W && (-L.sd[f] < kb || (-L.sd[f] == kb && f < fb))) {
-      kb = -L.sd[f]; fb = f;
+  unsigned taken = 0u;                     // bit k: face lane + 64 k chosen
+  for (int r = 0; r < LH_BATCH; ++r) {
+    double kb = INFINITY;
+    int fb = INT_MAX;
+    for (int k = 0; lane + 64 * k < nf; ++k) {
+      const int f = lane + 64 * k;
+      const double v = -L.sd[f];
+      if (!((taken >> k) & 1u) && L.alive[f] && !L.cert[f] && v <= W && (v < kb || (v == kb && f < fb))) {
+        kb = v; fb = f;
+      }
     }
 #pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    const double ok = __shfl_xor(kb, off);
-    const int of = __shfl_xor(fb, off);
-    if (ok < kb || (ok == kb && of < fb)) { kb = ok; fb = of; }
+    for (int off = 32; off >= 1; off >>= 1) {
+      const double ok = __shfl_xor(kb, off);
+      const int of = __shfl_xor(fb, off);
+      if (ok < kb || (ok == kb && of < fb)) { kb = ok; fb = of; }
+    }
+    if (fb == INT_MAX) break;
+    if ((fb & 63) == lane) taken |= 1u << (fb >> 6);
+    if (lane == 0) L.bf[nb] = fb;
+    nb++;
   }
-  if (fb != INT_MAX) {
-    if (lane == 0) { L.task = 2; L.tface = fb; }
+  if (nb) {
+    if (lane == 0) { L.task = 2; L.nb = nb; }
     return;
   }
   for (int w = lane; w < LH_VMAX / 32; w += 64) L.vmark[w] = 0u;
@@ -141,22 +165,28 @@ __device__ __forceinline__ void lh_choose(LHullL& L, int lane, double margin) {
     if (L.alive[f] && -L.sd[f] <= W)
       for (int k = 0; k < 3; ++k) atomicOr(&L.vmark[L.fv[f][k] >> 5], 1u << (L.fv[f][k] & 31));
   hl_sync();
-  t = INT_MAX;
-  for (int f = lane; f < nf; f += 64) {
-    if (!L.alive[f] || L.cert[f]) continue;
+  for (int f0 = 0; f0 < nf && nb < LH_BATCH; f0 += 64) {
+    const int f = f0 + lane;
     bool touch = false;
-    for (int k = 0; k < 3; ++k) touch |= ((L.vmark[L.fv[f][k] >> 5] >> (L.fv[f][k] & 31)) & 1u) != 0;
-    if (touch) t = min(t, f);
+    if (f < nf && L.alive[f] && !L.cert[f])
+      for (int k = 0; k < 3; ++k) touch |= ((L.vmark[L.fv[f][k] >> 5] >> (L.fv[f][k] & 31)) & 1u) != 0;
+    unsigned long long m = __ballot(touch);
+    while (m && nb < LH_BATCH) {
+      if (lane == 0) L.bf[nb] = f0 + __builtin_ctzll(m);
+      m &= m - 1;
+      nb++;
+    }
   }
-  t = lh_wmin(t);
-  if (lane == 0) { L.task = t != INT_MAX ? 3 : 0; L.tface = t; }
+  if (lane == 0) { L.task = nb ? 3 : 0; L.nb = nb; }
 }
 
-// insert point q (beyond at least one face) into Q: the visible faces go,
-// a cone joins the horizon to the new vertex.  Workgroup-wide.
+// insert point q into Q: the faces it is beyond go, a cone joins the
+// horizon to the new vertex (nothing visible: q is inside Q, no change).
+// Workgroup-wide; slots are assigned by workgroup scans in face / edge order,
+// so Q's evolution (and which pairs are handed over) is deterministic.
 __device__ __forceinline__ void lh_insert(LHullL& L, const double* Pr, int q, double eps2, double band2,
                                           const double* vrel) {
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, bd = blockDim.x;
   const double p0 = Pr[3 * q], p1 = Pr[3 * q + 1], p2 = Pr[3 * q + 2];
   if (tid == 0) {
     if (L.nv >= LH_VMAX) L.fail = 24;
@@ -164,46 +194,72 @@ __device__ __forceinline__ void lh_insert(LHullL& L, const double* Pr, int q, do
       L.vx[L.nv][0] = p0; L.vx[L.nv][1] = p1; L.vx[L.nv][2] = p2;
       L.vpid[L.nv] = q;
     }
-    L.ne = 0;
-    L.nh = 0;
   }
   hl_bar();
   if (L.fail) return;
-  const int v = L.nv, nf = L.nf;
-  for (int f = tid; f < nf; f += blockDim.x) {
-    if (!L.alive[f]) continue;
-    const double* a = L.vx[L.fv[f][0]];
-    const double d = L.fn[f][0] * (p0 - a[0]) + L.fn[f][1] * (p1 - a[1]) + L.fn[f][2] * (p2 - a[2]);
-    const double nn = L.fn[f][3];
-    if (d > 0.0 && d * d > eps2 * nn) {
-      if (L.cert[f]) { L.fail = 25; continue; }      // cannot happen: nothing is beyond a certified face
-      const int e = atomicAdd(&L.ne, 3);
-      if (e + 3 > LH_EMAX) { L.fail = 26; continue; }
-      for (int k = 0; k < 3; ++k) { L.ea[e + k] = L.fv[f][k]; L.eb[e + k] = L.fv[f][(k + 1) % 3]; }
-      L.alive[f] = 0;
-      L.freel[atomicAdd(&L.nfree, 1)] = (unsigned short)f;
-    } else if (d > 0.0 || d * d <= band2 * nn) {
-      L.fail = 27;                                     // near-coplanar with the new vertex
+  const int v = L.nv, nf = L.nf, nfree0 = L.nfree;
+  int nvis = 0;
+  for (int f0 = 0; f0 < nf; f0 += bd) {
+    const int f = f0 + tid;
+    bool vis = false;
+    if (f < nf && L.alive[f]) {
+      const double* a = L.vx[L.fv[f][0]];
+      const double d = L.fn[f][0] * (p0 - a[0]) + L.fn[f][1] * (p1 - a[1]) + L.fn[f][2] * (p2 - a[2]);
+      const double nn = L.fn[f][3];
+      if (d > 0.0 && d * d > eps2 * nn) {
+        vis = true;
+        if (L.cert[f]) L.fail = 25;                  // cannot happen: nothing is beyond a certified face
+      } else if (d > 0.0 || d * d <= band2 * nn) {
+        L.fail = 27;                                 // near-coplanar with the new vertex
+      }
     }
+    int tot;
+    const int pos = nvis + hl_scan(L, vis ? 1 : 0, &tot);
+    if (vis) {
+      if (3 * pos + 3 > LH_EMAX) L.fail = 26;
+      else {
+        for (int k = 0; k < 3; ++k) { L.ea[3 * pos + k] = L.fv[f][k]; L.eb[3 * pos + k] = L.fv[f][(k + 1) % 3]; }
+        L.freel[nfree0 + pos] = (unsigned short)f;
+      }
+    }
+    nvis += tot;
   }
   hl_bar();
-  if (L.fail || L.ne == 0) return;   // nothing visible: q is inside Q
-  const int ne = L.ne, nfree = L.nfree;
-  for (int e = tid; e < ne; e += blockDim.x) {
-    const int a = L.ea[e], b = L.eb[e];
-    bool hz = true;
-    for (int e2 = 0; e2 < ne; ++e2)
-      if (L.ea[e2] == b && L.eb[e2] == a) { hz = false; break; }
-    if (!hz) continue;
-    const int k = atomicAdd(&L.nh, 1);
-    const int f = k < nfree ? L.freel[nfree - 1 - k] : nf + (k - nfree);
-    if (f >= LH_FMAX) { L.fail = 28; continue; }
-    L.fv[f][0] = (unsigned short)a; L.fv[f][1] = (unsigned short)b; L.fv[f][2] = (unsigned short)v;
-    lh_face(L, f, vrel);
+  if (L.fail || nvis == 0) return;   // nothing visible: q is inside Q
+  for (int f0 = 0; f0 < nf; f0 += bd) {
+    const int f = f0 + tid;
+    if (f < nf && L.alive[f]) {
+      const double* a = L.vx[L.fv[f][0]];
+      const double d = L.fn[f][0] * (p0 - a[0]) + L.fn[f][1] * (p1 - a[1]) + L.fn[f][2] * (p2 - a[2]);
+      if (d > 0.0 && d * d > eps2 * L.fn[f][3]) L.alive[f] = 0;
+    }
+  }
+  const int ne = 3 * nvis, nfree = nfree0 + nvis;
+  int nh = 0;
+  for (int e0 = 0; e0 < ne; e0 += bd) {
+    const int e = e0 + tid;
+    bool hz = false;
+    int a = 0, b = 0;
+    if (e < ne) {
+      a = L.ea[e]; b = L.eb[e];
+      hz = true;
+      for (int e2 = 0; e2 < ne; ++e2)
+        if (L.ea[e2] == b && L.eb[e2] == a) { hz = false; break; }
+    }
+    int tot;
+    const int k = nh + hl_scan(L, hz ? 1 : 0, &tot);
+    if (hz) {
+      const int f = k < nfree ? L.freel[nfree - 1 - k] : nf + (k - nfree);
+      if (f >= LH_FMAX) L.fail = 28;
+      else {
+        L.fv[f][0] = (unsigned short)a; L.fv[f][1] = (unsigned short)b; L.fv[f][2] = (unsigned short)v;
+        lh_face(L, f, vrel);
+      }
+    }
+    nh += tot;
   }
   hl_bar();
   if (tid == 0 && !L.fail) {
-    const int nh = L.nh;
     if (nh < 3) L.fail = 29;
     if (nh <= nfree) L.nfree = nfree - nh;
     else { L.nf = nf + (nh - nfree); L.nfree = 0; }
@@ -256,14 +312,25 @@ __device__ __forceinline__ void lh_support(LHullL& L, const double* Pr, int n) {
   hl_bar();
 }
 
-// Drop the live points that are inside Q by more than band from every face
-// plane: Q only grows, so such a point is never beyond a later face nor
-// within band of one.  Workgroup-wide; the survivors go to the other buffer.
-__device__ __forceinline__ void lh_compact(LHullL& L, double4* C0, double4* C1, double band2) {
+// Drop the live points that are inside Q by more than band / 2 from every
+// face plane: Q only grows, so such a point is never beyond a later face nor
+// within a few eps of one (the test n.p < n.a - band |n| / 2 differs from
+// n.(p - a) by rounding far below band).  Workgroup-wide; the survivors go to
+// the other buffer, and into LDS when they fit.
+__device__ __forceinline__ void lh_compact(LHullL& L, double4* C0, double4* C1, double band) {
   const int tid = threadIdx.x;
+  if (tid == 0) L.npk = 0;
+  hl_bar();
+  for (int f = tid; f < L.nf; f += blockDim.x) {
+    if (!L.alive[f]) continue;
+    const double* a = L.vx[L.fv[f][0]];
+    const double n0 = L.fn[f][0], n1 = L.fn[f][1], n2 = L.fn[f][2];
+    L.pk[atomicAdd(&L.npk, 1)] = make_double4(n0, n1, n2, n0 * a[0] + n1 * a[1] + n2 * a[2] - 0.5 * band * sqrt(L.fn[f][3]));
+  }
+  hl_bar();
   const double4* src = L.inlds ? L.lp : (L.cb ? C1 : C0);
   double4* dst = L.cb ? C0 : C1;
-  const int nc = L.nc, nf = L.nf;
+  const int nc = L.nc, npk = L.npk;
   int base = 0;
   for (int k0 = 0; k0 < nc; k0 += blockDim.x) {
     const int k = k0 + tid;
@@ -271,11 +338,12 @@ __device__ __forceinline__ void lh_compact(LHullL& L, double4* C0, double4* C1, 
     double4 c;
     if (k < nc) {
       c = src[k];
-      for (int f = 0; f < nf && !keep; ++f) {
-        if (!L.alive[f]) continue;
-        const double* a = L.vx[L.fv[f][0]];
-        const double d = L.fn[f][0] * (c.x - a[0]) + L.fn[f][1] * (c.y - a[1]) + L.fn[f][2] * (c.z - a[2]);
-        keep = d >= 0.0 || d * d <= band2 * L.fn[f][3];
+      for (int g = 0; g < npk && !keep; g += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const double4 P = L.pk[min(g + u, npk - 1)];
+          keep |= P.x * c.x + P.y * c.y + P.z * c.z >= P.w;
+        }
       }
     }
     int tot;
@@ -293,27 +361,71 @@ __device__ __forceinline__ void lh_compact(LHullL& L, double4* C0, double4* C1, 
   hl_bar();
 }
 
-// arg-max of n.(c - a) over the live points (ids x0, x1, x2 excluded), lowest
-// id on ties; per thread (the caller reduces over the workgroup)
+// for each of the nb batch faces, the arg-max of n.(c - a) over the live
+// points (the face's own vertices excluded), lowest id on ties -> L.bkey /
+// L.bidx.  Workgroup-wide.
 template <int U, class P>
-__device__ __forceinline__ void lh_scan_pts(const P* C, int nc, double n0, double n1, double n2, double a0, double a1,
-                                            double a2, int x0, int x1, int x2, double& key, int& idx) {
-  const int tid = threadIdx.x, bd = blockDim.x;
+__device__ __forceinline__ void lh_scan_batch(LHullL& L, const P* C, int nc, int nb) {
+  const int tid = threadIdx.x, bd = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = bd >> 6;
+  double n0[LH_BATCH], n1[LH_BATCH], n2[LH_BATCH], a0[LH_BATCH], a1[LH_BATCH], a2[LH_BATCH], key[LH_BATCH];
+  int x0[LH_BATCH], x1[LH_BATCH], x2[LH_BATCH], idx[LH_BATCH];
+#pragma unroll
+  for (int b = 0; b < LH_BATCH; ++b) {
+    const int f = L.bf[b < nb ? b : 0];
+    n0[b] = L.fn[f][0]; n1[b] = L.fn[f][1]; n2[b] = L.fn[f][2];
+    const double* av = L.vx[L.fv[f][0]];
+    a0[b] = av[0]; a1[b] = av[1]; a2[b] = av[2];
+    x0[b] = L.vpid[L.fv[f][0]]; x1[b] = L.vpid[L.fv[f][1]]; x2[b] = L.vpid[L.fv[f][2]];
+    key[b] = -INFINITY; idx[b] = INT_MAX;
+  }
   for (int k0 = tid; k0 < nc; k0 += U * bd) {
     double4 c[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int k = k0 + u * bd;
-      if (k < nc) c[u] = C[k];
-      else c[u] = make_double4(0.0, 0.0, 0.0, -1.0);
+      c[u] = k < nc ? C[k] : make_double4(0.0, 0.0, 0.0, -1.0);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int q = (int)c[u].w;
-      const double d = n0 * (c[u].x - a0) + n1 * (c[u].y - a1) + n2 * (c[u].z - a2);
-      if (q >= 0 && q != x0 && q != x1 && q != x2 && (d > key || (d == key && q < idx))) { key = d; idx = q; }
+      if (q < 0) continue;
+#pragma unroll
+      for (int b = 0; b < LH_BATCH; ++b) {
+        if (b >= nb) break;
+        const double d = n0[b] * (c[u].x - a0[b]) + n1[b] * (c[u].y - a1[b]) + n2[b] * (c[u].z - a2[b]);
+        if (q != x0[b] && q != x1[b] && q != x2[b] && (d > key[b] || (d == key[b] && q < idx[b]))) {
+          key[b] = d; idx[b] = q;
+        }
+      }
     }
   }
+#pragma unroll
+  for (int b = 0; b < LH_BATCH; ++b) {
+    if (b >= nb) break;
+    double k = key[b];
+    int i = idx[b];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const double ok = __shfl_xor(k, off);
+      const int oi = __shfl_xor(i, off);
+      if (ok > k || (ok == k && oi < i)) { k = ok; i = oi; }
+    }
+    if (lane == 0) { L.sk[b * nw + wave] = k; L.si[b * nw + wave] = i; }
+  }
+  hl_bar();
+  if (tid < nb) {
+    double k = L.sk[tid * nw];
+    int i = L.si[tid * nw];
+    for (int w = 1; w < nw; ++w) {
+      const double ok = L.sk[tid * nw + w];
+      const int oi = L.si[tid * nw + w];
+      if (ok > k || (ok == k && oi < i)) { k = ok; i = oi; }
+    }
+    L.bkey[tid] = k;
+    L.bidx[tid] = i;
+    for (int e = 0; e < 3; ++e) L.bt[tid][e] = L.fv[L.bf[tid]][e];
+  }
+  hl_bar();
 }
 
 __device__ __forceinline__ void lhull_body(const HullArgs& A, LHullL& L) {
@@ -338,7 +450,8 @@ __device__ __forceinline__ void lhull_body(const HullArgs& A, LHullL& L) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     const int n = hull_points(A, L, Ti, Ni, xi, xj, vrel, Pr, Pf);
     const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-    int iters = 0, nscan = 0;
+    int iters = 0, ncomp = 0;
+    unsigned long long tcomp = 0, tset = 0;
     const double eps = L.eps, eps2 = eps * eps;
     const double band = 64.0 * eps, band2 = band * band;
     {
@@ -375,55 +488,63 @@ __device__ __forceinline__ void lhull_body(const HullArgs& A, LHullL& L) {
       }
       if (tid == 0) L.ncompact = L.nv;
       hl_bar();
+      tset = __builtin_amdgcn_s_memrealtime() - t1;
       for (int it = 0;; ++it) {
-        if (L.nv >= L.ncompact) lh_compact(L, C0, C1, band2);
+        if (L.nv >= L.ncompact) {
+          const unsigned long long tc = __builtin_amdgcn_s_memrealtime();
+          lh_compact(L, C0, C1, band);
+          tcomp += __builtin_amdgcn_s_memrealtime() - tc;
+          ncomp++;
+        }
         if (wave == 0) lh_choose(L, lane, band);
         hl_bar();
-        const int task = L.task, f = L.tface;
+        const int task = L.task, nb = L.nb;
         iters = it;
         if (task == 0) break;
         if (it >= LH_ITERS) {
           if (tid == 0) L.fail = 21;
           break;
         }
-        // the furthest point beyond face f (its own vertices excluded)
-        const double n0 = L.fn[f][0], n1 = L.fn[f][1], n2 = L.fn[f][2], nn = L.fn[f][3];
-        const double* av = L.vx[L.fv[f][0]];
-        const double a0 = av[0], a1 = av[1], a2 = av[2];
-        const int x0 = L.vpid[L.fv[f][0]], x1 = L.vpid[L.fv[f][1]], x2 = L.vpid[L.fv[f][2]];
-        double key = -INFINITY;
-        int idx = INT_MAX;
-        if (L.inlds) lh_scan_pts<2>(L.lp, L.nc, n0, n1, n2, a0, a1, a2, x0, x1, x2, key, idx);
-        else lh_scan_pts<8>(L.cb ? C1 : C0, L.nc, n0, n1, n2, a0, a1, a2, x0, x1, x2, key, idx);
-        hl_argmax(L, key, idx);
-        if (key > 0.0 && key * key > eps2 * nn) {
-          lh_insert(L, Pr, idx, eps2, band2, vrel);
-          if (L.fail) break;
-        } else if (key > 0.0 || key * key <= band2 * nn) {
-          if (tid == 0) L.fail = 22;                     // a point near the facet's plane
-          break;
-        } else if (task == 1) {
-          if (tid == 0) L.fail = 23;                     // vrel on or beyond a full-hull facet
-          break;
-        } else {
-          if (tid == 0) {
-            L.cert[f] = 1;
-            L.best = fmin(L.best, lh_rule(L, f, Pr, Pf, vrel));
+        // the batch faces' furthest points, one pass over the live points
+        if (L.inlds) lh_scan_batch<1>(L, L.lp, L.nc, nb);
+        else lh_scan_batch<2>(L, L.cb ? C1 : C0, L.nc, nb);
+        // in batch order: a face with a point beyond it takes that point (an
+        // earlier insertion may have removed it), one without is certified
+        for (int b = 0; b < nb && !L.fail; ++b) {
+          const int f = L.bf[b];
+          // gone, or its slot now holds a face of an earlier insertion
+          if (!L.alive[f] || L.fv[f][0] != L.bt[b][0] || L.fv[f][1] != L.bt[b][1] || L.fv[f][2] != L.bt[b][2])
+            continue;
+          const double key = L.bkey[b], nn = L.fn[f][3];
+          if (key > 0.0 && key * key > eps2 * nn) {
+            lh_insert(L, Pr, L.bidx[b], eps2, band2, vrel);
+          } else if (key > 0.0 || key * key <= band2 * nn) {
+            if (tid == 0) L.fail = 22;                   // a point near the facet's plane
+            hl_bar();
+          } else if (task == 1) {
+            if (tid == 0) L.fail = 23;                   // vrel on or beyond a full-hull facet
+            hl_bar();
+          } else {
+            if (tid == 0) {
+              L.cert[f] = 1;
+              L.best = fmin(L.best, lh_rule(L, f, Pr, Pf, vrel));
+            }
+            hl_bar();
           }
-          hl_bar();
         }
+        if (L.fail) break;
       }
     }
     hl_bar();
     const unsigned long long t2 = __builtin_amdgcn_s_memrealtime();
     if (tid == 0 && A.ljobs && L.job < 4096) {
       unsigned long long* J = A.ljobs + 4 * (size_t)L.job;
-      J[0] = t1 - t0;
-      J[1] = t2 - t1;
+      J[0] = (t1 - t0) | (tset << 32);
+      J[1] = (t2 - t1) | (tcomp << 32);
       J[2] = (unsigned long long)iters | ((unsigned long long)L.nv << 16) | ((unsigned long long)L.nc << 32);
-      J[3] = (unsigned long long)n | ((unsigned long long)L.fail << 32) | ((unsigned long long)L.nf << 40);
+      J[3] = (unsigned long long)n | ((unsigned long long)L.fail << 32) | ((unsigned long long)L.nf << 40) |
+             ((unsigned long long)min(ncomp, 255) << 56);
     }
-    (void)nscan;
     if (!L.fail) {
       hull_select(A, L, L, Pr, Pf, L.vpid, L.nf, [&](int g) { return L.alive[g] && L.cert[g]; }, xi, vrel, slot,
                   true);

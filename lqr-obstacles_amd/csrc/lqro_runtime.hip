@@ -369,8 +369,9 @@ struct lqro_ctx {
   int hot_cap;
   int hot_on;                // LQRO_HOT (default 1)
   int hull_big_only;         // LQRO_HULL_BIG: skip the LDS hull (A/B)
-  int local_hull;            // LQRO_LOCAL_HULL (default 0 until it beats the overlap): k_lhull first, k_hull for what it hands over
+  int local_hull;            // LQRO_LOCAL_HULL (default 1): k_lhull first, k_hull for what it hands over
   int* d_lq;                 // k_lhull -> k_hull queue
+  int lside_cus;             // side CUs with the local hull (LQRO_LOCAL_SIDE_CUS, default 3/16 of the CUs)
   double hot_t, hot_r;       // k_prio horizon (s) and radius (m): LQRO_HOT_T, LQRO_HOT_R
   // inside-hull pairs of an earlier step (pinned, copied at the end of each
   // step; ~0 = none yet) size the side stream: beyond 2 per side CU it widens
@@ -560,7 +561,11 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
     const char* hb = getenv("LQRO_HULL_BIG");   // every hull job in k_hull_big (A/B runs)
     c->hull_big_only = hb ? atoi(hb) != 0 : 0;
     const char* lh = getenv("LQRO_LOCAL_HULL");
-    c->local_hull = lh ? atoi(lh) != 0 : 0;
+    c->local_hull = lh ? atoi(lh) != 0 : 1;
+    const char* ls = getenv("LQRO_LOCAL_SIDE_CUS");
+    c->lside_cus = ls ? atoi(ls) : (3 * c->n_cu) / 16;
+    if (c->lside_cus < 0) c->lside_cus = 0;
+    if (c->lside_cus > c->n_cu / 2) c->lside_cus = c->n_cu / 2;
     const char* h = getenv("LQRO_HOT");
     c->hot_on = h ? atoi(h) != 0 : 1;
     const char* ht = getenv("LQRO_HOT_T");
@@ -754,14 +759,21 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   // schedule gives bit-identical results) take the plain schedule
   const unsigned long long inside_prev = *(volatile unsigned long long*)c->h_inside;
   const bool known = inside_prev != ~0ull;
-  int side = c->side_cus;
-  if (known && inside_prev > 2ull * (unsigned long long)side) side = std::min(c->n_cu / 2, (4 * side) / 3);
+  int side = c->local_hull ? c->lside_cus : c->side_cus;
+  if (c->local_hull) {
+    // local hulls: ~3.7 inside-hull pairs per side CU (C3: 177 on 48 CUs),
+    // widening up to half the CUs as the swarm gets denser
+    if (known && inside_prev * (unsigned long long)c->lside_cus > 177ull * (unsigned long long)side)
+      side = (int)std::min<unsigned long long>(c->n_cu / 2, inside_prev * (unsigned long long)c->lside_cus / 177ull);
+  } else if (known && inside_prev > 2ull * (unsigned long long)side) {
+    side = std::min(c->n_cu / 2, (4 * side) / 3);
+  }
   const long max_inside = c->hot_max_inside >= 0 ? c->hot_max_inside : 4L * side;
   const bool crowded = known && inside_prev > (unsigned long long)max_inside;
-  // the local hull decides nearly every inside pair in ~1/10 of a full
-  // hull's time, so the hulls no longer need the side CUs: plain schedule
-  const bool hot = !c->local_hull && c->hot_on && lds_ok && (size_t)g.horizon * g.n_points <= 16383 && side_waves >= 1 &&
-                   c->n_cu >= 64 && slots >= 65536 && c->nbr_k <= 0 && !crowded;
+  // with the local hull the side stream is k_pair(hot) -> k_lhull -> k_pair
+  // (rows, the same row queue): no LDS-topology condition
+  const bool hot = c->hot_on && c->n_cu >= 64 && slots >= 65536 && c->nbr_k <= 0 && !crowded && side >= 1 &&
+                   (c->local_hull || (lds_ok && (size_t)g.horizon * g.n_points <= 16383 && side_waves >= 1));
   const int nwait = hot ? side : 0;
   P.row_split = std::max(1, std::min(16, (2 * c->n_cu + c->nrows - 1) / c->nrows));
   const int units = c->nrows * P.row_split;
@@ -817,11 +829,22 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
     Ph.hot_only = 1;
     launch_pair(g.x_dim, dim3(nwait), dim3(P.waves * 64), c->lds_bytes, c->side, Ph);
     HIPCHK(hipGetLastError());
-    PairArgs Pt = P;
-    Pt.max_waves = side_waves;
-    if (nside == 0) Pt.nrows = 0;
-    launch_side(g.x_dim, dim3(nwait), dim3(HULL_CTHREADS), c->side, Hh, Pt);
-    HIPCHK(hipGetLastError());
+    if (c->local_hull) {
+      // the hot pairs' local hulls (k_lhull leaves when the queue is empty:
+      // later jobs go to the k_lhull after the sweep), then the row sweep
+      launch_lhull(dim3(nwait), c->side, Hh);
+      HIPCHK(hipGetLastError());
+      if (nside > 0) {
+        launch_pair(g.x_dim, dim3(nwait), dim3(P.waves * 64), c->lds_bytes, c->side, P);
+        HIPCHK(hipGetLastError());
+      }
+    } else {
+      PairArgs Pt = P;
+      Pt.max_waves = side_waves;
+      if (nside == 0) Pt.nrows = 0;
+      launch_side(g.x_dim, dim3(nwait), dim3(HULL_CTHREADS), c->side, Hh, Pt);
+      HIPCHK(hipGetLastError());
+    }
     HIPCHK(hipEventRecord(c->xev[1], c->side));
     HIPCHK(hipStreamWaitEvent(s, c->xev[1], 0));
   }

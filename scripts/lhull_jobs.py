@@ -10,6 +10,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "lqr-obstacles_amd")]
+os.environ.setdefault("LQRO_LOCAL_HULL", "1")
 import lqro  # noqa: E402
 
 box = float(sys.argv[1]) if len(sys.argv) > 1 else None
@@ -27,16 +28,21 @@ assert lqro.lib().lqro_debug_local_hull_jobs(ctx._h, buf) == 0
 st = ctx.stats()
 ctx.close()
 J = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 4)[: min(st["inside"], 4096)]
-pts_us = J[:, 0] / 100.0
-loop_us = J[:, 1] / 100.0
+pts_us = (J[:, 0] & 0xFFFFFFFF) / 100.0
+set_us = (J[:, 0] >> 32) / 100.0
+loop_us = (J[:, 1] & 0xFFFFFFFF) / 100.0
+comp_us = (J[:, 1] >> 32) / 100.0
+ncomp = J[:, 3] >> 56
 it = J[:, 2] & 0xFFFF
 nv = (J[:, 2] >> 16) & 0xFFFF
 nc = J[:, 2] >> 32
 n = J[:, 3] & 0xFFFFFFFF
 fail = (J[:, 3] >> 32) & 0xFF
-nf = J[:, 3] >> 40
+nf = (J[:, 3] >> 40) & 0xFFFF
 print(f"inside pairs {st['inside']}, timings {t}")
-for name, v in (("points us", pts_us), ("loop us", loop_us), ("iterations", it), ("vertices", nv),
+for name, v in (("points us", pts_us), ("hull us", loop_us), ("  setup us", set_us), ("  compact us", comp_us),
+                ("  compactions", ncomp), ("iterations", it), ("vertices", nv),
                 ("faces (slots)", nf), ("live points", nc), ("points", n)):
     print(f"  {name:14s} mean {v.mean():9.1f}  median {np.median(v):9.1f}  max {v.max():9.1f}")
-print(f"  loop us / iteration: mean {np.mean(loop_us / np.maximum(it, 1)):.2f}; handed over {int((fail != 0).sum())}")
+it_us = (loop_us - set_us - comp_us) / np.maximum(it, 1)
+print(f"  us / iteration (excl. setup, compaction): mean {it_us.mean():.2f}; handed over {int((fail != 0).sum())}")

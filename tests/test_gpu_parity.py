@@ -300,7 +300,8 @@ def test_local_hull_identical(lqro_mod, gains, monkeypatch, case):
     on a dense swarm, the C3 bench swarm, a crowded C3-sized swarm (22 m box,
     ~1,100 inside-hull pairs) and C5's shape (X = 12, H = 200, per-agent
     gains); the local hull decides nearly every inside pair (the rest are
-    handed to k_hull)."""
+    handed to k_hull), in the overlapped schedule (k_pair hot -> k_lhull ->
+    k_pair rows on the side stream) and, for crowded swarms, the plain one."""
     import ctypes as C
     N, H, NP, X, box, seed, per_agent = 1024, 100, 100, 16, None, None, False
     if case == "dense":
@@ -323,6 +324,13 @@ def test_local_hull_identical(lqro_mod, gains, monkeypatch, case):
         ctx.set_gains(g["A"], g["B"], g["L"], g["E"], per_agent=per_agent)
         v = ctx.step(x, vg)
         r = ctx.records()
+        if flag == "1":
+            # a second step is scheduled by the first's inside-hull count
+            # (side width, or the plain schedule for crowded swarms)
+            assert np.array_equal(ctx.step(x, vg), v)
+            r2 = ctx.records()
+            for f in ("flags", "facet", "dist", "plane_point", "plane_normal"):
+                assert np.array_equal(r2[f], r[f]), f
         st = ctx.stats()
         out = (C.c_longlong * 18)()
         assert lqro_mod.lib().lqro_debug_local_hull(ctx._h, out) == 0
