@@ -428,6 +428,80 @@ __device__ __forceinline__ void lh_scan_batch(LHullL& L, const P* C, int nc, int
   hl_bar();
 }
 
+// hull_points for k_lhull: the same points, in the same order and
+// arithmetic, with the row's T_k, the sphere and the pair's translations
+// staged in LDS (the lp region, free until the first compaction), one
+// workgroup scan per round, and eps, delta and the live-point list produced
+// in the same pass.  Sets L.n, L.fail, L.eps, L.delta.
+static_assert(LH_LCAP * 4 >= 12 * 256 + 3 * 256, "lp stages T_k, translations (H <= 256) and the sphere (NP <= 256)");
+__device__ __forceinline__ int lh_points(const HullArgs& A, LHullL& L, const double* Ti, const double* Ni,
+                                         const double* xi, const double* xj, const double* vrel, double* Pr,
+                                         double* Pf, double4* C0) {
+  const int tid = threadIdx.x, bd = blockDim.x;
+  const int H = A.H, NP = A.NP;
+  double* sT = reinterpret_cast<double*>(L.lp);
+  double* str = sT + H * 9;
+  double* sS = str + H * 3;
+  for (int q = tid; q < H * 9; q += bd) sT[q] = Ti[q];
+  for (int q = tid; q < NP * 3; q += bd) sS[q] = A.S[q];
+  for (int it = tid; it < 3 * H; it += bd) {
+    const int k = it / 3, r = it % 3;
+    double d = 0.0;
+    for (int c = 0; c < A.X; ++c) d += Ni[((size_t)k * 3 + r) * A.X + c] * (xi[c] - xj[c]);
+    str[it] = d;
+  }
+  if (tid == 0) L.fail = 0;
+  hl_bar();
+  int base = 0, oor = 0;
+  double mx = 0.0, md = 0.0;
+  const int ncand = H * NP;
+  for (int q0 = 0; q0 < ncand; q0 += bd) {
+    const int q = q0 + tid;
+    bool ok = false;
+    double p0 = 0, p1 = 0, p2 = 0;
+    if (q < ncand) {
+      const int k = q / NP, p = q % NP;
+      const double* Tk = sT + k * 9;
+      const double* tk = str + k * 3;
+      const double u0 = sS[3 * p] + tk[0], u1 = sS[3 * p + 1] + tk[1], u2 = sS[3 * p + 2] + tk[2];
+      p0 = ((0.0 + Tk[0] * u0) + Tk[1] * u1) + Tk[2] * u2;
+      p1 = ((0.0 + Tk[3] * u0) + Tk[4] * u1) + Tk[5] * u2;
+      p2 = ((0.0 + Tk[6] * u0) + Tk[7] * u1) + Tk[8] * u2;
+      const double a = p0 - vrel[0], b = p1 - vrel[1], c = p2 - vrel[2];
+      const double t = a * a + b * b + c * c;
+      if (t < A.r2_lo) ok = true;
+      else if (t > A.r2_hi) ok = false;
+      else ok = (a * a) / A.r2 + (b * b) / A.r2 + (c * c) / A.r2 < 1.0;
+    }
+    int tot;
+    const int pos = base + hl_scan(L, ok ? 1 : 0, &tot);
+    if (ok) {
+      const double r0 = round6(p0, &oor), r1 = round6(p1, &oor), r2 = round6(p2, &oor);
+      Pf[3 * pos] = p0; Pf[3 * pos + 1] = p1; Pf[3 * pos + 2] = p2;
+      Pr[3 * pos] = r0; Pr[3 * pos + 1] = r1; Pr[3 * pos + 2] = r2;
+      C0[pos] = make_double4(r0, r1, r2, (double)pos);
+      mx = fmax(mx, fmax(fabs(r0), fmax(fabs(r1), fabs(r2))));
+      const double dx = p0 - r0, dy = p1 - r1, dz = p2 - r2;
+      md = fmax(md, dx * dx + dy * dy + dz * dz);
+    }
+    base += tot;
+  }
+  if (oor) L.fail = 7;
+  int dmy = 0;
+  hl_argmax(L, mx, dmy);
+  dmy = 0;
+  hl_argmax(L, md, dmy);
+  if (tid == 0) {
+    L.n = base;
+    L.eps = 1e-13 * (mx + 1.0);
+    // delta = max |P - P_rounded|, with room for the rule's rounding
+    L.delta = sqrt(md) * (1.0 + 1e-6) + 64.0 * L.eps;
+    if (base < 4) L.fail = 8;
+  }
+  hl_bar();
+  return base;
+}
+
 __device__ __forceinline__ void lhull_body(const HullArgs& A, LHullL& L) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int HNP = A.H * A.NP;
@@ -448,24 +522,12 @@ __device__ __forceinline__ void lhull_body(const HullArgs& A, LHullL& L) {
     const double* Ni = A.NCF + (A.per_agent ? (size_t)i * A.H * 3 * A.X : 0);
     const double vrel[3] = {xi[3] - xj[3], xi[4] - xj[4], xi[5] - xj[5]};
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    const int n = hull_points(A, L, Ti, Ni, xi, xj, vrel, Pr, Pf);
+    const int n = lh_points(A, L, Ti, Ni, xi, xj, vrel, Pr, Pf, C0);
     const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
     int iters = 0, ncomp = 0;
     unsigned long long tcomp = 0, tset = 0;
     const double eps = L.eps, eps2 = eps * eps;
     const double band = 64.0 * eps, band2 = band * band;
-    {
-      // delta = max |P - P_rounded|, with room for the rule's rounding
-      double m = 0.0;
-      int dmy = 0;
-      for (int q = tid; q < n; q += blockDim.x) {
-        const double dx = Pf[3 * q] - Pr[3 * q], dy = Pf[3 * q + 1] - Pr[3 * q + 1], dz = Pf[3 * q + 2] - Pr[3 * q + 2];
-        m = fmax(m, dx * dx + dy * dy + dz * dz);
-        C0[q] = make_double4(Pr[3 * q], Pr[3 * q + 1], Pr[3 * q + 2], (double)q);
-      }
-      hl_argmax(L, m, dmy);
-      if (tid == 0) L.delta = sqrt(m) * (1.0 + 1e-6) + band;
-    }
     if (!L.fail) {
       hull_tetra(L, L, Pr, n, eps, eps2, L.vpid);
       hl_bar();
@@ -541,8 +603,10 @@ __device__ __forceinline__ void lhull_body(const HullArgs& A, LHullL& L) {
       unsigned long long* J = A.ljobs + 4 * (size_t)L.job;
       J[0] = (t1 - t0) | (tset << 32);
       J[1] = (t2 - t1) | (tcomp << 32);
-      J[2] = (unsigned long long)iters | ((unsigned long long)L.nv << 16) | ((unsigned long long)L.nc << 32);
-      J[3] = (unsigned long long)n | ((unsigned long long)L.fail << 32) | ((unsigned long long)L.nf << 40) |
+      J[2] = (unsigned long long)iters | ((unsigned long long)L.nv << 16) | ((unsigned long long)(L.nc & 0xFFFF) << 32) |
+             ((unsigned long long)gridDim.x << 48);
+      J[3] = (unsigned long long)(n & 0xFFFF) | ((unsigned long long)blockIdx.x << 16) |
+             ((unsigned long long)L.fail << 32) | ((unsigned long long)L.nf << 40) |
              ((unsigned long long)min(ncomp, 255) << 56);
     }
     if (!L.fail) {

@@ -761,14 +761,19 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   const bool known = inside_prev != ~0ull;
   int side = c->local_hull ? c->lside_cus : c->side_cus;
   if (c->local_hull) {
-    // local hulls: ~3.7 inside-hull pairs per side CU (C3: 177 on 48 CUs),
-    // widening up to half the CUs as the swarm gets denser
-    if (known && inside_prev * (unsigned long long)c->lside_cus > 177ull * (unsigned long long)side)
-      side = (int)std::min<unsigned long long>(c->n_cu / 2, inside_prev * (unsigned long long)c->lside_cus / 177ull);
+    // local hulls: at most ~3.7 inside-hull pairs per side CU (C3: 177 on
+    // 48 CUs), widening up to half the CUs as the swarm gets denser
+    if (known)
+      side = (int)std::max<unsigned long long>(
+          (unsigned long long)side,
+          std::min<unsigned long long>(c->n_cu / 2, (inside_prev * 10ull + 36ull) / 37ull));
   } else if (known && inside_prev > 2ull * (unsigned long long)side) {
     side = std::min(c->n_cu / 2, (4 * side) / 3);
   }
-  const long max_inside = c->hot_max_inside >= 0 ? c->hot_max_inside : 4L * side;
+  // local hulls: the overlap pays up to ~16 inside-hull pairs per CU of the
+  // widest side (1,067 at 22 m: 15.5 vs 18.0 ms plain; 2,496 at 16 m: a tie)
+  const long max_inside = c->hot_max_inside >= 0 ? c->hot_max_inside
+                                                  : (c->local_hull ? 16L * std::max(side, c->n_cu / 2) : 4L * side);
   const bool crowded = known && inside_prev > (unsigned long long)max_inside;
   // with the local hull the side stream is k_pair(hot) -> k_lhull -> k_pair
   // (rows, the same row queue): no LDS-topology condition
@@ -834,6 +839,15 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
       // later jobs go to the k_lhull after the sweep), then the row sweep
       launch_lhull(dim3(nwait), c->side, Hh);
       HIPCHK(hipGetLastError());
+      if (lds_ok) {
+        // the pairs it handed over (rare: near-coplanar input) in the full
+        // hull right away, still beside the sweep (scratch blocks 0..nwait-1;
+        // the k_hull after the sweep uses nwait.. and starts after the side)
+        HullArgs Hf = Hh;
+        Hf.queue = c->d_lq; Hf.count = c->d_hcount + 11; Hf.next = c->d_hcount + 12;
+        launch_hull(dim3(nwait), c->side, Hf);
+        HIPCHK(hipGetLastError());
+      }
       if (nside > 0) {
         launch_pair(g.x_dim, dim3(nwait), dim3(P.waves * 64), c->lds_bytes, c->side, P);
         HIPCHK(hipGetLastError());

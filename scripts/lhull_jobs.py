@@ -35,8 +35,10 @@ comp_us = (J[:, 1] >> 32) / 100.0
 ncomp = J[:, 3] >> 56
 it = J[:, 2] & 0xFFFF
 nv = (J[:, 2] >> 16) & 0xFFFF
-nc = J[:, 2] >> 32
-n = J[:, 3] & 0xFFFFFFFF
+nc = (J[:, 2] >> 32) & 0xFFFF
+grid = J[:, 2] >> 48
+blk = (J[:, 3] >> 16) & 0xFFFF
+n = J[:, 3] & 0xFFFF
 fail = (J[:, 3] >> 32) & 0xFF
 nf = (J[:, 3] >> 40) & 0xFFFF
 print(f"inside pairs {st['inside']}, timings {t}")
@@ -46,3 +48,8 @@ for name, v in (("points us", pts_us), ("hull us", loop_us), ("  setup us", set_
     print(f"  {name:14s} mean {v.mean():9.1f}  median {np.median(v):9.1f}  max {v.max():9.1f}")
 it_us = (loop_us - set_us - comp_us) / np.maximum(it, 1)
 print(f"  us / iteration (excl. setup, compaction): mean {it_us.mean():.2f}; handed over {int((fail != 0).sum())}")
+for g in sorted(set(grid.tolist())):
+    sel = grid == g
+    tot = pts_us[sel] + loop_us[sel]
+    print(f"  launch of {g} workgroups: {int(sel.sum())} jobs (queue positions {np.flatnonzero(sel).min()}..{np.flatnonzero(sel).max()}), "
+          f"points+hull us mean {tot.mean():.0f} max {tot.max():.0f}")
