@@ -103,6 +103,12 @@ struct HullArgs {
   int* ldone;                       // k_lhull: pairs it decided
   unsigned long long* lfail;        // k_lhull: hand-over reasons (16 counters, cumulative)
   unsigned long long* ljobs;        // k_lhull: per job (< 4096) 4 words: point / loop ticks (100 MHz), counts
+  // lqro_debug_hull_points (test hook): the job's points given (already
+  // rounded: P = P_rounded), k_hull's facets written out
+  const double* ext_pts;
+  int ext_n, ext_max;
+  int* ext_facets;                  // ext_max x 3 point ids
+  int* ext_nf;
   unsigned long long* stats;
   unsigned long long* prof;          // LQRO_HULL_PROFILE: per-phase cycles
 };
@@ -378,9 +384,11 @@ __device__ __forceinline__ int hull_points(const HullArgs& A, LT& L, const doubl
                                            const double* xi, const double* xj, const double* vrel,
                                            double* Pr, double* Pf) {
   const int tid = threadIdx.x;
-  if (tid == 0) { L.n = 0; L.fail = 0; }
+  if (tid == 0) { L.n = A.ext_pts ? A.ext_n : 0; L.fail = 0; }
   hl_bar();
-  for (int k0 = 0; k0 < A.H; k0 += 128) {
+  if (A.ext_pts)
+    for (int q = tid; q < 3 * A.ext_n; q += blockDim.x) Pr[q] = Pf[q] = A.ext_pts[q];
+  for (int k0 = 0; k0 < (A.ext_pts ? 0 : A.H); k0 += 128) {
     for (int it = tid; it < 3 * 128; it += blockDim.x) {
       const int k = k0 + it / 3, r = it % 3;
       if (k < A.H) {
@@ -1491,6 +1499,13 @@ __device__ __forceinline__ void hull_body_mw(const HullArgs& A, HullMemC& M, Hul
     HSTAMP(8);
     // 6. facet selection
     const int nf = L.nf;
+    if (A.ext_facets && !L.fail)
+      for (int f = tid; f < nf; f += blockDim.x)
+        if ((M.own[f] >> 24) != 0xFFu) {
+          const int k = atomicAdd(A.ext_nf, 1);
+          if (k < A.ext_max)
+            for (int e = 0; e < 3; ++e) A.ext_facets[3 * k + e] = vpid[M.fv[f][e]];
+        }
     hull_select(A, M, L, Pr, Pf, vpid, nf, [&](int f) { return (M.own[f] >> 24) != 0xFFu; }, xi, vrel,
                 slot, false);
     HSTAMP(9);

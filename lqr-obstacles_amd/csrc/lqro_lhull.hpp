@@ -454,12 +454,15 @@ __device__ __forceinline__ int lh_points(const HullArgs& A, LHullL& L, const dou
   hl_bar();
   int base = 0, oor = 0;
   double mx = 0.0, md = 0.0;
-  const int ncand = H * NP;
+  const int ncand = A.ext_pts ? A.ext_n : H * NP;
   for (int q0 = 0; q0 < ncand; q0 += bd) {
     const int q = q0 + tid;
     bool ok = false;
     double p0 = 0, p1 = 0, p2 = 0;
-    if (q < ncand) {
+    if (q < ncand && A.ext_pts) {
+      ok = true;   // lqro_debug_hull_points: the points as given (rounded already)
+      p0 = A.ext_pts[3 * q]; p1 = A.ext_pts[3 * q + 1]; p2 = A.ext_pts[3 * q + 2];
+    } else if (q < ncand) {
       const int k = q / NP, p = q % NP;
       const double* Tk = sT + k * 9;
       const double* tk = str + k * 3;
@@ -476,7 +479,9 @@ __device__ __forceinline__ int lh_points(const HullArgs& A, LHullL& L, const dou
     int tot;
     const int pos = base + hl_scan(L, ok ? 1 : 0, &tot);
     if (ok) {
-      const double r0 = round6(p0, &oor), r1 = round6(p1, &oor), r2 = round6(p2, &oor);
+      const bool given = A.ext_pts != nullptr;   // given points are rounded already (k_hull: P = P_rounded)
+      const double r0 = given ? p0 : round6(p0, &oor), r1 = given ? p1 : round6(p1, &oor),
+                   r2 = given ? p2 : round6(p2, &oor);
       Pf[3 * pos] = p0; Pf[3 * pos + 1] = p1; Pf[3 * pos + 2] = p2;
       Pr[3 * pos] = r0; Pr[3 * pos + 1] = r1; Pr[3 * pos + 2] = r2;
       C0[pos] = make_double4(r0, r1, r2, (double)pos);

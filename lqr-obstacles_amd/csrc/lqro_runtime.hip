@@ -819,6 +819,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   Hh.big_main = 0;
   Hh.lqueue = c->d_lq; Hh.lcount = c->d_hcount + 11; Hh.ldone = c->d_hcount + 13;
   Hh.lfail = c->d_prof + 32 + 2 * 4096 + 32;
+  Hh.ext_pts = nullptr; Hh.ext_n = 0; Hh.ext_max = 0; Hh.ext_facets = nullptr; Hh.ext_nf = nullptr;
   Hh.ljobs = c->d_prof + 32 + 2 * 4096 + 48;
   if (g.x_dim != 16 && g.x_dim != 12) return LQRO_E_ARG;
   // the row launch is submitted before the side stream's work: should the two
@@ -1162,6 +1163,86 @@ int lqro_debug_local_hull(lqro_ctx* c, long long* out) {
   out[1] = h[11];
   for (int k = 0; k < 16; ++k) out[2 + k] = (long long)r[k];
   return LQRO_OK;
+}
+
+/* test hook (not in lqro.h): the inside-hull branch on n given points
+ * (already %g-rounded, as qconvex reads them; n <= H * NP of the context)
+ * with relative velocity vrel.  local = 0: k_hull, its facets (point ids)
+ * into facets (max_facets x 3) and their count into *n_facets; local = 1:
+ * k_lhull (no facet list; *n_facets = -1 when it handed the points over).
+ * rec receives the selected facet, distance and normal (hull_select). */
+int lqro_debug_hull_points(lqro_ctx* c, const double* pts, int32_t n, const double* vrel, int32_t local,
+                           int32_t* facets, int32_t max_facets, int32_t* n_facets, lqro_pair_record* rec) {
+  if (!c || !pts || !vrel || !n_facets || !rec || n < 4 || (size_t)n > (size_t)c->cfg.horizon * c->cfg.n_points ||
+      (!local && (!facets || max_facets < 1)))
+    return LQRO_E_ARG;
+  const lqro_config& g = c->cfg;
+  HIPCHK(hipSetDevice(g.device));
+  HIPCHK(wait_last_step(c));
+  const int X = g.x_dim;
+  std::vector<double> xh(2 * (size_t)X, 0.0);
+  for (int q = 0; q < 3; ++q) xh[3 + q] = vrel[q];       // x_i - x_j = vrel, at rest otherwise
+  double *d_pts = nullptr, *d_x = nullptr;
+  int *d_q = nullptr, *d_f = nullptr;
+  lqro_pair_record* d_rec = nullptr;
+  float* d_pl = nullptr;
+  int rc = LQRO_OK;
+  const int fmax = local ? 1 : max_facets;
+  if (hipMalloc(&d_pts, sizeof(double) * 3 * n) != hipSuccess || hipMalloc(&d_x, sizeof(double) * 2 * X) != hipSuccess ||
+      hipMalloc(&d_q, sizeof(int) * 16) != hipSuccess || hipMalloc(&d_f, sizeof(int) * 3 * fmax) != hipSuccess ||
+      hipMalloc(&d_rec, sizeof(lqro_pair_record)) != hipSuccess || hipMalloc(&d_pl, sizeof(float) * 8) != hipSuccess) {
+    rc = LQRO_E_NOMEM;
+  } else {
+    // queue = {slot 0}; count 1; next, local hand-over count / next, done, facet count 0
+    const int q0[16] = {0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    lqro_pair_record r0;
+    memset(&r0, 0, sizeof r0);
+    r0.flags = LQRO_REC_INSIDE;
+    if (hipMemcpy(d_pts, pts, sizeof(double) * 3 * n, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_x, xh.data(), sizeof(double) * 2 * X, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_q, q0, sizeof q0, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_rec, &r0, sizeof r0, hipMemcpyHostToDevice) != hipSuccess) {
+      rc = LQRO_E_HIP;
+    } else {
+      HullArgs Hh;
+      memset(&Hh, 0, sizeof Hh);
+      Hh.N = 2; Hh.X = X; Hh.H = g.horizon; Hh.NP = g.n_points;
+      Hh.row_begin = 0; Hh.row_stride = 1; Hh.npr = 1; Hh.per_agent = 0;
+      Hh.r2 = g.vmax_reach * g.vmax_reach; Hh.r2_lo = Hh.r2; Hh.r2_hi = Hh.r2;
+      Hh.T = c->d_T; Hh.NCF = c->d_NCF; Hh.S = c->d_S; Hh.x = d_x;
+      Hh.planes = d_pl; Hh.recs = d_rec;
+      Hh.queue = d_q + 8; Hh.count = d_q + 1; Hh.cap = 1; Hh.next = d_q + 2;   // d_q[8] = 0: slot 0
+      Hh.scratch = c->d_hscratch; Hh.iscratch = c->d_hiscratch; Hh.fscratch = c->d_hfscratch;
+      Hh.sb = reinterpret_cast<HullPt*>(c->d_hfaces);
+      Hh.fbest = c->d_hfbest; Hh.vpid = c->d_hvpid; Hh.stack = c->d_hstack;
+      Hh.rqueue = d_q + 12; Hh.rcount = d_q + 3; Hh.rnext = d_q + 4;
+      Hh.bigmem = c->d_hbig; Hh.wide = c->d_hwide; Hh.bag = c->d_hbag;
+      Hh.stats = c->d_stats; Hh.prof = nullptr;
+      Hh.lqueue = d_q + 13; Hh.lcount = d_q + 5; Hh.ldone = d_q + 6;
+      Hh.ext_pts = d_pts; Hh.ext_n = n; Hh.ext_max = fmax; Hh.ext_facets = local ? nullptr : d_f; Hh.ext_nf = d_q + 7;
+      if (local) launch_lhull(dim3(1), c->stream, Hh);
+      else launch_hull(dim3(1), c->stream, Hh);
+      if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
+        rc = LQRO_E_HIP;
+      } else {
+        int qh[16];
+        if (hipMemcpy(qh, d_q, sizeof qh, hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(rec, d_rec, sizeof *rec, hipMemcpyDeviceToHost) != hipSuccess) {
+          rc = LQRO_E_HIP;
+        } else if (local) {
+          *n_facets = qh[5] > 0 ? -1 : 0;   // handed over: the full hull would decide
+        } else {
+          *n_facets = qh[7];
+          if (qh[3] > 0) *n_facets = -2;     // k_hull's capacity: k_hull_big would decide
+          const int k = std::min(qh[7], max_facets);
+          if (k > 0 && hipMemcpy(facets, d_f, sizeof(int) * 3 * k, hipMemcpyDeviceToHost) != hipSuccess) rc = LQRO_E_HIP;
+        }
+      }
+    }
+  }
+  for (void* p : {(void*)d_pts, (void*)d_x, (void*)d_q, (void*)d_f, (void*)d_rec, (void*)d_pl})
+    if (p) (void)hipFree(p);
+  return rc;
 }
 
 /* diagnostic (not in lqro.h): k_lhull's per-job words of the last step
