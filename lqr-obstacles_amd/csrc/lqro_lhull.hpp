@@ -3,7 +3,7 @@
 // convexHull (LQRObstacles.cpp:867-969) needs only the hull facets near
 // vrel: the rule takes the facet minimising
 //     | n_f . (vrel - P[t0(f)]) |
-// n_f from the rounded points, P at full precision.  k_lhull (one 4-wave
+// n_f from the rounded points, P at full precision.  k_lhull (one 8-wave
 // workgroup per inside-hull pair, persistent over the queue k_pair fills)
 // grows a small hull Q of the pair's rounded points EPA-style instead of the
 // whole hull (~800 vertices at C3):

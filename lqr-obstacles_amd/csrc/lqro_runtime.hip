@@ -37,7 +37,10 @@
 #include "lqro_dyn.hpp"
 #include "lqro_kern.hpp"
 
-#define LQRO_PROF_WORDS (32 + 2 * 4096 + 16 + 16 + 16 + 4 * 4096)   // hull: 32 counters + 2 words per job; pair: 16; hull wave phases: 16; local hull hand-overs: 16
+// hull: 32 counters + 2 words per job; pair: 16; hull wave phases: 16; local hull hand-overs: 16;
+// local-hull per-job words 4 x 4096
+#define LQRO_PROF_WORDS (32 + 2 * 4096 + 16 + 16 + 16 + 4 * 4096)
+#define LQRO_PROF_HULL_WORDS (32 + 2 * 4096 + 32)   // what lqro_debug_hull_profile returns
 
 using namespace lqro;
 
@@ -378,7 +381,9 @@ struct lqro_ctx {
   // by a third (at most half the CUs), beyond 4 per (widened) side CU the
   // side CUs cannot keep up with the hulls and the plain schedule (every CU
   // on the hulls after the sweep) is faster (scripts/crowded.py)
-  unsigned long long* h_inside;
+  unsigned long long* h_inside;   // 2 pinned slots: step t writes slot t & 1
+  hipEvent_t iev[2];              // recorded after the copy into slot k
+  long long nstep;                // steps enqueued
   long hot_max_inside;       // LQRO_HOT_MAX_INSIDE (-1: 4 x the side CUs)
   int hull_big_blocks;
   int n_cu;
@@ -394,6 +399,7 @@ struct lqro_ctx {
   unsigned long long* d_prof;
   int lds_bytes;
   int stepped;               // a step was enqueued (ev[3] recorded)
+  int lhull_prof;            // LQRO_LHULL_PROFILE: k_lhull writes its per-job words
   PairArgs pa;
 };
 
@@ -461,8 +467,10 @@ void lqro_destroy(lqro_ctx* c) {
     if (p) (void)hipFree(p);
   for (int k = 0; k < 5; ++k)
     if (c->ev[k]) (void)hipEventDestroy(c->ev[k]);
-  for (int k = 0; k < 2; ++k)
+  for (int k = 0; k < 2; ++k) {
     if (c->xev[k]) (void)hipEventDestroy(c->xev[k]);
+    if (c->iev[k]) (void)hipEventDestroy(c->iev[k]);
+  }
   if (c->h_inside) (void)hipHostFree(c->h_inside);
   if (c->side) (void)hipStreamDestroy(c->side);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -507,8 +515,9 @@ static int ctx_alloc(lqro_ctx* c) {
   HIPCHK(hipMalloc(&c->d_lq, sizeof(int) * c->hull_cap));
   HIPCHK(hipMalloc(&c->d_err, sizeof(int)));
   HIPCHK(hipMalloc(&c->d_stats, sizeof(unsigned long long) * 8));
-  HIPCHK(hipHostMalloc((void**)&c->h_inside, sizeof(unsigned long long), hipHostMallocDefault));
-  *c->h_inside = ~0ull;
+  HIPCHK(hipHostMalloc((void**)&c->h_inside, 2 * sizeof(unsigned long long), hipHostMallocDefault));
+  c->h_inside[0] = c->h_inside[1] = ~0ull;
+  for (int k = 0; k < 2; ++k) HIPCHK(hipEventCreateWithFlags(&c->iev[k], hipEventDisableTiming));
   HIPCHK(hipMalloc(&c->d_prof, sizeof(unsigned long long) * LQRO_PROF_WORDS));
   HIPCHK(hipMemset(c->d_prof, 0, sizeof(unsigned long long) * LQRO_PROF_WORDS));
   c->hull_blocks = 256;   // one 138 KB-LDS workgroup per CU, persistent over the queue
@@ -572,6 +581,8 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
     const char* hr = getenv("LQRO_HOT_R");
     c->hot_t = ht ? atof(ht) : 3.0;
     c->hot_r = hr ? atof(hr) : 3.0;
+    const char* lp = getenv("LQRO_LHULL_PROFILE");
+    c->lhull_prof = lp ? atoi(lp) != 0 : 0;
     const char* hm = getenv("LQRO_HOT_MAX_INSIDE");
     c->hot_max_inside = hm ? atol(hm) : -1L;
   }
@@ -680,6 +691,7 @@ int lqro_set_gains(lqro_ctx* c, const double* A, const double* B, const double* 
   HIPCHK(hipSetDevice(g.device));
   const size_t X = g.x_dim, U = g.u_dim, N = g.n_agents;
   const size_t na = per_agent ? N : 1;
+  HIPCHK(wait_last_step(c));   // a step in flight still reads d_T / d_NCF
   HIPCHK(hipMemcpyAsync(c->d_A, A, sizeof(double) * X * X, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(c->d_B, B, sizeof(double) * X * U, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(c->d_L, L, sizeof(double) * na * U * X, hipMemcpyHostToDevice, c->stream));
@@ -729,6 +741,10 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   // add up to one workgroup per CU.  Hull jobs the prediction missed are
   // taken by the k_hull after the sweep.
   P.row_counter = c->d_hcount + 4;
+  // the context's scratch (queues, counters, plane slots, tables) is reused by
+  // every step: a step enqueued on another stream than the last one, or a
+  // set_gains on c->stream, must not overlap the step still in flight
+  if (c->stepped) HIPCHK(hipStreamWaitEvent(s, c->ev[3], 0));
   HIPCHK(hipEventRecord(c->ev[0], s));
   HIPCHK(hipMemsetAsync(c->d_hcount, 0, sizeof(int) * 16, s));
   HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * 8, s));
@@ -757,7 +773,15 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   // crowded swarms (many inside-hull pairs in an earlier step: the value is
   // read without waiting for the copy, it only picks the schedule, and every
   // schedule gives bit-identical results) take the plain schedule
-  const unsigned long long inside_prev = *(volatile unsigned long long*)c->h_inside;
+  // The inside-hull count that picks the schedule is step t-2's, read after
+  // that step's copy completed (the host runs at most one step ahead of the
+  // GPU here), so the schedule does not depend on host/GPU timing.
+  const int slot = (int)(c->nstep & 1);
+  unsigned long long inside_prev = ~0ull;
+  if (c->nstep >= 2) {
+    HIPCHK(hipEventSynchronize(c->iev[slot]));
+    inside_prev = c->h_inside[slot];
+  }
   const bool known = inside_prev != ~0ull;
   int side = c->local_hull ? c->lside_cus : c->side_cus;
   if (c->local_hull) {
@@ -820,7 +844,9 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   Hh.lqueue = c->d_lq; Hh.lcount = c->d_hcount + 11; Hh.ldone = c->d_hcount + 13;
   Hh.lfail = c->d_prof + 32 + 2 * 4096 + 32;
   Hh.ext_pts = nullptr; Hh.ext_n = 0; Hh.ext_max = 0; Hh.ext_facets = nullptr; Hh.ext_nf = nullptr;
-  Hh.ljobs = c->d_prof + 32 + 2 * 4096 + 48;
+  // per-job stamps only when asked for (LQRO_LHULL_PROFILE=1, scripts/lhull_jobs.py);
+  // lfail counts hand-over reasons since the context was created
+  Hh.ljobs = c->lhull_prof ? c->d_prof + 32 + 2 * 4096 + 48 : nullptr;
   if (g.x_dim != 16 && g.x_dim != 12) return LQRO_E_ARG;
   // the row launch is submitted before the side stream's work: should the two
   // streams land on one hardware queue (a second context in the process), the
@@ -887,9 +913,11 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   La.vgoal = d_vgoal; La.newv = d_newv; La.prof = c->d_prof;
   La.lp4_list = c->d_lp4; La.lp4_count = c->d_hcount + 9; La.lp4_next = c->d_hcount + 10;
   HIPCHK(launch_lp(La, s));
-  HIPCHK(hipMemcpyAsync(c->h_inside, c->d_stats + 2, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(c->h_inside + slot, c->d_stats + 2, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipEventRecord(c->iev[slot], s));
   HIPCHK(hipEventRecord(c->ev[3], s));
   c->stepped = 1;
+  c->nstep++;
   return LQRO_OK;
 }
 
@@ -1186,9 +1214,12 @@ int lqro_debug_hull_points(lqro_ctx* c, const double* pts, int32_t n, const doub
   int *d_q = nullptr, *d_f = nullptr;
   lqro_pair_record* d_rec = nullptr;
   float* d_pl = nullptr;
+  unsigned long long* d_st = nullptr;
   int rc = LQRO_OK;
   const int fmax = local ? 1 : max_facets;
-  if (hipMalloc(&d_pts, sizeof(double) * 3 * n) != hipSuccess || hipMalloc(&d_x, sizeof(double) * 2 * X) != hipSuccess ||
+  if (hipMalloc(&d_st, sizeof(unsigned long long) * 8) != hipSuccess ||
+      hipMemset(d_st, 0, sizeof(unsigned long long) * 8) != hipSuccess ||
+      hipMalloc(&d_pts, sizeof(double) * 3 * n) != hipSuccess || hipMalloc(&d_x, sizeof(double) * 2 * X) != hipSuccess ||
       hipMalloc(&d_q, sizeof(int) * 16) != hipSuccess || hipMalloc(&d_f, sizeof(int) * 3 * fmax) != hipSuccess ||
       hipMalloc(&d_rec, sizeof(lqro_pair_record)) != hipSuccess || hipMalloc(&d_pl, sizeof(float) * 8) != hipSuccess) {
     rc = LQRO_E_NOMEM;
@@ -1217,7 +1248,7 @@ int lqro_debug_hull_points(lqro_ctx* c, const double* pts, int32_t n, const doub
       Hh.fbest = c->d_hfbest; Hh.vpid = c->d_hvpid; Hh.stack = c->d_hstack;
       Hh.rqueue = d_q + 12; Hh.rcount = d_q + 3; Hh.rnext = d_q + 4;
       Hh.bigmem = c->d_hbig; Hh.wide = c->d_hwide; Hh.bag = c->d_hbag;
-      Hh.stats = c->d_stats; Hh.prof = nullptr;
+      Hh.stats = d_st; Hh.prof = nullptr;   // the hook never alters the step's statistics
       Hh.lqueue = d_q + 13; Hh.lcount = d_q + 5; Hh.ldone = d_q + 6;
       Hh.ext_pts = d_pts; Hh.ext_n = n; Hh.ext_max = fmax; Hh.ext_facets = local ? nullptr : d_f; Hh.ext_nf = d_q + 7;
       if (local) launch_lhull(dim3(1), c->stream, Hh);
@@ -1240,7 +1271,7 @@ int lqro_debug_hull_points(lqro_ctx* c, const double* pts, int32_t n, const doub
       }
     }
   }
-  for (void* p : {(void*)d_pts, (void*)d_x, (void*)d_q, (void*)d_f, (void*)d_rec, (void*)d_pl})
+  for (void* p : {(void*)d_pts, (void*)d_x, (void*)d_q, (void*)d_f, (void*)d_rec, (void*)d_pl, (void*)d_st})
     if (p) (void)hipFree(p);
   return rc;
 }
@@ -1262,7 +1293,9 @@ int lqro_debug_hull_profile(lqro_ctx* c, unsigned long long* out16) {
   if (!c || !out16) return LQRO_E_ARG;
   HIPCHK(hipSetDevice(c->cfg.device));
   HIPCHK(wait_last_step(c));
-  HIPCHK(hipMemcpy(out16, c->d_prof, sizeof(unsigned long long) * LQRO_PROF_WORDS, hipMemcpyDeviceToHost));
+  // the documented prefix only (32 hull counters, 2 x 4096 job words, 32
+  // pair / wave-phase words): callers size their buffer to it
+  HIPCHK(hipMemcpy(out16, c->d_prof, sizeof(unsigned long long) * LQRO_PROF_HULL_WORDS, hipMemcpyDeviceToHost));
   return LQRO_OK;
 }
 

@@ -11,6 +11,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "lqr-obstacles_amd")]
 os.environ.setdefault("LQRO_LOCAL_HULL", "1")
+os.environ.setdefault("LQRO_LHULL_PROFILE", "1")   # k_lhull writes its per-job words
 import lqro  # noqa: E402
 
 box = float(sys.argv[1]) if len(sys.argv) > 1 else None

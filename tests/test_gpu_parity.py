@@ -218,8 +218,9 @@ def test_overlap_schedule_identical(lqro_mod, gains, monkeypatch, kind):
 def test_adaptive_schedule_identical(lqro_mod, gains, monkeypatch):
     """The schedule adapts to the inside-hull count of an earlier step: a
     crowded swarm (1024 agents in a 22 m box, ~1,100 inside-hull pairs) takes
-    the plain schedule from its second step on, a moderately dense one (30 m,
-    ~420) a widened side stream.  Records and new velocities of those steps
+    the plain schedule from its third step on (a step is scheduled by the
+    count of the step two before it), a moderately dense one (30 m, ~420) a
+    widened side stream.  Records and new velocities of those steps
     equal the plain schedule's and the forced overlap's bit for bit."""
     N, H, NP = 1024, 100, 100
     for box in (22.0, 30.0):
@@ -233,7 +234,8 @@ def test_adaptive_schedule_identical(lqro_mod, gains, monkeypatch):
                 monkeypatch.setenv(k, v)
             ctx = lqro_mod.Context(lqro_mod.config(N, H, NP, flags=lqro_mod.LQRO_FLAG_RECORDS))
             ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
-            ctx.step(x, vg)                  # the count the next steps are scheduled by
+            ctx.step(x, vg)                  # the count steps 3 and 4 are scheduled by
+            ctx.step(x, vg)
             v = ctx.step(x, vg)
             r = ctx.records()
             v3 = ctx.step(x, vg)
@@ -325,8 +327,9 @@ def test_local_hull_identical(lqro_mod, gains, monkeypatch, case):
         v = ctx.step(x, vg)
         r = ctx.records()
         if flag == "1":
-            # a second step is scheduled by the first's inside-hull count
+            # a third step is scheduled by the first's inside-hull count
             # (side width, or the plain schedule for crowded swarms)
+            assert np.array_equal(ctx.step(x, vg), v)
             assert np.array_equal(ctx.step(x, vg), v)
             r2 = ctx.records()
             for f in ("flags", "facet", "dist", "plane_point", "plane_normal"):
