@@ -39,6 +39,11 @@ enum {
 
 /* ---- flags ------------------------------------------------------------- */
 #define LQRO_FLAG_RECORDS     0x1  /* keep per-pair records for lqro_get_records */
+#define LQRO_FLAG_QHULL_ORDER 0x2  /* inside-hull branch with the reference's own rule   */
+                                   /*   (LQRO:925-968): Qhull's facet order and each    */
+                                   /*   facet's first Fv vertex, strict '<', and the    */
+                                   /*   loop-carried normalVector when facet 0 wins     */
+                                   /*   (LQRO:956-968, 1385); built in-kernel by k_qhull */
 
 /* per-pair record flags (lqro_pair_record.flags) */
 #define LQRO_REC_PLANE    0x01  /* n_reach > min_reach: a half-plane was emitted (LQRO:1409) */
@@ -47,6 +52,10 @@ enum {
 #define LQRO_REC_HULL     0x08  /* the in-kernel hull produced the plane (LQRO:867-969) */
 #define LQRO_REC_HULLFAIL 0x10  /* hull degenerate / capacity exceeded                  */
 #define LQRO_REC_LOCAL    0x20  /* the plane came from the local hull (k_lhull)          */
+#define LQRO_REC_STALE    0x40  /* Qhull order: facet 0 won, normal = the loop-carried    */
+                                /*   normalVector of the previous pair (LQRO:956-968)    */
+#define LQRO_REC_QHMERGE  0x80  /* Qhull order: Qhull would merge facets in this hull;   */
+                                /*   built merge-free                       */
 
 /* Static configuration.  The names follow the reference's compile-time
  * macros (LQRO:9-14) and the constants of its driver (LQRO:1387, 1224). */
@@ -88,8 +97,11 @@ typedef struct lqro_pair_record {
   int32_t gjk_iters;      /* G-tests performed by gjk_distance               */
   int32_t simplex_n;      /* final GJK simplex size                          */
   int32_t simplex[4];     /* final GJK simplex: indices into reachablePoints */
-  int32_t facet[3];       /* hull branch: arg-min facet (reachable indices)  */
-  int32_t n_facets;       /* hull branch: number of hull facets              */
+  int32_t facet[3];       /* hull branch: arg-min facet (reachable indices); */
+                          /*   Qhull order: in Fv order, facet[0] = the vertex */
+                          /*   the distance is measured from (LQRO:934-937)  */
+  int32_t n_facets;       /* hull branch: number of hull facets (LQRO_REC_LOCAL: */
+                          /*   the certified facets of the local hull)       */
   uint64_t reach_hash;    /* sum of splitmix64(q) over reachable point ids q */
   double dist;            /* distance before the *0.5 of LQRO:1416           */
   double normal[3];       /* normalVector fed to createHalfPlanes            */
@@ -187,6 +199,13 @@ int lqro_step_device(lqro_ctx* ctx, const double* d_x, const double* d_vgoal,
  * velocity vgoal[3r..3r+2]; writes newv[3r..3r+2].  Synchronous. */
 int lqro_calculate_new_v(const float* planes, const int64_t* offsets, int32_t n_agents,
                          const double* vgoal, double vmax_lp, double* newv, int32_t device);
+
+/* LQRO_FLAG_QHULL_ORDER: the loop-carried normalVector (LQRO:1385) entering
+ * the context's first row (set; 0,0,0 at creation) and leaving its last
+ * eligible pair after the last step (get).  A single context carries it
+ * from step to step itself; row-sharded callers chain ranks with these. */
+int lqro_set_carry_normal(lqro_ctx* ctx, const double* n3);
+int lqro_get_carry_normal(lqro_ctx* ctx, double* n3);
 
 /* Per-pair records of the last step (LQRO_FLAG_RECORDS): rows
  * [row_begin,row_end) x (n_agents-1) neighbours in j order. */

@@ -9,6 +9,7 @@
  * expression chains associate left to right, unary minus binds first.
  */
 #include "lqro_oracle.h"
+#include "lqro_qhull.h"
 
 #include <float.h>
 #include <math.h>
@@ -1038,6 +1039,58 @@ int orc_hull_branch(int n, const double* pts_full, const double vrel[3], double*
   return nf;
 }
 
+/* The reference's own selection rule (convexHull, LQRO:867-969) over
+ * Qhull's output (lqro_qhull.c): facets in Qhull's order, each measured from
+ * its FIRST Fv vertex at full precision (LQRO:934-937), strict '<'
+ * (LQRO:955-967); facet 0 never writes `normal` (LQRO:956-958): *stale = 1
+ * then, and the caller keeps the loop-carried normalVector.  round16 = 1
+ * reads the planes back as qconvex prints them (%.16g, LQRO:895-899).
+ * *qstatus: lqro_qhull.h QHO_* bits (non-zero: Qhull would have merged
+ * facets; the hull was built on merge-free).  Returns the facet count or
+ * <= 0 on failure. */
+static int g_hull_rule = 0, g_round16 = 0;
+static double g_carry[3] = {0.0, 0.0, 0.0};
+
+void orc_set_hull_rule(int rule, int round16) { g_hull_rule = rule; g_round16 = round16; }
+void orc_set_carry_normal(const double* n) { g_carry[0] = n[0]; g_carry[1] = n[1]; g_carry[2] = n[2]; }
+void orc_get_carry_normal(double* n) { n[0] = g_carry[0]; n[1] = g_carry[1]; n[2] = g_carry[2]; }
+
+static double g16(double v) {
+  char b[64];
+  snprintf(b, sizeof b, "%.16g", v);
+  return strtod(b, NULL);
+}
+
+int orc_hull_branch_ref(int n, const double* pts_full, const double vrel[3], double* dist,
+                        double normal[3], int facet[3], int* stale, int* qstatus) {
+  double* rp = (double*)malloc(sizeof(double) * 3 * (size_t)n);
+  for (int i = 0; i < 3 * n; i++) rp[i] = orc_round6(pts_full[i]);      /* LQRO:871-873 */
+  orc_qhull_out o;
+  const int nf = orc_qhull_ex(rp, n, &o, 1);
+  *qstatus = o.status;
+  *stale = 0;
+  if (nf <= 0) { orc_qhull_free(&o); free(rp); return nf <= 0 ? -1 : nf; }
+  int best = 0;
+  double d = 0.0;
+  for (int f = 0; f < nf; f++) {
+    double pl[3];
+    for (int k = 0; k < 3; k++) pl[k] = g_round16 ? g16(o.plane[4 * f + k]) : o.plane[4 * f + k];
+    const double* P = pts_full + 3 * (size_t)o.fv[3 * f];              /* first Fv vertex */
+    const double t = fabs(pl[0] * (vrel[0] - P[0]) + pl[1] * (vrel[1] - P[1]) + pl[2] * (vrel[2] - P[2]));
+    if (f == 0 || t < d) {
+      d = t;
+      best = f;
+      if (f > 0) { normal[0] = pl[0]; normal[1] = pl[1]; normal[2] = pl[2]; }
+    }
+  }
+  *dist = d;
+  *stale = best == 0;
+  for (int k = 0; k < 3; k++) facet[k] = o.fv[3 * best + k];
+  orc_qhull_free(&o);
+  free(rp);
+  return nf;
+}
+
 /* ------------------------------------------------------------------------ */
 /* Per pair                                                                   */
 /* ------------------------------------------------------------------------ */
@@ -1104,7 +1157,18 @@ int orc_pair(int X, int H, int NP, int min_reach, double vmax_reach, const doubl
     rec->flags = LQRO_REC_PLANE | (inside ? LQRO_REC_INSIDE : 0) | (backup ? LQRO_REC_BACKUP : 0);
     rec->gjk_iters = iters; rec->simplex_n = sn;
     for (int k = 0; k < 3; k++) { rec->wpt_vrel[k] = w1[k]; rec->wpt_hull[k] = w2[k]; }
-    if (inside) {                                                 /* LQRO:1411-1412 */
+    int stale = 0;
+    if (inside && g_hull_rule) {                                  /* LQRO:1411-1412 */
+      int qst = 0;
+      int nf = orc_hull_branch_ref(n, pts, vrel, &distance, normal, rec->facet, &stale, &qst);
+      rec->n_facets = nf;
+      if (nf > 0) rec->flags |= LQRO_REC_HULL; else rec->flags |= LQRO_REC_HULLFAIL;
+      if (qst) rec->flags |= LQRO_REC_QHMERGE;
+      if (stale) {   /* normalVector keeps the previous pair's value: resolved by the row loop */
+        rec->flags |= LQRO_REC_STALE;
+        normal[0] = normal[1] = normal[2] = 0.0;
+      }
+    } else if (inside) {
       int nf = orc_hull_branch(n, pts, vrel, &distance, normal, rec->facet);
       rec->n_facets = nf;
       if (nf > 0) rec->flags |= LQRO_REC_HULL; else rec->flags |= LQRO_REC_HULLFAIL;
@@ -1340,10 +1404,33 @@ typedef struct {
   const double *A, *B, *L, *E;
 } faith_t;
 
+/* Qhull-order rule: the loop-carried normalVector (LQRO:1385) across the
+ * pairs of a row is resolved in step_rows; a row whose first eligible pairs
+ * are stale waits for the previous row's last normal (rows run on several
+ * threads): its planes are kept and resolve_rows finishes it in row order. */
+typedef struct {
+  int kind;            /* 0: no eligible pair; 1: `last` is the row's last normal; */
+                       /* 2: every eligible pair is a leading stale pair          */
+  double last[3];
+  int m, nlead;
+  float* planes;       /* m x 6, kept when nlead > 0 */
+  int* lead_plane;     /* plane index of each leading stale pair */
+  int* lead_rec;       /* its record index */
+  double* lead_dist;   /* its 0.5 * dist */
+} rowstate_t;
+
+static void stale_plane(const double* xi, double half_dist, const double* n, float* pp, float* pn) {
+  const double mult = 1.0;                                        /* inside, LQRO:1212-1213 */
+  for (int k = 0; k < 3; k++) {
+    pn[k] = (float)n[k];
+    pp[k] = (float)(xi[3 + k] + mult * half_dist * n[k]);
+  }
+}
+
 static int step_rows(int N, int X, int H, int NP, int min_reach, double vmax_reach, double vmax_lp,
                      int per_agent, const double* T, const double* NCF, const double* S,
                      const double* x, const double* vgoal, int r0, int r1, double* newv,
-                     lqro_pair_record* recs, const faith_t* fa) {
+                     lqro_pair_record* recs, const faith_t* fa, rowstate_t* rs) {
   unsigned char* sel = (unsigned char*)malloc((size_t)N);
   double* pts = (double*)malloc(sizeof(double) * 3 * (size_t)H * (size_t)NP);
   float* planes = (float*)malloc(sizeof(float) * 6 * (size_t)(N > 1 ? N - 1 : 1));
@@ -1356,6 +1443,11 @@ static int step_rows(int N, int X, int H, int NP, int min_reach, double vmax_rea
     const double* Ni = per_agent ? NCF + (size_t)i * H * 3 * X : NCF;
     if (fa) { Ti = Tf; Ni = Nf; }
     int m = 0;
+    int have = 0, nlead = 0;
+    double cur[3] = {0.0, 0.0, 0.0};
+    int* lead_plane = NULL;
+    int* lead_rec = NULL;
+    double* lead_dist = NULL;
     if (g_nbr_k > 0) orc_neighbors(N, X, x, i, g_nbr_r2, g_nbr_k, sel);
     for (int j = 0; j < N; ++j) {
       if (j == i) continue;
@@ -1388,6 +1480,28 @@ static int step_rows(int N, int X, int H, int NP, int min_reach, double vmax_rea
         volatile double sq2 = orc_gjk(vrel, rec.n_reach, pts, w1, w2, &it2, &sn2, simp, &bk2);
         (void)sq2;
       }
+      if (rs && (rec.flags & LQRO_REC_PLANE)) {
+        if (rec.flags & LQRO_REC_STALE) {
+          if (have) {
+            for (int k = 0; k < 3; k++) rec.normal[k] = cur[k];
+            stale_plane(x + (size_t)i * X, 0.5 * rec.dist, cur, rec.plane_point, rec.plane_normal);
+          } else {
+            if (!lead_plane) {
+              lead_plane = (int*)malloc(sizeof(int) * (size_t)N);
+              lead_rec = (int*)malloc(sizeof(int) * (size_t)N);
+              lead_dist = (double*)malloc(sizeof(double) * (size_t)N);
+            }
+            lead_plane[nlead] = m;
+            lead_rec[nlead] = (int)((i - r0) * (N - 1) + (j < i ? j : j - 1));
+            lead_dist[nlead] = 0.5 * rec.dist;
+            nlead++;
+          }
+        }
+        if (have || !(rec.flags & LQRO_REC_STALE)) {
+          for (int k = 0; k < 3; k++) cur[k] = rec.normal[k];
+          have = 1;
+        }
+      }
       if (recs) recs[(size_t)(i - r0) * (N - 1) + (j < i ? j : j - 1)] = rec;
       if (rec.flags & LQRO_REC_PLANE) {
         for (int k = 0; k < 3; k++) {
@@ -1397,6 +1511,20 @@ static int step_rows(int N, int X, int H, int NP, int min_reach, double vmax_rea
         m++;
       }
     }
+    if (rs) {
+      rowstate_t* R = &rs[i - r0];
+      R->kind = have ? 1 : (nlead ? 2 : 0);
+      for (int k = 0; k < 3; k++) R->last[k] = cur[k];
+      R->m = m;
+      R->nlead = nlead;
+      if (nlead) {   /* the LP waits for the previous row's normal (resolve_rows) */
+        R->planes = (float*)malloc(sizeof(float) * 6 * (size_t)(m ? m : 1));
+        memcpy(R->planes, planes, sizeof(float) * 6 * (size_t)m);
+        R->lead_plane = lead_plane; R->lead_rec = lead_rec; R->lead_dist = lead_dist;
+        continue;
+      }
+      free(lead_plane); free(lead_rec); free(lead_dist);
+    }
     orc_newv(m, planes, vgoal + (size_t)i * 3, vmax_lp, newv + (size_t)i * 3);  /* LQRO:1435 */
   }
 out:
@@ -1404,12 +1532,46 @@ out:
   return rc;
 }
 
+/* The rows in order (LQRO:1393): leading stale pairs take the normal the
+ * previous row left (g_carry for the first row), then the row's LP runs;
+ * g_carry leaves with the last row's normal, for the next step. */
+static void resolve_rows(int N, int X, double vmax_lp, const double* x, const double* vgoal, int r0, int r1,
+                         double* newv, lqro_pair_record* recs, rowstate_t* rs) {
+  double carry[3] = {g_carry[0], g_carry[1], g_carry[2]};
+  for (int i = r0; i < r1; ++i) {
+    rowstate_t* R = &rs[i - r0];
+    if (R->nlead) {
+      for (int q = 0; q < R->nlead; q++) {
+        float* pl = R->planes + 6 * (size_t)R->lead_plane[q];
+        stale_plane(x + (size_t)i * X, R->lead_dist[q], carry, pl, pl + 3);
+        if (recs) {
+          lqro_pair_record* r = &recs[R->lead_rec[q]];
+          for (int k = 0; k < 3; k++) {
+            r->normal[k] = carry[k];
+            r->plane_point[k] = pl[k];
+            r->plane_normal[k] = pl[3 + k];
+          }
+        }
+      }
+      orc_newv(R->m, R->planes, vgoal + (size_t)i * 3, vmax_lp, newv + (size_t)i * 3);   /* LQRO:1435 */
+      free(R->planes); free(R->lead_plane); free(R->lead_rec); free(R->lead_dist);
+    }
+    if (R->kind == 1)
+      for (int k = 0; k < 3; k++) carry[k] = R->last[k];
+  }
+  for (int k = 0; k < 3; k++) g_carry[k] = carry[k];
+}
+
 int orc_step(int N, int X, int H, int NP, int min_reach, double vmax_reach, double vmax_lp,
              int per_agent, const double* T, const double* NCF, const double* S,
              const double* x, const double* vgoal, int r0, int r1, double* newv,
              lqro_pair_record* recs) {
-  return step_rows(N, X, H, NP, min_reach, vmax_reach, vmax_lp, per_agent, T, NCF, S, x, vgoal, r0,
-                   r1, newv, recs, NULL);
+  rowstate_t* rs = g_hull_rule ? (rowstate_t*)calloc((size_t)(r1 - r0 > 0 ? r1 - r0 : 1), sizeof(rowstate_t)) : NULL;
+  int rc = step_rows(N, X, H, NP, min_reach, vmax_reach, vmax_lp, per_agent, T, NCF, S, x, vgoal, r0,
+                     r1, newv, recs, NULL, rs);
+  if (rs && !rc) resolve_rows(N, X, vmax_lp, x, vgoal, r0, r1, newv, recs, rs);
+  free(rs);
+  return rc;
 }
 
 typedef struct {
@@ -1420,13 +1582,15 @@ typedef struct {
   lqro_pair_record* recs;
   int rbase;
   const faith_t* fa;
+  rowstate_t* rs;
 } mt_arg;
 
 static void* mt_body(void* p) {
   mt_arg* a = (mt_arg*)p;
   a->rc = step_rows(a->N, a->X, a->H, a->NP, a->min_reach, a->vmax_reach, a->vmax_lp, a->per_agent,
                     a->T, a->NCF, a->S, a->x, a->vgoal, a->r0, a->r1, a->newv,
-                    a->recs ? a->recs + (size_t)(a->r0 - a->rbase) * (a->N - 1) : NULL, a->fa);
+                    a->recs ? a->recs + (size_t)(a->r0 - a->rbase) * (a->N - 1) : NULL, a->fa,
+                    a->rs ? a->rs + (a->r0 - a->rbase) : NULL);
   return NULL;
 }
 
@@ -1461,8 +1625,14 @@ static int step_mt(int N, int X, int H, int NP, int min_reach, double vmax_reach
                    int per_agent, const double* T, const double* NCF, const double* S,
                    const double* x, const double* vgoal, int r0, int r1, double* newv,
                    lqro_pair_record* recs, int threads, const faith_t* fa) {
-  if (threads <= 1) return step_rows(N, X, H, NP, min_reach, vmax_reach, vmax_lp, per_agent, T, NCF,
-                                     S, x, vgoal, r0, r1, newv, recs, fa);
+  rowstate_t* rs = g_hull_rule ? (rowstate_t*)calloc((size_t)(r1 - r0 > 0 ? r1 - r0 : 1), sizeof(rowstate_t)) : NULL;
+  if (threads <= 1) {
+    int rc1 = step_rows(N, X, H, NP, min_reach, vmax_reach, vmax_lp, per_agent, T, NCF, S, x, vgoal, r0,
+                        r1, newv, recs, fa, rs);
+    if (rs && !rc1) resolve_rows(N, X, vmax_lp, x, vgoal, r0, r1, newv, recs, rs);
+    free(rs);
+    return rc1;
+  }
   pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)threads);
   mt_arg* args = (mt_arg*)malloc(sizeof(mt_arg) * (size_t)threads);
   int rows = r1 - r0, rc = 0;
@@ -1470,7 +1640,7 @@ static int step_mt(int N, int X, int H, int NP, int min_reach, double vmax_reach
     mt_arg* a = &args[t];
     a->N = N; a->X = X; a->H = H; a->NP = NP; a->min_reach = min_reach; a->per_agent = per_agent;
     a->vmax_reach = vmax_reach; a->vmax_lp = vmax_lp; a->T = T; a->NCF = NCF; a->S = S; a->x = x;
-    a->vgoal = vgoal; a->newv = newv; a->recs = recs; a->rbase = r0; a->fa = fa;
+    a->vgoal = vgoal; a->newv = newv; a->recs = recs; a->rbase = r0; a->fa = fa; a->rs = rs;
     a->r0 = r0 + (int)((long long)rows * t / threads);
     a->r1 = r0 + (int)((long long)rows * (t + 1) / threads);
     a->rc = 0;
@@ -1478,6 +1648,8 @@ static int step_mt(int N, int X, int H, int NP, int min_reach, double vmax_reach
   }
   for (int t = 0; t < threads; t++) { pthread_join(th[t], NULL); if (args[t].rc) rc = args[t].rc; }
   free(th); free(args);
+  if (rs && !rc) resolve_rows(N, X, vmax_lp, x, vgoal, r0, r1, newv, recs, rs);
+  free(rs);
   return rc;
 }
 

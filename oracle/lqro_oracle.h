@@ -117,6 +117,20 @@ double orc_gjk(const double vrel[3], int n, const double* pts, double wpt1[3],
 int  orc_hull_branch(int n, const double* pts_full, const double vrel[3],
                      double* dist, double normal[3], int facet[3]);
 
+/* The reference's own rule over Qhull's output (lqro_qhull.c): facets in
+ * Qhull's order, first Fv vertex, strict '<' (LQRO:925-968).  *stale = 1 when
+ * facet 0 wins (normal untouched, LQRO:956-958); *qstatus = QHO_* bits of a
+ * hull Qhull would merge (built merge-free).  Returns the facet count. */
+int  orc_hull_branch_ref(int n, const double* pts_full, const double vrel[3], double* dist,
+                         double normal[3], int facet[3], int* stale, int* qstatus);
+/* rule 0: the canonical rule above (default); 1: the reference's rule for
+ * orc_pair / orc_step*, with the loop-carried normalVector resolved in row
+ * order from the carry (set/get: the value entering / leaving a step's
+ * rows).  round16: planes read back as qconvex prints them (%.16g). */
+void orc_set_hull_rule(int rule, int round16);
+void orc_set_carry_normal(const double* n);
+void orc_get_carry_normal(double* n);
+
 /* Full hull of n points (no rounding applied here): writes up to cap facets
  * as outward-oriented index triples; returns the facet count or <0. */
 int  orc_hull(int n, const double* pts, int32_t* facets, int cap);

@@ -278,3 +278,76 @@ def keyframes(t: float, x_true, rot_true) -> np.ndarray:
     for a in range(n):
         lib().orc_keyframe(float(t), _p(x_true[a]), _p(rot_true[a]), _p(out[a]))
     return out
+
+
+class _QhullOut(C.Structure):
+    _fields_ = [("nfacets", C.c_int), ("nvertices", C.c_int), ("fv", C.POINTER(C.c_int)),
+                ("plane", C.POINTER(C.c_double)), ("facet_id", C.POINTER(C.c_int)),
+                ("status", C.c_int)] + [(k, C.c_int) for k in (
+                    "st_addpoints", "st_partition", "st_horizon_max", "st_horizon_sum", "st_cop_max",
+                    "st_old_append", "st_visible_max", "st_new_max", "st_partition_max", "st_facets_created")]
+
+
+def qhull(points: np.ndarray, keep_going: bool = False):
+    """orc_qhull: Qhull 2019.1's build restated (lqro_qhull.c) on n x 3
+    points.  Returns (status, fv (F x 3, Fv order), planes (F x 4), facet ids);
+    status != 0 means the hull needs Qhull's merging (not restated)."""
+    o = lib()
+    if not getattr(o, "_qh_init", False):
+        o.orc_qhull.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+        o.orc_qhull_ex.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int]
+        o.orc_qhull_free.argtypes = [C.c_void_p]
+        o._qh_init = True
+    points = np.ascontiguousarray(points, np.float64)
+    out = _QhullOut()
+    o.orc_qhull_ex(_p(points), points.shape[0], C.byref(out), int(keep_going))
+    nf = out.nfacets
+    if (out.status and not keep_going) or nf <= 0:
+        st = out.status
+        o.orc_qhull_free(C.byref(out))
+        return st, None, None, None
+    fv = np.ctypeslib.as_array(out.fv, shape=(nf, 3)).copy()
+    pl = np.ctypeslib.as_array(out.plane, shape=(nf, 4)).copy()
+    fid = np.ctypeslib.as_array(out.facet_id, shape=(nf,)).copy()
+    st = out.status
+    global last_qhull_stats
+    last_qhull_stats = {k: getattr(out, k) for k, _ in _QhullOut._fields_ if k.startswith("st_")}
+    o.orc_qhull_free(C.byref(out))
+    return st, fv, pl, fid
+
+
+def set_hull_rule(rule: int, round16: bool = False):
+    """0: the canonical rule (default); 1: the reference's rule over Qhull's
+    order (orc_hull_branch_ref), loop-carried normal resolved in row order.
+    round16: planes read back as qconvex prints them (%.16g).  Process-wide."""
+    o = lib()
+    o.orc_set_hull_rule.argtypes = [C.c_int, C.c_int]
+    o.orc_set_hull_rule(int(rule), int(round16))
+
+
+def carry_normal(n=None):
+    """Get (n=None) or set the loop-carried normalVector entering the next step."""
+    o = lib()
+    o.orc_get_carry_normal.argtypes = [C.c_void_p]
+    o.orc_set_carry_normal.argtypes = [C.c_void_p]
+    if n is None:
+        out = np.zeros(3)
+        o.orc_get_carry_normal(_p(out))
+        return out
+    v = np.ascontiguousarray(n, np.float64)
+    o.orc_set_carry_normal(_p(v))
+
+
+def hull_branch_ref(points_full: np.ndarray, vrel):
+    """orc_hull_branch_ref: (nfacets, dist, normal or None if stale, Fv triple, qstatus)."""
+    o = lib()
+    o.orc_hull_branch_ref.argtypes = [C.c_int] + [C.c_void_p] * 7
+    points_full = np.ascontiguousarray(points_full, np.float64)
+    v = np.ascontiguousarray(vrel, np.float64)
+    d = np.zeros(1)
+    nrm = np.zeros(3)
+    fac = np.zeros(3, np.int32)
+    st = np.zeros(2, np.int32)
+    k = o.orc_hull_branch_ref(points_full.shape[0], _p(points_full), _p(v), _p(d), _p(nrm), _p(fac),
+                              _p(st[:1]), _p(st[1:]))
+    return k, float(d[0]), (None if st[0] else nrm), fac, int(st[1])
