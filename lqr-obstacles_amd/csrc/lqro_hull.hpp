@@ -107,10 +107,19 @@ struct HullArgs {
   // rounded: P = P_rounded), k_hull's facets written out
   const double* ext_pts;
   int ext_n, ext_max;
+  int ext_full;                     // ext_pts also holds the full-precision points (k_qhull hook)
   int* ext_facets;                  // ext_max x 3 point ids
   int* ext_nf;
   unsigned long long* stats;
   unsigned long long* prof;          // LQRO_HULL_PROFILE: per-phase cycles
+  // k_qhull (LQRO_FLAG_QHULL_ORDER): per-worker scratch, per-slot normal and
+  // distance, the slots whose facet 0 won (resolved by k_stale)
+  char* qscratch;
+  size_t qstride;
+  double* qnrm;
+  int* qstale;
+  int* qstale_count;
+  int qstale_cap;
 };
 
 // Hull topology and vertex coordinates for k_hull_big (global scratch).
@@ -387,7 +396,10 @@ __device__ __forceinline__ int hull_points(const HullArgs& A, LT& L, const doubl
   if (tid == 0) { L.n = A.ext_pts ? A.ext_n : 0; L.fail = 0; }
   hl_bar();
   if (A.ext_pts)
-    for (int q = tid; q < 3 * A.ext_n; q += blockDim.x) Pr[q] = Pf[q] = A.ext_pts[q];
+    for (int q = tid; q < 3 * A.ext_n; q += blockDim.x) {
+      Pr[q] = A.ext_pts[q];
+      Pf[q] = A.ext_full ? A.ext_pts[3 * A.ext_n + q] : A.ext_pts[q];
+    }
   for (int k0 = 0; k0 < (A.ext_pts ? 0 : A.H); k0 += 128) {
     for (int it = tid; it < 3 * 128; it += blockDim.x) {
       const int k = k0 + it / 3, r = it % 3;

@@ -15,6 +15,15 @@ void launch_hull_big(dim3 grid, hipStream_t s, const HullArgs& A);
 // k_lhull: grid x 4 waves, one inside-hull pair at a time from a local hull
 // around vrel; the pairs it cannot decide go to A.lqueue (for k_hull)
 void launch_lhull(dim3 grid, hipStream_t s, const HullArgs& A);
+// k_qhull (LQRO_FLAG_QHULL_ORDER): grid x 1 wave, one inside-hull pair per
+// wave with Qhull's build order (lqro_qhull.hpp); A.qscratch holds
+// A.block_base + grid workers of qhull_worker_bytes(H*NP) bytes
+void launch_qhull(dim3 grid, hipStream_t s, const HullArgs& A);
+size_t qhull_worker_bytes(int hnp);
+// k_stale: the facet-0 pairs' loop-carried normals, then the carry out
+void launch_stale(hipStream_t s, float* planes, const double* qnrm, const int* list, const int* count, int cap,
+                  const double* x, int X, int npr, int row_begin, int row_stride, double* carry,
+                  lqro_pair_record* recs, long nslots);
 // controlMatrices for n models into out (stride X*X + 12X + 25 doubles):
 // k_synthw (one wave per agent) or, lane = true, k_synth (one agent per lane)
 void launch_synth(int x_dim, bool lane, const lqro_model* d_models, int n, double* d_out);

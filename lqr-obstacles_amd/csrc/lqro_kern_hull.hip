@@ -1,11 +1,12 @@
 // lqro_kern_hull.hip — the hull kernels (k_hull, k_hull_big; lqro_hull.hpp; k_lhull;
-// lqro_lhull.hpp)
+// lqro_lhull.hpp; k_qhull, k_stale: lqro_qhull.hpp)
 // and their launch functions (lqro_kern.hpp).
 #define LQRO_HULL_TU 1
 #include <hip/hip_runtime.h>
 
 #include "lqro_hull.hpp"
 #include "lqro_lhull.hpp"
+#include "lqro_qhull.hpp"
 #include "lqro_kern.hpp"
 
 namespace lqro {
@@ -20,6 +21,24 @@ void launch_hull_big(dim3 grid, hipStream_t s, const HullArgs& A) {
 
 void launch_lhull(dim3 grid, hipStream_t s, const HullArgs& A) {
   hipLaunchKernelGGL(k_lhull, grid, dim3(LH_THREADS), 0, s, A);
+}
+
+__global__ void __launch_bounds__(64) k_qhull(HullArgs A) {
+  __shared__ QhL L;
+  qh_body(A, L);
+}
+
+void launch_qhull(dim3 grid, hipStream_t s, const HullArgs& A) {
+  hipLaunchKernelGGL(k_qhull, grid, dim3(64), 0, s, A);
+}
+
+size_t qhull_worker_bytes(int hnp) { return qh_worker_bytes(hnp); }
+
+void launch_stale(hipStream_t s, float* planes, const double* qnrm, const int* list, const int* count, int cap,
+                  const double* x, int X, int npr, int row_begin, int row_stride, double* carry,
+                  lqro_pair_record* recs, long nslots) {
+  hipLaunchKernelGGL(k_stale, dim3(16), dim3(64), 0, s, planes, qnrm, list, count, cap, x, X, npr, row_begin,
+                     row_stride, carry, recs, nslots);
 }
 
 }  // namespace lqro

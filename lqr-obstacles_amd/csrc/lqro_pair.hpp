@@ -74,6 +74,7 @@ struct PairArgs {
   int hot_cap;
   int hot_only;                       // 1: this launch computes the hot list only
   const int* nbr_list;                // culling on: per row npr (= K) neighbour jj, ascending, -1 = none
+  double* qnrm;                       // LQRO_FLAG_QHULL_ORDER: per slot normal, dist (k_stale reads them)
   // LDS layout, in doubles
   int XP, lds_T, lds_N, lds_S, lds_R, lds_TF, lds_H, lds_wave, wave_doubles;
 };
@@ -696,6 +697,10 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
       float4* dst = reinterpret_cast<float4*>(P.planes + slot * 8);
       dst[0] = make_float4(pl[0], pl[1], pl[2], pl[3]);
       dst[1] = make_float4(pl[4], pl[5], pl[6], pl[7]);
+      if (P.qnrm && flags && !inside) {   // normalVector as run_gjk left it (LQRO:850-852)
+        double4* qd = reinterpret_cast<double4*>(P.qnrm + slot * 4);
+        *qd = make_double4(nrm[0], nrm[1], nrm[2], dist);
+      }
       lds_count(&W.st[0], (unsigned long long)n);
       if (flags) {
         lds_count(&W.st[1], (unsigned long long)go.iters);

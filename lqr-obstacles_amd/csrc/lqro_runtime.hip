@@ -400,6 +400,15 @@ struct lqro_ctx {
   int lds_bytes;
   int stepped;               // a step was enqueued (ev[3] recorded)
   int lhull_prof;            // LQRO_LHULL_PROFILE: k_lhull writes its per-job words
+  // LQRO_FLAG_QHULL_ORDER: k_qhull workers, per-slot normals, facet-0 slots,
+  // the loop-carried normal in [0..2], out [3..5]
+  int qhull_order;
+  int qworkers;
+  size_t qstride;
+  char* d_qscratch;
+  double* d_qnrm;
+  int* d_qstale;
+  double* d_carry;
   PairArgs pa;
 };
 
@@ -462,7 +471,8 @@ void lqro_destroy(lqro_ctx* c) {
   (void)hipSetDevice(c->cfg.device);
   void* ps[] = {c->d_R, c->d_TF, c->d_shash, c->d_T, c->d_NCF, c->d_S, c->d_x, c->d_vgoal, c->d_newv, c->d_A, c->d_B,
                 c->d_L, c->d_E, c->d_planes, c->d_lpscratch, c->d_lpcompact, c->d_recs, c->d_hq, c->d_hcount,
-                c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats, c->d_prof, c->d_rq, c->d_hbig, c->d_hwide, c->d_hbag, c->d_lp4, c->d_hotlist, c->d_hotmark, c->d_nbrlist, c->d_hfbest, c->d_hvpid, c->d_hstack, c->d_lq};
+                c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats, c->d_prof, c->d_rq, c->d_hbig, c->d_hwide, c->d_hbag, c->d_lp4, c->d_hotlist, c->d_hotmark, c->d_nbrlist, c->d_hfbest, c->d_hvpid, c->d_hstack, c->d_lq,
+                c->d_qscratch, c->d_qnrm, c->d_qstale, c->d_carry};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (int k = 0; k < 5; ++k)
@@ -537,6 +547,16 @@ static int ctx_alloc(lqro_ctx* c) {
   HIPCHK(hipMalloc(&c->d_hotlist, sizeof(int) * c->hot_cap));
   HIPCHK(hipMalloc(&c->d_hotmark, slots ? slots : 1));
   HIPCHK(hipMalloc(&c->d_lp4, sizeof(int) * 6 * (size_t)std::max(1, c->nrows)));
+  HIPCHK(hipMalloc(&c->d_carry, sizeof(double) * 6));
+  HIPCHK(hipMemset(c->d_carry, 0, sizeof(double) * 6));
+  if (c->qhull_order) {
+    // k_qhull: QH_WPC one-wave workers per CU, each with its own build scratch
+    c->qworkers = c->n_cu * 4;
+    c->qstride = (qhull_worker_bytes((int)(H * NP)) + 255) & ~(size_t)255;
+    HIPCHK(hipMalloc(&c->d_qscratch, c->qstride * (size_t)c->qworkers));
+    HIPCHK(hipMalloc(&c->d_qnrm, sizeof(double) * 4 * (slots ? slots : 1)));
+    HIPCHK(hipMalloc(&c->d_qstale, sizeof(int) * (slots ? slots : 1)));
+  }
   return LQRO_OK;
 }
 
@@ -561,6 +581,7 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
   memset(c, 0, sizeof *c);
   c->cfg = g;
   c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  c->qhull_order = (g.flags & LQRO_FLAG_QHULL_ORDER) ? 1 : 0;
   {
     // CUs running k_hull workers beside k_pair (the hot-pair hulls); default 3/8
     const char* e = getenv("LQRO_SIDE_HULL_CUS");
@@ -741,6 +762,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   // add up to one workgroup per CU.  Hull jobs the prediction missed are
   // taken by the k_hull after the sweep.
   P.row_counter = c->d_hcount + 4;
+  P.qnrm = c->qhull_order ? c->d_qnrm : nullptr;
   // the context's scratch (queues, counters, plane slots, tables) is reused by
   // every step: a step enqueued on another stream than the last one, or a
   // set_gains on c->stream, must not overlap the step still in flight
@@ -749,6 +771,9 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   HIPCHK(hipMemsetAsync(c->d_hcount, 0, sizeof(int) * 16, s));
   HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * 8, s));
   HIPCHK(hipMemsetAsync(c->d_hq, 0xFF, sizeof(int) * (size_t)c->hull_cap, s));
+  // Qhull order: the normal the last step's last eligible pair left enters this step
+  if (c->qhull_order)
+    HIPCHK(hipMemcpyAsync(c->d_carry, c->d_carry + 3, sizeof(double) * 3, hipMemcpyDeviceToDevice, s));
   P.nbr_list = nullptr;
   if (c->nbr_k > 0) {
     hipLaunchKernelGGL(k_nbr, dim3((unsigned)c->nrows), dim3(64), 0, s, d_x, g.x_dim, g.n_agents, c->rb, c->rs,
@@ -783,8 +808,9 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
     inside_prev = c->h_inside[slot];
   }
   const bool known = inside_prev != ~0ull;
-  int side = c->local_hull ? c->lside_cus : c->side_cus;
-  if (c->local_hull) {
+  const bool lhull = c->local_hull || c->qhull_order;   // k_lhull or k_qhull on the side
+  int side = lhull ? c->lside_cus : c->side_cus;
+  if (lhull) {
     // local hulls: at most ~3.7 inside-hull pairs per side CU (C3: 177 on
     // 48 CUs), widening up to half the CUs as the swarm gets denser
     if (known)
@@ -797,12 +823,12 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   // local hulls: the overlap pays up to ~16 inside-hull pairs per CU of the
   // widest side (1,067 at 22 m: 15.5 vs 18.0 ms plain; 2,496 at 16 m: a tie)
   const long max_inside = c->hot_max_inside >= 0 ? c->hot_max_inside
-                                                  : (c->local_hull ? 16L * std::max(side, c->n_cu / 2) : 4L * side);
+                                                  : (lhull ? 16L * std::max(side, c->n_cu / 2) : 4L * side);
   const bool crowded = known && inside_prev > (unsigned long long)max_inside;
   // with the local hull the side stream is k_pair(hot) -> k_lhull -> k_pair
   // (rows, the same row queue): no LDS-topology condition
   const bool hot = c->hot_on && c->n_cu >= 64 && slots >= 65536 && c->nbr_k <= 0 && !crowded && side >= 1 &&
-                   (c->local_hull || (lds_ok && (size_t)g.horizon * g.n_points <= 16383 && side_waves >= 1));
+                   (lhull || (lds_ok && (size_t)g.horizon * g.n_points <= 16383 && side_waves >= 1));
   const int nwait = hot ? side : 0;
   P.row_split = std::max(1, std::min(16, (2 * c->n_cu + c->nrows - 1) / c->nrows));
   const int units = c->nrows * P.row_split;
@@ -844,9 +870,12 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   Hh.lqueue = c->d_lq; Hh.lcount = c->d_hcount + 11; Hh.ldone = c->d_hcount + 13;
   Hh.lfail = c->d_prof + 32 + 2 * 4096 + 32;
   Hh.ext_pts = nullptr; Hh.ext_n = 0; Hh.ext_max = 0; Hh.ext_facets = nullptr; Hh.ext_nf = nullptr;
+  Hh.ext_full = 0;
   // per-job stamps only when asked for (LQRO_LHULL_PROFILE=1, scripts/lhull_jobs.py);
   // lfail counts hand-over reasons since the context was created
   Hh.ljobs = c->lhull_prof ? c->d_prof + 32 + 2 * 4096 + 48 : nullptr;
+  Hh.qscratch = c->d_qscratch; Hh.qstride = c->qstride; Hh.qnrm = c->d_qnrm;
+  Hh.qstale = c->d_qstale; Hh.qstale_count = c->d_hcount + 15; Hh.qstale_cap = c->hull_cap;
   if (g.x_dim != 16 && g.x_dim != 12) return LQRO_E_ARG;
   // the row launch is submitted before the side stream's work: should the two
   // streams land on one hardware queue (a second context in the process), the
@@ -861,7 +890,16 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
     Ph.hot_only = 1;
     launch_pair(g.x_dim, dim3(nwait), dim3(P.waves * 64), c->lds_bytes, c->side, Ph);
     HIPCHK(hipGetLastError());
-    if (c->local_hull) {
+    if (c->qhull_order) {
+      // the hot pairs' hulls in Qhull's order (k_qhull leaves when the queue
+      // is empty), then the row sweep
+      launch_qhull(dim3(std::min(nwait * 4, c->qworkers)), c->side, Hh);
+      HIPCHK(hipGetLastError());
+      if (nside > 0) {
+        launch_pair(g.x_dim, dim3(nwait), dim3(P.waves * 64), c->lds_bytes, c->side, P);
+        HIPCHK(hipGetLastError());
+      }
+    } else if (c->local_hull) {
       // the hot pairs' local hulls (k_lhull leaves when the queue is empty:
       // later jobs go to the k_lhull after the sweep), then the row sweep
       launch_lhull(dim3(nwait), c->side, Hh);
@@ -890,22 +928,31 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
     HIPCHK(hipStreamWaitEvent(s, c->xev[1], 0));
   }
   HIPCHK(hipEventRecord(c->ev[1], s));
-  if (c->local_hull) {
+  if (c->qhull_order) {
+    // every hull job left, then the facet-0 pairs' loop-carried normals
+    launch_qhull(dim3(c->qworkers), s, Hh);
+    HIPCHK(hipGetLastError());
+    launch_stale(s, c->d_planes, c->d_qnrm, c->d_qstale, c->d_hcount + 15, c->hull_cap, d_x, g.x_dim, npr, c->rb,
+                 c->rs, c->d_carry, c->d_recs, slots);
+    HIPCHK(hipGetLastError());
+  } else if (c->local_hull) {
     // k_lhull takes the queue k_pair filled; k_hull / k_hull_big then take
     // the pairs it handed over (scratch: hull_blocks blocks of 6 H*NP doubles)
     launch_lhull(dim3(c->hull_blocks), s, Hh);
     HIPCHK(hipGetLastError());
     Hh.queue = c->d_lq; Hh.count = c->d_hcount + 11; Hh.next = c->d_hcount + 12;
   }
-  Hh.block_base = nwait;
-  Hh.big_main = lds_ok ? 0 : 1;
-  if (lds_ok) {
-    launch_hull(dim3(c->hull_blocks - nwait), s, Hh);
+  if (!c->qhull_order) {
+    Hh.block_base = nwait;
+    Hh.big_main = lds_ok ? 0 : 1;
+    if (lds_ok) {
+      launch_hull(dim3(c->hull_blocks - nwait), s, Hh);
+      HIPCHK(hipGetLastError());
+    }
+    Hh.block_base = 0;
+    launch_hull_big(dim3(c->hull_big_blocks), s, Hh);
     HIPCHK(hipGetLastError());
   }
-  Hh.block_base = 0;
-  launch_hull_big(dim3(c->hull_big_blocks), s, Hh);
-  HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev[2], s));
   LpArgs La;
   La.npr = npr; La.nrows = c->nrows; La.row_begin = c->rb; La.row_stride = c->rs; La.vmax = g.vmax_lp;
@@ -1152,6 +1199,23 @@ int lqro_calculate_new_v(const float* planes, const int64_t* offsets, int32_t n_
   return rc;
 }
 
+int lqro_set_carry_normal(lqro_ctx* c, const double* n3) {
+  if (!c || !n3) return LQRO_E_ARG;
+  HIPCHK(hipSetDevice(c->cfg.device));
+  HIPCHK(wait_last_step(c));
+  const double v[6] = {n3[0], n3[1], n3[2], n3[0], n3[1], n3[2]};
+  HIPCHK(hipMemcpy(c->d_carry, v, sizeof v, hipMemcpyHostToDevice));
+  return LQRO_OK;
+}
+
+int lqro_get_carry_normal(lqro_ctx* c, double* n3) {
+  if (!c || !n3) return LQRO_E_ARG;
+  HIPCHK(hipSetDevice(c->cfg.device));
+  HIPCHK(wait_last_step(c));
+  HIPCHK(hipMemcpy(n3, c->d_carry + 3, sizeof(double) * 3, hipMemcpyDeviceToHost));
+  return LQRO_OK;
+}
+
 int lqro_get_records(lqro_ctx* c, lqro_pair_record* out, int64_t cap, int64_t* n_out) {
   if (!c || !out) return LQRO_E_ARG;
   if (!c->d_recs) return LQRO_E_STATE;
@@ -1197,12 +1261,15 @@ int lqro_debug_local_hull(lqro_ctx* c, long long* out) {
  * (already %g-rounded, as qconvex reads them; n <= H * NP of the context)
  * with relative velocity vrel.  local = 0: k_hull, its facets (point ids)
  * into facets (max_facets x 3) and their count into *n_facets; local = 1:
- * k_lhull (no facet list; *n_facets = -1 when it handed the points over).
- * rec receives the selected facet, distance and normal (hull_select). */
+ * k_lhull (no facet list; *n_facets = -1 when it handed the points over);
+ * local = 2: k_qhull, Qhull's build order and the reference's selection;
+ * pts then holds the n rounded points followed by the n full-precision ones
+ * (*n_facets = the build's status bits, 0: Qhull's build reproduced).
+ * rec receives the selected facet, distance and normal. */
 int lqro_debug_hull_points(lqro_ctx* c, const double* pts, int32_t n, const double* vrel, int32_t local,
                            int32_t* facets, int32_t max_facets, int32_t* n_facets, lqro_pair_record* rec) {
   if (!c || !pts || !vrel || !n_facets || !rec || n < 4 || (size_t)n > (size_t)c->cfg.horizon * c->cfg.n_points ||
-      (!local && (!facets || max_facets < 1)))
+      (!local && (!facets || max_facets < 1)) || local < 0 || local > 2)
     return LQRO_E_ARG;
   const lqro_config& g = c->cfg;
   HIPCHK(hipSetDevice(g.device));
@@ -1215,11 +1282,17 @@ int lqro_debug_hull_points(lqro_ctx* c, const double* pts, int32_t n, const doub
   lqro_pair_record* d_rec = nullptr;
   float* d_pl = nullptr;
   unsigned long long* d_st = nullptr;
+  char* d_qw = nullptr;
+  double* d_qn = nullptr;
   int rc = LQRO_OK;
-  const int fmax = local ? 1 : max_facets;
-  if (hipMalloc(&d_st, sizeof(unsigned long long) * 8) != hipSuccess ||
+  const int fmax = (local == 1 || !facets) ? 1 : max_facets;
+  const size_t qstride = (qhull_worker_bytes(g.horizon * g.n_points) + 255) & ~(size_t)255;
+  if (local == 2 && (hipMalloc(&d_qw, qstride) != hipSuccess || hipMalloc(&d_qn, sizeof(double) * 8) != hipSuccess))
+    rc = LQRO_E_NOMEM;
+  if (rc != LQRO_OK) {
+  } else if (hipMalloc(&d_st, sizeof(unsigned long long) * 8) != hipSuccess ||
       hipMemset(d_st, 0, sizeof(unsigned long long) * 8) != hipSuccess ||
-      hipMalloc(&d_pts, sizeof(double) * 3 * n) != hipSuccess || hipMalloc(&d_x, sizeof(double) * 2 * X) != hipSuccess ||
+      hipMalloc(&d_pts, sizeof(double) * (local == 2 ? 6 : 3) * n) != hipSuccess || hipMalloc(&d_x, sizeof(double) * 2 * X) != hipSuccess ||
       hipMalloc(&d_q, sizeof(int) * 16) != hipSuccess || hipMalloc(&d_f, sizeof(int) * 3 * fmax) != hipSuccess ||
       hipMalloc(&d_rec, sizeof(lqro_pair_record)) != hipSuccess || hipMalloc(&d_pl, sizeof(float) * 8) != hipSuccess) {
     rc = LQRO_E_NOMEM;
@@ -1229,7 +1302,7 @@ int lqro_debug_hull_points(lqro_ctx* c, const double* pts, int32_t n, const doub
     lqro_pair_record r0;
     memset(&r0, 0, sizeof r0);
     r0.flags = LQRO_REC_INSIDE;
-    if (hipMemcpy(d_pts, pts, sizeof(double) * 3 * n, hipMemcpyHostToDevice) != hipSuccess ||
+    if (hipMemcpy(d_pts, pts, sizeof(double) * (local == 2 ? 6 : 3) * n, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(d_x, xh.data(), sizeof(double) * 2 * X, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(d_q, q0, sizeof q0, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(d_rec, &r0, sizeof r0, hipMemcpyHostToDevice) != hipSuccess) {
@@ -1250,8 +1323,13 @@ int lqro_debug_hull_points(lqro_ctx* c, const double* pts, int32_t n, const doub
       Hh.bigmem = c->d_hbig; Hh.wide = c->d_hwide; Hh.bag = c->d_hbag;
       Hh.stats = d_st; Hh.prof = nullptr;   // the hook never alters the step's statistics
       Hh.lqueue = d_q + 13; Hh.lcount = d_q + 5; Hh.ldone = d_q + 6;
-      Hh.ext_pts = d_pts; Hh.ext_n = n; Hh.ext_max = fmax; Hh.ext_facets = local ? nullptr : d_f; Hh.ext_nf = d_q + 7;
-      if (local) launch_lhull(dim3(1), c->stream, Hh);
+      Hh.ext_pts = d_pts; Hh.ext_n = n; Hh.ext_max = fmax;
+      Hh.ext_facets = (local == 1 || !facets) ? nullptr : d_f; Hh.ext_nf = d_q + 7;
+      Hh.ext_full = local == 2;   // k_qhull: rounded points, then the full-precision ones
+      Hh.qscratch = d_qw; Hh.qstride = qstride; Hh.qnrm = d_qn;
+      Hh.qstale = d_q + 14; Hh.qstale_count = d_q + 9; Hh.qstale_cap = 1;
+      if (local == 2) launch_qhull(dim3(1), c->stream, Hh);
+      else if (local) launch_lhull(dim3(1), c->stream, Hh);
       else launch_hull(dim3(1), c->stream, Hh);
       if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
         rc = LQRO_E_HIP;
@@ -1260,6 +1338,10 @@ int lqro_debug_hull_points(lqro_ctx* c, const double* pts, int32_t n, const doub
         if (hipMemcpy(qh, d_q, sizeof qh, hipMemcpyDeviceToHost) != hipSuccess ||
             hipMemcpy(rec, d_rec, sizeof *rec, hipMemcpyDeviceToHost) != hipSuccess) {
           rc = LQRO_E_HIP;
+        } else if (local == 2) {
+          *n_facets = qh[7];                 // k_qhull's build status
+          if (facets && hipMemcpy(facets, d_f, sizeof(int) * 3 * fmax, hipMemcpyDeviceToHost) != hipSuccess)
+            rc = LQRO_E_HIP;
         } else if (local) {
           *n_facets = qh[5] > 0 ? -1 : 0;   // handed over: the full hull would decide
         } else {
@@ -1271,7 +1353,8 @@ int lqro_debug_hull_points(lqro_ctx* c, const double* pts, int32_t n, const doub
       }
     }
   }
-  for (void* p : {(void*)d_pts, (void*)d_x, (void*)d_q, (void*)d_f, (void*)d_rec, (void*)d_pl, (void*)d_st})
+  for (void* p : {(void*)d_pts, (void*)d_x, (void*)d_q, (void*)d_f, (void*)d_rec, (void*)d_pl, (void*)d_st,
+                  (void*)d_qw, (void*)d_qn})
     if (p) (void)hipFree(p);
   return rc;
 }

@@ -26,7 +26,9 @@ LIB_PATH = os.path.join(_HERE, "liblqro.so")
 
 LQRO_OK = 0
 LQRO_FLAG_RECORDS = 0x1
+LQRO_FLAG_QHULL_ORDER = 0x2   # the reference's own hull rule over Qhull's build order (k_qhull)
 REC_PLANE, REC_INSIDE, REC_BACKUP, REC_HULL, REC_HULLFAIL, REC_LOCAL = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20
+REC_STALE, REC_QHMERGE = 0x40, 0x80
 
 
 class Config(C.Structure):
@@ -74,6 +76,7 @@ EXPORTS = (
     "lqro_version", "lqro_calculate_new_v", "lqro_synthesize_gains_batch",
     "lqro_dynamics_step", "lqro_dynamics_step_device", "lqro_normals", "lqro_set_neighbors",
     "lqro_synthesize_gains_x", "lqro_synthesize_gains_batch_x",
+    "lqro_set_carry_normal", "lqro_get_carry_normal",
 )
 
 NORMALS_PER_AGENT = 22   # LQRO_NORMALS_PER_AGENT: 16 propagate + 6 observation
@@ -119,6 +122,8 @@ def lib() -> C.CDLL:
         L.lqro_dynamics_step_device.argtypes = [vp, i32, i32, i32, C.POINTER(Agents), vp]
         L.lqro_normals.argtypes = [C.POINTER(C.c_uint32), i64, vp]
         L.lqro_set_neighbors.argtypes = [vp, dbl, i32]
+        L.lqro_set_carry_normal.argtypes = [vp, vp]
+        L.lqro_get_carry_normal.argtypes = [vp, vp]
         _lib = L
     return _lib
 
@@ -285,6 +290,37 @@ class Context:
         keys = ("pairs", "planes", "inside", "hull_ok", "hull_fail", "gjk_backups",
                 "sum_n_reach", "sum_gtests")
         return dict(zip(keys, (int(v) for v in s)))
+
+    def carry_normal(self, n=None):
+        """LQRO_FLAG_QHULL_ORDER: get (n=None) the loop-carried normalVector
+        (LQRO:1385) the last step left, or set the one entering the next."""
+        if n is None:
+            out = np.zeros(3)
+            _check(lib().lqro_get_carry_normal(self._h, _p(out)), "lqro_get_carry_normal")
+            return out
+        v = np.ascontiguousarray(n, dtype=np.float64)
+        _check(lib().lqro_set_carry_normal(self._h, _p(v)), "lqro_set_carry_normal")
+
+    def debug_qhull(self, rounded: np.ndarray, full: np.ndarray, vrel, max_facets: int = 0):
+        """Test hook: k_qhull on given points (rounded = qconvex's input, full =
+        the distances' points): (record, build status bits[, facet list in
+        Qhull's order, Fv triples, when max_facets > 0])."""
+        n = rounded.shape[0]
+        pts = np.ascontiguousarray(np.concatenate([rounded.reshape(-1), full.reshape(-1)]), dtype=np.float64)
+        v = np.ascontiguousarray(vrel, dtype=np.float64)
+        rec = PairRecord()
+        nf = C.c_int32()
+        fn = lib().lqro_debug_hull_points
+        fn.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32,
+                       C.POINTER(C.c_int32), C.POINTER(PairRecord)]
+        fl = np.zeros((max(max_facets, 1), 3), np.int32)
+        _check(fn(self._h, _p(pts), n, _p(v), 2, _p(fl) if max_facets else None, max_facets, C.byref(nf),
+                  C.byref(rec)), "lqro_debug_hull_points")
+        r = np.frombuffer(bytes(rec), dtype=RECORD_DTYPE)[0]
+        if max_facets:
+            end = np.nonzero(fl[:, 0] < 0)[0]
+            return r, int(nf.value), fl[: end[0] if len(end) else max_facets]
+        return r, int(nf.value)
 
     def timings(self) -> dict:
         t = np.zeros(4, dtype=np.float32)

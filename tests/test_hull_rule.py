@@ -12,8 +12,11 @@ Pinned here:
     order, stale normal when facet 0 wins): distance within 1e-4 absolute
     (6-significant-digit rounding of the hull input, SURVEY §7 hazard 1)
     on every pair; same normal on every pair whose arg-min facet agrees.
-The rule itself is NOT reproduced: parity of the hull branch's
-half-plane against the reference is "unpinned" beyond these bounds."""
+The canonical rule (the default without LQRO_FLAG_QHULL_ORDER) is a
+DEVIATION, not parity: test_canonical_rule_is_not_parity fails if its newV
+were reported as the reference's.  The reference's own rule — Qhull's build
+order restated (oracle/lqro_qhull.c, k_qhull) — is pinned bit for bit in
+tests/test_qhull_order.py and tests/test_gpu_qhull_order.py."""
 import os
 
 import numpy as np
@@ -72,3 +75,18 @@ def test_reference_rule_live_with_qhull(oracle, lqro_mod, gains):
         dist, nrm, _, _ = reference_rule(pts, x[i, 3:6] - x[j, 3:6])
         assert dist == d["dense_dist_ref"][k]
         assert np.array_equal(nrm, d["dense_normal_ref"][k])
+
+
+def test_canonical_rule_is_not_parity():
+    """The canonical rule's newV (hull_rule.npz) against the reference loop
+    over live Qhull (qhull_order.npz): rows with a hull pair differ beyond
+    1e-5 — the canonical rule must not be reported as reference parity; the
+    Qhull-order rule (LQRO_FLAG_QHULL_ORDER) is."""
+    a = np.load(FIX)
+    b = np.load(os.path.join(GOLDEN, "qhull_order.npz"))
+    for w, need in (("dense", 1), ("c3", 1)):
+        rows = a[f"{w}_rows"]
+        ref = b[f"{w}_newv"][rows]
+        ours = a[f"{w}_newv_ours"]
+        rel = np.abs(ours - ref).max(1) / np.maximum(np.abs(ref).max(1), 1e-30)
+        assert (rel > 1e-5).sum() >= need, w

@@ -1,0 +1,93 @@
+"""The oracle's restatement of Qhull's build (oracle/lqro_qhull.c) and the
+reference's own hull rule over it (orc_hull_branch_ref, LQRObstacles.cpp:
+867-969) — CPU.
+
+qconvex.exe is never run; its stand-in is scipy's bundled Qhull 2019.1
+called exactly like qconvex (tests/golden/qhull_lib.py), which
+reproduces the reference's own fixture (tests/golden/qhull).  Pinned here:
+  * orc_qhull against live Qhull: facet order, every facet's Fv vertex list,
+    every plane bit for bit — on the reference's fixture, random clouds and
+    path hulls;
+  * the same against tests/golden/qhull_order.npz's Qhull output (no live
+    Qhull needed);
+  * the oracle's step with the reference's rule (planes read back as
+    printed) against the golden reference loop, bit for bit: every inside
+    pair's facet, distance and carried normal, every row's newV."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+QO = os.path.join(GOLDEN, "qhull_order.npz")
+
+
+def _live():
+    sys.path.insert(0, GOLDEN)
+    try:
+        import qhull_lib
+        qhull_lib._lib()
+        return qhull_lib
+    except Exception as e:   # scipy's Qhull internals not loadable here
+        pytest.skip(f"live Qhull unavailable: {e}")
+
+
+def _same_as_qhull(oracle, q, pts):
+    st, fv, pl, _ = oracle.qhull(pts)
+    assert st == 0
+    planes, qfv, _, _ = q.qconvex(pts)
+    assert [list(f) for f in qfv] == fv.tolist()
+    from scipy.spatial import ConvexHull
+    eq = ConvexHull(pts).equations          # the same build's unprinted planes
+    assert np.array_equal(eq, pl)
+    assert (np.abs(planes - pl) <= 1e-15 * np.maximum(1.0, np.abs(pl))).all()   # as printed (%.16g)
+
+
+def test_oracle_qhull_on_reference_fixture(oracle):
+    q = _live()
+    _same_as_qhull(oracle, q, q.read_pointlist(os.path.join(GOLDEN, "qhull", "pointList.txt")))
+
+
+def test_oracle_qhull_random_clouds(oracle):
+    q = _live()
+    rng = np.random.default_rng(3)
+    for t in range(12):
+        n = int(rng.integers(8, 400))
+        pts = np.round(rng.normal(size=(n, 3)) * 10 ** rng.uniform(-1, 2), int(rng.integers(2, 6)))
+        _same_as_qhull(oracle, q, pts)
+
+
+def test_oracle_qhull_golden_hulls(oracle):
+    """The six dense-swarm hulls stored with Qhull's output: no live Qhull."""
+    d = np.load(QO)
+    for k in range(6):
+        st, fv, pl, _ = oracle.qhull(d[f"inject{k}_rounded"])
+        assert st == 0
+        assert np.array_equal(fv, d[f"inject{k}_fv"])
+        g = d[f"inject{k}_planes"]
+        assert (np.abs(pl[:, :4] - g) <= 1e-15 * np.maximum(1.0, np.abs(g))).all()
+
+
+@pytest.mark.parametrize("case", ["dense", "c2"])
+def test_oracle_reference_rule_step(oracle, lqro_mod, gains, case):
+    d = np.load(QO)
+    N, H, box, seed = (32, 45, 3.0, 11) if case == "dense" else (64, 50, None, None)
+    x, vg = lqro_mod.synthetic_swarm(N, box=box, seed=seed) if box else lqro_mod.synthetic_swarm(N)
+    T, NCF = oracle.tables(gains["A"], gains["B"], gains["L"], gains["E"], H)
+    oracle.set_hull_rule(1, round16=True)
+    oracle.carry_normal(np.zeros(3))
+    try:
+        v, r = oracle.step(T, NCF, oracle.sphere(100), x, vg, threads=4)
+    finally:
+        oracle.set_hull_rule(0)
+    g = d[f"{case}_pairs"]
+    ins = r[(r["flags"] & 2) != 0]
+    assert np.array_equal(ins["i"], g["i"]) and np.array_equal(ins["j"], g["j"])
+    assert np.array_equal(ins["facet"], g["fv"])
+    assert np.array_equal(ins["dist"].view(np.uint64), g["dist"].view(np.uint64))
+    assert np.array_equal(ins["normal"].view(np.uint64), g["normal"].view(np.uint64))
+    assert np.array_equal((ins["flags"] & 0x40) != 0, g["stale"] != 0)
+    assert np.array_equal(v.view(np.uint64), d[f"{case}_newv"].view(np.uint64))
+    assert np.array_equal(oracle.carry_normal(), d[f"{case}_carry"])
