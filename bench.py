@@ -93,46 +93,107 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(x, vg, gains, seconds_target=10.0):
+def usable_cores() -> tuple:
+    """Cores this process can run on: its CPU affinity, capped by the cgroup
+    CPU quota when one is set (the GPU box gives each GPU a share of a large
+    host); (cores, affinity count, quota or None)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    return (min(aff, quota) if quota else aff), aff, quota
+
+
+def cpu_baseline(x, vg, gains, hull_rule="qhull", seconds_target=10.0):
     """The reference-faithful CPU restatement (oracle/, orc_step_faithful_mt:
-    the reference's per-pair findFG recursion, LQRO:1401-1406, and its two
-    GJK runs per outside pair, LQRO:1410/1414; calibrated against the
-    reference's own code compiled in the build container) on the
-    host cores: rows of the same C3 step, on 1 core and on all the cores this
-    box gives the process (16), each for ~seconds_target."""
+    the reference's per-pair findFG recursion, LQRO:1401-1406, its two GJK
+    runs per outside pair, LQRO:1410/1414, and — hull_rule "qhull" — Qhull's
+    own build for the inside-hull pairs, oracle/lqro_qhull.c, as qconvex
+    computes them; calibrated against the reference's own code compiled in
+    the build container) on the host cores, BASELINE.md §3:
+    C3 rows on 1 core and on every usable core (~seconds_target each, the
+    hull branch's time and inside-hull pairs reported apart), C1 and C2 whole
+    steps, C4 and C5 extrapolated from measured per-pair rates (labelled)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle  # test infrastructure, used here only as the timed CPU baseline
+    import lqro
 
-    cores = max(1, min(int(os.environ.get("LQRO_CPU_THREADS", "16")), os.cpu_count() or 1))
+    cores, aff, quota = usable_cores()
+    pyoracle.set_hull_rule(1 if hull_rule == "qhull" else 0)
     S = pyoracle.sphere(N_POINTS)
+
+    def timed(xx, vv, g, H, rows, threads, per_agent=False):
+        pyoracle.hull_time(reset=True)
+        t0 = time.perf_counter()
+        pyoracle.step_faithful(g["A"], g["B"], g["L"], g["E"], pyoracle.sphere(N_POINTS), xx, vv, H,
+                               rows=rows, threads=threads, records=False, per_agent=per_agent)
+        dt = time.perf_counter() - t0
+        hs, hc = pyoracle.hull_time(reset=True)
+        return dt, hs, hc
 
     def rate(threads, row0):
         # calibrate on one row per thread, then scale the sample to the target
-        t0 = time.perf_counter()
-        pyoracle.step_faithful(gains["A"], gains["B"], gains["L"], gains["E"], S, x, vg, HORIZON,
-                               rows=(row0, row0 + threads), threads=threads, records=False)
-        dt = time.perf_counter() - t0
+        dt, _, _ = timed(x, vg, gains, HORIZON, (row0, row0 + threads), threads)
         more = int(max(0, min(N_AGENTS - row0 - threads, (seconds_target - dt) / max(dt, 1e-9) * threads)))
         more = (more // threads) * threads
-        rows, secs = threads, dt
+        rows, secs, hs, hc = threads, dt, 0.0, 0
         if more > 0:
-            t0 = time.perf_counter()
-            pyoracle.step_faithful(gains["A"], gains["B"], gains["L"], gains["E"], S, x, vg, HORIZON,
-                                   rows=(row0 + threads, row0 + threads + more), threads=threads,
-                                   records=False)
-            rows, secs = more, time.perf_counter() - t0
-        return rows * (N_AGENTS - 1) / secs, rows
+            secs, hs, hc = timed(x, vg, gains, HORIZON, (row0 + threads, row0 + threads + more), threads)
+            rows = more
+        return rows * (N_AGENTS - 1) / secs, rows, secs, hs, hc
 
-    one, rows1 = rate(1, 0)
-    allc, rows_all = rate(cores, 64)
+    one, rows1, _, _, _ = rate(1, 0)
+    allc, rows_all, secs_all, hsec, hcnt = rate(cores, 64)
+    small = {}
+    for name, N, H in (("c1", 4, 50), ("c2", 64, 50)):
+        xx, vv = lqro.synthetic_swarm(N)
+        dt, _, hc = timed(xx, vv, gains, H, (0, N), min(cores, N))
+        small[name] = {"agents": N, "horizon": H, "pairs": N * (N - 1), "ms_per_step": dt * 1e3,
+                       "evals_per_s": N * (N - 1) / dt, "inside_hull_pairs": hc, "threads": min(cores, N),
+                       "kind": "measured"}
+    # C5: 12-D reduced model, per-agent gains, H = 200 — a sample of rows, extrapolated
+    N5 = 16384
+    x5, v5 = lqro.synthetic_swarm(N5, x_dim=12)
+    ms = [pyoracle.synthesize(pyoracle.Model(*[getattr(m, f) for f, _ in pyoracle.Model._fields_]), x_dim=12)
+          for m in lqro.perturbed_models(64)]
+    g0 = pyoracle.synthesize(x_dim=12)
+    g5 = dict(A=g0["A"], B=g0["B"], L=np.repeat(np.array([m["L"] for m in ms]), N5 // 64, axis=0),
+              E=np.repeat(np.array([m["E"] for m in ms]), N5 // 64, axis=0))
+    dt5, _, hc5 = timed(x5, v5, g5, 200, (0, cores), cores, per_agent=True)
+    r5 = cores * (N5 - 1) / dt5
+    pairs4, pairs5 = 4096 * 4095, N5 * (N5 - 1)
+    small["c4"] = {"agents": 4096, "horizon": 100, "pairs": pairs4, "ms_per_step": pairs4 / allc * 1e3,
+                   "kind": "extrapolated from the C3 per-pair rate on all cores"}
+    small["c5"] = {"agents": N5, "horizon": 200, "x_dim": 12, "pairs": pairs5, "ms_per_step": pairs5 / r5 * 1e3,
+                   "sample": f"{cores} rows x {N5 - 1} pairs in {dt5:.1f} s ({hc5} inside-hull pairs)",
+                   "kind": "extrapolated from a sampled per-pair rate on all cores"}
+    pyoracle.set_hull_rule(0)
     return {"value": allc, "unit": "agent-pair evals/s", "cores": cores, "kind": "port",
-            "mode": "reference-faithful (per-pair findFG, GJK twice per outside pair; bit-identical results)",
+            "mode": "reference-faithful (per-pair findFG, GJK twice per outside pair, " +
+                    ("Qhull's build for inside-hull pairs" if hull_rule == "qhull" else "canonical hull rule") +
+                    "; bit-identical results to the GPU path's rule)",
             "cores_1": one, "cores_all": allc, "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
+            "cpu_affinity": aff, "cgroup_cpu_quota": quota,
+            "c3_hull_seconds_all_cores": hsec, "c3_hull_fraction": hsec / max(secs_all * cores, 1e-9),
+            "c3_sample_inside_hull_pairs": hcnt,
+            "configs": small,
             "sample": f"C3 step rows: {rows1} rows on 1 core, {rows_all} rows on {cores} threads "
                       f"({N_AGENTS - 1} pairs per row)"}
 
 
-def closed_loop(lqro, torch, dev, x, vg, gains, reps, world=1, dist=None, rank=0, mode="block"):
+def hull_flags(lqro, rule: str) -> int:
+    """qhull: the reference's own inside-hull rule over Qhull's build order
+    (LQRO_FLAG_QHULL_ORDER, k_qhull: results equal the reference loop over
+    Qhull); canonical: this build's faster canonical facet rule (a measured
+    deviation)."""
+    return lqro.LQRO_FLAG_QHULL_ORDER if rule == "qhull" else 0
+
+
+def closed_loop(lqro, torch, dev, x, vg, gains, reps, world=1, dist=None, rank=0, mode="block", flags=0):
     """The whole control step on the GPU, measured after the timed steps:
     lqro.DeviceLoop — the pair step, then the agent loop LQRO:1437-1446
     (k_dynw: findU, propagate, kalmanFilter1/2, findVGoal) on this rank's
@@ -142,7 +203,7 @@ def closed_loop(lqro, torch, dev, x, vg, gains, reps, world=1, dist=None, rank=0
     buffers start from the bench's swarm, so the roofline probe after it sees
     the timed steps' inputs."""
     loop = lqro.DeviceLoop(x, vg, dict(gains, l=np.zeros(4)), HORIZON, N_POINTS,
-                           rank=rank, world=world, dist=dist, device=dev, rows=mode)
+                           rank=rank, world=world, dist=dist, device=dev, rows=mode, flags=flags)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     it_ms, its, dms = [], [], []
     for _ in range(reps):
@@ -167,7 +228,7 @@ def closed_loop(lqro, torch, dev, x, vg, gains, reps, world=1, dist=None, rank=0
                     "dynamics_plus_gather_ms from events on the launch stream"}
 
 
-def config_runs(lqro, torch, dev, local, world, rank, dist, steps, mode="block"):
+def config_runs(lqro, torch, dev, local, world, rank, dist, steps, mode="block", flags=0):
     """BASELINE configs 4 and 5 beside the headline (never in `value`):
     strong scaling — the whole swarm's rows sharded over the ranks, the
     per-step exchange as in the headline; max over ranks of the time for
@@ -184,7 +245,7 @@ def config_runs(lqro, torch, dev, local, world, rank, dist, steps, mode="block")
             gains, per_agent = dict(A=g0["A"], B=g0["B"], L=g["L"], E=g["E"]), True
         else:
             gains, per_agent = lqro.synthesize_gains(), False
-        ctx = lqro.Context(lqro.config(N, H, N_POINTS, x_dim=X, device=local, **sh))
+        ctx = lqro.Context(lqro.config(N, H, N_POINTS, x_dim=X, device=local, flags=flags, **sh))
         ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"], per_agent=per_agent)
         d_x = torch.from_numpy(x).to(dev)
         d_vg = torch.from_numpy(vg).to(dev)
@@ -232,6 +293,8 @@ def main():
     ap.add_argument("--no-configs", action="store_true", help="skip the C4 / C5 strong-scaling runs")
     ap.add_argument("--rows", choices=("block", "cyclic"), default=os.environ.get("LQRO_ROWS", "block"),
                     help="row sharding over ranks: contiguous blocks or cyclic (row_stride = world)")
+    ap.add_argument("--hull-rule", choices=("qhull", "canonical"), default=os.environ.get("LQRO_HULL_RULE", "qhull"),
+                    help="inside-hull rule: the reference's (Qhull's build order, default) or the canonical one")
     args = ap.parse_args()
 
     import torch
@@ -262,7 +325,8 @@ def main():
     rows = len(lqro.shard_row_ids(N, rank, world, args.rows))
     x, vg = lqro.synthetic_swarm(N)
     gains = lqro.synthesize_gains()
-    ctx = lqro.Context(lqro.config(N, HORIZON, N_POINTS, device=local, **sh))
+    flags = hull_flags(lqro, args.hull_rule)
+    ctx = lqro.Context(lqro.config(N, HORIZON, N_POINTS, device=local, flags=flags, **sh))
     ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
     d_x = torch.from_numpy(x).to(dev)
     d_vg = torch.from_numpy(vg).to(dev)
@@ -313,7 +377,7 @@ def main():
     # the closed loop runs before the probe creates a second context (whose
     # stream can share a hardware queue with this context's side stream)
     ctx.close()   # one context at a time: a second one's streams can share hardware queues
-    closed = closed_loop(lqro, torch, dev, x, vg, gains, min(args.steps, 5), world, dist, rank, args.rows)
+    closed = closed_loop(lqro, torch, dev, x, vg, gains, min(args.steps, 5), world, dist, rank, args.rows, flags)
     pk_ms = sweep_ms
     probe = "sweep (k_prio + k_pair launches + overlapped side hull), timed steps"
     if not args.no_roofline_probe:
@@ -349,7 +413,8 @@ def main():
         "config": {
             "workload": (f"C3: 1024 quadrotors" if N == N_AGENTS else f"{N} quadrotors (C3 pairs per GPU)") +
                         ", horizon 100, 100 points/ellipsoid, 16-D state; "
-                        "reference-exact fp64 pair sweep+GJK+hull+half-plane, fp32 LP",
+                        "reference-exact fp64 pair sweep+GJK+hull+half-plane, fp32 LP"
+                        + ("" if args.hull_rule == "qhull" else " (canonical hull rule)"),
             "n_agents": N, "horizon": HORIZON, "n_points": N_POINTS, "x_dim": X_DIM,
             "pairs_per_step": pairs_step,
             "parallelism": f"rows sharded ({args.rows}) over {world} rank(s)" +
@@ -379,11 +444,14 @@ def main():
         "closed_loop": closed,
         "inside_hull_pairs_per_step": st["inside"],
         "hull_failures": st["hull_fail"],
+        "hull_rule": ("reference: Qhull's facet order and first Fv vertex, strict <, loop-carried normal "
+                      "(LQRO:925-968; k_qhull, LQRO_FLAG_QHULL_ORDER)" if args.hull_rule == "qhull" else
+                      "canonical (a measured deviation from the reference's rule, DESIGN §5.1)"),
     }
     if not args.no_configs:
-        out["configs"] = config_runs(lqro, torch, dev, local, world, rank, dist, 2, args.rows)
+        out["configs"] = config_runs(lqro, torch, dev, local, world, rank, dist, 2, args.rows, flags)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb = cpu_baseline(x, vg, gains)
+        cb = cpu_baseline(x, vg, gains, args.hull_rule)
         out["cpu_baseline"] = cb
         out["gpu_over_cpu"] = value / cb["value"]
     if rank == 0:

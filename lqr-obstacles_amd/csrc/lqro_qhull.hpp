@@ -149,7 +149,13 @@ struct QhS {
   double MAXabs_coord, MAXsumcoord, MAXwidth, NEARzero[3];
   double DISTround, MINvisible, MAXcoplanar, MINoutside, MINdenom, MINdenom_2, max_outside;
   double interior[3];
+  unsigned long long tph[12];   // LQRO_QHULL_PROFILE: cycles per phase
 };
+#ifdef LQRO_QHULL_PROFILE
+#define QHT(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); S.tph[k] += t_ - tq_; tq_ = t_; } while (0)
+#else
+#define QHT(k) do {} while (0)
+#endif
 
 // ---- the facet list (poly_r.c: qh_appendfacet, qh_removefacet, qh_prependfacet) ----
 __device__ __forceinline__ int qh_prev(const QhW& W, int f) { return W.flink[2 * f]; }
@@ -710,6 +716,10 @@ __device__ inline double qh_detsimplex(const QhS& S, const double* Pr, const int
 
 // qh_qhull on W.Pr[0..n): S holds the final facet list
 __device__ inline void qh_build(const QhW& W, QhS& S, QhL& L, int n, int lane) {
+#ifdef LQRO_QHULL_PROFILE
+  unsigned long long tq_ = __builtin_amdgcn_s_memtime();
+  for (int k = 0; k < 12; k++) S.tph[k] = 0;
+#endif
   S.status = 0;
   S.nalloc = 1;   // slot 0: the tail sentinel
   S.nfree = 0;
@@ -946,6 +956,7 @@ __device__ inline void qh_build(const QhW& W, QhS& S, QhL& L, int n, int lane) {
       hl_sync();
     }
   }
+  QHT(0);
   if (S.status & (QHS_INPUT | QHS_TOPOLOGY | QHS_CAPACITY)) return;
   // qh_furthestnext
   {
@@ -983,6 +994,7 @@ __device__ inline void qh_build(const QhW& W, QhS& S, QhL& L, int n, int lane) {
       W.fseg[2 * facet + 1] = cnt - 1;
       break;
     }
+    QHT(1);
     if (furthest < 0) break;
     const double* apexp = W.Pr + 3 * (size_t)furthest;
     // qh_findhorizon
@@ -1017,6 +1029,7 @@ __device__ inline void qh_build(const QhW& W, QhS& S, QhL& L, int n, int lane) {
         hl_sync();
       }
     }
+    QHT(2);
     // qh_makenewfacets -> qh_makenew_simplicial
     S.newfacet_list = S.facet_tail;
     const int apex = S.nv++;
@@ -1055,6 +1068,7 @@ __device__ inline void qh_build(const QhW& W, QhS& S, QhL& L, int n, int lane) {
       W.frep[vis] = newfacet;
     }
     hl_sync();
+    QHT(3);
     // qh_matchnewfacets (nb[1] shares {apex, v2}, nb[2] shares {apex, v1}),
     // qh_makenewplanes, qh_checkzero: one new facet per lane
     int ls = 0;
@@ -1095,6 +1109,7 @@ __device__ inline void qh_build(const QhW& W, QhS& S, QhL& L, int n, int lane) {
       }
     }
     S.status |= qh_wave_or(ls);
+    QHT(4);
     if (S.status & (QHS_TOPOLOGY | QHS_CAPACITY)) return;
     // qh_partitionvisible: the visible facets' outside sets, in order
     {
@@ -1118,9 +1133,12 @@ __device__ inline void qh_build(const QhW& W, QhS& S, QhL& L, int n, int lane) {
       S.notsharp = 0;
       S.nmov = 0;
       const int sharp = qh_sharpnewfacets(W, S, L);
+      QHT(5);
       if (np2) {
         qh_locate_seq(W, S, L, np2, sharp, false, lane);
+        QHT(6);
         qh_emit_seq(W, S, L, np2, lane);
+        QHT(7);
       }
     }
     // deleted vertices (a visible facet's vertex on no new facet) close to a
@@ -1143,6 +1161,7 @@ __device__ inline void qh_build(const QhW& W, QhS& S, QhL& L, int n, int lane) {
       }
       S.status |= qh_wave_or(lsd);
     }
+    QHT(8);
     if (S.status & QHS_CAPACITY) return;
     S.findbestnew = 0;
     S.notsharp = 0;
@@ -1164,6 +1183,7 @@ __device__ inline void qh_build(const QhW& W, QhS& S, QhL& L, int n, int lane) {
     S.nnew = 0;
     S.nmov = 0;
     hl_sync();
+    QHT(9);
   }
 }
 
@@ -1279,13 +1299,25 @@ __device__ inline void qh_body(const HullArgs& A, QhL& L) {
     const double vrel[3] = {xi[3] - xj[3], xi[4] - xj[4], xi[5] - xj[5]};
     const int n = hull_points(A, L, Ti, Ni, xi, xj, vrel, W.Pr, W.Pf);
     QhS S;
+#ifdef LQRO_QHULL_PROFILE
+    for (int k = 0; k < 12; k++) S.tph[k] = 0;
+#endif
     S.status = 0;
     S.nalloc = 1;
     S.facet_list = S.facet_tail = 0;
     if (L.fail || n < 4) S.status = QHS_INPUT;
     else qh_build(W, S, L, n, lane);
     hl_sync();
+#ifdef LQRO_QHULL_PROFILE
+    unsigned long long tq_ = __builtin_amdgcn_s_memtime();
+#endif
     qh_select(A, W, S, lane, xi, vrel, slot);
+#ifdef LQRO_QHULL_PROFILE
+    S.tph[10] = __builtin_amdgcn_s_memtime() - tq_;
+    S.tph[11] = 1;
+    if (A.prof && lane == 0)
+      for (int k = 0; k < 12; k++) atomicAdd(&A.prof[k], S.tph[k]);
+#endif
     if (A.ext_nf && lane == 0) *A.ext_nf = S.status;   // test hook: the build's status bits
     if (A.ext_facets && lane == 0) {                     // test hook: the facet list, Fv order
       int k = 0;

@@ -654,7 +654,8 @@ class DeviceLoop:
 
     def __init__(self, x0, vgoal0, gains: dict, horizon: int, n_points: int = 100, *,
                  p_goal=None, rank: int = 0, world: int = 1, dist=None, device=None,
-                 model: Model | None = None, seed: int = 1, stream=None, rows: str = "block"):
+                 model: Model | None = None, seed: int = 1, stream=None, rows: str = "block",
+                 flags: int = 0):
         import torch
         self.torch = torch
         self.dev = torch.device("cuda", torch.cuda.current_device()) if device is None else device
@@ -669,7 +670,7 @@ class DeviceLoop:
         self.model = model or default_model()
         self.seed = seed
         f64 = dict(dtype=torch.float64, device=self.dev)
-        self.ctx = Context(config(n, horizon, n_points, device=self.dev.index, **sh))
+        self.ctx = Context(config(n, horizon, n_points, device=self.dev.index, flags=flags, **sh))
         self.ids_h = ids
         self.ids = torch.from_numpy(ids.astype(np.int64)).to(self.dev)
         self.ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])

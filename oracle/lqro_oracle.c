@@ -14,6 +14,7 @@
 #include <float.h>
 #include <math.h>
 #include <pthread.h>
+#include <time.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -1049,6 +1050,17 @@ int orc_hull_branch(int n, const double* pts_full, const double vrel[3], double*
  * facets; the hull was built on merge-free).  Returns the facet count or
  * <= 0 on failure. */
 static int g_hull_rule = 0, g_round16 = 0;
+static long long g_hull_ns = 0, g_hull_count = 0;
+
+/* time spent in the hull branch and inside-hull pairs since the last reset */
+void orc_hull_time(double* seconds, long long* count, int reset) {
+  *seconds = 1e-9 * (double)__atomic_load_n(&g_hull_ns, __ATOMIC_RELAXED);
+  *count = __atomic_load_n(&g_hull_count, __ATOMIC_RELAXED);
+  if (reset) {
+    __atomic_store_n(&g_hull_ns, 0LL, __ATOMIC_RELAXED);
+    __atomic_store_n(&g_hull_count, 0LL, __ATOMIC_RELAXED);
+  }
+}
 static double g_carry[3] = {0.0, 0.0, 0.0};
 
 void orc_set_hull_rule(int rule, int round16) { g_hull_rule = rule; g_round16 = round16; }
@@ -1158,6 +1170,8 @@ int orc_pair(int X, int H, int NP, int min_reach, double vmax_reach, const doubl
     rec->gjk_iters = iters; rec->simplex_n = sn;
     for (int k = 0; k < 3; k++) { rec->wpt_vrel[k] = w1[k]; rec->wpt_hull[k] = w2[k]; }
     int stale = 0;
+    struct timespec h0, h1;
+    if (inside) clock_gettime(CLOCK_MONOTONIC, &h0);
     if (inside && g_hull_rule) {                                  /* LQRO:1411-1412 */
       int qst = 0;
       int nf = orc_hull_branch_ref(n, pts, vrel, &distance, normal, rec->facet, &stale, &qst);
@@ -1172,6 +1186,12 @@ int orc_pair(int X, int H, int NP, int min_reach, double vmax_reach, const doubl
       int nf = orc_hull_branch(n, pts, vrel, &distance, normal, rec->facet);
       rec->n_facets = nf;
       if (nf > 0) rec->flags |= LQRO_REC_HULL; else rec->flags |= LQRO_REC_HULLFAIL;
+    }
+    if (inside) {   /* the hull branch's cost (the CPU baseline reports it apart) */
+      clock_gettime(CLOCK_MONOTONIC, &h1);
+      __atomic_add_fetch(&g_hull_ns, (long long)(h1.tv_sec - h0.tv_sec) * 1000000000LL + (h1.tv_nsec - h0.tv_nsec),
+                         __ATOMIC_RELAXED);
+      __atomic_add_fetch(&g_hull_count, 1LL, __ATOMIC_RELAXED);
     }
     rec->dist = distance;
     for (int k = 0; k < 3; k++) rec->normal[k] = normal[k];

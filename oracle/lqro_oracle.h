@@ -128,6 +128,9 @@ int  orc_hull_branch_ref(int n, const double* pts_full, const double vrel[3], do
  * order from the carry (set/get: the value entering / leaving a step's
  * rows).  round16: planes read back as qconvex prints them (%.16g). */
 void orc_set_hull_rule(int rule, int round16);
+/* thread-time spent in the hull branch and inside-hull pairs (all threads)
+ * since the last reset */
+void orc_hull_time(double* seconds, long long* count, int reset);
 void orc_set_carry_normal(const double* n);
 void orc_get_carry_normal(double* n);
 

@@ -351,3 +351,13 @@ def hull_branch_ref(points_full: np.ndarray, vrel):
     k = o.orc_hull_branch_ref(points_full.shape[0], _p(points_full), _p(v), _p(d), _p(nrm), _p(fac),
                               _p(st[:1]), _p(st[1:]))
     return k, float(d[0]), (None if st[0] else nrm), fac, int(st[1])
+
+
+def hull_time(reset: bool = True):
+    """(thread-seconds in the hull branch, inside-hull pairs) since the last reset."""
+    o = lib()
+    o.orc_hull_time.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+    sec = C.c_double()
+    cnt = C.c_longlong()
+    o.orc_hull_time(C.byref(sec), C.byref(cnt), int(reset))
+    return sec.value, cnt.value

@@ -1,0 +1,31 @@
+"""k_qhull phase profile of one C3 step in Qhull order (needs
+liblqro_qprof.so: scripts/build_variant.sh liblqro_qprof.so -DLQRO_QHULL_PROFILE):
+cycles per phase summed over the step's hulls (s_memtime, 100 MHz)."""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+sys.path[:0] = [os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "lqr-obstacles_amd")]
+import lqro  # noqa: E402
+
+lqro.LIB_PATH = os.path.join(os.path.dirname(lqro.LIB_PATH), os.environ.get("LQRO_LIB", "liblqro_qprof.so"))
+L = lqro.lib()
+box = float(sys.argv[1]) if len(sys.argv) > 1 else None
+N, H, NP = 1024, 100, 100
+x, vg = lqro.synthetic_swarm(N, box=box, seed=7) if box else lqro.synthetic_swarm(N)
+g = lqro.synthesize_gains()
+c = lqro.Context(lqro.config(N, H, NP, flags=lqro.LQRO_FLAG_QHULL_ORDER))
+c.set_gains(g["A"], g["B"], g["L"], g["E"])
+c.step(x, vg)
+print(c.timings(), c.stats())
+out = np.zeros(32 + 2 * 4096 + 32, np.uint64)
+L.lqro_debug_hull_profile(c._h, out.ctypes.data_as(C.c_void_p))
+names = ["init+partitionall", "nextfurthest", "findhorizon", "makenew", "match+planes+checkzero",
+         "gather", "locate", "emit", "delvertex", "delete+reset", "select", "jobs"]
+jobs = max(int(out[11]), 1)
+tot = sum(int(out[k]) for k in range(11))
+for k, nm in enumerate(names[:11]):
+    print(f"{nm:24s} {int(out[k]) / jobs / 100:10.1f} us/hull  {100 * int(out[k]) / max(tot, 1):5.1f}%")
+print("hulls", jobs, "total us/hull", tot / jobs / 100)

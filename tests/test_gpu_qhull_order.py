@@ -108,7 +108,11 @@ def test_qhull_order_vs_reference_loop(lqro_mod, oracle, gains, case):
         [(int(b["i"]), int(b["j"]), int(b["n_reach"]), -int(b["n_facets"]) - 1) for b in bad]
     assert np.array_equal(ins["i"], g["i"]) and np.array_equal(ins["j"], g["j"])
     assert np.array_equal(ins["facet"], g["fv"])
-    assert np.array_equal(ins["n_facets"], g["n_facets"])
+    # a hull Qhull resolves by merging facets is built merge-free (REC_QHMERGE):
+    # its facet count may differ; its selection must not
+    merged = (ins["flags"] & lqro_mod.REC_QHMERGE) != 0
+    assert merged.sum() <= max(2, len(ins) // 200)
+    assert np.array_equal(ins["n_facets"][~merged], g["n_facets"][~merged])
     assert np.array_equal((ins["flags"] & lqro_mod.REC_STALE) != 0, g["stale"] != 0)
     np.testing.assert_allclose(ins["dist"], g["dist"], rtol=1e-12, atol=1e-15)
     np.testing.assert_allclose(ins["normal"], g["normal"], rtol=0, atol=1e-14)
