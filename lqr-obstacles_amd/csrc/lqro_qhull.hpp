@@ -1281,13 +1281,14 @@ __device__ inline void qh_select(const HullArgs& A, const QhW& W, const QhS& S, 
   hl_sync();
 }
 
-// one inside-hull pair per wave, persistent over the hull queue
-__device__ inline void qh_body(const HullArgs& A, QhL& L) {
+// one inside-hull pair per wave, persistent over the hull queue (k_qhull_big:
+// the retry queue k_qhull's caps fill, or the main queue under LQRO_QHULL_BIG)
+__device__ inline void qh_body(const HullArgs& A, QhL& L, bool retryq) {
   const int lane = threadIdx.x & 63;
   const int HNP = A.H * A.NP;
   const QhW W = qh_worker(A.qscratch + (size_t)(A.block_base + blockIdx.x) * A.qstride, HNP);
   for (;;) {
-    const int slot = hull_take_job(A, L, false);
+    const int slot = hull_take_job(A, L, retryq);
     if (slot < 0) break;
     const int lrow = slot / A.npr, jj = A.nbr_list ? A.nbr_list[slot] : slot % A.npr;
     const int i = A.row_begin + lrow * A.row_stride;

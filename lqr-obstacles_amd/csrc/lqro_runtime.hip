@@ -403,6 +403,7 @@ struct lqro_ctx {
   // LQRO_FLAG_QHULL_ORDER: k_qhull workers, per-slot normals, facet-0 slots,
   // the loop-carried normal in [0..2], out [3..5]
   int qhull_order;
+  int qhull_big;            // LQRO_QHULL_BIG=1: every pair in k_qhull_big (A/B runs)
   int qworkers;
   size_t qstride;
   char* d_qscratch;
@@ -582,6 +583,10 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
   c->cfg = g;
   c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   c->qhull_order = (g.flags & LQRO_FLAG_QHULL_ORDER) ? 1 : 0;
+  {
+    const char* qb = getenv("LQRO_QHULL_BIG");
+    c->qhull_big = qb ? atoi(qb) != 0 : 0;
+  }
   {
     // CUs running k_hull workers beside k_pair (the hot-pair hulls); default 3/8
     const char* e = getenv("LQRO_SIDE_HULL_CUS");
@@ -893,8 +898,10 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
     if (c->qhull_order) {
       // the hot pairs' hulls in Qhull's order (k_qhull leaves when the queue
       // is empty), then the row sweep
-      launch_qhull(dim3(std::min(nwait * 4, c->qworkers)), c->side, Hh);
-      HIPCHK(hipGetLastError());
+      if (!c->qhull_big) {
+        launch_qhull(dim3(std::min(nwait * 4, c->qworkers)), c->side, Hh);
+        HIPCHK(hipGetLastError());
+      }
       if (nside > 0) {
         launch_pair(g.x_dim, dim3(nwait), dim3(P.waves * 64), c->lds_bytes, c->side, P);
         HIPCHK(hipGetLastError());
@@ -929,9 +936,16 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   }
   HIPCHK(hipEventRecord(c->ev[1], s));
   if (c->qhull_order) {
-    // every hull job left, then the facet-0 pairs' loop-carried normals
-    launch_qhull(dim3(c->qworkers), s, Hh);
+    // every hull job left, the ones beyond k_qhull's caps, then the facet-0
+    // pairs' loop-carried normals
+    if (!c->qhull_big) {
+      launch_qhull(dim3(c->qworkers), s, Hh);
+      HIPCHK(hipGetLastError());
+    }
+    Hh.big_main = c->qhull_big;
+    launch_qhull_big(dim3(c->qworkers), s, Hh);
     HIPCHK(hipGetLastError());
+    Hh.big_main = 0;
     launch_stale(s, c->d_planes, c->d_qnrm, c->d_qstale, c->d_hcount + 15, c->hull_cap, d_x, g.x_dim, npr, c->rb,
                  c->rs, c->d_carry, c->d_recs, slots);
     HIPCHK(hipGetLastError());
@@ -1328,7 +1342,11 @@ int lqro_debug_hull_points(lqro_ctx* c, const double* pts, int32_t n, const doub
       Hh.ext_full = local == 2;   // k_qhull: rounded points, then the full-precision ones
       Hh.qscratch = d_qw; Hh.qstride = qstride; Hh.qnrm = d_qn;
       Hh.qstale = d_q + 14; Hh.qstale_count = d_q + 9; Hh.qstale_cap = 1;
-      if (local == 2) launch_qhull(dim3(1), c->stream, Hh);
+      if (local == 2) {
+        Hh.big_main = c->qhull_big;
+        if (!c->qhull_big) launch_qhull(dim3(1), c->stream, Hh);
+        launch_qhull_big(dim3(1), c->stream, Hh);
+      }
       else if (local) launch_lhull(dim3(1), c->stream, Hh);
       else launch_hull(dim3(1), c->stream, Hh);
       if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
