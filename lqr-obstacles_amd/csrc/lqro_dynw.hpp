@@ -108,7 +108,7 @@ __device__ __forceinline__ void pivot(const double* m, const int* rp, const int*
 // X = P^-1 Q by full pivoting with the reference's final reshuffle
 // (operator%, MAT:370-442, = synth::solve): m (P) and x (Q) in LDS, both
 // overwritten; the solution is left in x.
-__device__ void solve(double* m, double* x, int* ip, int lane) {
+__device__ __forceinline__ void solve(double* m, double* x, int* ip, int lane) {
   int* rp = ip;
   int* cp = ip + 16;
   int* irp = ip + 32;
@@ -169,7 +169,7 @@ __device__ void solve(double* m, double* x, int* ip, int lane) {
 
 // out = exp(q) (MAT:763-790, = synth::expm<16>); q and out may not alias the
 // six work matrices E0..E5
-__device__ void expm(const double* q, double* out, double* w, int lane) {
+__device__ __forceinline__ void expm(const double* q, double* out, double* w, int lane) {
   const double b0 = 1729728e1, b1 = 864864e1, b2 = 199584e1, b3 = 2772e2, b4 = 252e2, b5 = 1512e0,
                b6 = 56e0, b7 = 1e0, lim = 9.504178996162932e-1;
   double* A = w + oE0;
@@ -404,10 +404,21 @@ __device__ void kalman_update(const Quad& q, Mat<kX, 1>& x, Mat<3, 3>& R, const 
     S[lane] = acc + Nz.e[lane];
   }
   sync();
-  Mat<kZ, kZ> Sm;
+  // S^-1 (the pseudo-inverse of synth::inverse: data-dependent indexing, so
+  // private memory): one lane computes it, LDS hands it to the others
+  double* Sinv = w + oE1 + 224;   // 6x6
+  if (lane == 0) {
+    Mat<kZ, kZ> Sm;
 #pragma unroll
-  for (int k = 0; k < 36; ++k) Sm.e[k] = S[k];
-  const Mat<kZ, kZ> Si = synth::inverse(Sm);
+    for (int k = 0; k < 36; ++k) Sm.e[k] = S[k];
+    const Mat<kZ, kZ> Si0 = synth::inverse(Sm);
+#pragma unroll
+    for (int k = 0; k < 36; ++k) Sinv[k] = Si0.e[k];
+  }
+  sync();
+  Mat<kZ, kZ> Si;
+#pragma unroll
+  for (int k = 0; k < 36; ++k) Si.e[k] = Sinv[k];
   for (int e = lane; e < 96; e += 64) {   // K = P H^T S^-1
     const int i = e / 6, j = e % 6;
     double acc = 0.0;
@@ -478,7 +489,20 @@ __device__ void agent_step(const dyn::AgentParams& a, double* x_, double* rot_, 
     sync();
     dyn::reset_rot(x, R);
   }
-  const Mat<kZ, 1> z = dyn::sample_gaussian(dyn::observe(xtrue), Nz, a.normals + kX);
+  // the observation draw (6x6 Jacobi: data-dependent indexing) on one lane
+  Mat<kZ, 1> z;
+  {
+    double* zb = w + oT1;
+    if (lane == 0) {
+      const Mat<kZ, 1> z0 = dyn::sample_gaussian(dyn::observe(xtrue), Nz, a.normals + kX);
+#pragma unroll
+      for (int k = 0; k < kZ; ++k) zb[k] = z0.e[k];
+    }
+    sync();
+#pragma unroll
+    for (int k = 0; k < kZ; ++k) z.e[k] = zb[k];
+    sync();
+  }
   kalman_update(q, x, R, z, Nz, w, lane);                                             // kalmanFilter2
   const Vec3 vn = dyn::control_position(x, R, get<3, 1>(a.p_goal), ug, get<kV, kX>(a.Lh),
                                         get<kV, kV>(a.Eh));                           // findVGoal

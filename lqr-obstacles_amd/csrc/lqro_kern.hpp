@@ -16,7 +16,7 @@ void launch_hull_big(dim3 grid, hipStream_t s, const HullArgs& A);
 // around vrel; the pairs it cannot decide go to A.lqueue (for k_hull)
 void launch_lhull(dim3 grid, hipStream_t s, const HullArgs& A);
 // k_qhull (LQRO_FLAG_QHULL_ORDER): grid x 1 wave, one inside-hull pair per
-// wave with Qhull's build order (lqro_qhull2.hpp); A.qscratch holds
+// wave (one wave per CU: its LDS) with Qhull's build order (lqro_qhull3.hpp); A.qscratch holds
 // A.block_base + grid workers of qhull_worker_bytes(H*NP) bytes.  Pairs beyond
 // its per-insertion caps go to A.rqueue for k_qhull_big (lqro_qhull.hpp),
 // which with A.big_main takes the main queue instead.

@@ -1,5 +1,5 @@
 // lqro_kern_hull.hip — the hull kernels (k_hull, k_hull_big; lqro_hull.hpp; k_lhull;
-// lqro_lhull.hpp; k_qhull: lqro_qhull2.hpp; k_qhull_big, k_stale: lqro_qhull.hpp)
+// lqro_lhull.hpp; k_qhull: lqro_qhull3.hpp; k_qhull_big, k_stale: lqro_qhull.hpp)
 // and their launch functions (lqro_kern.hpp).
 #define LQRO_HULL_TU 1
 #include <hip/hip_runtime.h>
@@ -7,7 +7,7 @@
 #include "lqro_hull.hpp"
 #include "lqro_lhull.hpp"
 #include "lqro_qhull.hpp"
-#include "lqro_qhull2.hpp"
+#include "lqro_qhull3.hpp"
 #include "lqro_kern.hpp"
 
 namespace lqro {
@@ -25,8 +25,8 @@ void launch_lhull(dim3 grid, hipStream_t s, const HullArgs& A) {
 }
 
 __global__ void __launch_bounds__(64) k_qhull(HullArgs A) {
-  __shared__ Q2L L;
-  q2_body(A, L);
+  __shared__ Q3L L;
+  q3_body(A, L);
 }
 
 // the pairs k_qhull's caps turned away (the retry queue), or with
@@ -45,7 +45,7 @@ void launch_qhull_big(dim3 grid, hipStream_t s, const HullArgs& A) {
 }
 
 size_t qhull_worker_bytes(int hnp) {
-  const size_t a = qh_worker_bytes(hnp), b = q2_worker_bytes(hnp);
+  const size_t a = qh_worker_bytes(hnp), b = q3_worker_bytes(hnp);
   return a > b ? a : b;
 }
 

@@ -1,0 +1,1574 @@
+// lqro_qhull3.hpp — k_qhull: Qhull 2019.1's build (the restatement in
+// lqro_qhull.hpp, which stays as k_qhull_big, the fallback for builds beyond
+// this kernel's caps), laid out for the CU instead of transcribed.  The build
+// is one long chain of dependent steps per pair, so its speed is the latency
+// of each step; this layout keeps that chain in LDS:
+//
+//  * the facets' hot fields — plane, neighbours, flags, list key, outside-set
+//    count and furthest point — live in LDS for the first Q3_FL facet slots
+//    (a whole CU's LDS, one wave per CU); slots beyond spill to a 64-byte
+//    global record.  Vertices (as point ids), outside-set offsets and
+//    furthest distances, touched once per insertion in parallel, stay in
+//    global memory;
+//  * no linked facet list: Qhull's list order is the order facets were
+//    appended (qh_appendfacet), so each facet carries a key — its position in
+//    that order (0 for the facet qh_furthestnext prepends, a fresh key when
+//    qh_partitionpoint moves an old facet behind the new ones) — and
+//    qh_nextfurthest's cursor is a queue of the facets that received outside
+//    points, in key order, validated 64 entries at a time;
+//  * qh_findhorizon's breadth-first search runs a level at a time over the
+//    lanes (same visiting order: a facet is taken by the first visible facet
+//    in queue order that reaches it); qh_makenew_simplicial runs one horizon
+//    ridge per lane (creation order = the ridges in visible-list order); new
+//    facets reuse the visible facets' slots;
+//  * outside-set entries carry their point's coordinates (one load per
+//    point re-partitioned), and the partition sequence is read straight from
+//    the visible facets' sets;
+//  * the point search keeps Qhull's sequential semantics as lqro_qhull.hpp
+//    does (order-dependent state changes applied at their point, the rest of
+//    the sequence re-evaluated), and counts each point into its destination
+//    as soon as its result is final.
+#pragma once
+#include "lqro_qhull.hpp"
+
+namespace lqro {
+
+#define Q3_NEWCAP 128     // new facets of one insertion (more: the pair goes to k_qhull_big)
+#define Q3_VISCAP 128     // visible facets of one insertion
+#define Q3_MOVCAP 16      // old facets moved / receiving points in one partition
+#define Q3_HZCAP 24       // facets one point's horizon walk visits
+#define Q3_COPCAP 8       // its coplanar facet set
+#define Q3_FSTK 512       // free facet slots kept for reuse (more are left unused)
+#define Q3_ND (Q3_NEWCAP + Q3_MOVCAP)
+#ifndef Q3_FL
+#define Q3_FL 2752        // facet slots with their hot fields in LDS
+#endif
+
+struct Q3G {              // a facet slot >= Q3_FL, 64 B
+  double pl[4];
+  int nb[3];
+  int fa;                 // QF_* | new-facet index << 8
+  unsigned key;
+  unsigned cc;            // outside set: count | furthest point << 16
+  int pad[2];
+};
+
+struct Q3V {              // a facet's vertices: rounded points and point ids, Fv order (newest first)
+  double p[9];
+  double pad;
+  int id[4];
+};
+
+struct Q3W {
+  double* Pr;             // 3 HNP rounded points (qconvex's input)
+  double* Pf;             // 3 HNP full precision
+  Q3G* G;                 // FC - Q3_FL spilled slots
+  Q3V* vv;                // FC: vertices
+  double* ncoord;         // 9 Q3_NEWCAP: the new facets' ridge and opposite points (a cone too wide for registers)
+  HullPt* pseq;           // HNP: the partition sequence's points (a sequence longer than 64)
+  int* soff;              // FC: outside set offset in sb
+  double* fdist;          // FC: furthest outside distance
+  HullPt* sb;             // SB outside-set entries (point, coordinates)
+  int* pq;                // HNP: qh_partitionall's remainder
+  int* pdst;              // HNP: partition sequence -> destination index
+  double* pdd;            // HNP: its distance
+  int* fq;                // QC: facets that received points, key order
+  unsigned* fqk;          // QC: their key then
+  int FC, SB, HNP, QC;
+};
+
+__host__ __device__ inline size_t q3_align(size_t b) { return (b + 255) & ~(size_t)255; }
+
+__host__ __device__ inline size_t q3_worker_bytes(int HNP) {
+  const size_t FC = 2 * (size_t)HNP + Q3_NEWCAP + 16, SB = (size_t)QH_SBMULT * HNP, QC = 4 * (size_t)HNP + 64;
+  const size_t NG = FC > Q3_FL ? FC - Q3_FL : 1;
+  return q3_align(24 * (size_t)HNP) * 2 + q3_align(64 * NG) + q3_align(96 * FC) + q3_align(72 * Q3_NEWCAP) +
+         q3_align(32 * (size_t)HNP) + q3_align(4 * FC) +
+         q3_align(8 * FC) + q3_align(32 * SB) + q3_align(4 * (size_t)HNP) * 2 + q3_align(8 * (size_t)HNP) +
+         q3_align(4 * QC) * 2;
+}
+
+__device__ inline Q3W q3_worker(char* base, int HNP) {
+  Q3W W;
+  W.HNP = HNP;
+  W.FC = 2 * HNP + Q3_NEWCAP + 16;
+  W.SB = QH_SBMULT * HNP;
+  W.QC = 4 * HNP + 64;
+  const size_t NG = W.FC > Q3_FL ? W.FC - Q3_FL : 1;
+  char* p = base;
+  auto take = [&](size_t bytes) { char* r = p; p += q3_align(bytes); return r; };
+  W.Pr = reinterpret_cast<double*>(take(24 * (size_t)HNP));
+  W.Pf = reinterpret_cast<double*>(take(24 * (size_t)HNP));
+  W.G = reinterpret_cast<Q3G*>(take(64 * NG));
+  W.vv = reinterpret_cast<Q3V*>(take(96 * (size_t)W.FC));
+  W.ncoord = reinterpret_cast<double*>(take(72 * (size_t)Q3_NEWCAP));
+  W.pseq = reinterpret_cast<HullPt*>(take(32 * (size_t)HNP));
+  W.soff = reinterpret_cast<int*>(take(4 * (size_t)W.FC));
+  W.fdist = reinterpret_cast<double*>(take(8 * (size_t)W.FC));
+  W.sb = reinterpret_cast<HullPt*>(take(32 * (size_t)W.SB));
+  W.pq = reinterpret_cast<int*>(take(4 * (size_t)HNP));
+  W.pdst = reinterpret_cast<int*>(take(4 * (size_t)HNP));
+  W.pdd = reinterpret_cast<double*>(take(8 * (size_t)HNP));
+  W.fq = reinterpret_cast<int*>(take(4 * (size_t)W.QC));
+  W.fqk = reinterpret_cast<unsigned*>(take(4 * (size_t)W.QC));
+  return W;
+}
+
+// the wave's LDS (one wave per CU)
+struct Q3L {
+  // hull_points / hull_take_job interface
+  int n, fail, job, slot;
+  double eps;
+  double tr[3 * 128];
+  double rk[1];
+  int ri[1];
+  int scan[1];
+  // facet slots < Q3_FL
+  double4 pl[Q3_FL];
+  ushort4 tp[Q3_FL];                 // neighbours, QF_* | new-facet index << 8
+  unsigned key[Q3_FL];
+  unsigned cc[Q3_FL];
+  unsigned short fstk[Q3_FSTK];
+  // the insertion: visible facets (qh_findhorizon order) and what their
+  // slots held (the cone reuses them)
+  int visf[Q3_VISCAP];
+  int vsoff[Q3_VISCAP], vscnt[Q3_VISCAP], vinc[Q3_VISCAP];
+  int vvert[3 * Q3_VISCAP];
+  int repl[Q3_VISCAP];               // qh_getreplacement: new-facet index
+  // the new facets, creation order: slot, vertices (point ids), horizon
+  // facet and its ridge index, neighbours nb1/nb2 (new
+  // indices), plane, flags
+  int nslot[Q3_NEWCAP];
+  int nv[3 * Q3_NEWCAP];
+  int nhz[Q3_NEWCAP], nhskip[Q3_NEWCAP];
+  int nn1[Q3_NEWCAP], nn2[Q3_NEWCAP];
+  double npl[4 * Q3_NEWCAP];
+  int nflag[Q3_NEWCAP];
+  int movf[Q3_MOVCAP];               // old facets moved behind the new ones (scan order)
+  int oldf[Q3_MOVCAP];               // old facets receiving points (destinations Q3_NEWCAP + k)
+  // partition destinations: new facets 0.., old facets Q3_NEWCAP + k
+  int dfac[Q3_ND], dcnt[Q3_ND], doff[Q3_ND], dchamp[Q3_ND], pcnt[Q3_ND];
+  double dmax[Q3_ND];
+  double dchp[3 * Q3_ND];            // the furthest point's coordinates
+  int cop[Q3_COPCAP * 64];           // the horizon walks' coplanar facet sets, [k][lane]
+};
+static_assert(sizeof(Q3L) <= 160 * 1024, "k_qhull's LDS exceeds a CU");
+
+struct Q3S {
+  int nalloc, nfs, sbtop, status, qhead, qtail;
+  unsigned keyc;
+  int nnew, nvis, nmov, nold;
+  int findbestnew, notsharp;
+  double MAXabs_coord, MAXsumcoord, MAXwidth, NEARzero[3];
+  double DISTround, MINvisible, MAXcoplanar, MINoutside, MINdenom, MINdenom_2, max_outside;
+  double interior[3];
+  unsigned long long tph[24];
+  unsigned long long tq;         // LQRO_QHULL_PROFILE: the last stamp
+};
+
+#ifdef LQRO_QHULL_PROFILE
+// (every outstanding load and store drained first: a phase is charged its own memory waits)
+#define Q3T(k) do { __builtin_amdgcn_s_waitcnt(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); S.tph[k] += t_ - S.tq; S.tq = t_; } while (0)
+#else
+#define Q3T(k) do {} while (0)
+#endif
+
+// ---- facet fields: LDS below Q3_FL, the global record beyond ----
+__device__ __forceinline__ void q3_get(const Q3W& W, const Q3L& L, int f, double* q, int* nb, int* fa) {
+  if (f < Q3_FL) {
+    const double4 p = L.pl[f];
+    const ushort4 t = L.tp[f];
+    q[0] = p.x; q[1] = p.y; q[2] = p.z; q[3] = p.w;
+    nb[0] = t.x; nb[1] = t.y; nb[2] = t.z; *fa = t.w;
+  } else {
+    const Q3G& g = W.G[f - Q3_FL];
+    q[0] = g.pl[0]; q[1] = g.pl[1]; q[2] = g.pl[2]; q[3] = g.pl[3];
+    nb[0] = g.nb[0]; nb[1] = g.nb[1]; nb[2] = g.nb[2]; *fa = g.fa;
+  }
+}
+__device__ __forceinline__ void q3_pl(const Q3W& W, const Q3L& L, int f, double* q) {
+  if (f < Q3_FL) {
+    const double4 p = L.pl[f];
+    q[0] = p.x; q[1] = p.y; q[2] = p.z; q[3] = p.w;
+  } else {
+    const Q3G& g = W.G[f - Q3_FL];
+    q[0] = g.pl[0]; q[1] = g.pl[1]; q[2] = g.pl[2]; q[3] = g.pl[3];
+  }
+}
+__device__ __forceinline__ int q3_nb(const Q3W& W, const Q3L& L, int f, int k) {
+  if (f < Q3_FL) return reinterpret_cast<const unsigned short*>(&L.tp[f])[k];
+  return W.G[f - Q3_FL].nb[k];
+}
+__device__ __forceinline__ void q3_tp(const Q3W& W, const Q3L& L, int f, int* nb, int* fa) {
+  if (f < Q3_FL) {
+    const ushort4 t = L.tp[f];
+    nb[0] = t.x; nb[1] = t.y; nb[2] = t.z; *fa = t.w;
+  } else {
+    const Q3G& g = W.G[f - Q3_FL];
+    nb[0] = g.nb[0]; nb[1] = g.nb[1]; nb[2] = g.nb[2]; *fa = g.fa;
+  }
+}
+__device__ __forceinline__ int q3_fa(const Q3W& W, const Q3L& L, int f) {
+  return f < Q3_FL ? (int)L.tp[f].w : W.G[f - Q3_FL].fa;
+}
+__device__ __forceinline__ unsigned q3_key(const Q3W& W, const Q3L& L, int f) {
+  return f < Q3_FL ? L.key[f] : W.G[f - Q3_FL].key;
+}
+__device__ __forceinline__ unsigned q3_cc(const Q3W& W, const Q3L& L, int f) {
+  return f < Q3_FL ? L.cc[f] : W.G[f - Q3_FL].cc;
+}
+__device__ __forceinline__ void q3_set_fa(const Q3W& W, Q3L& L, int f, int fa) {
+  if (f < Q3_FL) L.tp[f].w = (unsigned short)fa;
+  else W.G[f - Q3_FL].fa = fa;
+}
+__device__ __forceinline__ void q3_set_nb(const Q3W& W, Q3L& L, int f, int k, int v) {
+  if (f < Q3_FL) reinterpret_cast<unsigned short*>(&L.tp[f])[k] = (unsigned short)v;
+  else W.G[f - Q3_FL].nb[k] = v;
+}
+__device__ __forceinline__ void q3_set_key(const Q3W& W, Q3L& L, int f, unsigned k) {
+  if (f < Q3_FL) L.key[f] = k;
+  else W.G[f - Q3_FL].key = k;
+}
+__device__ __forceinline__ void q3_set_cc(const Q3W& W, Q3L& L, int f, unsigned c) {
+  if (f < Q3_FL) L.cc[f] = c;
+  else W.G[f - Q3_FL].cc = c;
+}
+__device__ __forceinline__ void q3_set_facet(const Q3W& W, Q3L& L, int f, const double* q, int nb0, int nb1, int nb2,
+                                             int fa) {
+  if (f < Q3_FL) {
+    L.pl[f] = make_double4(q[0], q[1], q[2], q[3]);
+    L.tp[f] = make_ushort4((unsigned short)nb0, (unsigned short)nb1, (unsigned short)nb2, (unsigned short)fa);
+  } else {
+    Q3G& g = W.G[f - Q3_FL];
+    *reinterpret_cast<double4*>(g.pl) = make_double4(q[0], q[1], q[2], q[3]);
+    *reinterpret_cast<int4*>(g.nb) = make_int4(nb0, nb1, nb2, fa);
+  }
+}
+
+// the adapter that lets the verified plane code (qh_plane_gauss, qh_detsimplex) read Q3S
+__device__ __forceinline__ QhS q3_as_qhs(const Q3S& S) {
+  QhS T;
+  T.DISTround = S.DISTround;
+  T.MINdenom = S.MINdenom;
+  T.MINdenom_2 = S.MINdenom_2;
+  for (int k = 0; k < 3; k++) T.NEARzero[k] = S.NEARzero[k];
+  return T;
+}
+
+// qh_setfacetplane (qh_sethyperplane_det, nearly singular -> _gauss) for a
+// facet with vertex points r0, r1, r2 in its vertex order; qh_checkflipped
+__device__ inline void q3_plane(const Q3S& S, int& status, const double* r0, const double* r1, const double* r2,
+                                int top, double* q, bool* flipped) {
+  const double dX10 = r1[0] - r0[0], dY10 = r1[1] - r0[1], dZ10 = r1[2] - r0[2];
+  const double dX20 = r2[0] - r0[0], dY20 = r2[1] - r0[1], dZ20 = r2[2] - r0[2];
+  double n[3];
+  n[0] = QH_DET2(dY20, dZ20, dY10, dZ10);
+  n[1] = QH_DET2(dX10, dZ10, dX20, dZ20);
+  n[2] = QH_DET2(dX20, dY20, dX10, dY10);
+  double norm = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+  if (norm > S.MINdenom) {
+    if (!top) norm = -norm;
+    n[0] /= norm;
+    n[1] /= norm;
+    n[2] /= norm;
+  } else {
+    status |= QHS_SINGULAR;
+  }
+  double off = -(r0[0] * n[0] + r0[1] * n[1] + r0[2] * n[2]);
+  const double d2 = off + (r2[0] * n[0] + r2[1] * n[1] + r2[2] * n[2]);
+  const double d1 = off + (r1[0] * n[0] + r1[1] * n[1] + r1[2] * n[2]);
+  if (d2 > S.DISTround || d2 < -S.DISTround || d1 > S.DISTround || d1 < -S.DISTround) {
+    const QhS T = q3_as_qhs(S);
+    qh_plane_gauss(T, status, r0, r1, r2, top, n, &off);
+  }
+  q[0] = n[0]; q[1] = n[1]; q[2] = n[2]; q[3] = off;
+  const double di = off + S.interior[0] * n[0] + S.interior[1] * n[1] + S.interior[2] * n[2];
+  *flipped = di >= -S.DISTround;
+}
+
+__device__ __forceinline__ double q3_distq(const double* q, const double* p) {   // qh_distplane
+  return q[3] + p[0] * q[0] + p[1] * q[1] + p[2] * q[2];
+}
+
+// inclusive wave scan (sum) with DPP row shifts and row broadcasts
+__device__ __forceinline__ int q3_scan_add(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);   // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);   // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);   // row_bcast:15 -> rows 1, 3
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);   // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
+// ---- point location, per lane (geom_r.c) ----
+// qh_findbesthorizon; a step reads the three neighbours together, and the
+// one the walk moves to brings its own neighbours along
+__device__ inline int q3_findbesthorizon(const Q3W& W, const Q3S& S, const Q3L& L, const double* p, int startfacet,
+                                         double* bestdist, int& lstatus) {
+  int bestfacet = startfacet;
+  const double searchdist = S.max_outside + 2 * S.DISTround + fmax(S.MINvisible, S.MAXcoplanar);
+  double minsearch = *bestdist - searchdist;
+  int vis[Q3_HZCAP];
+  int nvis = 0;
+  int* cop = const_cast<int*>(L.cop) + (threadIdx.x & 63);   // qh.coplanarfacetset
+  int ncop = 0;
+  int nextfacet = -1, nextnb[3] = {-1, -1, -1};
+  vis[nvis++] = startfacet;
+  int cur[3] = {q3_nb(W, L, startfacet, 0), q3_nb(W, L, startfacet, 1), q3_nb(W, L, startfacet, 2)};
+  for (;;) {
+    double q[3][4];
+    int fl[3], nn[3][3];
+    for (int k = 0; k < 3; k++) q3_get(W, L, cur[k], q[k], nn[k], &fl[k]);
+    for (int k = 0; k < 3; k++) {
+      const int nb = cur[k];
+      bool seen = false;
+      for (int t = 0; t < nvis; t++) seen |= vis[t] == nb;
+      if (seen) continue;
+      if (nvis == Q3_HZCAP) { lstatus |= QHS_CAPACITY; return bestfacet; }
+      vis[nvis++] = nb;
+      if (!(fl[k] & QF_FLIPPED)) {
+        const double dist = q3_distq(q[k], p);
+        if (dist > *bestdist) {
+          minsearch = dist - searchdist;
+          if (dist > *bestdist + searchdist) ncop = 0;
+          bestfacet = nb;
+          *bestdist = dist;
+        } else if (dist < minsearch) {
+          continue;
+        }
+      }
+      if (nextfacet >= 0) {
+        if (ncop == Q3_COPCAP) { lstatus |= QHS_CAPACITY; return bestfacet; }
+        cop[64 * ncop++] = nextfacet;
+      }
+      nextfacet = nb;
+      nextnb[0] = nn[k][0]; nextnb[1] = nn[k][1]; nextnb[2] = nn[k][2];
+    }
+    if (nextfacet >= 0) {
+      nextfacet = -1;
+      cur[0] = nextnb[0]; cur[1] = nextnb[1]; cur[2] = nextnb[2];
+      continue;
+    }
+    if (!ncop) break;
+    int facet;
+    if (ncop == 1) { facet = cop[0]; ncop = 0; }
+    else facet = cop[64 * --ncop];
+    cur[0] = q3_nb(W, L, facet, 0); cur[1] = q3_nb(W, L, facet, 1); cur[2] = q3_nb(W, L, facet, 2);
+  }
+  return bestfacet;
+}
+
+// qh_findbestnew over the scan list: the new facets from index s0, the moved
+// old facets, the new facets before s0 (the facet list from startfacet to
+// its end, then from qh.newfacet_list)
+__device__ inline int q3_findbestnew(const Q3W& W, const Q3S& S, const Q3L& L, const double* p, int s0,
+                                     double* dist, int bestoutside, int* isoutside, int& lstatus) {
+  double bestdist = -DBL_MAX / 2;
+  int bestfacet = -1;
+  const double distoutside = fmax(2 * S.MINoutside, S.max_outside);    // qh_DISToutside
+  *isoutside = 1;
+  const int total = S.nnew + S.nmov;
+  for (int t = 0; t < total; t++) {
+    int f, fl;
+    double q[4];
+    if (t < S.nnew - s0 || t >= S.nnew - s0 + S.nmov) {
+      const int u = t < S.nnew - s0 ? s0 + t : t - (S.nnew - s0) - S.nmov;
+      f = L.nslot[u];
+      for (int k = 0; k < 4; k++) q[k] = L.npl[4 * u + k];
+      fl = L.nflag[u];
+    } else {
+      f = L.movf[t - (S.nnew - s0)];
+      q3_pl(W, L, f, q);
+      fl = q3_fa(W, L, f);
+    }
+    if (fl & QF_FLIPPED) continue;
+    const double d = q3_distq(q, p);
+    if (d > bestdist) {
+      bestfacet = f;
+      if (!bestoutside && d >= distoutside) { *dist = d; return bestfacet; }
+      bestdist = d;
+    }
+  }
+  bestfacet = q3_findbesthorizon(W, S, L, p, bestfacet >= 0 ? bestfacet : L.nslot[s0], &bestdist, lstatus);
+  *dist = bestdist;
+  if (bestdist < S.MINoutside) *isoutside = 0;
+  return bestfacet;
+}
+
+// qh_sharpnewfacets: a new facet's normal in another quadrant than the first's
+__device__ inline int q3_sharpnewfacets(const Q3S& S, const Q3L& L, int lane) {
+  if (S.nnew == 0) return 0;
+  const bool q0 = L.npl[0] > 0, q1 = L.npl[1] > 0, q2 = L.npl[2] > 0;
+  bool diff = false;
+  for (int t = lane; t < S.nnew; t += 64) {
+    const double* n = L.npl + 4 * t;
+    diff |= (n[0] > 0) != q0 || (n[1] > 0) != q1 || (n[2] > 0) != q2;
+  }
+  return __ballot(diff) != 0ull;
+}
+
+// One partitioned point under the state (S.findbestnew, S.notsharp): its
+// facet and distance, and whether it changes the state (lqro_qhull.hpp
+// qh_locate).  s0: the start facet's new-facet index; sharp = 2:
+// qh_findbestnew(bestoutside) for a deleted vertex.
+__device__ inline int q3_locate(const Q3W& W, const Q3S& S, const Q3L& L, const double* p, int s0, int sharp,
+                                double* bestdist_out, int* isoutside, int* trigger, int& lstatus) {
+  *trigger = 0;
+  if (sharp == 2) return q3_findbestnew(W, S, L, p, s0, bestdist_out, 1, isoutside, lstatus);
+  if (S.findbestnew) return q3_findbestnew(W, S, L, p, s0, bestdist_out, 0, isoutside, lstatus);
+  // qh_findbest(point, startfacet, bestoutside 0, isnewfacets 1, noupper 0):
+  // the new facets only, their neighbours nb1 / nb2 (nb0 is the horizon facet)
+  double bestdist = -DBL_MAX / 2;
+  int bestu = -1;
+  *isoutside = 1;
+  unsigned long long m0 = 0ull, m1 = 0ull;   // new facets visited (index < Q3_NEWCAP = 128)
+  if (!(L.nflag[s0] & QF_FLIPPED)) {
+    const double d = q3_distq(L.npl + 4 * s0, p);
+    if (d >= S.MINoutside) { *bestdist_out = d; return L.nslot[s0]; }
+    bestdist = d;
+    bestu = s0;
+  }
+  if (s0 < 64) m0 |= 1ull << s0; else m1 |= 1ull << (s0 - 64);
+  int u = s0;
+  while (u >= 0) {
+    int nxt = -1;
+    const int cand[2] = {L.nn1[u], L.nn2[u]};
+    for (int k = 0; k < 2; k++) {
+      const int c = cand[k];
+      const bool was = c < 64 ? (m0 >> c) & 1ull : (m1 >> (c - 64)) & 1ull;
+      if (was) continue;
+      if (c < 64) m0 |= 1ull << c; else m1 |= 1ull << (c - 64);
+      if (!(L.nflag[c] & QF_FLIPPED)) {
+        const double d = q3_distq(L.npl + 4 * c, p);
+        if (d > bestdist) {
+          if (d >= S.MINoutside) { *bestdist_out = d; return L.nslot[c]; }
+          bestu = c;
+          bestdist = d;
+          nxt = c;
+          break;
+        }
+      }
+    }
+    u = nxt;
+  }
+  if (bestu < 0) return q3_findbestnew(W, S, L, p, 0, bestdist_out, 0, isoutside, lstatus);
+  if (!S.notsharp && bestdist < -S.DISTround) {
+    *trigger = 1;
+    if (sharp) return q3_findbestnew(W, S, L, p, bestu, bestdist_out, 0, isoutside, lstatus);
+  }
+  const int bf = q3_findbesthorizon(W, S, L, p, L.nslot[bestu], &bestdist, lstatus);
+  *bestdist_out = bestdist;
+  if (bestdist < S.MINoutside) *isoutside = 0;
+  return bf;
+}
+
+__device__ __forceinline__ bool q3_in_movf(const Q3S& S, const Q3L& L, int f) {
+  for (int t = 0; t < S.nmov; t++)
+    if (L.movf[t] == f) return true;
+  return false;
+}
+
+// the partition sequence's point at pos and its start facet (new-facet
+// index): qh_partitionall's remainder (W.pq), or the visible facets' outside
+// sets in visible order (qh_partitionvisible)
+__device__ __forceinline__ HullPt q3_seqpt(const Q3W& W, const Q3L& L, int nvis, bool init, int pos, int* start) {
+  HullPt r;
+  if (init) {
+    const int q = W.pq[pos];
+    r.x = W.Pr[3 * (size_t)q]; r.y = W.Pr[3 * (size_t)q + 1]; r.z = W.Pr[3 * (size_t)q + 2];
+    r.q = q;
+    r.pad = 0;
+    *start = 0;
+    return r;
+  }
+  int a = 0, b = nvis - 1;
+  while (a < b) {
+    const int mid = (a + b) >> 1;
+    if (L.vinc[mid] > pos) b = mid;
+    else a = mid + 1;
+  }
+  *start = L.repl[a] >= 0 ? L.repl[a] : 0;
+  return W.sb[L.vsoff[a] + pos - (L.vinc[a] - L.vscnt[a])];
+}
+
+// Locate the partition sequence in order (lqro_qhull.hpp qh_locate_seq) and
+// count each point into its destination (a new facet's index, or Q3_NEWCAP
+// + k for the k-th old facet to receive points) once its result is final.
+// Chunks stay aligned to the lanes (position 64 k + lane), so a sequence of
+// at most 64 points leaves each lane's final destination, distance and point
+// in rg, rd, rpt; a longer one goes through W.pdst, W.pdd, W.pseq.  pre /
+// prestart: position `lane`'s point, fetched by the caller (havepre).
+// init: qh_partitionall's remainder (the scan list is the facet list; a
+// moved facet goes to its end).
+__device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int sharp, bool init, int lane,
+                                     const HullPt& pre, int prestart, bool havepre, int& rg, double& rd,
+                                     HullPt& rpt) {
+  for (int t = lane; t < Q3_NEWCAP; t += 64) L.pcnt[t] = 0;
+  S.nold = 0;
+  rg = -1;
+  rd = 0.0;
+  rpt = pre;
+  hl_sync();
+  int from = 0;
+  while (from < np) {
+    int ev_pos = np, ev_kind = 0, ev_dst = -1;
+    double ev_d = 0.0;
+    for (int c = from & ~63; c < np; c += 64) {
+      const int pos = c + lane;
+      const bool act = pos >= from && pos < np;
+      int kind = 0, ls = 0, dst = -1, dfa = 0;
+      double d = 0.0;
+      HullPt pt = pre;
+      if (act) {
+        int start = prestart;
+        if (!(havepre && c == 0)) pt = q3_seqpt(W, L, S.nvis, init, pos, &start);
+        const double p[3] = {pt.x, pt.y, pt.z};
+        Q3T(12);
+        int isout, trig;
+        const int f = q3_locate(W, S, L, p, start, sharp, &d, &isout, &trig, ls);
+        Q3T(13);
+        if (isout) {
+          dst = f;
+          dfa = q3_fa(W, L, f);
+          if (!(dfa & QF_NEW) && (q3_cc(W, L, f) & 0xffffu) == 0 && !q3_in_movf(S, L, f)) kind |= 4;
+        } else if (d >= -S.MAXcoplanar && d > S.max_outside) {
+          kind |= 2;
+        }
+        if (trig) kind |= 1;
+      }
+      S.status |= qh_wave_or(ls);
+      const unsigned long long b = __ballot(kind != 0);
+      const int last = b ? __ffsll((long long)b) - 1 : 63;   // positions up to c+last are final
+      const bool fin = act && lane <= last;
+      int g = -1;
+      if (fin && dst >= 0 && (dfa & QF_NEW)) {
+        g = dfa >> 8;
+        atomicAdd(&L.pcnt[g], 1);
+      }
+      unsigned long long old = __ballot(fin && dst >= 0 && !(dfa & QF_NEW));
+      while (old) {   // old facets: registered in sequence order (rare)
+        const int l = __ffsll((long long)old) - 1;
+        old &= old - 1;
+        const int f = __builtin_amdgcn_readlane(dst, l);
+        int k = -1;
+        for (int t = 0; t < S.nold; t++)
+          if (L.oldf[t] == f) k = t;
+        if (k < 0) {
+          if (S.nold == Q3_MOVCAP) { S.status |= QHS_CAPACITY; continue; }
+          k = S.nold++;
+          if (lane == 0) { L.oldf[k] = f; L.pcnt[Q3_NEWCAP + k] = 0; L.dfac[Q3_NEWCAP + k] = f; }
+          hl_sync();
+        }
+        if (lane == 0) L.pcnt[Q3_NEWCAP + k]++;
+        if (lane == l) g = Q3_NEWCAP + k;
+        hl_sync();
+      }
+      if (fin) {
+        rg = g;
+        rd = d;
+        rpt = pt;
+        if (np > 64) {
+          W.pdst[pos] = g;
+          W.pdd[pos] = d;
+          W.pseq[pos] = pt;
+        }
+      }
+      hl_sync();
+      Q3T(14);
+      if (b) {
+        ev_pos = c + last;
+        ev_kind = __builtin_amdgcn_readlane(kind, last);
+        ev_dst = __builtin_amdgcn_readlane(dst, last);
+        ev_d = hl_rl(d, last);
+        break;
+      }
+    }
+    if (ev_pos < np) {
+      if (ev_kind & 1) {
+        if (sharp) S.findbestnew = 1;
+        else S.notsharp = 1;
+      }
+      if (ev_kind & 2) S.max_outside = ev_d;
+      if (ev_kind & 4) {
+        // qh_partitionpoint: "make sure it's after qh.facet_next" — the old
+        // facet moves behind the new ones (a fresh key)
+        const int f = ev_dst;
+        if (S.nmov == Q3_MOVCAP) {
+          S.status |= QHS_CAPACITY;
+          return;
+        }
+        if (lane == 0) {
+          L.movf[S.nmov] = f;
+          if (init) {
+            // the remainder's scan list is the facet list itself: f to its end
+            int t0 = 0;
+            for (int t = 0; t < S.nnew; t++)
+              if (L.nslot[t] == f) t0 = t;
+            for (int t = t0; t + 1 < S.nnew; t++) {
+              L.nslot[t] = L.nslot[t + 1];
+              for (int k = 0; k < 4; k++) L.npl[4 * t + k] = L.npl[4 * (t + 1) + k];
+              L.nflag[t] = L.nflag[t + 1];
+            }
+            double q[4];
+            q3_pl(W, L, f, q);
+            L.nslot[S.nnew - 1] = f;
+            for (int k = 0; k < 4; k++) L.npl[4 * (S.nnew - 1) + k] = q[k];
+            L.nflag[S.nnew - 1] = q3_fa(W, L, f);
+          }
+        }
+        q3_set_key(W, L, f, S.keyc);   // (every lane writes the same value)
+        S.keyc++;
+        S.nmov++;
+      }
+      hl_sync();
+    }
+    from = ev_pos + 1;
+  }
+}
+
+// The located points into their destinations' outside sets, in sequence
+// order, with Qhull's placement (lqro_qhull.hpp qh_emit_seq: the furthest
+// point so far held aside, a displaced one stays where it was).  Old
+// facets continue their set in a fresh segment.  ndnew: new-facet
+// destinations (0 in qh_partitionall).  The new facets that received
+// points, then the moved old facets, join the queue in key order.
+__device__ inline void q3_emit_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int ndnew, bool init, int lane, int rg,
+                                   double rd, const HullPt& rpt) {
+  if (S.status & QHS_CAPACITY) return;
+  // segments: an exclusive scan of the destinations' sizes
+  const int nd = ndnew + S.nold;
+  int base = S.sbtop;
+  for (int c0 = 0; c0 < nd; c0 += 64) {
+    const int i = c0 + lane;
+    int size = 0, g = -1, cnt0 = 0;
+    if (i < nd) {
+      g = i < ndnew ? i : Q3_NEWCAP + (i - ndnew);
+      if (g < Q3_NEWCAP) L.dfac[g] = L.nslot[g];
+      if (L.pcnt[g]) {
+        cnt0 = g < Q3_NEWCAP ? 0 : (int)(q3_cc(W, L, L.dfac[g]) & 0xffffu);
+        size = cnt0 + L.pcnt[g];
+      }
+    }
+    int inc = size;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int o = __shfl_up(inc, off);
+      if (lane >= off) inc += o;
+    }
+    if (size) {
+      L.doff[g] = base + inc - size;
+      L.dcnt[g] = cnt0;
+      L.dmax[g] = 0.0;
+      L.dchamp[g] = -1;
+    }
+    base += __shfl(inc, 63);
+  }
+  if (base > W.SB) {
+    S.status |= QHS_CAPACITY;
+    return;
+  }
+  S.sbtop = base;
+  hl_sync();
+  // old destinations (rare): their set so far, furthest point held aside
+  for (int k = 0; k < S.nold; k++) {
+    const int g = Q3_NEWCAP + k;
+    const int f = L.dfac[g];
+    const int cnt0 = L.dcnt[g];
+    if (!L.pcnt[g] || !cnt0) continue;
+    const int off0 = W.soff[f];
+    const int off = L.doff[g];
+    for (int t = lane; t < cnt0 - 1; t += 64) W.sb[off + t] = W.sb[off0 + t];
+    const HullPt ch = W.sb[off0 + cnt0 - 1];
+    const double fd = W.fdist[f];
+    if (lane == 0) {
+      L.dchamp[g] = ch.q;
+      L.dchp[3 * g] = ch.x; L.dchp[3 * g + 1] = ch.y; L.dchp[3 * g + 2] = ch.z;
+      L.dmax[g] = fd;
+    }
+    hl_sync();
+  }
+  hl_sync();
+  Q3T(15);
+  // the sequence in order: a chunk's lanes, grouped by destination
+  for (int c = 0; c < np; c += 64) {
+    const int pos = c + lane;
+    const bool act = pos < np;
+    int g = rg;
+    double dd = rd;
+    HullPt pt = rpt;
+    if (np > 64) {   // (at most 64: the lanes' own results)
+      g = act ? W.pdst[pos] : -1;
+      dd = act ? W.pdd[pos] : 0.0;
+      if (g >= 0) pt = W.pseq[pos];
+    } else if (!act) {
+      g = -1;
+    }
+    Q3T(16);
+    unsigned long long todo = __ballot(g >= 0);
+    while (todo) {
+      const int lead = __ffsll((long long)todo) - 1;
+      const int gg = __builtin_amdgcn_readlane(g, lead);
+      const unsigned long long grp = __ballot(g == gg);
+      todo &= ~grp;
+      int cnt = L.dcnt[gg];
+      double mx = L.dmax[gg];
+      int champ = L.dchamp[gg];
+      double cx = L.dchp[3 * gg], cy = L.dchp[3 * gg + 1], cz = L.dchp[3 * gg + 2];
+      const int off = L.doff[gg];
+      unsigned long long m = grp;
+      while (m) {
+        const int l = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        const double dq = hl_rl(dd, l);
+        if (cnt == 0 || mx < dq) {
+          if (cnt > 0 && lane == 0) {   // the displaced furthest point stays at the end so far
+            HullPt r;
+            r.x = cx; r.y = cy; r.z = cz; r.q = champ; r.pad = 0;
+            W.sb[off + cnt - 1] = r;
+          }
+          champ = __builtin_amdgcn_readlane(pt.q, l);
+          cx = hl_rl(pt.x, l); cy = hl_rl(pt.y, l); cz = hl_rl(pt.z, l);
+          mx = dq;
+        } else if (lane == l) {
+          W.sb[off + cnt - 1] = pt;
+        }
+        cnt++;
+      }
+      if (lane == 0) {
+        L.dcnt[gg] = cnt; L.dmax[gg] = mx; L.dchamp[gg] = champ;
+        L.dchp[3 * gg] = cx; L.dchp[3 * gg + 1] = cy; L.dchp[3 * gg + 2] = cz;
+      }
+      hl_sync();
+    }
+  }
+  hl_sync();
+  Q3T(17);
+  // the furthest point ends each set
+  for (int i = lane; i < nd; i += 64) {
+    const int g = i < ndnew ? i : Q3_NEWCAP + (i - ndnew);
+    if (!L.pcnt[g]) continue;
+    const int f = L.dfac[g];
+    HullPt r;
+    r.x = L.dchp[3 * g]; r.y = L.dchp[3 * g + 1]; r.z = L.dchp[3 * g + 2]; r.q = L.dchamp[g]; r.pad = 0;
+    W.sb[L.doff[g] + L.dcnt[g] - 1] = r;
+    W.soff[f] = L.doff[g];
+    W.fdist[f] = L.dmax[g];
+    q3_set_cc(W, L, f, (unsigned)L.dcnt[g] | ((unsigned)L.dchamp[g] << 16));
+  }
+  hl_sync();
+  if (init) return;   // qh_partitionall: the queue is built after qh_furthestnext
+  // the queue (qh.facet_next's walk): new facets with points in key order,
+  // then the moved old facets in move order
+  int qt = S.qtail;
+  for (int c = 0; c < ndnew; c += 64) {
+    const int t = c + lane;
+    const bool has = t < ndnew && L.pcnt[t] > 0;
+    const unsigned long long b = __ballot(has);
+    if (has) {
+      const int at = qt + __popcll(b & ((1ull << lane) - 1ull));
+      if (at < W.QC) { W.fq[at] = L.nslot[t]; W.fqk[at] = q3_key(W, L, L.nslot[t]); }
+    }
+    qt += __popcll(b);
+  }
+  for (int t = lane; t < S.nmov; t += 64)
+    if (qt + t < W.QC) { W.fq[qt + t] = L.movf[t]; W.fqk[qt + t] = q3_key(W, L, L.movf[t]); }
+  qt += S.nmov;
+  if (qt > W.QC) S.status |= QHS_CAPACITY;
+  S.qtail = qt;
+  hl_sync();
+  Q3T(18);
+}
+
+// the slot of the t-th new facet: the visible facets' slots, then free
+// ones, then fresh ones
+__device__ __forceinline__ int q3_alloc(const Q3S& S, const Q3L& L, int t) {
+  if (t < S.nvis) return L.visf[t];
+  const int e = t - S.nvis;
+  if (e < S.nfs) return L.fstk[S.nfs - 1 - e];
+  return S.nalloc + (e - S.nfs);
+}
+
+// qh_qhull on W.Pr[0..n) (qconvex's defaults; lqro_qhull.hpp qh_build step
+// for step)
+__device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
+#ifdef LQRO_QHULL_PROFILE
+  S.tq = __builtin_amdgcn_s_memtime();
+#endif
+  const unsigned long long ltmask = (1ull << lane) - 1ull;
+  S.status = 0;
+  S.nalloc = 1;
+  S.nfs = 0;
+  S.sbtop = 0;
+  S.nnew = S.nvis = S.nmov = S.nold = 0;
+  S.findbestnew = S.notsharp = 0;
+  S.keyc = 1;
+  S.qhead = S.qtail = 0;
+  if (W.FC > 65535) {   // 16-bit facet and point ids
+    S.status |= QHS_CAPACITY;
+    return;
+  }
+  // qh_maxmin
+  int maxpoints[6];
+  S.max_outside = 0.0;
+  S.MAXabs_coord = 0.0;
+  S.MAXwidth = -DBL_MAX;
+  S.MAXsumcoord = 0.0;
+  for (int k = 0; k < 3; k++) {
+    int mn, mx;
+    qh_extreme(W.Pr, n, k, false, lane, &mn);
+    qh_extreme(W.Pr, n, k, true, lane, &mx);
+    const double maxk = W.Pr[3 * (size_t)mx + k], mink = W.Pr[3 * (size_t)mn + k];
+    const double maxcoord = fmax(maxk, -mink);
+    const double temp = maxk - mink;
+    if (temp > S.MAXwidth) S.MAXwidth = temp;
+    if (maxcoord > S.MAXabs_coord) S.MAXabs_coord = maxcoord;
+    S.MAXsumcoord += maxcoord;
+    maxpoints[2 * k] = mn;
+    maxpoints[2 * k + 1] = mx;
+    S.NEARzero[k] = 80 * S.MAXsumcoord * DBL_EPSILON;
+  }
+  // qh_detroundoff (C-0)
+  {
+    double maxdistsum = sqrt(3.0) * S.MAXabs_coord;
+    if (S.MAXsumcoord < maxdistsum) maxdistsum = S.MAXsumcoord;
+    S.DISTround = DBL_EPSILON * (3 * maxdistsum * 1.01 + S.MAXabs_coord);
+    const double MINdenom_1 = fmax(1.0 / DBL_MAX, DBL_MIN);
+    S.MINdenom = MINdenom_1 * S.MAXabs_coord;
+    S.MINdenom_2 = sqrt(MINdenom_1 * 3) * S.MAXabs_coord;
+    S.MINvisible = 0.0 + 2 * S.DISTround;
+    S.MAXcoplanar = S.MINvisible;
+    S.MINoutside = 2 * S.MINvisible;
+  }
+  // qh_maxsimplex
+  int simplex[4];
+  {
+    const QhS T = q3_as_qhs(S);
+    double maxcoord = -DBL_MAX, mincoord = DBL_MAX;
+    int minx = -1, maxx = -1;
+    for (int i = 0; i < 6; i++) {
+      const double c = W.Pr[3 * (size_t)maxpoints[i]];
+      if (maxcoord < c) { maxcoord = c; maxx = maxpoints[i]; }
+      if (mincoord > c) { mincoord = c; minx = maxpoints[i]; }
+    }
+    double maxdet = maxcoord - mincoord;
+    int ns = 0;
+    simplex[ns++] = minx;
+    if (maxx != minx) simplex[ns++] = maxx;
+    if (ns < 2) { S.status |= QHS_INPUT; return; }
+    for (int i = 2; i < 4; i++) {
+      const double prevdet = maxdet;
+      int maxpoint = -1, maxnearzero = 0, nearzero;
+      maxdet = -1.0;
+      for (int m = 0; m < 6; m++) {
+        const int p = maxpoints[m];
+        bool ins = false;
+        for (int t = 0; t < i; t++) ins |= simplex[t] == p;
+        if (!ins && p != maxpoint) {
+          const double det = fabs(qh_detsimplex(T, W.Pr, simplex, i, p, &nearzero));
+          if (det > maxdet) { maxdet = det; maxpoint = p; maxnearzero = nearzero; }
+        }
+      }
+      const double targetdet = prevdet * S.MAXwidth;
+      const bool falsenarrow = maxdet > 0.0 && maxdet / targetdet < 1.0e-3;
+      if (maxpoint < 0 || maxnearzero || falsenarrow) {
+        double key = -1.0;
+        int idx = 0x7fffffff;
+        for (int q = lane; q < n; q += 64) {
+          bool skip = false;
+          for (int t = 0; t < 6; t++) skip |= maxpoints[t] == q;
+          for (int t = 0; t < i; t++) skip |= simplex[t] == q;
+          if (skip) continue;
+          const double det = fabs(qh_detsimplex(T, W.Pr, simplex, i, q, &nearzero));
+          if (det > key || (det == key && q < idx)) { key = det; idx = q; }
+        }
+        for (int off = 32; off >= 1; off >>= 1) {
+          const double ok = __shfl_xor(key, off);
+          const int oi = __shfl_xor(idx, off);
+          if (ok > key || (ok == key && oi < idx)) { key = ok; idx = oi; }
+        }
+        if (idx != 0x7fffffff && key > maxdet) { maxdet = key; maxpoint = idx; }
+      }
+      if (maxpoint < 0) { S.status |= QHS_INPUT; return; }
+      simplex[i] = maxpoint;
+    }
+  }
+  // qh_initialvertices (the vertex set is [v4 v3 v2 v1], v_k = simplex[k-1]),
+  // qh_createsimplex: facet slots 1..4, keys 1..4, facet i without vertex i
+  const int pset[4] = {simplex[3], simplex[2], simplex[1], simplex[0]};
+  int fs[4];
+  {
+    int top = 1, tops[4];
+    for (int i = 0; i < 4; i++) {
+      fs[i] = S.nalloc++;
+      tops[i] = top;
+      top ^= 1;
+    }
+    for (int k = 0; k < 3; k++) {
+      double c = 0.0;
+      for (int t = 0; t < 4; t++) c += W.Pr[3 * (size_t)pset[t] + k];
+      S.interior[k] = c / 4;
+    }
+    int fv[4][3];
+    for (int i = 0; i < 4; i++) {
+      int m = 0;
+      for (int t = 0; t < 4; t++)
+        if (t != i) fv[i][m++] = pset[t];
+    }
+    // qh_initialhull: the first facet's orientation decides
+    int ls = 0;
+    double q[4][4];
+    bool fl[4];
+    q3_plane(S, ls, W.Pr + 3 * (size_t)fv[0][0], W.Pr + 3 * (size_t)fv[0][1], W.Pr + 3 * (size_t)fv[0][2], tops[0],
+             q[0], &fl[0]);
+    if (q3_distq(q[0], S.interior) > S.DISTround)
+      for (int i = 0; i < 4; i++) tops[i] ^= 1;
+    bool anyflip = false;
+    for (int i = 0; i < 4; i++) {
+      q3_plane(S, ls, W.Pr + 3 * (size_t)fv[i][0], W.Pr + 3 * (size_t)fv[i][1], W.Pr + 3 * (size_t)fv[i][2],
+               tops[i], q[i], &fl[i]);
+      anyflip |= fl[i];
+    }
+    if (anyflip) ls |= QHS_FLIPPED;
+    int nbs[4][3];
+    for (int i = 0; i < 4; i++) {
+      int m = 0;
+      for (int t = 0; t < 4; t++)
+        if (t != i) nbs[i][m++] = fs[t];
+    }
+    double minangle = DBL_MAX;
+    for (int i = 0; i < 4; i++)
+      for (int t = 0; t < 3; t++) {
+        int j = 0;
+        for (int u = 0; u < 4; u++)
+          if (fs[u] == nbs[i][t]) j = u;
+        double angle = 0.0;
+        for (int k = 0; k < 3; k++) angle += q[i][k] * q[j][k];
+        if (angle < minangle) minangle = angle;
+      }
+    if (minangle < -0.99999999) ls |= QHS_NARROW;
+    S.status |= ls;
+    hl_sync();
+    if (lane == 0)
+      for (int i = 0; i < 4; i++) {
+        const int f = fs[i];
+        q3_set_facet(W, L, f, q[i], nbs[i][0], nbs[i][1], nbs[i][2],
+                     QF_LIVE | (tops[i] ? QF_TOP : 0) | (fl[i] ? QF_FLIPPED : 0));
+        q3_set_key(W, L, f, S.keyc + i);
+        q3_set_cc(W, L, f, 0u);
+        Q3V& v = W.vv[f];
+        for (int t = 0; t < 3; t++) {
+          for (int k = 0; k < 3; k++) v.p[3 * t + k] = W.Pr[3 * (size_t)fv[i][t] + k];
+          v.id[t] = fv[i][t];
+        }
+      }
+    S.keyc += 4;
+    hl_sync();
+    // qh_partitionall: every point but the simplex, in index order; each
+    // facet in list order takes the ones at or beyond distoutside
+    int np = 0;
+    for (int c = 0; c < n; c += 64) {
+      const int qi = c + lane;
+      const bool ok = qi < n && qi != simplex[0] && qi != simplex[1] && qi != simplex[2] && qi != simplex[3];
+      const unsigned long long b = __ballot(ok);
+      if (ok) W.pq[np + __popcll(b & ltmask)] = qi;
+      np += __popcll(b);
+    }
+    hl_sync();
+    const double distoutside = fmax(2 * S.MINoutside, S.max_outside);
+    for (int i = 0; i < 4; i++) {
+      const int f = fs[i];
+      int cnt = 0;
+      const int off = S.sbtop;
+      double mx = 0.0, cx = 0.0, cy = 0.0, cz = 0.0;
+      int champ = -1, w = 0;
+      for (int c = 0; c < np; c += 64) {
+        const int pos = c + lane;
+        HullPt pt;
+        pt.x = pt.y = pt.z = 0.0;
+        pt.q = -1;
+        pt.pad = 0;
+        double d = -DBL_MAX;
+        if (pos < np) {
+          pt.q = W.pq[pos];
+          pt.x = W.Pr[3 * (size_t)pt.q]; pt.y = W.Pr[3 * (size_t)pt.q + 1]; pt.z = W.Pr[3 * (size_t)pt.q + 2];
+          const double p[3] = {pt.x, pt.y, pt.z};
+          d = q3_distq(q[i], p);
+        }
+        const bool out = pos < np && d >= distoutside;
+        const bool keep = pos < np && !out;
+        const unsigned long long bk = __ballot(keep);
+        hl_sync();
+        if (keep) W.pq[w + __popcll(bk & ltmask)] = pt.q;
+        w += __popcll(bk);
+        unsigned long long bo = __ballot(out);
+        while (bo) {
+          const int l = __ffsll((long long)bo) - 1;
+          bo &= bo - 1;
+          const double dq = hl_rl(d, l);
+          if (cnt == 0 || dq > mx) {
+            if (cnt > 0 && lane == 0 && off + cnt - 1 < W.SB) {
+              HullPt r;
+              r.x = cx; r.y = cy; r.z = cz; r.q = champ; r.pad = 0;
+              W.sb[off + cnt - 1] = r;
+            }
+            champ = __builtin_amdgcn_readlane(pt.q, l);
+            cx = hl_rl(pt.x, l); cy = hl_rl(pt.y, l); cz = hl_rl(pt.z, l);
+            mx = dq;
+          } else if (lane == l && off + cnt - 1 < W.SB) {
+            W.sb[off + cnt - 1] = pt;
+          }
+          cnt++;
+        }
+        hl_sync();
+      }
+      if (cnt) {
+        if (off + cnt > W.SB) { S.status |= QHS_CAPACITY; return; }
+        if (lane == 0) {
+          HullPt r;
+          r.x = cx; r.y = cy; r.z = cz; r.q = champ; r.pad = 0;
+          W.sb[off + cnt - 1] = r;
+          W.soff[f] = off;
+          W.fdist[f] = mx;
+          q3_set_cc(W, L, f, (unsigned)cnt | ((unsigned)champ << 16));
+        }
+        S.sbtop += cnt;
+      }
+      np = w;
+      hl_sync();
+    }
+    // the remainder: qh_partitionpoint with findbestnew from the head of the
+    // facet list (MERGING): the scan list is the facet list
+    if (np > 0) {
+      S.nnew = 4;
+      if (lane == 0)
+        for (int i = 0; i < 4; i++) {
+          L.nslot[i] = fs[i];
+          for (int k = 0; k < 4; k++) L.npl[4 * i + k] = q[i][k];
+          L.nflag[i] = q3_fa(W, L, fs[i]);
+          L.nn1[i] = L.nn2[i] = 0;
+        }
+      S.nmov = 0;
+      S.findbestnew = 1;
+      hl_sync();
+      int rg;
+      double rd;
+      HullPt rpt, pre;
+      pre.x = pre.y = pre.z = 0.0;
+      pre.q = -1;
+      pre.pad = 0;
+      q3_locate_seq(W, S, L, np, 0, true, lane, pre, 0, false, rg, rd, rpt);
+      q3_emit_seq(W, S, L, np, 0, true, lane, rg, rd, rpt);
+      S.findbestnew = 0;
+      S.nnew = 0;
+      S.nmov = 0;
+      hl_sync();
+    }
+    if (S.status & (QHS_INPUT | QHS_TOPOLOGY | QHS_CAPACITY)) return;
+    // qh_furthestnext: the first facet in list order with the furthest
+    // outside point moves to the front (key 0); the queue: the facets with
+    // points in list order
+    {
+      int order[4] = {fs[0], fs[1], fs[2], fs[3]};
+      unsigned kk[4];
+      for (int i = 0; i < 4; i++) kk[i] = q3_key(W, L, order[i]);
+      for (int a = 0; a < 4; a++)
+        for (int b = a + 1; b < 4; b++)
+          if (kk[b] < kk[a]) {
+            const unsigned tk = kk[a]; kk[a] = kk[b]; kk[b] = tk;
+            const int to = order[a]; order[a] = order[b]; order[b] = to;
+          }
+      int best = -1;
+      double bd = -DBL_MAX;
+      for (int i = 0; i < 4; i++) {
+        const int f = order[i];
+        if ((q3_cc(W, L, f) & 0xffffu) && W.fdist[f] > bd) { best = f; bd = W.fdist[f]; }
+      }
+      hl_sync();
+      if (best >= 0) {
+        q3_set_key(W, L, best, 0u);
+        for (int i = 0; i < 4; i++)
+          if (order[i] == best) {
+            for (int t = i; t > 0; t--) { order[t] = order[t - 1]; kk[t] = kk[t - 1]; }
+            order[0] = best;
+            kk[0] = 0;
+            break;
+          }
+      }
+      int qt = 0;
+      for (int i = 0; i < 4; i++)
+        if (q3_cc(W, L, order[i]) & 0xffffu) {
+          if (lane == 0) { W.fq[qt] = order[i]; W.fqk[qt] = kk[i]; }
+          qt++;
+        }
+      S.qhead = 0;
+      S.qtail = qt;
+      hl_sync();
+    }
+  }
+  Q3T(0);
+  // qh_buildhull
+  for (;;) {
+    // qh_nextfurthest: the first queued facet still alive (same key) with
+    // points, 64 entries at a time
+    int facet = -1, furthest = -1;
+    while (S.qhead < S.qtail) {
+      const int pos = S.qhead + lane;
+      bool ok = false;
+      int f = 0;
+      unsigned c = 0;
+      if (pos < S.qtail) {
+        f = W.fq[pos];
+        const unsigned k = W.fqk[pos];
+        const int fa = q3_fa(W, L, f);
+        c = q3_cc(W, L, f);
+        ok = (fa & QF_LIVE) && q3_key(W, L, f) == k && (c & 0xffffu) > 0;
+      }
+      const unsigned long long b = __ballot(ok);
+      if (b) {
+        const int l = __ffsll((long long)b) - 1;
+        S.qhead += l;
+        facet = __builtin_amdgcn_readlane(f, l);
+        const unsigned cf = (unsigned)__builtin_amdgcn_readlane((int)c, l);
+        furthest = (int)(cf >> 16);
+        hl_sync();
+        q3_set_cc(W, L, facet, (cf & 0xffffu) - 1u);   // qh_setdellast (the facet is visible: no new furthest)
+        hl_sync();
+        break;
+      }
+      S.qhead += min(64, S.qtail - S.qhead);
+    }
+    Q3T(1);
+    if (furthest < 0) break;
+    const double apexp[3] = {W.Pr[3 * (size_t)furthest], W.Pr[3 * (size_t)furthest + 1],
+                             W.Pr[3 * (size_t)furthest + 2]};
+    // qh_findhorizon, a level of the breadth-first search at a time: the
+    // candidates of a level in (visible facet, neighbour) order, a facet
+    // taken at its first occurrence
+    {
+      const int fa0 = q3_fa(W, L, facet);
+      hl_sync();
+      if (lane == 0) L.visf[0] = facet;
+      q3_set_fa(W, L, facet, fa0 | QF_VISIBLE);
+      hl_sync();
+    }
+    int ls = 0, nvis = 1;
+    for (int lo = 0; lo < nvis;) {
+      const int hi = nvis;
+      const int ncand = 3 * (hi - lo);
+      for (int c0 = 0; c0 < ncand; c0 += 64) {
+        const int c = c0 + lane;
+        int nb = -1, fa = QF_VISIBLE;
+        double q[4] = {0.0, 0.0, 0.0, 0.0};
+        if (c < ncand) {
+          nb = q3_nb(W, L, L.visf[lo + c / 3], c % 3);
+          int nn[3];
+          q3_get(W, L, nb, q, nn, &fa);
+        }
+        bool cand = !(fa & QF_VISIBLE);
+        bool dup = false;
+        for (unsigned long long mm = __ballot(cand); mm;) {
+          const int l = __ffsll((long long)mm) - 1;
+          mm &= mm - 1;
+          dup |= (l < lane) && __builtin_amdgcn_readlane(nb, l) == nb;
+        }
+        cand = cand && !dup;
+        const double dist = cand ? q3_distq(q, apexp) : 0.0;
+        const bool vis = cand && dist >= S.MINvisible;
+        if (cand && !vis && dist >= -S.MAXcoplanar) ls |= QHS_COPLANAR;   // Qhull merges it: built on merge-free
+        const unsigned long long bv = __ballot(vis);
+        if (vis) {
+          const int at = nvis + __popcll(bv & ltmask);
+          if (at < Q3_VISCAP) L.visf[at] = nb;
+          q3_set_fa(W, L, nb, fa | QF_VISIBLE);
+        }
+        nvis += __popcll(bv);
+        hl_sync();
+      }
+      lo = hi;
+      if (nvis > Q3_VISCAP) { S.status |= QHS_CAPACITY; return; }
+    }
+    S.status |= qh_wave_or(ls);
+    S.nvis = nvis;
+    Q3T(2);
+    // qh_makenew_simplicial: one new facet per horizon ridge, created in
+    // (visible facet, neighbour) order, its plane (qh_makenewplanes) made by
+    // the ridge's lane from the horizon facet's vertex record; with it what
+    // the visible facets' slots still hold.  When every ridge fits one pass
+    // (3 nvis <= 64) the lane keeps its facet's points for qh_checkzero.
+    for (int vi = lane; vi < nvis; vi += 64) L.repl[vi] = -1;
+    hl_sync();
+    const bool one = 3 * nvis <= 64;
+    int nnew = 0, ts = 0, lm = 0, my_t = -1;
+    double P1[3] = {0.0, 0.0, 0.0}, P2[3] = {0.0, 0.0, 0.0}, PO[3] = {0.0, 0.0, 0.0};
+    for (int c0 = 0; c0 < 3 * nvis; c0 += 64) {
+      const int c = c0 + lane;
+      int vis = -1, nb = -1, hfa = QF_VISIBLE;
+      int hn[3] = {-1, -1, -1};
+      if (c < 3 * nvis) {
+        const int vi = c / 3;
+        vis = L.visf[vi];
+        nb = q3_nb(W, L, vis, c - 3 * vi);
+        q3_tp(W, L, nb, hn, &hfa);
+        if (c == 3 * vi) {
+          const Q3V& vw = W.vv[vis];
+          L.vvert[3 * vi] = vw.id[0]; L.vvert[3 * vi + 1] = vw.id[1]; L.vvert[3 * vi + 2] = vw.id[2];
+          L.vsoff[vi] = W.soff[vis];
+          L.vscnt[vi] = (int)(q3_cc(W, L, vis) & 0xffffu);
+        }
+      }
+      const bool ridge = !(hfa & QF_VISIBLE);
+      const unsigned long long b = __ballot(ridge);
+      if (ridge) {
+        const int t = nnew + __popcll(b & ltmask);
+        const int hskip = hn[0] == vis ? 0 : hn[1] == vis ? 1 : hn[2] == vis ? 2 : -1;
+        if (hskip < 0) {
+          ts |= QHS_TOPOLOGY;
+        } else if (t < Q3_NEWCAP) {
+          const Q3V& h = W.vv[nb];
+          const int top = (hfa & QF_TOP) ? (hskip & 1) : ((hskip & 1) ^ 1);
+          // the ridge: the horizon facet's vertices but the one opposite the visible facet
+          const int i1 = hskip == 0 ? 1 : 0, i2 = hskip == 2 ? 1 : 2;
+          double p1[3], p2[3], po[3];
+          for (int k = 0; k < 3; k++) {
+            p1[k] = h.p[3 * i1 + k];
+            p2[k] = h.p[3 * i2 + k];
+            po[k] = h.p[3 * hskip + k];
+          }
+          L.nv[3 * t] = furthest;
+          L.nv[3 * t + 1] = h.id[i1];
+          L.nv[3 * t + 2] = h.id[i2];
+          L.nhz[t] = nb;
+          L.nhskip[t] = hskip;
+          atomicMax(&L.repl[c / 3], t);     // qh_getreplacement: the visible facet's last new facet
+          double q[4];
+          bool flipped;
+          int fl = QF_NEW | QF_LIVE | (top ? QF_TOP : 0);
+          q3_plane(S, lm, apexp, p1, p2, top, q, &flipped);
+          if (flipped) { fl |= QF_FLIPPED; lm |= QHS_FLIPPED; }
+          L.nflag[t] = fl;
+          L.npl[4 * t] = q[0]; L.npl[4 * t + 1] = q[1]; L.npl[4 * t + 2] = q[2]; L.npl[4 * t + 3] = q[3];
+          if (one) {
+            my_t = t;
+            for (int k = 0; k < 3; k++) { P1[k] = p1[k]; P2[k] = p2[k]; PO[k] = po[k]; }
+          } else {
+            for (int k = 0; k < 3; k++) {
+              W.ncoord[9 * t + k] = p1[k]; W.ncoord[9 * t + 3 + k] = p2[k]; W.ncoord[9 * t + 6 + k] = po[k];
+            }
+          }
+        }
+      }
+      nnew += __popcll(b);
+    }
+    Q3T(19);
+    S.status |= qh_wave_or(ts);
+    if (nnew > Q3_NEWCAP) S.status |= QHS_CAPACITY;
+    if (S.status & (QHS_TOPOLOGY | QHS_CAPACITY)) return;
+    S.nnew = nnew;
+    hl_sync();
+    // qh_partitionvisible's sequence: the visible facets' outside sets in
+    // visible order; its first 64 points are fetched now, under the cone's
+    // construction
+    int np2 = 0;
+    for (int c0 = 0; c0 < nvis; c0 += 64) {
+      const int vi = c0 + lane;
+      const int cnt = vi < nvis ? L.vscnt[vi] : 0;
+      const int inc = q3_scan_add(cnt);
+      if (vi < nvis) L.vinc[vi] = np2 + inc;
+      np2 += __builtin_amdgcn_readlane(inc, 63);
+    }
+    hl_sync();
+    HullPt pre;
+    pre.x = pre.y = pre.z = 0.0;
+    pre.q = -1;
+    pre.pad = 0;
+    int prestart = 0;
+    if (lane < np2) pre = q3_seqpt(W, L, nvis, false, lane, &prestart);
+    {
+      // slots: the visible facets', then free ones, then fresh ones
+      const int extra = nnew > nvis ? nnew - nvis : 0;
+      const int take = extra < S.nfs ? extra : S.nfs;
+      if (S.nalloc + extra - take > W.FC) { S.status |= QHS_CAPACITY; return; }
+      for (int t = lane; t < nnew; t += 64) L.nslot[t] = q3_alloc(S, L, t);
+      S.nfs -= take;
+      S.nalloc += extra - take;
+      hl_sync();
+    }
+    Q3T(3);
+    // qh_matchnewfacets (nb[1] shares {apex, v2}, nb[2] shares {apex, v1});
+    // the new facets' fields and vertex records; the horizon facets' links
+    const unsigned key0 = S.keyc;
+    auto finish = [&](int t, const double* p1, const double* p2) {
+      int nbu[2];
+      for (int k = 1; k < 3; k++) {
+        const int w = L.nv[3 * t + 3 - k];
+        int found = -1, cnt = 0;
+        for (int u = 0; u < nnew; u++)
+          if (u != t && (L.nv[3 * u + 1] == w || L.nv[3 * u + 2] == w)) { found = u; cnt++; }
+        if (cnt != 1) lm |= QHS_TOPOLOGY;
+        nbu[k - 1] = found;
+      }
+      L.nn1[t] = nbu[0] >= 0 ? nbu[0] : 0;
+      L.nn2[t] = nbu[1] >= 0 ? nbu[1] : 0;
+      const int s = L.nslot[t];
+      const double q[4] = {L.npl[4 * t], L.npl[4 * t + 1], L.npl[4 * t + 2], L.npl[4 * t + 3]};
+      q3_set_facet(W, L, s, q, L.nhz[t], nbu[0] >= 0 ? L.nslot[nbu[0]] : 0, nbu[1] >= 0 ? L.nslot[nbu[1]] : 0,
+                   L.nflag[t] | (t << 8));
+      q3_set_key(W, L, s, key0 + (unsigned)t);
+      q3_set_cc(W, L, s, 0u);
+      Q3V& v = W.vv[s];
+      *reinterpret_cast<double4*>(v.p) = make_double4(apexp[0], apexp[1], apexp[2], p1[0]);
+      *reinterpret_cast<double4*>(v.p + 4) = make_double4(p1[1], p1[2], p2[0], p2[1]);
+      *reinterpret_cast<double2*>(v.p + 8) = make_double2(p2[2], 0.0);
+      *reinterpret_cast<int4*>(v.id) = make_int4(furthest, L.nv[3 * t + 1], L.nv[3 * t + 2], 0);
+      q3_set_nb(W, L, L.nhz[t], L.nhskip[t], s);
+    };
+    if (one) {
+      if (my_t >= 0) finish(my_t, P1, P2);
+    } else {
+      for (int t = lane; t < nnew; t += 64) {
+        double p1[3], p2[3];
+        for (int k = 0; k < 3; k++) { p1[k] = W.ncoord[9 * t + k]; p2[k] = W.ncoord[9 * t + 3 + k]; }
+        finish(t, p1, p2);
+      }
+    }
+    S.keyc += (unsigned)nnew;
+    hl_sync();
+    // qh_checkzero: each new facet clearly convex to its neighbours
+    if (!(qh_wave_or(lm) & QHS_FLIPPED)) {
+      auto zero = [&](int t, const double* p1, const double* p2, const double* po) {
+        const double d1 = q3_distq(L.npl + 4 * L.nn1[t], p1);
+        const double d2 = q3_distq(L.npl + 4 * L.nn2[t], p2);
+        const double d3 = q3_distq(L.npl + 4 * t, po);
+        if (d1 >= -2 * S.DISTround || d2 >= -2 * S.DISTround || d3 >= -2 * S.DISTround) lm |= QHS_NONCONVEX;
+      };
+      if (one) {
+        if (my_t >= 0) zero(my_t, P1, P2, PO);
+      } else {
+        for (int t = lane; t < nnew; t += 64) {
+          double p1[3], p2[3], po[3];
+          for (int k = 0; k < 3; k++) {
+            p1[k] = W.ncoord[9 * t + k]; p2[k] = W.ncoord[9 * t + 3 + k]; po[k] = W.ncoord[9 * t + 6 + k];
+          }
+          zero(t, p1, p2, po);
+        }
+      }
+    }
+    S.status |= qh_wave_or(lm);
+    Q3T(4);
+    if (S.status & (QHS_TOPOLOGY | QHS_CAPACITY)) return;
+    S.findbestnew = 0;
+    S.notsharp = 0;
+    S.nmov = 0;
+    Q3T(5);
+    const int sharp = q3_sharpnewfacets(S, L, lane);
+    Q3T(20);
+    if (np2) {
+      int rg;
+      double rd;
+      HullPt rpt;
+      q3_locate_seq(W, S, L, np2, sharp, false, lane, pre, prestart, true, rg, rd, rpt);
+      Q3T(6);
+      q3_emit_seq(W, S, L, np2, nnew, false, lane, rg, rd, rpt);
+      Q3T(7);
+    }
+    if (S.status & QHS_CAPACITY) return;
+    // deleted vertices (a visible facet's vertex on no new facet) close to a
+    // new facet: Qhull's qh_partitioncoplanar would act (not restated)
+    {
+      int lsd = 0;
+      for (int t = lane; t < 3 * nvis; t += 64) {
+        const int v = L.vvert[t];
+        bool skip = false;
+        for (int u = 0; u < nnew && !skip; u++) skip = L.nv[3 * u + 1] == v || L.nv[3 * u + 2] == v;
+        for (int e = 0; e < t && !skip; e++) skip = L.vvert[e] == v;
+        if (skip) continue;
+        const double p[3] = {W.Pr[3 * (size_t)v], W.Pr[3 * (size_t)v + 1], W.Pr[3 * (size_t)v + 2]};
+        double d;
+        int iso, trig;
+        q3_locate(W, S, L, p, 0, 2, &d, &iso, &trig, lsd);
+        if (d >= -S.MAXcoplanar) lsd |= QHS_COPLANAR;
+      }
+      S.status |= qh_wave_or(lsd);
+    }
+    Q3T(8);
+    if (S.status & QHS_CAPACITY) return;
+    // qh_deletevisible: the visible slots no new facet took are freed; the
+    // new facets become old
+    for (int t = nnew + lane; t < nvis; t += 64) {
+      const int f = L.visf[t];
+      q3_set_fa(W, L, f, 0);
+      const int at = S.nfs + (t - nnew);
+      if (at < Q3_FSTK) L.fstk[at] = (unsigned short)f;
+    }
+    if (nvis > nnew) S.nfs = min(Q3_FSTK, S.nfs + (nvis - nnew));
+    for (int t = lane; t < nnew; t += 64) q3_set_fa(W, L, L.nslot[t], L.nflag[t] & ~QF_NEW);
+    S.nnew = 0;
+    S.nmov = 0;
+    S.findbestnew = 0;
+    S.notsharp = 0;
+    hl_sync();
+    Q3T(9);
+  }
+}
+
+// the reference's selection (LQRO:925-968; lqro_qhull.hpp qh_select) over
+// the finished hull: Qhull's facet order is key order, so a tie goes to the
+// smaller key and facet 0 is the smallest key alive
+__device__ inline void q3_select(const HullArgs& A, const Q3W& W, const Q3L& L, const Q3S& S, int lane,
+                                 const double* xi, const double* vrel, int slot) {
+  const bool fail = (S.status & (QHS_INPUT | QHS_TOPOLOGY | QHS_CAPACITY)) != 0;
+  double best = INFINITY;
+  unsigned bkey = 0xffffffffu, minkey = 0xffffffffu;
+  int bf = -1, nfac = 0;
+  if (!fail) {
+    for (int f0 = 1; f0 < S.nalloc; f0 += 256) {
+      // four slots a lane: their first vertices' points in one round trip
+      int fs[4], fa[4], v[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        fs[u] = f0 + 64 * u + lane;
+        fa[u] = fs[u] < S.nalloc ? q3_fa(W, L, fs[u]) : 0;
+        v[u] = (fa[u] & QF_LIVE) ? W.vv[fs[u]].id[0] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        if (!(fa[u] & QF_LIVE)) continue;
+        const int f = fs[u];
+        nfac++;
+        const unsigned k = q3_key(W, L, f);
+        minkey = k < minkey ? k : minkey;
+        double q[4];
+        q3_pl(W, L, f, q);
+        const double* P = W.Pf + 3 * (size_t)v[u];
+        const double d = fabs(q[0] * (vrel[0] - P[0]) + q[1] * (vrel[1] - P[1]) + q[2] * (vrel[2] - P[2]));
+        if (d < best || (d == best && k < bkey)) { best = d; bkey = k; bf = f; }
+      }
+    }
+  }
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double ob = __shfl_xor(best, off);
+    const unsigned ok = (unsigned)__shfl_xor((int)bkey, off);
+    const int of = __shfl_xor(bf, off);
+    const unsigned om = (unsigned)__shfl_xor((int)minkey, off);
+    nfac += __shfl_xor(nfac, off);
+    minkey = om < minkey ? om : minkey;
+    if (ob < best || (ob == best && ok < bkey)) { best = ob; bkey = ok; bf = of; }
+  }
+  const bool ok = !fail && nfac > 0 && bf >= 0;
+  const bool stale = ok && bkey == minkey;
+  const bool merged = (S.status & (QHS_COPLANAR | QHS_NONCONVEX | QHS_FLIPPED | QHS_NARROW | QHS_SINGULAR)) != 0;
+  double bq[4] = {0.0, 0.0, 0.0, 0.0};
+  int bv[3] = {0, 0, 0};
+  if (ok) {
+    q3_pl(W, L, bf, bq);
+    for (int t = 0; t < 3; t++) bv[t] = W.vv[bf].id[t];
+  }
+  if (lane == 0) {
+    float* pl = A.planes + (size_t)slot * 8;
+    double* qn = A.qnrm + (size_t)slot * 4;
+    double nrm[3] = {0.0, 0.0, 0.0};
+    if (ok && !stale) {
+      nrm[0] = bq[0]; nrm[1] = bq[1]; nrm[2] = bq[2];
+      const double dh = best * 0.5;                      // :1416
+      const double mult = 1.0;                           // :1213
+      pl[0] = (float)(xi[3] + mult * dh * nrm[0]);
+      pl[1] = (float)(xi[4] + mult * dh * nrm[1]);
+      pl[2] = (float)(xi[5] + mult * dh * nrm[2]);
+      pl[3] = (float)nrm[0]; pl[4] = (float)nrm[1]; pl[5] = (float)nrm[2];
+      pl[6] = __int_as_float(1);
+      qn[0] = nrm[0]; qn[1] = nrm[1]; qn[2] = nrm[2]; qn[3] = best;
+      atomicAdd(&A.stats[3], 1ull);
+    } else if (stale) {
+      pl[6] = __int_as_float(3);                         // pending: the loop-carried normal (k_stale)
+      qn[0] = qn[1] = qn[2] = 0.0; qn[3] = best;
+      const int k = atomicAdd(A.qstale_count, 1);
+      if (k < A.qstale_cap) A.qstale[k] = slot;
+      atomicAdd(&A.stats[3], 1ull);
+    } else {
+      pl[6] = __int_as_float(0);
+      atomicAdd(&A.stats[4], 1ull);
+    }
+    if (A.recs) {
+      lqro_pair_record& rec = A.recs[slot];
+      rec.flags |= ok ? LQRO_REC_HULL : LQRO_REC_HULLFAIL;
+      if (stale) rec.flags |= LQRO_REC_STALE;
+      if (merged) rec.flags |= LQRO_REC_QHMERGE;
+      rec.n_facets = ok ? nfac : -(S.status & 0xffff) - 1;
+      if (ok) {
+        rec.facet[0] = bv[0]; rec.facet[1] = bv[1]; rec.facet[2] = bv[2];
+        rec.dist = best;
+        for (int q = 0; q < 3; ++q) {
+          rec.normal[q] = nrm[q];
+          rec.plane_point[q] = stale ? 0.0f : pl[q];
+          rec.plane_normal[q] = stale ? 0.0f : pl[3 + q];
+        }
+      }
+    }
+  }
+  hl_sync();
+}
+
+// one inside-hull pair per wave (one wave per CU), persistent over the hull
+// queue; a build beyond this kernel's caps goes to the retry queue
+// (k_qhull_big)
+__device__ inline void q3_body(const HullArgs& A, Q3L& L) {
+  const int lane = threadIdx.x & 63;
+  const int HNP = A.H * A.NP;
+  const Q3W W = q3_worker(A.qscratch + (size_t)(A.block_base + blockIdx.x) * A.qstride, HNP);
+  for (;;) {
+    const int slot = hull_take_job(A, L, false);
+    if (slot < 0) break;
+    const int lrow = slot / A.npr, jj = A.nbr_list ? A.nbr_list[slot] : slot % A.npr;
+    const int i = A.row_begin + lrow * A.row_stride;
+    const int j = jj < i ? jj : jj + 1;
+    const double* xi = A.x + (size_t)i * A.X;
+    const double* xj = A.x + (size_t)j * A.X;
+    const double* Ti = A.T + (A.per_agent ? (size_t)i * A.H * 9 : 0);
+    const double* Ni = A.NCF + (A.per_agent ? (size_t)i * A.H * 3 * A.X : 0);
+    const double vrel[3] = {xi[3] - xj[3], xi[4] - xj[4], xi[5] - xj[5]};
+    const int n = hull_points(A, L, Ti, Ni, xi, xj, vrel, W.Pr, W.Pf);
+    Q3S S;
+#ifdef LQRO_QHULL_PROFILE
+    for (int k = 0; k < 24; k++) S.tph[k] = 0;
+#endif
+    S.status = 0;
+    S.nalloc = 1;
+    if (L.fail || n < 4) S.status = QHS_INPUT;
+    else q3_build(W, S, L, n, lane);
+    hl_sync();
+    if (S.status & QHS_CAPACITY) {
+      if (lane == 0) {
+        const int r = atomicAdd(A.rcount, 1);
+        if (r < A.cap) A.rqueue[r] = slot;
+      }
+      hl_sync();
+      continue;
+    }
+#ifdef LQRO_QHULL_PROFILE
+    unsigned long long tq_ = __builtin_amdgcn_s_memtime();
+#endif
+    q3_select(A, W, L, S, lane, xi, vrel, slot);
+#ifdef LQRO_QHULL_PROFILE
+    S.tph[10] = __builtin_amdgcn_s_memtime() - tq_;
+    S.tph[11] = 1;
+    if (A.prof && lane == 0)
+      for (int k = 0; k < 24; k++) atomicAdd(&A.prof[k], S.tph[k]);
+#endif
+    if (A.ext_nf && lane == 0) *A.ext_nf = S.status;   // test hook: the build's status bits
+    if (A.ext_facets) {                                  // test hook: the facet list in key order
+      for (int f = 1 + lane; f < S.nalloc; f += 64) {
+        if (!(q3_fa(W, L, f) & QF_LIVE)) continue;
+        const unsigned k = q3_key(W, L, f);
+        int rank = 0, nl = 0;
+        for (int g = 1; g < S.nalloc; g++)
+          if (q3_fa(W, L, g) & QF_LIVE) { nl++; rank += q3_key(W, L, g) < k; }
+        if (rank < A.ext_max)
+          for (int t = 0; t < 3; t++) A.ext_facets[3 * rank + t] = W.vv[f].id[t];
+        if (rank == 0 && nl < A.ext_max) A.ext_facets[3 * nl] = -1;
+      }
+      hl_sync();
+    }
+  }
+}
+
+}  // namespace lqro

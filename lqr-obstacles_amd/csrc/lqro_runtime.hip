@@ -551,8 +551,9 @@ static int ctx_alloc(lqro_ctx* c) {
   HIPCHK(hipMalloc(&c->d_carry, sizeof(double) * 6));
   HIPCHK(hipMemset(c->d_carry, 0, sizeof(double) * 6));
   if (c->qhull_order) {
-    // k_qhull: QH_WPC one-wave workers per CU, each with its own build scratch
-    c->qworkers = c->n_cu * 4;
+    // k_qhull: one one-wave worker per CU (the build's facets fill the CU's
+    // LDS), each with its own build scratch
+    c->qworkers = c->n_cu;
     c->qstride = (qhull_worker_bytes((int)(H * NP)) + 255) & ~(size_t)255;
     HIPCHK(hipMalloc(&c->d_qscratch, c->qstride * (size_t)c->qworkers));
     HIPCHK(hipMalloc(&c->d_qnrm, sizeof(double) * 4 * (slots ? slots : 1)));
@@ -899,7 +900,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
       // the hot pairs' hulls in Qhull's order (k_qhull leaves when the queue
       // is empty), then the row sweep
       if (!c->qhull_big) {
-        launch_qhull(dim3(std::min(nwait * 4, c->qworkers)), c->side, Hh);
+        launch_qhull(dim3(std::min(nwait, c->qworkers)), c->side, Hh);
         HIPCHK(hipGetLastError());
       }
       if (nside > 0) {

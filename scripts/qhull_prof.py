@@ -23,9 +23,13 @@ print(c.timings(), c.stats())
 out = np.zeros(32 + 2 * 4096 + 32, np.uint64)
 L.lqro_debug_hull_profile(c._h, out.ctypes.data_as(C.c_void_p))
 names = ["init+partitionall", "nextfurthest", "findhorizon", "makenew", "match+planes+checkzero",
-         "gather", "locate", "emit", "delvertex", "delete+reset", "select", "jobs"]
+         "gather", "locate", "emit", "delvertex", "delete+reset", "select", "jobs",
+         "locate:fetch", "locate:search", "locate:count", "emit:segments", "emit:loads", "emit:groups",
+         "emit:final+queue", "makenew:ridges", "sharp", "-", "-", "-"]
 jobs = max(int(out[11]), 1)
-tot = sum(int(out[k]) for k in range(11))
-for k, nm in enumerate(names[:11]):
-    print(f"{nm:24s} {int(out[k]) / jobs / 100:10.1f} us/hull  {100 * int(out[k]) / max(tot, 1):5.1f}%")
-print("hulls", jobs, "total us/hull", tot / jobs / 100)
+ks = [k for k in range(24) if k != 11 and names[k] != "-"]
+tot = sum(int(out[k]) for k in ks)
+GHZ = 2.4   # s_memtime counts shader cycles (MI355X_MICROARCH.md, PMC units)
+for k in ks:
+    print(f"{names[k]:24s} {int(out[k]) / jobs / GHZ / 1e3:10.3f} ms/hull  {100 * int(out[k]) / max(tot, 1):5.1f}%")
+print("hulls", jobs, "total ms/hull", tot / jobs / GHZ / 1e3)

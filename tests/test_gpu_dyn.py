@@ -105,7 +105,15 @@ class _Hip:
     (libamdhip64): torch's bundled runtime is not initialised in this process."""
 
     def __init__(self):
-        self.h = C.CDLL("libamdhip64.so")
+        # the copy liblqro.so loaded (a second HIP runtime in one process, e.g.
+        # torch's bundled one, sees no device)
+        path = "libamdhip64.so"
+        with open("/proc/self/maps") as f:
+            for line in f:
+                if "libamdhip64" in line and "/opt/rocm" in line:
+                    path = line.split()[-1]
+                    break
+        self.h = C.CDLL(path)
         self.ptrs = []
 
     def put(self, a: np.ndarray) -> int:
