@@ -281,6 +281,35 @@ def config_runs(lqro, torch, dev, local, world, rank, dist, steps, mode="block",
     return out
 
 
+def canonical_rule_run(lqro, torch, dev, sh, gains, d_x, d_vg, d_newv, stream, steps, N, world, rank, mode):
+    """The canonical hull rule (no LQRO_FLAG_QHULL_ORDER, k_lhull) on the
+    timed steps' inputs, beside the headline: its step time, and the rows
+    whose newV it moves beyond 1e-5 (relative) from the reference rule's
+    newV of the last timed step — the deviation the default rule would
+    carry.  Never in `value`."""
+    ref = d_newv.clone()
+    c = lqro.Context(lqro.config(N, HORIZON, N_POINTS, device=dev.index, **sh))
+    c.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
+    out = torch.zeros_like(d_newv)
+    for _ in range(2):
+        c.step_device(d_x.data_ptr(), d_vg.data_ptr(), out.data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        c.step_device(d_x.data_ptr(), d_vg.data_ptr(), out.data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    c.close()
+    rows = lqro.shard_row_ids(N, rank, world, mode)
+    a, b = out[rows].cpu().numpy(), ref[rows].cpu().numpy()
+    rel = np.abs(a - b).max(1) / np.maximum(np.abs(b).max(1), 1e-30)
+    return {"ms_per_step": el / steps * 1e3, "evals_per_s": len(rows) * (N - 1) * steps / el,
+            "hull_rule_rows_off": int((rel > 1e-5).sum()), "rows": len(rows),
+            "max_rel_newv_diff": float(rel.max()) if len(rel) else 0.0,
+            "note": "canonical facet rule (k_lhull), same inputs; rows_off = rows whose newV differs from "
+                    "the reference rule's beyond 1e-5 relative (this rank's rows)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -377,6 +406,10 @@ def main():
     # the closed loop runs before the probe creates a second context (whose
     # stream can share a hardware queue with this context's side stream)
     ctx.close()   # one context at a time: a second one's streams can share hardware queues
+    other = None
+    if args.hull_rule == "qhull":
+        other = canonical_rule_run(lqro, torch, dev, sh, gains, d_x, d_vg, d_newv, stream, args.steps, N, world, rank,
+                                   args.rows)
     closed = closed_loop(lqro, torch, dev, x, vg, gains, min(args.steps, 5), world, dist, rank, args.rows, flags)
     pk_ms = sweep_ms
     probe = "sweep (k_prio + k_pair launches + overlapped side hull), timed steps"
@@ -444,6 +477,7 @@ def main():
         "closed_loop": closed,
         "inside_hull_pairs_per_step": st["inside"],
         "hull_failures": st["hull_fail"],
+        "hull_rule_canonical": other,
         "hull_rule": ("reference: Qhull's facet order and first Fv vertex, strict <, loop-carried normal "
                       "(LQRO:925-968; k_qhull, LQRO_FLAG_QHULL_ORDER)" if args.hull_rule == "qhull" else
                       "canonical (a measured deviation from the reference's rule, DESIGN §5.1)"),

@@ -162,7 +162,7 @@ struct Q3S {
   double MAXabs_coord, MAXsumcoord, MAXwidth, NEARzero[3];
   double DISTround, MINvisible, MAXcoplanar, MINoutside, MINdenom, MINdenom_2, max_outside;
   double interior[3];
-  unsigned long long tph[24];
+  unsigned long long tph[32];   // LQRO_QHULL_PROFILE: phase cycles 0..20, counters 21..28
   unsigned long long tq;         // LQRO_QHULL_PROFILE: the last stamp
 };
 
@@ -172,76 +172,130 @@ struct Q3S {
 #else
 #define Q3T(k) do {} while (0)
 #endif
+// LQRO_QHULL_PROFILE counters: 21 insertions, 22 partitioned points, 23 located
+// chunks, 24 sequence events, 25 emitted destination groups
+#ifdef LQRO_QHULL_PROFILE
+#define Q3C(k, v) do { S.tph[k] += (unsigned long long)(v); } while (0)
+#else
+#define Q3C(k, v) do {} while (0)
+#endif
 
 // ---- facet fields: LDS below Q3_FL, the global record beyond ----
+// Every access names its address space: with two generic pointers the
+// compiler merges the LDS and the global load of an accessor into one flat
+// load behind a pointer select, and a flat load waits for every outstanding
+// global access (s_waitcnt vmcnt(0) lgkmcnt(0)).
+#define Q3_AS3 __attribute__((address_space(3)))
+#define Q3_AS1 __attribute__((address_space(1)))
+template <class T> __device__ __forceinline__ T q3_lds(const T& r) { return *(const Q3_AS3 T*)(&r); }
+template <class T> __device__ __forceinline__ void q3_lds_st(T& r, const T& v) { *(Q3_AS3 T*)(&r) = v; }
+template <class T> __device__ __forceinline__ T q3_glb(const T& r) { return *(const Q3_AS1 T*)(&r); }
+template <class T> __device__ __forceinline__ void q3_glb_st(T& r, const T& v) { *(Q3_AS1 T*)(&r) = v; }
+typedef double q3_v4d __attribute__((ext_vector_type(4)));
+typedef int q3_v4i __attribute__((ext_vector_type(4)));
+typedef unsigned q3_v2u __attribute__((ext_vector_type(2)));
+// the vector records (HIP's vector classes have no address-space copies)
+__device__ __forceinline__ double4 q3_lds(const double4& r) {
+  const q3_v4d v = *(const Q3_AS3 q3_v4d*)(&r);
+  return make_double4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void q3_lds_st(double4& r, const double4& v) {
+  q3_v4d t; t.x = v.x; t.y = v.y; t.z = v.z; t.w = v.w;
+  *(Q3_AS3 q3_v4d*)(&r) = t;
+}
+__device__ __forceinline__ ushort4 q3_lds(const ushort4& r) {
+  const q3_v2u v = *(const Q3_AS3 q3_v2u*)(&r);
+  return make_ushort4((unsigned short)(v.x & 0xffffu), (unsigned short)(v.x >> 16), (unsigned short)(v.y & 0xffffu),
+                      (unsigned short)(v.y >> 16));
+}
+__device__ __forceinline__ void q3_lds_st(ushort4& r, const ushort4& v) {
+  q3_v2u t;
+  t.x = (unsigned)v.x | ((unsigned)v.y << 16);
+  t.y = (unsigned)v.z | ((unsigned)v.w << 16);
+  *(Q3_AS3 q3_v2u*)(&r) = t;
+}
+__device__ __forceinline__ double4 q3_glb(const double4& r) {
+  const q3_v4d v = *(const Q3_AS1 q3_v4d*)(&r);
+  return make_double4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void q3_glb_st(double4& r, const double4& v) {
+  q3_v4d t; t.x = v.x; t.y = v.y; t.z = v.z; t.w = v.w;
+  *(Q3_AS1 q3_v4d*)(&r) = t;
+}
+__device__ __forceinline__ int4 q3_glb(const int4& r) {
+  const q3_v4i v = *(const Q3_AS1 q3_v4i*)(&r);
+  return make_int4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void q3_glb_st(int4& r, const int4& v) {
+  q3_v4i t; t.x = v.x; t.y = v.y; t.z = v.z; t.w = v.w;
+  *(Q3_AS1 q3_v4i*)(&r) = t;
+}
+
 __device__ __forceinline__ void q3_get(const Q3W& W, const Q3L& L, int f, double* q, int* nb, int* fa) {
   if (f < Q3_FL) {
-    const double4 p = L.pl[f];
-    const ushort4 t = L.tp[f];
+    const double4 p = q3_lds(L.pl[f]);
+    const ushort4 t = q3_lds(L.tp[f]);
     q[0] = p.x; q[1] = p.y; q[2] = p.z; q[3] = p.w;
     nb[0] = t.x; nb[1] = t.y; nb[2] = t.z; *fa = t.w;
   } else {
     const Q3G& g = W.G[f - Q3_FL];
-    q[0] = g.pl[0]; q[1] = g.pl[1]; q[2] = g.pl[2]; q[3] = g.pl[3];
-    nb[0] = g.nb[0]; nb[1] = g.nb[1]; nb[2] = g.nb[2]; *fa = g.fa;
+    const double4 p = q3_glb(*reinterpret_cast<const double4*>(g.pl));
+    const int4 t = q3_glb(*reinterpret_cast<const int4*>(g.nb));
+    q[0] = p.x; q[1] = p.y; q[2] = p.z; q[3] = p.w;
+    nb[0] = t.x; nb[1] = t.y; nb[2] = t.z; *fa = t.w;
   }
 }
 __device__ __forceinline__ void q3_pl(const Q3W& W, const Q3L& L, int f, double* q) {
-  if (f < Q3_FL) {
-    const double4 p = L.pl[f];
-    q[0] = p.x; q[1] = p.y; q[2] = p.z; q[3] = p.w;
-  } else {
-    const Q3G& g = W.G[f - Q3_FL];
-    q[0] = g.pl[0]; q[1] = g.pl[1]; q[2] = g.pl[2]; q[3] = g.pl[3];
-  }
+  const double4 p = f < Q3_FL ? q3_lds(L.pl[f]) : q3_glb(*reinterpret_cast<const double4*>(W.G[f - Q3_FL].pl));
+  q[0] = p.x; q[1] = p.y; q[2] = p.z; q[3] = p.w;
 }
 __device__ __forceinline__ int q3_nb(const Q3W& W, const Q3L& L, int f, int k) {
-  if (f < Q3_FL) return reinterpret_cast<const unsigned short*>(&L.tp[f])[k];
-  return W.G[f - Q3_FL].nb[k];
+  if (f < Q3_FL) return q3_lds(reinterpret_cast<const unsigned short*>(&L.tp[f])[k]);
+  return q3_glb(W.G[f - Q3_FL].nb[k]);
 }
 __device__ __forceinline__ void q3_tp(const Q3W& W, const Q3L& L, int f, int* nb, int* fa) {
   if (f < Q3_FL) {
-    const ushort4 t = L.tp[f];
+    const ushort4 t = q3_lds(L.tp[f]);
     nb[0] = t.x; nb[1] = t.y; nb[2] = t.z; *fa = t.w;
   } else {
-    const Q3G& g = W.G[f - Q3_FL];
-    nb[0] = g.nb[0]; nb[1] = g.nb[1]; nb[2] = g.nb[2]; *fa = g.fa;
+    const int4 t = q3_glb(*reinterpret_cast<const int4*>(W.G[f - Q3_FL].nb));
+    nb[0] = t.x; nb[1] = t.y; nb[2] = t.z; *fa = t.w;
   }
 }
 __device__ __forceinline__ int q3_fa(const Q3W& W, const Q3L& L, int f) {
-  return f < Q3_FL ? (int)L.tp[f].w : W.G[f - Q3_FL].fa;
+  return f < Q3_FL ? (int)q3_lds(L.tp[f].w) : q3_glb(W.G[f - Q3_FL].fa);
 }
 __device__ __forceinline__ unsigned q3_key(const Q3W& W, const Q3L& L, int f) {
-  return f < Q3_FL ? L.key[f] : W.G[f - Q3_FL].key;
+  return f < Q3_FL ? q3_lds(L.key[f]) : q3_glb(W.G[f - Q3_FL].key);
 }
 __device__ __forceinline__ unsigned q3_cc(const Q3W& W, const Q3L& L, int f) {
-  return f < Q3_FL ? L.cc[f] : W.G[f - Q3_FL].cc;
+  return f < Q3_FL ? q3_lds(L.cc[f]) : q3_glb(W.G[f - Q3_FL].cc);
 }
 __device__ __forceinline__ void q3_set_fa(const Q3W& W, Q3L& L, int f, int fa) {
-  if (f < Q3_FL) L.tp[f].w = (unsigned short)fa;
-  else W.G[f - Q3_FL].fa = fa;
+  if (f < Q3_FL) q3_lds_st(L.tp[f].w, (unsigned short)fa);
+  else q3_glb_st(W.G[f - Q3_FL].fa, fa);
 }
 __device__ __forceinline__ void q3_set_nb(const Q3W& W, Q3L& L, int f, int k, int v) {
-  if (f < Q3_FL) reinterpret_cast<unsigned short*>(&L.tp[f])[k] = (unsigned short)v;
-  else W.G[f - Q3_FL].nb[k] = v;
+  if (f < Q3_FL) q3_lds_st(reinterpret_cast<unsigned short*>(&L.tp[f])[k], (unsigned short)v);
+  else q3_glb_st(W.G[f - Q3_FL].nb[k], v);
 }
 __device__ __forceinline__ void q3_set_key(const Q3W& W, Q3L& L, int f, unsigned k) {
-  if (f < Q3_FL) L.key[f] = k;
-  else W.G[f - Q3_FL].key = k;
+  if (f < Q3_FL) q3_lds_st(L.key[f], k);
+  else q3_glb_st(W.G[f - Q3_FL].key, k);
 }
 __device__ __forceinline__ void q3_set_cc(const Q3W& W, Q3L& L, int f, unsigned c) {
-  if (f < Q3_FL) L.cc[f] = c;
-  else W.G[f - Q3_FL].cc = c;
+  if (f < Q3_FL) q3_lds_st(L.cc[f], c);
+  else q3_glb_st(W.G[f - Q3_FL].cc, c);
 }
 __device__ __forceinline__ void q3_set_facet(const Q3W& W, Q3L& L, int f, const double* q, int nb0, int nb1, int nb2,
                                              int fa) {
   if (f < Q3_FL) {
-    L.pl[f] = make_double4(q[0], q[1], q[2], q[3]);
-    L.tp[f] = make_ushort4((unsigned short)nb0, (unsigned short)nb1, (unsigned short)nb2, (unsigned short)fa);
+    q3_lds_st(L.pl[f], make_double4(q[0], q[1], q[2], q[3]));
+    q3_lds_st(L.tp[f], make_ushort4((unsigned short)nb0, (unsigned short)nb1, (unsigned short)nb2, (unsigned short)fa));
   } else {
     Q3G& g = W.G[f - Q3_FL];
-    *reinterpret_cast<double4*>(g.pl) = make_double4(q[0], q[1], q[2], q[3]);
-    *reinterpret_cast<int4*>(g.nb) = make_int4(nb0, nb1, nb2, fa);
+    q3_glb_st(*reinterpret_cast<double4*>(g.pl), make_double4(q[0], q[1], q[2], q[3]));
+    q3_glb_st(*reinterpret_cast<int4*>(g.nb), make_int4(nb0, nb1, nb2, fa));
   }
 }
 
@@ -299,6 +353,70 @@ __device__ __forceinline__ int q3_scan_add(int v) {
   v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);   // row_bcast:15 -> rows 1, 3
   v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);   // row_bcast:31 -> rows 2, 3
   return v;
+}
+
+// inclusive wave scan (max) of a double, -DBL_MAX where a lane has no
+// predecessor (DPP on the two halves)
+#define Q3_MAXSTEP(V, CTRL, RM)                                                                    \
+  do {                                                                                           \
+    const long long u_ = __double_as_longlong(V);                                                \
+    const int lo_ = __builtin_amdgcn_update_dpp(-1, (int)u_, CTRL, RM, 0xf, false);              \
+    const int hi_ = __builtin_amdgcn_update_dpp((int)0xFFEFFFFF, (int)(u_ >> 32), CTRL, RM, 0xf, false); \
+    V = fmax(V, __longlong_as_double(((long long)hi_ << 32) | (long long)(unsigned)lo_));        \
+  } while (0)
+__device__ __forceinline__ double q3_scan_max(double v) {
+  Q3_MAXSTEP(v, 0x111, 0xf);   // row_shr:1
+  Q3_MAXSTEP(v, 0x112, 0xf);   // row_shr:2
+  Q3_MAXSTEP(v, 0x114, 0xf);   // row_shr:4
+  Q3_MAXSTEP(v, 0x118, 0xf);   // row_shr:8
+  Q3_MAXSTEP(v, 0x142, 0xa);   // row_bcast:15 -> rows 1, 3
+  Q3_MAXSTEP(v, 0x143, 0xc);   // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
+// Qhull's outside-set placement (qh_partitionpoint: a point further than the
+// set's furthest point is appended and becomes the furthest; any other is
+// put second-to-last, before the furthest) for the lanes of grp in lane
+// order, all at once.  A point's slot is fixed when it arrives (the count
+// before it, less one) unless it is a new furthest point: that one stays
+// last until the next new furthest point arrives, and is then fixed just
+// before it.  The furthest point itself is held aside (cx, cy, cz, champ)
+// and written by the caller at the end.  Entries at or beyond lim are not
+// written (the caller reports the capacity).
+__device__ __forceinline__ void q3_place(const Q3W& W, unsigned long long grp, int lane, unsigned long long ltmask,
+                                         double dd, const HullPt& pt, int off, int lim, int& cnt, double& mx,
+                                         int& champ, double& cx, double& cy, double& cz) {
+  const bool mem = (grp >> lane) & 1ull;
+  const int cb = cnt + __popcll(grp & ltmask);   // points before this one in the set
+  double run = -DBL_MAX;                         // the largest distance among them
+  if (grp & (grp - 1ull)) {
+    const double inc = q3_scan_max(mem ? dd : -DBL_MAX);
+    run = __shfl_up(inc, 1);
+    if (lane == 0) run = -DBL_MAX;
+  }
+  if (cnt > 0) run = fmax(run, mx);
+  const bool rec = mem && (cb == 0 || run < dd);
+  const unsigned long long recm = __ballot(rec);
+  const unsigned long long prevm = recm & ltmask;
+  const int pl = prevm ? 63 - __clzll((long long)prevm) : lane;
+  const double px = __shfl(pt.x, pl), py = __shfl(pt.y, pl), pz = __shfl(pt.z, pl);
+  const int pq = __shfl(pt.q, pl);
+  if (mem && cb > 0 && off + cb - 1 < lim) {
+    HullPt r = pt;
+    if (rec) {   // the furthest point it displaces: the previous new furthest here, or the held one
+      if (prevm) { r.x = px; r.y = py; r.z = pz; r.q = pq; }
+      else { r.x = cx; r.y = cy; r.z = cz; r.q = champ; }
+      r.pad = 0;
+    }
+    W.sb[off + cb - 1] = r;
+  }
+  if (recm) {
+    const int l = 63 - __clzll((long long)recm);
+    champ = __builtin_amdgcn_readlane(pt.q, l);
+    cx = hl_rl(pt.x, l); cy = hl_rl(pt.y, l); cz = hl_rl(pt.z, l);
+    mx = hl_rl(dd, l);
+  }
+  cnt += __popcll(grp);
 }
 
 // ---- point location, per lane (geom_r.c) ----
@@ -515,6 +633,7 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
     int ev_pos = np, ev_kind = 0, ev_dst = -1;
     double ev_d = 0.0;
     for (int c = from & ~63; c < np; c += 64) {
+      Q3C(23, 1);
       const int pos = c + lane;
       const bool act = pos >= from && pos < np;
       int kind = 0, ls = 0, dst = -1, dfa = 0;
@@ -585,6 +704,7 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
       }
     }
     if (ev_pos < np) {
+      Q3C(24, 1);
       if (ev_kind & 1) {
         if (sharp) S.findbestnew = 1;
         else S.notsharp = 1;
@@ -705,6 +825,7 @@ __device__ inline void q3_emit_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int ndn
     }
     Q3T(16);
     unsigned long long todo = __ballot(g >= 0);
+    const unsigned long long ltmask = (1ull << lane) - 1ull;
     while (todo) {
       const int lead = __ffsll((long long)todo) - 1;
       const int gg = __builtin_amdgcn_readlane(g, lead);
@@ -715,25 +836,8 @@ __device__ inline void q3_emit_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int ndn
       int champ = L.dchamp[gg];
       double cx = L.dchp[3 * gg], cy = L.dchp[3 * gg + 1], cz = L.dchp[3 * gg + 2];
       const int off = L.doff[gg];
-      unsigned long long m = grp;
-      while (m) {
-        const int l = __ffsll((long long)m) - 1;
-        m &= m - 1;
-        const double dq = hl_rl(dd, l);
-        if (cnt == 0 || mx < dq) {
-          if (cnt > 0 && lane == 0) {   // the displaced furthest point stays at the end so far
-            HullPt r;
-            r.x = cx; r.y = cy; r.z = cz; r.q = champ; r.pad = 0;
-            W.sb[off + cnt - 1] = r;
-          }
-          champ = __builtin_amdgcn_readlane(pt.q, l);
-          cx = hl_rl(pt.x, l); cy = hl_rl(pt.y, l); cz = hl_rl(pt.z, l);
-          mx = dq;
-        } else if (lane == l) {
-          W.sb[off + cnt - 1] = pt;
-        }
-        cnt++;
-      }
+      q3_place(W, grp, lane, ltmask, dd, pt, off, W.SB, cnt, mx, champ, cx, cy, cz);
+      Q3C(25, 1);
       if (lane == 0) {
         L.dcnt[gg] = cnt; L.dmax[gg] = mx; L.dchamp[gg] = champ;
         L.dchp[3 * gg] = cx; L.dchp[3 * gg + 1] = cy; L.dchp[3 * gg + 2] = cz;
@@ -1000,25 +1104,8 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
         hl_sync();
         if (keep) W.pq[w + __popcll(bk & ltmask)] = pt.q;
         w += __popcll(bk);
-        unsigned long long bo = __ballot(out);
-        while (bo) {
-          const int l = __ffsll((long long)bo) - 1;
-          bo &= bo - 1;
-          const double dq = hl_rl(d, l);
-          if (cnt == 0 || dq > mx) {
-            if (cnt > 0 && lane == 0 && off + cnt - 1 < W.SB) {
-              HullPt r;
-              r.x = cx; r.y = cy; r.z = cz; r.q = champ; r.pad = 0;
-              W.sb[off + cnt - 1] = r;
-            }
-            champ = __builtin_amdgcn_readlane(pt.q, l);
-            cx = hl_rl(pt.x, l); cy = hl_rl(pt.y, l); cz = hl_rl(pt.z, l);
-            mx = dq;
-          } else if (lane == l && off + cnt - 1 < W.SB) {
-            W.sb[off + cnt - 1] = pt;
-          }
-          cnt++;
-        }
+        const unsigned long long bo = __ballot(out);
+        if (bo) q3_place(W, bo, lane, ltmask, d, pt, off, W.SB, cnt, mx, champ, cx, cy, cz);
         hl_sync();
       }
       if (cnt) {
@@ -1362,6 +1449,8 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     Q3T(5);
     const int sharp = q3_sharpnewfacets(S, L, lane);
     Q3T(20);
+    Q3C(21, 1);
+    Q3C(22, np2);
     if (np2) {
       int rg;
       double rd;
@@ -1529,7 +1618,8 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
     const int n = hull_points(A, L, Ti, Ni, xi, xj, vrel, W.Pr, W.Pf);
     Q3S S;
 #ifdef LQRO_QHULL_PROFILE
-    for (int k = 0; k < 24; k++) S.tph[k] = 0;
+    for (int k = 0; k < 32; k++) S.tph[k] = 0;
+    const unsigned long long tjob_ = __builtin_amdgcn_s_memtime();
 #endif
     S.status = 0;
     S.nalloc = 1;
@@ -1550,9 +1640,19 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
     q3_select(A, W, L, S, lane, xi, vrel, slot);
 #ifdef LQRO_QHULL_PROFILE
     S.tph[10] = __builtin_amdgcn_s_memtime() - tq_;
-    S.tph[11] = 1;
-    if (A.prof && lane == 0)
-      for (int k = 0; k < 24; k++) atomicAdd(&A.prof[k], S.tph[k]);
+    S.tph[27] = __builtin_amdgcn_s_memtime() - tjob_;   // the whole job (26: its max over jobs)
+    S.tph[28] = (unsigned long long)n;
+    if (A.prof && lane == 0) {
+      for (int k = 0; k < 32; k++)
+        if (k != 26 && k != 11) atomicAdd(&A.prof[k], S.tph[k]);
+      atomicMax(&A.prof[26], S.tph[27]);
+      // per job (words 32 + 2j): cycles; insertions | points << 20 | facet slots << 40
+      const unsigned long long j = atomicAdd(&A.prof[11], 1ull);
+      if (j < 4096) {
+        A.prof[32 + 2 * j] = S.tph[27];
+        A.prof[33 + 2 * j] = S.tph[21] | ((unsigned long long)n << 20) | ((unsigned long long)S.nalloc << 40);
+      }
+    }
 #endif
     if (A.ext_nf && lane == 0) *A.ext_nf = S.status;   // test hook: the build's status bits
     if (A.ext_facets) {                                  // test hook: the facet list in key order

@@ -816,7 +816,15 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   const bool known = inside_prev != ~0ull;
   const bool lhull = c->local_hull || c->qhull_order;   // k_lhull or k_qhull on the side
   int side = lhull ? c->lside_cus : c->side_cus;
-  if (lhull) {
+  if (c->qhull_order) {
+    // Qhull's build is one long dependent chain per pair (one wave per CU):
+    // the side takes one CU per expected hull, so every hot hull starts at
+    // once, leaving at least an eighth of the CUs to the sweep (unknown
+    // count: half the CUs)
+    const unsigned long long want = known ? inside_prev + inside_prev / 16 + 4 : (unsigned long long)(c->n_cu / 2);
+    side = (int)std::min<unsigned long long>((unsigned long long)(c->n_cu - c->n_cu / 8),
+                                             std::max<unsigned long long>((unsigned long long)side, want));
+  } else if (lhull) {
     // local hulls: at most ~3.7 inside-hull pairs per side CU (C3: 177 on
     // 48 CUs), widening up to half the CUs as the swarm gets denser
     if (known)
@@ -828,8 +836,10 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   }
   // local hulls: the overlap pays up to ~16 inside-hull pairs per CU of the
   // widest side (1,067 at 22 m: 15.5 vs 18.0 ms plain; 2,496 at 16 m: a tie)
+  // (Qhull's order: the overlap always pays, the hulls outlast the sweep)
   const long max_inside = c->hot_max_inside >= 0 ? c->hot_max_inside
-                                                  : (lhull ? 16L * std::max(side, c->n_cu / 2) : 4L * side);
+                          : c->qhull_order   ? LONG_MAX
+                          : (lhull ? 16L * std::max(side, c->n_cu / 2) : 4L * side);
   const bool crowded = known && inside_prev > (unsigned long long)max_inside;
   // with the local hull the side stream is k_pair(hot) -> k_lhull -> k_pair
   // (rows, the same row queue): no LDS-topology condition

@@ -31,5 +31,23 @@ ks = [k for k in range(24) if k != 11 and names[k] != "-"]
 tot = sum(int(out[k]) for k in ks)
 GHZ = 2.4   # s_memtime counts shader cycles (MI355X_MICROARCH.md, PMC units)
 for k in ks:
-    print(f"{names[k]:24s} {int(out[k]) / jobs / GHZ / 1e3:10.3f} ms/hull  {100 * int(out[k]) / max(tot, 1):5.1f}%")
-print("hulls", jobs, "total ms/hull", tot / jobs / GHZ / 1e3)
+    print(f"{names[k]:24s} {int(out[k]) / jobs / GHZ / 1e6:10.3f} ms/hull  {100 * int(out[k]) / max(tot, 1):5.1f}%")
+print("hulls", jobs, "phase sum ms/hull", tot / jobs / GHZ / 1e6)
+print("job ms/hull (mean, max)", int(out[27]) / jobs / GHZ / 1e6, int(out[26]) / GHZ / 1e6,
+      "points/hull", int(out[28]) / jobs)
+for k, nm in ((21, "insertions"), (22, "partitioned points"), (23, "located chunks"), (24, "sequence events"),
+              (25, "emitted groups")):
+    print(f"{nm:24s} {int(out[k]) / jobs:12.1f} per hull")
+nj = min(jobs, 4096)
+pj = out[32:32 + 2 * nj].reshape(nj, 2)
+cyc = pj[:, 0].astype(np.float64) / GHZ / 1e6
+ins = (pj[:, 1] & 0xFFFFF).astype(np.int64)
+npt = ((pj[:, 1] >> 20) & 0xFFFFF).astype(np.int64)
+nsl = (pj[:, 1] >> 40).astype(np.int64)
+o = np.argsort(-cyc)
+print("slowest hulls: ms, insertions, points, facet slots, us/insertion")
+for k in o[:8]:
+    print(f"  {cyc[k]:8.3f} {ins[k]:6d} {npt[k]:6d} {nsl[k]:6d} {1e3 * cyc[k] / max(ins[k], 1):8.2f}")
+print("us/insertion: all", 1e3 * cyc.sum() / max(ins.sum(), 1),
+      "slots < 2752:", 1e3 * cyc[nsl < 2752].sum() / max(ins[nsl < 2752].sum(), 1),
+      "slots >= 2752:", 1e3 * cyc[nsl >= 2752].sum() / max(ins[nsl >= 2752].sum(), 1), int((nsl >= 2752).sum()), "hulls")
