@@ -74,6 +74,7 @@ struct Q3W {
   double* pdd;            // HNP: its distance
   int* fq;                // QC: facets that received points, key order
   unsigned* fqk;          // QC: their key then
+  HullPt* fqc;            // QC: their furthest point then (q = -1: not recorded)
   int FC, SB, HNP, QC;
 };
 
@@ -85,7 +86,7 @@ __host__ __device__ inline size_t q3_worker_bytes(int HNP) {
   return q3_align(24 * (size_t)HNP) * 2 + q3_align(64 * NG) + q3_align(96 * FC) + q3_align(72 * Q3_NEWCAP) +
          q3_align(32 * (size_t)HNP) + q3_align(4 * FC) +
          q3_align(8 * FC) + q3_align(32 * SB) + q3_align(4 * (size_t)HNP) * 2 + q3_align(8 * (size_t)HNP) +
-         q3_align(4 * QC) * 2;
+         q3_align(4 * QC) * 2 + q3_align(32 * QC);
 }
 
 __device__ inline Q3W q3_worker(char* base, int HNP) {
@@ -111,6 +112,7 @@ __device__ inline Q3W q3_worker(char* base, int HNP) {
   W.pdd = reinterpret_cast<double*>(take(8 * (size_t)HNP));
   W.fq = reinterpret_cast<int*>(take(4 * (size_t)W.QC));
   W.fqk = reinterpret_cast<unsigned*>(take(4 * (size_t)W.QC));
+  W.fqc = reinterpret_cast<HullPt*>(take(32 * (size_t)W.QC));
   return W;
 }
 
@@ -151,6 +153,7 @@ struct Q3L {
   double dmax[Q3_ND];
   double dchp[3 * Q3_ND];            // the furthest point's coordinates
   int cop[Q3_COPCAP * 64];           // the horizon walks' coplanar facet sets, [k][lane]
+  unsigned short hvis[Q3_HZCAP * 64];  // the horizon walks' visited facets, [k][lane]
 };
 static_assert(sizeof(Q3L) <= 160 * 1024, "k_qhull's LDS exceeds a CU");
 
@@ -427,24 +430,33 @@ __device__ inline int q3_findbesthorizon(const Q3W& W, const Q3S& S, const Q3L& 
   int bestfacet = startfacet;
   const double searchdist = S.max_outside + 2 * S.DISTround + fmax(S.MINvisible, S.MAXcoplanar);
   double minsearch = *bestdist - searchdist;
-  int vis[Q3_HZCAP];
+  // the facets visited (qh.visit_id), in the lane's LDS column: a register
+  // array with a run-time length compiles to a select per slot and check
+  unsigned short* vis = const_cast<unsigned short*>(L.hvis) + (threadIdx.x & 63);
   int nvis = 0;
   int* cop = const_cast<int*>(L.cop) + (threadIdx.x & 63);   // qh.coplanarfacetset
   int ncop = 0;
   int nextfacet = -1, nextnb[3] = {-1, -1, -1};
-  vis[nvis++] = startfacet;
+  q3_lds_st(vis[0], (unsigned short)startfacet);
+  nvis = 1;
   int cur[3] = {q3_nb(W, L, startfacet, 0), q3_nb(W, L, startfacet, 1), q3_nb(W, L, startfacet, 2)};
   for (;;) {
     double q[3][4];
     int fl[3], nn[3][3];
     for (int k = 0; k < 3; k++) q3_get(W, L, cur[k], q[k], nn[k], &fl[k]);
+    bool seen3[3] = {false, false, false};
+    for (int t = 0; t < nvis; t++) {
+      const int v = q3_lds(vis[64 * t]);
+      seen3[0] |= v == cur[0]; seen3[1] |= v == cur[1]; seen3[2] |= v == cur[2];
+    }
     for (int k = 0; k < 3; k++) {
       const int nb = cur[k];
-      bool seen = false;
-      for (int t = 0; t < nvis; t++) seen |= vis[t] == nb;
+      // (a neighbour listed twice: the first takes it)
+      const bool seen = seen3[k] || (k >= 1 && nb == cur[0]) || (k == 2 && nb == cur[1]);
       if (seen) continue;
       if (nvis == Q3_HZCAP) { lstatus |= QHS_CAPACITY; return bestfacet; }
-      vis[nvis++] = nb;
+      q3_lds_st(vis[64 * nvis], (unsigned short)nb);
+      nvis++;
       if (!(fl[k] & QF_FLIPPED)) {
         const double dist = q3_distq(q[k], p);
         if (dist > *bestdist) {
@@ -870,12 +882,24 @@ __device__ inline void q3_emit_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int ndn
     const unsigned long long b = __ballot(has);
     if (has) {
       const int at = qt + __popcll(b & ((1ull << lane) - 1ull));
-      if (at < W.QC) { W.fq[at] = L.nslot[t]; W.fqk[at] = q3_key(W, L, L.nslot[t]); }
+      if (at < W.QC) {
+        W.fq[at] = L.nslot[t];
+        W.fqk[at] = q3_key(W, L, L.nslot[t]);
+        HullPt r;
+        r.x = L.dchp[3 * t]; r.y = L.dchp[3 * t + 1]; r.z = L.dchp[3 * t + 2]; r.q = L.dchamp[t]; r.pad = 0;
+        W.fqc[at] = r;
+      }
     }
     qt += __popcll(b);
   }
   for (int t = lane; t < S.nmov; t += 64)
-    if (qt + t < W.QC) { W.fq[qt + t] = L.movf[t]; W.fqk[qt + t] = q3_key(W, L, L.movf[t]); }
+    if (qt + t < W.QC) {
+      W.fq[qt + t] = L.movf[t];
+      W.fqk[qt + t] = q3_key(W, L, L.movf[t]);
+      HullPt r;
+      r.x = r.y = r.z = 0.0; r.q = -1; r.pad = 0;   // (rare: the apex is read from the points)
+      W.fqc[qt + t] = r;
+    }
   qt += S.nmov;
   if (qt > W.QC) S.status |= QHS_CAPACITY;
   S.qtail = qt;
@@ -1184,7 +1208,13 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
       int qt = 0;
       for (int i = 0; i < 4; i++)
         if (q3_cc(W, L, order[i]) & 0xffffu) {
-          if (lane == 0) { W.fq[qt] = order[i]; W.fqk[qt] = kk[i]; }
+          if (lane == 0) {
+            W.fq[qt] = order[i];
+            W.fqk[qt] = kk[i];
+            HullPt r;
+            r.x = r.y = r.z = 0.0; r.q = -1; r.pad = 0;
+            W.fqc[qt] = r;
+          }
           qt++;
         }
       S.qhead = 0;
@@ -1194,40 +1224,59 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
   }
   Q3T(0);
   // qh_buildhull
+  // the queue's next 64 entries stay in the lanes (lane k: entry qcb + k;
+  // entries never change once written, appends go to the tail), with the
+  // furthest point each facet had when it was queued
+  int qcb = 0, qcn = 0;
+  int qf = 0, qp = -1;
+  unsigned qk = 0;
+  double qx = 0.0, qy = 0.0, qz = 0.0;
   for (;;) {
     // qh_nextfurthest: the first queued facet still alive (same key) with
-    // points, 64 entries at a time
+    // points
     int facet = -1, furthest = -1;
+    double apexp[3] = {0.0, 0.0, 0.0};
     while (S.qhead < S.qtail) {
-      const int pos = S.qhead + lane;
+      if (S.qhead >= qcb + qcn) {
+        qcb = S.qhead;
+        qcn = min(64, S.qtail - S.qhead);
+        if (lane < qcn) {
+          qf = W.fq[qcb + lane];
+          qk = W.fqk[qcb + lane];
+          const HullPt e = W.fqc[qcb + lane];
+          qx = e.x; qy = e.y; qz = e.z; qp = e.q;
+        }
+      }
       bool ok = false;
-      int f = 0;
       unsigned c = 0;
-      if (pos < S.qtail) {
-        f = W.fq[pos];
-        const unsigned k = W.fqk[pos];
-        const int fa = q3_fa(W, L, f);
-        c = q3_cc(W, L, f);
-        ok = (fa & QF_LIVE) && q3_key(W, L, f) == k && (c & 0xffffu) > 0;
+      if (lane < qcn && qcb + lane >= S.qhead) {
+        const int fa = q3_fa(W, L, qf);
+        c = q3_cc(W, L, qf);
+        ok = (fa & QF_LIVE) && q3_key(W, L, qf) == qk && (c & 0xffffu) > 0;
       }
       const unsigned long long b = __ballot(ok);
       if (b) {
         const int l = __ffsll((long long)b) - 1;
-        S.qhead += l;
-        facet = __builtin_amdgcn_readlane(f, l);
+        S.qhead = qcb + l;
+        facet = __builtin_amdgcn_readlane(qf, l);
         const unsigned cf = (unsigned)__builtin_amdgcn_readlane((int)c, l);
         furthest = (int)(cf >> 16);
+        if (__builtin_amdgcn_readlane(qp, l) == furthest) {
+          apexp[0] = hl_rl(qx, l); apexp[1] = hl_rl(qy, l); apexp[2] = hl_rl(qz, l);
+        } else {   // a further point arrived since (or none was recorded)
+          apexp[0] = W.Pr[3 * (size_t)furthest];
+          apexp[1] = W.Pr[3 * (size_t)furthest + 1];
+          apexp[2] = W.Pr[3 * (size_t)furthest + 2];
+        }
         hl_sync();
         q3_set_cc(W, L, facet, (cf & 0xffffu) - 1u);   // qh_setdellast (the facet is visible: no new furthest)
         hl_sync();
         break;
       }
-      S.qhead += min(64, S.qtail - S.qhead);
+      S.qhead = qcb + qcn;
     }
     Q3T(1);
     if (furthest < 0) break;
-    const double apexp[3] = {W.Pr[3 * (size_t)furthest], W.Pr[3 * (size_t)furthest + 1],
-                             W.Pr[3 * (size_t)furthest + 2]};
     // qh_findhorizon, a level of the breadth-first search at a time: the
     // candidates of a level in (visible facet, neighbour) order, a facet
     // taken at its first occurrence
@@ -1251,17 +1300,19 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
           int nn[3];
           q3_get(W, L, nb, q, nn, &fa);
         }
-        bool cand = !(fa & QF_VISIBLE);
+        const bool cand = !(fa & QF_VISIBLE);
+        const double dist = cand ? q3_distq(q, apexp) : 0.0;
+        bool vis = cand && dist >= S.MINvisible;
+        if (cand && !vis && dist >= -S.MAXcoplanar) ls |= QHS_COPLANAR;   // Qhull merges it: built on merge-free
+        // a facet reached twice in this pass is taken at its first occurrence
+        // (its copies compute the same distance: only visible ones matter)
         bool dup = false;
-        for (unsigned long long mm = __ballot(cand); mm;) {
+        for (unsigned long long mm = __ballot(vis); mm;) {
           const int l = __ffsll((long long)mm) - 1;
           mm &= mm - 1;
           dup |= (l < lane) && __builtin_amdgcn_readlane(nb, l) == nb;
         }
-        cand = cand && !dup;
-        const double dist = cand ? q3_distq(q, apexp) : 0.0;
-        const bool vis = cand && dist >= S.MINvisible;
-        if (cand && !vis && dist >= -S.MAXcoplanar) ls |= QHS_COPLANAR;   // Qhull merges it: built on merge-free
+        vis = vis && !dup;
         const unsigned long long bv = __ballot(vis);
         if (vis) {
           const int at = nvis + __popcll(bv & ltmask);
@@ -1385,15 +1436,17 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     // the new facets' fields and vertex records; the horizon facets' links
     const unsigned key0 = S.keyc;
     auto finish = [&](int t, const double* p1, const double* p2) {
-      int nbu[2];
-      for (int k = 1; k < 3; k++) {
-        const int w = L.nv[3 * t + 3 - k];
-        int found = -1, cnt = 0;
-        for (int u = 0; u < nnew; u++)
-          if (u != t && (L.nv[3 * u + 1] == w || L.nv[3 * u + 2] == w)) { found = u; cnt++; }
-        if (cnt != 1) lm |= QHS_TOPOLOGY;
-        nbu[k - 1] = found;
+      // nb1: the other new facet with v2, nb2: the other one with v1 (one pass)
+      int nbu[2] = {-1, -1}, cnt[2] = {0, 0};
+      const int w0 = L.nv[3 * t + 2], w1 = L.nv[3 * t + 1];
+#pragma unroll 4
+      for (int u = 0; u < nnew; u++) {
+        const int a = L.nv[3 * u + 1], b = L.nv[3 * u + 2];
+        const bool o = u != t;
+        if (o && (a == w0 || b == w0)) { nbu[0] = u; cnt[0]++; }
+        if (o && (a == w1 || b == w1)) { nbu[1] = u; cnt[1]++; }
       }
+      if (cnt[0] != 1 || cnt[1] != 1) lm |= QHS_TOPOLOGY;
       L.nn1[t] = nbu[0] >= 0 ? nbu[0] : 0;
       L.nn2[t] = nbu[1] >= 0 ? nbu[1] : 0;
       const int s = L.nslot[t];
