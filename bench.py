@@ -251,10 +251,10 @@ def config_runs(lqro, torch, dev, local, world, rank, dist, steps, mode="block",
         d_vg = torch.from_numpy(vg).to(dev)
         d_newv = torch.zeros((N, 3), dtype=torch.float64, device=dev)
 
+        rowtab = torch.zeros((N, 4), dtype=torch.float64, device=dev)
+
         def step():
-            ctx.step_device(d_x.data_ptr(), d_vg.data_ptr(), d_newv.data_ptr(), 0)
-            if world > 1:
-                lqro.allgather_rows(dist, d_newv, rank, world, mode=mode)
+            lqro.step_rows(ctx, dist, d_x, d_vg, d_newv, rowtab, rank, world, mode)
         step()
         torch.cuda.synchronize(dev)
         if world > 1:
@@ -288,7 +288,7 @@ def canonical_rule_run(lqro, torch, dev, sh, gains, d_x, d_vg, d_newv, stream, s
     newV of the last timed step — the deviation the default rule would
     carry.  Never in `value`."""
     ref = d_newv.clone()
-    c = lqro.Context(lqro.config(N, HORIZON, N_POINTS, device=dev.index, **sh))
+    c = lqro.Context(lqro.config(N, HORIZON, N_POINTS, device=dev.index, flags=0, **sh))
     c.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
     out = torch.zeros_like(d_newv)
     for _ in range(2):
@@ -362,10 +362,11 @@ def main():
     d_newv = torch.zeros((N, 3), dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream(dev)
 
+    rowtab = torch.zeros((N, 4), dtype=torch.float64, device=dev)
+
     def step():
-        ctx.step_device(d_x.data_ptr(), d_vg.data_ptr(), d_newv.data_ptr(), stream.cuda_stream)
-        if world > 1:
-            lqro.allgather_rows(dist, d_newv, rank, world, mode=args.rows)
+        # (Qhull order, world > 1: split around the row-normal all-gather)
+        lqro.step_rows(ctx, dist, d_x, d_vg, d_newv, rowtab, rank, world, args.rows, stream)
 
     for _ in range(args.warmup):
         step()
@@ -415,7 +416,7 @@ def main():
     probe = "sweep (k_prio + k_pair launches + overlapped side hull), timed steps"
     if not args.no_roofline_probe:
         os.environ["LQRO_HOT"] = "0"
-        pctx = lqro.Context(lqro.config(N, HORIZON, N_POINTS, device=local, **sh))
+        pctx = lqro.Context(lqro.config(N, HORIZON, N_POINTS, device=local, flags=0, **sh))   # k_pair only
         del os.environ["LQRO_HOT"]
         pctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
         pk = []

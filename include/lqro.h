@@ -113,7 +113,10 @@ typedef struct lqro_pair_record {
 
 typedef struct lqro_ctx lqro_ctx;
 
-/* Defaults: LQRO's constants (N given by the caller). */
+/* Defaults: LQRO's constants (N given by the caller); flags =
+ * LQRO_FLAG_QHULL_ORDER, the reference's own inside-hull rule.  Clearing it
+ * selects the faster canonical facet rule, a measured deviation from the
+ * reference. */
 void lqro_config_default(lqro_config* cfg, int32_t n_agents, int32_t horizon, int32_t n_points);
 void lqro_model_default(lqro_model* m);
 
@@ -192,6 +195,25 @@ int lqro_step(lqro_ctx* ctx, const double* x, const double* vgoal, double* newv)
  * entry per pair slot, so a step cannot overflow it. */
 int lqro_step_device(lqro_ctx* ctx, const double* d_x, const double* d_vgoal,
                      double* d_newv, void* stream);
+
+/* lqro_step_device in two halves around the exchange a row-sharded caller
+ * needs in Qhull order (LQRO_FLAG_QHULL_ORDER): the loop-carried
+ * normalVector (LQRO:1385) runs through every pair of the swarm in (i, j)
+ * order, across the shards.  _begin enqueues the sweep and the hulls and
+ * writes, for each of the context's own rows i, the normal of its last pair
+ * with one: d_rowtab[4 i + 0..2], d_rowtab[4 i + 3] = 1 (0 0 0 0 for none, or
+ * without the flag).  The caller then fills the other ranks' rows of the
+ * n_agents x 4 table (an all-gather) and calls _end, which resolves the
+ * facet-0 pairs from the whole table (their own row's earlier pairs, else
+ * the last row before theirs with a normal, else the normal entering the
+ * step), runs the LP and writes d_newv.  Every rank then carries the same
+ * normal into the next step.  For a context that owns every row the two
+ * halves equal lqro_step_device.  lqro_step / lqro_step_device on a shard
+ * other than the first resolve facet-0 pairs from the context's own rows
+ * only. */
+int lqro_step_device_begin(lqro_ctx* ctx, const double* d_x, const double* d_vgoal,
+                           double* d_rowtab, void* stream);
+int lqro_step_device_end(lqro_ctx* ctx, const double* d_rowtab, double* d_newv, void* stream);
 
 /* calculateNewV (LQRO:1223-1234) for a batch of independent agents on the
  * GPU: agent r's planes are planes[offsets[r] .. offsets[r+1]) (6 floats

@@ -11,7 +11,10 @@
 // inside an iteration.
 //
 //   per iteration, on `stream`:
-//     lqro_step_device            the pair loop for rows [row_begin, row_end)
+//     lqro_step_device_begin      the pair loop's sweep and hulls for rows [row_begin, row_end)
+//     ncclAllGather               each row's last normal (the reference's loop-carried
+//                                 normalVector, LQRO:1385, runs through every row)
+//     lqro_step_device_end        the facet-0 pairs' normals, the LP: newV of the own rows
 //     hipMemcpyAsync              vGoal = newV (LQRO:1438), own rows
 //     lqro_dynamics_step_device   findU, propagate, kalmanFilter1/2, findVGoal (LQRO:1439-1445), own rows
 //     ncclAllGather               x of every agent, in place
@@ -70,6 +73,7 @@ class ShardedSimulator {
     alloc(&d_x_, npad * kX);
     alloc(&d_vg_, npad * kV);
     alloc(&d_newv_, npad * kV);
+    alloc(&d_rowtab_, npad * 4);
     alloc(&d_rot_, r * 9);
     alloc(&d_xt_, r * kX);
     alloc(&d_rott_, r * 9);
@@ -89,7 +93,7 @@ class ShardedSimulator {
   }
   ~ShardedSimulator() {
     if (comm_) ncclCommDestroy(comm_);
-    for (double* p : {d_x_, d_vg_, d_newv_, d_rot_, d_xt_, d_rott_, d_P_, d_ug_, d_pg_, d_nrm_, d_L_, d_E_, d_l_,
+    for (double* p : {d_x_, d_vg_, d_newv_, d_rowtab_, d_rot_, d_xt_, d_rott_, d_P_, d_ug_, d_pg_, d_nrm_, d_L_, d_E_, d_l_,
                       d_Lh_, d_Eh_, d_M_, d_N_})
       if (p) (void)hipFree(p);
     if (d_model_) (void)hipFree(d_model_);
@@ -127,7 +131,17 @@ class ShardedSimulator {
   uint32_t iterate(uint32_t seed) {
     nrm_.resize((size_t)n_ * LQRO_NORMALS_PER_AGENT);
     check(lqro_normals(&seed, (int64_t)nrm_.size(), nrm_.data()), "lqro_normals");
-    check(lqro_step_device(ctx_, d_x_, d_vg_, d_newv_, stream_), "lqro_step_device");
+    if (world_ > 1) {
+      // Qhull order (lqro_config_default): the normal entering each shard is
+      // the last one of the rows before it, on whichever rank
+      check(lqro_step_device_begin(ctx_, d_x_, d_vg_, d_rowtab_, stream_), "lqro_step_device_begin");
+      check_nccl(ncclAllGather(d_rowtab_ + (size_t)rank_ * chunk_ * 4, d_rowtab_, (size_t)chunk_ * 4, ncclDouble,
+                               comm_, stream_),
+                 "ncclAllGather");
+      check(lqro_step_device_end(ctx_, d_rowtab_, d_newv_, stream_), "lqro_step_device_end");
+    } else {
+      check(lqro_step_device(ctx_, d_x_, d_vg_, d_newv_, stream_), "lqro_step_device");
+    }
     if (rows_ > 0) {
       check_hip(hipMemcpyAsync(d_vg_ + (size_t)rb_ * kV, d_newv_ + (size_t)rb_ * kV, sizeof(double) * rows_ * kV,
                                hipMemcpyDeviceToDevice, stream_),
@@ -237,7 +251,7 @@ class ShardedSimulator {
   std::array<double, kX * kX> A_{};
   std::array<double, kX * kU> B_{};
   std::vector<double> nrm_;
-  double *d_x_ = nullptr, *d_vg_ = nullptr, *d_newv_ = nullptr, *d_rot_ = nullptr, *d_xt_ = nullptr,
+  double *d_x_ = nullptr, *d_vg_ = nullptr, *d_newv_ = nullptr, *d_rowtab_ = nullptr, *d_rot_ = nullptr, *d_xt_ = nullptr,
          *d_rott_ = nullptr, *d_P_ = nullptr, *d_ug_ = nullptr, *d_pg_ = nullptr, *d_nrm_ = nullptr, *d_L_ = nullptr,
          *d_E_ = nullptr, *d_l_ = nullptr, *d_Lh_ = nullptr, *d_Eh_ = nullptr, *d_M_ = nullptr, *d_N_ = nullptr;
   lqro_model* d_model_ = nullptr;

@@ -27,6 +27,11 @@ size_t qhull_worker_bytes(int hnp);
 void launch_stale(hipStream_t s, float* planes, const double* qnrm, const int* list, const int* count, int cap,
                   const double* x, int X, int npr, int row_begin, int row_stride, double* carry,
                   lqro_pair_record* recs, long nslots);
+void launch_rowlast(hipStream_t s, const float* planes, const double* qnrm, int npr, int nrows, int row_begin,
+                    int row_stride, double* rowtab);
+void launch_stale_rows(hipStream_t s, float* planes, const double* qnrm, const int* list, const int* count, int cap,
+                       const double* x, int X, int npr, int row_begin, int row_stride, const double* rowtab, int N,
+                       double* carry, lqro_pair_record* recs, long nslots);
 // controlMatrices for n models into out (stride X*X + 12X + 25 doubles):
 // k_synthw (one wave per agent) or, lane = true, k_synth (one agent per lane)
 void launch_synth(int x_dim, bool lane, const lqro_model* d_models, int n, double* d_out);

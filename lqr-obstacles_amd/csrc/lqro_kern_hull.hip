@@ -56,4 +56,18 @@ void launch_stale(hipStream_t s, float* planes, const double* qnrm, const int* l
                      row_stride, carry, recs, nslots);
 }
 
+void launch_rowlast(hipStream_t s, const float* planes, const double* qnrm, int npr, int nrows, int row_begin,
+                    int row_stride, double* rowtab) {
+  hipLaunchKernelGGL(k_rowlast, dim3((unsigned)std::min(std::max(nrows, 1), 4096)), dim3(64), 0, s, planes, qnrm, npr,
+                     nrows, row_begin, row_stride, rowtab);
+}
+
+void launch_stale_rows(hipStream_t s, float* planes, const double* qnrm, const int* list, const int* count, int cap,
+                       const double* x, int X, int npr, int row_begin, int row_stride, const double* rowtab, int N,
+                       double* carry, lqro_pair_record* recs, long nslots) {
+  (void)nslots;
+  hipLaunchKernelGGL(k_stale_rows, dim3(16), dim3(64), 0, s, planes, qnrm, list, count, cap, x, X, npr, row_begin,
+                     row_stride, rowtab, N, carry, recs);
+}
+
 }  // namespace lqro

@@ -1389,4 +1389,99 @@ __global__ void __launch_bounds__(64) k_stale(float* planes, const double* qnrm,
   }
 }
 
+// Row shards (lqro_step_device_begin / _end): the loop-carried normal
+// crosses the shard boundaries.  k_rowlast leaves, per own row, the normal of
+// its last pair with one (rowtab[4 i + 0..2], rowtab[4 i + 3] = 1; 0 0 0 0
+// for none, or without Qhull order: planes == nullptr); the caller gathers
+// every rank's rows.  k_stale_rows then resolves a facet-0 pair from its own
+// row's earlier slots, else the last row before it (any rank) with a normal,
+// else the carry entering the step — the reference's (t, i, j) order over
+// the whole swarm — and leaves the swarm's last normal in carry[3..5].
+__global__ void __launch_bounds__(64) k_rowlast(const float* planes, const double* qnrm, int npr, int nrows,
+                                                int row_begin, int row_stride, double* rowtab) {
+  const int lane = threadIdx.x & 63;
+  for (int r = blockIdx.x; r < nrows; r += gridDim.x) {
+    const long s_lo = (long)r * npr;
+    long found = -1;
+    if (planes)
+      for (long b = s_lo + npr - 1; b >= s_lo && found < 0; b -= 64) {
+        const long sl = b - lane;
+        const bool hit = sl >= s_lo && qh_slot_normal(planes, qnrm, sl);
+        const unsigned long long m = __ballot(hit);
+        if (m) found = b - (__ffsll((long long)m) - 1);
+      }
+    if (lane == 0) {
+      double* o = rowtab + 4 * ((size_t)row_begin + (size_t)r * row_stride);
+      for (int k = 0; k < 3; k++) o[k] = found >= 0 ? qnrm[(size_t)found * 4 + k] : 0.0;
+      o[3] = found >= 0 ? 1.0 : 0.0;
+    }
+  }
+}
+
+// the last row before `i` (agent order) with a normal: its index, or -1
+__device__ __forceinline__ int qh_row_before(const double* rowtab, int i) {
+  const int lane = threadIdx.x & 63;
+  for (int b = i - 1; b >= 0; b -= 64) {
+    const int r = b - lane;
+    const bool hit = r >= 0 && rowtab[4 * (size_t)r + 3] != 0.0;
+    const unsigned long long m = __ballot(hit);
+    if (m) return b - (__ffsll((long long)m) - 1);
+  }
+  return -1;
+}
+
+__global__ void __launch_bounds__(64) k_stale_rows(float* planes, const double* qnrm, const int* list,
+                                                   const int* count, int cap, const double* x, int X, int npr,
+                                                   int row_begin, int row_stride, const double* rowtab, int N,
+                                                   double* carry, lqro_pair_record* recs) {
+  const int lane = threadIdx.x & 63;
+  const int n = min(*count, cap);
+  for (int e = blockIdx.x; e <= n; e += gridDim.x) {
+    double nrm[3];
+    if (e == n) {   // the normal the swarm's last eligible pair leaves
+      const int r = qh_row_before(rowtab, N);
+      for (int k = 0; k < 3; k++) nrm[k] = r >= 0 ? rowtab[4 * (size_t)r + k] : carry[k];
+      if (lane == 0)
+        for (int k = 0; k < 3; k++) carry[3 + k] = nrm[k];
+      continue;
+    }
+    const long s0 = (long)list[e];
+    const int lrow = (int)(s0 / npr);
+    const long s_lo = (long)lrow * npr;
+    const int i = row_begin + lrow * row_stride;
+    long found = -1;
+    for (long b = s0 - 1; b >= s_lo && found < 0; b -= 64) {
+      const long sl = b - lane;
+      const bool hit = sl >= s_lo && qh_slot_normal(planes, qnrm, sl);
+      const unsigned long long m = __ballot(hit);
+      if (m) found = b - (__ffsll((long long)m) - 1);
+    }
+    if (found >= 0) {
+      for (int k = 0; k < 3; k++) nrm[k] = qnrm[(size_t)found * 4 + k];
+    } else {
+      const int r = qh_row_before(rowtab, i);
+      for (int k = 0; k < 3; k++) nrm[k] = r >= 0 ? rowtab[4 * (size_t)r + k] : carry[k];
+    }
+    if (lane != 0) continue;
+    const double* xi = x + (size_t)i * X;
+    const double dh = qnrm[(size_t)s0 * 4 + 3] * 0.5;   // :1416
+    const double mult = 1.0;                            // :1213
+    float* pl = planes + (size_t)s0 * 8;
+    pl[0] = (float)(xi[3] + mult * dh * nrm[0]);
+    pl[1] = (float)(xi[4] + mult * dh * nrm[1]);
+    pl[2] = (float)(xi[5] + mult * dh * nrm[2]);
+    pl[3] = (float)nrm[0]; pl[4] = (float)nrm[1]; pl[5] = (float)nrm[2];
+    pl[7] = 0.0f;
+    __hip_atomic_store(reinterpret_cast<int*>(pl + 6), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (recs) {
+      lqro_pair_record& rec = recs[s0];
+      for (int q = 0; q < 3; ++q) {
+        rec.normal[q] = nrm[q];
+        rec.plane_point[q] = pl[q];
+        rec.plane_normal[q] = pl[3 + q];
+      }
+    }
+  }
+}
+
 }  // namespace lqro

@@ -399,6 +399,10 @@ struct lqro_ctx {
   unsigned long long* d_prof;
   int lds_bytes;
   int stepped;               // a step was enqueued (ev[3] recorded)
+  int pending;               // lqro_step_device_begin ran, _end not yet
+  const double* pend_x;
+  const double* pend_vgoal;
+  hipStream_t pend_stream;
   int lhull_prof;            // LQRO_LHULL_PROFILE: k_lhull writes its per-job words
   // LQRO_FLAG_QHULL_ORDER: k_qhull workers, per-slot normals, facet-0 slots,
   // the loop-carried normal in [0..2], out [3..5]
@@ -464,7 +468,7 @@ void lqro_config_default(lqro_config* c, int32_t n, int32_t h, int32_t np) {
   c->row_end = 0;
   c->row_stride = 0;
   c->device = 0;
-  c->flags = 0;
+  c->flags = LQRO_FLAG_QHULL_ORDER;   // the reference's own inside-hull rule (drop-in default)
 }
 
 void lqro_destroy(lqro_ctx* c) {
@@ -738,8 +742,16 @@ int lqro_set_gains(lqro_ctx* c, const double* A, const double* B, const double* 
   return LQRO_OK;
 }
 
+static int enqueue_tail(lqro_ctx* c, const double* d_x, const double* d_vgoal, double* d_newv, hipStream_t s,
+                        const double* d_rowtab);
+
+// phase 0: the whole step.  Row shards in Qhull order split it around the
+// exchange of the loop-carried normal (lqro_step_device_begin / _end):
+// phase 1 runs the sweep and the hulls and writes each own row's last
+// normal into d_rowtab; phase 2 (enqueue_tail) resolves the facet-0 pairs
+// against every rank's rows and runs the LP.
 static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, double* d_newv,
-                        hipStream_t s) {
+                        hipStream_t s, int phase = 0, double* d_rowtab = nullptr) {
   const lqro_config& g = c->cfg;
   PairArgs P = c->pa;
   P.N = g.n_agents; P.H = g.horizon; P.NP = g.n_points; P.min_reach = g.min_reach;
@@ -957,9 +969,11 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
     launch_qhull_big(dim3(c->qworkers), s, Hh);
     HIPCHK(hipGetLastError());
     Hh.big_main = 0;
-    launch_stale(s, c->d_planes, c->d_qnrm, c->d_qstale, c->d_hcount + 15, c->hull_cap, d_x, g.x_dim, npr, c->rb,
-                 c->rs, c->d_carry, c->d_recs, slots);
-    HIPCHK(hipGetLastError());
+    if (phase == 0) {
+      launch_stale(s, c->d_planes, c->d_qnrm, c->d_qstale, c->d_hcount + 15, c->hull_cap, d_x, g.x_dim, npr, c->rb,
+                   c->rs, c->d_carry, c->d_recs, slots);
+      HIPCHK(hipGetLastError());
+    }
   } else if (c->local_hull) {
     // k_lhull takes the queue k_pair filled; k_hull / k_hull_big then take
     // the pairs it handed over (scratch: hull_blocks blocks of 6 H*NP doubles)
@@ -979,6 +993,31 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipEventRecord(c->ev[2], s));
+  if (phase == 1) {
+    // each own row's last normal (none without Qhull order)
+    launch_rowlast(s, c->qhull_order ? c->d_planes : nullptr, c->d_qnrm, npr, c->nrows, c->rb, c->rs, d_rowtab);
+    HIPCHK(hipGetLastError());
+    c->pend_x = d_x;
+    c->pend_vgoal = d_vgoal;
+    c->pend_stream = s;
+    c->pending = 1;
+    return LQRO_OK;
+  }
+  return enqueue_tail(c, d_x, d_vgoal, d_newv, s, nullptr);
+}
+
+static int enqueue_tail(lqro_ctx* c, const double* d_x, const double* d_vgoal, double* d_newv, hipStream_t s,
+                        const double* d_rowtab) {
+  const lqro_config& g = c->cfg;
+  const int npr = c->nbr_k > 0 ? std::min(c->nbr_k, c->npr) : c->npr;
+  const long slots = (long)c->nrows * npr;
+  const int slot = (int)(c->nstep & 1);
+  if (d_rowtab && c->qhull_order) {
+    launch_stale_rows(s, c->d_planes, c->d_qnrm, c->d_qstale, c->d_hcount + 15, c->hull_cap, d_x, g.x_dim, npr,
+                      c->rb, c->rs, d_rowtab, g.n_agents, c->d_carry, c->d_recs, slots);
+    HIPCHK(hipGetLastError());
+  }
+  c->pending = 0;
   LpArgs La;
   La.npr = npr; La.nrows = c->nrows; La.row_begin = c->rb; La.row_stride = c->rs; La.vmax = g.vmax_lp;
   La.slots = c->d_planes; La.compact = c->d_lpcompact; La.proj = c->d_lpscratch;
@@ -999,14 +1038,34 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
 int lqro_step_device(lqro_ctx* c, const double* d_x, const double* d_vgoal, double* d_newv,
                      void* stream) {
   if (!c || !d_x || !d_vgoal || !d_newv) return LQRO_E_ARG;
-  if (!c->have_gains) return LQRO_E_STATE;
+  if (!c->have_gains || c->pending) return LQRO_E_STATE;
   HIPCHK(hipSetDevice(c->cfg.device));
   return enqueue_step(c, d_x, d_vgoal, d_newv, (hipStream_t)stream);
 }
 
+int lqro_step_device_begin(lqro_ctx* c, const double* d_x, const double* d_vgoal, double* d_rowtab, void* stream) {
+  if (!c || !d_x || !d_vgoal || !d_rowtab) return LQRO_E_ARG;
+  if (!c->have_gains) return LQRO_E_STATE;
+  if (c->pending) return LQRO_E_STATE;
+  HIPCHK(hipSetDevice(c->cfg.device));
+  return enqueue_step(c, d_x, d_vgoal, nullptr, (hipStream_t)stream, 1, d_rowtab);
+}
+
+int lqro_step_device_end(lqro_ctx* c, const double* d_rowtab, double* d_newv, void* stream) {
+  if (!c || !d_rowtab || !d_newv) return LQRO_E_ARG;
+  if (!c->pending) return LQRO_E_STATE;
+  HIPCHK(hipSetDevice(c->cfg.device));
+  hipStream_t s = (hipStream_t)stream;
+  if (s != c->pend_stream) {   // the begin's work first
+    HIPCHK(hipEventRecord(c->xev[0], c->pend_stream));
+    HIPCHK(hipStreamWaitEvent(s, c->xev[0], 0));
+  }
+  return enqueue_tail(c, c->pend_x, c->pend_vgoal, d_newv, s, d_rowtab);
+}
+
 int lqro_step(lqro_ctx* c, const double* x, const double* vgoal, double* newv) {
   if (!c || !x || !vgoal || !newv) return LQRO_E_ARG;
-  if (!c->have_gains) return LQRO_E_STATE;
+  if (!c->have_gains || c->pending) return LQRO_E_STATE;
   const lqro_config& g = c->cfg;
   HIPCHK(hipSetDevice(g.device));
   const size_t N = g.n_agents, X = g.x_dim;

@@ -77,6 +77,7 @@ EXPORTS = (
     "lqro_dynamics_step", "lqro_dynamics_step_device", "lqro_normals", "lqro_set_neighbors",
     "lqro_synthesize_gains_x", "lqro_synthesize_gains_batch_x",
     "lqro_set_carry_normal", "lqro_get_carry_normal",
+    "lqro_step_device_begin", "lqro_step_device_end",
 )
 
 NORMALS_PER_AGENT = 22   # LQRO_NORMALS_PER_AGENT: 16 propagate + 6 observation
@@ -114,6 +115,8 @@ def lib() -> C.CDLL:
         L.lqro_set_gains.argtypes = [vp, vp, vp, vp, vp, i32]
         L.lqro_step.argtypes = [vp, vp, vp, vp]
         L.lqro_step_device.argtypes = [vp, vp, vp, vp, vp]
+        L.lqro_step_device_begin.argtypes = [vp, vp, vp, vp, vp]
+        L.lqro_step_device_end.argtypes = [vp, vp, vp, vp]
         L.lqro_get_records.argtypes = [vp, vp, i64, C.POINTER(i64)]
         L.lqro_get_stats.argtypes = [vp, vp]
         L.lqro_get_timings.argtypes = [vp, vp]
@@ -276,6 +279,20 @@ class Context:
         _check(lib().lqro_step_device(self._h, C.c_void_p(d_x), C.c_void_p(d_vgoal),
                                       C.c_void_p(d_newv), C.c_void_p(stream or None)),
                "lqro_step_device")
+
+    def step_device_begin(self, d_x: int, d_vgoal: int, d_rowtab: int, stream: int = 0):
+        """The first half of step_device for row shards in Qhull order: sweep
+        and hulls; this context's rows of the (N, 4) row-normal table
+        d_rowtab are written (lqro_step_device_begin)."""
+        _check(lib().lqro_step_device_begin(self._h, C.c_void_p(d_x), C.c_void_p(d_vgoal),
+                                            C.c_void_p(d_rowtab), C.c_void_p(stream or None)),
+               "lqro_step_device_begin")
+
+    def step_device_end(self, d_rowtab: int, d_newv: int, stream: int = 0):
+        """The second half, once every rank's rows of d_rowtab are present:
+        the facet-0 pairs' loop-carried normals, then the LP."""
+        _check(lib().lqro_step_device_end(self._h, C.c_void_p(d_rowtab), C.c_void_p(d_newv),
+                                          C.c_void_p(stream or None)), "lqro_step_device_end")
 
     def records(self) -> np.ndarray:
         n = len(self.row_ids) * (self.cfg.n_agents - 1)
@@ -498,10 +515,14 @@ class Simulator:
     once, then ``step()`` each control step fills every ``Quadrotor.newV``."""
 
     def __init__(self, qlist, horizon: int = 45, n_points: int = 100, device: int = 0,
-                 records: bool = False, model: Model | None = None):
+                 records: bool = False, model: Model | None = None, hull_rule: str = "reference"):
         self.qlist = list(qlist)
         self.model = model or default_model()
-        flags = LQRO_FLAG_RECORDS if records else 0
+        # hull_rule "reference": the reference's own inside-hull rule (Qhull's
+        # order, LQRO:925-968); "canonical": the faster deviating rule (DESIGN §5.1)
+        if hull_rule not in ("reference", "canonical"):
+            raise ValueError(f"hull_rule {hull_rule!r}")
+        flags = (LQRO_FLAG_RECORDS if records else 0) | (LQRO_FLAG_QHULL_ORDER if hull_rule == "reference" else 0)
         self.device = device
         self.t = 0                 # control steps taken (LQRO:1392)
         self.trajectory = []       # keyframes per step (update())
@@ -604,6 +625,27 @@ def shard_row_ids(n_agents: int, rank: int, world: int, mode: str = "block") -> 
     return np.arange(f["row_begin"], f["row_end"], max(f["row_stride"], 1))
 
 
+def step_rows(ctx, dist, x, vgoal, newv, rowtab, rank: int, world: int, mode: str = "block", stream=None):
+    """One pair-loop step of this rank's rows on torch device tensors, then
+    the all-gather of newV.  In Qhull order with more than one rank the step
+    is split around the all-gather of the (N, 4) row-normal table `rowtab`
+    (lqro_step_device_begin / _end): the loop-carried normalVector
+    (LQRO:1385) runs through the whole swarm's pairs in (i, j) order."""
+    import torch
+    st = stream if stream is not None else torch.cuda.current_stream(x.device)
+    sid = st.cuda_stream
+    if world > 1 and ctx.cfg.flags & LQRO_FLAG_QHULL_ORDER:
+        ctx.step_device_begin(x.data_ptr(), vgoal.data_ptr(), rowtab.data_ptr(), sid)
+        with torch.cuda.stream(st):
+            allgather_rows(dist, rowtab, rank, world, mode=mode)
+        ctx.step_device_end(rowtab.data_ptr(), newv.data_ptr(), sid)
+    else:
+        ctx.step_device(x.data_ptr(), vgoal.data_ptr(), newv.data_ptr(), sid)
+    if world > 1:
+        with torch.cuda.stream(st):
+            allgather_rows(dist, newv, rank, world, mode=mode)
+
+
 def allgather_rows(dist, full, rank: int, world: int, group=None, mode: str = "block"):
     """The per-step exchange: every rank holds its own rows of `full`
     (an (N, k) tensor, rows from shard_rows(mode)); afterwards every rank
@@ -655,7 +697,7 @@ class DeviceLoop:
     def __init__(self, x0, vgoal0, gains: dict, horizon: int, n_points: int = 100, *,
                  p_goal=None, rank: int = 0, world: int = 1, dist=None, device=None,
                  model: Model | None = None, seed: int = 1, stream=None, rows: str = "block",
-                 flags: int = 0):
+                 flags: int = LQRO_FLAG_QHULL_ORDER):
         import torch
         self.torch = torch
         self.dev = torch.device("cuda", torch.cuda.current_device()) if device is None else device
@@ -677,6 +719,8 @@ class DeviceLoop:
         self.x = torch.from_numpy(np.ascontiguousarray(x0, np.float64)).to(self.dev)
         self.vgoal = torch.from_numpy(np.ascontiguousarray(vgoal0, np.float64)).to(self.dev)
         self.newv = torch.zeros((n, 3), **f64)
+        self.flags = flags
+        self.rowtab = torch.zeros((n, 4), **f64)   # per-row loop-carried normals (Qhull order, world > 1)
         eye3 = torch.eye(3, **f64).repeat(rows, 1, 1).contiguous()
         hover = self.model.gravity * self.model.mass / 4
         pg = np.zeros((n, 3)) if p_goal is None else np.asarray(p_goal, np.float64)
@@ -699,7 +743,16 @@ class DeviceLoop:
     def step(self, gather: bool = False):
         """The pair loop for the own rows; newV of the own rows on the device
         (all rows with gather=True: one all-gather of newV)."""
-        self.ctx.step_device(self.x.data_ptr(), self.vgoal.data_ptr(), self.newv.data_ptr(), self._sid())
+        if self.world > 1 and self.flags & LQRO_FLAG_QHULL_ORDER:
+            # the loop-carried normal crosses the shards: the row-normal
+            # table's all-gather between the hulls and the LP
+            self.ctx.step_device_begin(self.x.data_ptr(), self.vgoal.data_ptr(), self.rowtab.data_ptr(),
+                                       self._sid())
+            with self.torch.cuda.stream(self.stream):
+                allgather_rows(self.dist, self.rowtab, self.rank, self.world, mode=self.mode)
+            self.ctx.step_device_end(self.rowtab.data_ptr(), self.newv.data_ptr(), self._sid())
+        else:
+            self.ctx.step_device(self.x.data_ptr(), self.vgoal.data_ptr(), self.newv.data_ptr(), self._sid())
         if gather and self.world > 1:
             with self.torch.cuda.stream(self.stream):
                 allgather_rows(self.dist, self.newv, self.rank, self.world, mode=self.mode)

@@ -12,7 +12,7 @@ for path in libs:
     lqro._lib = None
     lqro.LIB_PATH = path
     L = lqro.lib()
-    c = lqro.Context(lqro.config(N, H, NP))
+    c = lqro.Context(lqro.config(N, H, NP, flags=0))
     c.set_gains(g["A"], g["B"], g["L"], g["E"])
     ctxs.append((path, c, L))
 res = {p: [] for p in libs}

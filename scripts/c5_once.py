@@ -15,7 +15,7 @@ steps = int(os.environ.get("C5_STEPS", "2"))
 g = lqro.synthesize_gains_batch(lqro.perturbed_models(N), x_dim=X)
 A, B = lqro.synthesize_gains(x_dim=X)["A"], lqro.synthesize_gains(x_dim=X)["B"]
 x, vg = lqro.synthetic_swarm(N, x_dim=X)
-ctx = lqro.Context(lqro.config(N, H, NP, x_dim=X, row_begin=rows[0], row_end=rows[1]))
+ctx = lqro.Context(lqro.config(N, H, NP, x_dim=X, row_begin=rows[0], row_end=rows[1], flags=0))
 ctx.set_gains(A, B, g["L"], g["E"], per_agent=True)
 for s in range(steps):
     t0 = time.perf_counter()
@@ -27,7 +27,7 @@ ctx.close()
 # capacity, 4 = face capacity, 6 = segment buffer, 9 = stall guard, 11 = queue)
 import ctypes as C  # noqa: E402
 import numpy as np  # noqa: E402
-ctx = lqro.Context(lqro.config(N, H, NP, x_dim=X, row_begin=rows[0], row_end=rows[1]))
+ctx = lqro.Context(lqro.config(N, H, NP, x_dim=X, row_begin=rows[0], row_end=rows[1], flags=0))
 ctx.set_gains(A, B, g["L"], g["E"], per_agent=True)
 ctx.step(x, vg)
 out = np.zeros(32 + 2 * 4096 + 32, np.uint64)

@@ -13,7 +13,7 @@ if len(sys.argv) > 1 and sys.argv[1] == "--one":
     side = float(sys.argv[2])
     x, vg = lqro.synthetic_swarm(1024, box=side)
     g = lqro.synthesize_gains()
-    c = lqro.Context(lqro.config(1024, 100, 100))
+    c = lqro.Context(lqro.config(1024, 100, 100, flags=0))
     c.set_gains(g["A"], g["B"], g["L"], g["E"])
     t = []
     for rnd in range(5):

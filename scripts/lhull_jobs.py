@@ -18,7 +18,7 @@ box = float(sys.argv[1]) if len(sys.argv) > 1 else None
 N, H, NP = 1024, 100, 100
 x, vg = lqro.synthetic_swarm(N, box=box, seed=7) if box else lqro.synthetic_swarm(N)
 g = lqro.synthesize_gains()
-ctx = lqro.Context(lqro.config(N, H, NP))
+ctx = lqro.Context(lqro.config(N, H, NP, flags=0))
 ctx.set_gains(g["A"], g["B"], g["L"], g["E"])
 for _ in range(3):
     ctx.step(x, vg)

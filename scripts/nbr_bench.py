@@ -18,7 +18,7 @@ def main():
     out = []
     for N, k, r in ((4096, 16, 6.0), (16384, 16, 6.0), (16384, 32, 8.0)):
         x, vg = lqro.synthetic_swarm(N)
-        ctx = lqro.Context(lqro.config(N, 100, 100))
+        ctx = lqro.Context(lqro.config(N, 100, 100, flags=0))
         ctx.set_gains(g["A"], g["B"], g["L"], g["E"])
         ctx.set_neighbors(r, k)
         ctx.step(x, vg)

@@ -8,7 +8,7 @@ x, vg = lqro.synthetic_swarm(N)
 g = lqro.synthesize_gains()
 import os
 os.environ.setdefault("LQRO_HOT", "0")   # one k_pair launch over all pairs
-ctx = lqro.Context(lqro.config(N, H, NP))
+ctx = lqro.Context(lqro.config(N, H, NP, flags=0))
 ctx.set_gains(g["A"], g["B"], g["L"], g["E"])
 for _ in range(steps):
     ctx.step(x, vg)

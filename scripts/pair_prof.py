@@ -7,7 +7,7 @@ L = lqro.lib()
 N, H, NP = 1024, 100, 100
 x, vg = lqro.synthetic_swarm(N)
 g = lqro.synthesize_gains()
-c = lqro.Context(lqro.config(N, H, NP))
+c = lqro.Context(lqro.config(N, H, NP, flags=0))
 c.set_gains(g["A"], g["B"], g["L"], g["E"])
 c.step(x, vg)
 print(c.timings(), c.stats())

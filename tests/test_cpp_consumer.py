@@ -60,15 +60,21 @@ def test_cpp_consumer_matches_oracle(demo, lqro_mod, oracle, tmp_path):
     ref = lqro_mod.agent_states(x, p_goal=pg)
     ref["vgoal"][:] = vg
     sd = seed
-    for t in range(steps):
-        newv = out[t, :N * 3].reshape(N, 3)
-        xs = out[t, N * 3:].reshape(N, 16)
-        rv, rr = oracle.step(T, NCF, S, ref["x"], ref["vgoal"], threads=8)
-        if t == 0:
-            assert np.array_equal(newv.view(np.uint64), rv.view(np.uint64))
-        else:   # x went through one GPU dynamics step (libm last-bit differences)
-            np.testing.assert_allclose(newv, rv, rtol=1e-5, atol=1e-6)
-        ref["vgoal"][:] = rv
-        nrm, sd = lqro_mod.normals(sd, N * lqro_mod.NORMALS_PER_AGENT)
-        oracle.agent_step(ref, g, nrm)
-        np.testing.assert_allclose(xs, ref["x"], rtol=1e-7, atol=1e-9)
+    # lqro::Simulator takes lqro_config_default: the reference's own hull rule
+    oracle.set_hull_rule(1, round16=False)
+    oracle.carry_normal(np.zeros(3))
+    try:
+        for t in range(steps):
+            newv = out[t, :N * 3].reshape(N, 3)
+            xs = out[t, N * 3:].reshape(N, 16)
+            rv, rr = oracle.step(T, NCF, S, ref["x"], ref["vgoal"], threads=8)
+            if t == 0:
+                assert np.array_equal(newv.view(np.uint64), rv.view(np.uint64))
+            else:   # x went through one GPU dynamics step (libm last-bit differences)
+                np.testing.assert_allclose(newv, rv, rtol=1e-5, atol=1e-6)
+            ref["vgoal"][:] = rv
+            nrm, sd = lqro_mod.normals(sd, N * lqro_mod.NORMALS_PER_AGENT)
+            oracle.agent_step(ref, g, nrm)
+            np.testing.assert_allclose(xs, ref["x"], rtol=1e-7, atol=1e-9)
+    finally:
+        oracle.set_hull_rule(0)

@@ -157,7 +157,7 @@ def test_device_resident_closed_loop(lqro_mod, oracle, gains):
         gd = {k: hip.put(np.ascontiguousarray(g[k], np.float64)) for k in ("L", "E", "l", "Lh", "Eh")}
         Md, Nd = hip.put(1e-9 * np.eye(16)), hip.put(1e-9 * np.eye(6))
         models_d = hip.put(np.frombuffer(bytes(lqro_mod.default_model()), dtype=np.uint8))
-        ctx = lqro_mod.Context(lqro_mod.config(n, H, NP))
+        ctx = lqro_mod.Context(lqro_mod.config(n, H, NP, flags=0))   # the oracle's default (canonical) rule
         ctx.set_gains(g["A"], g["B"], g["L"], g["E"])
         T, NCF = oracle.tables(g["A"], g["B"], g["L"], g["E"], H)
         S = oracle.sphere(NP)
@@ -214,13 +214,19 @@ def test_simulator_loop(lqro_mod, oracle, tmp_path):
     T, NCF = oracle.tables(g["A"], g["B"], g["L"], g["E"], H)
     S = oracle.sphere(NP)
     seed = seed_ref = 3
-    for t in range(2):
-        sim.step()
-        seed = sim.update(seed)
-        newv, _ = oracle.step(T, NCF, S, ref["x"], ref["vgoal"], records=False)
-        ref["vgoal"][:] = newv
-        nrm, seed_ref = lqro_mod.normals(seed_ref, n * lqro_mod.NORMALS_PER_AGENT)
-        oracle.agent_step(ref, g, nrm)
+    # the Simulator runs the reference's own hull rule (LQRO_FLAG_QHULL_ORDER)
+    oracle.set_hull_rule(1, round16=False)
+    oracle.carry_normal(np.zeros(3))
+    try:
+        for t in range(2):
+            sim.step()
+            seed = sim.update(seed)
+            newv, _ = oracle.step(T, NCF, S, ref["x"], ref["vgoal"], records=False)
+            ref["vgoal"][:] = newv
+            nrm, seed_ref = lqro_mod.normals(seed_ref, n * lqro_mod.NORMALS_PER_AGENT)
+            oracle.agent_step(ref, g, nrm)
+    finally:
+        oracle.set_hull_rule(0)
     got = dict(x=np.stack([q.x for q in qs]), rot=np.stack([q.Rot for q in qs]),
                x_true=np.stack([q.xTrue for q in qs]), rot_true=np.stack([q.RotTrue for q in qs]),
                P=np.stack([q.P for q in qs]), vgoal=np.stack([q.vGoal for q in qs]))
