@@ -189,7 +189,7 @@ def hull_flags(lqro, rule: str) -> int:
     """qhull: the reference's own inside-hull rule over Qhull's build order
     (LQRO_FLAG_QHULL_ORDER, k_qhull: results equal the reference loop over
     Qhull); canonical: this build's faster canonical facet rule (a measured
-    deviation, DESIGN §5.1)."""
+    deviation, DESIGN §5.2)."""
     return lqro.LQRO_FLAG_QHULL_ORDER if rule == "qhull" else 0
 
 
@@ -286,7 +286,7 @@ def canonical_rule_run(lqro, torch, dev, sh, gains, d_x, d_vg, d_newv, stream, s
     timed steps' inputs, beside the headline: its step time, and the rows
     whose newV it moves beyond 1e-5 (relative) from the reference rule's
     newV of the last timed step — the deviation the default rule would
-    carry (DESIGN §5.1).  Never in `value`."""
+    carry (DESIGN §5.2).  Never in `value`."""
     ref = d_newv.clone()
     c = lqro.Context(lqro.config(N, HORIZON, N_POINTS, device=dev.index, flags=0, **sh))
     c.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
@@ -481,7 +481,7 @@ def main():
         "hull_rule_canonical": other,
         "hull_rule": ("reference: Qhull's facet order and first Fv vertex, strict <, loop-carried normal "
                       "(LQRO:925-968; k_qhull, LQRO_FLAG_QHULL_ORDER)" if args.hull_rule == "qhull" else
-                      "canonical (a measured deviation from the reference's rule, DESIGN §5.1)"),
+                      "canonical (a measured deviation from the reference's rule, DESIGN §5.2)"),
     }
     if not args.no_configs:
         out["configs"] = config_runs(lqro, torch, dev, local, world, rank, dist, 2, args.rows, flags)

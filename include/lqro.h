@@ -116,7 +116,7 @@ typedef struct lqro_ctx lqro_ctx;
 /* Defaults: LQRO's constants (N given by the caller); flags =
  * LQRO_FLAG_QHULL_ORDER, the reference's own inside-hull rule.  Clearing it
  * selects the faster canonical facet rule, a measured deviation from the
- * reference (DESIGN.md §5.1). */
+ * reference (DESIGN.md §5.2). */
 void lqro_config_default(lqro_config* cfg, int32_t n_agents, int32_t horizon, int32_t n_points);
 void lqro_model_default(lqro_model* m);
 

@@ -40,8 +40,8 @@
 
 namespace lqro {
 
-#define QH_NEWCAP 256     // new facets of one insertion
-#define QH_VISCAP 256     // visible facets of one insertion
+#define QH_NEWCAP 1024    // new facets of one insertion (C5: > 256 seen)
+#define QH_VISCAP 2048    // visible facets of one insertion (C5: > 256 seen)
 #define QH_HZCAP 64       // facets one point's horizon walk visits (per lane)
 #define QH_COPCAP 16      // qh.coplanarfacetset of one walk (per lane)
 #define QH_MOVCAP 32      // old facets moved behind the new ones in one partition
@@ -62,6 +62,14 @@ namespace lqro {
 #define QHS_SINGULAR 32
 #define QHS_TOPOLOGY 64
 #define QHS_CAPACITY 128   // a cap of this kernel (not Qhull's): the pair's record is a hull failure
+// which cap (k_qhull_big; in the record's status with QHS_CAPACITY)
+#define QHS_CAP_HZ 0x100
+#define QHS_CAP_COP 0x200
+#define QHS_CAP_MOV 0x400
+#define QHS_CAP_SB 0x800
+#define QHS_CAP_VIS 0x1000
+#define QHS_CAP_NEW 0x2000
+#define QHS_CAP_FACETS 0x4000
 
 struct QhW {
   double* Pr;      // 3 HNP rounded points (qconvex's input)
@@ -83,12 +91,15 @@ struct QhW {
   int* pdst;       // HNP: destination facet (-1: not outside) | event bits
   int* fstack;     // FC: free facet slots
   int* fvis;       // FC: qh_findhorizon visit stamp
+  unsigned* vstamp;  // (QH_NEWCAP - 256) x 64: qh_findbest's visit marks of new facets >= 256, per lane
+  unsigned* vctr;    // 64: each lane's last stamp (zeroed with the scratch, never reset)
   int FC, SB, HNP;
 };
 
 __host__ __device__ inline size_t qh_worker_bytes(int HNP) {
   const size_t FC = 2 * (size_t)HNP + QH_NEWCAP + 16, SB = (size_t)QH_SBMULT * HNP;
-  return 8 * (7 * (size_t)HNP + 5 * FC) + 4 * (15 * FC + 4 * (size_t)HNP + 8 + SB) + 256;
+  return 8 * (7 * (size_t)HNP + 5 * FC) + 4 * (15 * FC + 4 * (size_t)HNP + 8 + SB) + 256 +
+         4 * ((size_t)(QH_NEWCAP - 256) * 64 + 64);
 }
 
 __device__ inline QhW qh_worker(char* base, int HNP) {
@@ -112,6 +123,8 @@ __device__ inline QhW qh_worker(char* base, int HNP) {
   W.fnew = p; p += W.FC;
   W.fstack = p; p += W.FC;
   W.fvis = p; p += W.FC;
+  W.vstamp = reinterpret_cast<unsigned*>(p); p += (size_t)(QH_NEWCAP - 256) * 64;
+  W.vctr = reinterpret_cast<unsigned*>(p); p += 64;
   W.vpt = p; p += HNP + 8;
   W.pq = p; p += HNP;
   W.pst = p; p += HNP;
@@ -194,7 +207,7 @@ __device__ __forceinline__ int qh_newfacet(const QhW& W, QhS& S) {
   int f;
   if (S.nfree > 0) f = W.fstack[--S.nfree];
   else if (S.nalloc < W.FC) f = S.nalloc++;
-  else { S.status |= QHS_CAPACITY; f = 0; }
+  else { S.status |= QHS_CAPACITY | QHS_CAP_FACETS; f = 0; }
   W.fv[3 * f] = W.fv[3 * f + 1] = W.fv[3 * f + 2] = 0;
   W.fnb[3 * f] = W.fnb[3 * f + 1] = W.fnb[3 * f + 2] = -1;
   W.flink[2 * f] = W.flink[2 * f + 1] = -1;
@@ -324,7 +337,7 @@ __device__ inline int qh_findbesthorizon(const QhW& W, const QhS& S, const doubl
       bool seen = false;
       for (int t = 0; t < nvis; t++) seen |= vis[t] == nb;
       if (seen) continue;
-      if (nvis == QH_HZCAP) { lstatus |= QHS_CAPACITY; return bestfacet; }
+      if (nvis == QH_HZCAP) { lstatus |= QHS_CAPACITY | QHS_CAP_HZ; return bestfacet; }
       vis[nvis++] = nb;
       if (!(W.fflag[nb] & QF_FLIPPED)) {
         const double dist = qh_dist(W, p, nb);
@@ -338,7 +351,7 @@ __device__ inline int qh_findbesthorizon(const QhW& W, const QhS& S, const doubl
         }
       }
       if (nextfacet >= 0) {
-        if (ncop == QH_COPCAP) { lstatus |= QHS_CAPACITY; return bestfacet; }
+        if (ncop == QH_COPCAP) { lstatus |= QHS_CAPACITY | QHS_CAP_COP; return bestfacet; }
         cop[ncop++] = nextfacet;
       }
       nextfacet = nb;
@@ -410,10 +423,19 @@ __device__ inline int qh_locate(const QhW& W, const QhS& S, const QhL& L, const 
   double bestdist = -DBL_MAX / 2;
   int bestfacet = -1;
   *isoutside = 1;
-  // new facets visited: a bit per new-facet index (< QH_NEWCAP = 256)
+  // new facets visited: a bit per new-facet index below 256; beyond (an
+  // insertion with more than 256 new facets, C5), a per-lane stamp in the
+  // worker's scratch, fresh for this call
   unsigned long long s0 = 0ull, s1 = 0ull, s2 = 0ull, s3 = 0ull;
+  const int ln = threadIdx.x & 63;
+  unsigned stamp = 0u;
   auto mark = [&](int f) {
     const int t = W.fnew[f];
+    if (t >= 256) {
+      if (!stamp) { stamp = W.vctr[ln] + 1u; if (!stamp) stamp = 1u; W.vctr[ln] = stamp; }
+      W.vstamp[(size_t)(t - 256) * 64 + ln] = stamp;
+      return;
+    }
     const unsigned long long b = 1ull << (t & 63);
     if (t < 64) s0 |= b;
     else if (t < 128) s1 |= b;
@@ -422,6 +444,7 @@ __device__ inline int qh_locate(const QhW& W, const QhS& S, const QhL& L, const 
   };
   auto was = [&](int f) -> bool {
     const int t = W.fnew[f];
+    if (t >= 256) return stamp && W.vstamp[(size_t)(t - 256) * 64 + ln] == stamp;
     const unsigned long long w = t < 64 ? s0 : t < 128 ? s1 : t < 192 ? s2 : s3;
     return (w >> (t & 63)) & 1ull;
   };
@@ -533,7 +556,7 @@ __device__ inline void qh_locate_seq(const QhW& W, QhS& S, QhL& L, int np, int s
       if (ev_kind & 2) S.max_outside = W.pdd[ev_pos];
       if (ev_kind & 4) {
         const int f = W.pdst[ev_pos];
-        if (S.nmov == QH_MOVCAP) S.status |= QHS_CAPACITY;
+        if (S.nmov == QH_MOVCAP) S.status |= QHS_CAPACITY | QHS_CAP_MOV;
         else {
           qh_removefacet(W, S, f);        // "make sure it's after qh.facet_next"
           qh_appendfacet(W, S, f);
@@ -586,7 +609,7 @@ __device__ inline void qh_emit_seq(const QhW& W, QhS& S, QhL& L, int np, int lan
       for (int t = 0; t < S.nold; t++)
         if (L.oldf[t] == f) k = t;
       if (k < 0) {
-        if (S.nold == QH_MOVCAP) { S.status |= QHS_CAPACITY; continue; }
+        if (S.nold == QH_MOVCAP) { S.status |= QHS_CAPACITY | QHS_CAP_MOV; continue; }
         k = S.nold++;
         if (lane == 0) { L.oldf[k] = f; L.pcnt[QH_NEWCAP + k] = 0; L.dfac[QH_NEWCAP + k] = f; }
         hl_sync();
@@ -606,7 +629,7 @@ __device__ inline void qh_emit_seq(const QhW& W, QhS& S, QhL& L, int np, int lan
     const int f = L.dfac[g];
     const int cnt0 = W.fseg[2 * f + 1], off0 = W.fseg[2 * f];
     const int size = cnt0 + add;
-    if (S.sbtop + size > W.SB) { S.status |= QHS_CAPACITY; return; }
+    if (S.sbtop + size > W.SB) { S.status |= QHS_CAPACITY | QHS_CAP_SB; return; }
     const int off = S.sbtop;
     S.sbtop += size;
     for (int t = lane; t < cnt0 - 1; t += 64) W.sb[off + t] = W.sb[off0 + t];
@@ -923,7 +946,7 @@ __device__ inline void qh_build(const QhW& W, QhS& S, QhL& L, int n, int lane) {
         hl_sync();
       }
       if (cnt) {
-        if (off + cnt > W.SB) { S.status |= QHS_CAPACITY; return; }
+        if (off + cnt > W.SB) { S.status |= QHS_CAPACITY | QHS_CAP_SB; return; }
         if (lane == 0) W.sb[off + cnt - 1] = champ;
         W.fseg[2 * f] = off;
         W.fseg[2 * f + 1] = cnt;
@@ -1020,7 +1043,7 @@ __device__ inline void qh_build(const QhW& W, QhS& S, QhL& L, int n, int lane) {
           qh_appendfacet(W, S, nb);
           W.fflag[nb] |= QF_VISIBLE;
           W.frep[nb] = -1;
-          if (S.nvis == QH_VISCAP) { S.status |= QHS_CAPACITY; return; }
+          if (S.nvis == QH_VISCAP) { S.status |= QHS_CAPACITY | QHS_CAP_VIS; return; }
           if (lane == 0) L.visf[S.nvis] = nb;
           S.nvis++;
         } else if (dist >= -S.MAXcoplanar) {
@@ -1049,7 +1072,7 @@ __device__ inline void qh_build(const QhW& W, QhS& S, QhL& L, int n, int lane) {
         int vs[2], m = 0;
         for (int t = 0; t < 3; t++)
           if (t != hskip) vs[m++] = W.fv[3 * nb + t];
-        if (S.nnew == QH_NEWCAP) { S.status |= QHS_CAPACITY; return; }
+        if (S.nnew == QH_NEWCAP) { S.status |= QHS_CAPACITY | QHS_CAP_NEW; return; }
         const int nf = qh_newfacet(W, S);
         if (S.status & QHS_CAPACITY) return;
         W.fv[3 * nf] = apex;

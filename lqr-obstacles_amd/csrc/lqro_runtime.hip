@@ -560,6 +560,7 @@ static int ctx_alloc(lqro_ctx* c) {
     c->qworkers = c->n_cu;
     c->qstride = (qhull_worker_bytes((int)(H * NP)) + 255) & ~(size_t)255;
     HIPCHK(hipMalloc(&c->d_qscratch, c->qstride * (size_t)c->qworkers));
+    HIPCHK(hipMemset(c->d_qscratch, 0, c->qstride * (size_t)c->qworkers));   // k_qhull_big's visit stamps
     HIPCHK(hipMalloc(&c->d_qnrm, sizeof(double) * 4 * (slots ? slots : 1)));
     HIPCHK(hipMalloc(&c->d_qstale, sizeof(int) * (slots ? slots : 1)));
   }
@@ -1371,7 +1372,8 @@ int lqro_debug_hull_points(lqro_ctx* c, const double* pts, int32_t n, const doub
   int rc = LQRO_OK;
   const int fmax = (local == 1 || !facets) ? 1 : max_facets;
   const size_t qstride = (qhull_worker_bytes(g.horizon * g.n_points) + 255) & ~(size_t)255;
-  if (local == 2 && (hipMalloc(&d_qw, qstride) != hipSuccess || hipMalloc(&d_qn, sizeof(double) * 8) != hipSuccess))
+  if (local == 2 && (hipMalloc(&d_qw, qstride) != hipSuccess || hipMemset(d_qw, 0, qstride) != hipSuccess ||
+                     hipMalloc(&d_qn, sizeof(double) * 8) != hipSuccess))
     rc = LQRO_E_NOMEM;
   if (rc != LQRO_OK) {
   } else if (hipMalloc(&d_st, sizeof(unsigned long long) * 8) != hipSuccess ||

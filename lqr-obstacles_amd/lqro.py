@@ -519,7 +519,7 @@ class Simulator:
         self.qlist = list(qlist)
         self.model = model or default_model()
         # hull_rule "reference": the reference's own inside-hull rule (Qhull's
-        # order, LQRO:925-968); "canonical": the faster deviating rule (DESIGN §5.1)
+        # order, LQRO:925-968); "canonical": the faster deviating rule (DESIGN §5.2)
         if hull_rule not in ("reference", "canonical"):
             raise ValueError(f"hull_rule {hull_rule!r}")
         flags = (LQRO_FLAG_RECORDS if records else 0) | (LQRO_FLAG_QHULL_ORDER if hull_rule == "reference" else 0)

@@ -137,3 +137,40 @@ def test_c5_rows_records(lqro_mod, oracle, c5):
     _compare(recs, rrecs)
     _hull_exact(recs, rrecs)
     np.testing.assert_allclose(newv[rows[0]:rows[1]], rv[rows[0]:rows[1]], rtol=1e-5, atol=1e-6)
+
+
+def test_c5_qhull_order_largest_hulls(lqro_mod, oracle, c5):
+    """Qhull order (the default rule) on C5: a shard with hulls of ~19,000
+    points whose single insertions see more than 256 visible and new facets
+    (k_qhull_big, QH_VISCAP / QH_NEWCAP) builds every hull; three such rows
+    against the oracle's restatement of Qhull's build, bit for bit."""
+    c = c5
+    ctx = lqro_mod.Context(lqro_mod.config(c["N"], c["H"], c["NP"], x_dim=c["X"], row_begin=2048, row_end=4096,
+                                           flags=lqro_mod.LQRO_FLAG_QHULL_ORDER))
+    ctx.set_gains(c["A"], c["B"], c["L"], c["E"], per_agent=True)
+    ctx.step(c["x"], c["vg"])
+    st = ctx.stats()
+    ctx.close()
+    assert st["hull_fail"] == 0 and st["inside"] > 500, st
+    S = oracle.sphere(c["NP"])
+    oracle.set_hull_rule(1, round16=False)
+    try:
+        for r in (3014, 3155, 5156):
+            ctx = lqro_mod.Context(lqro_mod.config(c["N"], c["H"], c["NP"], x_dim=c["X"], row_begin=r, row_end=r + 1,
+                                                   flags=lqro_mod.LQRO_FLAG_RECORDS | lqro_mod.LQRO_FLAG_QHULL_ORDER))
+            ctx.set_gains(c["A"], c["B"], c["L"], c["E"], per_agent=True)
+            newv = ctx.step(c["x"], c["vg"])
+            recs = ctx.records()
+            ctx.close()
+            T = np.zeros((c["N"], c["H"], 9))
+            NCF = np.zeros((c["N"], c["H"], 3, c["X"]))
+            T[r], NCF[r] = oracle.tables(c["A"], c["B"], c["L"][r], c["E"][r], c["H"], X=c["X"])
+            oracle.carry_normal(np.zeros(3))
+            rv, rrecs = oracle.step(T, NCF, S, c["x"], c["vg"], rows=(r, r + 1), per_agent=True, threads=16)
+            ins = (rrecs["flags"] & lqro_mod.REC_INSIDE) != 0
+            assert ins.any() and not (recs["flags"][ins] & lqro_mod.REC_HULLFAIL).any(), r
+            for f in ("facet", "dist", "normal", "plane_point", "plane_normal"):
+                assert np.array_equal(recs[f][ins], rrecs[f][ins]), (r, f)
+            assert np.array_equal(newv[r].view(np.uint64), rv[r].view(np.uint64)), r
+    finally:
+        oracle.set_hull_rule(0)

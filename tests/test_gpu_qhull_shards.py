@@ -26,14 +26,13 @@ def _full(lqro_mod, gains, x, vg, H, steps):
 
 @pytest.mark.parametrize("world,mode", [(2, "block"), (3, "block"), (3, "cyclic")])
 def test_shards_match_one_context(lqro_mod, gains, world, mode):
-    import torch
+    from test_gpu_dyn import _Hip   # device buffers through liblqro's own HIP runtime
     N, H, steps = 32, 45, 2
     x, vg = lqro_mod.synthetic_swarm(N, box=3.0, seed=11)
     ref = _full(lqro_mod, gains, x, vg, H, steps)
     assert sum(int((r["flags"] & lqro_mod.REC_STALE).astype(bool).sum()) for _, r, _ in ref) > 0
-    dev = torch.device("cuda", 0)
-    d_x = torch.from_numpy(x).to(dev)
-    d_vg = torch.from_numpy(vg).to(dev)
+    hip = _Hip()
+    d_x, d_vg = hip.put(x), hip.put(vg)
     ctxs = []
     for g in range(world):
         c = lqro_mod.Context(lqro_mod.config(N, H, 100, flags=lqro_mod.LQRO_FLAG_RECORDS | lqro_mod.LQRO_FLAG_QHULL_ORDER,
@@ -41,23 +40,25 @@ def test_shards_match_one_context(lqro_mod, gains, world, mode):
         c.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
         ctxs.append(c)
     try:
+        zt, zv = np.zeros((N, 4)), np.zeros((N, 3))
         for t in range(steps):
-            tabs = [torch.zeros((N, 4), dtype=torch.float64, device=dev) for _ in range(world)]
-            newv = [torch.zeros((N, 3), dtype=torch.float64, device=dev) for _ in range(world)]
+            tabs = [hip.put(zt) for _ in range(world)]
+            newv = [hip.put(zv) for _ in range(world)]
             for g, c in enumerate(ctxs):
-                c.step_device_begin(d_x.data_ptr(), d_vg.data_ptr(), tabs[g].data_ptr(), 0)
-            torch.cuda.synchronize()
-            whole = torch.zeros((N, 4), dtype=torch.float64, device=dev)
+                c.step_device_begin(d_x, d_vg, tabs[g], 0)
+            hip.sync()
+            whole = np.zeros((N, 4))
             for g in range(world):   # the all-gather: each rank's own rows
-                ids = torch.from_numpy(lqro_mod.shard_row_ids(N, g, world, mode).astype(np.int64)).to(dev)
-                whole[ids] = tabs[g][ids]
+                ids = lqro_mod.shard_row_ids(N, g, world, mode)
+                whole[ids] = hip.get(tabs[g], zt)[ids]
+            d_whole = hip.put(whole)
             for g, c in enumerate(ctxs):
-                c.step_device_end(whole.data_ptr(), newv[g].data_ptr(), 0)
-            torch.cuda.synchronize()
+                c.step_device_end(d_whole, newv[g], 0)
+            hip.sync()
             v_ref, r_ref, carry_ref = ref[t]
             for g, c in enumerate(ctxs):
                 ids = lqro_mod.shard_row_ids(N, g, world, mode)
-                got = newv[g].cpu().numpy()[ids]
+                got = hip.get(newv[g], zv)[ids]
                 assert np.array_equal(got.view(np.uint64), v_ref[ids].view(np.uint64)), (t, g)
                 rr = c.records().reshape(len(ids), N - 1)
                 want = r_ref.reshape(N, N - 1)[ids]
@@ -67,26 +68,28 @@ def test_shards_match_one_context(lqro_mod, gains, world, mode):
     finally:
         for c in ctxs:
             c.close()
+        hip.free()
 
 
 def test_begin_end_call_order(lqro_mod, gains):
-    import torch
+    from test_gpu_dyn import _Hip
     N, H = 8, 20
     x, vg = lqro_mod.synthetic_swarm(N)
     c = lqro_mod.Context(lqro_mod.config(N, H, 50))
     c.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
-    dev = torch.device("cuda", 0)
-    d_x, d_vg = torch.from_numpy(x).to(dev), torch.from_numpy(vg).to(dev)
-    tab = torch.zeros((N, 4), dtype=torch.float64, device=dev)
-    nv = torch.zeros((N, 3), dtype=torch.float64, device=dev)
+    hip = _Hip()
+    d_x, d_vg = hip.put(x), hip.put(vg)
+    tab, nv = hip.put(np.zeros((N, 4))), hip.put(np.zeros((N, 3)))
     try:
         with pytest.raises(RuntimeError):
-            c.step_device_end(tab.data_ptr(), nv.data_ptr(), 0)      # no begin
-        c.step_device_begin(d_x.data_ptr(), d_vg.data_ptr(), tab.data_ptr(), 0)
+            c.step_device_end(tab, nv, 0)      # no begin
+        c.step_device_begin(d_x, d_vg, tab, 0)
         with pytest.raises(RuntimeError):
-            c.step_device(d_x.data_ptr(), d_vg.data_ptr(), nv.data_ptr(), 0)   # a step in the middle
-        c.step_device_end(tab.data_ptr(), nv.data_ptr(), 0)
-        torch.cuda.synchronize()
-        assert np.array_equal(nv.cpu().numpy().view(np.uint64), c.step(x, vg).view(np.uint64))
+            c.step_device(d_x, d_vg, nv, 0)   # a step in the middle
+        c.step_device_end(tab, nv, 0)
+        hip.sync()
+        got = hip.get(nv, np.zeros((N, 3)))
+        assert np.array_equal(got.view(np.uint64), c.step(x, vg).view(np.uint64))
     finally:
         c.close()
+        hip.free()
