@@ -491,9 +491,17 @@ __device__ inline int qh_locate(const QhW& W, const QhS& S, const QhL& L, const 
 
 // ---- partitioning in Qhull's order ----
 // wave-wide OR of a lane flag
+// (no lane flagged — the common case — costs one ballot; otherwise a DPP
+// reduction to lane 63, no LDS round trip)
 __device__ __forceinline__ int qh_wave_or(int v) {
-  for (int off = 32; off >= 1; off >>= 1) v |= __shfl_xor(v, off);
-  return v;
+  if (!__ballot(v != 0)) return 0;
+  v |= __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+  v |= __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+  v |= __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);   // row_shr:4
+  v |= __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);   // row_shr:8
+  v |= __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);   // row_bcast:15 -> rows 1, 3
+  v |= __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);   // row_bcast:31 -> rows 2, 3
+  return __builtin_amdgcn_readlane(v, 63);
 }
 
 __device__ __forceinline__ bool qh_in_movf(const QhS& S, const QhL& L, int f) {

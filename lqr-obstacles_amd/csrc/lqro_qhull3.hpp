@@ -144,7 +144,7 @@ struct Q3L {
   int nv[3 * Q3_NEWCAP];
   int nhz[Q3_NEWCAP], nhskip[Q3_NEWCAP];
   int nn1[Q3_NEWCAP], nn2[Q3_NEWCAP];
-  double npl[4 * Q3_NEWCAP];
+  alignas(32) double npl[4 * Q3_NEWCAP];
   int nflag[Q3_NEWCAP];
   int movf[Q3_MOVCAP];               // old facets moved behind the new ones (scan order)
   int oldf[Q3_MOVCAP];               // old facets receiving points (destinations Q3_NEWCAP + k)
@@ -401,9 +401,13 @@ __device__ __forceinline__ void q3_place(const Q3W& W, unsigned long long grp, i
   const bool rec = mem && (cb == 0 || run < dd);
   const unsigned long long recm = __ballot(rec);
   const unsigned long long prevm = recm & ltmask;
-  const int pl = prevm ? 63 - __clzll((long long)prevm) : lane;
-  const double px = __shfl(pt.x, pl), py = __shfl(pt.y, pl), pz = __shfl(pt.z, pl);
-  const int pq = __shfl(pt.q, pl);
+  double px = 0.0, py = 0.0, pz = 0.0;
+  int pq = 0;
+  if (recm & (recm - 1ull)) {   // a new furthest point displacing another one of this pass
+    const int pl = prevm ? 63 - __clzll((long long)prevm) : lane;
+    px = __shfl(pt.x, pl); py = __shfl(pt.y, pl); pz = __shfl(pt.z, pl);
+    pq = __shfl(pt.q, pl);
+  }
   if (mem && cb > 0 && off + cb - 1 < lim) {
     HullPt r = pt;
     if (rec) {   // the furthest point it displaces: the previous new furthest here, or the held one
@@ -499,25 +503,38 @@ __device__ inline int q3_findbestnew(const Q3W& W, const Q3S& S, const Q3L& L, c
   const double distoutside = fmax(2 * S.MINoutside, S.max_outside);    // qh_DISToutside
   *isoutside = 1;
   const int total = S.nnew + S.nmov;
-  for (int t = 0; t < total; t++) {
-    int f, fl;
-    double q[4];
+  // the scan list, four facets' planes fetched at a time (in order; the
+  // first one at or beyond distoutside ends the scan)
+  auto fetch = [&](int t, int& f, int& fl, double* q) {
     if (t < S.nnew - s0 || t >= S.nnew - s0 + S.nmov) {
       const int u = t < S.nnew - s0 ? s0 + t : t - (S.nnew - s0) - S.nmov;
       f = L.nslot[u];
-      for (int k = 0; k < 4; k++) q[k] = L.npl[4 * u + k];
+      const double4 v = q3_lds(*reinterpret_cast<const double4*>(L.npl + 4 * u));
+      q[0] = v.x; q[1] = v.y; q[2] = v.z; q[3] = v.w;
       fl = L.nflag[u];
     } else {
       f = L.movf[t - (S.nnew - s0)];
       q3_pl(W, L, f, q);
       fl = q3_fa(W, L, f);
     }
-    if (fl & QF_FLIPPED) continue;
-    const double d = q3_distq(q, p);
-    if (d > bestdist) {
-      bestfacet = f;
-      if (!bestoutside && d >= distoutside) { *dist = d; return bestfacet; }
-      bestdist = d;
+  };
+  for (int t0 = 0; t0 < total; t0 += 4) {
+    int f[4], fl[4];
+    double q[4][4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      f[k] = -1; fl[k] = QF_FLIPPED;
+      if (t0 + k < total) fetch(t0 + k, f[k], fl[k], q[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (fl[k] & QF_FLIPPED) continue;
+      const double d = q3_distq(q[k], p);
+      if (d > bestdist) {
+        bestfacet = f[k];
+        if (!bestoutside && d >= distoutside) { *dist = d; return bestfacet; }
+        bestdist = d;
+      }
     }
   }
   bestfacet = q3_findbesthorizon(W, S, L, p, bestfacet >= 0 ? bestfacet : L.nslot[s0], &bestdist, lstatus);
@@ -564,13 +581,22 @@ __device__ inline int q3_locate(const Q3W& W, const Q3S& S, const Q3L& L, const 
   while (u >= 0) {
     int nxt = -1;
     const int cand[2] = {L.nn1[u], L.nn2[u]};
+    // both neighbours' flags and planes in one round trip
+    const int cfl[2] = {L.nflag[cand[0]], L.nflag[cand[1]]};
+    double cq[2][4];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const double4 v = q3_lds(*reinterpret_cast<const double4*>(L.npl + 4 * cand[k]));
+      cq[k][0] = v.x; cq[k][1] = v.y; cq[k][2] = v.z; cq[k][3] = v.w;
+    }
+#pragma unroll
     for (int k = 0; k < 2; k++) {
       const int c = cand[k];
       const bool was = c < 64 ? (m0 >> c) & 1ull : (m1 >> (c - 64)) & 1ull;
       if (was) continue;
       if (c < 64) m0 |= 1ull << c; else m1 |= 1ull << (c - 64);
-      if (!(L.nflag[c] & QF_FLIPPED)) {
-        const double d = q3_distq(L.npl + 4 * c, p);
+      if (!(cfl[k] & QF_FLIPPED)) {
+        const double d = q3_distq(cq[k], p);
         if (d > bestdist) {
           if (d >= S.MINoutside) { *bestdist_out = d; return L.nslot[c]; }
           bestu = c;
