@@ -41,7 +41,7 @@ namespace lqro {
 #define Q3_FSTK 512       // free facet slots kept for reuse (more are left unused)
 #define Q3_ND (Q3_NEWCAP + Q3_MOVCAP)
 #ifndef Q3_FL
-#define Q3_FL 2752        // facet slots with their hot fields in LDS
+#define Q3_FL 2432        // facet slots with their hot fields in LDS
 #endif
 
 struct Q3G {              // a facet slot >= Q3_FL, 64 B
@@ -72,6 +72,9 @@ struct Q3W {
   int* pq;                // HNP: qh_partitionall's remainder
   int* pdst;              // HNP: partition sequence -> destination index
   double* pdd;            // HNP: its distance
+  double* ncoord2;        // 9 Q3_NEWCAP: the speculated cone's ridge and opposite points (wave 1)
+  unsigned* mark2;        // FC: wave 1's visit epochs of slots >= Q3_FL
+  unsigned* ctr;          // wave 1's last epoch (across jobs; zeroed with the scratch)
   int* fq;                // QC: facets that received points, key order
   unsigned* fqk;          // QC: their key then
   HullPt* fqc;            // QC: their furthest point then (q = -1: not recorded)
@@ -86,7 +89,7 @@ __host__ __device__ inline size_t q3_worker_bytes(int HNP) {
   return q3_align(24 * (size_t)HNP) * 2 + q3_align(64 * NG) + q3_align(96 * FC) + q3_align(72 * Q3_NEWCAP) +
          q3_align(32 * (size_t)HNP) + q3_align(4 * FC) +
          q3_align(8 * FC) + q3_align(32 * SB) + q3_align(4 * (size_t)HNP) * 2 + q3_align(8 * (size_t)HNP) +
-         q3_align(4 * QC) * 2 + q3_align(32 * QC);
+         q3_align(4 * QC) * 2 + q3_align(32 * QC) + q3_align(72 * Q3_NEWCAP) + q3_align(4 * FC) + 256;
 }
 
 __device__ inline Q3W q3_worker(char* base, int HNP) {
@@ -113,6 +116,9 @@ __device__ inline Q3W q3_worker(char* base, int HNP) {
   W.fq = reinterpret_cast<int*>(take(4 * (size_t)W.QC));
   W.fqk = reinterpret_cast<unsigned*>(take(4 * (size_t)W.QC));
   W.fqc = reinterpret_cast<HullPt*>(take(32 * (size_t)W.QC));
+  W.ncoord2 = reinterpret_cast<double*>(take(72 * (size_t)Q3_NEWCAP));
+  W.mark2 = reinterpret_cast<unsigned*>(take(4 * (size_t)W.FC));
+  W.ctr = reinterpret_cast<unsigned*>(take(256));
   return W;
 }
 
@@ -122,9 +128,9 @@ struct Q3L {
   int n, fail, job, slot;
   double eps;
   double tr[3 * 128];
-  double rk[1];
-  int ri[1];
-  int scan[1];
+  double rk[2];                      // (two waves: hull_points' block scans)
+  int ri[2];
+  int scan[2];
   // facet slots < Q3_FL
   double4 pl[Q3_FL];
   ushort4 tp[Q3_FL];                 // neighbours, QF_* | new-facet index << 8
@@ -154,6 +160,20 @@ struct Q3L {
   double dchp[3 * Q3_ND];            // the furthest point's coordinates
   int cop[Q3_COPCAP * 64];           // the horizon walks' coplanar facet sets, [k][lane]
   unsigned short hvis[Q3_HZCAP * 64];  // the horizon walks' visited facets, [k][lane]
+  // Two-wave build: while wave 0 partitions insertion k, wave 1 speculates
+  // insertion k+1's horizon and cone (q3_spec) into these; wave 0 adopts them
+  // when the facet is still the queue's next with the same furthest point.
+  int sp_visf[Q3_VISCAP];
+  int sp_repl[Q3_VISCAP];
+  int sp_v1[Q3_NEWCAP], sp_v2[Q3_NEWCAP], sp_nhz[Q3_NEWCAP], sp_nhskip[Q3_NEWCAP], sp_nflag[Q3_NEWCAP];
+  alignas(32) double sp_npl[4 * Q3_NEWCAP];
+  unsigned short mark[Q3_FL];        // wave 1's visit epochs (slots < Q3_FL)
+  double sp_apex[3];
+  double c_dist[8];                  // MINvisible, MAXcoplanar, DISTround, MINdenom, MINdenom_2, NEARzero[3]
+  double c_interior[3];
+  int ph, sp_done, sp_ok, sp_facet, sp_furthest, sp_pos, sp_nvis, sp_nnew, sp_status;
+  unsigned sp_key;
+  int pub_qhead, pub_qtail;
 };
 static_assert(sizeof(Q3L) <= 160 * 1024, "k_qhull's LDS exceeds a CU");
 
@@ -176,7 +196,7 @@ struct Q3S {
 #define Q3T(k) do {} while (0)
 #endif
 // LQRO_QHULL_PROFILE counters: 21 insertions, 22 partitioned points, 23 located
-// chunks, 24 sequence events, 25 emitted destination groups
+// chunks, 24 sequence events, 25 emitted destination groups, 31 adopted speculations
 #ifdef LQRO_QHULL_PROFILE
 #define Q3C(k, v) do { S.tph[k] += (unsigned long long)(v); } while (0)
 #else
@@ -942,6 +962,193 @@ __device__ __forceinline__ int q3_alloc(const Q3S& S, const Q3L& L, int t) {
   return S.nalloc + (e - S.nfs);
 }
 
+// ---- wave 1: the next insertion, speculated (two-wave build) ----
+// Handshake (LDS, workgroup scope): wave 0 publishes L.ph = k after insertion
+// k's cone is built (the queue head and tail, the topology fixed until its
+// partition ends); wave 1 speculates insertion k+1 — the queue's next live
+// facet with points, its furthest point, qh_findhorizon, the cone's ridges
+// and planes — and answers L.sp_done = k.  Insertion k's partition changes
+// no neighbour link, plane or FLIPPED / TOP flag, so the speculated horizon
+// and cone are exactly the sequential ones as long as the facet is still the
+// queue's next with the same key and furthest point when wave 0 checks it.
+// Wave 1 marks visited facets with its own epochs (no facet flag written).
+__device__ __forceinline__ int q3_ld_acq(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void q3_st_rel(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// wait (bounded) until *p != v (ne) or == v (!ne); the last value read
+__device__ __forceinline__ int q3_wait(const int* p, int v, bool ne) {
+  int x = q3_ld_acq(p);
+  for (long w = 0; (ne ? x == v : x != v) && w < (1l << 24); ++w) {
+    __builtin_amdgcn_s_sleep(1);
+    x = q3_ld_acq(p);
+  }
+  return x;
+}
+
+__device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep, unsigned ep2) {
+  const unsigned long long ltmask = (1ull << lane) - 1ull;
+  Q3S C;   // the constants q3_plane reads
+  C.MINvisible = L.c_dist[0]; C.MAXcoplanar = L.c_dist[1]; C.DISTround = L.c_dist[2];
+  C.MINdenom = L.c_dist[3]; C.MINdenom_2 = L.c_dist[4];
+  for (int k = 0; k < 3; k++) { C.NEARzero[k] = L.c_dist[5 + k]; C.interior[k] = L.c_interior[k]; }
+  auto marked = [&](int f) -> bool {
+    return f < Q3_FL ? q3_lds(L.mark[f]) == ep : q3_glb(W.mark2[f]) == ep2;
+  };
+  auto mark = [&](int f) {
+    if (f < Q3_FL) q3_lds_st(L.mark[f], ep);
+    else q3_glb_st(W.mark2[f], ep2);
+  };
+  int ok = 0;
+  // 1. the queue's next live facet with points (not one insertion k made visible)
+  const int qt = L.pub_qtail;
+  int facet = -1, furthest = -1, fpos = -1;
+  unsigned fkey = 0;
+  double apex[3] = {0.0, 0.0, 0.0};
+  for (int qh = L.pub_qhead; qh < qt; qh += 64) {
+    const int pos = qh + lane;
+    bool good = false;
+    int f = 0;
+    unsigned k = 0, c = 0;
+    if (pos < qt) {
+      f = W.fq[pos];
+      k = W.fqk[pos];
+      const int fa = q3_fa(W, L, f);
+      c = q3_cc(W, L, f);
+      good = (fa & QF_LIVE) && !(fa & QF_VISIBLE) && q3_key(W, L, f) == k && (c & 0xffffu) > 0;
+    }
+    const unsigned long long b = __ballot(good);
+    if (b) {
+      const int l = __ffsll((long long)b) - 1;
+      fpos = qh + l;
+      facet = __builtin_amdgcn_readlane(f, l);
+      fkey = (unsigned)__builtin_amdgcn_readlane((int)k, l);
+      furthest = (int)((unsigned)__builtin_amdgcn_readlane((int)c, l) >> 16);
+      const HullPt e = W.fqc[fpos];
+      if (e.q == furthest) { apex[0] = e.x; apex[1] = e.y; apex[2] = e.z; }
+      else {
+        apex[0] = W.Pr[3 * (size_t)furthest];
+        apex[1] = W.Pr[3 * (size_t)furthest + 1];
+        apex[2] = W.Pr[3 * (size_t)furthest + 2];
+      }
+      break;
+    }
+  }
+  int ls = 0, nvis = 0, nnew = 0, ts = 0, lm = 0;
+  if (facet >= 0) {
+    // 2. qh_findhorizon, as wave 0's (level order, first occurrence), visits as epochs
+    if (lane == 0) L.sp_visf[0] = facet;
+    mark(facet);
+    hl_sync();
+    nvis = 1;
+    bool cap = false;
+    for (int lo = 0; lo < nvis && !cap;) {
+      const int hi = nvis;
+      const int ncand = 3 * (hi - lo);
+      for (int c0 = 0; c0 < ncand; c0 += 64) {
+        const int c = c0 + lane;
+        int nb = -1;
+        bool cand = false;
+        double q[4] = {0.0, 0.0, 0.0, 0.0};
+        if (c < ncand) {
+          nb = q3_nb(W, L, L.sp_visf[lo + c / 3], c % 3);
+          int nn[3], fa;
+          q3_get(W, L, nb, q, nn, &fa);
+          cand = !marked(nb);
+        }
+        const double dist = cand ? q3_distq(q, apex) : 0.0;
+        bool vis = cand && dist >= C.MINvisible;
+        if (cand && !vis && dist >= -C.MAXcoplanar) ls |= QHS_COPLANAR;
+        bool dup = false;
+        for (unsigned long long mm = __ballot(vis); mm;) {
+          const int l = __ffsll((long long)mm) - 1;
+          mm &= mm - 1;
+          dup |= (l < lane) && __builtin_amdgcn_readlane(nb, l) == nb;
+        }
+        vis = vis && !dup;
+        const unsigned long long bv = __ballot(vis);
+        if (vis) {
+          const int at = nvis + __popcll(bv & ltmask);
+          if (at < Q3_VISCAP) L.sp_visf[at] = nb;
+          mark(nb);
+        }
+        nvis += __popcll(bv);
+        hl_sync();
+      }
+      lo = hi;
+      if (nvis > Q3_VISCAP) cap = true;
+    }
+    // 3. the cone: one new facet per horizon ridge, as wave 0's
+    if (!cap) {
+      for (int vi = lane; vi < nvis; vi += 64) L.sp_repl[vi] = -1;
+      hl_sync();
+      for (int c0 = 0; c0 < 3 * nvis; c0 += 64) {
+        const int c = c0 + lane;
+        int vis = -1, nb = -1, hfa = 0;
+        bool ridge = false;
+        int hn[3] = {-1, -1, -1};
+        if (c < 3 * nvis) {
+          const int vi = c / 3;
+          vis = L.sp_visf[vi];
+          nb = q3_nb(W, L, vis, c - 3 * vi);
+          q3_tp(W, L, nb, hn, &hfa);
+          ridge = !marked(nb);
+        }
+        const unsigned long long b = __ballot(ridge);
+        if (ridge) {
+          const int t = nnew + __popcll(b & ltmask);
+          const int hskip = hn[0] == vis ? 0 : hn[1] == vis ? 1 : hn[2] == vis ? 2 : -1;
+          if (hskip < 0) {
+            ts |= QHS_TOPOLOGY;
+          } else if (t < Q3_NEWCAP) {
+            const Q3V& h = W.vv[nb];
+            const int top = (hfa & QF_TOP) ? (hskip & 1) : ((hskip & 1) ^ 1);
+            const int i1 = hskip == 0 ? 1 : 0, i2 = hskip == 2 ? 1 : 2;
+            double p1[3], p2[3], po[3];
+            for (int k = 0; k < 3; k++) {
+              p1[k] = h.p[3 * i1 + k];
+              p2[k] = h.p[3 * i2 + k];
+              po[k] = h.p[3 * hskip + k];
+            }
+            L.sp_v1[t] = h.id[i1];
+            L.sp_v2[t] = h.id[i2];
+            L.sp_nhz[t] = nb;
+            L.sp_nhskip[t] = hskip;
+            atomicMax(&L.sp_repl[c / 3], t);
+            double q[4];
+            bool flipped;
+            int fl = QF_NEW | QF_LIVE | (top ? QF_TOP : 0);
+            q3_plane(C, lm, apex, p1, p2, top, q, &flipped);
+            if (flipped) { fl |= QF_FLIPPED; lm |= QHS_FLIPPED; }
+            L.sp_nflag[t] = fl;
+            L.sp_npl[4 * t] = q[0]; L.sp_npl[4 * t + 1] = q[1]; L.sp_npl[4 * t + 2] = q[2]; L.sp_npl[4 * t + 3] = q[3];
+            for (int k = 0; k < 3; k++) {
+              W.ncoord2[9 * t + k] = p1[k]; W.ncoord2[9 * t + 3 + k] = p2[k]; W.ncoord2[9 * t + 6 + k] = po[k];
+            }
+          }
+        }
+        nnew += __popcll(b);
+      }
+      ok = nnew <= Q3_NEWCAP;
+    }
+  }
+  const int st = qh_wave_or(ls | ts | lm);
+  hl_sync();
+  if (lane == 0) {
+    L.sp_ok = ok;
+    L.sp_facet = facet;
+    L.sp_key = fkey;
+    L.sp_furthest = furthest;
+    L.sp_pos = fpos;
+    L.sp_nvis = nvis;
+    L.sp_nnew = nnew;
+    L.sp_status = st;
+    L.sp_apex[0] = apex[0]; L.sp_apex[1] = apex[1]; L.sp_apex[2] = apex[2];
+  }
+}
+
 // qh_qhull on W.Pr[0..n) (qconvex's defaults; lqro_qhull.hpp qh_build step
 // for step)
 __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
@@ -1249,6 +1456,13 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     }
   }
   Q3T(0);
+  // the constants wave 1's speculation needs (published with the first phase)
+  if (lane == 0) {
+    L.c_dist[0] = S.MINvisible; L.c_dist[1] = S.MAXcoplanar; L.c_dist[2] = S.DISTround;
+    L.c_dist[3] = S.MINdenom; L.c_dist[4] = S.MINdenom_2;
+    for (int k = 0; k < 3; k++) { L.c_dist[5 + k] = S.NEARzero[k]; L.c_interior[k] = S.interior[k]; }
+  }
+  int phase = 0;
   // qh_buildhull
   // the queue's next 64 entries stay in the lanes (lane k: entry qcb + k;
   // entries never change once written, appends go to the tail), with the
@@ -1262,7 +1476,28 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     // points
     int facet = -1, furthest = -1;
     double apexp[3] = {0.0, 0.0, 0.0};
-    while (S.qhead < S.qtail) {
+    // wave 1's speculation of this insertion: adopted when its facet is still
+    // the queue's next live one with points and the same furthest point
+    bool adopt = false;
+    if (phase > 0) {
+      const int dn = q3_wait(&L.sp_done, phase, false);
+      if (dn == phase && L.sp_ok) {
+        const int F = L.sp_facet;
+        const unsigned c = q3_cc(W, L, F);
+        adopt = (q3_fa(W, L, F) & QF_LIVE) && q3_key(W, L, F) == L.sp_key && (c & 0xffffu) > 0 &&
+                (int)(c >> 16) == L.sp_furthest;
+        if (adopt) {
+          facet = F;
+          furthest = L.sp_furthest;
+          apexp[0] = L.sp_apex[0]; apexp[1] = L.sp_apex[1]; apexp[2] = L.sp_apex[2];
+          S.qhead = L.sp_pos;
+          hl_sync();
+          q3_set_cc(W, L, facet, (c & 0xffffu) - 1u);   // qh_setdellast
+          hl_sync();
+        }
+      }
+    }
+    while (!adopt && S.qhead < S.qtail) {
       if (S.qhead >= qcb + qcn) {
         qcb = S.qhead;
         qcn = min(64, S.qtail - S.qhead);
@@ -1302,7 +1537,41 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
       S.qhead = qcb + qcn;
     }
     Q3T(1);
+#ifdef LQRO_QHULL_PROFILE
+    const unsigned long long tins_ = S.tq;   // this insertion's start (for the long-sequence split)
+#endif
     if (furthest < 0) break;
+    int nvis = 0, nnew = 0, ts = 0, lm = 0, my_t = -1;
+    bool one = false;
+    const double* ncb = W.ncoord;
+    double P1[3] = {0.0, 0.0, 0.0}, P2[3] = {0.0, 0.0, 0.0}, PO[3] = {0.0, 0.0, 0.0};
+    if (adopt) {
+      // the speculated visible set (flagged now) and cone
+      nvis = L.sp_nvis;
+      nnew = L.sp_nnew;
+      for (int vi = lane; vi < nvis; vi += 64) {
+        const int f = L.sp_visf[vi];
+        L.visf[vi] = f;
+        L.repl[vi] = L.sp_repl[vi];
+        q3_set_fa(W, L, f, q3_fa(W, L, f) | QF_VISIBLE);
+        const Q3V& vw = W.vv[f];
+        L.vvert[3 * vi] = vw.id[0]; L.vvert[3 * vi + 1] = vw.id[1]; L.vvert[3 * vi + 2] = vw.id[2];
+        L.vsoff[vi] = W.soff[f];
+        L.vscnt[vi] = (int)(q3_cc(W, L, f) & 0xffffu);
+      }
+      for (int t = lane; t < nnew; t += 64) {
+        L.nv[3 * t] = furthest; L.nv[3 * t + 1] = L.sp_v1[t]; L.nv[3 * t + 2] = L.sp_v2[t];
+        L.nhz[t] = L.sp_nhz[t];
+        L.nhskip[t] = L.sp_nhskip[t];
+        L.nflag[t] = L.sp_nflag[t];
+        for (int k = 0; k < 4; k++) L.npl[4 * t + k] = L.sp_npl[4 * t + k];
+      }
+      S.status |= L.sp_status;
+      S.nvis = nvis;
+      lm = L.sp_status & QHS_FLIPPED;   // (qh_checkzero skips a cone with a flipped facet)
+      ncb = W.ncoord2;
+      hl_sync();
+    } else {
     // qh_findhorizon, a level of the breadth-first search at a time: the
     // candidates of a level in (visible facet, neighbour) order, a facet
     // taken at its first occurrence
@@ -1313,7 +1582,8 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
       q3_set_fa(W, L, facet, fa0 | QF_VISIBLE);
       hl_sync();
     }
-    int ls = 0, nvis = 1;
+    int ls = 0;
+    nvis = 1;
     for (int lo = 0; lo < nvis;) {
       const int hi = nvis;
       const int ncand = 3 * (hi - lo);
@@ -1361,9 +1631,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     // (3 nvis <= 64) the lane keeps its facet's points for qh_checkzero.
     for (int vi = lane; vi < nvis; vi += 64) L.repl[vi] = -1;
     hl_sync();
-    const bool one = 3 * nvis <= 64;
-    int nnew = 0, ts = 0, lm = 0, my_t = -1;
-    double P1[3] = {0.0, 0.0, 0.0}, P2[3] = {0.0, 0.0, 0.0}, PO[3] = {0.0, 0.0, 0.0};
+    one = 3 * nvis <= 64;
     for (int c0 = 0; c0 < 3 * nvis; c0 += 64) {
       const int c = c0 + lane;
       int vis = -1, nb = -1, hfa = QF_VISIBLE;
@@ -1424,6 +1692,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
       nnew += __popcll(b);
     }
     Q3T(19);
+    }   // (speculation adopted / computed here)
     S.status |= qh_wave_or(ts);
     if (nnew > Q3_NEWCAP) S.status |= QHS_CAPACITY;
     if (S.status & (QHS_TOPOLOGY | QHS_CAPACITY)) return;
@@ -1493,7 +1762,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     } else {
       for (int t = lane; t < nnew; t += 64) {
         double p1[3], p2[3];
-        for (int k = 0; k < 3; k++) { p1[k] = W.ncoord[9 * t + k]; p2[k] = W.ncoord[9 * t + 3 + k]; }
+        for (int k = 0; k < 3; k++) { p1[k] = ncb[9 * t + k]; p2[k] = ncb[9 * t + 3 + k]; }
         finish(t, p1, p2);
       }
     }
@@ -1513,7 +1782,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
         for (int t = lane; t < nnew; t += 64) {
           double p1[3], p2[3], po[3];
           for (int k = 0; k < 3; k++) {
-            p1[k] = W.ncoord[9 * t + k]; p2[k] = W.ncoord[9 * t + 3 + k]; po[k] = W.ncoord[9 * t + 6 + k];
+            p1[k] = ncb[9 * t + k]; p2[k] = ncb[9 * t + 3 + k]; po[k] = ncb[9 * t + 6 + k];
           }
           zero(t, p1, p2, po);
         }
@@ -1522,6 +1791,14 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     S.status |= qh_wave_or(lm);
     Q3T(4);
     if (S.status & (QHS_TOPOLOGY | QHS_CAPACITY)) return;
+    // the cone is built: wave 1 may speculate the next insertion meanwhile
+    hl_sync();
+    if (lane == 0) {
+      L.pub_qhead = S.qhead;
+      L.pub_qtail = S.qtail;
+    }
+    ++phase;
+    if (lane == 0) q3_st_rel(&L.ph, phase);
     S.findbestnew = 0;
     S.notsharp = 0;
     S.nmov = 0;
@@ -1529,6 +1806,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     const int sharp = q3_sharpnewfacets(S, L, lane);
     Q3T(20);
     Q3C(21, 1);
+    Q3C(31, adopt ? 1 : 0);   // insertions whose horizon and cone wave 1 speculated
     Q3C(22, np2);
     if (np2) {
       int rg;
@@ -1576,6 +1854,10 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     S.notsharp = 0;
     hl_sync();
     Q3T(9);
+#ifdef LQRO_QHULL_PROFILE
+    // insertions whose partition sequence is longer than one chunk: 29 cycles, 30 count
+    if (np2 > 64) { S.tph[29] += S.tq - tins_; S.tph[30] += 1; }
+#endif
   }
 }
 
@@ -1681,11 +1963,16 @@ __device__ inline void q3_select(const HullArgs& A, const Q3W& W, const Q3L& L, 
 // (k_qhull_big)
 __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
   const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // 0: the build, 1: its speculation
   const int HNP = A.H * A.NP;
   const Q3W W = q3_worker(A.qscratch + (size_t)(A.block_base + blockIdx.x) * A.qstride, HNP);
   for (;;) {
     const int slot = hull_take_job(A, L, false);
     if (slot < 0) break;
+    // a fresh handshake and wave 1's epochs for this job (ordered by
+    // hull_points' barriers)
+    if (threadIdx.x == 0) { L.ph = 0; L.sp_done = 0; }
+    for (int q = threadIdx.x; q < Q3_FL / 2; q += blockDim.x) reinterpret_cast<unsigned*>(L.mark)[q] = 0u;
     const int lrow = slot / A.npr, jj = A.nbr_list ? A.nbr_list[slot] : slot % A.npr;
     const int i = A.row_begin + lrow * A.row_stride;
     const int j = jj < i ? jj : jj + 1;
@@ -1695,6 +1982,24 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
     const double* Ni = A.NCF + (A.per_agent ? (size_t)i * A.H * 3 * A.X : 0);
     const double vrel[3] = {xi[3] - xj[3], xi[4] - xj[4], xi[5] - xj[5]};
     const int n = hull_points(A, L, Ti, Ni, xi, xj, vrel, W.Pr, W.Pf);
+    if (wave == 1) {
+      // speculate each published phase until the build ends (ph = -1)
+      unsigned ep2 = W.ctr[0];
+      unsigned short ep = 0;
+      int last = 0;
+      for (;;) {
+        const int p = q3_wait(&L.ph, last, true);
+        if (p < 0 || p == last) break;
+        last = p;
+        ++ep;
+        ++ep2;
+        q3_spec(W, L, lane, ep, ep2);
+        hl_sync();
+        if (lane == 0) q3_st_rel(&L.sp_done, p);
+      }
+      if (lane == 0) W.ctr[0] = ep2;
+      continue;   // (hull_take_job's barrier meets wave 0 there)
+    }
     Q3S S;
 #ifdef LQRO_QHULL_PROFILE
     for (int k = 0; k < 32; k++) S.tph[k] = 0;
@@ -1705,6 +2010,7 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
     if (L.fail || n < 4) S.status = QHS_INPUT;
     else q3_build(W, S, L, n, lane);
     hl_sync();
+    if (lane == 0) q3_st_rel(&L.ph, -1);   // the build is over: wave 1 stops
     if (S.status & QHS_CAPACITY) {
       if (lane == 0) {
         const int r = atomicAdd(A.rcount, 1);

@@ -38,6 +38,9 @@ print("job ms/hull (mean, max)", int(out[27]) / jobs / GHZ / 1e6, int(out[26]) /
 for k, nm in ((21, "insertions"), (22, "partitioned points"), (23, "located chunks"), (24, "sequence events"),
               (25, "emitted groups")):
     print(f"{nm:24s} {int(out[k]) / jobs:12.1f} per hull")
+print("insertions adopted from wave 1's speculation:", int(out[31]) / jobs, "per hull")
+print("insertions with > 64 partitioned points:", int(out[30]) / jobs, "per hull,",
+      int(out[29]) / jobs / GHZ / 1e6, "ms per hull")
 nj = min(jobs, 4096)
 pj = out[32:32 + 2 * nj].reshape(nj, 2)
 cyc = pj[:, 0].astype(np.float64) / GHZ / 1e6
