@@ -41,7 +41,7 @@ namespace lqro {
 #define Q3_FSTK 512       // free facet slots kept for reuse (more are left unused)
 #define Q3_ND (Q3_NEWCAP + Q3_MOVCAP)
 #ifndef Q3_FL
-#define Q3_FL 2432        // facet slots with their hot fields in LDS
+#define Q3_FL 2368        // facet slots with their hot fields in LDS
 #endif
 
 struct Q3G {              // a facet slot >= Q3_FL, 64 B
@@ -166,14 +166,17 @@ struct Q3L {
   int sp_visf[Q3_VISCAP];
   int sp_repl[Q3_VISCAP];
   int sp_v1[Q3_NEWCAP], sp_v2[Q3_NEWCAP], sp_nhz[Q3_NEWCAP], sp_nhskip[Q3_NEWCAP], sp_nflag[Q3_NEWCAP];
+  int sp_nn1[Q3_NEWCAP], sp_nn2[Q3_NEWCAP];   // qh_matchnewfacets' neighbours (new-facet indices)
+  int sp_vvert[3 * Q3_VISCAP];                 // the visible facets' vertices
   alignas(32) double sp_npl[4 * Q3_NEWCAP];
   unsigned short mark[Q3_FL];        // wave 1's visit epochs (slots < Q3_FL)
   double sp_apex[3];
   double c_dist[8];                  // MINvisible, MAXcoplanar, DISTround, MINdenom, MINdenom_2, NEARzero[3]
   double c_interior[3];
-  int ph, sp_done, sp_ok, sp_facet, sp_furthest, sp_pos, sp_nvis, sp_nnew, sp_status;
+  int ph, sp_done, sp_ok, sp_facet, sp_furthest, sp_pos, sp_nvis, sp_nnew, sp_status, sp_sharp;
   unsigned sp_key;
   int pub_qhead, pub_qtail;
+  int pub_adopt, pub_nnew;           // the published cone was wave 1's: it writes the vertex records
 };
 static_assert(sizeof(Q3L) <= 160 * 1024, "k_qhull's LDS exceeds a CU");
 
@@ -988,7 +991,15 @@ __device__ __forceinline__ int q3_wait(const int* p, int v, bool ne) {
   return x;
 }
 
-__device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep, unsigned ep2) {
+// Wave 1's queue window: entries qcb .. qcb + qcn - 1 in its lanes (entries
+// never change once written), across the speculations of one build.
+struct Q3QC {
+  int qcb, qcn, qf, qp;
+  unsigned qk;
+  double qx, qy, qz;
+};
+
+__device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep, unsigned ep2, Q3QC& Q) {
   const unsigned long long ltmask = (1ull << lane) - 1ull;
   Q3S C;   // the constants q3_plane reads
   C.MINvisible = L.c_dist[0]; C.MAXcoplanar = L.c_dist[1]; C.DISTround = L.c_dist[2];
@@ -1001,40 +1012,62 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
     if (f < Q3_FL) q3_lds_st(L.mark[f], ep);
     else q3_glb_st(W.mark2[f], ep2);
   };
+  // 0. the cone wave 0 adopted from the last speculation: its vertex records
+  // (slots allocated by wave 0, points in this wave's ncoord2, apex in
+  // sp_apex), before any of them is read
+  if (L.pub_adopt) {
+    const int nn = L.pub_nnew;
+    for (int t = lane; t < nn; t += 64) {
+      Q3V& v = W.vv[L.nslot[t]];
+      const double* nc = W.ncoord2 + 9 * t;
+      *reinterpret_cast<double4*>(v.p) = make_double4(L.sp_apex[0], L.sp_apex[1], L.sp_apex[2], nc[0]);
+      *reinterpret_cast<double4*>(v.p + 4) = make_double4(nc[1], nc[2], nc[3], nc[4]);
+      *reinterpret_cast<double2*>(v.p + 8) = make_double2(nc[5], 0.0);
+      *reinterpret_cast<int4*>(v.id) = make_int4(L.nv[3 * t], L.nv[3 * t + 1], L.nv[3 * t + 2], 0);
+    }
+    hl_sync();
+  }
   int ok = 0;
   // 1. the queue's next live facet with points (not one insertion k made visible)
   const int qt = L.pub_qtail;
   int facet = -1, furthest = -1, fpos = -1;
   unsigned fkey = 0;
   double apex[3] = {0.0, 0.0, 0.0};
-  for (int qh = L.pub_qhead; qh < qt; qh += 64) {
-    const int pos = qh + lane;
+  for (int qh = L.pub_qhead; qh < qt;) {
+    if (qh >= Q.qcb + Q.qcn || qh < Q.qcb) {
+      Q.qcb = qh;
+      Q.qcn = min(64, qt - qh);
+      if (lane < Q.qcn) {
+        Q.qf = W.fq[qh + lane];
+        Q.qk = W.fqk[qh + lane];
+        const HullPt e = W.fqc[qh + lane];
+        Q.qx = e.x; Q.qy = e.y; Q.qz = e.z; Q.qp = e.q;
+      }
+    }
     bool good = false;
-    int f = 0;
-    unsigned k = 0, c = 0;
-    if (pos < qt) {
-      f = W.fq[pos];
-      k = W.fqk[pos];
-      const int fa = q3_fa(W, L, f);
-      c = q3_cc(W, L, f);
-      good = (fa & QF_LIVE) && !(fa & QF_VISIBLE) && q3_key(W, L, f) == k && (c & 0xffffu) > 0;
+    unsigned c = 0;
+    if (lane < Q.qcn && Q.qcb + lane >= qh && Q.qcb + lane < qt) {
+      const int fa = q3_fa(W, L, Q.qf);
+      c = q3_cc(W, L, Q.qf);
+      good = (fa & QF_LIVE) && !(fa & QF_VISIBLE) && q3_key(W, L, Q.qf) == Q.qk && (c & 0xffffu) > 0;
     }
     const unsigned long long b = __ballot(good);
     if (b) {
       const int l = __ffsll((long long)b) - 1;
-      fpos = qh + l;
-      facet = __builtin_amdgcn_readlane(f, l);
-      fkey = (unsigned)__builtin_amdgcn_readlane((int)k, l);
+      fpos = Q.qcb + l;
+      facet = __builtin_amdgcn_readlane(Q.qf, l);
+      fkey = (unsigned)__builtin_amdgcn_readlane((int)Q.qk, l);
       furthest = (int)((unsigned)__builtin_amdgcn_readlane((int)c, l) >> 16);
-      const HullPt e = W.fqc[fpos];
-      if (e.q == furthest) { apex[0] = e.x; apex[1] = e.y; apex[2] = e.z; }
-      else {
+      if (__builtin_amdgcn_readlane(Q.qp, l) == furthest) {
+        apex[0] = hl_rl(Q.qx, l); apex[1] = hl_rl(Q.qy, l); apex[2] = hl_rl(Q.qz, l);
+      } else {
         apex[0] = W.Pr[3 * (size_t)furthest];
         apex[1] = W.Pr[3 * (size_t)furthest + 1];
         apex[2] = W.Pr[3 * (size_t)furthest + 2];
       }
       break;
     }
+    qh = Q.qcb + Q.qcn;
   }
   int ls = 0, nvis = 0, nnew = 0, ts = 0, lm = 0;
   if (facet >= 0) {
@@ -1081,6 +1114,9 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
       if (nvis > Q3_VISCAP) cap = true;
     }
     // 3. the cone: one new facet per horizon ridge, as wave 0's
+    const bool one = 3 * nvis <= 64;   // one ridge per lane: its points stay in registers
+    int my_t = -1;
+    double P1[3] = {0.0, 0.0, 0.0}, P2[3] = {0.0, 0.0, 0.0}, PO[3] = {0.0, 0.0, 0.0};
     if (!cap) {
       for (int vi = lane; vi < nvis; vi += 64) L.sp_repl[vi] = -1;
       hl_sync();
@@ -1095,6 +1131,10 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
           nb = q3_nb(W, L, vis, c - 3 * vi);
           q3_tp(W, L, nb, hn, &hfa);
           ridge = !marked(nb);
+          if (c == 3 * vi) {
+            const Q3V& vw = W.vv[vis];
+            L.sp_vvert[3 * vi] = vw.id[0]; L.sp_vvert[3 * vi + 1] = vw.id[1]; L.sp_vvert[3 * vi + 2] = vw.id[2];
+          }
         }
         const unsigned long long b = __ballot(ridge);
         if (ridge) {
@@ -1122,6 +1162,10 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
             int fl = QF_NEW | QF_LIVE | (top ? QF_TOP : 0);
             q3_plane(C, lm, apex, p1, p2, top, q, &flipped);
             if (flipped) { fl |= QF_FLIPPED; lm |= QHS_FLIPPED; }
+            if (one) {
+              my_t = t;
+              for (int k = 0; k < 3; k++) { P1[k] = p1[k]; P2[k] = p2[k]; PO[k] = po[k]; }
+            }
             L.sp_nflag[t] = fl;
             L.sp_npl[4 * t] = q[0]; L.sp_npl[4 * t + 1] = q[1]; L.sp_npl[4 * t + 2] = q[2]; L.sp_npl[4 * t + 3] = q[3];
             for (int k = 0; k < 3; k++) {
@@ -1132,6 +1176,56 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
         nnew += __popcll(b);
       }
       ok = nnew <= Q3_NEWCAP;
+      if (ok) {
+        hl_sync();
+        // qh_matchnewfacets (nb1: the other new facet with v2, nb2: with v1) and
+        // qh_checkzero, as wave 0's
+        for (int t = lane; t < nnew; t += 64) {
+          int nbu[2] = {-1, -1}, cnt[2] = {0, 0};
+          const int w0 = L.sp_v2[t], w1 = L.sp_v1[t];
+#pragma unroll 4
+          for (int u = 0; u < nnew; u++) {
+            const int a = L.sp_v1[u], bb = L.sp_v2[u];
+            const bool o = u != t;
+            if (o && (a == w0 || bb == w0)) { nbu[0] = u; cnt[0]++; }
+            if (o && (a == w1 || bb == w1)) { nbu[1] = u; cnt[1]++; }
+          }
+          if (cnt[0] != 1 || cnt[1] != 1) lm |= QHS_TOPOLOGY;
+          L.sp_nn1[t] = nbu[0] >= 0 ? nbu[0] : 0;
+          L.sp_nn2[t] = nbu[1] >= 0 ? nbu[1] : 0;
+        }
+        hl_sync();
+        if (!(qh_wave_or(lm) & QHS_FLIPPED)) {
+          auto zero = [&](int t, const double* p1, const double* p2, const double* po) {
+            const double d1 = q3_distq(L.sp_npl + 4 * L.sp_nn1[t], p1);
+            const double d2 = q3_distq(L.sp_npl + 4 * L.sp_nn2[t], p2);
+            const double d3 = q3_distq(L.sp_npl + 4 * t, po);
+            if (d1 >= -2 * C.DISTround || d2 >= -2 * C.DISTround || d3 >= -2 * C.DISTround) lm |= QHS_NONCONVEX;
+          };
+          if (one) {
+            if (my_t >= 0) zero(my_t, P1, P2, PO);
+          } else {
+            for (int t = lane; t < nnew; t += 64) {
+              double p1[3], p2[3], po[3];
+              for (int k = 0; k < 3; k++) {
+                p1[k] = W.ncoord2[9 * t + k]; p2[k] = W.ncoord2[9 * t + 3 + k]; po[k] = W.ncoord2[9 * t + 6 + k];
+              }
+              zero(t, p1, p2, po);
+            }
+          }
+        }
+        // qh_sharpnewfacets
+        bool diff = false;
+        if (nnew > 0) {
+          const bool q0 = L.sp_npl[0] > 0, q1 = L.sp_npl[1] > 0, q2 = L.sp_npl[2] > 0;
+          for (int t = lane; t < nnew; t += 64) {
+            const double* nn = L.sp_npl + 4 * t;
+            diff |= (nn[0] > 0) != q0 || (nn[1] > 0) != q1 || (nn[2] > 0) != q2;
+          }
+        }
+        const bool sh = __ballot(diff) != 0ull;
+        if (lane == 0) L.sp_sharp = sh;
+      }
     }
   }
   const int st = qh_wave_or(ls | ts | lm);
@@ -1554,8 +1648,8 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
         L.visf[vi] = f;
         L.repl[vi] = L.sp_repl[vi];
         q3_set_fa(W, L, f, q3_fa(W, L, f) | QF_VISIBLE);
-        const Q3V& vw = W.vv[f];
-        L.vvert[3 * vi] = vw.id[0]; L.vvert[3 * vi + 1] = vw.id[1]; L.vvert[3 * vi + 2] = vw.id[2];
+        L.vvert[3 * vi] = L.sp_vvert[3 * vi]; L.vvert[3 * vi + 1] = L.sp_vvert[3 * vi + 1];
+        L.vvert[3 * vi + 2] = L.sp_vvert[3 * vi + 2];
         L.vsoff[vi] = W.soff[f];
         L.vscnt[vi] = (int)(q3_cc(W, L, f) & 0xffffu);
       }
@@ -1564,6 +1658,8 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
         L.nhz[t] = L.sp_nhz[t];
         L.nhskip[t] = L.sp_nhskip[t];
         L.nflag[t] = L.sp_nflag[t];
+        L.nn1[t] = L.sp_nn1[t];
+        L.nn2[t] = L.sp_nn2[t];
         for (int k = 0; k < 4; k++) L.npl[4 * t + k] = L.sp_npl[4 * t + k];
       }
       S.status |= L.sp_status;
@@ -1732,44 +1828,54 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     const unsigned key0 = S.keyc;
     auto finish = [&](int t, const double* p1, const double* p2) {
       // nb1: the other new facet with v2, nb2: the other one with v1 (one pass)
-      int nbu[2] = {-1, -1}, cnt[2] = {0, 0};
-      const int w0 = L.nv[3 * t + 2], w1 = L.nv[3 * t + 1];
+      int nbu[2] = {-1, -1};
+      if (adopt) {   // matched by wave 1 (a topology failure is in its status)
+        nbu[0] = L.nn1[t];
+        nbu[1] = L.nn2[t];
+      } else {
+        int cnt[2] = {0, 0};
+        const int w0 = L.nv[3 * t + 2], w1 = L.nv[3 * t + 1];
 #pragma unroll 4
-      for (int u = 0; u < nnew; u++) {
-        const int a = L.nv[3 * u + 1], b = L.nv[3 * u + 2];
-        const bool o = u != t;
-        if (o && (a == w0 || b == w0)) { nbu[0] = u; cnt[0]++; }
-        if (o && (a == w1 || b == w1)) { nbu[1] = u; cnt[1]++; }
+        for (int u = 0; u < nnew; u++) {
+          const int a = L.nv[3 * u + 1], b = L.nv[3 * u + 2];
+          const bool o = u != t;
+          if (o && (a == w0 || b == w0)) { nbu[0] = u; cnt[0]++; }
+          if (o && (a == w1 || b == w1)) { nbu[1] = u; cnt[1]++; }
+        }
+        if (cnt[0] != 1 || cnt[1] != 1) lm |= QHS_TOPOLOGY;
+        L.nn1[t] = nbu[0] >= 0 ? nbu[0] : 0;
+        L.nn2[t] = nbu[1] >= 0 ? nbu[1] : 0;
       }
-      if (cnt[0] != 1 || cnt[1] != 1) lm |= QHS_TOPOLOGY;
-      L.nn1[t] = nbu[0] >= 0 ? nbu[0] : 0;
-      L.nn2[t] = nbu[1] >= 0 ? nbu[1] : 0;
       const int s = L.nslot[t];
       const double q[4] = {L.npl[4 * t], L.npl[4 * t + 1], L.npl[4 * t + 2], L.npl[4 * t + 3]};
       q3_set_facet(W, L, s, q, L.nhz[t], nbu[0] >= 0 ? L.nslot[nbu[0]] : 0, nbu[1] >= 0 ? L.nslot[nbu[1]] : 0,
                    L.nflag[t] | (t << 8));
       q3_set_key(W, L, s, key0 + (unsigned)t);
       q3_set_cc(W, L, s, 0u);
-      Q3V& v = W.vv[s];
-      *reinterpret_cast<double4*>(v.p) = make_double4(apexp[0], apexp[1], apexp[2], p1[0]);
-      *reinterpret_cast<double4*>(v.p + 4) = make_double4(p1[1], p1[2], p2[0], p2[1]);
-      *reinterpret_cast<double2*>(v.p + 8) = make_double2(p2[2], 0.0);
-      *reinterpret_cast<int4*>(v.id) = make_int4(furthest, L.nv[3 * t + 1], L.nv[3 * t + 2], 0);
+      if (!adopt) {   // (an adopted cone's records: wave 1 writes them from its copy)
+        Q3V& v = W.vv[s];
+        *reinterpret_cast<double4*>(v.p) = make_double4(apexp[0], apexp[1], apexp[2], p1[0]);
+        *reinterpret_cast<double4*>(v.p + 4) = make_double4(p1[1], p1[2], p2[0], p2[1]);
+        *reinterpret_cast<double2*>(v.p + 8) = make_double2(p2[2], 0.0);
+        *reinterpret_cast<int4*>(v.id) = make_int4(furthest, L.nv[3 * t + 1], L.nv[3 * t + 2], 0);
+      }
       q3_set_nb(W, L, L.nhz[t], L.nhskip[t], s);
     };
     if (one) {
       if (my_t >= 0) finish(my_t, P1, P2);
     } else {
       for (int t = lane; t < nnew; t += 64) {
-        double p1[3], p2[3];
-        for (int k = 0; k < 3; k++) { p1[k] = ncb[9 * t + k]; p2[k] = ncb[9 * t + 3 + k]; }
+        double p1[3] = {0.0, 0.0, 0.0}, p2[3] = {0.0, 0.0, 0.0};
+        if (!adopt)
+          for (int k = 0; k < 3; k++) { p1[k] = ncb[9 * t + k]; p2[k] = ncb[9 * t + 3 + k]; }
         finish(t, p1, p2);
       }
     }
     S.keyc += (unsigned)nnew;
     hl_sync();
-    // qh_checkzero: each new facet clearly convex to its neighbours
-    if (!(qh_wave_or(lm) & QHS_FLIPPED)) {
+    // qh_checkzero: each new facet clearly convex to its neighbours (an
+    // adopted cone's: wave 1's, in its status)
+    if (!adopt && !(qh_wave_or(lm) & QHS_FLIPPED)) {
       auto zero = [&](int t, const double* p1, const double* p2, const double* po) {
         const double d1 = q3_distq(L.npl + 4 * L.nn1[t], p1);
         const double d2 = q3_distq(L.npl + 4 * L.nn2[t], p2);
@@ -1796,6 +1902,8 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     if (lane == 0) {
       L.pub_qhead = S.qhead;
       L.pub_qtail = S.qtail;
+      L.pub_adopt = adopt ? 1 : 0;
+      L.pub_nnew = nnew;
     }
     ++phase;
     if (lane == 0) q3_st_rel(&L.ph, phase);
@@ -1803,7 +1911,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     S.notsharp = 0;
     S.nmov = 0;
     Q3T(5);
-    const int sharp = q3_sharpnewfacets(S, L, lane);
+    const int sharp = adopt ? L.sp_sharp : q3_sharpnewfacets(S, L, lane);
     Q3T(20);
     Q3C(21, 1);
     Q3C(31, adopt ? 1 : 0);   // insertions whose horizon and cone wave 1 speculated
@@ -1987,13 +2095,15 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
       unsigned ep2 = W.ctr[0];
       unsigned short ep = 0;
       int last = 0;
+      Q3QC Q;
+      Q.qcb = 0; Q.qcn = 0; Q.qf = 0; Q.qp = -1; Q.qk = 0u; Q.qx = Q.qy = Q.qz = 0.0;
       for (;;) {
         const int p = q3_wait(&L.ph, last, true);
         if (p < 0 || p == last) break;
         last = p;
         ++ep;
         ++ep2;
-        q3_spec(W, L, lane, ep, ep2);
+        q3_spec(W, L, lane, ep, ep2, Q);
         hl_sync();
         if (lane == 0) q3_st_rel(&L.sp_done, p);
       }
