@@ -41,7 +41,7 @@ namespace lqro {
 #define Q3_FSTK 512       // free facet slots kept for reuse (more are left unused)
 #define Q3_ND (Q3_NEWCAP + Q3_MOVCAP)
 #ifndef Q3_FL
-#define Q3_FL 2368        // facet slots with their hot fields in LDS
+#define Q3_FL 2304        // facet slots with their hot fields in LDS
 #endif
 
 struct Q3G {              // a facet slot >= Q3_FL, 64 B
@@ -177,6 +177,16 @@ struct Q3L {
   unsigned sp_key;
   int pub_qhead, pub_qtail;
   int pub_adopt, pub_nnew;           // the published cone was wave 1's: it writes the vertex records
+  // wave 1 locating a long partition sequence's odd chunks (request hq_*,
+  // results hr_*, sequence numbers hreq / hres, hbusy: the request it took)
+  HullPt hr_pt[64];
+  double hr_d[64];
+  int hr_f[64], hr_k[64];
+  int hr_ls;
+  int hstate;                        // request r: 4 r + 1 posted, + 2 taken, + 3 done; 4 r cancelled
+  int hq_c, hq_from, hq_np, hq_sharp, hq_init, hq_prestart;
+  int hq_findbestnew, hq_notsharp, hq_nnew, hq_nmov, hq_nvis;
+  double hq_max_outside;
 };
 static_assert(sizeof(Q3L) <= 160 * 1024, "k_qhull's LDS exceeds a CU");
 
@@ -671,6 +681,63 @@ __device__ __forceinline__ HullPt q3_seqpt(const Q3W& W, const Q3L& L, int nvis,
   return W.sb[L.vsoff[a] + pos - (L.vinc[a] - L.vscnt[a])];
 }
 
+__device__ __forceinline__ int q3_ld_acq(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void q3_st_rel(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// wait (bounded) until *p != v (ne) or == v (!ne); the last value read
+__device__ __forceinline__ int q3_wait(const int* p, int v, bool ne) {
+  int x = q3_ld_acq(p);
+  for (long w = 0; (ne ? x == v : x != v) && w < (1l << 24); ++w) {
+    __builtin_amdgcn_s_sleep(1);
+    x = q3_ld_acq(p);
+  }
+  return x;
+}
+
+// One chunk of the partition sequence located under the state S: the point
+// at position c + lane (when from <= pos < np), its facet, distance and
+// flags (qh_locate).  Wave 0 runs it for its chunks, wave 1 for the odd
+// chunks of a long sequence under a copy of wave 0's state.
+__device__ __forceinline__ void q3_chunk_locate(const Q3W& W, const Q3S& S, const Q3L& L, int c, int from, int np,
+                                                int sharp, bool init, int lane, const HullPt& pre, int prestart,
+                                                bool havepre, HullPt& pt, int& f, double& d, int& isout, int& trig,
+                                                int& ls) {
+  const int pos = c + lane;
+  pt = pre;
+  f = -1; d = 0.0; isout = 0; trig = 0;
+  if (pos >= from && pos < np) {
+    int start = prestart;
+    if (!(havepre && c == 0)) pt = q3_seqpt(W, L, S.nvis, init, pos, &start);
+    const double p[3] = {pt.x, pt.y, pt.z};
+    f = q3_locate(W, S, L, p, start, sharp, &d, &isout, &trig, ls);
+  }
+}
+
+// wave 1: serve a chunk request (the state wave 0 had when it asked)
+__device__ inline void q3_serve_chunk(const Q3W& W, Q3L& L, int lane) {
+  Q3S S;
+  S.MINvisible = L.c_dist[0]; S.MAXcoplanar = L.c_dist[1]; S.DISTround = L.c_dist[2];
+  S.MINoutside = 2 * S.MINvisible;
+  S.findbestnew = L.hq_findbestnew; S.notsharp = L.hq_notsharp;
+  S.nnew = L.hq_nnew; S.nmov = L.hq_nmov; S.nvis = L.hq_nvis;
+  S.max_outside = L.hq_max_outside;
+  HullPt pt, pre;
+  pre.x = pre.y = pre.z = 0.0; pre.q = -1; pre.pad = 0;
+  int f, isout, trig, ls = 0;
+  double d;
+  q3_chunk_locate(W, S, L, L.hq_c, L.hq_from, L.hq_np, L.hq_sharp, L.hq_init != 0, lane, pre, L.hq_prestart, false,
+                  pt, f, d, isout, trig, ls);
+  L.hr_pt[lane] = pt;
+  L.hr_d[lane] = d;
+  L.hr_f[lane] = f;
+  L.hr_k[lane] = isout | (trig << 1);
+  const int st = qh_wave_or(ls);
+  if (lane == 0) L.hr_ls = st;
+}
+
 // Locate the partition sequence in order (lqro_qhull.hpp qh_locate_seq) and
 // count each point into its destination (a new facet's index, or Q3_NEWCAP
 // + k for the k-th old facet to receive points) once its result is final.
@@ -689,6 +756,35 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
   rd = 0.0;
   rpt = pre;
   hl_sync();
+  // a sequence of more than two chunks: wave 1 locates every other chunk
+  // (requested one chunk ahead under the current state; a result computed
+  // before an event changed the state is never asked for)
+  const bool help = np > 128;
+  int req = L.hstate >> 2, req_c = -1;   // the last request and its chunk
+  auto resolve = [&]() -> bool {   // true: wave 1 answered request `req`
+    if (req_c < 0) return false;
+    req_c = -1;
+    int st = q3_ld_acq(&L.hstate);
+    if (st == 4 * req + 1) {   // not taken yet: withdraw it
+      const int o = lane == 0 ? atomicCAS(&L.hstate, 4 * req + 1, 4 * req) : 0;
+      st = __builtin_amdgcn_readlane(o, 0);
+      if (st == 4 * req + 1) return false;
+    }
+    st = q3_wait(&L.hstate, 4 * req + 3, false);
+    return st == 4 * req + 3;
+  };
+  auto post = [&](int c2, int from2) {
+    resolve();
+    ++req;
+    if (lane == 0) {
+      L.hq_c = c2; L.hq_from = from2; L.hq_np = np; L.hq_sharp = sharp; L.hq_init = init ? 1 : 0;
+      L.hq_prestart = prestart;
+      L.hq_findbestnew = S.findbestnew; L.hq_notsharp = S.notsharp; L.hq_nnew = S.nnew; L.hq_nmov = S.nmov;
+      L.hq_nvis = S.nvis; L.hq_max_outside = S.max_outside;
+      q3_st_rel(&L.hstate, 4 * req + 1);
+    }
+    req_c = c2;
+  };
   int from = 0;
   while (from < np) {
     int ev_pos = np, ev_kind = 0, ev_dst = -1;
@@ -700,14 +796,23 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
       int kind = 0, ls = 0, dst = -1, dfa = 0;
       double d = 0.0;
       HullPt pt = pre;
+      int f = -1, isout = 0, trig = 0;
+      bool got = false;
+      if (help && req_c == c) {
+        got = resolve();
+        if (got) {
+          pt = L.hr_pt[lane]; d = L.hr_d[lane]; f = L.hr_f[lane];
+          isout = L.hr_k[lane] & 1; trig = (L.hr_k[lane] >> 1) & 1;
+          ls = L.hr_ls;
+        }
+      } else if (help && c + 64 < np) {
+        post(c + 64, from);   // the next chunk to wave 1
+      }
+      Q3T(12);
+      if (!got)
+        q3_chunk_locate(W, S, L, c, from, np, sharp, init, lane, pre, prestart, havepre, pt, f, d, isout, trig, ls);
+      Q3T(13);
       if (act) {
-        int start = prestart;
-        if (!(havepre && c == 0)) pt = q3_seqpt(W, L, S.nvis, init, pos, &start);
-        const double p[3] = {pt.x, pt.y, pt.z};
-        Q3T(12);
-        int isout, trig;
-        const int f = q3_locate(W, S, L, p, start, sharp, &d, &isout, &trig, ls);
-        Q3T(13);
         if (isout) {
           dst = f;
           dfa = q3_fa(W, L, f);
@@ -766,6 +871,7 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
     }
     if (ev_pos < np) {
       Q3C(24, 1);
+      resolve();   // (a chunk wave 1 located under the old state is not used)
       if (ev_kind & 1) {
         if (sharp) S.findbestnew = 1;
         else S.notsharp = 1;
@@ -806,6 +912,7 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
     }
     from = ev_pos + 1;
   }
+  resolve();   // wave 1 is not left working on this sequence
 }
 
 // The located points into their destinations' outside sets, in sequence
@@ -975,22 +1082,6 @@ __device__ __forceinline__ int q3_alloc(const Q3S& S, const Q3L& L, int t) {
 // and cone are exactly the sequential ones as long as the facet is still the
 // queue's next with the same key and furthest point when wave 0 checks it.
 // Wave 1 marks visited facets with its own epochs (no facet flag written).
-__device__ __forceinline__ int q3_ld_acq(const int* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void q3_st_rel(int* p, int v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// wait (bounded) until *p != v (ne) or == v (!ne); the last value read
-__device__ __forceinline__ int q3_wait(const int* p, int v, bool ne) {
-  int x = q3_ld_acq(p);
-  for (long w = 0; (ne ? x == v : x != v) && w < (1l << 24); ++w) {
-    __builtin_amdgcn_s_sleep(1);
-    x = q3_ld_acq(p);
-  }
-  return x;
-}
-
 // Wave 1's queue window: entries qcb .. qcb + qcn - 1 in its lanes (entries
 // never change once written), across the speculations of one build.
 struct Q3QC {
@@ -2079,7 +2170,7 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
     if (slot < 0) break;
     // a fresh handshake and wave 1's epochs for this job (ordered by
     // hull_points' barriers)
-    if (threadIdx.x == 0) { L.ph = 0; L.sp_done = 0; }
+    if (threadIdx.x == 0) { L.ph = 0; L.sp_done = 0; L.hstate = 0; }
     for (int q = threadIdx.x; q < Q3_FL / 2; q += blockDim.x) reinterpret_cast<unsigned*>(L.mark)[q] = 0u;
     const int lrow = slot / A.npr, jj = A.nbr_list ? A.nbr_list[slot] : slot % A.npr;
     const int i = A.row_begin + lrow * A.row_stride;
@@ -2097,15 +2188,33 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
       int last = 0;
       Q3QC Q;
       Q.qcb = 0; Q.qcn = 0; Q.qf = 0; Q.qp = -1; Q.qk = 0u; Q.qx = Q.qy = Q.qz = 0.0;
+      long idle = 0;
       for (;;) {
-        const int p = q3_wait(&L.ph, last, true);
-        if (p < 0 || p == last) break;
-        last = p;
-        ++ep;
-        ++ep2;
-        q3_spec(W, L, lane, ep, ep2, Q);
-        hl_sync();
-        if (lane == 0) q3_st_rel(&L.sp_done, p);
+        const int p = q3_ld_acq(&L.ph);
+        if (p != last) {
+          if (p < 0) break;
+          last = p;
+          ++ep;
+          ++ep2;
+          q3_spec(W, L, lane, ep, ep2, Q);
+          hl_sync();
+          if (lane == 0) q3_st_rel(&L.sp_done, p);
+          idle = 0;
+          continue;
+        }
+        const int hs = q3_ld_acq(&L.hstate);
+        if ((hs & 3) == 1) {   // a chunk request: take it unless wave 0 withdrew it
+          const int o = lane == 0 ? atomicCAS(&L.hstate, hs, hs + 1) : 0;
+          if (__builtin_amdgcn_readlane(o, 0) == hs) {
+            q3_serve_chunk(W, L, lane);
+            hl_sync();
+            if (lane == 0) q3_st_rel(&L.hstate, hs + 2);
+          }
+          idle = 0;
+          continue;
+        }
+        if (++idle > (1l << 24)) break;
+        __builtin_amdgcn_s_sleep(1);
       }
       if (lane == 0) W.ctr[0] = ep2;
       continue;   // (hull_take_job's barrier meets wave 0 there)
