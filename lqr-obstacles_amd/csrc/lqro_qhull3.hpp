@@ -42,6 +42,12 @@ namespace lqro {
 #define Q3_ND (Q3_NEWCAP + Q3_MOVCAP)
 #ifndef Q3_FL
 #define Q3_FL 2304        // facet slots with their hot fields in LDS
+#define Q3_PROF_RETRY (32 + 2 * 4096 + 16)   // profile words: builds handed to k_qhull_big (16)
+#ifdef LQRO_QHULL_PROFILE
+#define Q3_CAPBIT(b) (b)   // which cap sent a build to k_qhull_big (scripts/qhull_prof.py)
+#else
+#define Q3_CAPBIT(b) 0
+#endif
 #endif
 
 struct Q3G {              // a facet slot >= Q3_FL, 64 B
@@ -491,7 +497,7 @@ __device__ inline int q3_findbesthorizon(const Q3W& W, const Q3S& S, const Q3L& 
       // (a neighbour listed twice: the first takes it)
       const bool seen = seen3[k] || (k >= 1 && nb == cur[0]) || (k == 2 && nb == cur[1]);
       if (seen) continue;
-      if (nvis == Q3_HZCAP) { lstatus |= QHS_CAPACITY; return bestfacet; }
+      if (nvis == Q3_HZCAP) { lstatus |= QHS_CAPACITY | Q3_CAPBIT(QHS_CAP_HZ); return bestfacet; }
       q3_lds_st(vis[64 * nvis], (unsigned short)nb);
       nvis++;
       if (!(fl[k] & QF_FLIPPED)) {
@@ -506,7 +512,7 @@ __device__ inline int q3_findbesthorizon(const Q3W& W, const Q3S& S, const Q3L& 
         }
       }
       if (nextfacet >= 0) {
-        if (ncop == Q3_COPCAP) { lstatus |= QHS_CAPACITY; return bestfacet; }
+        if (ncop == Q3_COPCAP) { lstatus |= QHS_CAPACITY | Q3_CAPBIT(QHS_CAP_COP); return bestfacet; }
         cop[64 * ncop++] = nextfacet;
       }
       nextfacet = nb;
@@ -840,7 +846,7 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
         for (int t = 0; t < S.nold; t++)
           if (L.oldf[t] == f) k = t;
         if (k < 0) {
-          if (S.nold == Q3_MOVCAP) { S.status |= QHS_CAPACITY; continue; }
+          if (S.nold == Q3_MOVCAP) { S.status |= QHS_CAPACITY | Q3_CAPBIT(QHS_CAP_MOV); continue; }
           k = S.nold++;
           if (lane == 0) { L.oldf[k] = f; L.pcnt[Q3_NEWCAP + k] = 0; L.dfac[Q3_NEWCAP + k] = f; }
           hl_sync();
@@ -882,7 +888,7 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
         // facet moves behind the new ones (a fresh key)
         const int f = ev_dst;
         if (S.nmov == Q3_MOVCAP) {
-          S.status |= QHS_CAPACITY;
+          S.status |= QHS_CAPACITY | Q3_CAPBIT(QHS_CAP_MOV);
           return;
         }
         if (lane == 0) {
@@ -952,7 +958,7 @@ __device__ inline void q3_emit_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int ndn
     base += __shfl(inc, 63);
   }
   if (base > W.SB) {
-    S.status |= QHS_CAPACITY;
+    S.status |= QHS_CAPACITY | Q3_CAPBIT(QHS_CAP_SB);
     return;
   }
   S.sbtop = base;
@@ -1057,7 +1063,7 @@ __device__ inline void q3_emit_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int ndn
       W.fqc[qt + t] = r;
     }
   qt += S.nmov;
-  if (qt > W.QC) S.status |= QHS_CAPACITY;
+  if (qt > W.QC) S.status |= QHS_CAPACITY | Q3_CAPBIT(QHS_CAP_FACETS);
   S.qtail = qt;
   hl_sync();
   Q3T(18);
@@ -1350,7 +1356,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
   S.keyc = 1;
   S.qhead = S.qtail = 0;
   if (W.FC > 65535) {   // 16-bit facet and point ids
-    S.status |= QHS_CAPACITY;
+    S.status |= QHS_CAPACITY | Q3_CAPBIT(QHS_CAP_FACETS);
     return;
   }
   // qh_maxmin
@@ -1551,7 +1557,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
         hl_sync();
       }
       if (cnt) {
-        if (off + cnt > W.SB) { S.status |= QHS_CAPACITY; return; }
+        if (off + cnt > W.SB) { S.status |= QHS_CAPACITY | Q3_CAPBIT(QHS_CAP_SB); return; }
         if (lane == 0) {
           HullPt r;
           r.x = cx; r.y = cy; r.z = cz; r.q = champ; r.pad = 0;
@@ -1806,7 +1812,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
         hl_sync();
       }
       lo = hi;
-      if (nvis > Q3_VISCAP) { S.status |= QHS_CAPACITY; return; }
+      if (nvis > Q3_VISCAP) { S.status |= QHS_CAPACITY | Q3_CAPBIT(QHS_CAP_VIS); return; }
     }
     S.status |= qh_wave_or(ls);
     S.nvis = nvis;
@@ -1881,7 +1887,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     Q3T(19);
     }   // (speculation adopted / computed here)
     S.status |= qh_wave_or(ts);
-    if (nnew > Q3_NEWCAP) S.status |= QHS_CAPACITY;
+    if (nnew > Q3_NEWCAP) S.status |= QHS_CAPACITY | Q3_CAPBIT(QHS_CAP_NEW);
     if (S.status & (QHS_TOPOLOGY | QHS_CAPACITY)) return;
     S.nnew = nnew;
     hl_sync();
@@ -1907,7 +1913,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
       // slots: the visible facets', then free ones, then fresh ones
       const int extra = nnew > nvis ? nnew - nvis : 0;
       const int take = extra < S.nfs ? extra : S.nfs;
-      if (S.nalloc + extra - take > W.FC) { S.status |= QHS_CAPACITY; return; }
+      if (S.nalloc + extra - take > W.FC) { S.status |= QHS_CAPACITY | Q3_CAPBIT(QHS_CAP_FACETS); return; }
       for (int t = lane; t < nnew; t += 64) L.nslot[t] = q3_alloc(S, L, t);
       S.nfs -= take;
       S.nalloc += extra - take;
@@ -2234,6 +2240,14 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
       if (lane == 0) {
         const int r = atomicAdd(A.rcount, 1);
         if (r < A.cap) A.rqueue[r] = slot;
+#ifdef LQRO_QHULL_PROFILE
+        // the builds handed to k_qhull_big: count, the caps they hit, slots
+        if (A.prof) {
+          const unsigned long long k = atomicAdd(&A.prof[Q3_PROF_RETRY], 1ull);
+          atomicOr(&A.prof[Q3_PROF_RETRY + 1], (unsigned long long)S.status);
+          if (k < 14) A.prof[Q3_PROF_RETRY + 2 + k] = (unsigned long long)slot | ((unsigned long long)S.status << 32);
+        }
+#endif
       }
       hl_sync();
       continue;

@@ -14,7 +14,7 @@ lqro.LIB_PATH = os.path.join(os.path.dirname(lqro.LIB_PATH), os.environ.get("LQR
 L = lqro.lib()
 box = float(sys.argv[1]) if len(sys.argv) > 1 else None
 N, H, NP = 1024, 100, 100
-x, vg = lqro.synthetic_swarm(N, box=box, seed=7) if box else lqro.synthetic_swarm(N)
+x, vg = lqro.synthetic_swarm(N, box=box) if box else lqro.synthetic_swarm(N)
 g = lqro.synthesize_gains()
 c = lqro.Context(lqro.config(N, H, NP, flags=lqro.LQRO_FLAG_QHULL_ORDER))
 c.set_gains(g["A"], g["B"], g["L"], g["E"])
@@ -54,3 +54,10 @@ for k in o[:8]:
 print("us/insertion: all", 1e3 * cyc.sum() / max(ins.sum(), 1),
       "slots < 2752:", 1e3 * cyc[nsl < 2752].sum() / max(ins[nsl < 2752].sum(), 1),
       "slots >= 2752:", 1e3 * cyc[nsl >= 2752].sum() / max(ins[nsl >= 2752].sum(), 1), int((nsl >= 2752).sum()), "hulls")
+nr = int(out[32 + 2 * 4096 + 16])
+if nr:
+    caps = {0x100: "horizon walk", 0x200: "coplanar set", 0x400: "moved facets", 0x800: "outside-set buffer",
+            0x1000: "visible facets", 0x2000: "new facets", 0x4000: "facet slots / queue"}
+    st = int(out[32 + 2 * 4096 + 17])
+    print("builds handed to k_qhull_big:", nr, "caps:", [v for b, v in caps.items() if st & b],
+          "slots:", [(int(w) & 0xffffffff, hex(int(w) >> 32)) for w in out[32 + 2 * 4096 + 18:32 + 2 * 4096 + 18 + min(nr, 14)]])
