@@ -91,3 +91,23 @@ def test_oracle_reference_rule_step(oracle, lqro_mod, gains, case):
     assert np.array_equal((ins["flags"] & 0x40) != 0, g["stale"] != 0)
     assert np.array_equal(v.view(np.uint64), d[f"{case}_newv"].view(np.uint64))
     assert np.array_equal(oracle.carry_normal(), d[f"{case}_carry"])
+
+
+def test_k_qhull_caps_and_the_wide_insertion(oracle, lqro_mod, gains):
+    """k_qhull's per-insertion caps (csrc/lqro_qhull3.hpp) against the widest
+    insertion of the crowded 30 m swarm (scripts/qhull_caps.py over its 421
+    inside-hull pairs, oracle build statistics): pair (1018, 516) has one
+    insertion with 166 visible and 116 new facets, beyond Q3_VISCAP, so its
+    build goes to k_qhull_big (measured: 70 ms of the 30 m step's 108 ms hull
+    phase, profiles/r3h_crowded30_plain_trace.txt); every other cap holds."""
+    import re
+    src = open(os.path.join(os.path.dirname(__file__), "..", "lqr-obstacles_amd", "csrc", "lqro_qhull3.hpp")).read()
+    cap = {k: int(re.search(rf"#define Q3_{k} (\d+)", src).group(1)) for k in ("VISCAP", "NEWCAP", "HZCAP", "COPCAP")}
+    x, _ = lqro_mod.synthetic_swarm(1024, box=30.0)
+    T, NCF = oracle.tables(gains["A"], gains["B"], gains["L"], gains["E"], 100)
+    _, _, pts = oracle.pair(T, NCF, oracle.sphere(100), x[1018], x[516], 1018, 516, want_points=True)
+    oracle.qhull(pts)
+    st = oracle.last_qhull_stats
+    assert st["st_visible_max"] == 166 and st["st_new_max"] == 116, st
+    assert st["st_visible_max"] > cap["VISCAP"] and st["st_new_max"] <= cap["NEWCAP"]
+    assert st["st_horizon_max"] <= cap["HZCAP"] and st["st_cop_max"] <= cap["COPCAP"]
