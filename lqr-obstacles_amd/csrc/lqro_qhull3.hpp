@@ -34,7 +34,9 @@
 namespace lqro {
 
 #define Q3_NEWCAP 128     // new facets of one insertion (more: the pair goes to k_qhull_big)
-#define Q3_VISCAP 128     // visible facets of one insertion
+#ifndef Q3_VISCAP
+#define Q3_VISCAP 128     // visible facets of one insertion (-DQ3_VISCAP=192: scripts/build_variant.sh)
+#endif
 #define Q3_MOVCAP 16      // old facets moved / receiving points in one partition
 #define Q3_HZCAP 24       // facets one point's horizon walk visits
 #define Q3_COPCAP 8       // its coplanar facet set
