@@ -34,7 +34,10 @@ enum {
   LQRO_E_STATE = -4,     /* call order violated (e.g. step before gains)   */
   LQRO_E_SINGULAR = -5,  /* singular 3x3 C*G_k (reference asserts, MAT:632) */
   LQRO_E_NODEVICE = -6,  /* no usable gfx950 device                        */
-  LQRO_E_OVERFLOW = -7   /* an internal work queue overflowed              */
+  LQRO_E_OVERFLOW = -7,  /* an internal work queue overflowed              */
+  LQRO_E_HULL = -8       /* an inside-hull pair's hull exceeded the in-kernel */
+                         /*   hull's capacity: its half-plane is missing     */
+                         /*   (lqro_get_hull_failures names the pairs)       */
 };
 
 /* ---- flags ------------------------------------------------------------- */
@@ -183,7 +186,8 @@ int lqro_set_neighbors(lqro_ctx* ctx, double neighbor_dist, int32_t max_neighbor
 /* One control step: the pair loop LQRO:1393-1436 for the context's rows.
  * x: n_agents*X agent states (Quadrotor::x), vgoal: n_agents*3,
  * newv: n_agents*3 (only rows [row_begin,row_end) are written).  Host
- * pointers; blocks until newv is ready. */
+ * pointers; blocks until newv is ready.  Returns LQRO_E_HULL (newv still
+ * written) when an inside-hull pair got no half-plane. */
 int lqro_step(lqro_ctx* ctx, const double* x, const double* vgoal, double* newv);
 
 /* Same, device-resident: d_x, d_vgoal, d_newv are device pointers on the
@@ -195,6 +199,10 @@ int lqro_step(lqro_ctx* ctx, const double* x, const double* vgoal, double* newv)
  * entry per pair slot, so a step cannot overflow it. */
 int lqro_step_device(lqro_ctx* ctx, const double* d_x, const double* d_vgoal,
                      double* d_newv, void* stream);
+/* (The device-resident calls cannot report a hull failure when they return:
+ * lqro_get_stats()[4] / lqro_get_hull_failures after the step do.  While a
+ * lqro_step_device_begin is pending, every call but lqro_step_device_end
+ * returns LQRO_E_STATE.) */
 
 /* lqro_step_device in two halves around the exchange a row-sharded caller
  * needs in Qhull order (LQRO_FLAG_QHULL_ORDER): the loop-carried
@@ -236,6 +244,19 @@ int lqro_get_records(lqro_ctx* ctx, lqro_pair_record* out, int64_t capacity, int
 /* Counters of the last step: [0]=pairs, [1]=planes, [2]=inside, [3]=hull ok,
  * [4]=hull fail, [5]=gjk backups, [6]=sum n_reach, [7]=sum G-tests. */
 int lqro_get_stats(lqro_ctx* ctx, int64_t* stats8);
+/* The same counters and n - 8 more (n <= 11; words past 10 read 0):
+ * [8] LQRO_FLAG_QHULL_ORDER hulls in which Qhull would merge facets
+ *     (LQRO_REC_QHMERGE: built merge-free);
+ * [9] builds k_qhull's per-insertion caps handed to k_qhull_big;
+ * [10] of those, the ones a wave handshake timeout stopped. */
+int lqro_get_stats_ex(lqro_ctx* ctx, int64_t* stats, int32_t n);
+
+/* The pairs of the last step left without a half-plane because their hull
+ * exceeded the in-kernel hull's capacity (stats [4]; lqro_step then returns
+ * LQRO_E_HULL, the reference's qconvex always returns a hull, LQRO:879-880):
+ * *n_out = their number; pairs[2k], pairs[2k+1] = (i, j) of the first
+ * min(*n_out, 64, capacity). */
+int lqro_get_hull_failures(lqro_ctx* ctx, int64_t* pairs, int64_t capacity, int64_t* n_out);
 
 /* Device time of the kernels of the last step, ms, measured with HIP events on
  * the context's stream: [0]=pair sweep+GJK, [1]=hull, [2]=LP, [3]=whole step. */

@@ -216,6 +216,28 @@ struct HullLdsC {
 // the compiler has to be kept from moving memory operations across this
 // point; no s_waitcnt / s_barrier is needed (a workgroup fence would stall on
 // every outstanding global store).
+// The step's counters (lqro_get_stats_ex): [0..7] lqro_get_stats' words;
+// [8] Qhull-order hulls Qhull would merge facets in (LQRO_REC_QHMERGE);
+// [9] builds k_qhull's caps handed to k_qhull_big; [10] k_qhull wave-handshake
+// timeouts (the build went to k_qhull_big); [11] pairs left without their
+// half-plane, the first LQRO_ST_FAILMAX of their slots in [16 ..]
+#define LQRO_ST_MERGED 8
+#define LQRO_ST_RETRY 9
+#define LQRO_ST_TIMEOUT 10
+#define LQRO_ST_NFAIL 11
+#define LQRO_ST_FAILS 16
+#define LQRO_ST_FAILMAX 64
+#define LQRO_ST_WORDS (LQRO_ST_FAILS + LQRO_ST_FAILMAX)
+
+// an inside-hull pair left without its half-plane (a hull capacity): counted
+// in stats[4] and named, so the step reports it (LQRO_E_HULL) instead of
+// dropping the constraint silently
+__device__ __forceinline__ void hull_fail_note(unsigned long long* stats, int slot) {
+  atomicAdd(&stats[4], 1ull);
+  const unsigned long long k = atomicAdd(&stats[LQRO_ST_NFAIL], 1ull);
+  if (k < LQRO_ST_FAILMAX) stats[LQRO_ST_FAILS + k] = (unsigned long long)slot;
+}
+
 __device__ __forceinline__ void hl_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -617,7 +639,7 @@ __device__ __forceinline__ void hull_select(const HullArgs& A, const Mem& M, LT&
       atomicAdd(&A.stats[3], 1ull);
     } else {
       pl[6] = __int_as_float(0);                         // no usable plane
-      atomicAdd(&A.stats[4], 1ull);
+      hull_fail_note(A.stats, slot);
     }
     if (A.recs && !retry) {
       lqro_pair_record& rec = A.recs[slot];

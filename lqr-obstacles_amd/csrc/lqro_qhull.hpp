@@ -70,6 +70,7 @@ namespace lqro {
 #define QHS_CAP_VIS 0x1000
 #define QHS_CAP_NEW 0x2000
 #define QHS_CAP_FACETS 0x4000
+#define QHS_TIMEOUT 0x8000  // k_qhull: a wave handshake timed out (with QHS_CAPACITY: k_qhull_big rebuilds the pair)
 
 struct QhW {
   double* Pr;      // 3 HNP rounded points (qconvex's input)
@@ -1290,8 +1291,9 @@ __device__ inline void qh_select(const HullArgs& A, const QhW& W, const QhS& S, 
       atomicAdd(&A.stats[3], 1ull);
     } else {
       pl[6] = __int_as_float(0);
-      atomicAdd(&A.stats[4], 1ull);
+      hull_fail_note(A.stats, slot);
     }
+    if (ok && merged) atomicAdd(&A.stats[LQRO_ST_MERGED], 1ull);
     if (A.recs) {
       lqro_pair_record& rec = A.recs[slot];
       rec.flags |= ok ? LQRO_REC_HULL : LQRO_REC_HULLFAIL;

@@ -779,10 +779,14 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
       if (st == 4 * req + 1) return false;
     }
     st = q3_wait(&L.hstate, 4 * req + 3, false);
+    // wave 1 took the request and never answered: it may still write the
+    // results, so the build stops here and k_qhull_big rebuilds the pair
+    if (st != 4 * req + 3) S.status |= QHS_CAPACITY | QHS_TIMEOUT;
     return st == 4 * req + 3;
   };
   auto post = [&](int c2, int from2) {
     resolve();
+    if (S.status & QHS_CAPACITY) return;
     ++req;
     if (lane == 0) {
       L.hq_c = c2; L.hq_from = from2; L.hq_np = np; L.hq_sharp = sharp; L.hq_init = init ? 1 : 0;
@@ -794,7 +798,7 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
     req_c = c2;
   };
   int from = 0;
-  while (from < np) {
+  while (from < np && !(S.status & QHS_CAPACITY)) {
     int ev_pos = np, ev_kind = 0, ev_dst = -1;
     double ev_d = 0.0;
     for (int c = from & ~63; c < np; c += 64) {
@@ -1674,7 +1678,11 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     bool adopt = false;
     if (phase > 0) {
       const int dn = q3_wait(&L.sp_done, phase, false);
-      if (dn == phase && L.sp_ok) {
+      if (dn != phase) {   // wave 1 still speculating (it writes vertex records from L.nslot): stop
+        S.status |= QHS_CAPACITY | QHS_TIMEOUT;
+        return;
+      }
+      if (L.sp_ok) {
         const int F = L.sp_facet;
         const unsigned c = q3_cc(W, L, F);
         adopt = (q3_fa(W, L, F) & QF_LIVE) && q3_key(W, L, F) == L.sp_key && (c & 0xffffu) > 0 &&
@@ -2143,8 +2151,9 @@ __device__ inline void q3_select(const HullArgs& A, const Q3W& W, const Q3L& L, 
       atomicAdd(&A.stats[3], 1ull);
     } else {
       pl[6] = __int_as_float(0);
-      atomicAdd(&A.stats[4], 1ull);
+      hull_fail_note(A.stats, slot);
     }
+    if (ok && merged) atomicAdd(&A.stats[LQRO_ST_MERGED], 1ull);
     if (A.recs) {
       lqro_pair_record& rec = A.recs[slot];
       rec.flags |= ok ? LQRO_REC_HULL : LQRO_REC_HULLFAIL;
@@ -2240,6 +2249,8 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
     if (lane == 0) q3_st_rel(&L.ph, -1);   // the build is over: wave 1 stops
     if (S.status & QHS_CAPACITY) {
       if (lane == 0) {
+        atomicAdd(&A.stats[LQRO_ST_RETRY], 1ull);
+        if (S.status & QHS_TIMEOUT) atomicAdd(&A.stats[LQRO_ST_TIMEOUT], 1ull);
         const int r = atomicAdd(A.rcount, 1);
         if (r < A.cap) A.rqueue[r] = slot;
 #ifdef LQRO_QHULL_PROFILE

@@ -449,6 +449,7 @@ const char* lqro_status_string(int s) {
     case LQRO_E_SINGULAR: return "singular C*G_k";
     case LQRO_E_NODEVICE: return "no gfx950 device";
     case LQRO_E_OVERFLOW: return "work queue overflow";
+    case LQRO_E_HULL: return "an inside-hull pair's hull exceeded the kernel's capacity (lqro_get_hull_failures)";
   }
   return "unknown";
 }
@@ -529,7 +530,7 @@ static int ctx_alloc(lqro_ctx* c) {
   HIPCHK(hipMalloc(&c->d_rq, sizeof(int) * c->hull_cap));
   HIPCHK(hipMalloc(&c->d_lq, sizeof(int) * c->hull_cap));
   HIPCHK(hipMalloc(&c->d_err, sizeof(int)));
-  HIPCHK(hipMalloc(&c->d_stats, sizeof(unsigned long long) * 8));
+  HIPCHK(hipMalloc(&c->d_stats, sizeof(unsigned long long) * LQRO_ST_WORDS));
   HIPCHK(hipHostMalloc((void**)&c->h_inside, 2 * sizeof(unsigned long long), hipHostMallocDefault));
   c->h_inside[0] = c->h_inside[1] = ~0ull;
   for (int k = 0; k < 2; ++k) HIPCHK(hipEventCreateWithFlags(&c->iev[k], hipEventDisableTiming));
@@ -700,6 +701,7 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
 
 int lqro_set_neighbors(lqro_ctx* c, double neighbor_dist, int32_t max_neighbors) {
   if (!c) return LQRO_E_ARG;
+  if (c->pending) return LQRO_E_STATE;   // lqro_step_device_begin's half-step still reads them
   if (max_neighbors <= 0) { c->nbr_k = 0; return LQRO_OK; }
   if (!(neighbor_dist > 0)) return LQRO_E_ARG;
   HIPCHK(hipSetDevice(c->cfg.device));
@@ -719,6 +721,7 @@ int lqro_set_neighbors(lqro_ctx* c, double neighbor_dist, int32_t max_neighbors)
 int lqro_set_gains(lqro_ctx* c, const double* A, const double* B, const double* L,
                    const double* E, int32_t per_agent) {
   if (!c || !A || !B || !L || !E) return LQRO_E_ARG;
+  if (c->pending) return LQRO_E_STATE;   // the pending half-step reads d_T / d_NCF on the caller's stream
   const lqro_config& g = c->cfg;
   HIPCHK(hipSetDevice(g.device));
   const size_t X = g.x_dim, U = g.u_dim, N = g.n_agents;
@@ -788,7 +791,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   if (c->stepped) HIPCHK(hipStreamWaitEvent(s, c->ev[3], 0));
   HIPCHK(hipEventRecord(c->ev[0], s));
   HIPCHK(hipMemsetAsync(c->d_hcount, 0, sizeof(int) * 16, s));
-  HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * 8, s));
+  HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * LQRO_ST_WORDS, s));
   HIPCHK(hipMemsetAsync(c->d_hq, 0xFF, sizeof(int) * (size_t)c->hull_cap, s));
   // Qhull order: the normal the last step's last eligible pair left enters this step
   if (c->qhull_order)
@@ -1090,6 +1093,11 @@ int lqro_step(lqro_ctx* c, const double* x, const double* vgoal, double* newv) {
   int hc = 0;
   HIPCHK(hipMemcpy(&hc, c->d_hcount, sizeof(int), hipMemcpyDeviceToHost));
   if (hc > c->hull_cap) return LQRO_E_OVERFLOW;
+  // a pair whose hull the kernels could not build has no half-plane: the
+  // step says so (the reference always gets a hull from qconvex, LQRO:879-880)
+  unsigned long long nf = 0;
+  HIPCHK(hipMemcpy(&nf, c->d_stats + 4, sizeof nf, hipMemcpyDeviceToHost));
+  if (nf) return LQRO_E_HULL;
   return LQRO_OK;
 }
 
@@ -1286,6 +1294,7 @@ int lqro_calculate_new_v(const float* planes, const int64_t* offsets, int32_t n_
 
 int lqro_set_carry_normal(lqro_ctx* c, const double* n3) {
   if (!c || !n3) return LQRO_E_ARG;
+  if (c->pending) return LQRO_E_STATE;
   HIPCHK(hipSetDevice(c->cfg.device));
   HIPCHK(wait_last_step(c));
   const double v[6] = {n3[0], n3[1], n3[2], n3[0], n3[1], n3[2]};
@@ -1295,6 +1304,7 @@ int lqro_set_carry_normal(lqro_ctx* c, const double* n3) {
 
 int lqro_get_carry_normal(lqro_ctx* c, double* n3) {
   if (!c || !n3) return LQRO_E_ARG;
+  if (c->pending) return LQRO_E_STATE;
   HIPCHK(hipSetDevice(c->cfg.device));
   HIPCHK(wait_last_step(c));
   HIPCHK(hipMemcpy(n3, c->d_carry + 3, sizeof(double) * 3, hipMemcpyDeviceToHost));
@@ -1303,7 +1313,7 @@ int lqro_get_carry_normal(lqro_ctx* c, double* n3) {
 
 int lqro_get_records(lqro_ctx* c, lqro_pair_record* out, int64_t cap, int64_t* n_out) {
   if (!c || !out) return LQRO_E_ARG;
-  if (!c->d_recs) return LQRO_E_STATE;
+  if (!c->d_recs || c->pending) return LQRO_E_STATE;
   const int64_t n = (int64_t)c->nrows * (c->nbr_k > 0 ? std::min(c->nbr_k, c->npr) : c->npr);
   if (cap < n) return LQRO_E_ARG;
   HIPCHK(hipSetDevice(c->cfg.device));
@@ -1313,14 +1323,43 @@ int lqro_get_records(lqro_ctx* c, lqro_pair_record* out, int64_t cap, int64_t* n
   return LQRO_OK;
 }
 
-int lqro_get_stats(lqro_ctx* c, int64_t* st) {
-  if (!c || !st) return LQRO_E_ARG;
+int lqro_get_stats_ex(lqro_ctx* c, int64_t* st, int32_t n) {
+  if (!c || !st || n < 1) return LQRO_E_ARG;
+  if (c->pending) return LQRO_E_STATE;   // the half-step's counters are not final
   HIPCHK(hipSetDevice(c->cfg.device));
   HIPCHK(wait_last_step(c));
-  unsigned long long h[8];
+  unsigned long long h[LQRO_ST_FAILS];
   HIPCHK(hipMemcpy(h, c->d_stats, sizeof h, hipMemcpyDeviceToHost));
-  for (int k = 0; k < 8; ++k) st[k] = (int64_t)h[k];
-  if (c->nbr_k <= 0) st[0] = (int64_t)c->nrows * c->npr;   // else k_nbr counted the kept pairs
+  if (c->nbr_k <= 0) h[0] = (unsigned long long)c->nrows * c->npr;   // else k_nbr counted the kept pairs
+  for (int k = 0; k < n; ++k) st[k] = k < LQRO_ST_NFAIL ? (int64_t)h[k] : 0;
+  return LQRO_OK;
+}
+
+int lqro_get_stats(lqro_ctx* c, int64_t* st) { return lqro_get_stats_ex(c, st, 8); }
+
+int lqro_get_hull_failures(lqro_ctx* c, int64_t* pairs, int64_t cap, int64_t* n_out) {
+  if (!c || !n_out || (cap > 0 && !pairs)) return LQRO_E_ARG;
+  if (c->pending) return LQRO_E_STATE;
+  HIPCHK(hipSetDevice(c->cfg.device));
+  HIPCHK(wait_last_step(c));
+  unsigned long long h[LQRO_ST_WORDS];
+  HIPCHK(hipMemcpy(h, c->d_stats, sizeof h, hipMemcpyDeviceToHost));
+  const int64_t n = (int64_t)h[LQRO_ST_NFAIL];
+  *n_out = n;
+  const int npr = c->nbr_k > 0 ? std::min(c->nbr_k, c->npr) : c->npr;
+  std::vector<int> nbr;
+  const int64_t m = std::min<int64_t>(std::min<int64_t>(n, LQRO_ST_FAILMAX), cap);
+  if (m > 0 && c->nbr_k > 0) {   // culled rows: slot -> neighbour index
+    nbr.resize((size_t)c->nrows * npr);
+    HIPCHK(hipMemcpy(nbr.data(), c->d_nbrlist, sizeof(int) * nbr.size(), hipMemcpyDeviceToHost));
+  }
+  for (int64_t k = 0; k < m; ++k) {
+    const long slot = (long)h[LQRO_ST_FAILS + k];
+    const int lrow = (int)(slot / npr), jj = nbr.empty() ? (int)(slot % npr) : nbr[slot];
+    const int i = c->rb + lrow * c->rs;
+    pairs[2 * k] = i;
+    pairs[2 * k + 1] = jj < i ? jj : jj + 1;
+  }
   return LQRO_OK;
 }
 
@@ -1376,8 +1415,8 @@ int lqro_debug_hull_points(lqro_ctx* c, const double* pts, int32_t n, const doub
                      hipMalloc(&d_qn, sizeof(double) * 8) != hipSuccess))
     rc = LQRO_E_NOMEM;
   if (rc != LQRO_OK) {
-  } else if (hipMalloc(&d_st, sizeof(unsigned long long) * 8) != hipSuccess ||
-      hipMemset(d_st, 0, sizeof(unsigned long long) * 8) != hipSuccess ||
+  } else if (hipMalloc(&d_st, sizeof(unsigned long long) * LQRO_ST_WORDS) != hipSuccess ||
+      hipMemset(d_st, 0, sizeof(unsigned long long) * LQRO_ST_WORDS) != hipSuccess ||
       hipMalloc(&d_pts, sizeof(double) * (local == 2 ? 6 : 3) * n) != hipSuccess || hipMalloc(&d_x, sizeof(double) * 2 * X) != hipSuccess ||
       hipMalloc(&d_q, sizeof(int) * 16) != hipSuccess || hipMalloc(&d_f, sizeof(int) * 3 * fmax) != hipSuccess ||
       hipMalloc(&d_rec, sizeof(lqro_pair_record)) != hipSuccess || hipMalloc(&d_pl, sizeof(float) * 8) != hipSuccess) {

@@ -25,6 +25,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liblqro.so")
 
 LQRO_OK = 0
+LQRO_E_HULL = -8              # an inside-hull pair's hull exceeded the kernels' capacity (no half-plane)
 LQRO_FLAG_RECORDS = 0x1
 LQRO_FLAG_QHULL_ORDER = 0x2   # the reference's own hull rule over Qhull's build order (k_qhull)
 REC_PLANE, REC_INSIDE, REC_BACKUP, REC_HULL, REC_HULLFAIL, REC_LOCAL = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20
@@ -78,6 +79,7 @@ EXPORTS = (
     "lqro_synthesize_gains_x", "lqro_synthesize_gains_batch_x",
     "lqro_set_carry_normal", "lqro_get_carry_normal",
     "lqro_step_device_begin", "lqro_step_device_end",
+    "lqro_get_stats_ex", "lqro_get_hull_failures",
 )
 
 NORMALS_PER_AGENT = 22   # LQRO_NORMALS_PER_AGENT: 16 propagate + 6 observation
@@ -119,6 +121,8 @@ def lib() -> C.CDLL:
         L.lqro_step_device_end.argtypes = [vp, vp, vp, vp]
         L.lqro_get_records.argtypes = [vp, vp, i64, C.POINTER(i64)]
         L.lqro_get_stats.argtypes = [vp, vp]
+        L.lqro_get_stats_ex.argtypes = [vp, vp, i32]
+        L.lqro_get_hull_failures.argtypes = [vp, vp, i64, C.POINTER(i64)]
         L.lqro_get_timings.argtypes = [vp, vp]
         L.lqro_calculate_new_v.argtypes = [vp, vp, i32, vp, dbl, vp, i32]
         L.lqro_dynamics_step.argtypes = [C.POINTER(Model), i32, i32, i32, C.POINTER(Agents), i32]
@@ -133,6 +137,17 @@ def lib() -> C.CDLL:
 
 class LqroError(RuntimeError):
     pass
+
+
+class HullFailure(LqroError):
+    """lqro_step returned LQRO_E_HULL: inside-hull pairs whose hull exceeded
+    the in-kernel hull's capacity got no half-plane (the reference's qconvex
+    always returns a hull, LQRO:879-880).  .pairs: their (i, j); .newv: the
+    step's new velocities, computed without those planes."""
+
+    def __init__(self, msg, pairs, newv):
+        super().__init__(msg)
+        self.pairs, self.newv = pairs, newv
 
 
 def _check(rc: int, what: str):
@@ -268,8 +283,20 @@ class Context:
         if vgoal.shape != (n, 3):
             raise LqroError(f"step: vgoal has shape {vgoal.shape}, expected {(n, 3)}")
         newv = np.zeros((self.cfg.n_agents, 3))
-        _check(lib().lqro_step(self._h, _p(x), _p(vgoal), _p(newv)), "lqro_step")
+        rc = lib().lqro_step(self._h, _p(x), _p(vgoal), _p(newv))
+        if rc == LQRO_E_HULL:
+            pairs = self.hull_failures()
+            raise HullFailure(f"lqro_step: {len(pairs)} inside-hull pair(s) without a half-plane: "
+                              f"{[tuple(p) for p in pairs[:8]]}", pairs, newv)
+        _check(rc, "lqro_step")
         return newv
+
+    def hull_failures(self) -> np.ndarray:
+        """(i, j) of the last step's pairs left without a half-plane (at most 64)."""
+        out = np.zeros((64, 2), np.int64)
+        n = C.c_int64()
+        _check(lib().lqro_get_hull_failures(self._h, _p(out), 64, C.byref(n)), "lqro_get_hull_failures")
+        return out[:min(n.value, 64)]
 
     def step_device(self, d_x: int, d_vgoal: int, d_newv: int, stream: int = 0):
         """Device pointers (e.g. torch tensor .data_ptr()) on the context's
@@ -302,10 +329,10 @@ class Context:
         return out[:got.value]   # rows x K with neighbour culling on
 
     def stats(self) -> dict:
-        s = np.zeros(8, dtype=np.int64)
-        _check(lib().lqro_get_stats(self._h, _p(s)), "lqro_get_stats")
+        s = np.zeros(11, dtype=np.int64)
+        _check(lib().lqro_get_stats_ex(self._h, _p(s), 11), "lqro_get_stats_ex")
         keys = ("pairs", "planes", "inside", "hull_ok", "hull_fail", "gjk_backups",
-                "sum_n_reach", "sum_gtests")
+                "sum_n_reach", "sum_gtests", "qhull_merged", "qhull_retried", "qhull_timeouts")
         return dict(zip(keys, (int(v) for v in s)))
 
     def carry_normal(self, n=None):

@@ -38,7 +38,7 @@ def test_lib_is_gfx950_code_object(lqro_mod):
 def test_version_and_status_strings(lqro_mod):
     L = lqro_mod.lib()
     assert L.lqro_version() >= 1
-    for rc in (0, -1, -2, -3, -4, -5, -6, -7):
+    for rc in (0, -1, -2, -3, -4, -5, -6, -7, -8):
         s = L.lqro_status_string(rc)
         assert s and len(s) >= 2
 
