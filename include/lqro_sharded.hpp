@@ -32,6 +32,7 @@
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
+#include <functional>
 #include <vector>
 
 #include "lqro_sim.hpp"
@@ -47,17 +48,37 @@ inline void check_nccl(ncclResult_t r, const char* what) {
 
 class ShardedSimulator {
  public:
+  // The row exchange: d is a row-major n x w device table of which every
+  // rank r holds rows [block_begin(n, r, world), block_begin(n, r+1, world));
+  // afterwards every rank holds all of it (an allgatherv), ordered on
+  // `stream`.  The default is RCCL (allgather_rows below); a caller running
+  // several ranks in one process passes its own (tests/cpp/lqro_sharded_main.cpp).
+  using Exchange = std::function<void(double* d, int w, hipStream_t stream)>;
+
   // qlist: every agent (each rank holds the whole list, as the reference's
-  // qlist); this rank owns rows [rank*chunk, min(n, (rank+1)*chunk)) with
-  // chunk = ceil(n / world).  id: ncclGetUniqueId on rank 0, handed to the
-  // others by the caller (a file, MPI, torch.distributed ...).
+  // qlist); rank r owns rows [r*n/world, (r+1)*n/world) — lqro.shard_rows'
+  // balanced blocks, so the C++ and Python hosts lay shards out alike; a
+  // rank may own no row (n < world) and still takes part in the exchanges.
+  // id: ncclGetUniqueId on rank 0, handed to the others by the caller (a
+  // file, MPI, torch.distributed ...).
   ShardedSimulator(std::vector<Quadrotor>& qlist, int horizon, int n_points, int rank, int world,
                    const ncclUniqueId& id, int device = 0)
       : q_(qlist), rank_(rank), world_(world), device_(device) {
+    init(horizon, n_points);
+    check_nccl(ncclCommInitRank(&comm_, world_, id, rank_), "ncclCommInitRank");
+    ex_ = [this](double* d, int w, hipStream_t s) { allgather_rows(d, w, s); };
+  }
+  ShardedSimulator(std::vector<Quadrotor>& qlist, int horizon, int n_points, int rank, int world, Exchange ex,
+                   int device = 0)
+      : q_(qlist), rank_(rank), world_(world), device_(device), ex_(std::move(ex)) {
+    init(horizon, n_points);
+  }
+
+ private:
+  void init(int horizon, int n_points) {
     n_ = (int)q_.size();
-    chunk_ = (n_ + world_ - 1) / world_;
-    rb_ = std::min(n_, rank_ * chunk_);
-    re_ = std::min(n_, rb_ + chunk_);
+    rb_ = block_begin(n_, rank_, world_);
+    re_ = block_begin(n_, rank_ + 1, world_);
     rows_ = re_ - rb_;
     lqro_model_default(&model_);
     lqro_config cfg;
@@ -65,15 +86,16 @@ class ShardedSimulator {
     cfg.device = device_;
     cfg.row_begin = rb_;
     cfg.row_end = re_;
-    check(lqro_create(&cfg, &ctx_), "lqro_create");   // fails loudly without a gfx950 device
+    // (a rank without rows needs no context; a zero-row context is invalid)
+    if (rows_ > 0) check(lqro_create(&cfg, &ctx_), "lqro_create");   // fails loudly without a gfx950 device
+    else check_device();
     check_hip(hipSetDevice(device_), "hipSetDevice");
     check_hip(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
-    check_nccl(ncclCommInitRank(&comm_, world_, id, rank_), "ncclCommInitRank");
-    const size_t npad = (size_t)chunk_ * world_, r = (size_t)std::max(rows_, 1);
-    alloc(&d_x_, npad * kX);
-    alloc(&d_vg_, npad * kV);
-    alloc(&d_newv_, npad * kV);
-    alloc(&d_rowtab_, npad * 4);
+    const size_t na = (size_t)n_, r = (size_t)std::max(rows_, 1);
+    alloc(&d_x_, na * kX);
+    alloc(&d_vg_, na * kV);
+    alloc(&d_newv_, na * kV);
+    alloc(&d_rowtab_, na * 4);
     alloc(&d_rot_, r * 9);
     alloc(&d_xt_, r * kX);
     alloc(&d_rott_, r * 9);
@@ -91,6 +113,8 @@ class ShardedSimulator {
     check_hip(hipMalloc(&d_model_, sizeof(lqro_model)), "hipMalloc");
     upload();
   }
+
+ public:
   ~ShardedSimulator() {
     if (comm_) ncclCommDestroy(comm_);
     for (double* p : {d_x_, d_vg_, d_newv_, d_rowtab_, d_rot_, d_xt_, d_rott_, d_P_, d_ug_, d_pg_, d_nrm_, d_L_, d_E_, d_l_,
@@ -98,13 +122,15 @@ class ShardedSimulator {
       if (p) (void)hipFree(p);
     if (d_model_) (void)hipFree(d_model_);
     if (stream_) (void)hipStreamDestroy(stream_);
-    lqro_destroy(ctx_);
+    if (ctx_) lqro_destroy(ctx_);
   }
   ShardedSimulator(const ShardedSimulator&) = delete;
   ShardedSimulator& operator=(const ShardedSimulator&) = delete;
 
   int row_begin() const { return rb_; }
   int row_end() const { return re_; }
+  // rank r's first row: floor(r n / world) (lqro.shard_rows' block mode)
+  static int block_begin(int n, int r, int world) { return (int)(((long long)r * n) / world); }
 
   // controlMatrices at hover (LQRO:1370-1373), the same synthesis as
   // Simulator::findMatrices, on every rank
@@ -116,7 +142,7 @@ class ShardedSimulator {
     for (auto& q : q_) {
       q.L = q_[0].L; q.E = q_[0].E; q.l = q_[0].l; q.Lh = q_[0].Lh; q.Eh = q_[0].Eh;
     }
-    check(lqro_set_gains(ctx_, A_.data(), B_.data(), q_[0].L.data(), q_[0].E.data(), 0), "lqro_set_gains");
+    if (ctx_) check(lqro_set_gains(ctx_, A_.data(), B_.data(), q_[0].L.data(), q_[0].E.data(), 0), "lqro_set_gains");
     put(d_L_, q_[0].L.data(), kU * kX);
     put(d_E_, q_[0].E.data(), kU * kV);
     put(d_l_, q_[0].l.data(), kU);
@@ -134,11 +160,9 @@ class ShardedSimulator {
     if (world_ > 1) {
       // Qhull order (lqro_config_default): the normal entering each shard is
       // the last one of the rows before it, on whichever rank
-      check(lqro_step_device_begin(ctx_, d_x_, d_vg_, d_rowtab_, stream_), "lqro_step_device_begin");
-      check_nccl(ncclAllGather(d_rowtab_ + (size_t)rank_ * chunk_ * 4, d_rowtab_, (size_t)chunk_ * 4, ncclDouble,
-                               comm_, stream_),
-                 "ncclAllGather");
-      check(lqro_step_device_end(ctx_, d_rowtab_, d_newv_, stream_), "lqro_step_device_end");
+      if (ctx_) check(lqro_step_device_begin(ctx_, d_x_, d_vg_, d_rowtab_, stream_), "lqro_step_device_begin");
+      ex_(d_rowtab_, 4, stream_);
+      if (ctx_) check(lqro_step_device_end(ctx_, d_rowtab_, d_newv_, stream_), "lqro_step_device_end");
     } else {
       check(lqro_step_device(ctx_, d_x_, d_vg_, d_newv_, stream_), "lqro_step_device");
     }
@@ -157,10 +181,8 @@ class ShardedSimulator {
       a.time = t_ * model_.dt;
       check(lqro_dynamics_step_device(d_model_, 1, rows_, 0, &a, stream_), "lqro_dynamics_step_device");
     }
-    // x of every agent for the next pair loop (in place: rank r's block is its send buffer)
-    check_nccl(ncclAllGather(d_x_ + (size_t)rank_ * chunk_ * kX, d_x_, (size_t)chunk_ * kX, ncclDouble, comm_,
-                             stream_),
-               "ncclAllGather");
+    // x of every agent for the next pair loop (in place: rank r's rows are its send buffer)
+    ex_(d_x_, kX, stream_);
     // the host copy waits for the iteration (the normals' staging buffer is reused)
     check_hip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
     ++t_;
@@ -194,6 +216,28 @@ class ShardedSimulator {
   }
 
  private:
+  // The all-gather of a row-major n x w table whose rows [rb_r, re_r) rank r
+  // holds: blocks of unequal size (n not a multiple of world), so one
+  // broadcast per rank, from its rows in place, in one group (allgatherv).
+  void allgather_rows(double* d, int w, hipStream_t stream) {
+    check_nccl(ncclGroupStart(), "ncclGroupStart");
+    for (int r = 0; r < world_; ++r) {
+      const int b = block_begin(n_, r, world_), e = block_begin(n_, r + 1, world_);
+      if (e > b)
+        check_nccl(ncclBroadcast(d + (size_t)b * w, d + (size_t)b * w, (size_t)(e - b) * w, ncclDouble, r, comm_,
+                                 stream),
+                   "ncclBroadcast");
+    }
+    check_nccl(ncclGroupEnd(), "ncclGroupEnd");
+  }
+  // what lqro_create checks, for a rank that owns no row
+  void check_device() {
+    int nd = 0;
+    if (hipGetDeviceCount(&nd) != hipSuccess || device_ >= nd) throw Error("no gfx950 device", LQRO_E_NODEVICE);
+    hipDeviceProp_t pr;
+    if (hipGetDeviceProperties(&pr, device_) != hipSuccess || std::string(pr.gcnArchName).rfind("gfx950", 0) != 0)
+      throw Error("no gfx950 device", LQRO_E_NODEVICE);
+  }
   void alloc(double** p, size_t n) {
     check_hip(hipMalloc(p, sizeof(double) * std::max<size_t>(n, 1)), "hipMalloc");
     check_hip(hipMemsetAsync(*p, 0, sizeof(double) * std::max<size_t>(n, 1), stream_), "hipMemsetAsync");
@@ -243,11 +287,12 @@ class ShardedSimulator {
   }
 
   std::vector<Quadrotor>& q_;
-  int n_ = 0, rank_ = 0, world_ = 1, device_ = 0, chunk_ = 0, rb_ = 0, re_ = 0, rows_ = 0, t_ = 0;
+  int n_ = 0, rank_ = 0, world_ = 1, device_ = 0, rb_ = 0, re_ = 0, rows_ = 0, t_ = 0;
   lqro_model model_;
   lqro_ctx* ctx_ = nullptr;
   hipStream_t stream_ = nullptr;
   ncclComm_t comm_ = nullptr;
+  Exchange ex_;
   std::array<double, kX * kX> A_{};
   std::array<double, kX * kU> B_{};
   std::vector<double> nrm_;
