@@ -208,6 +208,8 @@ struct Q3S {
   double interior[3];
   unsigned long long tph[32];   // LQRO_QHULL_PROFILE: phase cycles 0..20, counters 21..28
   unsigned long long tq;         // LQRO_QHULL_PROFILE: the last stamp
+  unsigned long long tw, nw;     // LQRO_QHULL_PROFILE: waiting for wave 1's speculation
+  unsigned long long tps[24], nps;   // LQRO_QHULL_PROFILE: phases of the one-chunk insertions
 };
 
 #ifdef LQRO_QHULL_PROFILE
@@ -218,6 +220,23 @@ struct Q3S {
 #endif
 // LQRO_QHULL_PROFILE counters: 21 insertions, 22 partitioned points, 23 located
 // chunks, 24 sequence events, 25 emitted destination groups, 31 adopted speculations
+// Wave 1's own phases and wave 0's wait for it (LQRO_QHULL_PROFILE): prof words
+// Q3_PROF_W1 + k: 0 speculation total, 1 the adopted cone's vertex records,
+// 2 queue scan, 3 horizon, 4 cone, 5 match / checkzero / sharp, 6 serving
+// chunks, 7 speculations, 8 chunks served, 9 wave 0 waiting for a speculation,
+// 10 waits; 16 + k: wave 0's phase k (Q3T) over the insertions whose partition
+// sequence fits one chunk (np <= 64), 40 their number; cycles summed over the
+// step's hulls (lqro_debug_prof_words)
+#define Q3_PROF_W1 (32 + 2 * 4096 + 48 + 4 * 4096)
+struct Q3P {
+  unsigned long long t[16];
+  unsigned long long tq;
+};
+#ifdef LQRO_QHULL_PROFILE
+#define W1T(k) do { __builtin_amdgcn_s_waitcnt(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); P.t[k] += t_ - P.tq; P.tq = t_; } while (0)
+#else
+#define W1T(k) do {} while (0)
+#endif
 #ifdef LQRO_QHULL_PROFILE
 #define Q3C(k, v) do { S.tph[k] += (unsigned long long)(v); } while (0)
 #else
@@ -1100,9 +1119,14 @@ struct Q3QC {
   int qcb, qcn, qf, qp;
   unsigned qk;
   double qx, qy, qz;
+  // the last speculated cone when it took one ridge per lane: this lane's new
+  // facet (rt, -1: none) and its ridge points, for its vertex record once
+  // wave 0 adopts the cone (no reload of ncoord2 from global memory)
+  int one, rt;
+  double r[6];
 };
 
-__device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep, unsigned ep2, Q3QC& Q) {
+__device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep, unsigned ep2, Q3QC& Q, Q3P& P) {
   const unsigned long long ltmask = (1ull << lane) - 1ull;
   Q3S C;   // the constants q3_plane reads
   C.MINvisible = L.c_dist[0]; C.MAXcoplanar = L.c_dist[1]; C.DISTround = L.c_dist[2];
@@ -1120,16 +1144,30 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
   // sp_apex), before any of them is read
   if (L.pub_adopt) {
     const int nn = L.pub_nnew;
-    for (int t = lane; t < nn; t += 64) {
-      Q3V& v = W.vv[L.nslot[t]];
-      const double* nc = W.ncoord2 + 9 * t;
-      *reinterpret_cast<double4*>(v.p) = make_double4(L.sp_apex[0], L.sp_apex[1], L.sp_apex[2], nc[0]);
-      *reinterpret_cast<double4*>(v.p + 4) = make_double4(nc[1], nc[2], nc[3], nc[4]);
-      *reinterpret_cast<double2*>(v.p + 8) = make_double2(nc[5], 0.0);
-      *reinterpret_cast<int4*>(v.id) = make_int4(L.nv[3 * t], L.nv[3 * t + 1], L.nv[3 * t + 2], 0);
+    if (Q.one) {
+      if (Q.rt >= 0) {
+        const int t = Q.rt;
+        Q3V& v = W.vv[L.nslot[t]];
+        *reinterpret_cast<double4*>(v.p) = make_double4(L.sp_apex[0], L.sp_apex[1], L.sp_apex[2], Q.r[0]);
+        *reinterpret_cast<double4*>(v.p + 4) = make_double4(Q.r[1], Q.r[2], Q.r[3], Q.r[4]);
+        *reinterpret_cast<double2*>(v.p + 8) = make_double2(Q.r[5], 0.0);
+        *reinterpret_cast<int4*>(v.id) = make_int4(L.nv[3 * t], L.nv[3 * t + 1], L.nv[3 * t + 2], 0);
+      }
+    } else {
+      for (int t = lane; t < nn; t += 64) {
+        Q3V& v = W.vv[L.nslot[t]];
+        const double* nc = W.ncoord2 + 9 * t;
+        *reinterpret_cast<double4*>(v.p) = make_double4(L.sp_apex[0], L.sp_apex[1], L.sp_apex[2], nc[0]);
+        *reinterpret_cast<double4*>(v.p + 4) = make_double4(nc[1], nc[2], nc[3], nc[4]);
+        *reinterpret_cast<double2*>(v.p + 8) = make_double2(nc[5], 0.0);
+        *reinterpret_cast<int4*>(v.id) = make_int4(L.nv[3 * t], L.nv[3 * t + 1], L.nv[3 * t + 2], 0);
+      }
     }
     hl_sync();
   }
+  Q.one = 0;
+  Q.rt = -1;
+  W1T(1);
   int ok = 0;
   // 1. the queue's next live facet with points (not one insertion k made visible)
   const int qt = L.pub_qtail;
@@ -1173,6 +1211,7 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
     qh = Q.qcb + Q.qcn;
   }
   int ls = 0, nvis = 0, nnew = 0, ts = 0, lm = 0;
+  W1T(2);
   if (facet >= 0) {
     // 2. qh_findhorizon, as wave 0's (level order, first occurrence), visits as epochs
     if (lane == 0) L.sp_visf[0] = facet;
@@ -1216,6 +1255,7 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
       lo = hi;
       if (nvis > Q3_VISCAP) cap = true;
     }
+    W1T(3);
     // 3. the cone: one new facet per horizon ridge, as wave 0's
     const bool one = 3 * nvis <= 64;   // one ridge per lane: its points stay in registers
     int my_t = -1;
@@ -1279,6 +1319,12 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
         nnew += __popcll(b);
       }
       ok = nnew <= Q3_NEWCAP;
+      if (one) {
+        Q.one = 1;
+        Q.rt = my_t;
+        for (int k = 0; k < 3; k++) { Q.r[k] = P1[k]; Q.r[3 + k] = P2[k]; }
+      }
+      W1T(4);
       if (ok) {
         hl_sync();
         // qh_matchnewfacets (nb1: the other new facet with v2, nb2: with v1) and
@@ -1332,6 +1378,7 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
     }
   }
   const int st = qh_wave_or(ls | ts | lm);
+  W1T(5);
   hl_sync();
   if (lane == 0) {
     L.sp_ok = ok;
@@ -1669,6 +1716,10 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
   unsigned qk = 0;
   double qx = 0.0, qy = 0.0, qz = 0.0;
   for (;;) {
+#ifdef LQRO_QHULL_PROFILE
+    unsigned long long snap_[21];
+    for (int k = 0; k < 21; k++) snap_[k] = S.tph[k];
+#endif
     // qh_nextfurthest: the first queued facet still alive (same key) with
     // points
     int facet = -1, furthest = -1;
@@ -1677,7 +1728,14 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     // the queue's next live one with points and the same furthest point
     bool adopt = false;
     if (phase > 0) {
+#ifdef LQRO_QHULL_PROFILE
+      const unsigned long long tw_ = __builtin_amdgcn_s_memtime();
+#endif
       const int dn = q3_wait(&L.sp_done, phase, false);
+#ifdef LQRO_QHULL_PROFILE
+      S.tw += __builtin_amdgcn_s_memtime() - tw_;
+      S.nw += 1;
+#endif
       if (dn != phase) {   // wave 1 still speculating (it writes vertex records from L.nslot): stop
         S.status |= QHS_CAPACITY | QHS_TIMEOUT;
         return;
@@ -2034,8 +2092,14 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     }
     if (S.status & QHS_CAPACITY) return;
     // deleted vertices (a visible facet's vertex on no new facet) close to a
-    // new facet: Qhull's qh_partitioncoplanar would act (not restated)
-    {
+    // new facet: Qhull's qh_partitioncoplanar would act (not restated).  The
+    // visible facets are a region of the triangulated sphere (genus 0) whose
+    // boundary is the horizon, one edge per new facet, and qh_matchnewfacets
+    // passed, so every boundary vertex is on exactly two horizon edges.  Euler:
+    // its interior vertices number 2 - b + (nvis - nnew) / 2 with b boundary
+    // cycles, so nnew == nvis + 2 forces b = 1 and none: no deleted vertex is
+    // possible then (97 % of the C3 insertions) and the search is skipped
+    if (nnew != nvis + 2) {
       int lsd = 0;
       for (int t = lane; t < 3 * nvis; t += 64) {
         const int v = L.vvert[t];
@@ -2072,6 +2136,10 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
 #ifdef LQRO_QHULL_PROFILE
     // insertions whose partition sequence is longer than one chunk: 29 cycles, 30 count
     if (np2 > 64) { S.tph[29] += S.tq - tins_; S.tph[30] += 1; }
+    else {
+      for (int k = 0; k < 21; k++) S.tps[k] += S.tph[k] - snap_[k];
+      S.nps += 1;
+    }
 #endif
   }
 }
@@ -2205,7 +2273,11 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
       int last = 0;
       Q3QC Q;
       Q.qcb = 0; Q.qcn = 0; Q.qf = 0; Q.qp = -1; Q.qk = 0u; Q.qx = Q.qy = Q.qz = 0.0;
+      Q.one = 0; Q.rt = -1;
+      for (int k = 0; k < 6; k++) Q.r[k] = 0.0;
       long idle = 0;
+      Q3P P;
+      for (int k = 0; k < 16; k++) P.t[k] = 0;
       for (;;) {
         const int p = q3_ld_acq(&L.ph);
         if (p != last) {
@@ -2213,9 +2285,17 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
           last = p;
           ++ep;
           ++ep2;
-          q3_spec(W, L, lane, ep, ep2, Q);
+#ifdef LQRO_QHULL_PROFILE
+          const unsigned long long t0_ = __builtin_amdgcn_s_memtime();
+          P.tq = t0_;
+#endif
+          q3_spec(W, L, lane, ep, ep2, Q, P);
           hl_sync();
           if (lane == 0) q3_st_rel(&L.sp_done, p);
+#ifdef LQRO_QHULL_PROFILE
+          P.t[0] += __builtin_amdgcn_s_memtime() - t0_;
+          P.t[7] += 1;
+#endif
           idle = 0;
           continue;
         }
@@ -2223,9 +2303,16 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
         if ((hs & 3) == 1) {   // a chunk request: take it unless wave 0 withdrew it
           const int o = lane == 0 ? atomicCAS(&L.hstate, hs, hs + 1) : 0;
           if (__builtin_amdgcn_readlane(o, 0) == hs) {
+#ifdef LQRO_QHULL_PROFILE
+            const unsigned long long t0_ = __builtin_amdgcn_s_memtime();
+#endif
             q3_serve_chunk(W, L, lane);
             hl_sync();
             if (lane == 0) q3_st_rel(&L.hstate, hs + 2);
+#ifdef LQRO_QHULL_PROFILE
+            P.t[6] += __builtin_amdgcn_s_memtime() - t0_;
+            P.t[8] += 1;
+#endif
           }
           idle = 0;
           continue;
@@ -2233,12 +2320,19 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
         if (++idle > (1l << 24)) break;
         __builtin_amdgcn_s_sleep(1);
       }
+#ifdef LQRO_QHULL_PROFILE
+      if (A.prof && lane == 0)
+        for (int k = 0; k < 9; k++) atomicAdd(&A.prof[Q3_PROF_W1 + k], P.t[k]);
+#endif
       if (lane == 0) W.ctr[0] = ep2;
       continue;   // (hull_take_job's barrier meets wave 0 there)
     }
     Q3S S;
 #ifdef LQRO_QHULL_PROFILE
     for (int k = 0; k < 32; k++) S.tph[k] = 0;
+    S.tw = S.nw = 0;
+    for (int k = 0; k < 24; k++) S.tps[k] = 0;
+    S.nps = 0;
     const unsigned long long tjob_ = __builtin_amdgcn_s_memtime();
 #endif
     S.status = 0;
@@ -2276,6 +2370,10 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
     if (A.prof && lane == 0) {
       for (int k = 0; k < 32; k++)
         if (k != 26 && k != 11) atomicAdd(&A.prof[k], S.tph[k]);
+      atomicAdd(&A.prof[Q3_PROF_W1 + 9], S.tw);
+      atomicAdd(&A.prof[Q3_PROF_W1 + 10], S.nw);
+      for (int k = 0; k < 24; k++) atomicAdd(&A.prof[Q3_PROF_W1 + 16 + k], S.tps[k]);
+      atomicAdd(&A.prof[Q3_PROF_W1 + 40], S.nps);
       atomicMax(&A.prof[26], S.tph[27]);
       // per job (words 32 + 2j): cycles; insertions | points << 20 | facet slots << 40
       const unsigned long long j = atomicAdd(&A.prof[11], 1ull);

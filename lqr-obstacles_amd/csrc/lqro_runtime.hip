@@ -39,7 +39,7 @@
 
 // hull: 32 counters + 2 words per job; pair: 16; hull wave phases: 16; local hull hand-overs: 16;
 // local-hull per-job words 4 x 4096
-#define LQRO_PROF_WORDS (32 + 2 * 4096 + 16 + 16 + 16 + 4 * 4096)
+#define LQRO_PROF_WORDS (32 + 2 * 4096 + 16 + 16 + 16 + 4 * 4096 + 64)   // + 64: k_qhull's wave 1 (Q3_PROF_W1)
 #define LQRO_PROF_HULL_WORDS (32 + 2 * 4096 + 32)   // what lqro_debug_hull_profile returns
 
 using namespace lqro;
@@ -1486,6 +1486,16 @@ int lqro_debug_hull_points(lqro_ctx* c, const double* pts, int32_t n, const doub
                   (void*)d_qw, (void*)d_qn})
     if (p) (void)hipFree(p);
   return rc;
+}
+
+/* diagnostic (not in lqro.h): n profile words from offset (k_qhull's wave 1
+ * and per-class phases of a -DLQRO_QHULL_PROFILE build: offset Q3_PROF_W1) */
+int lqro_debug_prof_words(lqro_ctx* c, int64_t offset, int64_t n, unsigned long long* out) {
+  if (!c || !out || offset < 0 || n < 0 || offset + n > LQRO_PROF_WORDS) return LQRO_E_ARG;
+  HIPCHK(hipSetDevice(c->cfg.device));
+  HIPCHK(wait_last_step(c));
+  HIPCHK(hipMemcpy(out, c->d_prof + offset, sizeof(unsigned long long) * (size_t)n, hipMemcpyDeviceToHost));
+  return LQRO_OK;
 }
 
 /* diagnostic (not in lqro.h): k_lhull's per-job words of the last step

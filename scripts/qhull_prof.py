@@ -61,3 +61,25 @@ if nr:
     st = int(out[32 + 2 * 4096 + 17])
     print("builds handed to k_qhull_big:", nr, "caps:", [v for b, v in caps.items() if st & b],
           "slots:", [(int(w) & 0xffffffff, hex(int(w) >> 32)) for w in out[32 + 2 * 4096 + 18:32 + 2 * 4096 + 18 + min(nr, 14)]])
+
+W1 = 32 + 2 * 4096 + 48 + 4 * 4096   # Q3_PROF_W1
+wv = np.zeros(64, np.uint64)
+L.lqro_debug_prof_words(c._h, C.c_int64(W1), C.c_int64(64), wv.ctypes.data_as(C.c_void_p))
+w1 = [int(v) for v in wv]
+if w1[7]:
+    print("wave 1: speculations", w1[7] / jobs, "per hull,", w1[0] / max(w1[7], 1) / GHZ / 1e3, "us each;",
+          "phases us/spec: records %.2f queue %.2f horizon %.2f cone %.2f match+zero+sharp %.2f" %
+          tuple(w1[k] / max(w1[7], 1) / GHZ / 1e3 for k in range(1, 6)))
+    print("wave 1: chunks served", w1[8] / jobs, "per hull,", w1[6] / max(w1[8], 1) / GHZ / 1e3, "us each")
+    print("wave 0 waiting for a speculation: %.3f ms/hull, %.2f us per wait (%d waits/hull)" %
+          (w1[9] / jobs / GHZ / 1e6, w1[9] / max(w1[10], 1) / GHZ / 1e3, w1[10] // jobs))
+nps = w1[16 + 24]
+if nps:
+    print("one-chunk insertions (np <= 64): %.1f per hull; us per insertion by phase:" % (nps / jobs))
+    tot1 = 0
+    for k in range(21):
+        if k != 11 and names[k] != "-":
+            v = w1[16 + k] / nps / GHZ / 1e3
+            tot1 += v
+            print(f"    {names[k]:24s} {v:8.3f}")
+    print("    total %.3f us" % tot1)

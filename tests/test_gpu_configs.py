@@ -18,7 +18,7 @@ C5: 16384 agents with the 12-DoF reduced model (lqro_synthesize_gains_x,
 import numpy as np
 import pytest
 
-from test_gpu_parity import _compare
+from test_gpu_parity import _compare, _flags, _hull_pairs_equal, _oracle_step
 
 pytestmark = pytest.mark.gpu
 
@@ -37,11 +37,14 @@ def _hull_exact(recs, rrecs):
     return inside
 
 
-def test_c4_shard(lqro_mod, oracle, gains):
+@pytest.mark.parametrize("rule", ["qhull", "canonical"])
+def test_c4_shard(lqro_mod, oracle, gains, rule):
+    """C4's first 8-way shard in both inside-hull rules (Qhull order, the
+    default: k_qhull, the carried normal entering the shard 0 as for rank 0)."""
     N, H, NP, rows = 4096, 100, 100, (0, 512)
     x, vg = lqro_mod.synthetic_swarm(N)
     ctx = lqro_mod.Context(lqro_mod.config(N, H, NP, row_begin=rows[0], row_end=rows[1],
-                                           flags=lqro_mod.LQRO_FLAG_RECORDS))
+                                           flags=_flags(lqro_mod, rule)))
     ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
     newv = ctx.step(x, vg)
     recs = ctx.records()
@@ -49,9 +52,9 @@ def test_c4_shard(lqro_mod, oracle, gains):
     ctx.close()
     assert st["pairs"] == 512 * 4095 and st["hull_fail"] == 0
     T, NCF = oracle.tables(gains["A"], gains["B"], gains["L"], gains["E"], H)
-    rv, rrecs = oracle.step(T, NCF, oracle.sphere(NP), x, vg, rows=rows, threads=16)
+    rv, rrecs = _oracle_step(oracle, rule, T, NCF, oracle.sphere(NP), x, vg, rows=rows, threads=16)
     _compare(recs, rrecs)
-    inside = _hull_exact(recs, rrecs)
+    inside = _hull_pairs_equal(lqro_mod, recs, rrecs, rule)
     assert inside.sum() > 0
     clean = np.ones(N, bool)
     clean[rrecs["i"][inside]] = False

@@ -4,16 +4,39 @@ Bar: integer outputs (n_reach, reachable-set hash, inside
 flag, GJK simplex, hull arg-min facet) bit-exact; fp64 GJK outputs and the
 fp32 half-planes bit-exact on the non-hull branch (same operation order);
 newV (fp32 LP) bit-exact when every plane matches.
+
+Tests marked with the `rule` parameter run both inside-hull rules: "qhull",
+the default (LQRO_FLAG_QHULL_ORDER: Qhull's build order, first Fv vertex,
+the loop-carried normal, k_qhull) against the oracle in set_hull_rule(1),
+and "canonical" (the opt-in local-hull rule) against the oracle's default.
 """
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
+RULES = ("qhull", "canonical")
 
-def _run(lqro_mod, oracle, gains, x, vg, H, NP, rows=None):
+
+def _flags(lqro_mod, rule):
+    return lqro_mod.LQRO_FLAG_RECORDS | (lqro_mod.LQRO_FLAG_QHULL_ORDER if rule == "qhull" else 0)
+
+
+def _oracle_step(oracle, rule, *a, **kw):
+    """oracle.step under the hull rule (Qhull order: the carried normal
+    entering the step is 0, as a fresh context's)."""
+    if rule == "qhull":
+        oracle.set_hull_rule(1, round16=False)
+        oracle.carry_normal(np.zeros(3))
+    try:
+        return oracle.step(*a, **kw)
+    finally:
+        oracle.set_hull_rule(0)
+
+
+def _run(lqro_mod, oracle, gains, x, vg, H, NP, rows=None, rule="canonical"):
     N = x.shape[0]
-    kw = dict(flags=lqro_mod.LQRO_FLAG_RECORDS)
+    kw = dict(flags=_flags(lqro_mod, rule))
     if rows is not None:
         kw.update(row_begin=rows[0], row_end=rows[1])
     ctx = lqro_mod.Context(lqro_mod.config(N, H, NP, **kw))
@@ -24,8 +47,25 @@ def _run(lqro_mod, oracle, gains, x, vg, H, NP, rows=None):
     ctx.close()
     T, NCF = oracle.tables(gains["A"], gains["B"], gains["L"], gains["E"], H)
     S = oracle.sphere(NP)
-    rv, rrecs = oracle.step(T, NCF, S, x, vg, rows=rows, threads=8)
+    rv, rrecs = _oracle_step(oracle, rule, T, NCF, S, x, vg, rows=rows, threads=8)
     return newv, recs, st, rv, rrecs
+
+
+def _hull_pairs_equal(lqro_mod, recs, rrecs, rule):
+    """Every inside-hull pair: a plane was built, the arg-min facet (Fv order
+    in Qhull order), the distance and the normal bit for bit; in Qhull order
+    also the stale-normal flag and the facet count."""
+    inside = (rrecs["flags"] & 2) != 0
+    assert np.all(recs["flags"][inside] & 8), "hull failed"
+    assert np.array_equal(recs["facet"][inside], rrecs["facet"][inside])
+    assert np.array_equal(recs["dist"][inside].view(np.uint64), rrecs["dist"][inside].view(np.uint64))
+    assert np.array_equal(recs["normal"][inside].view(np.uint64), rrecs["normal"][inside].view(np.uint64))
+    if rule == "qhull":
+        st = lqro_mod.REC_STALE
+        assert np.array_equal(recs["flags"][inside] & st, rrecs["flags"][inside] & st)
+        assert np.array_equal(recs["n_facets"][inside], rrecs["n_facets"][inside])
+        assert np.array_equal(recs["plane_point"][inside].view(np.uint32), rrecs["plane_point"][inside].view(np.uint32))
+    return inside
 
 
 def _compare(recs, rrecs):
@@ -45,11 +85,13 @@ def _compare(recs, rrecs):
     return o
 
 
+@pytest.mark.parametrize("rule", RULES)
 @pytest.mark.parametrize("N,H,NP", [(4, 50, 100), (24, 50, 100), (16, 100, 100), (10, 200, 50)])
-def test_step_bit_exact(lqro_mod, oracle, gains, N, H, NP):
+def test_step_bit_exact(lqro_mod, oracle, gains, N, H, NP, rule):
     x, vg = lqro_mod.synthetic_swarm(N)
-    newv, recs, st, rv, rrecs = _run(lqro_mod, oracle, gains, x, vg, H, NP)
+    newv, recs, st, rv, rrecs = _run(lqro_mod, oracle, gains, x, vg, H, NP, rule=rule)
     o = _compare(recs, rrecs)
+    _hull_pairs_equal(lqro_mod, recs, rrecs, rule)
     inside = (rrecs["flags"] & 2) != 0
     rows_clean = np.ones(N, bool)
     for r in rrecs[inside]:
@@ -57,10 +99,12 @@ def test_step_bit_exact(lqro_mod, oracle, gains, N, H, NP):
     assert np.array_equal(newv[rows_clean], rv[rows_clean])
 
 
-def test_c2_swarm(lqro_mod, oracle, gains):
+@pytest.mark.parametrize("rule", RULES)
+def test_c2_swarm(lqro_mod, oracle, gains, rule):
     """C2: 64 quadrotors, horizon 50 (4032 pairs)."""
     x, vg = lqro_mod.synthetic_swarm(64)
-    newv, recs, st, rv, rrecs = _run(lqro_mod, oracle, gains, x, vg, 50, 100)
+    newv, recs, st, rv, rrecs = _run(lqro_mod, oracle, gains, x, vg, 50, 100, rule=rule)
+    _hull_pairs_equal(lqro_mod, recs, rrecs, rule)
     _compare(recs, rrecs)
     assert st["pairs"] == 64 * 63
     inside = (rrecs["flags"] & 2) != 0
@@ -117,33 +161,31 @@ def test_cyclic_row_shards(lqro_mod, gains, world):
     assert seen == N * (N - 1)
 
 
-def test_dense_swarm_inside_hull(lqro_mod, oracle, gains):
+@pytest.mark.parametrize("rule", RULES)
+def test_dense_swarm_inside_hull(lqro_mod, oracle, gains, rule):
     """A tight swarm (collision courses) exercises the in-kernel hull."""
     x, vg = lqro_mod.synthetic_swarm(32, box=3.0, seed=11)
-    newv, recs, st, rv, rrecs = _run(lqro_mod, oracle, gains, x, vg, 45, 100)
+    newv, recs, st, rv, rrecs = _run(lqro_mod, oracle, gains, x, vg, 45, 100, rule=rule)
     _compare(recs, rrecs)
-    inside = (rrecs["flags"] & 2) != 0
+    inside = _hull_pairs_equal(lqro_mod, recs, rrecs, rule)
     assert inside.sum() > 0
-    assert np.all(recs["flags"][inside] & 8), "hull failed"
-    assert np.array_equal(recs["facet"][inside], rrecs["facet"][inside])
-    assert np.array_equal(recs["dist"][inside].view(np.uint64), rrecs["dist"][inside].view(np.uint64))
+    if rule == "qhull":   # every plane equals the oracle's: so does every row's LP
+        assert np.array_equal(newv.view(np.uint64), rv.view(np.uint64))
 
 
-@pytest.mark.parametrize("H", [200, 240])
-def test_large_horizon_hull(lqro_mod, oracle, gains, H):
-    """H*NP = 20000 (C5's hull size) runs in k_hull, the LDS topology with
-    its widened outside-set extents; H*NP = 24000 > 21845 runs every hull job
-    in k_hull_big (topology in global memory).  Facets and distances must
-    match the oracle either way."""
+@pytest.mark.parametrize("rule", RULES)
+@pytest.mark.parametrize("H", [200, 240, 256])
+def test_large_horizon_hull(lqro_mod, oracle, gains, H, rule):
+    """Canonical rule: H*NP = 20000 (C5's hull size) runs in k_hull, the LDS
+    topology with its widened outside-set extents; H*NP > 21845 runs every
+    hull job in k_hull_big (topology in global memory).  Qhull order: k_qhull
+    for every size (k_qhull_big beyond its per-insertion caps).  Facets,
+    distances and normals must match the oracle either way."""
     x, vg = lqro_mod.synthetic_swarm(8, box=2.5, seed=5)
-    newv, recs, st, rv, rrecs = _run(lqro_mod, oracle, gains, x, vg, H, 100)
+    newv, recs, st, rv, rrecs = _run(lqro_mod, oracle, gains, x, vg, H, 100, rule=rule)
     _compare(recs, rrecs)
-    inside = (rrecs["flags"] & 2) != 0
+    inside = _hull_pairs_equal(lqro_mod, recs, rrecs, rule)
     assert inside.any()
-    for r, q in zip(recs[inside], rrecs[inside]):
-        assert r["flags"] & 8, "hull failed"
-        assert np.array_equal(r["facet"], q["facet"])
-        assert r["dist"] == q["dist"]
 
 
 def test_c3_full_step(lqro_mod, oracle, gains):
@@ -252,8 +294,9 @@ def test_adaptive_schedule_identical(lqro_mod, gains, monkeypatch):
                 assert np.array_equal(r[f], r0[f]), f
 
 
+@pytest.mark.parametrize("rule", RULES)
 @pytest.mark.parametrize("case", ["two_agents", "far_apart", "max_horizon"])
-def test_edge_cases(lqro_mod, oracle, gains, case):
+def test_edge_cases(lqro_mod, oracle, gains, case, rule):
     """Edge sizes: a single pair each way; a swarm so sparse that no pair
     emits a plane (every LP sees zero planes); the largest horizon the kernels
     take (H = 256 slices, 4 per lane) with NP = 50."""
@@ -266,13 +309,11 @@ def test_edge_cases(lqro_mod, oracle, gains, case):
     else:
         x, vg = lqro_mod.synthetic_swarm(6, box=4.0, seed=4)
         H, NP = 256, 50
-    newv, recs, st, rv, rrecs = _run(lqro_mod, oracle, gains, x, vg, H, NP)
+    newv, recs, st, rv, rrecs = _run(lqro_mod, oracle, gains, x, vg, H, NP, rule=rule)
     _compare(recs, rrecs)
     if case == "far_apart":
         assert st["planes"] == 0 and st["inside"] == 0
-    inside = (rrecs["flags"] & 2) != 0
-    for r, q in zip(recs[inside], rrecs[inside]):
-        assert np.array_equal(r["facet"], q["facet"]) and r["dist"] == q["dist"]
+    _hull_pairs_equal(lqro_mod, recs, rrecs, rule)
     np.testing.assert_allclose(newv, rv, rtol=1e-5, atol=1e-6)
 
 
@@ -356,3 +397,30 @@ def test_local_hull_identical(lqro_mod, gains, monkeypatch, case):
             assert np.array_equal(a, b), f
     assert np.array_equal(v1.view(np.uint64), v0.view(np.uint64))
     assert done >= 0.8 * inside.sum()
+
+
+@pytest.mark.parametrize("kind", ["per_agent", "per_agent_x12_h200"])
+def test_qhull_order_per_agent_gains(lqro_mod, oracle, kind):
+    """The default rule (Qhull order) with per-agent gains from +-1 %-perturbed
+    models, X = 16 and config 5's X = 12 / H = 200, on a dense swarm against
+    the oracle: every record of every pair bit for bit, newV too."""
+    N, H, X = 24, 100, 16
+    if kind == "per_agent_x12_h200":
+        H, X = 200, 12
+    x, vg = lqro_mod.synthetic_swarm(N, box=4.0, seed=9, x_dim=X)
+    g = lqro_mod.synthesize_gains_batch(lqro_mod.perturbed_models(N, seed=17), x_dim=X)
+    A, B, L, E = g["A"][0], g["B"][0], g["L"], g["E"]
+    ctx = lqro_mod.Context(lqro_mod.config(N, H, 100, x_dim=X, flags=_flags(lqro_mod, "qhull")))
+    ctx.set_gains(A, B, L, E, per_agent=True)
+    newv = ctx.step(x, vg)
+    recs = ctx.records()
+    ctx.close()
+    T = np.zeros((N, H, 9))
+    NCF = np.zeros((N, H, 3, X))
+    for i in range(N):
+        T[i], NCF[i] = oracle.tables(A, B, L[i], E[i], H, X=X)
+    rv, rrecs = _oracle_step(oracle, "qhull", T, NCF, oracle.sphere(100), x, vg, per_agent=True, threads=8)
+    _compare(recs, rrecs)
+    inside = _hull_pairs_equal(lqro_mod, recs, rrecs, "qhull")
+    assert inside.sum() > 0
+    assert np.array_equal(newv.view(np.uint64), rv.view(np.uint64))

@@ -56,6 +56,38 @@ def test_qhull_hook_on_injected_pairs(lqro_mod, oracle, gains):
         ctx.close()
 
 
+def test_qhull_hook_on_reference_fixture(lqro_mod, oracle, gains):
+    """k_qhull on the reference's own Qhull fixture (tests/golden/qhull:
+    pointList.txt, the qconvex input LQRO:869-880 writes): the facet list in
+    the order of facetVertices.txt (qconvex Fv) with every facet's vertices
+    in Fv order, and for relative velocities inside the hull the selection
+    of LQRO:925-968 (first Fv vertex, strict '<', facet 0 keeps the carried
+    normal) equal to the oracle's, bit for bit."""
+    from test_oracle_golden import _qhull_fixture
+    pts, planes, fv = _qhull_fixture()
+    pts = np.ascontiguousarray(pts, np.float64)
+    ctx = lqro_mod.Context(lqro_mod.config(2, 100, 100))
+    ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
+    oracle.set_hull_rule(1, round16=False)
+    try:
+        cen = pts.mean(0)
+        for k in (None, 0, 100, 517, 1000):
+            vrel = cen if k is None else cen + 0.9 * (pts[k] - cen)
+            rec, st, fl = ctx.debug_qhull(pts, pts, vrel, max_facets=4096)
+            assert st == 0
+            assert [list(map(int, r)) for r in fl] == [f[1:] for f in fv]
+            nf, dist_o, nrm_o, fac_o, _ = oracle.hull_branch_ref(pts, vrel)
+            assert rec["n_facets"] == nf == len(fv)
+            assert list(rec["facet"]) == list(fac_o)
+            assert rec["dist"] == dist_o
+            assert bool(rec["flags"] & lqro_mod.REC_STALE) == (nrm_o is None)
+            if nrm_o is not None:
+                assert np.array_equal(rec["normal"], nrm_o)
+    finally:
+        oracle.set_hull_rule(0)
+        ctx.close()
+
+
 def _ref_step(lqro_mod, oracle, gains, N, H, box, seed, steps=1):
     kw = {} if box is None else dict(box=box, seed=seed)
     x, vg = lqro_mod.synthetic_swarm(N, **kw)

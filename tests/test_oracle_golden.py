@@ -175,6 +175,22 @@ def test_hull_matches_reference_qhull_fixture(oracle):
         assert abs(np.dot(pl[:3], a) + pl[3]) < 1e-9 * (1 + abs(pl[3]))
 
 
+def test_qhull_order_matches_reference_fixture_in_order(oracle):
+    """The oracle's restatement of Qhull's build (oracle/lqro_qhull.c) on the
+    reference's pointList.txt reproduces qconvex's own output IN ORDER: the
+    facet list of facetVertices.txt (qconvex Fv, LQRO:880) facet for facet,
+    each facet's vertex list in Fv order (its first vertex is the one
+    LQRO:925-937 measures the distance from), and the planes of Planes.txt
+    (qconvex n, LQRO:879, printed %.16g) to 1e-15 relative."""
+    pts, planes, fv = _qhull_fixture()
+    st, got, pl, _ = oracle.qhull(np.ascontiguousarray(pts, np.float64))
+    assert st == 0, f"build status {st}"
+    assert got.shape == (len(fv), 3)
+    assert [list(map(int, r)) for r in got] == [f[1:] for f in fv]
+    err = np.abs(pl - planes) / np.maximum(np.abs(planes), 1.0)
+    assert err.max() <= 1e-15, err.max()
+
+
 def test_hull_cases_are_closed_and_convex(oracle):
     """The inside-hull pairs of the dense golden set (whose qconvex step the
     reference cannot run here): the oracle's hull of the %g-rounded points is
