@@ -24,7 +24,7 @@ void launch_lhull(dim3 grid, hipStream_t s, const HullArgs& A) {
   hipLaunchKernelGGL(k_lhull, grid, dim3(LH_THREADS), 0, s, A);
 }
 
-__global__ void __launch_bounds__(128) k_qhull(HullArgs A) {
+__global__ void __launch_bounds__(192) k_qhull(HullArgs A) {
   __shared__ Q3L L;
   q3_body(A, L);
 }
@@ -37,7 +37,8 @@ __global__ void __launch_bounds__(64) k_qhull_big(HullArgs A) {
 }
 
 void launch_qhull(dim3 grid, hipStream_t s, const HullArgs& A) {
-  hipLaunchKernelGGL(k_qhull, grid, dim3(128), 0, s, A);   // wave 0 builds, wave 1 speculates
+  // wave 0 builds, wave 1 speculates the next insertion, wave 2 prefetches its partition sequence
+  hipLaunchKernelGGL(k_qhull, grid, dim3(192), 0, s, A);
 }
 
 void launch_qhull_big(dim3 grid, hipStream_t s, const HullArgs& A) {

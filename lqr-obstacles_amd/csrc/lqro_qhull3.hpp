@@ -136,9 +136,9 @@ struct Q3L {
   int n, fail, job, slot;
   double eps;
   double tr[3 * 128];
-  double rk[2];                      // (two waves: hull_points' block scans)
-  int ri[2];
-  int scan[2];
+  double rk[4];                      // (up to four waves: hull_points' block scans)
+  int ri[4];
+  int scan[4];
   // facet slots < Q3_FL
   double4 pl[Q3_FL];
   ushort4 tp[Q3_FL];                 // neighbours, QF_* | new-facet index << 8
@@ -178,6 +178,21 @@ struct Q3L {
   int sp_vvert[3 * Q3_VISCAP];                 // the visible facets' vertices
   alignas(32) double sp_npl[4 * Q3_NEWCAP];
   unsigned short mark[Q3_FL];        // wave 1's visit epochs (slots < Q3_FL)
+  // wave 1's horizon: the neighbours of the k-th visible facet, sp_cand[3 k ..],
+  // stored when it is found (its neighbour list is in hand then): a level's
+  // candidates and the cone's ridges are then one LDS read each
+  unsigned short sp_cand[3 * Q3_VISCAP];
+  // Wave 2 prefetches the next partition sequence's head while wave 1 builds
+  // the cone: once wave 1 publishes its horizon (sp_hz = phase, sp_hnvis), the
+  // visible facets' outside-set offsets and sizes and the sequence's first 64
+  // points (pf_pre, and the visible facet each came from, pf_prea) are read
+  // from global memory into LDS (pf_done = phase, pf_np the sequence length).
+  // Wave 0 takes them when no visible facet was a destination of the
+  // partition that ran meanwhile (their outside sets are then unchanged).
+  int sp_hz, sp_hnvis, pf_done, pf_np;
+  int pf_vsoff[Q3_VISCAP], pf_vscnt[Q3_VISCAP];
+  HullPt pf_pre[64];
+  unsigned char pf_prea[64];
   double sp_apex[3];
   double c_dist[8];                  // MINvisible, MAXcoplanar, DISTround, MINdenom, MINdenom_2, NEARzero[3]
   double c_interior[3];
@@ -201,6 +216,7 @@ static_assert(sizeof(Q3L) <= 160 * 1024, "k_qhull's LDS exceeds a CU");
 struct Q3S {
   int nalloc, nfs, sbtop, status, qhead, qtail;
   unsigned keyc;
+  unsigned key0_last;   // the first key of the last insertion's new facets
   int nnew, nvis, nmov, nold;
   int findbestnew, notsharp;
   double MAXabs_coord, MAXsumcoord, MAXwidth, NEARzero[3];
@@ -1126,7 +1142,8 @@ struct Q3QC {
   double r[6];
 };
 
-__device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep, unsigned ep2, Q3QC& Q, Q3P& P) {
+__device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep, unsigned ep2, Q3QC& Q, Q3P& P,
+                               int phase) {
   const unsigned long long ltmask = (1ull << lane) - 1ull;
   Q3S C;   // the constants q3_plane reads
   C.MINvisible = L.c_dist[0]; C.MAXcoplanar = L.c_dist[1]; C.DISTround = L.c_dist[2];
@@ -1215,6 +1232,7 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
   if (facet >= 0) {
     // 2. qh_findhorizon, as wave 0's (level order, first occurrence), visits as epochs
     if (lane == 0) L.sp_visf[0] = facet;
+    if (lane < 3) L.sp_cand[lane] = (unsigned short)q3_nb(W, L, facet, lane);
     mark(facet);
     hl_sync();
     nvis = 1;
@@ -1227,9 +1245,10 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
         int nb = -1;
         bool cand = false;
         double q[4] = {0.0, 0.0, 0.0, 0.0};
+        int nn[3] = {0, 0, 0};
         if (c < ncand) {
-          nb = q3_nb(W, L, L.sp_visf[lo + c / 3], c % 3);
-          int nn[3], fa;
+          nb = L.sp_cand[3 * lo + c];
+          int fa;
           q3_get(W, L, nb, q, nn, &fa);
           cand = !marked(nb);
         }
@@ -1246,7 +1265,12 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
         const unsigned long long bv = __ballot(vis);
         if (vis) {
           const int at = nvis + __popcll(bv & ltmask);
-          if (at < Q3_VISCAP) L.sp_visf[at] = nb;
+          if (at < Q3_VISCAP) {
+            L.sp_visf[at] = nb;
+            L.sp_cand[3 * at] = (unsigned short)nn[0];
+            L.sp_cand[3 * at + 1] = (unsigned short)nn[1];
+            L.sp_cand[3 * at + 2] = (unsigned short)nn[2];
+          }
           mark(nb);
         }
         nvis += __popcll(bv);
@@ -1254,12 +1278,21 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
       }
       lo = hi;
       if (nvis > Q3_VISCAP) cap = true;
+#ifdef LQRO_QHULL_PROFILE
+      P.t[11] += 1;
+#endif
+    }
+    // the horizon to wave 2, which fetches the partition sequence's head
+    if (!cap && lane == 0) {
+      L.sp_hnvis = nvis;
+      q3_st_rel(&L.sp_hz, phase);
     }
     W1T(3);
     // 3. the cone: one new facet per horizon ridge, as wave 0's
     const bool one = 3 * nvis <= 64;   // one ridge per lane: its points stay in registers
-    int my_t = -1;
+    int my_t = -1, rv1 = -1, rv2 = -1;
     double P1[3] = {0.0, 0.0, 0.0}, P2[3] = {0.0, 0.0, 0.0}, PO[3] = {0.0, 0.0, 0.0};
+    unsigned long long rb = 0ull;   // (one pass) the ridge lanes, in new-facet order
     if (!cap) {
       for (int vi = lane; vi < nvis; vi += 64) L.sp_repl[vi] = -1;
       hl_sync();
@@ -1271,7 +1304,7 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
         if (c < 3 * nvis) {
           const int vi = c / 3;
           vis = L.sp_visf[vi];
-          nb = q3_nb(W, L, vis, c - 3 * vi);
+          nb = L.sp_cand[c];
           q3_tp(W, L, nb, hn, &hfa);
           ridge = !marked(nb);
           if (c == 3 * vi) {
@@ -1280,6 +1313,7 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
           }
         }
         const unsigned long long b = __ballot(ridge);
+        if (one) rb = b;
         if (ridge) {
           const int t = nnew + __popcll(b & ltmask);
           const int hskip = hn[0] == vis ? 0 : hn[1] == vis ? 1 : hn[2] == vis ? 2 : -1;
@@ -1305,14 +1339,17 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
             int fl = QF_NEW | QF_LIVE | (top ? QF_TOP : 0);
             q3_plane(C, lm, apex, p1, p2, top, q, &flipped);
             if (flipped) { fl |= QF_FLIPPED; lm |= QHS_FLIPPED; }
-            if (one) {
-              my_t = t;
-              for (int k = 0; k < 3; k++) { P1[k] = p1[k]; P2[k] = p2[k]; PO[k] = po[k]; }
-            }
             L.sp_nflag[t] = fl;
             L.sp_npl[4 * t] = q[0]; L.sp_npl[4 * t + 1] = q[1]; L.sp_npl[4 * t + 2] = q[2]; L.sp_npl[4 * t + 3] = q[3];
-            for (int k = 0; k < 3; k++) {
-              W.ncoord2[9 * t + k] = p1[k]; W.ncoord2[9 * t + 3 + k] = p2[k]; W.ncoord2[9 * t + 6 + k] = po[k];
+            if (one) {   // the ridge's points stay in this lane (no ncoord2)
+              my_t = t;
+              rv1 = h.id[i1];
+              rv2 = h.id[i2];
+              for (int k = 0; k < 3; k++) { P1[k] = p1[k]; P2[k] = p2[k]; PO[k] = po[k]; }
+            } else {
+              for (int k = 0; k < 3; k++) {
+                W.ncoord2[9 * t + k] = p1[k]; W.ncoord2[9 * t + 3 + k] = p2[k]; W.ncoord2[9 * t + 6 + k] = po[k];
+              }
             }
           }
         }
@@ -1329,21 +1366,41 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
         hl_sync();
         // qh_matchnewfacets (nb1: the other new facet with v2, nb2: with v1) and
         // qh_checkzero, as wave 0's
-        for (int t = lane; t < nnew; t += 64) {
+        if (one) {
+          // the ridges are in the lanes in new-facet order: each lane walks
+          // the others' vertex pairs with lane reads (no LDS round trips)
           int nbu[2] = {-1, -1}, cnt[2] = {0, 0};
-          const int w0 = L.sp_v2[t], w1 = L.sp_v1[t];
-#pragma unroll 4
-          for (int u = 0; u < nnew; u++) {
-            const int a = L.sp_v1[u], bb = L.sp_v2[u];
-            const bool o = u != t;
-            if (o && (a == w0 || bb == w0)) { nbu[0] = u; cnt[0]++; }
-            if (o && (a == w1 || bb == w1)) { nbu[1] = u; cnt[1]++; }
+          int u = 0;
+          for (unsigned long long bb = rb; bb; bb &= bb - 1ull, ++u) {
+            const int l = __ffsll((long long)bb) - 1;
+            const int a = __builtin_amdgcn_readlane(rv1, l), c2 = __builtin_amdgcn_readlane(rv2, l);
+            const bool o = u != my_t;
+            if (o && (a == rv2 || c2 == rv2)) { nbu[0] = u; cnt[0]++; }
+            if (o && (a == rv1 || c2 == rv1)) { nbu[1] = u; cnt[1]++; }
           }
-          if (cnt[0] != 1 || cnt[1] != 1) lm |= QHS_TOPOLOGY;
-          L.sp_nn1[t] = nbu[0] >= 0 ? nbu[0] : 0;
-          L.sp_nn2[t] = nbu[1] >= 0 ? nbu[1] : 0;
+          if (my_t >= 0) {
+            if (cnt[0] != 1 || cnt[1] != 1) lm |= QHS_TOPOLOGY;
+            L.sp_nn1[my_t] = nbu[0] >= 0 ? nbu[0] : 0;
+            L.sp_nn2[my_t] = nbu[1] >= 0 ? nbu[1] : 0;
+          }
+        } else {
+          for (int t = lane; t < nnew; t += 64) {
+            int nbu[2] = {-1, -1}, cnt[2] = {0, 0};
+            const int w0 = L.sp_v2[t], w1 = L.sp_v1[t];
+#pragma unroll 4
+            for (int u = 0; u < nnew; u++) {
+              const int a = L.sp_v1[u], bb = L.sp_v2[u];
+              const bool o = u != t;
+              if (o && (a == w0 || bb == w0)) { nbu[0] = u; cnt[0]++; }
+              if (o && (a == w1 || bb == w1)) { nbu[1] = u; cnt[1]++; }
+            }
+            if (cnt[0] != 1 || cnt[1] != 1) lm |= QHS_TOPOLOGY;
+            L.sp_nn1[t] = nbu[0] >= 0 ? nbu[0] : 0;
+            L.sp_nn2[t] = nbu[1] >= 0 ? nbu[1] : 0;
+          }
         }
         hl_sync();
+        W1T(12);
         if (!(qh_wave_or(lm) & QHS_FLIPPED)) {
           auto zero = [&](int t, const double* p1, const double* p2, const double* po) {
             const double d1 = q3_distq(L.sp_npl + 4 * L.sp_nn1[t], p1);
@@ -1363,6 +1420,7 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
             }
           }
         }
+        W1T(13);
         // qh_sharpnewfacets
         bool diff = false;
         if (nnew > 0) {
@@ -1393,6 +1451,44 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
   }
 }
 
+// wave 2: the head of the next partition sequence (qh_partitionvisible: the
+// visible facets' outside sets in visible order) for the horizon wave 1
+// published, into LDS; the apex facet (visible facet 0) loses its furthest
+// point when wave 0 adopts the insertion, so its set counts one less
+__device__ inline void q3_prefetch(const Q3W& W, Q3L& L, int lane, int p) {
+  const int nvis = L.sp_hnvis;
+  int np = 0;
+  for (int c0 = 0; c0 < nvis; c0 += 64) {
+    const int vi = c0 + lane;
+    int cnt = 0;
+    if (vi < nvis) {
+      const int f = L.sp_visf[vi];
+      cnt = (int)(q3_cc(W, L, f) & 0xffffu) - (vi == 0 ? 1 : 0);
+      L.pf_vsoff[vi] = W.soff[f];
+      L.pf_vscnt[vi] = cnt;
+    }
+    np += __builtin_amdgcn_readlane(q3_scan_add(cnt), 63);
+  }
+  hl_sync();
+  if (lane < np) {
+    // the visible facet holding sequence position `lane`
+    int a = 0, base = 0;
+    for (;;) {
+      const int k = L.pf_vscnt[a];
+      if (lane < base + k || a == nvis - 1) break;
+      base += k;
+      ++a;
+    }
+    L.pf_pre[lane] = W.sb[L.pf_vsoff[a] + lane - base];
+    L.pf_prea[lane] = (unsigned char)a;
+  }
+  hl_sync();
+  if (lane == 0) {
+    L.pf_np = np;
+    q3_st_rel(&L.pf_done, p);
+  }
+}
+
 // qh_qhull on W.Pr[0..n) (qconvex's defaults; lqro_qhull.hpp qh_build step
 // for step)
 __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
@@ -1407,6 +1503,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
   S.nnew = S.nvis = S.nmov = S.nold = 0;
   S.findbestnew = S.notsharp = 0;
   S.keyc = 1;
+  S.key0_last = 0;
   S.qhead = S.qtail = 0;
   if (W.FC > 65535) {   // 16-bit facet and point ids
     S.status |= QHS_CAPACITY | Q3_CAPBIT(QHS_CAP_FACETS);
@@ -1727,6 +1824,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     // wave 1's speculation of this insertion: adopted when its facet is still
     // the queue's next live one with points and the same furthest point
     bool adopt = false;
+    bool pfv = false;   // wave 2's prefetch of this insertion's partition sequence is used
     if (phase > 0) {
 #ifdef LQRO_QHULL_PROFILE
       const unsigned long long tw_ = __builtin_amdgcn_s_memtime();
@@ -1808,6 +1906,19 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
       // the speculated visible set (flagged now) and cone
       nvis = L.sp_nvis;
       nnew = L.sp_nnew;
+      // wave 2's copy of the visible facets' outside sets holds unless one of
+      // them received points in the partition since (a destination then: a
+      // new or moved facet of the last insertion, key >= key0_last, or an
+      // old one listed in oldf)
+      if (q3_ld_acq(&L.pf_done) == phase) {
+        bool bad = false;
+        for (int vi = lane; vi < nvis; vi += 64) {
+          const int f = L.sp_visf[vi];
+          bad |= q3_key(W, L, f) >= S.key0_last;
+          for (int t = 0; t < S.nold; t++) bad |= L.oldf[t] == f;
+        }
+        pfv = __ballot(bad) == 0ull;
+      }
       for (int vi = lane; vi < nvis; vi += 64) {
         const int f = L.sp_visf[vi];
         L.visf[vi] = f;
@@ -1815,8 +1926,13 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
         q3_set_fa(W, L, f, q3_fa(W, L, f) | QF_VISIBLE);
         L.vvert[3 * vi] = L.sp_vvert[3 * vi]; L.vvert[3 * vi + 1] = L.sp_vvert[3 * vi + 1];
         L.vvert[3 * vi + 2] = L.sp_vvert[3 * vi + 2];
-        L.vsoff[vi] = W.soff[f];
-        L.vscnt[vi] = (int)(q3_cc(W, L, f) & 0xffffu);
+        if (pfv) {
+          L.vsoff[vi] = L.pf_vsoff[vi];
+          L.vscnt[vi] = L.pf_vscnt[vi];
+        } else {
+          L.vsoff[vi] = W.soff[f];
+          L.vscnt[vi] = (int)(q3_cc(W, L, f) & 0xffffu);
+        }
       }
       for (int t = lane; t < nnew; t += 64) {
         L.nv[3 * t] = furthest; L.nv[3 * t + 1] = L.sp_v1[t]; L.nv[3 * t + 2] = L.sp_v2[t];
@@ -1832,6 +1948,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
       lm = L.sp_status & QHS_FLIPPED;   // (qh_checkzero skips a cone with a flipped facet)
       ncb = W.ncoord2;
       hl_sync();
+      Q3T(2);   // (profile: the adopted cone's copy)
     } else {
     // qh_findhorizon, a level of the breadth-first search at a time: the
     // candidates of a level in (visible facet, neighbour) order, a facet
@@ -1971,12 +2088,21 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
       np2 += __builtin_amdgcn_readlane(inc, 63);
     }
     hl_sync();
+    if (adopt) Q3T(19);   // (profile: the sequence's extent)
     HullPt pre;
     pre.x = pre.y = pre.z = 0.0;
     pre.q = -1;
     pre.pad = 0;
     int prestart = 0;
-    if (lane < np2) pre = q3_seqpt(W, L, nvis, false, lane, &prestart);
+    if (pfv && np2 == L.pf_np) {   // wave 2's head of the sequence
+      if (lane < np2) {
+        pre = L.pf_pre[lane];
+        const int a = L.pf_prea[lane];
+        prestart = L.repl[a] >= 0 ? L.repl[a] : 0;
+      }
+    } else if (lane < np2) {
+      pre = q3_seqpt(W, L, nvis, false, lane, &prestart);
+    }
     {
       // slots: the visible facets', then free ones, then fresh ones
       const int extra = nnew > nvis ? nnew - nvis : 0;
@@ -2037,6 +2163,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
       }
     }
     S.keyc += (unsigned)nnew;
+    S.key0_last = key0;
     hl_sync();
     // qh_checkzero: each new facet clearly convex to its neighbours (an
     // adopted cone's: wave 1's, in its status)
@@ -2255,7 +2382,7 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
     if (slot < 0) break;
     // a fresh handshake and wave 1's epochs for this job (ordered by
     // hull_points' barriers)
-    if (threadIdx.x == 0) { L.ph = 0; L.sp_done = 0; L.hstate = 0; }
+    if (threadIdx.x == 0) { L.ph = 0; L.sp_done = 0; L.hstate = 0; L.sp_hz = 0; L.pf_done = 0; }
     for (int q = threadIdx.x; q < Q3_FL / 2; q += blockDim.x) reinterpret_cast<unsigned*>(L.mark)[q] = 0u;
     const int lrow = slot / A.npr, jj = A.nbr_list ? A.nbr_list[slot] : slot % A.npr;
     const int i = A.row_begin + lrow * A.row_stride;
@@ -2266,6 +2393,24 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
     const double* Ni = A.NCF + (A.per_agent ? (size_t)i * A.H * 3 * A.X : 0);
     const double vrel[3] = {xi[3] - xj[3], xi[4] - xj[4], xi[5] - xj[5]};
     const int n = hull_points(A, L, Ti, Ni, xi, xj, vrel, W.Pr, W.Pf);
+    if (wave == 2) {
+      // prefetch each horizon wave 1 publishes until the build ends
+      int last = 0;
+      long idle = 0;
+      for (;;) {
+        const int hz = q3_ld_acq(&L.sp_hz);
+        if (hz != last && hz > 0) {
+          last = hz;
+          q3_prefetch(W, L, lane, hz);
+          idle = 0;
+          continue;
+        }
+        if (q3_ld_acq(&L.ph) < 0) break;
+        if (++idle > (1l << 24)) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      continue;   // (hull_take_job's barrier meets the other waves there)
+    }
     if (wave == 1) {
       // speculate each published phase until the build ends (ph = -1)
       unsigned ep2 = W.ctr[0];
@@ -2289,7 +2434,7 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
           const unsigned long long t0_ = __builtin_amdgcn_s_memtime();
           P.tq = t0_;
 #endif
-          q3_spec(W, L, lane, ep, ep2, Q, P);
+          q3_spec(W, L, lane, ep, ep2, Q, P, p);
           hl_sync();
           if (lane == 0) q3_st_rel(&L.sp_done, p);
 #ifdef LQRO_QHULL_PROFILE
@@ -2322,7 +2467,7 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
       }
 #ifdef LQRO_QHULL_PROFILE
       if (A.prof && lane == 0)
-        for (int k = 0; k < 9; k++) atomicAdd(&A.prof[Q3_PROF_W1 + k], P.t[k]);
+        for (int k = 0; k < 16; k++) atomicAdd(&A.prof[Q3_PROF_W1 + k], P.t[k]);
 #endif
       if (lane == 0) W.ctr[0] = ep2;
       continue;   // (hull_take_job's barrier meets wave 0 there)

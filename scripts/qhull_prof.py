@@ -68,8 +68,9 @@ L.lqro_debug_prof_words(c._h, C.c_int64(W1), C.c_int64(64), wv.ctypes.data_as(C.
 w1 = [int(v) for v in wv]
 if w1[7]:
     print("wave 1: speculations", w1[7] / jobs, "per hull,", w1[0] / max(w1[7], 1) / GHZ / 1e3, "us each;",
-          "phases us/spec: records %.2f queue %.2f horizon %.2f cone %.2f match+zero+sharp %.2f" %
-          tuple(w1[k] / max(w1[7], 1) / GHZ / 1e3 for k in range(1, 6)))
+          "phases us/spec: records %.2f queue %.2f horizon %.2f cone %.2f match %.2f checkzero %.2f sharp %.2f;"
+          " horizon levels %.2f" %
+          (tuple(w1[k] / max(w1[7], 1) / GHZ / 1e3 for k in (1, 2, 3, 4, 12, 13, 5)) + (w1[11] / max(w1[7], 1),)))
     print("wave 1: chunks served", w1[8] / jobs, "per hull,", w1[6] / max(w1[8], 1) / GHZ / 1e3, "us each")
     print("wave 0 waiting for a speculation: %.3f ms/hull, %.2f us per wait (%d waits/hull)" %
           (w1[9] / jobs / GHZ / 1e6, w1[9] / max(w1[10], 1) / GHZ / 1e3, w1[10] // jobs))
