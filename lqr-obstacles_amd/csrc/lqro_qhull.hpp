@@ -40,8 +40,12 @@
 
 namespace lqro {
 
+#ifndef QH_NEWCAP
 #define QH_NEWCAP 1024    // new facets of one insertion (C5: > 256 seen)
+#endif
+#ifndef QH_VISCAP
 #define QH_VISCAP 2048    // visible facets of one insertion (C5: > 256 seen)
+#endif
 #define QH_HZCAP 64       // facets one point's horizon walk visits (per lane)
 #define QH_COPCAP 16      // qh.coplanarfacetset of one walk (per lane)
 #define QH_MOVCAP 32      // old facets moved behind the new ones in one partition

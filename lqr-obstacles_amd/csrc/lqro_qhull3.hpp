@@ -33,7 +33,9 @@
 
 namespace lqro {
 
+#ifndef Q3_NEWCAP
 #define Q3_NEWCAP 128     // new facets of one insertion (more: the pair goes to k_qhull_big)
+#endif
 #ifndef Q3_VISCAP
 #define Q3_VISCAP 128     // visible facets of one insertion (-DQ3_VISCAP=192: scripts/build_variant.sh)
 #endif
@@ -470,8 +472,11 @@ __device__ __forceinline__ void q3_place(const Q3W& W, unsigned long long grp, i
   double run = -DBL_MAX;                         // the largest distance among them
   if (grp & (grp - 1ull)) {
     const double inc = q3_scan_max(mem ? dd : -DBL_MAX);
-    run = __shfl_up(inc, 1);
-    if (lane == 0) run = -DBL_MAX;
+    // the running maximum before this lane: wave_shr:1 (lane 0 gets -DBL_MAX)
+    const long long u_ = __double_as_longlong(inc);
+    const int lo_ = __builtin_amdgcn_update_dpp(-1, (int)u_, 0x138, 0xf, 0xf, false);
+    const int hi_ = __builtin_amdgcn_update_dpp((int)0xFFEFFFFF, (int)(u_ >> 32), 0x138, 0xf, 0xf, false);
+    run = __longlong_as_double(((long long)hi_ << 32) | (long long)(unsigned)lo_);
   }
   if (cnt > 0) run = fmax(run, mx);
   const bool rec = mem && (cb == 0 || run < dd);
@@ -985,18 +990,14 @@ __device__ inline void q3_emit_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int ndn
         size = cnt0 + L.pcnt[g];
       }
     }
-    int inc = size;
-    for (int off = 1; off < 64; off <<= 1) {
-      const int o = __shfl_up(inc, off);
-      if (lane >= off) inc += o;
-    }
+    const int inc = q3_scan_add(size);   // (DPP: no LDS round trips)
     if (size) {
       L.doff[g] = base + inc - size;
       L.dcnt[g] = cnt0;
       L.dmax[g] = 0.0;
       L.dchamp[g] = -1;
     }
-    base += __shfl(inc, 63);
+    base += __builtin_amdgcn_readlane(inc, 63);
   }
   if (base > W.SB) {
     S.status |= QHS_CAPACITY | Q3_CAPBIT(QHS_CAP_SB);
@@ -1290,8 +1291,9 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
     W1T(3);
     // 3. the cone: one new facet per horizon ridge, as wave 0's
     const bool one = 3 * nvis <= 64;   // one ridge per lane: its points stay in registers
-    int my_t = -1, rv1 = -1, rv2 = -1;
+    int my_t = -1, rv1 = -1, rv2 = -1, mn1 = 0, mn2 = 0;
     double P1[3] = {0.0, 0.0, 0.0}, P2[3] = {0.0, 0.0, 0.0}, PO[3] = {0.0, 0.0, 0.0};
+    double Q4[4] = {0.0, 0.0, 0.0, 0.0};   // (one pass) this lane's new facet's plane
     unsigned long long rb = 0ull;   // (one pass) the ridge lanes, in new-facet order
     if (!cap) {
       for (int vi = lane; vi < nvis; vi += 64) L.sp_repl[vi] = -1;
@@ -1345,6 +1347,7 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
               my_t = t;
               rv1 = h.id[i1];
               rv2 = h.id[i2];
+              for (int k = 0; k < 4; k++) Q4[k] = q[k];
               for (int k = 0; k < 3; k++) { P1[k] = p1[k]; P2[k] = p2[k]; PO[k] = po[k]; }
             } else {
               for (int k = 0; k < 3; k++) {
@@ -1380,8 +1383,10 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
           }
           if (my_t >= 0) {
             if (cnt[0] != 1 || cnt[1] != 1) lm |= QHS_TOPOLOGY;
-            L.sp_nn1[my_t] = nbu[0] >= 0 ? nbu[0] : 0;
-            L.sp_nn2[my_t] = nbu[1] >= 0 ? nbu[1] : 0;
+            mn1 = nbu[0] >= 0 ? nbu[0] : 0;
+            mn2 = nbu[1] >= 0 ? nbu[1] : 0;
+            L.sp_nn1[my_t] = mn1;
+            L.sp_nn2[my_t] = mn2;
           }
         } else {
           for (int t = lane; t < nnew; t += 64) {
@@ -1408,8 +1413,14 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
             const double d3 = q3_distq(L.sp_npl + 4 * t, po);
             if (d1 >= -2 * C.DISTround || d2 >= -2 * C.DISTround || d3 >= -2 * C.DISTround) lm |= QHS_NONCONVEX;
           };
-          if (one) {
-            if (my_t >= 0) zero(my_t, P1, P2, PO);
+          if (one) {   // (the lane's own plane and neighbours from registers)
+            if (my_t >= 0) {
+              const double4 a = q3_lds(*reinterpret_cast<const double4*>(L.sp_npl + 4 * mn1));
+              const double4 b = q3_lds(*reinterpret_cast<const double4*>(L.sp_npl + 4 * mn2));
+              const double qa[4] = {a.x, a.y, a.z, a.w}, qb[4] = {b.x, b.y, b.z, b.w};
+              const double d1 = q3_distq(qa, P1), d2 = q3_distq(qb, P2), d3 = q3_distq(Q4, PO);
+              if (d1 >= -2 * C.DISTround || d2 >= -2 * C.DISTround || d3 >= -2 * C.DISTround) lm |= QHS_NONCONVEX;
+            }
           } else {
             for (int t = lane; t < nnew; t += 64) {
               double p1[3], p2[3], po[3];
@@ -1423,7 +1434,11 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
         W1T(13);
         // qh_sharpnewfacets
         bool diff = false;
-        if (nnew > 0) {
+        if (one && rb) {   // the planes are in the ridge lanes; new facet 0's is the first's
+          const int l0 = __ffsll((long long)rb) - 1;
+          const bool q0 = hl_rl(Q4[0], l0) > 0, q1 = hl_rl(Q4[1], l0) > 0, q2 = hl_rl(Q4[2], l0) > 0;
+          if (my_t >= 0) diff = (Q4[0] > 0) != q0 || (Q4[1] > 0) != q1 || (Q4[2] > 0) != q2;
+        } else if (nnew > 0) {
           const bool q0 = L.sp_npl[0] > 0, q1 = L.sp_npl[1] > 0, q2 = L.sp_npl[2] > 0;
           for (int t = lane; t < nnew; t += 64) {
             const double* nn = L.sp_npl + 4 * t;
@@ -1910,38 +1925,62 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
       // them received points in the partition since (a destination then: a
       // new or moved facet of the last insertion, key >= key0_last, or an
       // old one listed in oldf)
-      if (q3_ld_acq(&L.pf_done) == phase) {
+      // (every LDS read of a lane is issued before its writes: the compiler
+      // cannot tell the speculation's arrays from these and would otherwise
+      // wait on each read in turn)
+      const bool pfr = q3_ld_acq(&L.pf_done) == phase;
+      if (nvis <= 64) {
+        int f = 0, rp = 0, v0 = 0, v1 = 0, v2 = 0, pso = 0, psc = 0, fa = 0;
+        unsigned key = 0u;
         bool bad = false;
-        for (int vi = lane; vi < nvis; vi += 64) {
-          const int f = L.sp_visf[vi];
-          bad |= q3_key(W, L, f) >= S.key0_last;
+        if (lane < nvis) {
+          f = L.sp_visf[lane];
+          rp = L.sp_repl[lane];
+          v0 = L.sp_vvert[3 * lane]; v1 = L.sp_vvert[3 * lane + 1]; v2 = L.sp_vvert[3 * lane + 2];
+          pso = L.pf_vsoff[lane];
+          psc = L.pf_vscnt[lane];
+          fa = q3_fa(W, L, f);
+          key = q3_key(W, L, f);
+          bad = key >= S.key0_last;
           for (int t = 0; t < S.nold; t++) bad |= L.oldf[t] == f;
         }
-        pfv = __ballot(bad) == 0ull;
-      }
-      for (int vi = lane; vi < nvis; vi += 64) {
-        const int f = L.sp_visf[vi];
-        L.visf[vi] = f;
-        L.repl[vi] = L.sp_repl[vi];
-        q3_set_fa(W, L, f, q3_fa(W, L, f) | QF_VISIBLE);
-        L.vvert[3 * vi] = L.sp_vvert[3 * vi]; L.vvert[3 * vi + 1] = L.sp_vvert[3 * vi + 1];
-        L.vvert[3 * vi + 2] = L.sp_vvert[3 * vi + 2];
-        if (pfv) {
-          L.vsoff[vi] = L.pf_vsoff[vi];
-          L.vscnt[vi] = L.pf_vscnt[vi];
-        } else {
+        pfv = pfr && __ballot(bad) == 0ull;
+        if (lane < nvis) {
+          int so = pso, sc = psc;
+          if (!pfv) {
+            so = W.soff[f];
+            sc = (int)(q3_cc(W, L, f) & 0xffffu);
+          }
+          L.visf[lane] = f;
+          L.repl[lane] = rp;
+          q3_set_fa(W, L, f, fa | QF_VISIBLE);
+          L.vvert[3 * lane] = v0; L.vvert[3 * lane + 1] = v1; L.vvert[3 * lane + 2] = v2;
+          L.vsoff[lane] = so;
+          L.vscnt[lane] = sc;
+        }
+      } else {
+        for (int vi = lane; vi < nvis; vi += 64) {
+          const int f = L.sp_visf[vi];
+          L.visf[vi] = f;
+          L.repl[vi] = L.sp_repl[vi];
+          q3_set_fa(W, L, f, q3_fa(W, L, f) | QF_VISIBLE);
+          L.vvert[3 * vi] = L.sp_vvert[3 * vi]; L.vvert[3 * vi + 1] = L.sp_vvert[3 * vi + 1];
+          L.vvert[3 * vi + 2] = L.sp_vvert[3 * vi + 2];
           L.vsoff[vi] = W.soff[f];
           L.vscnt[vi] = (int)(q3_cc(W, L, f) & 0xffffu);
         }
       }
       for (int t = lane; t < nnew; t += 64) {
-        L.nv[3 * t] = furthest; L.nv[3 * t + 1] = L.sp_v1[t]; L.nv[3 * t + 2] = L.sp_v2[t];
-        L.nhz[t] = L.sp_nhz[t];
-        L.nhskip[t] = L.sp_nhskip[t];
-        L.nflag[t] = L.sp_nflag[t];
-        L.nn1[t] = L.sp_nn1[t];
-        L.nn2[t] = L.sp_nn2[t];
-        for (int k = 0; k < 4; k++) L.npl[4 * t + k] = L.sp_npl[4 * t + k];
+        const int a1 = L.sp_v1[t], a2 = L.sp_v2[t], hz = L.sp_nhz[t], hk = L.sp_nhskip[t], fl = L.sp_nflag[t];
+        const int m1 = L.sp_nn1[t], m2 = L.sp_nn2[t];
+        const double4 pl = q3_lds(*reinterpret_cast<const double4*>(L.sp_npl + 4 * t));
+        L.nv[3 * t] = furthest; L.nv[3 * t + 1] = a1; L.nv[3 * t + 2] = a2;
+        L.nhz[t] = hz;
+        L.nhskip[t] = hk;
+        L.nflag[t] = fl;
+        L.nn1[t] = m1;
+        L.nn2[t] = m2;
+        q3_lds_st(*reinterpret_cast<double4*>(L.npl + 4 * t), pl);
       }
       S.status |= L.sp_status;
       S.nvis = nvis;
@@ -2137,10 +2176,13 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
         L.nn1[t] = nbu[0] >= 0 ? nbu[0] : 0;
         L.nn2[t] = nbu[1] >= 0 ? nbu[1] : 0;
       }
+      // (every read before the first write: see the adoption above)
       const int s = L.nslot[t];
-      const double q[4] = {L.npl[4 * t], L.npl[4 * t + 1], L.npl[4 * t + 2], L.npl[4 * t + 3]};
-      q3_set_facet(W, L, s, q, L.nhz[t], nbu[0] >= 0 ? L.nslot[nbu[0]] : 0, nbu[1] >= 0 ? L.nslot[nbu[1]] : 0,
-                   L.nflag[t] | (t << 8));
+      const double4 q4 = q3_lds(*reinterpret_cast<const double4*>(L.npl + 4 * t));
+      const int hz = L.nhz[t], hk = L.nhskip[t], fl = L.nflag[t], id1 = L.nv[3 * t + 1], id2 = L.nv[3 * t + 2];
+      const int s1 = nbu[0] >= 0 ? L.nslot[nbu[0]] : 0, s2 = nbu[1] >= 0 ? L.nslot[nbu[1]] : 0;
+      const double q[4] = {q4.x, q4.y, q4.z, q4.w};
+      q3_set_facet(W, L, s, q, hz, s1, s2, fl | (t << 8));
       q3_set_key(W, L, s, key0 + (unsigned)t);
       q3_set_cc(W, L, s, 0u);
       if (!adopt) {   // (an adopted cone's records: wave 1 writes them from its copy)
@@ -2148,9 +2190,9 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
         *reinterpret_cast<double4*>(v.p) = make_double4(apexp[0], apexp[1], apexp[2], p1[0]);
         *reinterpret_cast<double4*>(v.p + 4) = make_double4(p1[1], p1[2], p2[0], p2[1]);
         *reinterpret_cast<double2*>(v.p + 8) = make_double2(p2[2], 0.0);
-        *reinterpret_cast<int4*>(v.id) = make_int4(furthest, L.nv[3 * t + 1], L.nv[3 * t + 2], 0);
+        *reinterpret_cast<int4*>(v.id) = make_int4(furthest, id1, id2, 0);
       }
-      q3_set_nb(W, L, L.nhz[t], L.nhskip[t], s);
+      q3_set_nb(W, L, hz, hk, s);
     };
     if (one) {
       if (my_t >= 0) finish(my_t, P1, P2);

@@ -94,9 +94,242 @@ LQRO_HD Mat<C, R> tr(const Mat<R, C>& a) {
   return m;
 }
 
+// ---- the pivoted small matrices without indexed storage (N <= 4) ----
+// The reference's full-pivot routines reach rows and columns through the
+// pivot permutations rp, cp (m(rp[i], cp[j])).  On the device a run-time
+// index into a per-lane array is private (scratch) memory: the 3x3
+// exponentials of f, the rotation resets and controllers and the 3x3 / 4x4
+// inverses ran through it in every lane of k_dynw.  For N <= 4 the routines
+// below keep the matrix in its pivoted order instead (M[i][j] = m(rp[i],
+// cp[j])) and move rows and columns with selects; every arithmetic operation
+// takes the operands the indexed version gives it, in the same order, so the
+// results are bit-identical (tests/test_host_abi.py::test_small_pivot_routines
+// checks them against the indexed versions, kept as inverse_ix / solve_ix).
+template <int N>
+LQRO_HD int sm_get(const int (&a)[N], int k) {
+  int r = a[0];
+#pragma unroll
+  for (int t = 1; t < N; ++t) r = k == t ? a[t] : r;
+  return r;
+}
+// the first strict maximum of |M[i][j]|, i, j >= k, in (row, col) order
+template <int N>
+LQRO_HD void sm_pivot(const double (&M)[N][N], int k, int& br, int& bc) {
+  double best = 0.0;
+  br = k;
+  bc = k;
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+      if (i >= k && j >= k) {
+        const double a = fabs(M[i][j]);
+        if (a > best) { best = a; br = i; bc = j; }
+      }
+}
+// swap rows k and r (r >= k run-time) of an N x C array
+template <int N, int C>
+LQRO_HD void sm_swap_rows(double (&M)[N][C], int k, int r) {
+#pragma unroll
+  for (int t = 0; t < N; ++t)
+    if (t > k) {
+      const bool s = r == t;
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        const double a = M[k][j], b = M[t][j];
+        M[k][j] = s ? b : a;
+        M[t][j] = s ? a : b;
+      }
+    }
+}
+template <int N, int C>
+LQRO_HD void sm_swap_cols(double (&M)[N][C], int k, int c) {
+#pragma unroll
+  for (int t = 0; t < C; ++t)
+    if (t > k) {
+      const bool s = c == t;
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const double a = M[i][k], b = M[i][t];
+        M[i][k] = s ? b : a;
+        M[i][t] = s ? a : b;
+      }
+    }
+}
+template <int N>
+LQRO_HD void sm_swap_ix(int (&a)[N], int k, int r) {
+  const int ak = a[k], ar = sm_get(a, r);
+#pragma unroll
+  for (int t = 0; t < N; ++t) {
+    if (t == k) a[t] = ar;
+    else if (t > k) a[t] = r == t ? ak : a[t];
+  }
+}
+
+// P X = Q (operator%, MAT:370-442) for N <= 4; = solve_ix below
+template <int N, int C>
+LQRO_HD Mat<N, C> solve_sm(const Mat<N, N>& p, const Mat<N, C>& q) {
+  double M[N][N], X[N][C];   // M[i][j] = m(rp[i], cp[j]), X[i][j] = x(rp[i], j)
+  int rp[N], cp[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    rp[i] = cp[i] = i;
+#pragma unroll
+    for (int j = 0; j < N; ++j) M[i][j] = p(i, j);
+#pragma unroll
+    for (int j = 0; j < C; ++j) X[i][j] = q(i, j);
+  }
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    int br, bc;
+    sm_pivot<N>(M, k, br, bc);
+    sm_swap_rows<N, N>(M, k, br);
+    sm_swap_rows<N, C>(X, k, br);
+    sm_swap_ix<N>(rp, k, br);
+    sm_swap_cols<N, N>(M, k, bc);
+    sm_swap_ix<N>(cp, k, bc);
+#pragma unroll
+    for (int i = k + 1; i < N; ++i) {
+      const double f = M[i][k] / M[k][k];
+#pragma unroll
+      for (int j = k + 1; j < N; ++j) M[i][j] -= f * M[k][j];
+#pragma unroll
+      for (int j = 0; j < C; ++j) X[i][j] -= f * X[k][j];
+    }
+  }
+#pragma unroll
+  for (int k = N - 1; k >= 0; --k) {
+    const double qk = M[k][k];
+#pragma unroll
+    for (int j = 0; j < C; ++j) X[k][j] /= qk;
+#pragma unroll
+    for (int i = 0; i < k; ++i) {
+      const double f = M[i][k];
+#pragma unroll
+      for (int j = 0; j < C; ++j) X[i][j] -= f * X[k][j];
+    }
+  }
+  // the reference's final reshuffle on the physical rows x(r) = X[l], rp[l] = r
+  double Y[N][C];
+  int irp[N];
+#pragma unroll
+  for (int r = 0; r < N; ++r) {
+#pragma unroll
+    for (int j = 0; j < C; ++j) Y[r][j] = 0.0;
+    irp[r] = 0;
+  }
+#pragma unroll
+  for (int l = 0; l < N; ++l)
+#pragma unroll
+    for (int r = 0; r < N; ++r)
+      if (rp[l] == r) {
+        irp[r] = l;
+#pragma unroll
+        for (int j = 0; j < C; ++j) Y[r][j] = X[l][j];
+      }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int a = cp[i], b = rp[i];
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      double ya = Y[0][j], yb = Y[0][j];
+#pragma unroll
+      for (int r = 1; r < N; ++r) { ya = a == r ? Y[r][j] : ya; yb = b == r ? Y[r][j] : yb; }
+      // x(a) = x(b), then x(b) = the old x(a) (a == b: unchanged)
+#pragma unroll
+      for (int r = 0; r < N; ++r) Y[r][j] = r == b ? ya : (r == a ? yb : Y[r][j]);
+    }
+    const int ia = sm_get(irp, a);
+    // rp[irp[cp[i]]] = rp[i]; irp[rp[i]] = irp[cp[i]]
+#pragma unroll
+    for (int t = 0; t < N; ++t) rp[t] = t == ia ? b : rp[t];
+#pragma unroll
+    for (int t = 0; t < N; ++t) irp[t] = t == b ? ia : irp[t];
+  }
+  Mat<N, C> out;
+#pragma unroll
+  for (int r = 0; r < N; ++r)
+#pragma unroll
+    for (int j = 0; j < C; ++j) out(r, j) = Y[r][j];
+  return out;
+}
+
+// operator! (MAT:603-671) for N <= 4; = inverse_ix below.  inv(rp[i], rp[j])
+// is held as I[i][j] while the rows are eliminated (a row swap of rp swaps
+// its rows and columns), inv(rp[i], j) as J[i][j] during back substitution.
+template <int N>
+LQRO_HD Mat<N, N> inverse_sm(const Mat<N, N>& q) {
+  double M[N][N], I[N][N];
+  int rp[N], cp[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    rp[i] = cp[i] = i;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      M[i][j] = q(i, j);
+      I[i][j] = i == j ? 1.0 : 0.0;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    int br, bc;
+    sm_pivot<N>(M, k, br, bc);
+    sm_swap_rows<N, N>(M, k, br);
+    sm_swap_rows<N, N>(I, k, br);
+    sm_swap_cols<N, N>(I, k, br);
+    sm_swap_ix<N>(rp, k, br);
+    sm_swap_cols<N, N>(M, k, bc);
+    sm_swap_ix<N>(cp, k, bc);
+#pragma unroll
+    for (int i = k + 1; i < N; ++i) {
+      const double f = M[i][k] / M[k][k];
+#pragma unroll
+      for (int j = k + 1; j < N; ++j) M[i][j] -= f * M[k][j];
+#pragma unroll
+      for (int j = 0; j < k; ++j) I[i][j] -= f * I[k][j];
+      I[i][k] = -f;
+    }
+  }
+  // J[i][c] = inv(rp[i], c) = I[i][l] with rp[l] = c
+  double J[N][N];
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int c = 0; c < N; ++c) {
+      double v = I[i][0];
+#pragma unroll
+      for (int l = 1; l < N; ++l) v = rp[l] == c ? I[i][l] : v;
+      J[i][c] = v;
+    }
+#pragma unroll
+  for (int k = N - 1; k >= 0; --k) {
+    const double qk = M[k][k];
+#pragma unroll
+    for (int j = 0; j < N; ++j) J[k][j] /= qk;
+#pragma unroll
+    for (int i = 0; i < k; ++i) {
+      const double f = M[i][k];
+#pragma unroll
+      for (int j = 0; j < N; ++j) J[i][j] -= f * J[k][j];
+    }
+  }
+  // m(cp[i], j) = inv(rp[i], j)
+  Mat<N, N> out;
+#pragma unroll
+  for (int r = 0; r < N; ++r)
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      double v = J[0][j];
+#pragma unroll
+      for (int i = 1; i < N; ++i) v = cp[i] == r ? J[i][j] : v;
+      out(r, j) = v;
+    }
+  return out;
+}
+
 // full-pivot Gauss-Jordan, pivot = first strict maximum in (row, col) scan order
 template <int N>
-LQRO_HD Mat<N, N> inverse(const Mat<N, N>& q) {
+LQRO_HD Mat<N, N> inverse_ix(const Mat<N, N>& q) {
   Mat<N, N> m = q, inv = eye<N>();
   int rp[N], cp[N];
   for (int i = 0; i < N; ++i) rp[i] = cp[i] = i;
@@ -132,7 +365,7 @@ LQRO_HD Mat<N, N> inverse(const Mat<N, N>& q) {
 
 // P X = Q by full-pivot elimination with the reference's final reshuffle
 template <int N, int C>
-LQRO_HD Mat<N, C> solve(const Mat<N, N>& p, const Mat<N, C>& q) {
+LQRO_HD Mat<N, C> solve_ix(const Mat<N, N>& p, const Mat<N, C>& q) {
   Mat<N, N> m = p;
   Mat<N, C> x = q;
   int rp[N], cp[N], irp[N];
@@ -172,6 +405,17 @@ LQRO_HD Mat<N, C> solve(const Mat<N, N>& p, const Mat<N, C>& q) {
     irp[rp[i]] = irp[cp[i]];
   }
   return x;
+}
+
+template <int N>
+LQRO_HD Mat<N, N> inverse(const Mat<N, N>& q) {
+  if constexpr (N <= 4) return inverse_sm<N>(q);
+  else return inverse_ix<N>(q);
+}
+template <int N, int C>
+LQRO_HD Mat<N, C> solve(const Mat<N, N>& p, const Mat<N, C>& q) {
+  if constexpr (N <= 4) return solve_sm<N, C>(p, q);
+  else return solve_ix<N, C>(p, q);
 }
 
 template <int N>

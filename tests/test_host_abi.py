@@ -158,3 +158,18 @@ def test_swarm_generator_is_stable(lqro_mod):
     assert np.all(np.abs(x[:, :3]) <= side / 2)
     x2, _ = lqro_mod.synthetic_swarm(4)
     assert np.array_equal(x, x2)
+
+
+def test_small_pivot_routines(tmp_path):
+    """lqro_synth.hpp's register-held pivoted routines (solve_sm, inverse_sm:
+    N <= 4, used by k_dynw's per-lane 3x3 work without private memory) equal
+    the indexed transcriptions of operator% / operator! (MAT:370-442,
+    603-671) bit for bit, ties and singular matrices included
+    (tests/cpp/small_pivot_check.cpp, host code)."""
+    import subprocess
+    exe = str(tmp_path / "spc")
+    src = os.path.join(ROOT, "tests", "cpp", "small_pivot_check.cpp")
+    subprocess.run(["/opt/rocm/bin/hipcc", "-std=c++17", "-O2", "-ffp-contract=off", "-fno-fast-math", "-x", "hip",
+                    "--offload-arch=gfx950", src, "-o", exe], check=True, capture_output=True, timeout=300)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
