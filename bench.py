@@ -281,6 +281,56 @@ def config_runs(lqro, torch, dev, local, world, rank, dist, steps, mode="block",
     return out
 
 
+CPP_BENCH = os.path.join(ROOT, "tests", "cpp", "lqro_bench_main")
+
+
+def cpp_host_run(lqro, x, vg, steps, warmup, world, rank, local, dist):
+    """The C++ multi-GPU host (include/lqro_sharded.hpp, lqro::ShardedSimulator)
+    on the same swarm: one child process per rank (tests/cpp/lqro_bench_main,
+    built by __graft_entry__.build), its own RCCL communicators, K iterations
+    of the reference's agent loop LQRO:1391-1446 — the pair loop (world > 1:
+    begin, row-normal all-gather, end), the dynamics and the all-gather of x —
+    timed between two barriers, max over ranks.  Returns rank 0's result (a
+    dict; {"error": ...} if the child failed)."""
+    import subprocess
+    import tempfile
+    N = x.shape[0]
+    token = [f"{os.getpid()}_{time.time_ns()}"]
+    if world > 1:
+        dist.broadcast_object_list(token, src=0)
+    tmp = tempfile.gettempdir()
+    uid = os.path.join(tmp, f"lqro_bench_uid_{token[0]}")
+    inp = os.path.join(tmp, f"lqro_bench_in_{token[0]}_{rank}.bin")
+    with open(inp, "wb") as f:
+        np.array([N, HORIZON, N_POINTS, steps], np.int32).tofile(f)
+        np.array([0x4C51524F], np.uint32).tofile(f)
+        for a in (x, vg, -x[:, :3]):
+            np.ascontiguousarray(a, np.float64).tofile(f)
+    try:
+        r = subprocess.run([CPP_BENCH, inp, uid, str(rank), str(world), str(local), str(warmup), str(steps)],
+                           capture_output=True, text=True, timeout=600)
+    except (OSError, subprocess.TimeoutExpired) as e:
+        return {"error": repr(e)[:300]}
+    finally:
+        os.remove(inp)
+    if world > 1:
+        dist.barrier()
+    if rank == 0 and os.path.exists(uid):
+        os.remove(uid)
+    if r.returncode != 0:
+        return {"error": f"rank {rank}: exit {r.returncode}: {r.stderr.strip()[-300:]}"}
+    if rank != 0:
+        return {}
+    kv = dict(t.split("=", 1) for t in r.stdout.split() if "=" in t)
+    el = float(kv["elapsed_s"])
+    return {"value": N * (N - 1) * steps / el, "ms_per_step": float(kv["ms_per_step"]), "steps": steps,
+            "warmup": warmup, "n_agents": N, "world": world,
+            "max_rank_inside_hull": int(float(kv["max_rank_inside"])),
+            "max_rank_hull_failures": int(float(kv["max_rank_hull_fail"])),
+            "host": "C++ lqro::ShardedSimulator (include/lqro_sharded.hpp), one process per GPU, RCCL",
+            "step": "pair loop + dynamics + x all-gather (LQRO:1391-1446), host-synchronised per iteration"}
+
+
 def canonical_rule_run(lqro, torch, dev, sh, gains, d_x, d_vg, d_newv, stream, steps, N, world, rank, mode):
     """The canonical hull rule (no LQRO_FLAG_QHULL_ORDER, k_lhull) on the
     timed steps' inputs, beside the headline: its step time, and the rows
@@ -324,6 +374,10 @@ def main():
                     help="row sharding over ranks: contiguous blocks or cyclic (row_stride = world)")
     ap.add_argument("--hull-rule", choices=("qhull", "canonical"), default=os.environ.get("LQRO_HULL_RULE", "qhull"),
                     help="inside-hull rule: the reference's (Qhull's build order, default) or the canonical one")
+    ap.add_argument("--host", choices=("python", "cpp"), default=os.environ.get("LQRO_BENCH_HOST", "python"),
+                    help="whose timed steps are `value`: the Python host (lqro.step_rows) or the C++ host "
+                         "(lqro::ShardedSimulator, a child process per rank); the other is reported beside it")
+    ap.add_argument("--no-host-cpp", action="store_true", help="skip the C++ host run (python host only)")
     args = ap.parse_args()
 
     import torch
@@ -412,6 +466,13 @@ def main():
         other = canonical_rule_run(lqro, torch, dev, sh, gains, d_x, d_vg, d_newv, stream, args.steps, N, world, rank,
                                    args.rows)
     closed = closed_loop(lqro, torch, dev, x, vg, gains, min(args.steps, 5), world, dist, rank, args.rows, flags)
+    host_cpp = None
+    if args.host == "cpp" or not args.no_host_cpp:
+        if args.rows != "block" or args.hull_rule != "qhull":
+            host_cpp = {"error": "the C++ host shards rows in blocks with the reference's hull rule"}
+        else:
+            host_cpp = cpp_host_run(lqro, x, vg, args.steps if args.host == "cpp" else min(args.steps, 5),
+                                    args.warmup if args.host == "cpp" else 1, world, rank, local, dist)
     pk_ms = sweep_ms
     probe = "sweep (k_prio + k_pair launches + overlapped side hull), timed steps"
     if not args.no_roofline_probe:
@@ -483,6 +544,15 @@ def main():
                       "(LQRO:925-968; k_qhull, LQRO_FLAG_QHULL_ORDER)" if args.hull_rule == "qhull" else
                       "canonical (a measured deviation from the reference's rule, DESIGN §5.2)"),
     }
+    if host_cpp is not None:
+        out["host_cpp"] = host_cpp
+        if args.host == "cpp":
+            if "value" not in host_cpp and rank == 0:
+                raise SystemExit(f"--host cpp: {host_cpp.get('error')}")
+            if rank == 0:
+                out["host_python"] = {"value": value, "ms_per_step": ms_step}
+                out["value"], out["ms_per_step"] = host_cpp["value"], host_cpp["ms_per_step"]
+                out["config"]["host"] = "cpp"
     if not args.no_configs:
         out["configs"] = config_runs(lqro, torch, dev, local, world, rank, dist, 2, args.rows, flags)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -128,6 +128,7 @@ class ShardedSimulator {
   ShardedSimulator& operator=(const ShardedSimulator&) = delete;
 
   int row_begin() const { return rb_; }
+  lqro_ctx* context() const { return ctx_; }   // null on a rank without rows
   int row_end() const { return re_; }
   // rank r's first row: floor(r n / world) (lqro.shard_rows' block mode)
   static int block_begin(int n, int r, int world) { return (int)(((long long)r * n) / world); }

@@ -13,6 +13,13 @@ namespace lqro {
 
 constexpr int kWave = 64;
 
+// A row's LP may run as soon as every one of its planes is final.  rowpend
+// (zeroed per step) adds LQRO_ROW_BIG for each finished row unit of the
+// sweep, +1 for each hot pair (k_prio) and each inside-hull pair the sweep
+// queues, -1 for each hot pair done without a hull and each hull job done:
+// it equals row_split * LQRO_ROW_BIG exactly when the row has nothing open.
+#define LQRO_ROW_BIG (1 << 20)
+
 // Workgroup-scope fence pair: orders this wave's LDS writes before other
 // lanes' later reads (LDS executes a wave's instructions in order; this keeps
 // the compiler from reordering and waits for lgkmcnt).

@@ -85,14 +85,15 @@ __device__ __forceinline__ void copy(const double* S, double* D, int lane) {
 
 // first strict maximum of |m| in (row, col) scan order over the trailing
 // (16-k)^2 block of the permuted matrix, as operator% / operator! pick it
+template <int N = 16>
 __device__ __forceinline__ void pivot(const double* m, const int* rp, const int* cp, int k, int lane,
                                       int& br, int& bc) {
-  const int w = 16 - k;
+  const int w = N - k;
   double best = 0.0;
   int bi = INT_MAX;
   for (int idx = lane; idx < w * w; idx += 64) {
     const int i = k + idx / w, j = k + idx % w;
-    const double a = fabs(m[rp[i] * 16 + cp[j]]);
+    const double a = fabs(m[rp[i] * N + cp[j]]);
     if (a > best) { best = a; bi = idx; }
   }
 #pragma unroll
@@ -221,13 +222,14 @@ __device__ __forceinline__ void expm(const double* q, double* out, double* w, in
   copy(cur, out, lane);
 }
 
-// jacobi (MAT:674-759, = dyn::jacobi<16>) of m: V, D in LDS
+// jacobi (MAT:674-759, = dyn::jacobi<N>) of m: V, D in LDS (row stride N);
+// the pivot scan in every lane, the rotation over lanes [0, N) (D) and
+// [N, 2N) (V)
+template <int N>
 __device__ void jacobi(const double* m, double* V, double* D, int lane) {
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int e = lane + 64 * t;
+  for (int e = lane; e < N * N; e += 64) {
     D[e] = m[e];
-    V[e] = ((e >> 4) == (e & 15)) ? 1.0 : 0.0;
+    V[e] = (e / N == e % N) ? 1.0 : 0.0;
   }
   sync();
   int pivot = 0, zeros = 0;
@@ -235,50 +237,93 @@ __device__ void jacobi(const double* m, double* V, double* D, int lane) {
     double maximum = 0;
     int p = 0, q = 0;
     for (int i = 0; i < pivot; ++i)
-      if (fabs(D[i * 16 + pivot]) > maximum) { maximum = fabs(D[i * 16 + pivot]); p = i; q = pivot; }
-    for (int j = pivot + 1; j < 16; ++j)
-      if (fabs(D[pivot * 16 + j]) > maximum) { maximum = fabs(D[pivot * 16 + j]); p = pivot; q = j; }
-    pivot = (pivot + 1) % 16;
+      if (fabs(D[i * N + pivot]) > maximum) { maximum = fabs(D[i * N + pivot]); p = i; q = pivot; }
+    for (int j = pivot + 1; j < N; ++j)
+      if (fabs(D[pivot * N + j]) > maximum) { maximum = fabs(D[pivot * N + j]); p = pivot; q = j; }
+    pivot = (pivot + 1) % N;
     if (maximum <= DBL_EPSILON) {
-      if (++zeros == 16) break;
+      if (++zeros == N) break;
       continue;
     }
     zeros = 0;
-    const double theta = 0.5 * (D[q * 16 + q] - D[p * 16 + p]) / D[p * 16 + q];
+    const double theta = 0.5 * (D[q * N + q] - D[p * N + p]) / D[p * N + q];
     double t = 1 / (fabs(theta) + hypot(theta, 1.0));
     if (theta < 0) t = -t;
     const double c = 1 / hypot(t, 1.0);
     const double s = c * t;
     const double tau = s / (1 + c);
     sync();   // every lane has read D for the scan
-    if (lane < 16 && lane != p && lane != q) {
+    if (lane < N && lane != p && lane != q) {
       const int r = lane;
       int ia, ib;   // the two entries row/col r of the rotation touches
-      if (r < p) { ia = r * 16 + p; ib = r * 16 + q; }
-      else if (r < q) { ia = p * 16 + r; ib = r * 16 + q; }
-      else { ia = p * 16 + r; ib = q * 16 + r; }
+      if (r < p) { ia = r * N + p; ib = r * N + q; }
+      else if (r < q) { ia = p * N + r; ib = r * N + q; }
+      else { ia = p * N + r; ib = q * N + r; }
       const double a = D[ia], b = D[ib];
       D[ia] -= s * (b + tau * a);
       D[ib] += s * (a - tau * b);
     }
-    if (lane >= 16 && lane < 32) {
-      const int r = lane - 16;
-      const double a = V[r * 16 + p], b = V[r * 16 + q];
-      V[r * 16 + p] -= s * (b + tau * a);
-      V[r * 16 + q] += s * (a - tau * b);
+    if (lane >= N && lane < 2 * N) {
+      const int r = lane - N;
+      const double a = V[r * N + p], b = V[r * N + q];
+      V[r * N + p] -= s * (b + tau * a);
+      V[r * N + q] += s * (a - tau * b);
     }
     sync();
     if (lane == 0) {
-      D[p * 16 + p] -= t * D[p * 16 + q];
-      D[q * 16 + q] += t * D[p * 16 + q];
-      D[p * 16 + q] = 0;
+      D[p * N + p] -= t * D[p * N + q];
+      D[q * N + q] += t * D[p * N + q];
+      D[p * N + q] = 0;
     }
     sync();
   }
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int e = lane + 64 * t, i = e >> 4, j = e & 15;
-    if (i != j) D[e] = 0;
+  for (int e = lane; e < N * N; e += 64)
+    if (e / N != e % N) D[e] = 0;
+  sync();
+}
+
+// operator! (MAT:603-671, = synth::inverse_ix<N>) of m in LDS, over the
+// lanes: full-pivot Gauss-Jordan, the same pivots and per-element operation
+// order; m is overwritten with the inverse, inv is work space
+template <int N>
+__device__ void inverse(double* m, double* inv, int* ip, int lane) {
+  int* rp = ip;
+  int* cp = ip + N;
+  for (int e = lane; e < N * N; e += 64) inv[e] = (e / N == e % N) ? 1.0 : 0.0;
+  if (lane < N) { rp[lane] = lane; cp[lane] = lane; }
+  sync();
+  for (int k = 0; k < N; ++k) {
+    int br, bc;
+    pivot<N>(m, rp, cp, k, lane, br, bc);
+    const int rk = rp[br], ck = cp[bc], rb = rp[k], cb = cp[k];
+    sync();
+    if (lane == 0) { rp[k] = rk; rp[br] = rb; cp[k] = ck; cp[bc] = cb; }
+    sync();
+    // rows i > k against row k: m's columns after k, inv's columns rp[j < k], inv(rp i, rp k) = -f
+    const double piv = m[rp[k] * N + cp[k]];
+    for (int idx = lane; idx < (N - 1 - k) * N; idx += 64) {
+      const int i = k + 1 + idx / N, c = idx % N;
+      const double f = m[rp[i] * N + cp[k]] / piv;
+      if (c > k) m[rp[i] * N + cp[c]] -= f * m[rp[k] * N + cp[c]];
+      else if (c < k) inv[rp[i] * N + rp[c]] -= f * inv[rp[k] * N + rp[c]];
+      else inv[rp[i] * N + rp[k]] = -f;
+    }
+    sync();
+  }
+  for (int k = N - 1; k >= 0; --k) {
+    const double qk = m[rp[k] * N + cp[k]];
+    if (lane < N) inv[rp[k] * N + lane] /= qk;
+    sync();
+    for (int idx = lane; idx < k * N; idx += 64) {
+      const int i = idx / N, j = idx % N;
+      const double f = m[rp[i] * N + cp[k]];
+      inv[rp[i] * N + j] -= f * inv[rp[k] * N + j];
+    }
+    sync();
+  }
+  for (int idx = lane; idx < N * N; idx += 64) {
+    const int i = idx / N, j = idx % N;
+    m[cp[i] * N + j] = inv[rp[i] * N + j];
   }
   sync();
 }
@@ -350,7 +395,7 @@ __device__ void discretize(const Quad& q, const Mat<kX, 1>& x, const Mat<3, 3>& 
 __device__ Mat<kX, 1> noise(double* w, const double* nrm, int lane) {
   double* V = w + oT1;
   double* D = w + oT2;
-  jacobi(w + oMM, V, D, lane);
+  jacobi<16>(w + oMM, V, D, lane);
   if (lane < 16) D[lane * 17] = sqrt(D[lane * 17]);
   sync();
   mm(V, D, w + oE0, lane);
@@ -362,7 +407,7 @@ __device__ Mat<kX, 1> noise(double* w, const double* nrm, int lane) {
 
 // kalmanFilter2 (LQRO:507-518) with P in LDS
 __device__ void kalman_update(const Quad& q, Mat<kX, 1>& x, Mat<3, 3>& R, const Mat<kZ, 1>& z,
-                              const Mat<kZ, kZ>& Nz, double* w, int lane) {
+                              const double* Nz, double* w, int lane) {
   double* P = w + oP;
   double* H = w + oE0;          // 6x16
   double* PHt = w + oE0 + 96;   // 16x6
@@ -371,14 +416,20 @@ __device__ void kalman_update(const Quad& q, Mat<kX, 1>& x, Mat<3, 3>& R, const 
   double* K = w + oE1 + 128;    // 16x6
   double* KH = w + oE2;         // 16x16
   double* T1 = w + oT1;
-  const int obs[6] = {9, 10, 11, 0, 1, 2};
-  // Jacobian_hx (LQRO:443-452)
+  // x through LDS: the lanes index it by their element (no private array)
+  double* xs = w + oE2 + 240;
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < kX; ++k) xs[k] = x.e[k];
+  sync();
+  // Jacobian_hx (LQRO:443-452): row k observes x[9 + k] (k < 3) or x[k - 3]
   for (int e = lane; e < 96; e += 64) {
     const int k = e >> 4, i = e & 15;
-    const double xv = x.e[i];
-    const bool hit = obs[k] == i;
-    const double hr = hit ? xv + q.h : x.e[obs[k]];
-    const double hl = hit ? xv - q.h : x.e[obs[k]];
+    const int ok = k < 3 ? 9 + k : k - 3;
+    const double xv = xs[i];
+    const bool hit = ok == i;
+    const double hr = hit ? xv + q.h : xs[ok];
+    const double hl = hit ? xv - q.h : xs[ok];
     H[e] = (hr - hl) / (2 * q.h);
   }
   sync();
@@ -401,29 +452,16 @@ __device__ void kalman_update(const Quad& q, Mat<kX, 1>& x, Mat<3, 3>& R, const 
     const int i = lane / 6, j = lane % 6;
     double acc = 0.0;
     for (int k = 0; k < 16; ++k) acc += HP[i * 16 + k] * H[j * 16 + k];
-    S[lane] = acc + Nz.e[lane];
+    S[lane] = acc + Nz[lane];
   }
   sync();
-  // S^-1 (the pseudo-inverse of synth::inverse: data-dependent indexing, so
-  // private memory): one lane computes it, LDS hands it to the others
-  double* Sinv = w + oE1 + 224;   // 6x6
-  if (lane == 0) {
-    Mat<kZ, kZ> Sm;
-#pragma unroll
-    for (int k = 0; k < 36; ++k) Sm.e[k] = S[k];
-    const Mat<kZ, kZ> Si0 = synth::inverse(Sm);
-#pragma unroll
-    for (int k = 0; k < 36; ++k) Sinv[k] = Si0.e[k];
-  }
-  sync();
-  Mat<kZ, kZ> Si;
-#pragma unroll
-  for (int k = 0; k < 36; ++k) Si.e[k] = Sinv[k];
+  // S^-1 (synth::inverse) over the lanes, in place
+  inverse<kZ>(S, w + oE1 + 224, reinterpret_cast<int*>(w + oInt), lane);
   for (int e = lane; e < 96; e += 64) {   // K = P H^T S^-1
     const int i = e / 6, j = e % 6;
     double acc = 0.0;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) acc += PHt[i * 6 + k] * Si.e[k * 6 + j];
+    for (int k = 0; k < 6; ++k) acc += PHt[i * 6 + k] * S[k * 6 + j];
     K[e] = acc;
   }
   sync();
@@ -466,7 +504,6 @@ __device__ void agent_step(const dyn::AgentParams& a, double* x_, double* rot_, 
   sync();
   Mat<kX, 1> x = get<kX, 1>(x_), xtrue = get<kX, 1>(xt_);
   Mat<3, 3> R = get<3, 3>(rot_), Rtrue = get<3, 3>(rott_);
-  const Mat<kZ, kZ> Nz = get<kZ, kZ>(a.Nz);
   const Mat<kU, 1> ug = get<kU, 1>(a.u_goal);
   const Mat<kU, 1> u = dyn::control_velocity(x, R, get<3, 1>(vgoal_), ug, get<kU, kX>(a.L),
                                              get<kU, kV>(a.E), get<kU, 1>(a.l));        // findU
@@ -489,21 +526,44 @@ __device__ void agent_step(const dyn::AgentParams& a, double* x_, double* rot_, 
     sync();
     dyn::reset_rot(x, R);
   }
-  // the observation draw (6x6 Jacobi: data-dependent indexing) on one lane
+  // the observation draw: sampleGaussian(h(xTrue), N) (simulator2.h:21-32,
+  // = dyn::sample_gaussian<6>) over the lanes
   Mat<kZ, 1> z;
   {
-    double* zb = w + oT1;
-    if (lane == 0) {
-      const Mat<kZ, 1> z0 = dyn::sample_gaussian(dyn::observe(xtrue), Nz, a.normals + kX);
+    double* Nm = w + oT1;          // 6x6
+    double* V = w + oT1 + 64;
+    double* D = w + oT1 + 128;
+    double* VD = w + oT1 + 192;
+    double* zb = w + oT2;
+    const Mat<kZ, 1> mean = dyn::observe(xtrue);
+    if (lane < kZ * kZ) Nm[lane] = a.Nz[lane];
+    if (lane == 0)
 #pragma unroll
-      for (int k = 0; k < kZ; ++k) zb[k] = z0.e[k];
+      for (int k = 0; k < kZ; ++k) zb[8 + k] = mean.e[k];
+    sync();
+    jacobi<kZ>(Nm, V, D, lane);
+    if (lane < kZ) D[lane * (kZ + 1)] = sqrt(D[lane * (kZ + 1)]);
+    sync();
+    if (lane < kZ * kZ) {   // V D
+      const int i = lane / kZ, j = lane % kZ;
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < kZ; ++k) acc += V[i * kZ + k] * D[k * kZ + j];
+      VD[lane] = acc;
+    }
+    sync();
+    if (lane < kZ) {        // (V D) smp + mean
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < kZ; ++k) acc += VD[lane * kZ + k] * a.normals[kX + k];
+      zb[lane] = acc + zb[8 + lane];
     }
     sync();
 #pragma unroll
     for (int k = 0; k < kZ; ++k) z.e[k] = zb[k];
     sync();
   }
-  kalman_update(q, x, R, z, Nz, w, lane);                                             // kalmanFilter2
+  kalman_update(q, x, R, z, a.Nz, w, lane);                                           // kalmanFilter2
   const Vec3 vn = dyn::control_position(x, R, get<3, 1>(a.p_goal), ug, get<kV, kX>(a.Lh),
                                         get<kV, kV>(a.Eh));                           // findVGoal
 #pragma unroll

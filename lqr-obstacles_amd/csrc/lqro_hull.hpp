@@ -120,7 +120,35 @@ struct HullArgs {
   int* qstale;
   int* qstale_count;
   int qstale_cap;
+  // early LP (lqro_runtime.hip, LQRO_ROW_BIG): rowpend counts each row's
+  // open work down, rowclaim says who runs its LP (0 free, 1 claimed, 2 late:
+  // a facet-0 pair waits for k_stale); the k_qhull job that completes a row
+  // runs calculateNewV for it (lp_vgoal -> lp_newv).  Null: off.
+  int* rowpend;
+  int* rowclaim;
+  int row_target;
+  const double* lp_vgoal;
+  double* lp_newv;
+  double lp_vmax;
 };
+
+// (LQRO_ROW_BIG, lqro_device.hpp: the row counter's protocol; the early LP
+// runs in k_qhull's facet-plane LDS: rows of at most LQRO_EARLY_LP_MAX_NPR
+// pairs, planes and projections 32 B each)
+#define LQRO_EARLY_LP_MAX_NPR 1152
+// lane 0, after the job's plane (or its pending / failed flag) is written:
+// count the row down; true when this job closed the row and claimed its LP
+// (can_run: the caller will run it)
+__device__ inline bool hull_row_done(const HullArgs& A, int slot, bool stale, bool can_run) {
+  if (!A.rowpend) return false;
+  const int lrow = slot / A.npr;
+  if (stale) atomicExch(&A.rowclaim[lrow], 2);
+  __threadfence();
+  const int old = atomicSub(&A.rowpend[lrow], 1);
+  const bool go = can_run && old - 1 == A.row_target && atomicCAS(&A.rowclaim[lrow], 0, 1) == 0;
+  __threadfence();
+  return go;
+}
 
 // Hull topology and vertex coordinates for k_hull_big (global scratch).
 template <int FMAX, int VTX, class SEG>

@@ -12,6 +12,20 @@
 //     failing plane or after the loop gives the same answer because tLeft
 //     only grows and tRight only shrinks.
 // So the result is bit-identical to the sequential fp32 LP.
+//
+// The LP is one long dependent chain (C3's hardest rows: ~1,500 violated
+// planes and linearProgram1 calls in sequence, almost all over fewer than
+// 64 planes), so the code is written for latency, not throughput:
+//   * each scan keeps its current 64-plane chunk in registers (one plane a
+//     lane, the next chunk's loads already issued); a violated plane is
+//     broadcast with readlane, and linearProgram1 over planes of that chunk
+//     reads the same registers — no LDS round trip per violation;
+//   * linearProgram2's line for plane i (direction, point: they depend on
+//     planes i and planeNo only, not on the current result) is computed for
+//     the whole chunk at its first violation, once per chunk, and each
+//     later violation in the chunk reads its lane's line;
+//   * linearProgram1's max/min reductions are DPP lane moves and four
+//     readlanes (uniform result), not ds_bpermute shuffles.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -72,26 +86,77 @@ __device__ __forceinline__ void st_plane(float* base, int i, v3 pt, v3 nm) {
   }
 }
 
-// first plane index in [i0, n) with normal.(point - r) > thresh, or n
+// orcaPlanes_ in push order (j order, LQRObstacles.cpp:1220): a row's plane
+// slots (k_pair's 32-B records, [6] = 1 for a plane) compacted into `planes`
+// (stride PS); returns their count
 template <int PS>
-__device__ __forceinline__ int first_violated(const float* planes, int i0, int n, v3 r, float thresh,
-                                              int lane) {
-  for (int base = i0; base < n; base += 64) {
-    const int i = base + lane;
-    bool v = false;
-    if (i < n) {
-      LPPlane p = ld_plane<PS>(planes, i);
-      v = vdot(p.normal, vsub(p.point, r)) > thresh;
+__device__ __forceinline__ int lp_compact(const float* src, int npr, float* planes, int lane) {
+  int m = 0;
+  for (int base = 0; base < npr; base += 64) {
+    const int sidx = base + lane;
+    float4 a = make_float4(0, 0, 0, 0), b = make_float4(0, 0, 0, 0);
+    bool f = false;
+    if (sidx < npr) {
+      const float4* p = reinterpret_cast<const float4*>(src + 8 * (size_t)sidx);
+      a = p[0];
+      b = p[1];
+      f = __float_as_int(b.z) == 1;
     }
-    unsigned long long b = __ballot(v);
-    if (b) return base + __ffsll((long long)b) - 1;
+    const unsigned long long bal = __ballot(f);
+    if (f)
+      st_plane<PS>(planes, m + __popcll(bal & ((1ull << lane) - 1ull)), V3(a.x, a.y, a.z), V3(a.w, b.x, b.y));
+    m += __popcll(bal);
   }
-  return n;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  return m;
 }
 
+// lane k's value of x (k uniform): the result is wave-uniform
+__device__ __forceinline__ float lp_rl(float x, int k) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), k));
+}
+__device__ __forceinline__ v3 lp_rl3(v3 a, int k) { return V3(lp_rl(a.x, k), lp_rl(a.y, k), lp_rl(a.z, k)); }
+template <int CTRL>
+__device__ __forceinline__ float lp_dpp(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+// max / min over the 64 lanes with stdmax / stdmin (all lanes active): xor 1,
+// xor 2 (quad_perm), half-row and row mirrors, then the four rows' values
+__device__ __forceinline__ float lp_wave_max(float v) {
+  v = stdmax(v, lp_dpp<0xB1>(v));
+  v = stdmax(v, lp_dpp<0x4E>(v));
+  v = stdmax(v, lp_dpp<0x141>(v));
+  v = stdmax(v, lp_dpp<0x140>(v));
+  return stdmax(stdmax(lp_rl(v, 0), lp_rl(v, 16)), stdmax(lp_rl(v, 32), lp_rl(v, 48)));
+}
+__device__ __forceinline__ float lp_wave_min(float v) {
+  v = stdmin(v, lp_dpp<0xB1>(v));
+  v = stdmin(v, lp_dpp<0x4E>(v));
+  v = stdmin(v, lp_dpp<0x141>(v));
+  v = stdmin(v, lp_dpp<0x140>(v));
+  return stdmin(stdmin(lp_rl(v, 0), lp_rl(v, 16)), stdmin(lp_rl(v, 32), lp_rl(v, 48)));
+}
 template <int PS>
-__device__ __forceinline__ bool w_lp1(const float* planes, int planeNo, v3 lpt, v3 ldir, float radius, v3 opt,
-                      bool dirOpt, v3& result, int lane) {
+__device__ __forceinline__ LPPlane ld_plane_if(const float* base, int i, int n) {
+  if (i < n) return ld_plane<PS>(base, i);
+  LPPlane z;
+  z.point = V3(0, 0, 0);
+  z.normal = V3(0, 0, 0);
+  return z;
+}
+// normal.(point - r) > thresh: plane violated by r (LQRO:1083, 1138, 1170)
+__device__ __forceinline__ bool lp_violates(const LPPlane& p, v3 r, float thresh) {
+  return vdot(p.normal, vsub(p.point, r)) > thresh;
+}
+
+// linearProgram1 (LQRO:1001-1046) on planes [0, planeNo) and the line (lpt,
+// ldir); the planes of chunk cb (64-aligned, planeNo <= cb + 64) are the
+// lanes' registers pc
+template <int PS>
+__device__ __forceinline__ bool w_lp1(const float* planes, int planeNo, int cb, const LPPlane& pc, v3 lpt,
+                                      v3 ldir, float radius, v3 opt, bool dirOpt, v3& result, int lane) {
   const float dotProduct = vdot(lpt, ldir);
   const float disc = sqrf(dotProduct) + sqrf(radius) - vdot(lpt, lpt);
   if (disc < 0.0f) return false;
@@ -100,26 +165,24 @@ __device__ __forceinline__ bool w_lp1(const float* planes, int planeNo, v3 lpt, 
   float tRight = -dotProduct + sq;
   float lmax = -INFINITY, lmin = INFINITY;
   bool reject = false;
-  for (int i = lane; i < planeNo; i += 64) {
-    LPPlane pi = ld_plane<PS>(planes, i);
-    const float numerator = vdot(vsub(pi.point, lpt), pi.normal);
-    const float denominator = vdot(ldir, pi.normal);
-    if (sqrf(denominator) <= kRvoEps) {
-      if (numerator > 0.0f) reject = true;
-      continue;
+  for (int base = 0; base < planeNo; base += 64) {
+    const int i = base + lane;
+    const LPPlane pi = base == cb ? pc : ld_plane_if<PS>(planes, i, planeNo);
+    if (i < planeNo) {
+      const float numerator = vdot(vsub(pi.point, lpt), pi.normal);
+      const float denominator = vdot(ldir, pi.normal);
+      if (sqrf(denominator) <= kRvoEps) {
+        if (numerator > 0.0f) reject = true;
+      } else {
+        const float t = numerator / denominator;
+        if (denominator >= 0.0f) lmax = stdmax(lmax, t);
+        else lmin = stdmin(lmin, t);
+      }
     }
-    const float t = numerator / denominator;
-    if (denominator >= 0.0f) lmax = stdmax(lmax, t);
-    else lmin = stdmin(lmin, t);
   }
   if (__ballot(reject)) return false;
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    lmax = stdmax(lmax, __shfl_xor(lmax, off));
-    lmin = stdmin(lmin, __shfl_xor(lmin, off));
-  }
-  tLeft = stdmax(tLeft, lmax);
-  tRight = stdmin(tRight, lmin);
+  tLeft = stdmax(tLeft, lp_wave_max(lmax));
+  tRight = stdmin(tRight, lp_wave_min(lmin));
   if (tLeft > tRight) return false;
   if (dirOpt) {
     if (vdot(opt, ldir) > 0.0f) result = vadd(lpt, smul(tRight, ldir));
@@ -133,10 +196,11 @@ __device__ __forceinline__ bool w_lp1(const float* planes, int planeNo, v3 lpt, 
   return true;
 }
 
+// linearProgram2 (LQRO:1048-1104) for plane planeNo = pn; the planes of chunk
+// ob (64-aligned) are the caller's registers po
 template <int PS>
-__device__ __forceinline__ bool w_lp2(const float* planes, int planeNo, float radius, v3 opt, bool dirOpt,
-                      v3& result, int lane) {
-  const LPPlane pn = ld_plane<PS>(planes, planeNo);
+__device__ __forceinline__ bool w_lp2(const float* planes, int planeNo, const LPPlane& pn, int ob,
+                                      const LPPlane& po, float radius, v3 opt, bool dirOpt, v3& result, int lane) {
   const float planeDist = vdot(pn.point, pn.normal);
   const float planeDistSq = sqrf(planeDist);
   const float radiusSq = sqrf(radius);
@@ -156,38 +220,66 @@ __device__ __forceinline__ bool w_lp2(const float* planes, int planeNo, float ra
       result = vadd(planeCenter, smul(sqrtf(planeRadiusSq / prSq), pr));
     }
   }
-  for (int i = first_violated<PS>(planes, 0, planeNo, result, 0.0f, lane); i < planeNo;
-       i = first_violated<PS>(planes, i + 1, planeNo, result, 0.0f, lane)) {
-    const LPPlane pi = ld_plane<PS>(planes, i);
-    v3 cp = vcross(pi.normal, pn.normal);
-    if (vdot(cp, cp) <= kRvoEps) return false;
+  LPPlane nx = planeNo > 0 ? (ob == 0 ? po : ld_plane_if<PS>(planes, lane, planeNo)) : po;
+  for (int base = 0; base < planeNo; base += 64) {
+    const LPPlane pj = nx;
+    if (base + 64 < planeNo) nx = base + 64 == ob ? po : ld_plane_if<PS>(planes, base + 64 + lane, planeNo);
+    const bool inr = base + lane < planeNo;
+    unsigned long long b = __ballot(inr && lp_violates(pj, result, 0.0f));
+    if (!b) continue;
+    // the chunk's lines (LQRO:1086-1097), once, at its first violated plane
+    const v3 cp = vcross(pj.normal, pn.normal);
+    const unsigned long long parb = __ballot(vdot(cp, cp) <= kRvoEps);
     const v3 ldir = vnormalize(cp);
     const v3 lineNormal = vcross(ldir, pn.normal);
-    const v3 lpt = vadd(pn.point, smul(vdot(vsub(pi.point, pn.point), pi.normal) /
-                                           vdot(lineNormal, pi.normal),
+    const v3 lpt = vadd(pn.point, smul(vdot(vsub(pj.point, pn.point), pj.normal) / vdot(lineNormal, pj.normal),
                                        lineNormal));
-    if (!w_lp1<PS>(planes, i, lpt, ldir, radius, opt, dirOpt, result, lane)) return false;
+    for (;;) {
+      const int k = __ffsll((long long)b) - 1;
+      if ((parb >> k) & 1ull) return false;
+      if (!w_lp1<PS>(planes, base + k, base, pj, lp_rl3(lpt, k), lp_rl3(ldir, k), radius, opt, dirOpt, result,
+                     lane))
+        return false;
+      b = __ballot(inr && lane > k && lp_violates(pj, result, 0.0f));
+      if (!b) break;
+    }
   }
   return true;
 }
 
+// linearProgram3 (LQRO:1106-1129): the index of the plane it fails on, or m
 template <int PS>
 __device__ __forceinline__ int w_lp3(const float* planes, int m, double radius, v3 opt, bool dirOpt, v3& result,
-                     int lane) {
+                                     int lane) {
   const float rf = (float)radius;
   if (dirOpt) result = vmul(opt, rf);
   else if (vdot(opt, opt) > sqrf(rf)) result = vmul(vnormalize(opt), rf);
   else result = opt;
-  for (int i = first_violated<PS>(planes, 0, m, result, 0.0f, lane); i < m;
-       i = first_violated<PS>(planes, i + 1, m, result, 0.0f, lane)) {
-    const v3 tmp = result;
-    if (!w_lp2<PS>(planes, i, rf, opt, dirOpt, result, lane)) { result = tmp; return i; }
+  LPPlane nx = ld_plane_if<PS>(planes, lane, m);
+  for (int base = 0; base < m; base += 64) {
+    const LPPlane pj = nx;
+    if (base + 64 < m) nx = ld_plane_if<PS>(planes, base + 64 + lane, m);
+    const bool inr = base + lane < m;
+    unsigned long long b = __ballot(inr && lp_violates(pj, result, 0.0f));
+    while (b) {
+      const int k = __ffsll((long long)b) - 1;
+      LPPlane pn;
+      pn.point = lp_rl3(pj.point, k);
+      pn.normal = lp_rl3(pj.normal, k);
+      const v3 tmp = result;
+      if (!w_lp2<PS>(planes, base + k, pn, base, pj, rf, opt, dirOpt, result, lane)) {
+        result = tmp;
+        return base + k;
+      }
+      b = __ballot(inr && lane > k && lp_violates(pj, result, 0.0f));
+    }
   }
   return m;
 }
 
-// linearProgram4: the projected planes of plane i are built in parallel and
-// compacted in j order (skipped same-direction parallels keep their order).
+// linearProgram4 (LQRO:1131-1206): the projected planes of plane i are built
+// in parallel and compacted in j order (skipped same-direction parallels keep
+// their order)
 template <int PS>
 __device__ __forceinline__ void w_lp4(const float* planes, int m, int beginPlane, float radius, v3& result,
                       float* proj, int lane
@@ -196,42 +288,51 @@ __device__ __forceinline__ void w_lp4(const float* planes, int m, int beginPlane
 #endif
                       ) {
   float distance = 0.0f;
-  for (int i = first_violated<PS>(planes, beginPlane, m, result, distance, lane); i < m;
-       i = first_violated<PS>(planes, i + 1, m, result, distance, lane)) {
-    const LPPlane pi = ld_plane<PS>(planes, i);
-    int np = 0;
-    for (int base = 0; base < i; base += 64) {
-      const int j = base + lane;
-      bool keep = false;
-      v3 ppt = V3(0, 0, 0), pnm = V3(0, 0, 0);
-      if (j < i) {
-        const LPPlane pj = ld_plane<PS>(planes, j);
-        const v3 cp = vcross(pj.normal, pi.normal);
-        keep = true;
-        if (vdot(cp, cp) <= kRvoEps) {
-          if (vdot(pi.normal, pj.normal) > 0.0f) keep = false;
-          else ppt = smul(0.5f, vadd(pi.point, pj.point));
-        } else {
-          const v3 lineNormal = vcross(cp, pi.normal);
-          ppt = vadd(pi.point, smul(vdot(vsub(pj.point, pi.point), pj.normal) /
-                                        vdot(lineNormal, pj.normal),
-                                    lineNormal));
+  for (int base = beginPlane; base < m; base += 64) {
+    const LPPlane pc = ld_plane_if<PS>(planes, base + lane, m);
+    const bool inr = base + lane < m;
+    unsigned long long b = __ballot(inr && lp_violates(pc, result, distance));
+    while (b) {
+      const int k = __ffsll((long long)b) - 1;
+      const int i = base + k;
+      LPPlane pi;
+      pi.point = lp_rl3(pc.point, k);
+      pi.normal = lp_rl3(pc.normal, k);
+      int np = 0;
+      for (int jb = 0; jb < i; jb += 64) {
+        const int j = jb + lane;
+        bool keep = false;
+        v3 ppt = V3(0, 0, 0), pnm = V3(0, 0, 0);
+        if (j < i) {
+          const LPPlane pj = ld_plane<PS>(planes, j);
+          const v3 cp = vcross(pj.normal, pi.normal);
+          keep = true;
+          if (vdot(cp, cp) <= kRvoEps) {
+            if (vdot(pi.normal, pj.normal) > 0.0f) keep = false;
+            else ppt = smul(0.5f, vadd(pi.point, pj.point));
+          } else {
+            const v3 lineNormal = vcross(cp, pi.normal);
+            ppt = vadd(pi.point, smul(vdot(vsub(pj.point, pi.point), pj.normal) /
+                                          vdot(lineNormal, pj.normal),
+                                      lineNormal));
+          }
+          if (keep) pnm = vnormalize(vsub(pj.normal, pi.normal));
         }
-        if (keep) pnm = vnormalize(vsub(pj.normal, pi.normal));
+        const unsigned long long kb = __ballot(keep);
+        if (keep) st_plane<PS>(proj, np + __popcll(kb & ((1ull << lane) - 1ull)), ppt, pnm);
+        np += __popcll(kb);
       }
-      const unsigned long long b = __ballot(keep);
-      if (keep) st_plane<PS>(proj, np + __popcll(b & ((1ull << lane) - 1ull)), ppt, pnm);
-      np += __popcll(b);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    const v3 tmp = result;
-    if (w_lp3<PS>(proj, np, radius, pi.normal, true, result, lane) < np) result = tmp;
-    distance = vdot(pi.normal, vsub(pi.point, result));
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      const v3 tmp = result;
+      if (w_lp3<PS>(proj, np, radius, pi.normal, true, result, lane) < np) result = tmp;
+      distance = vdot(pi.normal, vsub(pi.point, result));
 #ifdef LQRO_LP_PROFILE
-    ++lp4_iters;
+      ++lp4_iters;
 #endif
+      b = __ballot(inr && lane > k && lp_violates(pc, result, distance));
+    }
   }
 }
 

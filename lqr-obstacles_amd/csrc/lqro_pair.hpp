@@ -75,6 +75,7 @@ struct PairArgs {
   int hot_only;                       // 1: this launch computes the hot list only
   const int* nbr_list;                // culling on: per row npr (= K) neighbour jj, ascending, -1 = none
   double* qnrm;                       // LQRO_FLAG_QHULL_ORDER: per slot normal, dist (k_stale reads them)
+  int* rowpend;                       // early LP: per row open work (LQRO_ROW_BIG), null: off
   // LDS layout, in doubles
   int XP, lds_T, lds_N, lds_S, lds_R, lds_TF, lds_H, lds_wave, wave_doubles;
 };
@@ -707,6 +708,15 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
         lds_count(&W.st[inside ? 3 : 2], 1ull);
         if (go.backup) lds_count(&W.st[4], 1ull);
       }
+      if constexpr (HOT != kRowLaunch) {
+        // a hot pair (counted by k_prio) is done unless its hull is open
+        if (P.rowpend && !inside) {
+          __threadfence();
+          atomicSub(&P.rowpend[lrow], 1);
+        }
+      } else {
+        if (P.rowpend && inside) atomicAdd(&P.rowpend[lrow], 1);   // before its job is visible
+      }
       if (inside) {
         // published with release: k_hull workers may already be polling
         const int qi = atomicAdd(P.hull_count, 1);
@@ -823,6 +833,12 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
     if (P.hot_mark != nullptr && P.hot_mark[(size_t)lrow * P.npr + jj]) continue;   // done in the hot phase
     do_pair(i, lrow, jj);
   }
+    if (P.rowpend) {
+      // the unit's planes are written: release them, then count the unit
+      __threadfence();
+      __syncthreads();
+      if (threadIdx.x == 0) atomicAdd(&P.rowpend[lrow], LQRO_ROW_BIG);
+    }
     __syncthreads();   // the row is done before s_row / the tables change
   }
   }   // row launch
@@ -967,6 +983,7 @@ struct PrioArgs {
   unsigned char* mark;
   int* count;
   int cap;
+  int* rowpend;   // early LP: +1 per listed pair (null: off)
 };
 
 __global__ void __launch_bounds__(256) k_prio(PrioArgs A) {
@@ -993,7 +1010,10 @@ __global__ void __launch_bounds__(256) k_prio(PrioArgs A) {
     if (lane == 0 && b) pos = atomicAdd(A.count, __popcll(b));
     pos = __shfl(pos, 0) + __popcll(b & ((1ull << lane) - 1ull));
     if (hot && pos >= A.cap) hot = false;
-    if (hot) A.list[pos] = (int)slot;
+    if (hot) {
+      A.list[pos] = (int)slot;
+      if (A.rowpend) atomicAdd(&A.rowpend[slot / A.npr], 1);
+    }
     if (slot < total) A.mark[slot] = hot ? 1 : 0;
   }
 }

@@ -1314,6 +1314,7 @@ __device__ inline void qh_select(const HullArgs& A, const QhW& W, const QhS& S, 
         }
       }
     }
+    hull_row_done(A, slot, stale, false);   // k_qhull_big leaves the LP to the tail
   }
   hl_sync();
 }

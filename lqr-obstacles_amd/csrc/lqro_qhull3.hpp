@@ -30,6 +30,7 @@
 //    as soon as its result is final.
 #pragma once
 #include "lqro_qhull.hpp"
+#include "lqro_lp.hpp"
 
 namespace lqro {
 
@@ -2316,7 +2317,9 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
 // the reference's selection (LQRO:925-968; lqro_qhull.hpp qh_select) over
 // the finished hull: Qhull's facet order is key order, so a tie goes to the
 // smaller key and facet 0 is the smallest key alive
-__device__ inline void q3_select(const HullArgs& A, const Q3W& W, const Q3L& L, const Q3S& S, int lane,
+// returns (wave-uniform) whether this job closed its row and claimed the
+// row's LP (hull_row_done)
+__device__ inline bool q3_select(const HullArgs& A, const Q3W& W, const Q3L& L, const Q3S& S, int lane,
                                  const double* xi, const double* vrel, int slot) {
   const bool fail = (S.status & (QHS_INPUT | QHS_TOPOLOGY | QHS_CAPACITY)) != 0;
   double best = INFINITY;
@@ -2365,6 +2368,7 @@ __device__ inline void q3_select(const HullArgs& A, const Q3W& W, const Q3L& L, 
     q3_pl(W, L, bf, bq);
     for (int t = 0; t < 3; t++) bv[t] = W.vv[bf].id[t];
   }
+  int go = 0;
   if (lane == 0) {
     float* pl = A.planes + (size_t)slot * 8;
     double* qn = A.qnrm + (size_t)slot * 4;
@@ -2407,6 +2411,32 @@ __device__ inline void q3_select(const HullArgs& A, const Q3W& W, const Q3L& L, 
         }
       }
     }
+    go = hull_row_done(A, slot, stale, true);
+  }
+  hl_sync();
+  return __builtin_amdgcn_readfirstlane(go) != 0;
+}
+
+// calculateNewV (LQRO:1223-1234) for the row a job closed (hull_row_done),
+// wave 0, in the LDS of the facet planes (the build is over): the row's
+// planes and linearProgram4's projections, 32 B each (the runtime enables
+// the early LP only where 2 * npr * 32 B fit)
+__device__ inline void q3_row_lp(const HullArgs& A, Q3L& L, int slot, int lane) {
+  static_assert(sizeof(L.pl) >= 2 * LQRO_EARLY_LP_MAX_NPR * 32, "q3_row_lp: the planes must fit");
+  const int lrow = slot / A.npr;
+  const int i = A.row_begin + lrow * A.row_stride;
+  float* planes = reinterpret_cast<float*>(L.pl);
+  float* proj = planes + (size_t)A.npr * 8;
+  __threadfence();   // the row's planes other workgroups wrote (acquire)
+  const int m = lp_compact<8>(A.planes + (size_t)lrow * A.npr * 8, A.npr, planes, lane);
+  const v3 pref = V3((float)A.lp_vgoal[3 * i], (float)A.lp_vgoal[3 * i + 1], (float)A.lp_vgoal[3 * i + 2]);
+  v3 nv = V3(0.0f, 0.0f, 0.0f);
+  const int fail = w_lp3<8>(planes, m, A.lp_vmax, pref, false, nv, lane);       // :1228
+  if (fail < m) w_lp4<8>(planes, m, fail, (float)A.lp_vmax, nv, proj, lane);    // :1230
+  if (lane == 0) {
+    A.lp_newv[3 * i] = nv.x;
+    A.lp_newv[3 * i + 1] = nv.y;
+    A.lp_newv[3 * i + 2] = nv.z;
   }
   hl_sync();
 }
@@ -2435,6 +2465,7 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
     const double* Ni = A.NCF + (A.per_agent ? (size_t)i * A.H * 3 * A.X : 0);
     const double vrel[3] = {xi[3] - xj[3], xi[4] - xj[4], xi[5] - xj[5]};
     const int n = hull_points(A, L, Ti, Ni, xi, xj, vrel, W.Pr, W.Pf);
+    bool lp_go = false;
     if (wave == 2) {
       // prefetch each horizon wave 1 publishes until the build ends
       int last = 0;
@@ -2451,9 +2482,7 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
         if (++idle > (1l << 24)) break;
         __builtin_amdgcn_s_sleep(1);
       }
-      continue;   // (hull_take_job's barrier meets the other waves there)
-    }
-    if (wave == 1) {
+    } else if (wave == 1) {
       // speculate each published phase until the build ends (ph = -1)
       unsigned ep2 = W.ctr[0];
       unsigned short ep = 0;
@@ -2512,8 +2541,7 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
         for (int k = 0; k < 16; k++) atomicAdd(&A.prof[Q3_PROF_W1 + k], P.t[k]);
 #endif
       if (lane == 0) W.ctr[0] = ep2;
-      continue;   // (hull_take_job's barrier meets wave 0 there)
-    }
+    } else {
     Q3S S;
 #ifdef LQRO_QHULL_PROFILE
     for (int k = 0; k < 32; k++) S.tph[k] = 0;
@@ -2544,12 +2572,11 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
 #endif
       }
       hl_sync();
-      continue;
-    }
+    } else {
 #ifdef LQRO_QHULL_PROFILE
     unsigned long long tq_ = __builtin_amdgcn_s_memtime();
 #endif
-    q3_select(A, W, L, S, lane, xi, vrel, slot);
+    lp_go = q3_select(A, W, L, S, lane, xi, vrel, slot);
 #ifdef LQRO_QHULL_PROFILE
     S.tph[10] = __builtin_amdgcn_s_memtime() - tq_;
     S.tph[27] = __builtin_amdgcn_s_memtime() - tjob_;   // the whole job (26: its max over jobs)
@@ -2583,6 +2610,15 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
         if (rank == 0 && nl < A.ext_max) A.ext_facets[3 * nl] = -1;
       }
       hl_sync();
+    }
+    }   // the build was not handed over
+    }   // wave 0
+    if (A.rowpend) {
+      // this job closed its row: wave 0 runs the row's LP in the facet
+      // planes' LDS once waves 1 and 2 (which read them while speculating)
+      // are done with the build (the next hull_take_job waits for it)
+      __syncthreads();
+      if (wave == 0 && lp_go) q3_row_lp(A, L, slot, lane);
     }
   }
 }

@@ -189,6 +189,13 @@ struct LpArgs {
   int* lp4_list;              // 6 ints per row: lrow, fail, m, nv.xyz (float bits)
   int* lp4_count;
   int* lp4_next;
+  // early LP (lqro_hull.hpp hull_row_done): mode 1 runs the rows whose
+  // count reached row_target and that it claims; mode 2 (the tail) skips the
+  // rows claimed earlier.  rowclaim null: every row.
+  const int* rowpend;
+  int* rowclaim;
+  int row_target;
+  int mode;
 };
 
 // one row's LP; `planes` holds its compacted plane list (stride PS floats:
@@ -196,27 +203,7 @@ struct LpArgs {
 template <int PS>
 __device__ __forceinline__ void lp_row(const LpArgs& A, int lrow, float* planes, int lane) {
   const int i = A.row_begin + lrow * A.row_stride;
-  const float* src = A.slots + (size_t)lrow * A.npr * 8;
-  // orcaPlanes_ in push order (j order, LQRObstacles.cpp:1220)
-  int m = 0;
-  for (int base = 0; base < A.npr; base += 64) {
-    const int sidx = base + lane;
-    float4 a = make_float4(0, 0, 0, 0), b = make_float4(0, 0, 0, 0);
-    bool f = false;
-    if (sidx < A.npr) {
-      const float4* p = reinterpret_cast<const float4*>(src + 8 * (size_t)sidx);
-      a = p[0];
-      b = p[1];
-      f = __float_as_int(b.z) == 1;
-    }
-    const unsigned long long bal = __ballot(f);
-    if (f)
-      st_plane<PS>(planes, m + __popcll(bal & ((1ull << lane) - 1ull)), V3(a.x, a.y, a.z), V3(a.w, b.x, b.y));
-    m += __popcll(bal);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  const int m = lp_compact<PS>(A.slots + (size_t)lrow * A.npr * 8, A.npr, planes, lane);
   const v3 pref = V3((float)A.vgoal[3 * i], (float)A.vgoal[3 * i + 1], (float)A.vgoal[3 * i + 2]);
   v3 nv = V3(0.0f, 0.0f, 0.0f);
   const int fail = w_lp3<PS>(planes, m, A.vmax, pref, false, nv, lane);          // :1228
@@ -267,6 +254,20 @@ __global__ void __launch_bounds__(64) k_lp_lds(LpArgs A) {
   extern __shared__ float lp_planes[];
   const int lrow = blockIdx.x;
   if (lrow >= A.nrows) return;
+  if (A.rowclaim) {
+    int go;
+    if (A.mode == 1) {
+      go = 0;
+      if (threadIdx.x == 0)
+        go = __hip_atomic_load(A.rowpend + lrow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == A.row_target &&
+             atomicCAS(A.rowclaim + lrow, 0, 1) == 0;
+      go = __builtin_amdgcn_readfirstlane(go);
+      __threadfence();   // the row's planes (acquire)
+    } else {
+      go = A.rowclaim[lrow] != 1;
+    }
+    if (!go) return;
+  }
 #ifdef LQRO_LP_PROFILE
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -414,6 +415,12 @@ struct lqro_ctx {
   double* d_qnrm;
   int* d_qstale;
   double* d_carry;
+  // early LP (LQRO_EARLY_LP, default 1): per row open work and LP claim
+  // (lqro_hull.hpp hull_row_done)
+  int early_lp;
+  int early_step;            // the step being enqueued runs the early LP
+  int* d_rowpend;
+  int* d_rowclaim;
   PairArgs pa;
 };
 
@@ -478,7 +485,7 @@ void lqro_destroy(lqro_ctx* c) {
   void* ps[] = {c->d_R, c->d_TF, c->d_shash, c->d_T, c->d_NCF, c->d_S, c->d_x, c->d_vgoal, c->d_newv, c->d_A, c->d_B,
                 c->d_L, c->d_E, c->d_planes, c->d_lpscratch, c->d_lpcompact, c->d_recs, c->d_hq, c->d_hcount,
                 c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats, c->d_prof, c->d_rq, c->d_hbig, c->d_hwide, c->d_hbag, c->d_lp4, c->d_hotlist, c->d_hotmark, c->d_nbrlist, c->d_hfbest, c->d_hvpid, c->d_hstack, c->d_lq,
-                c->d_qscratch, c->d_qnrm, c->d_qstale, c->d_carry};
+                c->d_qscratch, c->d_qnrm, c->d_qstale, c->d_carry, c->d_rowpend /* d_rowclaim inside */};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (int k = 0; k < 5; ++k)
@@ -554,6 +561,8 @@ static int ctx_alloc(lqro_ctx* c) {
   HIPCHK(hipMalloc(&c->d_hotmark, slots ? slots : 1));
   HIPCHK(hipMalloc(&c->d_lp4, sizeof(int) * 6 * (size_t)std::max(1, c->nrows)));
   HIPCHK(hipMalloc(&c->d_carry, sizeof(double) * 6));
+  HIPCHK(hipMalloc(&c->d_rowpend, sizeof(int) * 2 * (size_t)std::max(1, c->nrows)));
+  c->d_rowclaim = c->d_rowpend + std::max(1, c->nrows);
   HIPCHK(hipMemset(c->d_carry, 0, sizeof(double) * 6));
   if (c->qhull_order) {
     // k_qhull: one one-wave worker per CU (the build's facets fill the CU's
@@ -618,6 +627,8 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
     c->lhull_prof = lp ? atoi(lp) != 0 : 0;
     const char* hm = getenv("LQRO_HOT_MAX_INSIDE");
     c->hot_max_inside = hm ? atol(hm) : -1L;
+    const char* el = getenv("LQRO_EARLY_LP");
+    c->early_lp = el ? atoi(el) != 0 : 1;
   }
   c->rb = g.row_begin;
   c->re = (g.row_end > g.row_begin) ? g.row_end : g.n_agents;
@@ -749,6 +760,17 @@ int lqro_set_gains(lqro_ctx* c, const double* A, const double* B, const double* 
 static int enqueue_tail(lqro_ctx* c, const double* d_x, const double* d_vgoal, double* d_newv, hipStream_t s,
                         const double* d_rowtab);
 
+// the LP launch's arguments for this context's rows (every row, the tail's
+// k_lp4 list)
+static LpArgs lp_args(const lqro_ctx* c, int npr, const double* d_vgoal, double* d_newv) {
+  LpArgs La{};
+  La.npr = npr; La.nrows = c->nrows; La.row_begin = c->rb; La.row_stride = c->rs; La.vmax = c->cfg.vmax_lp;
+  La.slots = c->d_planes; La.compact = c->d_lpcompact; La.proj = c->d_lpscratch;
+  La.vgoal = d_vgoal; La.newv = d_newv; La.prof = c->d_prof;
+  La.lp4_list = c->d_lp4; La.lp4_count = c->d_hcount + 9; La.lp4_next = c->d_hcount + 10;
+  return La;
+}
+
 // phase 0: the whole step.  Row shards in Qhull order split it around the
 // exchange of the loop-carried normal (lqro_step_device_begin / _end):
 // phase 1 runs the sweep and the hulls and writes each own row's last
@@ -863,23 +885,33 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
                    (lhull || (lds_ok && (size_t)g.horizon * g.n_points <= 16383 && side_waves >= 1));
   const int nwait = hot ? side : 0;
   P.row_split = std::max(1, std::min(16, (2 * c->n_cu + c->nrows - 1) / c->nrows));
+  // early LP (Qhull order, beside the hulls): a row whose planes are all
+  // final runs its LP at once — in a k_lp_lds after the main sweep, or in the
+  // k_qhull job that completes it (lqro_hull.hpp hull_row_done) — and the
+  // tail only runs the rest (rows waiting on k_stale, rows closed late)
+  const bool early = hot && c->early_lp && c->qhull_order && !c->qhull_big && phase == 0 && c->nbr_k <= 0 &&
+                     (size_t)npr * 32 <= 64 * 1024 && npr <= LQRO_EARLY_LP_MAX_NPR && d_newv != nullptr;
+  c->early_step = early ? 1 : 0;
+  P.rowpend = early ? c->d_rowpend : nullptr;
+  if (early) HIPCHK(hipMemsetAsync(c->d_rowpend, 0, sizeof(int) * 2 * (size_t)c->nrows, s));
   const int units = c->nrows * P.row_split;
   const unsigned nblk = (unsigned)std::min(units, c->n_cu - nwait);
   const unsigned nside = (unsigned)std::max(0, std::min(units - (int)nblk, nwait));
   P.hot_list = nullptr; P.hot_mark = nullptr; P.hot_count = nullptr;
   P.hot_next = nullptr; P.hot_cap = 0; P.hot_only = 0;
   if (hot) {
-    PrioArgs Q;
+    PrioArgs Q{};
     Q.npr = c->npr; Q.nrows = c->nrows; Q.row_begin = c->rb; Q.row_stride = c->rs; Q.X = g.x_dim; Q.x = d_x;
     Q.t_hot = c->hot_t; Q.r2_hot = c->hot_r * c->hot_r;   // seconds, metres (scheduling heuristic)
     Q.list = c->d_hotlist; Q.mark = c->d_hotmark; Q.count = c->d_hcount + 6; Q.cap = c->hot_cap;
+    Q.rowpend = P.rowpend;
     const long nb = std::min<long>((slots + 255) / 256, 8L * c->n_cu);
     hipLaunchKernelGGL(k_prio, dim3((unsigned)nb), dim3(256), 0, s, Q);
     HIPCHK(hipGetLastError());
     P.hot_list = c->d_hotlist; P.hot_mark = c->d_hotmark; P.hot_count = c->d_hcount + 6;
     P.hot_next = c->d_hcount + 7; P.hot_cap = c->hot_cap;
   }
-  HullArgs Hh;
+  HullArgs Hh{};
   Hh.N = g.n_agents; Hh.X = g.x_dim; Hh.H = g.horizon; Hh.NP = g.n_points;
   Hh.row_begin = c->rb; Hh.row_stride = c->rs; Hh.npr = npr; Hh.per_agent = c->per_agent;
   Hh.nbr_list = P.nbr_list;
@@ -908,6 +940,9 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   Hh.ljobs = c->lhull_prof ? c->d_prof + 32 + 2 * 4096 + 48 : nullptr;
   Hh.qscratch = c->d_qscratch; Hh.qstride = c->qstride; Hh.qnrm = c->d_qnrm;
   Hh.qstale = c->d_qstale; Hh.qstale_count = c->d_hcount + 15; Hh.qstale_cap = c->hull_cap;
+  Hh.rowpend = P.rowpend; Hh.rowclaim = early ? c->d_rowclaim : nullptr;
+  Hh.row_target = P.row_split * LQRO_ROW_BIG;
+  Hh.lp_vgoal = d_vgoal; Hh.lp_newv = d_newv; Hh.lp_vmax = g.vmax_lp;
   if (g.x_dim != 16 && g.x_dim != 12) return LQRO_E_ARG;
   // the row launch is submitted before the side stream's work: should the two
   // streams land on one hardware queue (a second context in the process), the
@@ -916,6 +951,16 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   if (nwait > 0) HIPCHK(hipEventRecord(c->xev[0], s));
   launch_pair(g.x_dim, dim3(nblk), dim3(P.waves * 64), c->lds_bytes, s, P);
   HIPCHK(hipGetLastError());
+  if (early) {
+    // the rows the main sweep closed (no open hull): their LP on its CUs
+    // while the side stream's hulls run
+    LpArgs Le = lp_args(c, npr, d_vgoal, d_newv);
+    Le.lp4_list = nullptr;
+    Le.rowpend = c->d_rowpend; Le.rowclaim = c->d_rowclaim; Le.row_target = Hh.row_target; Le.mode = 1;
+    HIPCHK(hipFuncSetAttribute((const void*)k_lp_lds<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLpLdsMax));
+    hipLaunchKernelGGL(k_lp_lds<8>, dim3((unsigned)c->nrows), dim3(64), (size_t)npr * 32, s, Le);
+    HIPCHK(hipGetLastError());
+  }
   if (nwait > 0) {
     HIPCHK(hipStreamWaitEvent(c->side, c->xev[0], 0));
     PairArgs Ph = P;
@@ -1022,11 +1067,11 @@ static int enqueue_tail(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
     HIPCHK(hipGetLastError());
   }
   c->pending = 0;
-  LpArgs La;
-  La.npr = npr; La.nrows = c->nrows; La.row_begin = c->rb; La.row_stride = c->rs; La.vmax = g.vmax_lp;
-  La.slots = c->d_planes; La.compact = c->d_lpcompact; La.proj = c->d_lpscratch;
-  La.vgoal = d_vgoal; La.newv = d_newv; La.prof = c->d_prof;
-  La.lp4_list = c->d_lp4; La.lp4_count = c->d_hcount + 9; La.lp4_next = c->d_hcount + 10;
+  LpArgs La = lp_args(c, npr, d_vgoal, d_newv);
+  if (c->early_step) {   // the rows the early LP ran are done
+    La.rowclaim = c->d_rowclaim;
+    La.mode = 2;
+  }
   HIPCHK(launch_lp(La, s));
   HIPCHK(hipMemcpyAsync(c->h_inside + slot, c->d_stats + 2, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
   HIPCHK(hipEventRecord(c->iev[slot], s));
@@ -1278,7 +1323,7 @@ int lqro_calculate_new_v(const float* planes, const int64_t* offsets, int32_t n_
              hipMemcpy(d_vg, vgoal, sizeof(double) * 3 * n_agents, hipMemcpyHostToDevice) != hipSuccess) {
     rc = LQRO_E_HIP;
   } else {
-    LpArgs La;
+    LpArgs La{};
     La.npr = (int)mmax; La.nrows = n_agents; La.row_begin = 0; La.row_stride = 1; La.vmax = vmax_lp;
     La.slots = d_slots; La.compact = d_compact; La.proj = d_proj; La.vgoal = d_vg; La.newv = d_nv; La.prof = nullptr;
     La.lp4_list = d_l4; La.lp4_count = d_l4c; La.lp4_next = d_l4c + 1;
@@ -1433,7 +1478,7 @@ int lqro_debug_hull_points(lqro_ctx* c, const double* pts, int32_t n, const doub
         hipMemcpy(d_rec, &r0, sizeof r0, hipMemcpyHostToDevice) != hipSuccess) {
       rc = LQRO_E_HIP;
     } else {
-      HullArgs Hh;
+      HullArgs Hh{};
       memset(&Hh, 0, sizeof Hh);
       Hh.N = 2; Hh.X = X; Hh.H = g.horizon; Hh.NP = g.n_points;
       Hh.row_begin = 0; Hh.row_stride = 1; Hh.npr = 1; Hh.per_agent = 0;

@@ -1235,8 +1235,14 @@ static float fmins(float a, float b) { return (b < a) ? b : a; }  /* std::min */
 
 #define RVO_EPSILON 0.00001f
 
+/* the length of the LP's sequential chain (linearProgram1 calls plus
+ * violated planes met by the scans of linearProgram2-4) since the last
+ * orc_lp_chain: test instrumentation only, it does not change any result */
+static __thread long long g_lp_chain;
+
 static int lp1(const plane_t* planes, int planeNo, const line_t* line, float radius, v3 optVelocity,
                int directionOpt, v3* result) {
+  g_lp_chain++;
   const float dotProduct = vdot(line->point, line->direction);
   const float discriminant = sqrf(dotProduct) + sqrf(radius) - vabsSq(line->point);
   if (discriminant < 0.0f) return 0;
@@ -1292,6 +1298,7 @@ static int lp2(const plane_t* planes, int planeNo, float radius, v3 optVelocity,
   }
   for (int i = 0; i < planeNo; ++i) {
     if (vdot(planes[i].normal, vsub(planes[i].point, *result)) > 0.0f) {
+      g_lp_chain++;
       v3 crossProduct = vcross(planes[i].normal, planes[planeNo].normal);
       if (vabsSq(crossProduct) <= RVO_EPSILON) return 0;
       line_t line;
@@ -1314,6 +1321,7 @@ static int lp3(const plane_t* planes, int m, double radius, v3 optVelocity, int 
   else *result = optVelocity;
   for (int i = 0; i < m; ++i) {
     if (vdot(planes[i].normal, vsub(planes[i].point, *result)) > 0.0f) {
+      g_lp_chain++;
       const v3 tempResult = *result;
       if (!lp2(planes, i, (float)radius, optVelocity, directionOpt, result)) {
         *result = tempResult;
@@ -1329,6 +1337,7 @@ static void lp4(const plane_t* planes, int m, int beginPlane, float radius, v3* 
   float distance = 0.0f;
   for (int i = beginPlane; i < m; ++i) {
     if (vdot(planes[i].normal, vsub(planes[i].point, *result)) > distance) {
+      g_lp_chain++;
       int np = 0;
       for (int j = 0; j < i; ++j) {
         plane_t plane;
@@ -1367,6 +1376,27 @@ void orc_newv(int m, const float* pl, const double* vgoal, double vmax_lp, doubl
   if (planeFail < m) lp4(planes, m, planeFail, (float)maxSpeed_, &nv, scratch);
   newv[0] = nv.x; newv[1] = nv.y; newv[2] = nv.z;
   free(planes); free(scratch);
+}
+
+/* linearProgram4's share of the sequential chain of calculateNewV for one
+ * plane list (0 when linearProgram3 succeeds): ranks the hardest LPs for
+ * tests/golden/make_golden_lp_rows.py */
+long long orc_lp_chain(int m, const float* pl, const double* vgoal, double vmax_lp) {
+  double nv[3];
+  long long c0;
+  plane_t* planes = (plane_t*)malloc(sizeof(plane_t) * (size_t)(m > 0 ? m : 1));
+  for (int k = 0; k < m; k++) {
+    planes[k].point = V(pl[6 * k], pl[6 * k + 1], pl[6 * k + 2]);
+    planes[k].normal = V(pl[6 * k + 3], pl[6 * k + 4], pl[6 * k + 5]);
+  }
+  v3 pref = V((float)vgoal[0], (float)vgoal[1], (float)vgoal[2]);
+  v3 r = V(0.0f, 0.0f, 0.0f);
+  const int fail = lp3(planes, m, vmax_lp, pref, 0, &r);
+  free(planes);
+  if (fail >= m) return 0;
+  c0 = g_lp_chain;
+  orc_newv(m, pl, vgoal, vmax_lp, nv);
+  return g_lp_chain - c0;
 }
 
 /* operator! on a 3x3 / 4x4 matrix (MAT:603-671), for the tests */

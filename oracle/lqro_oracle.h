@@ -67,6 +67,7 @@ int  orc_pair(int X, int H, int NP, int min_reach, double vmax_reach,
 
 /* calculateNewV (LQRO:1223-1234) with linearProgram1-4 (LQRO:1001-1206),
  * fp32 Vector3 arithmetic (V3).  planes: m x {point[3], normal[3]} floats. */
+long long orc_lp_chain(int m, const float* planes, const double* vgoal, double vmax_lp);
 void orc_newv(int m, const float* planes, const double* vgoal, double vmax_lp,
               double* newv);
 

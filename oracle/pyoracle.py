@@ -48,6 +48,8 @@ def lib():
         _o.orc_step_faithful_mt.argtypes = _o.orc_step_mt.argtypes[:8] + [C.c_void_p] * 2 + \
             _o.orc_step_mt.argtypes[8:]
         _o.orc_newv.argtypes = [C.c_int, C.c_void_p, C.c_void_p, d, C.c_void_p]
+        _o.orc_lp_chain.argtypes = [C.c_int, C.c_void_p, C.c_void_p, d]
+        _o.orc_lp_chain.restype = C.c_longlong
         _o.orc_sphere.argtypes = [C.c_int, d, d, C.c_void_p]
         _o.orc_pinv.argtypes = [C.c_int, C.c_void_p, C.c_void_p]
         _o.orc_hull_branch.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
@@ -192,6 +194,13 @@ def newv(planes6: np.ndarray, vgoal, vmax_lp=100.0):
     out = np.zeros(3)
     lib().orc_newv(planes6.shape[0], _p(planes6), _p(v), vmax_lp, _p(out))
     return out
+
+
+def lp_chain(planes6: np.ndarray, vgoal, vmax_lp=100.0) -> int:
+    """linearProgram4's sequential chain length for one plane list (0: no LP4)."""
+    planes6 = np.ascontiguousarray(planes6, np.float32).reshape(-1, 6)
+    v = np.ascontiguousarray(vgoal, np.float64)
+    return int(lib().orc_lp_chain(planes6.shape[0], _p(planes6), _p(v), vmax_lp))
 
 
 def round6(v: float) -> float:

@@ -15,3 +15,14 @@ def test_lp_bit_exact(lqro_mod, oracle, seed, max_planes):
     ref = np.array([oracle.newv(c, g) for c, g in zip(cases, goals)])
     bad = np.where(~np.all(got == ref, axis=1))[0]
     assert bad.size == 0, (bad[:10], got[bad[:3]], ref[bad[:3]])
+
+
+def test_lp_c3_hardest_rows(lqro_mod):
+    """The C3 swarm's slowest linearProgram4 rows (tests/golden/lp_rows.npz,
+    1,023 planes each, made by make_golden_lp_rows.py from the oracle step
+    that qhull_order.npz pins): bit-exact new velocities."""
+    import os
+    from conftest import GOLDEN
+    d = np.load(os.path.join(GOLDEN, "lp_rows.npz"))
+    got = lqro_mod.calculate_new_v(list(d["planes"]), d["vgoal"], vmax_lp=float(d["vmax_lp"]))
+    assert np.array_equal(got.view(np.uint64), d["newv"].view(np.uint64))

@@ -93,6 +93,16 @@ def test_newv_bit_exact(oracle):
         assert _same_bits(got, d["newv"][k]), k
 
 
+def test_newv_c3_hardest_rows(oracle):
+    """The C3 rows whose LP runs linearProgram4 longest (lp_rows.npz, checked
+    against the reference's calculateNewV when made): the oracle bit for bit."""
+    d = _load("lp_rows.npz")
+    for k in range(d["newv"].shape[0]):
+        got = oracle.newv(d["planes"][k], d["vgoal"][k], float(d["vmax_lp"]))
+        assert _same_bits(got, d["newv"][k]), k
+        assert oracle.lp_chain(d["planes"][k], d["vgoal"][k], float(d["vmax_lp"])) == d["chain"][k]
+
+
 @pytest.mark.parametrize("scenario", ["c2", "swap"])
 def test_row_newv_bit_exact(oracle, scenario):
     """The whole row body (LQRO:1393-1435) for the golden rows."""
