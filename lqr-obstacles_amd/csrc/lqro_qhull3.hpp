@@ -213,6 +213,9 @@ struct Q3L {
   int hq_c, hq_from, hq_np, hq_sharp, hq_init, hq_prestart;
   int hq_findbestnew, hq_notsharp, hq_nnew, hq_nmov, hq_nvis;
   double hq_max_outside;
+#ifdef LQRO_QHULL_PROFILE
+  unsigned long long pub_t, done_t;   // the last publication / speculation end (handshake latencies)
+#endif
 };
 static_assert(sizeof(Q3L) <= 160 * 1024, "k_qhull's LDS exceeds a CU");
 
@@ -228,6 +231,9 @@ struct Q3S {
   unsigned long long tph[32];   // LQRO_QHULL_PROFILE: phase cycles 0..20, counters 21..28
   unsigned long long tq;         // LQRO_QHULL_PROFILE: the last stamp
   unsigned long long tw, nw;     // LQRO_QHULL_PROFILE: waiting for wave 1's speculation
+  unsigned long long tdl;        // LQRO_QHULL_PROFILE: its end until wave 0 sees it
+  unsigned long long tw1, nw1;   // LQRO_QHULL_PROFILE: the waits after one-chunk insertions
+  int prev1;
   unsigned long long tps[24], nps;   // LQRO_QHULL_PROFILE: phases of the one-chunk insertions
 };
 
@@ -752,14 +758,14 @@ __device__ __forceinline__ int q3_wait(const int* p, int v, bool ne) {
 // chunks of a long sequence under a copy of wave 0's state.
 __device__ __forceinline__ void q3_chunk_locate(const Q3W& W, const Q3S& S, const Q3L& L, int c, int from, int np,
                                                 int sharp, bool init, int lane, const HullPt& pre, int prestart,
-                                                bool havepre, HullPt& pt, int& f, double& d, int& isout, int& trig,
+                                                int prec, HullPt& pt, int& f, double& d, int& isout, int& trig,
                                                 int& ls) {
   const int pos = c + lane;
   pt = pre;
   f = -1; d = 0.0; isout = 0; trig = 0;
   if (pos >= from && pos < np) {
     int start = prestart;
-    if (!(havepre && c == 0)) pt = q3_seqpt(W, L, S.nvis, init, pos, &start);
+    if (c != prec) pt = q3_seqpt(W, L, S.nvis, init, pos, &start);   // (prec: the chunk pre holds)
     const double p[3] = {pt.x, pt.y, pt.z};
     f = q3_locate(W, S, L, p, start, sharp, &d, &isout, &trig, ls);
   }
@@ -777,7 +783,7 @@ __device__ inline void q3_serve_chunk(const Q3W& W, Q3L& L, int lane) {
   pre.x = pre.y = pre.z = 0.0; pre.q = -1; pre.pad = 0;
   int f, isout, trig, ls = 0;
   double d;
-  q3_chunk_locate(W, S, L, L.hq_c, L.hq_from, L.hq_np, L.hq_sharp, L.hq_init != 0, lane, pre, L.hq_prestart, false,
+  q3_chunk_locate(W, S, L, L.hq_c, L.hq_from, L.hq_np, L.hq_sharp, L.hq_init != 0, lane, pre, L.hq_prestart, -1,
                   pt, f, d, isout, trig, ls);
   L.hr_pt[lane] = pt;
   L.hr_d[lane] = d;
@@ -810,6 +816,10 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
   // before an event changed the state is never asked for)
   const bool help = np > 128;
   int req = L.hstate >> 2, req_c = -1;   // the last request and its chunk
+  // the next chunk this wave locates itself, its points fetched one chunk
+  // ahead (the sequence's points do not change while it is located)
+  HullPt cpre = pre;
+  int cstart = prestart, cprec = havepre ? 0 : -1;
   auto resolve = [&]() -> bool {   // true: wave 1 answered request `req`
     if (req_c < 0) return false;
     req_c = -1;
@@ -862,8 +872,16 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
         post(c + 64, from);   // the next chunk to wave 1
       }
       Q3T(12);
-      if (!got)
-        q3_chunk_locate(W, S, L, c, from, np, sharp, init, lane, pre, prestart, havepre, pt, f, d, isout, trig, ls);
+      if (!got) {
+        const int nc = c + (help ? 128 : 64);
+        HullPt npt = pre;
+        int nst = 0;
+        if (nc + lane < np) npt = q3_seqpt(W, L, S.nvis, init, nc + lane, &nst);
+        q3_chunk_locate(W, S, L, c, from, np, sharp, init, lane, cpre, cstart, cprec, pt, f, d, isout, trig, ls);
+        cpre = npt;
+        cstart = nst;
+        cprec = nc;
+      }
       Q3T(13);
       if (act) {
         if (isout) {
@@ -1026,7 +1044,18 @@ __device__ inline void q3_emit_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int ndn
   }
   hl_sync();
   Q3T(15);
-  // the sequence in order: a chunk's lanes, grouped by destination
+  // the sequence in order: a chunk's lanes, grouped by destination (a long
+  // sequence's next chunk loaded while this one is placed)
+  int ng = -1;
+  double ndd = 0.0;
+  HullPt npt = rpt;
+  auto ldc = [&](int c) {
+    const int pos = c + lane;
+    ng = pos < np ? W.pdst[pos] : -1;
+    ndd = pos < np ? W.pdd[pos] : 0.0;
+    if (ng >= 0) npt = W.pseq[pos];
+  };
+  if (np > 64) ldc(0);
   for (int c = 0; c < np; c += 64) {
     const int pos = c + lane;
     const bool act = pos < np;
@@ -1034,9 +1063,10 @@ __device__ inline void q3_emit_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int ndn
     double dd = rd;
     HullPt pt = rpt;
     if (np > 64) {   // (at most 64: the lanes' own results)
-      g = act ? W.pdst[pos] : -1;
-      dd = act ? W.pdd[pos] : 0.0;
-      if (g >= 0) pt = W.pseq[pos];
+      g = ng;
+      dd = ndd;
+      pt = npt;
+      if (c + 64 < np) ldc(c + 64);
     } else if (!act) {
       g = -1;
     }
@@ -1144,6 +1174,12 @@ struct Q3QC {
   double r[6];
 };
 
+// a vertex record's two cache lines requested (the value only feeds an empty
+// asm at the speculation's end, so the load is issued but not waited for)
+__device__ __forceinline__ unsigned q3_touch(const Q3V& v) {
+  return *reinterpret_cast<const unsigned*>(v.p) ^ *reinterpret_cast<const unsigned*>(v.id);
+}
+
 __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep, unsigned ep2, Q3QC& Q, Q3P& P,
                                int phase) {
   const unsigned long long ltmask = (1ull << lane) - 1ull;
@@ -1182,7 +1218,8 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
         *reinterpret_cast<int4*>(v.id) = make_int4(L.nv[3 * t], L.nv[3 * t + 1], L.nv[3 * t + 2], 0);
       }
     }
-    hl_sync();
+    // (no wait for the stores here: the horizon reads no record; the fence
+    // before the cone orders them)
   }
   Q.one = 0;
   Q.rt = -1;
@@ -1230,9 +1267,11 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
     qh = Q.qcb + Q.qcn;
   }
   int ls = 0, nvis = 0, nnew = 0, ts = 0, lm = 0;
+  unsigned touch = 0u;
   W1T(2);
   if (facet >= 0) {
     // 2. qh_findhorizon, as wave 0's (level order, first occurrence), visits as epochs
+    touch += q3_touch(W.vv[facet]);
     if (lane == 0) L.sp_visf[0] = facet;
     if (lane < 3) L.sp_cand[lane] = (unsigned short)q3_nb(W, L, facet, lane);
     mark(facet);
@@ -1264,6 +1303,10 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
           dup |= (l < lane) && __builtin_amdgcn_readlane(nb, l) == nb;
         }
         vis = vis && !dup;
+        // the cone reads the vertex records of the horizon facets (and the
+        // visible ones' ids): their lines are requested now, under the rest
+        // of the search (consumed only at the end of the speculation)
+        if (c < ncand && (vis || (cand && !vis))) touch += q3_touch(W.vv[nb]);
         const unsigned long long bv = __ballot(vis);
         if (vis) {
           const int at = nvis + __popcll(bv & ltmask);
@@ -1453,6 +1496,7 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
   }
   const int st = qh_wave_or(ls | ts | lm);
   W1T(5);
+  asm volatile("" ::"v"(touch));   // (the requested lines: waited for only here)
   hl_sync();
   if (lane == 0) {
     L.sp_ok = ok;
@@ -1847,8 +1891,13 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
 #endif
       const int dn = q3_wait(&L.sp_done, phase, false);
 #ifdef LQRO_QHULL_PROFILE
-      S.tw += __builtin_amdgcn_s_memtime() - tw_;
-      S.nw += 1;
+      {
+        const unsigned long long tn_ = __builtin_amdgcn_s_memtime();
+        S.tw += tn_ - tw_;
+        S.nw += 1;
+        if (tn_ - tw_ > 200) S.tdl += tn_ - L.done_t;   // (waited) speculation end -> seen here
+        if (S.prev1) { S.tw1 += tn_ - tw_; S.nw1 += 1; }   // after a one-chunk insertion
+      }
 #endif
       if (dn != phase) {   // wave 1 still speculating (it writes vertex records from L.nslot): stop
         S.status |= QHS_CAPACITY | QHS_TIMEOUT;
@@ -2116,32 +2165,17 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     if (S.status & (QHS_TOPOLOGY | QHS_CAPACITY)) return;
     S.nnew = nnew;
     hl_sync();
-    // qh_partitionvisible's sequence: the visible facets' outside sets in
-    // visible order; its first 64 points are fetched now, under the cone's
-    // construction
-    int np2 = 0;
-    for (int c0 = 0; c0 < nvis; c0 += 64) {
-      const int vi = c0 + lane;
-      const int cnt = vi < nvis ? L.vscnt[vi] : 0;
-      const int inc = q3_scan_add(cnt);
-      if (vi < nvis) L.vinc[vi] = np2 + inc;
-      np2 += __builtin_amdgcn_readlane(inc, 63);
-    }
-    hl_sync();
-    if (adopt) Q3T(19);   // (profile: the sequence's extent)
+    // wave 2's head of the partition sequence, read before wave 1 may start
+    // the next speculation (whose horizon restarts wave 2's prefetch)
     HullPt pre;
     pre.x = pre.y = pre.z = 0.0;
     pre.q = -1;
     pre.pad = 0;
-    int prestart = 0;
-    if (pfv && np2 == L.pf_np) {   // wave 2's head of the sequence
-      if (lane < np2) {
-        pre = L.pf_pre[lane];
-        const int a = L.pf_prea[lane];
-        prestart = L.repl[a] >= 0 ? L.repl[a] : 0;
-      }
-    } else if (lane < np2) {
-      pre = q3_seqpt(W, L, nvis, false, lane, &prestart);
+    int pfa = 0, pfnp = -1;
+    if (pfv) {
+      pfnp = L.pf_np;
+      pre = L.pf_pre[lane];
+      pfa = L.pf_prea[lane];
     }
     {
       // slots: the visible facets', then free ones, then fresh ones
@@ -2241,10 +2275,31 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
       L.pub_nnew = nnew;
     }
     ++phase;
+#ifdef LQRO_QHULL_PROFILE
+    if (lane == 0) L.pub_t = __builtin_amdgcn_s_memtime();
+#endif
     if (lane == 0) q3_st_rel(&L.ph, phase);
     S.findbestnew = 0;
     S.notsharp = 0;
     S.nmov = 0;
+    // qh_partitionvisible's sequence: the visible facets' outside sets in
+    // visible order (its extent and first 64 points: after the publication,
+    // beside the next speculation)
+    int np2 = 0;
+    for (int c0 = 0; c0 < nvis; c0 += 64) {
+      const int vi = c0 + lane;
+      const int cnt = vi < nvis ? L.vscnt[vi] : 0;
+      const int inc = q3_scan_add(cnt);
+      if (vi < nvis) L.vinc[vi] = np2 + inc;
+      np2 += __builtin_amdgcn_readlane(inc, 63);
+    }
+    hl_sync();
+    int prestart = 0;
+    if (pfv && np2 == pfnp) {   // wave 2's head of the sequence
+      if (lane < np2) prestart = L.repl[pfa] >= 0 ? L.repl[pfa] : 0;
+    } else if (lane < np2) {
+      pre = q3_seqpt(W, L, nvis, false, lane, &prestart);
+    }
     Q3T(5);
     const int sharp = adopt ? L.sp_sharp : q3_sharpnewfacets(S, L, lane);
     Q3T(20);
@@ -2305,6 +2360,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     Q3T(9);
 #ifdef LQRO_QHULL_PROFILE
     // insertions whose partition sequence is longer than one chunk: 29 cycles, 30 count
+    S.prev1 = np2 <= 64;
     if (np2 > 64) { S.tph[29] += S.tq - tins_; S.tph[30] += 1; }
     else {
       for (int k = 0; k < 21; k++) S.tps[k] += S.tph[k] - snap_[k];
@@ -2504,9 +2560,13 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
 #ifdef LQRO_QHULL_PROFILE
           const unsigned long long t0_ = __builtin_amdgcn_s_memtime();
           P.tq = t0_;
+          P.t[14] += t0_ - L.pub_t;   // publication -> speculation start
 #endif
           q3_spec(W, L, lane, ep, ep2, Q, P, p);
           hl_sync();
+#ifdef LQRO_QHULL_PROFILE
+          if (lane == 0) L.done_t = __builtin_amdgcn_s_memtime();
+#endif
           if (lane == 0) q3_st_rel(&L.sp_done, p);
 #ifdef LQRO_QHULL_PROFILE
           P.t[0] += __builtin_amdgcn_s_memtime() - t0_;
@@ -2546,6 +2606,9 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
 #ifdef LQRO_QHULL_PROFILE
     for (int k = 0; k < 32; k++) S.tph[k] = 0;
     S.tw = S.nw = 0;
+    S.tdl = 0;
+    S.tw1 = S.nw1 = 0;
+    S.prev1 = 0;
     for (int k = 0; k < 24; k++) S.tps[k] = 0;
     S.nps = 0;
     const unsigned long long tjob_ = __builtin_amdgcn_s_memtime();
@@ -2588,6 +2651,9 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
       atomicAdd(&A.prof[Q3_PROF_W1 + 10], S.nw);
       for (int k = 0; k < 24; k++) atomicAdd(&A.prof[Q3_PROF_W1 + 16 + k], S.tps[k]);
       atomicAdd(&A.prof[Q3_PROF_W1 + 40], S.nps);
+      atomicAdd(&A.prof[Q3_PROF_W1 + 41], S.tdl);
+      atomicAdd(&A.prof[Q3_PROF_W1 + 42], S.tw1);
+      atomicAdd(&A.prof[Q3_PROF_W1 + 43], S.nw1);
       atomicMax(&A.prof[26], S.tph[27]);
       // per job (words 32 + 2j): cycles; insertions | points << 20 | facet slots << 40
       const unsigned long long j = atomicAdd(&A.prof[11], 1ull);

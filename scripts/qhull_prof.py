@@ -71,6 +71,10 @@ if w1[7]:
           "phases us/spec: records %.2f queue %.2f horizon %.2f cone %.2f match %.2f checkzero %.2f sharp %.2f;"
           " horizon levels %.2f" %
           (tuple(w1[k] / max(w1[7], 1) / GHZ / 1e3 for k in (1, 2, 3, 4, 12, 13, 5)) + (w1[11] / max(w1[7], 1),)))
+    print("handshake: publication -> speculation start %.3f us, speculation end -> wave 0 sees it %.3f ms/hull"
+          " (when it waited); waits after one-chunk insertions %.3f us each (%d)" %
+          (w1[14] / max(w1[7], 1) / GHZ / 1e3, w1[41] / jobs / GHZ / 1e6, w1[42] / max(w1[43], 1) / GHZ / 1e3,
+           w1[43] // jobs))
     print("wave 1: chunks served", w1[8] / jobs, "per hull,", w1[6] / max(w1[8], 1) / GHZ / 1e3, "us each")
     print("wave 0 waiting for a speculation: %.3f ms/hull, %.2f us per wait (%d waits/hull)" %
           (w1[9] / jobs / GHZ / 1e6, w1[9] / max(w1[10], 1) / GHZ / 1e3, w1[10] // jobs))

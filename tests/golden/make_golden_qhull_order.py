@@ -24,6 +24,12 @@ Stores tests/golden/qhull_order.npz:
       facet's index in Qhull's order and Fv triple, dist, normal (after the
       carry), stale flag;
   <w>_newv: every row's newV under the reference's rule;
+  <w>_merged: per inside-hull pair whose qconvex output has a merged
+      (non-simplicial) facet — Qhull's default pre-merge (C-0) — i, j, the
+      merged hull's facet count, its non-simplicial facets' count and whether
+      the winning facet is one of them; <w>_merged_facets: those facets'
+      Fv lists (flattened, <w>_merged_offs: offsets per facet, per pair in
+      <w>_merged_pairoffs), first vertex and plane (<w>_merged_planes);
   inject_*: six dense-swarm pairs with Qhull's full output (rounded points,
       Fv lists, planes as read back) for the GPU selection test hook.
 and prints a summary (also to argv[1]).
@@ -64,7 +70,8 @@ def reference_hull(pts_full, vrel):
         t = abs(planes[i, 0] * (vrel[0] - P[0]) + planes[i, 1] * (vrel[1] - P[1]) + planes[i, 2] * (vrel[2] - P[2]))
         if dist is None or t < dist:
             dist, best = t, i
-    return dist, best, fv[best], planes[best, :3].copy(), len(fv), (rounded, fv, planes)
+    return dist, best, list(fv[best]) + [-1] * max(0, 3 - len(fv[best])), planes[best, :3].copy(), len(fv), \
+        (rounded, fv, planes)
 
 
 def workload(name, N, H, box, seed, g, inject=None):
@@ -74,7 +81,7 @@ def workload(name, N, H, box, seed, g, inject=None):
     pyoracle.set_hull_rule(0)
     _, recs = pyoracle.step(T, NCF, S, x, vg, threads=8)
     carry = np.zeros(3)                     # normalVector (LQRO:1385)
-    pairs, planes_row = [], {}
+    pairs, planes_row, merged = [], {}, []
     for r in recs:                          # (i, j) order: the reference's loop
         if not (r["flags"] & 1):
             continue                        # n <= 4: normalVector untouched (LQRO:1409)
@@ -85,6 +92,11 @@ def workload(name, N, H, box, seed, g, inject=None):
         _, _, pts = pyoracle.pair(T, NCF, S, x[i], x[j], i, j, want_points=True)
         vrel = x[i, 3:6] - x[j, 3:6]
         dist, best, fvb, nrm, nf, q = reference_hull(pts, vrel)
+        nonsimp = [k for k, f in enumerate(q[1]) if len(f) != 3]
+        if nonsimp:   # Qhull merged facets here (its default pre-merge)
+            merged.append((i, j, nf, len(nonsimp), int(best in nonsimp),
+                           [(list(q[1][k]), q[2][k].copy()) for k in nonsimp]))
+        fvb = fvb[:3]
         stale = best == 0
         if not stale:
             carry = nrm
@@ -113,7 +125,19 @@ def workload(name, N, H, box, seed, g, inject=None):
     arr = np.zeros(len(pairs), dt)
     for k, p in enumerate(pairs):
         arr[k] = (p[0], p[1], p[2], p[3], p[4], p[5:8], p[8], p[9:12], p[12])
-    return x, vg, arr, newv, carry
+    mdt = np.dtype([("i", "<i4"), ("j", "<i4"), ("n_facets", "<i4"), ("n_merged", "<i4"), ("winner_merged", "<i4")])
+    marr = np.zeros(len(merged), mdt)
+    mfac, moffs, mplanes, mpoffs = [], [0], [], [0]
+    for k, (i, j, nf, nm, wm, facets) in enumerate(merged):
+        marr[k] = (i, j, nf, nm, wm)
+        for f, pl in facets:
+            mfac.extend(int(v) for v in f)
+            moffs.append(len(mfac))
+            mplanes.append(pl)
+        mpoffs.append(len(mplanes))
+    mout = dict(merged=marr, merged_facets=np.array(mfac, np.int32), merged_offs=np.array(moffs, np.int64),
+                merged_planes=np.array(mplanes, np.float64).reshape(-1, 4), merged_pairoffs=np.array(mpoffs, np.int64))
+    return x, vg, arr, newv, carry, mout
 
 
 def main():
@@ -122,7 +146,9 @@ def main():
     inject = []
     for name, N, H, box, seed in WORKLOADS:
         t0 = time.time()
-        x, vg, arr, newv, carry = workload(name, N, H, box, seed, g, inject if name == "dense" else None)
+        x, vg, arr, newv, carry, mout = workload(name, N, H, box, seed, g, inject if name == "dense" else None)
+        for k, v in mout.items():
+            out[f"{name}_{k}"] = v
         out[f"{name}_pairs"] = arr
         out[f"{name}_newv"] = newv
         out[f"{name}_carry"] = carry
@@ -140,6 +166,8 @@ def main():
         summary[name] = dict(
             inside_pairs=len(arr), stale_pairs=int(arr["stale"].sum()),
             qhull_merge_pairs=int(((ins["flags"] & 0x80) != 0).sum()),
+            qconvex_merged_pairs=len(mout["merged"]),
+            qconvex_merged_winners=int(mout["merged"]["winner_merged"].sum()),
             oracle_pairs_bit_exact=same, oracle_rows_newv_bit_exact=int((v1 == newv).all(1).sum()),
             rows=N, seconds=round(time.time() - t0, 1))
         print(name, summary[name], flush=True)
