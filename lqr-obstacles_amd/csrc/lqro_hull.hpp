@@ -135,7 +135,7 @@ struct HullArgs {
 // (LQRO_ROW_BIG, lqro_device.hpp: the row counter's protocol; the early LP
 // runs in k_qhull's facet-plane LDS: rows of at most LQRO_EARLY_LP_MAX_NPR
 // pairs, planes and projections 32 B each)
-#define LQRO_EARLY_LP_MAX_NPR 1152
+#define LQRO_EARLY_LP_MAX_NPR 1024
 // lane 0, after the job's plane (or its pending / failed flag) is written:
 // count the row down; true when this job closed the row and claimed its LP
 // (can_run: the caller will run it)

@@ -22,6 +22,7 @@ void launch_lhull(dim3 grid, hipStream_t s, const HullArgs& A);
 // which with A.big_main takes the main queue instead.
 void launch_qhull(dim3 grid, hipStream_t s, const HullArgs& A);
 void launch_qhull_big(dim3 grid, hipStream_t s, const HullArgs& A);
+size_t qhull_lds_doubles();   // k_qhull's LDS block (k_qside sweeps rows in it)
 size_t qhull_worker_bytes(int hnp);
 // k_stale: the facet-0 pairs' loop-carried normals, then the carry out
 void launch_stale(hipStream_t s, float* planes, const double* qnrm, const int* list, const int* count, int cap,

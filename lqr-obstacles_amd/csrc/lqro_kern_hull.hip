@@ -45,6 +45,8 @@ void launch_qhull_big(dim3 grid, hipStream_t s, const HullArgs& A) {
   hipLaunchKernelGGL(k_qhull_big, grid, dim3(64), 0, s, A);
 }
 
+size_t qhull_lds_doubles() { return sizeof(Q3L) / 8; }
+
 size_t qhull_worker_bytes(int hnp) {
   const size_t a = qh_worker_bytes(hnp), b = q3_worker_bytes(hnp);
   return a > b ? a : b;

@@ -12,6 +12,7 @@
 
 #include "lqro_pair_launch.hpp"
 #include "lqro_hull.hpp"
+#include "lqro_qhull3.hpp"
 
 namespace lqro {
 
@@ -26,6 +27,25 @@ __global__ void __launch_bounds__(HULL_CTHREADS) k_side(HullArgs A, PairArgs P) 
   hull_body_mw<HULL_CWAVES>(A, M, L);
   __syncthreads();
   if (P.nrows > 0) pair_block<X, RECS, kRowLaunch>(P, reinterpret_cast<double*>(&M));
+}
+
+// k_qside: the side stream's k_qhull workers (the hot pairs' builds in
+// Qhull's order, 3 waves a CU), which turn into k_pair row workers once the
+// hull queue is drained: a CU whose build is done sweeps rows (finer row
+// units keep the 3-wave workers' last unit short) instead of idling until
+// the slowest build ends.  The pair tables and per-wave regions reuse the
+// build's LDS (the host checks the fit and sets P.max_waves).
+template <int X, bool RECS>
+__global__ void __launch_bounds__(192) k_qside(HullArgs A, PairArgs P) {
+  __shared__ Q3L L;
+  q3_body(A, L);
+  __syncthreads();
+  if (P.nrows > 0) pair_block<X, RECS, kRowLaunch>(P, reinterpret_cast<double*>(&L));
+}
+
+template <int X, bool R>
+void launch_qside_t(dim3 grid, hipStream_t s, const HullArgs& H, const PairArgs& P) {
+  hipLaunchKernelGGL((k_qside<X, R>), grid, dim3(192), 0, s, H, P);
 }
 
 template <int X, bool R>
@@ -54,5 +74,6 @@ template void launch_pair_t<LQRO_INST_X, (bool)LQRO_INST_RECS>(dim3, dim3, size_
 template void launch_side_t<LQRO_INST_X, (bool)LQRO_INST_RECS>(dim3, dim3, hipStream_t, const HullArgs&,
                                                                const PairArgs&);
 template bool pair_set_lds_t<LQRO_INST_X, (bool)LQRO_INST_RECS>(int);
+template void launch_qside_t<LQRO_INST_X, (bool)LQRO_INST_RECS>(dim3, hipStream_t, const HullArgs&, const PairArgs&);
 
 }  // namespace lqro

@@ -16,6 +16,9 @@ void launch_pair_t(dim3 grid, dim3 block, size_t lds, hipStream_t s, const PairA
 // k_side: hot hulls, then rows
 template <int X, bool R>
 void launch_side_t(dim3 grid, dim3 block, hipStream_t s, const HullArgs& H, const PairArgs& P);
+// k_qside: hot builds in Qhull's order, then rows
+template <int X, bool R>
+void launch_qside_t(dim3 grid, hipStream_t s, const HullArgs& H, const PairArgs& P);
 // dynamic LDS limit of the three k_pair launch kinds
 template <int X, bool R>
 bool pair_set_lds_t(int bytes);
@@ -28,6 +31,10 @@ extern template void launch_side_t<16, false>(dim3, dim3, hipStream_t, const Hul
 extern template void launch_side_t<16, true>(dim3, dim3, hipStream_t, const HullArgs&, const PairArgs&);
 extern template void launch_side_t<12, false>(dim3, dim3, hipStream_t, const HullArgs&, const PairArgs&);
 extern template void launch_side_t<12, true>(dim3, dim3, hipStream_t, const HullArgs&, const PairArgs&);
+extern template void launch_qside_t<16, false>(dim3, hipStream_t, const HullArgs&, const PairArgs&);
+extern template void launch_qside_t<16, true>(dim3, hipStream_t, const HullArgs&, const PairArgs&);
+extern template void launch_qside_t<12, false>(dim3, hipStream_t, const HullArgs&, const PairArgs&);
+extern template void launch_qside_t<12, true>(dim3, hipStream_t, const HullArgs&, const PairArgs&);
 extern template bool pair_set_lds_t<16, false>(int);
 extern template bool pair_set_lds_t<16, true>(int);
 extern template bool pair_set_lds_t<12, false>(int);

@@ -1381,6 +1381,7 @@ __device__ __forceinline__ bool qh_slot_normal(const float* planes, const double
   return !(q[0] == 0.0 && q[1] == 0.0 && q[2] == 0.0);
 }
 
+#ifdef LQRO_HULL_TU   // the kernels: defined once, in lqro_kern_hull.hip
 __global__ void __launch_bounds__(64) k_stale(float* planes, const double* qnrm, const int* list, const int* count,
                                               int cap, const double* x, int X, int npr, int row_begin,
                                               int row_stride, double* carry, lqro_pair_record* recs, long nslots) {
@@ -1521,5 +1522,7 @@ __global__ void __launch_bounds__(64) k_stale_rows(float* planes, const double* 
     }
   }
 }
+
+#endif  // LQRO_HULL_TU
 
 }  // namespace lqro

@@ -38,7 +38,7 @@ namespace lqro {
 #define Q3_NEWCAP 128     // new facets of one insertion (more: the pair goes to k_qhull_big)
 #endif
 #ifndef Q3_VISCAP
-#define Q3_VISCAP 128     // visible facets of one insertion (-DQ3_VISCAP=192: scripts/build_variant.sh)
+#define Q3_VISCAP 192     // visible facets of one insertion (the crowded 30 m swarm's widest: 166)
 #endif
 #define Q3_MOVCAP 16      // old facets moved / receiving points in one partition
 #define Q3_HZCAP 24       // facets one point's horizon walk visits
@@ -46,13 +46,13 @@ namespace lqro {
 #define Q3_FSTK 512       // free facet slots kept for reuse (more are left unused)
 #define Q3_ND (Q3_NEWCAP + Q3_MOVCAP)
 #ifndef Q3_FL
-#define Q3_FL 2304        // facet slots with their hot fields in LDS
+#define Q3_FL 2240        // facet slots with their hot fields in LDS (the rest of 160 KB)
+#endif
 #define Q3_PROF_RETRY (32 + 2 * 4096 + 16)   // profile words: builds handed to k_qhull_big (16)
 #ifdef LQRO_QHULL_PROFILE
 #define Q3_CAPBIT(b) (b)   // which cap sent a build to k_qhull_big (scripts/qhull_prof.py)
 #else
 #define Q3_CAPBIT(b) 0
-#endif
 #endif
 
 struct Q3G {              // a facet slot >= Q3_FL, 64 B
@@ -200,6 +200,11 @@ struct Q3L {
   double c_dist[8];                  // MINvisible, MAXcoplanar, DISTround, MINdenom, MINdenom_2, NEARzero[3]
   double c_interior[3];
   int ph, sp_done, sp_ok, sp_facet, sp_furthest, sp_pos, sp_nvis, sp_nnew, sp_status, sp_sharp;
+  // sp_done releases the speculation's LDS results only; sp_gdone, stored
+  // right after with a full release, its global stores too (the vertex
+  // records): wave 0 waits for it only where it reads them (its own cone,
+  // the selection)
+  int sp_gdone;
   unsigned sp_key;
   int pub_qhead, pub_qtail;
   int pub_adopt, pub_nnew;           // the published cone was wave 1's: it writes the vertex records
@@ -214,7 +219,8 @@ struct Q3L {
   int hq_findbestnew, hq_notsharp, hq_nnew, hq_nmov, hq_nvis;
   double hq_max_outside;
 #ifdef LQRO_QHULL_PROFILE
-  unsigned long long pub_t, done_t;   // the last publication / speculation end (handshake latencies)
+  unsigned long long pub_t, done_t, done_t2;   // the last publication / speculation end, after its store
+  unsigned long long pub_r, start_r, done_r;    // the same on the 100 MHz real-time clock (one clock for all waves)
 #endif
 };
 static_assert(sizeof(Q3L) <= 160 * 1024, "k_qhull's LDS exceeds a CU");
@@ -233,6 +239,10 @@ struct Q3S {
   unsigned long long tw, nw;     // LQRO_QHULL_PROFILE: waiting for wave 1's speculation
   unsigned long long tdl;        // LQRO_QHULL_PROFILE: its end until wave 0 sees it
   unsigned long long tw1, nw1;   // LQRO_QHULL_PROFILE: the waits after one-chunk insertions
+  unsigned long long tse, tsn;   // LQRO_QHULL_PROFILE: publication -> speculation end, -> wave 0 past the wait
+  unsigned long long tfr, nsp;   // LQRO_QHULL_PROFILE: the wait's first read, its spins
+  unsigned long long tfr2, trel;
+  unsigned long long r_start, r_done, r_seen, r_gseen;
   int prev1;
   unsigned long long tps[24], nps;   // LQRO_QHULL_PROFILE: phases of the one-chunk insertions
 };
@@ -742,6 +752,12 @@ __device__ __forceinline__ int q3_ld_acq(const int* p) {
 __device__ __forceinline__ void q3_st_rel(int* p, int v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+// a release of this wave's LDS writes only: no wait for its global stores
+// (a workgroup-scope release waits until every one of them is acknowledged)
+__device__ __forceinline__ void q3_st_rel_lds(int* p, int v) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 // wait (bounded) until *p != v (ne) or == v (!ne); the last value read
 __device__ __forceinline__ int q3_wait(const int* p, int v, bool ne) {
   int x = q3_ld_acq(p);
@@ -1174,12 +1190,6 @@ struct Q3QC {
   double r[6];
 };
 
-// a vertex record's two cache lines requested (the value only feeds an empty
-// asm at the speculation's end, so the load is issued but not waited for)
-__device__ __forceinline__ unsigned q3_touch(const Q3V& v) {
-  return *reinterpret_cast<const unsigned*>(v.p) ^ *reinterpret_cast<const unsigned*>(v.id);
-}
-
 __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep, unsigned ep2, Q3QC& Q, Q3P& P,
                                int phase) {
   const unsigned long long ltmask = (1ull << lane) - 1ull;
@@ -1267,11 +1277,9 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
     qh = Q.qcb + Q.qcn;
   }
   int ls = 0, nvis = 0, nnew = 0, ts = 0, lm = 0;
-  unsigned touch = 0u;
   W1T(2);
   if (facet >= 0) {
     // 2. qh_findhorizon, as wave 0's (level order, first occurrence), visits as epochs
-    touch += q3_touch(W.vv[facet]);
     if (lane == 0) L.sp_visf[0] = facet;
     if (lane < 3) L.sp_cand[lane] = (unsigned short)q3_nb(W, L, facet, lane);
     mark(facet);
@@ -1303,10 +1311,6 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
           dup |= (l < lane) && __builtin_amdgcn_readlane(nb, l) == nb;
         }
         vis = vis && !dup;
-        // the cone reads the vertex records of the horizon facets (and the
-        // visible ones' ids): their lines are requested now, under the rest
-        // of the search (consumed only at the end of the speculation)
-        if (c < ncand && (vis || (cand && !vis))) touch += q3_touch(W.vv[nb]);
         const unsigned long long bv = __ballot(vis);
         if (vis) {
           const int at = nvis + __popcll(bv & ltmask);
@@ -1496,7 +1500,6 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
   }
   const int st = qh_wave_or(ls | ts | lm);
   W1T(5);
-  asm volatile("" ::"v"(touch));   // (the requested lines: waited for only here)
   hl_sync();
   if (lane == 0) {
     L.sp_ok = ok;
@@ -1889,14 +1892,32 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
 #ifdef LQRO_QHULL_PROFILE
       const unsigned long long tw_ = __builtin_amdgcn_s_memtime();
 #endif
+#ifdef LQRO_QHULL_PROFILE
+      int spins_ = 0;
+      int dn = q3_ld_acq(&L.sp_done);
+      const unsigned long long tf_ = __builtin_amdgcn_s_memtime();   // the first read back
+      for (long w = 0; dn != phase && w < (1l << 24); ++w) {
+        __builtin_amdgcn_s_sleep(1);
+        dn = q3_ld_acq(&L.sp_done);
+        ++spins_;
+      }
+      if (S.prev1) { S.tfr += tf_ - tw_; S.nsp += (unsigned long long)spins_; }
+#else
       const int dn = q3_wait(&L.sp_done, phase, false);
+#endif
 #ifdef LQRO_QHULL_PROFILE
       {
         const unsigned long long tn_ = __builtin_amdgcn_s_memtime();
         S.tw += tn_ - tw_;
         S.nw += 1;
         if (tn_ - tw_ > 200) S.tdl += tn_ - L.done_t;   // (waited) speculation end -> seen here
-        if (S.prev1) { S.tw1 += tn_ - tw_; S.nw1 += 1; }   // after a one-chunk insertion
+        if (S.prev1) {   // after a one-chunk insertion: its wait, publication -> speculation end / -> seen
+          S.tw1 += tn_ - tw_; S.nw1 += 1;
+          S.tse += L.done_t - L.pub_t; S.tsn += tn_ - L.pub_t;
+          S.tfr2 += L.done_t2 - L.pub_t;
+          const unsigned long long nr_ = __builtin_amdgcn_s_memrealtime();
+          S.r_start += L.start_r - L.pub_r; S.r_done += L.done_r - L.pub_r; S.r_seen += nr_ - L.pub_r;
+        }
       }
 #endif
       if (dn != phase) {   // wave 1 still speculating (it writes vertex records from L.nslot): stop
@@ -1962,7 +1983,11 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
 #ifdef LQRO_QHULL_PROFILE
     const unsigned long long tins_ = S.tq;   // this insertion's start (for the long-sequence split)
 #endif
-    if (furthest < 0) break;
+    if (furthest < 0) {
+      // the build is done: the selection reads vertex records wave 1 wrote
+      if (phase > 0 && q3_wait(&L.sp_gdone, phase, false) != phase) S.status |= QHS_CAPACITY | QHS_TIMEOUT;
+      break;
+    }
     int nvis = 0, nnew = 0, ts = 0, lm = 0, my_t = -1;
     bool one = false;
     const double* ncb = W.ncoord;
@@ -2039,6 +2064,11 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
       hl_sync();
       Q3T(2);   // (profile: the adopted cone's copy)
     } else {
+    // this cone reads vertex records, some of which wave 1 wrote
+    if (phase > 0 && q3_wait(&L.sp_gdone, phase, false) != phase) {
+      S.status |= QHS_CAPACITY | QHS_TIMEOUT;
+      return;
+    }
     // qh_findhorizon, a level of the breadth-first search at a time: the
     // candidates of a level in (visible facet, neighbour) order, a facet
     // taken at its first occurrence
@@ -2276,9 +2306,12 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     }
     ++phase;
 #ifdef LQRO_QHULL_PROFILE
-    if (lane == 0) L.pub_t = __builtin_amdgcn_s_memtime();
+    if (lane == 0) { L.pub_t = __builtin_amdgcn_s_memtime(); L.pub_r = __builtin_amdgcn_s_memrealtime(); }
 #endif
     if (lane == 0) q3_st_rel(&L.ph, phase);
+#ifdef LQRO_QHULL_PROFILE
+    if (lane == 0) S.trel += __builtin_amdgcn_s_memtime() - L.pub_t;   // the release's own cost
+#endif
     S.findbestnew = 0;
     S.notsharp = 0;
     S.nmov = 0;
@@ -2510,7 +2543,7 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
     if (slot < 0) break;
     // a fresh handshake and wave 1's epochs for this job (ordered by
     // hull_points' barriers)
-    if (threadIdx.x == 0) { L.ph = 0; L.sp_done = 0; L.hstate = 0; L.sp_hz = 0; L.pf_done = 0; }
+    if (threadIdx.x == 0) { L.ph = 0; L.sp_done = 0; L.sp_gdone = 0; L.hstate = 0; L.sp_hz = 0; L.pf_done = 0; }
     for (int q = threadIdx.x; q < Q3_FL / 2; q += blockDim.x) reinterpret_cast<unsigned*>(L.mark)[q] = 0u;
     const int lrow = slot / A.npr, jj = A.nbr_list ? A.nbr_list[slot] : slot % A.npr;
     const int i = A.row_begin + lrow * A.row_stride;
@@ -2561,14 +2594,17 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
           const unsigned long long t0_ = __builtin_amdgcn_s_memtime();
           P.tq = t0_;
           P.t[14] += t0_ - L.pub_t;   // publication -> speculation start
+          if (lane == 0) L.start_r = __builtin_amdgcn_s_memrealtime();
 #endif
           q3_spec(W, L, lane, ep, ep2, Q, P, p);
           hl_sync();
 #ifdef LQRO_QHULL_PROFILE
           if (lane == 0) L.done_t = __builtin_amdgcn_s_memtime();
 #endif
-          if (lane == 0) q3_st_rel(&L.sp_done, p);
+          if (lane == 0) q3_st_rel_lds(&L.sp_done, p);
+          if (lane == 0) q3_st_rel(&L.sp_gdone, p);
 #ifdef LQRO_QHULL_PROFILE
+          if (lane == 0) { L.done_t2 = __builtin_amdgcn_s_memtime(); L.done_r = __builtin_amdgcn_s_memrealtime(); }
           P.t[0] += __builtin_amdgcn_s_memtime() - t0_;
           P.t[7] += 1;
 #endif
@@ -2584,7 +2620,7 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
 #endif
             q3_serve_chunk(W, L, lane);
             hl_sync();
-            if (lane == 0) q3_st_rel(&L.hstate, hs + 2);
+            if (lane == 0) q3_st_rel_lds(&L.hstate, hs + 2);   // (the results are in LDS)
 #ifdef LQRO_QHULL_PROFILE
             P.t[6] += __builtin_amdgcn_s_memtime() - t0_;
             P.t[8] += 1;
@@ -2608,6 +2644,11 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
     S.tw = S.nw = 0;
     S.tdl = 0;
     S.tw1 = S.nw1 = 0;
+    S.tse = S.tsn = 0;
+    S.tfr = S.nsp = 0;
+    S.tfr2 = 0;
+    S.trel = 0;
+    S.r_start = S.r_done = S.r_seen = S.r_gseen = 0;
     S.prev1 = 0;
     for (int k = 0; k < 24; k++) S.tps[k] = 0;
     S.nps = 0;
@@ -2654,6 +2695,16 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
       atomicAdd(&A.prof[Q3_PROF_W1 + 41], S.tdl);
       atomicAdd(&A.prof[Q3_PROF_W1 + 42], S.tw1);
       atomicAdd(&A.prof[Q3_PROF_W1 + 43], S.nw1);
+      atomicAdd(&A.prof[Q3_PROF_W1 + 44], S.tse);
+      atomicAdd(&A.prof[Q3_PROF_W1 + 45], S.tsn);
+      atomicAdd(&A.prof[Q3_PROF_W1 + 46], S.tfr);
+      atomicAdd(&A.prof[Q3_PROF_W1 + 47], S.nsp);
+      atomicAdd(&A.prof[Q3_PROF_W1 + 48], S.tfr2);
+      atomicAdd(&A.prof[Q3_PROF_W1 + 49], S.trel);
+      atomicAdd(&A.prof[Q3_PROF_W1 + 50], S.r_start);
+      atomicAdd(&A.prof[Q3_PROF_W1 + 51], S.r_done);
+      atomicAdd(&A.prof[Q3_PROF_W1 + 52], S.r_seen);
+      atomicAdd(&A.prof[Q3_PROF_W1 + 53], S.r_gseen);
       atomicMax(&A.prof[26], S.tph[27]);
       // per job (words 32 + 2j): cycles; insertions | points << 20 | facet slots << 40
       const unsigned long long j = atomicAdd(&A.prof[11], 1ull);

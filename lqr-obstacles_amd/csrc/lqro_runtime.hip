@@ -67,6 +67,17 @@ static void launch_side(int x_dim, dim3 grid, dim3 block, hipStream_t s, const H
   }
 }
 
+static void launch_qside(int x_dim, dim3 grid, hipStream_t s, const HullArgs& H, const PairArgs& P) {
+  const bool r = P.recs != nullptr;
+  if (x_dim == 16) {
+    if (r) launch_qside_t<16, true>(grid, s, H, P);
+    else launch_qside_t<16, false>(grid, s, H, P);
+  } else {
+    if (r) launch_qside_t<12, true>(grid, s, H, P);
+    else launch_qside_t<12, false>(grid, s, H, P);
+  }
+}
+
 #define LQRO_MAXX 16
 constexpr size_t kHullLdsMaxHNP = (size_t)(1 << 19) / HULL_SBMULT;   // 21,845 (C5: H*NP = 20,000)
 
@@ -419,6 +430,7 @@ struct lqro_ctx {
   // (lqro_hull.hpp hull_row_done)
   int early_lp;
   int early_step;            // the step being enqueued runs the early LP
+  int qside;                 // LQRO_QSIDE (default 1): k_qhull side workers sweep rows after their builds
   int* d_rowpend;
   int* d_rowclaim;
   PairArgs pa;
@@ -629,6 +641,8 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
     c->hot_max_inside = hm ? atol(hm) : -1L;
     const char* el = getenv("LQRO_EARLY_LP");
     c->early_lp = el ? atoi(el) != 0 : 1;
+    const char* qs = getenv("LQRO_QSIDE");
+    c->qside = qs ? atoi(qs) != 0 : 1;
   }
   c->rb = g.row_begin;
   c->re = (g.row_end > g.row_begin) ? g.row_end : g.n_agents;
@@ -885,6 +899,14 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
                    (lhull || (lds_ok && (size_t)g.horizon * g.n_points <= 16383 && side_waves >= 1));
   const int nwait = hot ? side : 0;
   P.row_split = std::max(1, std::min(16, (2 * c->n_cu + c->nrows - 1) / c->nrows));
+  // Qhull order: the side's k_qhull workers sweep rows in their build's LDS
+  // once the hot builds are taken (k_qside, 3 waves a CU): rows in units of
+  // ~128 pairs, so a 3-wave worker's last unit ends soon after the 16-wave
+  // workgroups' (shared gains: the tables are staged once per workgroup)
+  const long qside_room = (long)qhull_lds_doubles() - P.lds_wave;
+  const int qside_waves = qside_room > 0 ? (int)std::min<long>(3, qside_room / P.wave_doubles) : 0;
+  const bool qside = hot && c->qside && c->qhull_order && !c->qhull_big && qside_waves >= 1;
+  if (qside && !c->per_agent) P.row_split = std::max(P.row_split, std::min(16, std::max(1, npr / 128)));
   // early LP (Qhull order, beside the hulls): a row whose planes are all
   // final runs its LP at once — in a k_lp_lds after the main sweep, or in the
   // k_qhull job that completes it (lqro_hull.hpp hull_row_done) — and the
@@ -970,13 +992,21 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
     if (c->qhull_order) {
       // the hot pairs' hulls in Qhull's order (k_qhull leaves when the queue
       // is empty), then the row sweep
-      if (!c->qhull_big) {
-        launch_qhull(dim3(std::min(nwait, c->qworkers)), c->side, Hh);
+      if (qside) {
+        PairArgs Pq = P;
+        Pq.max_waves = qside_waves;
+        if (nside == 0) Pq.nrows = 0;
+        launch_qside(g.x_dim, dim3(std::min(nwait, c->qworkers)), c->side, Hh, Pq);
         HIPCHK(hipGetLastError());
-      }
-      if (nside > 0) {
-        launch_pair(g.x_dim, dim3(nwait), dim3(P.waves * 64), c->lds_bytes, c->side, P);
-        HIPCHK(hipGetLastError());
+      } else {
+        if (!c->qhull_big) {
+          launch_qhull(dim3(std::min(nwait, c->qworkers)), c->side, Hh);
+          HIPCHK(hipGetLastError());
+        }
+        if (nside > 0) {
+          launch_pair(g.x_dim, dim3(nwait), dim3(P.waves * 64), c->lds_bytes, c->side, P);
+          HIPCHK(hipGetLastError());
+        }
       }
     } else if (c->local_hull) {
       // the hot pairs' local hulls (k_lhull leaves when the queue is empty:

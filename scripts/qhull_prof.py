@@ -75,6 +75,13 @@ if w1[7]:
           " (when it waited); waits after one-chunk insertions %.3f us each (%d)" %
           (w1[14] / max(w1[7], 1) / GHZ / 1e3, w1[41] / jobs / GHZ / 1e6, w1[42] / max(w1[43], 1) / GHZ / 1e3,
            w1[43] // jobs))
+    print("after one-chunk insertions: publication -> speculation end %.3f us, -> wave 0 past its wait %.3f us" %
+          (w1[44] / max(w1[43], 1) / GHZ / 1e3, w1[45] / max(w1[43], 1) / GHZ / 1e3))
+    print("  the wait's first read back %.3f us, spins %.2f; publication -> after wave 1's store %.3f us" %
+          (w1[46] / max(w1[43], 1) / GHZ / 1e3, w1[47] / max(w1[43], 1), w1[48] / max(w1[43], 1) / GHZ / 1e3))
+    print("  wave 0's publication release %.3f us each (all insertions)" % (w1[49] / max(w1[10], 1) / GHZ / 1e3))
+    print("  real-time clock (100 MHz), after one-chunk insertions: publication -> spec start %.3f us, -> spec end %.3f us,"
+          " -> wave 0 sees it %.3f us (global copy %.3f)" % tuple(w1[k] / max(w1[43], 1) / 100.0 for k in (50, 51, 52, 53)))
     print("wave 1: chunks served", w1[8] / jobs, "per hull,", w1[6] / max(w1[8], 1) / GHZ / 1e3, "us each")
     print("wave 0 waiting for a speculation: %.3f ms/hull, %.2f us per wait (%d waits/hull)" %
           (w1[9] / jobs / GHZ / 1e6, w1[9] / max(w1[10], 1) / GHZ / 1e3, w1[10] // jobs))

@@ -97,9 +97,11 @@ def test_k_qhull_caps_and_the_wide_insertion(oracle, lqro_mod, gains):
     """k_qhull's per-insertion caps (csrc/lqro_qhull3.hpp) against the widest
     insertion of the crowded 30 m swarm (scripts/qhull_caps.py over its 421
     inside-hull pairs, oracle build statistics): pair (1018, 516) has one
-    insertion with 166 visible and 116 new facets, beyond Q3_VISCAP, so its
-    build goes to k_qhull_big (measured: 70 ms of the 30 m step's 108 ms hull
-    phase, profiles/r3h_crowded30_plain_trace.txt); every other cap holds."""
+    insertion with 166 visible and 116 new facets.  Round 3's Q3_VISCAP of 128
+    sent that build to k_qhull_big (70 ms of the 30 m step's 108 ms hull
+    phase, profiles/r3h_crowded30_plain_trace.txt); Q3_VISCAP = 192 (the LDS
+    facet slots cut to 2,240 to make room) keeps it in k_qhull: every cap
+    holds."""
     import re
     src = open(os.path.join(os.path.dirname(__file__), "..", "lqr-obstacles_amd", "csrc", "lqro_qhull3.hpp")).read()
     cap = {k: int(re.search(rf"#define Q3_{k} (\d+)", src).group(1)) for k in ("VISCAP", "NEWCAP", "HZCAP", "COPCAP")}
@@ -109,5 +111,5 @@ def test_k_qhull_caps_and_the_wide_insertion(oracle, lqro_mod, gains):
     oracle.qhull(pts)
     st = oracle.last_qhull_stats
     assert st["st_visible_max"] == 166 and st["st_new_max"] == 116, st
-    assert st["st_visible_max"] > cap["VISCAP"] and st["st_new_max"] <= cap["NEWCAP"]
+    assert st["st_visible_max"] <= cap["VISCAP"] and st["st_new_max"] <= cap["NEWCAP"]
     assert st["st_horizon_max"] <= cap["HZCAP"] and st["st_cop_max"] <= cap["COPCAP"]
