@@ -19,6 +19,12 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/prof_fe
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/prof_write -o run -- $B > $O/prof_write.log 2>&1
 python3 scripts/pmc_traffic.py $O/prof_fetch $O/prof_write $O/${TAG}_pmc_traffic.json > /dev/null
 cp $O/${TAG}_pmc_traffic.json profiles/${TAG}_pmc_traffic.json
+# k_qhull's own traffic: with LQRO_QSIDE=0 the side builds run as k_qhull
+# launches (not inside k_qside, whose count mixes the builds with its rows)
+LQRO_QSIDE=0 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/prof_fetch_q -o run -- $B > $O/prof_fetch_q.log 2>&1
+LQRO_QSIDE=0 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/prof_write_q -o run -- $B > $O/prof_write_q.log 2>&1
+python3 scripts/pmc_traffic.py $O/prof_fetch_q $O/prof_write_q $O/${TAG}_pmc_traffic_qhull.json > /dev/null
+cp $O/${TAG}_pmc_traffic_qhull.json profiles/${TAG}_pmc_traffic_qhull.json
 timeout -k 10 300 python bench.py > $O/${TAG}_bench.json 2> $O/${TAG}_bench.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_kt -o run -- $B > $O/prof_kt.log 2>&1
 python3 scripts/kernel_breakdown.py $O/prof_kt $O/${TAG}_kernel_breakdown.json > /dev/null
