@@ -276,6 +276,7 @@ LQRO_HD void keyframe(float* out, double time, const Mat<kX, 1>& xtrue, const Ma
 template <int R, int C>
 LQRO_HD Mat<R, C> get(const double* p) {
   Mat<R, C> m;
+#pragma unroll
   for (int i = 0; i < R * C; ++i) m.e[i] = p[i];
   return m;
 }

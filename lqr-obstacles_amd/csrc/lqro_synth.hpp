@@ -221,12 +221,12 @@ LQRO_HD Mat<N, C> solve_sm(const Mat<N, N>& p, const Mat<N, C>& q) {
 #pragma unroll
   for (int l = 0; l < N; ++l)
 #pragma unroll
-    for (int r = 0; r < N; ++r)
-      if (rp[l] == r) {
-        irp[r] = l;
+    for (int r = 0; r < N; ++r) {   // (selects, not branches: the arrays stay in registers)
+      const bool hit = rp[l] == r;
+      irp[r] = hit ? l : irp[r];
 #pragma unroll
-        for (int j = 0; j < C; ++j) Y[r][j] = X[l][j];
-      }
+      for (int j = 0; j < C; ++j) Y[r][j] = hit ? X[l][j] : Y[r][j];
+    }
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     const int a = cp[i], b = rp[i];
@@ -631,6 +631,7 @@ LQRO_HD Mat<X, 1> dynamics(const Quad& q, const Mat<X, 1>& x, const Mat<3, 3>& R
 template <int R, int C>
 LQRO_HD void put(double* out, const Mat<R, C>& m) {
   if (out)
+#pragma unroll
     for (int i = 0; i < R * C; ++i) out[i] = m.e[i];
 }
 
