@@ -370,8 +370,9 @@ def main():
                     help="swarm size (default: round(1024 sqrt(world)), C3's pairs per GPU)")
     ap.add_argument("--no-roofline-probe", action="store_true")
     ap.add_argument("--no-configs", action="store_true", help="skip the C4 / C5 strong-scaling runs")
-    ap.add_argument("--rows", choices=("block", "cyclic"), default=os.environ.get("LQRO_ROWS", "block"),
-                    help="row sharding over ranks: contiguous blocks or cyclic (row_stride = world)")
+    ap.add_argument("--rows", choices=("auto", "block", "cyclic"), default=os.environ.get("LQRO_ROWS", "auto"),
+                    help="row sharding over ranks: contiguous blocks, cyclic (row_stride = world), or auto: "
+                         "blocks unless the warm-up steps' inside-hull pairs per rank differ by more than 10 %%")
     ap.add_argument("--hull-rule", choices=("qhull", "canonical"), default=os.environ.get("LQRO_HULL_RULE", "qhull"),
                     help="inside-hull rule: the reference's (Qhull's build order, default) or the canonical one")
     ap.add_argument("--host", choices=("python", "cpp"), default=os.environ.get("LQRO_BENCH_HOST", "python"),
@@ -404,27 +405,56 @@ def main():
     torch.cuda.set_device(dev)
 
     N = args.agents if args.agents > 0 else int(round(N_AGENTS * world ** 0.5))
-    sh = lqro.shard_rows(N, rank, world, args.rows)
-    rows = len(lqro.shard_row_ids(N, rank, world, args.rows))
     x, vg = lqro.synthetic_swarm(N)
     gains = lqro.synthesize_gains()
     flags = hull_flags(lqro, args.hull_rule)
-    ctx = lqro.Context(lqro.config(N, HORIZON, N_POINTS, device=local, flags=flags, **sh))
-    ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
     d_x = torch.from_numpy(x).to(dev)
     d_vg = torch.from_numpy(vg).to(dev)
     d_newv = torch.zeros((N, 3), dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream(dev)
-
     rowtab = torch.zeros((N, 4), dtype=torch.float64, device=dev)
+
+    def make_ctx(mode):
+        c = lqro.Context(lqro.config(N, HORIZON, N_POINTS, device=local, flags=flags,
+                                     **lqro.shard_rows(N, rank, world, mode)))
+        c.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
+        return c
+
+    # row sharding: an inside-hull pair costs ~50x a plain one and follows the
+    # swarm's geometry, so "auto" keeps contiguous blocks unless the warm-up
+    # steps show one rank holding > 10 % more of them than the mean (then
+    # cyclic rows spread them)
+    mode = "block" if args.rows == "auto" else args.rows
+    ctx = make_ctx(mode)
+    rows_auto = None
 
     def step():
         # (Qhull order, world > 1: split around the row-normal all-gather)
-        lqro.step_rows(ctx, dist, d_x, d_vg, d_newv, rowtab, rank, world, args.rows, stream)
+        lqro.step_rows(ctx, dist, d_x, d_vg, d_newv, rowtab, rank, world, mode, stream)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    if args.rows == "auto" and world > 1:
+        mine = float(ctx.stats()["inside"])
+        cmax = torch.tensor([mine], dtype=torch.float64, device=dev)
+        csum = torch.tensor([mine], dtype=torch.float64, device=dev)
+        dist.all_reduce(cmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(csum)
+        mean = float(csum.item()) / world
+        imb = float(cmax.item()) / mean if mean > 0 else 1.0
+        rows_auto = {"block_inside_max_rank": float(cmax.item()), "block_inside_mean": mean, "imbalance": imb,
+                     "chose": "cyclic" if imb > 1.10 else "block"}
+        if imb > 1.10:
+            ctx.close()
+            mode = "cyclic"
+            ctx = make_ctx(mode)
+            for _ in range(max(1, args.warmup)):
+                step()
+            torch.cuda.synchronize(dev)
+    args.rows = mode
+    sh = lqro.shard_rows(N, rank, world, mode)
+    rows = len(lqro.shard_row_ids(N, rank, world, mode))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -512,6 +542,7 @@ def main():
                         + ("" if args.hull_rule == "qhull" else " (canonical hull rule)"),
             "n_agents": N, "horizon": HORIZON, "n_points": N_POINTS, "x_dim": X_DIM,
             "pairs_per_step": pairs_step,
+            "rows_auto": rows_auto,
             "parallelism": f"rows sharded ({args.rows}) over {world} rank(s)" +
                            ((" + RCCL all-gather of newV" if backend == "nccl" else f" + {backend} all-gather of newV")
                             if world > 1 else ""),
