@@ -243,6 +243,7 @@ struct Q3S {
   unsigned long long tfr, nsp;   // LQRO_QHULL_PROFILE: the wait's first read, its spins
   unsigned long long tfr2, trel;
   unsigned long long r_start, r_done, r_seen, r_gseen;
+  unsigned long long tseen, tpre, npre, tstart;
   int prev1;
   unsigned long long tps[24], nps;   // LQRO_QHULL_PROFILE: phases of the one-chunk insertions
 };
@@ -264,6 +265,7 @@ struct Q3S {
 // step's hulls (lqro_debug_prof_words)
 #define Q3_PROF_W1 (32 + 2 * 4096 + 48 + 4 * 4096)
 struct Q3P {
+  unsigned long long tq2 = 0;   // LQRO_QHULL_PROFILE: the last speculation's end (this wave's clock)
   unsigned long long t[16];
   unsigned long long tq;
 };
@@ -1911,6 +1913,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
         S.tw += tn_ - tw_;
         S.nw += 1;
         if (tn_ - tw_ > 200) S.tdl += tn_ - L.done_t;   // (waited) speculation end -> seen here
+        S.tseen = tn_;
         if (S.prev1) {   // after a one-chunk insertion: its wait, publication -> speculation end / -> seen
           S.tw1 += tn_ - tw_; S.nw1 += 1;
           S.tse += L.done_t - L.pub_t; S.tsn += tn_ - L.pub_t;
@@ -2307,6 +2310,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     ++phase;
 #ifdef LQRO_QHULL_PROFILE
     if (lane == 0) { L.pub_t = __builtin_amdgcn_s_memtime(); L.pub_r = __builtin_amdgcn_s_memrealtime(); }
+    if (S.tseen) { S.tpre += __builtin_amdgcn_s_memtime() - S.tseen; S.npre += 1; }   // (this wave's clock) seen -> publication
 #endif
     if (lane == 0) q3_st_rel(&L.ph, phase);
 #ifdef LQRO_QHULL_PROFILE
@@ -2594,6 +2598,7 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
           const unsigned long long t0_ = __builtin_amdgcn_s_memtime();
           P.tq = t0_;
           P.t[14] += t0_ - L.pub_t;   // publication -> speculation start
+          if (P.tq2) P.t[15] += t0_ - P.tq2;   // (this wave's clock) its last speculation's end -> this start
           if (lane == 0) L.start_r = __builtin_amdgcn_s_memrealtime();
 #endif
           q3_spec(W, L, lane, ep, ep2, Q, P, p);
@@ -2605,6 +2610,7 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
           if (lane == 0) q3_st_rel(&L.sp_gdone, p);
 #ifdef LQRO_QHULL_PROFILE
           if (lane == 0) { L.done_t2 = __builtin_amdgcn_s_memtime(); L.done_r = __builtin_amdgcn_s_memrealtime(); }
+          P.tq2 = __builtin_amdgcn_s_memtime();
           P.t[0] += __builtin_amdgcn_s_memtime() - t0_;
           P.t[7] += 1;
 #endif
@@ -2649,6 +2655,7 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
     S.tfr2 = 0;
     S.trel = 0;
     S.r_start = S.r_done = S.r_seen = S.r_gseen = 0;
+    S.tseen = S.tpre = S.npre = S.tstart = 0;
     S.prev1 = 0;
     for (int k = 0; k < 24; k++) S.tps[k] = 0;
     S.nps = 0;
@@ -2705,6 +2712,9 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
       atomicAdd(&A.prof[Q3_PROF_W1 + 51], S.r_done);
       atomicAdd(&A.prof[Q3_PROF_W1 + 52], S.r_seen);
       atomicAdd(&A.prof[Q3_PROF_W1 + 53], S.r_gseen);
+      atomicAdd(&A.prof[Q3_PROF_W1 + 54], S.tpre);
+      atomicAdd(&A.prof[Q3_PROF_W1 + 55], S.npre);
+      atomicAdd(&A.prof[Q3_PROF_W1 + 56], S.tstart);
       atomicMax(&A.prof[26], S.tph[27]);
       // per job (words 32 + 2j): cycles; insertions | points << 20 | facet slots << 40
       const unsigned long long j = atomicAdd(&A.prof[11], 1ull);

@@ -82,6 +82,9 @@ if w1[7]:
     print("  wave 0's publication release %.3f us each (all insertions)" % (w1[49] / max(w1[10], 1) / GHZ / 1e3))
     print("  real-time clock (100 MHz), after one-chunk insertions: publication -> spec start %.3f us, -> spec end %.3f us,"
           " -> wave 0 sees it %.3f us (global copy %.3f)" % tuple(w1[k] / max(w1[43], 1) / 100.0 for k in (50, 51, 52, 53)))
+    print("  each wave's own clock: wave 1 idle between speculations %.3f us; wave 0 from seeing one to the next publication %.3f us"
+          % (w1[15] / max(w1[7], 1) / GHZ / 1e3, w1[54] / max(w1[55], 1) / GHZ / 1e3))
+    print("  (STARTSIG builds) wave 0 sees wave 1 start %.3f us after publishing" % (w1[56] / max(w1[55], 1) / GHZ / 1e3))
     print("wave 1: chunks served", w1[8] / jobs, "per hull,", w1[6] / max(w1[8], 1) / GHZ / 1e3, "us each")
     print("wave 0 waiting for a speculation: %.3f ms/hull, %.2f us per wait (%d waits/hull)" %
           (w1[9] / jobs / GHZ / 1e6, w1[9] / max(w1[10], 1) / GHZ / 1e3, w1[10] // jobs))
