@@ -430,7 +430,7 @@ struct lqro_ctx {
   // (lqro_hull.hpp hull_row_done)
   int early_lp;
   int early_step;            // the step being enqueued runs the early LP
-  int qside;                 // LQRO_QSIDE (default 1): k_qhull side workers sweep rows after their builds
+  int qside;                 // LQRO_QSIDE=1: k_qhull side workers sweep rows after their builds (default off)
   int* d_rowpend;
   int* d_rowclaim;
   PairArgs pa;
@@ -641,8 +641,11 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
     c->hot_max_inside = hm ? atol(hm) : -1L;
     const char* el = getenv("LQRO_EARLY_LP");
     c->early_lp = el ? atoi(el) != 0 : 1;
+    // off by default: with 3 waves a CU the side workers sweep rows at ~1/5 of a
+    // 16-wave workgroup's rate, so where the sweep outlasts the builds (C4:
+    // 227 vs 114 ms per step) it loses; at C3 it ties (22.0 ms either way)
     const char* qs = getenv("LQRO_QSIDE");
-    c->qside = qs ? atoi(qs) != 0 : 1;
+    c->qside = qs ? atoi(qs) != 0 : 0;
   }
   c->rb = g.row_begin;
   c->re = (g.row_end > g.row_begin) ? g.row_end : g.n_agents;
