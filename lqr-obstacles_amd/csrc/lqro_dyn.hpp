@@ -145,7 +145,9 @@ LQRO_HD Mat<kZ, kX> jac_hx(const Quad& q, const Mat<kX, 1>& x) {
 }
 
 // R = R*exp([x_6:9]); x_6:9 = 0 (the rotation-error reset, LQRO:483-485)
-LQRO_HD void reset_rot(Mat<kX, 1>& x, Mat<3, 3>& R) {
+// (always inlined: as a call, k_dynw kept its live registers in scratch
+// around each of the three resets)
+__host__ __device__ __forceinline__ void reset_rot(Mat<kX, 1>& x, Mat<3, 3>& R) {
   Vec3 r;
   for (int k = 0; k < 3; ++k) r.e[k] = x.e[6 + k];
   R = R * expm(skew(r));

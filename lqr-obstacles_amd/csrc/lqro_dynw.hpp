@@ -226,7 +226,7 @@ __device__ __forceinline__ void expm(const double* q, double* out, double* w, in
 // the pivot scan in every lane, the rotation over lanes [0, N) (D) and
 // [N, 2N) (V)
 template <int N>
-__device__ void jacobi(const double* m, double* V, double* D, int lane) {
+__device__ __forceinline__ void jacobi(const double* m, double* V, double* D, int lane) {
   for (int e = lane; e < N * N; e += 64) {
     D[e] = m[e];
     V[e] = (e / N == e % N) ? 1.0 : 0.0;
@@ -286,7 +286,7 @@ __device__ void jacobi(const double* m, double* V, double* D, int lane) {
 // lanes: full-pivot Gauss-Jordan, the same pivots and per-element operation
 // order; m is overwritten with the inverse, inv is work space
 template <int N>
-__device__ void inverse(double* m, double* inv, int* ip, int lane) {
+__device__ __forceinline__ void inverse(double* m, double* inv, int* ip, int lane) {
   int* rp = ip;
   int* cp = ip + N;
   for (int e = lane; e < N * N; e += 64) inv[e] = (e / N == e % N) ? 1.0 : 0.0;
@@ -330,8 +330,8 @@ __device__ void inverse(double* m, double* inv, int* ip, int lane) {
 
 // A = exp(dt F), A2 = exp(dt/2 F), MM, dx as dyn::discretize; F from 32
 // lanes' f evaluations
-__device__ void discretize(const Quad& q, const Mat<kX, 1>& x, const Mat<3, 3>& R, const Mat<kU, 1>& u,
-                           double* w, int lane, Mat<kX, 1>& dx) {
+__device__ __forceinline__ void discretize(const Quad& q, const Mat<kX, 1>& x, const Mat<3, 3>& R,
+                                          const Mat<kU, 1>& u, double* w, int lane, Mat<kX, 1>& dx) {
   double* fr = w + oE0;   // rows 0..15 f(x + h e_i), 16..31 f(x - h e_i), 32 f(x)
   {
     Mat<kX, 1> xp;
@@ -392,7 +392,7 @@ __device__ void discretize(const Quad& q, const Mat<kX, 1>& x, const Mat<3, 3>& 
 }
 
 // sampleGaussian(0, MM, nrm) (simulator2.h:21-32) on the LDS matrix MM
-__device__ Mat<kX, 1> noise(double* w, const double* nrm, int lane) {
+__device__ __forceinline__ Mat<kX, 1> noise(double* w, const double* nrm, int lane) {
   double* V = w + oT1;
   double* D = w + oT2;
   jacobi<16>(w + oMM, V, D, lane);
@@ -405,8 +405,8 @@ __device__ Mat<kX, 1> noise(double* w, const double* nrm, int lane) {
   return mv(w + oE0, smp, w + oE1, lane) + Mat<kX, 1>::zero();
 }
 
-// kalmanFilter2 (LQRO:507-518) with P in LDS
-__device__ void kalman_update(const Quad& q, Mat<kX, 1>& x, Mat<3, 3>& R, const Mat<kZ, 1>& z,
+// kalmanFilter2 (LQRO:507-518) with P in LDS (inlined: no call frame)
+__device__ __forceinline__ void kalman_update(const Quad& q, Mat<kX, 1>& x, Mat<3, 3>& R, const Mat<kZ, 1>& z,
                               const double* Nz, double* w, int lane) {
   double* P = w + oP;
   double* H = w + oE0;          // 6x16
@@ -492,7 +492,7 @@ __device__ void kalman_update(const Quad& q, Mat<kX, 1>& x, Mat<3, 3>& R, const 
 }
 
 // One agent through LQRO:1438-1445 (= dyn::agent_step), one wave
-__device__ void agent_step(const dyn::AgentParams& a, double* x_, double* rot_, double* xt_, double* rott_,
+__device__ __forceinline__ void agent_step(const dyn::AgentParams& a, double* x_, double* rot_, double* xt_, double* rott_,
                            double* P_, double* vgoal_, double* u_out, double* w, int lane) {
   using dyn::get;
   const Quad q = dyn::quad(a.model);

@@ -45,6 +45,17 @@ namespace lqro {
 #define Q3_COPCAP 8       // its coplanar facet set
 #define Q3_FSTK 512       // free facet slots kept for reuse (more are left unused)
 #define Q3_ND (Q3_NEWCAP + Q3_MOVCAP)
+// poll intervals (s_sleep units of 64 clocks): wave 0 waiting on wave 1, and
+// the idle loops of waves 1 and 2
+#ifndef Q3_W0_SLEEP
+#define Q3_W0_SLEEP 1
+#endif
+#ifndef Q3_W1_SLEEP
+#define Q3_W1_SLEEP 1
+#endif
+#ifndef Q3_W2_SLEEP
+#define Q3_W2_SLEEP 1
+#endif
 #ifndef Q3_FL
 #define Q3_FL 2240        // facet slots with their hot fields in LDS (the rest of 160 KB)
 #endif
@@ -248,7 +259,11 @@ struct Q3S {
   unsigned long long tps[24], nps;   // LQRO_QHULL_PROFILE: phases of the one-chunk insertions
 };
 
-#ifdef LQRO_QHULL_PROFILE
+#if defined(LQRO_QHULL_PROFILE) && defined(LQRO_QHULL_PROF_LIGHT)
+// (light: no drain — a phase is charged the waits the build itself makes
+// there, so the phases add up to the undisturbed critical path)
+#define Q3T(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); S.tph[k] += t_ - S.tq; S.tq = t_; } while (0)
+#elif defined(LQRO_QHULL_PROFILE)
 // (every outstanding load and store drained first: a phase is charged its own memory waits)
 #define Q3T(k) do { __builtin_amdgcn_s_waitcnt(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); S.tph[k] += t_ - S.tq; S.tq = t_; } while (0)
 #else
@@ -269,7 +284,9 @@ struct Q3P {
   unsigned long long t[16];
   unsigned long long tq;
 };
-#ifdef LQRO_QHULL_PROFILE
+#if defined(LQRO_QHULL_PROFILE) && defined(LQRO_QHULL_PROF_LIGHT)
+#define W1T(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); P.t[k] += t_ - P.tq; P.tq = t_; } while (0)
+#elif defined(LQRO_QHULL_PROFILE)
 #define W1T(k) do { __builtin_amdgcn_s_waitcnt(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); P.t[k] += t_ - P.tq; P.tq = t_; } while (0)
 #else
 #define W1T(k) do {} while (0)
@@ -482,10 +499,14 @@ __device__ __forceinline__ double q3_scan_max(double v) {
 // last until the next new furthest point arrives, and is then fixed just
 // before it.  The furthest point itself is held aside (cx, cy, cz, champ)
 // and written by the caller at the end.  Entries at or beyond lim are not
-// written (the caller reports the capacity).
-__device__ __forceinline__ void q3_place(const Q3W& W, unsigned long long grp, int lane, unsigned long long ltmask,
+// written (the caller reports the capacity).  The lane's entry is returned
+// (wpos >= 0, wr), not stored: a chunk's lanes are in one group each, so the
+// caller stores once per chunk after all its groups — a fixed number of
+// stores between the next chunk's loads and their use (vmcnt is in order:
+// a data-dependent store count made every chunk wait for all its stores)
+__device__ __forceinline__ void q3_place(unsigned long long grp, int lane, unsigned long long ltmask,
                                          double dd, const HullPt& pt, int off, int lim, int& cnt, double& mx,
-                                         int& champ, double& cx, double& cy, double& cz) {
+                                         int& champ, double& cx, double& cy, double& cz, int& wpos, HullPt& wr) {
   const bool mem = (grp >> lane) & 1ull;
   const int cb = cnt + __popcll(grp & ltmask);   // points before this one in the set
   double run = -DBL_MAX;                         // the largest distance among them
@@ -515,7 +536,8 @@ __device__ __forceinline__ void q3_place(const Q3W& W, unsigned long long grp, i
       else { r.x = cx; r.y = cy; r.z = cz; r.q = champ; }
       r.pad = 0;
     }
-    W.sb[off + cb - 1] = r;
+    wpos = off + cb - 1;
+    wr = r;
   }
   if (recm) {
     const int l = 63 - __clzll((long long)recm);
@@ -764,7 +786,7 @@ __device__ __forceinline__ void q3_st_rel_lds(int* p, int v) {
 __device__ __forceinline__ int q3_wait(const int* p, int v, bool ne) {
   int x = q3_ld_acq(p);
   for (long w = 0; (ne ? x == v : x != v) && w < (1l << 24); ++w) {
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(Q3_W0_SLEEP);
     x = q3_ld_acq(p);
   }
   return x;
@@ -1067,11 +1089,17 @@ __device__ inline void q3_emit_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int ndn
   int ng = -1;
   double ndd = 0.0;
   HullPt npt = rpt;
+  // (the three loads are independent: the point is read whatever its
+  // destination, not behind a branch on the loaded one)
   auto ldc = [&](int c) {
     const int pos = c + lane;
-    ng = pos < np ? W.pdst[pos] : -1;
-    ndd = pos < np ? W.pdd[pos] : 0.0;
-    if (ng >= 0) npt = W.pseq[pos];
+    ng = -1;
+    ndd = 0.0;
+    if (pos < np) {
+      ng = W.pdst[pos];
+      ndd = W.pdd[pos];
+      npt = W.pseq[pos];
+    }
   };
   if (np > 64) ldc(0);
   for (int c = 0; c < np; c += 64) {
@@ -1091,6 +1119,9 @@ __device__ inline void q3_emit_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int ndn
     Q3T(16);
     unsigned long long todo = __ballot(g >= 0);
     const unsigned long long ltmask = (1ull << lane) - 1ull;
+    int wpos = -1;
+    HullPt wr;
+    wr.x = wr.y = wr.z = 0.0; wr.q = 0; wr.pad = 0;
     while (todo) {
       const int lead = __ffsll((long long)todo) - 1;
       const int gg = __builtin_amdgcn_readlane(g, lead);
@@ -1101,7 +1132,7 @@ __device__ inline void q3_emit_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int ndn
       int champ = L.dchamp[gg];
       double cx = L.dchp[3 * gg], cy = L.dchp[3 * gg + 1], cz = L.dchp[3 * gg + 2];
       const int off = L.doff[gg];
-      q3_place(W, grp, lane, ltmask, dd, pt, off, W.SB, cnt, mx, champ, cx, cy, cz);
+      q3_place(grp, lane, ltmask, dd, pt, off, W.SB, cnt, mx, champ, cx, cy, cz, wpos, wr);
       Q3C(25, 1);
       if (lane == 0) {
         L.dcnt[gg] = cnt; L.dmax[gg] = mx; L.dchamp[gg] = champ;
@@ -1109,6 +1140,7 @@ __device__ inline void q3_emit_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int ndn
       }
       hl_sync();
     }
+    if (wpos >= 0) W.sb[wpos] = wr;
   }
   hl_sync();
   Q3T(17);
@@ -1768,7 +1800,12 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
         if (keep) W.pq[w + __popcll(bk & ltmask)] = pt.q;
         w += __popcll(bk);
         const unsigned long long bo = __ballot(out);
-        if (bo) q3_place(W, bo, lane, ltmask, d, pt, off, W.SB, cnt, mx, champ, cx, cy, cz);
+        if (bo) {
+          int wpos = -1;
+          HullPt wr;
+          q3_place(bo, lane, ltmask, d, pt, off, W.SB, cnt, mx, champ, cx, cy, cz, wpos, wr);
+          if (wpos >= 0) W.sb[wpos] = wr;
+        }
         hl_sync();
       }
       if (cnt) {
@@ -1899,7 +1936,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
       int dn = q3_ld_acq(&L.sp_done);
       const unsigned long long tf_ = __builtin_amdgcn_s_memtime();   // the first read back
       for (long w = 0; dn != phase && w < (1l << 24); ++w) {
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(Q3_W0_SLEEP);
         dn = q3_ld_acq(&L.sp_done);
         ++spins_;
       }
@@ -2573,7 +2610,7 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
         }
         if (q3_ld_acq(&L.ph) < 0) break;
         if (++idle > (1l << 24)) break;
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(Q3_W2_SLEEP);
       }
     } else if (wave == 1) {
       // speculate each published phase until the build ends (ph = -1)
@@ -2636,7 +2673,7 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
           continue;
         }
         if (++idle > (1l << 24)) break;
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(Q3_W1_SLEEP);
       }
 #ifdef LQRO_QHULL_PROFILE
       if (A.prof && lane == 0)

@@ -105,12 +105,19 @@ LQRO_HD Mat<C, R> tr(const Mat<R, C>& a) {
 // takes the operands the indexed version gives it, in the same order, so the
 // results are bit-identical (tests/test_host_abi.py::test_small_pivot_routines
 // checks them against the indexed versions, kept as inverse_ix / solve_ix).
+// The permutations themselves are packed 4 bits an entry into one integer:
+// the compiler turned select chains over a 3-int array back into an indexed
+// load, which put the array in scratch again (k_dynw's resets).
 template <int N>
-LQRO_HD int sm_get(const int (&a)[N], int k) {
-  int r = a[0];
-#pragma unroll
-  for (int t = 1; t < N; ++t) r = k == t ? a[t] : r;
-  return r;
+struct SmIx {
+  static_assert(N <= 8, "4 bits an entry");
+  unsigned v = 0u;
+  LQRO_HD int operator[](int i) const { return (int)((v >> (4 * i)) & 15u); }
+  LQRO_HD void set(int i, int x) { v = (v & ~(15u << (4 * i))) | ((unsigned)x << (4 * i)); }
+};
+template <int N>
+LQRO_HD int sm_get(const SmIx<N>& a, int k) {
+  return a[k];
 }
 // the first strict maximum of |M[i][j]|, i, j >= k, in (row, col) order
 template <int N>
@@ -157,23 +164,21 @@ LQRO_HD void sm_swap_cols(double (&M)[N][C], int k, int c) {
     }
 }
 template <int N>
-LQRO_HD void sm_swap_ix(int (&a)[N], int k, int r) {
-  const int ak = a[k], ar = sm_get(a, r);
-#pragma unroll
-  for (int t = 0; t < N; ++t) {
-    if (t == k) a[t] = ar;
-    else if (t > k) a[t] = r == t ? ak : a[t];
-  }
+LQRO_HD void sm_swap_ix(SmIx<N>& a, int k, int r) {
+  const int ak = a[k], ar = a[r];
+  a.set(r, ak);
+  a.set(k, ar);
 }
 
 // P X = Q (operator%, MAT:370-442) for N <= 4; = solve_ix below
 template <int N, int C>
 LQRO_HD Mat<N, C> solve_sm(const Mat<N, N>& p, const Mat<N, C>& q) {
   double M[N][N], X[N][C];   // M[i][j] = m(rp[i], cp[j]), X[i][j] = x(rp[i], j)
-  int rp[N], cp[N];
+  SmIx<N> rp, cp;
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    rp[i] = cp[i] = i;
+    rp.set(i, i);
+    cp.set(i, i);
 #pragma unroll
     for (int j = 0; j < N; ++j) M[i][j] = p(i, j);
 #pragma unroll
@@ -211,19 +216,18 @@ LQRO_HD Mat<N, C> solve_sm(const Mat<N, N>& p, const Mat<N, C>& q) {
   }
   // the reference's final reshuffle on the physical rows x(r) = X[l], rp[l] = r
   double Y[N][C];
-  int irp[N];
+  SmIx<N> irp;
 #pragma unroll
   for (int r = 0; r < N; ++r) {
 #pragma unroll
     for (int j = 0; j < C; ++j) Y[r][j] = 0.0;
-    irp[r] = 0;
   }
 #pragma unroll
   for (int l = 0; l < N; ++l)
 #pragma unroll
     for (int r = 0; r < N; ++r) {   // (selects, not branches: the arrays stay in registers)
       const bool hit = rp[l] == r;
-      irp[r] = hit ? l : irp[r];
+      if (hit) irp.set(r, l);
 #pragma unroll
       for (int j = 0; j < C; ++j) Y[r][j] = hit ? X[l][j] : Y[r][j];
     }
@@ -241,10 +245,8 @@ LQRO_HD Mat<N, C> solve_sm(const Mat<N, N>& p, const Mat<N, C>& q) {
     }
     const int ia = sm_get(irp, a);
     // rp[irp[cp[i]]] = rp[i]; irp[rp[i]] = irp[cp[i]]
-#pragma unroll
-    for (int t = 0; t < N; ++t) rp[t] = t == ia ? b : rp[t];
-#pragma unroll
-    for (int t = 0; t < N; ++t) irp[t] = t == b ? ia : irp[t];
+    rp.set(ia, b);
+    irp.set(b, ia);
   }
   Mat<N, C> out;
 #pragma unroll
@@ -260,10 +262,11 @@ LQRO_HD Mat<N, C> solve_sm(const Mat<N, N>& p, const Mat<N, C>& q) {
 template <int N>
 LQRO_HD Mat<N, N> inverse_sm(const Mat<N, N>& q) {
   double M[N][N], I[N][N];
-  int rp[N], cp[N];
+  SmIx<N> rp, cp;
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    rp[i] = cp[i] = i;
+    rp.set(i, i);
+    cp.set(i, i);
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       M[i][j] = q(i, j);
