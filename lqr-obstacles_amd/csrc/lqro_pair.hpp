@@ -784,7 +784,20 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
         B.R = P.R + i * H;
         B.TF = P.TF + i * H;
       }
+#ifdef LQRO_HOT_STAMPS
+      // diagnostic: each hot pair's start / end on the 100 MHz clock, bit 63
+      // of the end = inside-hull (scripts/hot_stamps.py)
+      const unsigned long long hs0 = __builtin_amdgcn_s_memrealtime();
+#endif
       do_pair(P.row_begin + lrow * P.row_stride, lrow, slot - lrow * P.npr);
+#ifdef LQRO_HOT_STAMPS
+      if (lane == 0 && P.prof && h < 8192) {
+        const unsigned long long hs1 = __builtin_amdgcn_s_memrealtime();
+        const int fl = __float_as_int(P.planes[(size_t)slot * 8 + 6]);
+        P.prof[48 + 2 * h] = hs0;
+        P.prof[49 + 2 * h] = hs1 | ((unsigned long long)(fl == 2) << 63);
+      }
+#endif
     }
   } else {
   // Persistent: the workgroup takes whole rows (agent i) off a queue; its
