@@ -82,6 +82,47 @@ def pmc_traffic(kernel: str = "k_pair"):
     return None
 
 
+def qhull_traffic():
+    """HBM bytes per Qhull-order hull build from the committed PMC passes
+    (profiles/*_qhull_traffic.json, scripts/qhull_traffic.py), cited only
+    when its build stamp is the liblqro.so this bench runs."""
+    import glob
+    sha = lib_sha256()
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_qhull_traffic.json")), reverse=True):
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("build", {}).get("lib_sha256") == sha:
+            return d, os.path.relpath(path, ROOT)
+    return None
+
+
+def critical_path(ctx):
+    """The step's critical path in the default rule: its Qhull-order hull
+    builds (k_qhull, lqro_get_hull_builds of the last timed step, the GPU's
+    100 MHz clock): the slowest build, the mean, microseconds per insertion,
+    and the HBM bytes per build from the stamped PMC passes."""
+    b = ctx.hull_builds()
+    if len(b) == 0:
+        return None
+    dur = (b["t_end"].astype(np.int64) - b["t_start"].astype(np.int64)) / 1e5      # ms
+    k = int(np.argmax(dur))
+    t0 = int(b["t_start"].min())
+    tr = qhull_traffic()
+    return {"kernel": "k_qhull", "builds": int(len(b)),
+            "builds_k_qhull_big": int((b["kernel"] == 1).sum()),
+            "slowest_build_ms": float(dur[k]), "slowest_build_pair": [int(b["i"][k]), int(b["j"][k])],
+            "slowest_build_insertions": int(b["insertions"][k]), "slowest_build_points": int(b["n_points"][k]),
+            "slowest_us_per_insertion": float(dur[k] * 1e3 / max(1, b["insertions"][k])),
+            "mean_build_ms": float(dur.mean()),
+            "mean_us_per_insertion": float(dur.sum() * 1e3 / max(1, int(b["insertions"].sum()))),
+            "last_build_end_ms": float((int(b["t_end"].max()) - t0) / 1e5),
+            "hbm_bytes_per_build": tr[0]["hbm_bytes_per_build"] if tr else None,
+            "algorithmic_bytes_per_build": tr[0]["algorithmic_bytes_per_build"] if tr else None,
+            "traffic_source": tr[1] if tr else None,
+            "note": "LQRO:867-969 per inside-hull pair (qconvex's build restated in-kernel); times from each "
+                    "build's job start to its half-plane, s_memrealtime; last_build_end_ms from the first build's start"}
+
+
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -278,7 +319,48 @@ def config_runs(lqro, torch, dev, local, world, rank, dist, steps, mode="block",
                      "pairs_per_step": N * (N - 1), "steps": steps, "ms_per_step": el / steps * 1e3,
                      "evals_per_s": N * (N - 1) * steps / el, "scaling": "strong",
                      "rank0_inside_hull": st["inside"], "rank0_hull_failures": st["hull_fail"]}
+        if world == 1:
+            out[name]["rank_shard_g8"] = rank_shard_run(lqro, torch, dev, local, N, H, X, gains, per_agent, x, vg,
+                                                        steps, flags, out[name]["ms_per_step"])
     return out
+
+
+def rank_shard_run(lqro, torch, dev, local, N, H, X, gains, per_agent, x, vg, steps, flags, whole_ms):
+    """One rank's work at G = 8 on this GPU: rows [0, N/8) with the full
+    schedule of a rank (lqro_step_device_begin, the row-normal table, _end;
+    the all-gathers themselves are not timed: no other rank).  The 8-GPU
+    step cannot be shorter than this; whole_ms / ms_per_step is the strong-
+    scaling ceiling this build has at 8 GPUs."""
+    rows = (0, N // 8)
+    ctx = lqro.Context(lqro.config(N, H, N_POINTS, x_dim=X, device=local, flags=flags,
+                                   row_begin=rows[0], row_end=rows[1]))
+    ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"], per_agent=per_agent)
+    d_x = torch.from_numpy(x).to(dev)
+    d_vg = torch.from_numpy(vg).to(dev)
+    d_newv = torch.zeros((N, 3), dtype=torch.float64, device=dev)
+    rowtab = torch.zeros((N, 4), dtype=torch.float64, device=dev)
+    s = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        ctx.step_device_begin(d_x.data_ptr(), d_vg.data_ptr(), rowtab.data_ptr(), s)
+        ctx.step_device_end(rowtab.data_ptr(), d_newv.data_ptr(), s)
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    st = ctx.stats()
+    crit = critical_path(ctx) if flags & lqro.LQRO_FLAG_QHULL_ORDER else None
+    ctx.close()
+    ms = el / steps * 1e3
+    return {"rows": list(rows), "pairs_per_step": (rows[1] - rows[0]) * (N - 1), "steps": steps,
+            "ms_per_step": ms, "strong_scaling_ceiling_g8": whole_ms / ms, "inside_hull": st["inside"],
+            "hull_failures": st["hull_fail"],
+            "slowest_build_ms": crit["slowest_build_ms"] if crit else None,
+            "note": "one rank's rows of the 8-GPU strong-scaled swarm, on this one GPU"}
 
 
 CPP_BENCH = os.path.join(ROOT, "tests", "cpp", "lqro_bench_main")
@@ -471,6 +553,7 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     st = ctx.stats()
+    crit = critical_path(ctx) if flags & lqro.LQRO_FLAG_QHULL_ORDER else None
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -565,6 +648,7 @@ def main():
             "hbm_algorithmic_gbs": gbs,
             "hbm_frac": gbs / HBM_PEAK_GBS,
         },
+        "critical": crit,
         "step_device_ms": float(np.mean(step_dev_ms)),
         "sweep_ms": sweep_ms,
         "closed_loop": closed,

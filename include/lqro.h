@@ -35,9 +35,10 @@ enum {
   LQRO_E_SINGULAR = -5,  /* singular 3x3 C*G_k (reference asserts, MAT:632) */
   LQRO_E_NODEVICE = -6,  /* no usable gfx950 device                        */
   LQRO_E_OVERFLOW = -7,  /* an internal work queue overflowed              */
-  LQRO_E_HULL = -8       /* an inside-hull pair's hull exceeded the in-kernel */
-                         /*   hull's capacity: its half-plane is missing     */
-                         /*   (lqro_get_hull_failures names the pairs)       */
+  LQRO_E_HULL = -8       /* an inside-hull pair's hull could not be built    */
+                         /*   (degenerate / too few points, or every hull    */
+                         /*   kernel's capacity exceeded): its half-plane is */
+                         /*   missing (lqro_get_hull_failures names pairs)   */
 };
 
 /* ---- flags ------------------------------------------------------------- */
@@ -59,6 +60,13 @@ enum {
                                 /*   normalVector of the previous pair (LQRO:956-968)    */
 #define LQRO_REC_QHMERGE  0x80  /* Qhull order: Qhull would merge facets in this hull;   */
                                 /*   built merge-free                       */
+#define LQRO_REC_QHMERGE_WIN 0x100 /* with LQRO_REC_QHMERGE: a facet within 1e-6 of the  */
+                                /*   winning distance has another hull vertex within    */
+                                /*   1e-9 (|coord|max + 1) of its plane, so qconvex's     */
+                                /*   pre-merge may have joined the winner into a merged */
+                                /*   facet: the pair's facet, distance and normal are    */
+                                /*   then not pinned to the reference;    */
+                                /*   lqro_get_stats_ex [11] counts these pairs           */
 
 /* Static configuration.  The names follow the reference's compile-time
  * macros (LQRO:9-14) and the constants of its driver (LQRO:1387, 1224). */
@@ -244,15 +252,37 @@ int lqro_get_records(lqro_ctx* ctx, lqro_pair_record* out, int64_t capacity, int
 /* Counters of the last step: [0]=pairs, [1]=planes, [2]=inside, [3]=hull ok,
  * [4]=hull fail, [5]=gjk backups, [6]=sum n_reach, [7]=sum G-tests. */
 int lqro_get_stats(lqro_ctx* ctx, int64_t* stats8);
-/* The same counters and n - 8 more (n <= 11; words past 10 read 0):
+/* The same counters and n - 8 more (n <= 12; words past 11 read 0):
  * [8] LQRO_FLAG_QHULL_ORDER hulls in which Qhull would merge facets
  *     (LQRO_REC_QHMERGE: built merge-free);
  * [9] builds k_qhull's per-insertion caps handed to k_qhull_big;
- * [10] of those, the ones a wave handshake timeout stopped. */
+ * [10] of those, the ones a wave handshake timeout stopped;
+ * [11] pairs whose winning facet qconvex's pre-merge may have merged
+ *     (LQRO_REC_QHMERGE_WIN). */
 int lqro_get_stats_ex(lqro_ctx* ctx, int64_t* stats, int32_t n);
 
+/* One Qhull-order hull build of the last step (LQRO_FLAG_QHULL_ORDER): the
+ * in-kernel replacement of convexHull's qconvex run (LQRO:867-969) for the
+ * pair (i, j), timed on the GPU's constant 100 MHz clock (s_memrealtime,
+ * shared by every CU): from taking the job (the pair's points are computed
+ * first) to its half-plane.  kernel: 0 k_qhull, 1 k_qhull_big (the build
+ * beyond k_qhull's caps), 2 a k_qhull build handed to k_qhull_big (its
+ * record ends where the hand-over happened). */
+typedef struct lqro_hull_build {
+  int32_t i, j;
+  int32_t n_points;       /* reachablePoints.size(), qconvex's input             */
+  int32_t insertions;     /* points Qhull added (qh_addpoint calls)              */
+  int32_t facet_slots;    /* facets created (slots used)                         */
+  int32_t kernel;
+  uint64_t t_start, t_end;  /* 100 MHz ticks                                     */
+} lqro_hull_build;
+/* *n_out = the builds of the last step (at most the first `capacity` and
+ * 16384 are written, in completion order). */
+int lqro_get_hull_builds(lqro_ctx* ctx, lqro_hull_build* out, int64_t capacity, int64_t* n_out);
+
 /* The pairs of the last step left without a half-plane because their hull
- * exceeded the in-kernel hull's capacity (stats [4]; lqro_step then returns
+ * could not be built — degenerate input or every hull kernel's capacity
+ * exceeded (stats [4]; lqro_step then returns
  * LQRO_E_HULL, the reference's qconvex always returns a hull, LQRO:879-880):
  * *n_out = their number; pairs[2k], pairs[2k+1] = (i, j) of the first
  * min(*n_out, 64, capacity). */

@@ -18,6 +18,8 @@
 //     hipMemcpyAsync              vGoal = newV (LQRO:1438), own rows
 //     lqro_dynamics_step_device   findU, propagate, kalmanFilter1/2, findVGoal (LQRO:1439-1445), own rows
 //     ncclAllGather               x of every agent, in place
+//     (host)                      the iteration's hull failures, exchanged so every
+//                                 rank throws lqro::Error(LQRO_E_HULL) together
 //
 // The noise draws follow the reference's single rand() stream in agent order
 // (normal(), LQRO:334-350): every rank draws the whole iteration's stream
@@ -96,6 +98,7 @@ class ShardedSimulator {
     alloc(&d_vg_, na * kV);
     alloc(&d_newv_, na * kV);
     alloc(&d_rowtab_, na * 4);
+    alloc(&d_fail_, na);
     alloc(&d_rot_, r * 9);
     alloc(&d_xt_, r * kX);
     alloc(&d_rott_, r * 9);
@@ -117,7 +120,7 @@ class ShardedSimulator {
  public:
   ~ShardedSimulator() {
     if (comm_) ncclCommDestroy(comm_);
-    for (double* p : {d_x_, d_vg_, d_newv_, d_rowtab_, d_rot_, d_xt_, d_rott_, d_P_, d_ug_, d_pg_, d_nrm_, d_L_, d_E_, d_l_,
+    for (double* p : {d_x_, d_vg_, d_newv_, d_rowtab_, d_fail_, d_rot_, d_xt_, d_rott_, d_P_, d_ug_, d_pg_, d_nrm_, d_L_, d_E_, d_l_,
                       d_Lh_, d_Eh_, d_M_, d_N_})
       if (p) (void)hipFree(p);
     if (d_model_) (void)hipFree(d_model_);
@@ -187,8 +190,36 @@ class ShardedSimulator {
     // the host copy waits for the iteration (the normals' staging buffer is reused)
     check_hip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
     ++t_;
+    // A hull this rank could not build left a pair without its half-plane
+    // (the reference's qconvex always returns one, LQRO:879-880): never
+    // silently.  Every rank learns the swarm's total (one n x 1 exchange:
+    // each rank's count in its first row), so all of them throw together
+    // and none is left waiting in the next iteration's collectives.
+    int64_t st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (ctx_) check(lqro_get_stats(ctx_, st), "lqro_get_stats");
+    rank_hull_fail_ = st[4];
+    std::vector<double> f((size_t)n_, 0.0);
+    if (rows_ > 0) {
+      f[(size_t)rb_] = (double)st[4];
+      put(d_fail_ + rb_, f.data() + rb_, (size_t)rows_);
+    }
+    ex_(d_fail_, 1, stream_);
+    get(f.data(), d_fail_, (size_t)n_);
+    double tot = 0.0;
+    for (double v : f) tot += v;
+    hull_fail_ = (int64_t)tot;
+    if (hull_fail_ > 0)
+      throw Error("lqro::ShardedSimulator: " + std::to_string(hull_fail_) +
+                      " inside-hull pair(s) left without a half-plane (rank " + std::to_string(rank_) + ": " +
+                      std::to_string(rank_hull_fail_) + "; lqro_get_hull_failures)",
+                  LQRO_E_HULL);
     return seed;
   }
+
+  // hull failures of the last iteration: the whole swarm's (every rank sees
+  // the same number) and this rank's own rows'
+  int64_t hull_failures() const { return hull_fail_; }
+  int64_t rank_hull_failures() const { return rank_hull_fail_; }
 
   // The device state back into qlist: every agent's x, this rank's rows'
   // full state and newV.
@@ -218,9 +249,16 @@ class ShardedSimulator {
 
  private:
   // The all-gather of a row-major n x w table whose rows [rb_r, re_r) rank r
-  // holds: blocks of unequal size (n not a multiple of world), so one
-  // broadcast per rank, from its rows in place, in one group (allgatherv).
+  // holds.  Equal blocks (n a multiple of world: C4, C5 at 8 GPUs): one
+  // in-place ncclAllGather (rank r's send buffer is its own rows of d).
+  // Unequal blocks: one broadcast per rank, from its rows in place, in one
+  // group (an allgatherv).
   void allgather_rows(double* d, int w, hipStream_t stream) {
+    if (n_ % world_ == 0) {
+      const size_t cnt = (size_t)(n_ / world_) * w;
+      check_nccl(ncclAllGather(d + (size_t)rb_ * w, d, cnt, ncclDouble, comm_, stream), "ncclAllGather");
+      return;
+    }
     check_nccl(ncclGroupStart(), "ncclGroupStart");
     for (int r = 0; r < world_; ++r) {
       const int b = block_begin(n_, r, world_), e = block_begin(n_, r + 1, world_);
@@ -289,6 +327,7 @@ class ShardedSimulator {
 
   std::vector<Quadrotor>& q_;
   int n_ = 0, rank_ = 0, world_ = 1, device_ = 0, rb_ = 0, re_ = 0, rows_ = 0, t_ = 0;
+  int64_t hull_fail_ = 0, rank_hull_fail_ = 0;
   lqro_model model_;
   lqro_ctx* ctx_ = nullptr;
   hipStream_t stream_ = nullptr;
@@ -297,7 +336,7 @@ class ShardedSimulator {
   std::array<double, kX * kX> A_{};
   std::array<double, kX * kU> B_{};
   std::vector<double> nrm_;
-  double *d_x_ = nullptr, *d_vg_ = nullptr, *d_newv_ = nullptr, *d_rowtab_ = nullptr, *d_rot_ = nullptr, *d_xt_ = nullptr,
+  double *d_x_ = nullptr, *d_vg_ = nullptr, *d_newv_ = nullptr, *d_rowtab_ = nullptr, *d_fail_ = nullptr, *d_rot_ = nullptr, *d_xt_ = nullptr,
          *d_rott_ = nullptr, *d_P_ = nullptr, *d_ug_ = nullptr, *d_pg_ = nullptr, *d_nrm_ = nullptr, *d_L_ = nullptr,
          *d_E_ = nullptr, *d_l_ = nullptr, *d_Lh_ = nullptr, *d_Eh_ = nullptr, *d_M_ = nullptr, *d_N_ = nullptr;
   lqro_model* d_model_ = nullptr;

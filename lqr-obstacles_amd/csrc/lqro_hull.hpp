@@ -130,6 +130,9 @@ struct HullArgs {
   const double* lp_vgoal;
   double* lp_newv;
   double lp_vmax;
+  // Qhull order: one timing record per build (hull_build_note), null: off
+  unsigned long long* hbuild;
+  int hbuild_cap;
 };
 
 // (LQRO_ROW_BIG, lqro_device.hpp: the row counter's protocol; the early LP
@@ -253,6 +256,9 @@ struct HullLdsC {
 #define LQRO_ST_RETRY 9
 #define LQRO_ST_TIMEOUT 10
 #define LQRO_ST_NFAIL 11
+#define LQRO_ST_MWIN 12     // pairs flagged LQRO_REC_QHMERGE_WIN (lqro_get_stats_ex [11])
+#define LQRO_ST_NBUILD 13   // Qhull-order build records written (A.hbuild)
+#define LQRO_HBUILD_CAP 16384
 #define LQRO_ST_FAILS 16
 #define LQRO_ST_FAILMAX 64
 #define LQRO_ST_WORDS (LQRO_ST_FAILS + LQRO_ST_FAILMAX)
@@ -264,6 +270,23 @@ __device__ __forceinline__ void hull_fail_note(unsigned long long* stats, int sl
   atomicAdd(&stats[4], 1ull);
   const unsigned long long k = atomicAdd(&stats[LQRO_ST_NFAIL], 1ull);
   if (k < LQRO_ST_FAILMAX) stats[LQRO_ST_FAILS + k] = (unsigned long long)slot;
+}
+
+// lane 0: a Qhull-order build's timing record (lqro_get_hull_builds):
+// slot | kernel << 40, start, end (s_memrealtime, 100 MHz), points |
+// insertions << 20 | facet slots << 40
+__device__ __forceinline__ void hull_build_note(const HullArgs& A, int slot, int kernel, unsigned long long t0,
+                                                int n, int nins, int nfac) {
+  if (!A.hbuild) return;
+  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long k = atomicAdd(&A.stats[LQRO_ST_NBUILD], 1ull);
+  if (k >= (unsigned long long)A.hbuild_cap) return;
+  unsigned long long* r = A.hbuild + 4 * k;
+  r[0] = (unsigned long long)(unsigned)slot | ((unsigned long long)kernel << 40);
+  r[1] = t0;
+  r[2] = t1;
+  r[3] = (unsigned long long)(n & 0xFFFFF) | ((unsigned long long)(nins & 0xFFFFF) << 20) |
+         ((unsigned long long)(nfac & 0xFFFFF) << 40);
 }
 
 __device__ __forceinline__ void hl_sync() {

@@ -37,6 +37,7 @@
 #include <float.h>
 
 #include "lqro_hull.hpp"
+#include "lqro_dec16.hpp"
 
 namespace lqro {
 
@@ -161,6 +162,7 @@ struct QhL {
 // Qhull's scalar state of one build (registers, uniform over the wave)
 struct QhS {
   int facet_list, facet_tail, facet_next, newfacet_list, visible_list;
+  int nins;                     // insertions (qh_addpoint calls), for the build's timing record
   int nalloc, nfree, nv, sbtop, status;
   int nnew, nvis, nmov, nold, epoch;
   int findbestnew, notsharp;
@@ -1032,6 +1034,7 @@ __device__ inline void qh_build(const QhW& W, QhS& S, QhL& L, int n, int lane) {
     }
     QHT(1);
     if (furthest < 0) break;
+    S.nins++;
     const double* apexp = W.Pr + 3 * (size_t)furthest;
     // qh_findhorizon
     S.epoch++;
@@ -1224,60 +1227,138 @@ __device__ inline void qh_build(const QhW& W, QhS& S, QhL& L, int n, int lane) {
 }
 
 // ---- the reference's selection (LQRO:925-968) over the finished hull ----
+// convexHull measures facet f as |n_f . (vrel - P_f)| with n_f the plane as
+// qconvex prints it and operator>> reads it back (16 significant digits,
+// LQRO:889-899; lqro_dec16.hpp) and P_f the first Fv vertex at full
+// precision (LQRO:925-939).  qsel_dist: that distance with Qhull's own
+// plane, and a bound b on its change under the read-back (the decimal
+// rounding <= 6.2e-16 |n_k| per coefficient, both evaluations' rounding
+// <= 3.4e-16 of sum |n_k| |vrel_k - P_k| each; b is 3x their sum);
+// qsel_dist16: the distance with the read-back plane, exactly the reference's
+// expression.
+__device__ __forceinline__ double qsel_dist(const double* q, const double* P, const double* vrel, double* b) {
+  const double a0 = vrel[0] - P[0], a1 = vrel[1] - P[1], a2 = vrel[2] - P[2];
+  *b = 4e-15 * (fabs(q[0] * a0) + fabs(q[1] * a1) + fabs(q[2] * a2)) + 1e-300;
+  return fabs(q[0] * a0 + q[1] * a1 + q[2] * a2);
+}
+__device__ inline double qsel_dist16(const double* q, const double* P, const double* vrel, double* n16) {
+  bool e0, e1, e2;
+  n16[0] = dec16(q[0], &e0);
+  n16[1] = dec16(q[1], &e1);
+  n16[2] = dec16(q[2], &e2);
+  return fabs(n16[0] * (vrel[0] - P[0]) + n16[1] * (vrel[1] - P[1]) + n16[2] * (vrel[2] - P[2]));
+}
+
+// LQRO_REC_QHMERGE_WIN, as q3_merge_suspect (lqro_qhull3.hpp): a facet
+// within 1e-6 of the winning distance with another hull vertex within
+// 1e-9 (|coord|max + 1) of its plane; wave-uniform
+__device__ inline bool qh_merge_suspect(const QhW& W, const QhS& S, int lane, const double* vrel, double best) {
+  const double T = -1e-9 * (S.MAXabs_coord + 1.0);
+  bool sus = false;
+  for (int f0 = 1; f0 < S.nalloc; f0 += 64) {
+    const int f = f0 + lane;
+    bool con = false;
+    if (f < S.nalloc && (W.fflag[f] & QF_LIVE)) {
+      const double* q = W.pl + 4 * (size_t)f;
+      const double* P = W.Pf + 3 * (size_t)W.vpt[W.fv[3 * f]];
+      con = fabs(q[0] * (vrel[0] - P[0]) + q[1] * (vrel[1] - P[1]) + q[2] * (vrel[2] - P[2])) <= best + 1e-6;
+    }
+    unsigned long long m = __ballot(con);
+    while (m) {
+      const int src = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      const int fc = __shfl(f, src);
+      const double* qc = W.pl + 4 * (size_t)fc;
+      const int a = W.vpt[W.fv[3 * fc]], b = W.vpt[W.fv[3 * fc + 1]], c = W.vpt[W.fv[3 * fc + 2]];
+      for (int g = 1 + lane; g < S.nalloc; g += 64) {
+        if (!(W.fflag[g] & QF_LIVE)) continue;
+        for (int t = 0; t < 3; t++) {
+          const int id = W.vpt[W.fv[3 * g + t]];
+          if (id == a || id == b || id == c) continue;
+          const double* p = W.Pr + 3 * (size_t)id;
+          if (qc[3] + p[0] * qc[0] + p[1] * qc[1] + p[2] * qc[2] >= T) sus = true;
+        }
+      }
+    }
+  }
+  return __ballot(sus) != 0;
+}
+
 // Facets in Qhull's order, each measured from its first Fv vertex (its
-// newest) at full precision, strict '<': the minimum, the earliest facet in
-// list order on a tie (a walk of the list, only then).  Facet 0 (the list
-// head) winning leaves `normal` to the loop-carried value: the plane waits
-// for k_stale.
+// newest) with the read-back plane, strict '<': the minimum, the earliest
+// facet in list order on a tie (a walk of the list, only then).  Facet 0 (the
+// list head) winning leaves `normal` to the loop-carried value: the plane
+// waits for k_stale.  Two passes: every facet at full precision for the
+// bound on the minimum, then the read-back planes of the facets within it.
 __device__ inline void qh_select(const HullArgs& A, const QhW& W, const QhS& S, int lane, const double* xi,
                                  const double* vrel, int slot) {
   const bool fail = (S.status & (QHS_INPUT | QHS_TOPOLOGY | QHS_CAPACITY)) != 0;
-  double best = INFINITY;
-  int bf = 0x7fffffff, nfac = 0;
+  double ub = INFINITY;
+  int nfac = 0;
   if (!fail) {
     for (int f = 1 + lane; f < S.nalloc; f += 64) {
       if (!(W.fflag[f] & QF_LIVE)) continue;
       nfac++;
       const double* q = W.pl + 4 * (size_t)f;
       const double* P = W.Pf + 3 * (size_t)W.vpt[W.fv[3 * f]];
-      const double d = fabs(q[0] * (vrel[0] - P[0]) + q[1] * (vrel[1] - P[1]) + q[2] * (vrel[2] - P[2]));
-      if (d < best || (d == best && f < bf)) { best = d; bf = f; }
+      double b;
+      const double d = qsel_dist(q, P, vrel, &b);
+      ub = fmin(ub, d + b);
+    }
+  }
+  for (int off = 32; off >= 1; off >>= 1) {
+    nfac += __shfl_xor(nfac, off);
+    ub = fmin(ub, __shfl_xor(ub, off));
+  }
+  double best = INFINITY, bn[3] = {0.0, 0.0, 0.0};
+  int bf = 0x7fffffff;
+  if (!fail) {
+    for (int f = 1 + lane; f < S.nalloc; f += 64) {
+      if (!(W.fflag[f] & QF_LIVE)) continue;
+      const double* q = W.pl + 4 * (size_t)f;
+      const double* P = W.Pf + 3 * (size_t)W.vpt[W.fv[3 * f]];
+      double b, n16[3];
+      if (qsel_dist(q, P, vrel, &b) - b > ub) continue;
+      const double d = qsel_dist16(q, P, vrel, n16);
+      if (d < best || (d == best && f < bf)) { best = d; bf = f; bn[0] = n16[0]; bn[1] = n16[1]; bn[2] = n16[2]; }
     }
   }
   int ties = 0;
   for (int off = 32; off >= 1; off >>= 1) {
     const double ob = __shfl_xor(best, off);
     const int of = __shfl_xor(bf, off);
-    nfac += __shfl_xor(nfac, off);
-    if (ob < best || (ob == best && of < bf)) { best = ob; bf = of; }
+    const double o0 = __shfl_xor(bn[0], off), o1 = __shfl_xor(bn[1], off), o2 = __shfl_xor(bn[2], off);
+    if (ob < best || (ob == best && of < bf)) { best = ob; bf = of; bn[0] = o0; bn[1] = o1; bn[2] = o2; }
   }
   if (!fail) {
     for (int f = 1 + lane; f < S.nalloc; f += 64) {
       if (!(W.fflag[f] & QF_LIVE)) continue;
       const double* q = W.pl + 4 * (size_t)f;
       const double* P = W.Pf + 3 * (size_t)W.vpt[W.fv[3 * f]];
-      const double d = fabs(q[0] * (vrel[0] - P[0]) + q[1] * (vrel[1] - P[1]) + q[2] * (vrel[2] - P[2]));
-      ties += d == best;
+      double b, n16[3];
+      if (qsel_dist(q, P, vrel, &b) - b > ub) continue;
+      ties += qsel_dist16(q, P, vrel, n16) == best;
     }
     for (int off = 32; off >= 1; off >>= 1) ties += __shfl_xor(ties, off);
     if (ties > 1)   // the first in Qhull's order
       for (int f = S.facet_list; f != S.facet_tail; f = qh_next(W, f)) {
         const double* q = W.pl + 4 * (size_t)f;
         const double* P = W.Pf + 3 * (size_t)W.vpt[W.fv[3 * f]];
-        const double d = fabs(q[0] * (vrel[0] - P[0]) + q[1] * (vrel[1] - P[1]) + q[2] * (vrel[2] - P[2]));
-        if (d == best) { bf = f; break; }
+        double b, n16[3];
+        if (qsel_dist(q, P, vrel, &b) - b > ub) continue;
+        if (qsel_dist16(q, P, vrel, n16) == best) { bf = f; bn[0] = n16[0]; bn[1] = n16[1]; bn[2] = n16[2]; break; }
       }
   }
   const bool ok = !fail && nfac > 0 && bf != 0x7fffffff;
   const bool stale = ok && bf == S.facet_list;
   const bool merged = (S.status & (QHS_COPLANAR | QHS_NONCONVEX | QHS_FLIPPED | QHS_NARROW | QHS_SINGULAR)) != 0;
+  const bool mwin = ok && merged && qh_merge_suspect(W, S, lane, vrel, best);
   if (lane == 0) {
     float* pl = A.planes + (size_t)slot * 8;
     double* qn = A.qnrm + (size_t)slot * 4;
     double nrm[3] = {0.0, 0.0, 0.0};
     if (ok && !stale) {
-      const double* q = W.pl + 4 * (size_t)bf;
-      nrm[0] = q[0]; nrm[1] = q[1]; nrm[2] = q[2];
+      nrm[0] = bn[0]; nrm[1] = bn[1]; nrm[2] = bn[2];
       const double dh = best * 0.5;                      // :1416
       const double mult = 1.0;                           // :1213
       pl[0] = (float)(xi[3] + mult * dh * nrm[0]);
@@ -1298,11 +1379,13 @@ __device__ inline void qh_select(const HullArgs& A, const QhW& W, const QhS& S, 
       hull_fail_note(A.stats, slot);
     }
     if (ok && merged) atomicAdd(&A.stats[LQRO_ST_MERGED], 1ull);
+    if (mwin) atomicAdd(&A.stats[LQRO_ST_MWIN], 1ull);
     if (A.recs) {
       lqro_pair_record& rec = A.recs[slot];
       rec.flags |= ok ? LQRO_REC_HULL : LQRO_REC_HULLFAIL;
       if (stale) rec.flags |= LQRO_REC_STALE;
       if (merged) rec.flags |= LQRO_REC_QHMERGE;
+      if (mwin) rec.flags |= LQRO_REC_QHMERGE_WIN;
       rec.n_facets = ok ? nfac : -(S.status & 0xffff) - 1;   // a failure: -(build status bits) - 1
       if (ok) {
         for (int k = 0; k < 3; k++) rec.facet[k] = W.vpt[W.fv[3 * bf + k]];
@@ -1328,6 +1411,7 @@ __device__ inline void qh_body(const HullArgs& A, QhL& L, bool retryq) {
   for (;;) {
     const int slot = hull_take_job(A, L, retryq);
     if (slot < 0) break;
+    const unsigned long long tjob = __builtin_amdgcn_s_memrealtime();   // (lqro_get_hull_builds)
     const int lrow = slot / A.npr, jj = A.nbr_list ? A.nbr_list[slot] : slot % A.npr;
     const int i = A.row_begin + lrow * A.row_stride;
     const int j = jj < i ? jj : jj + 1;
@@ -1343,6 +1427,7 @@ __device__ inline void qh_body(const HullArgs& A, QhL& L, bool retryq) {
 #endif
     S.status = 0;
     S.nalloc = 1;
+    S.nins = 0;
     S.facet_list = S.facet_tail = 0;
     if (L.fail || n < 4) S.status = QHS_INPUT;
     else qh_build(W, S, L, n, lane);
@@ -1351,6 +1436,7 @@ __device__ inline void qh_body(const HullArgs& A, QhL& L, bool retryq) {
     unsigned long long tq_ = __builtin_amdgcn_s_memtime();
 #endif
     qh_select(A, W, S, lane, xi, vrel, slot);
+    if (lane == 0) hull_build_note(A, slot, 1, tjob, n, S.nins, S.nalloc - 1);
 #ifdef LQRO_QHULL_PROFILE
     S.tph[10] = __builtin_amdgcn_s_memtime() - tq_;
     S.tph[11] = 1;

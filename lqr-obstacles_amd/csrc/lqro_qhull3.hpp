@@ -238,6 +238,7 @@ static_assert(sizeof(Q3L) <= 160 * 1024, "k_qhull's LDS exceeds a CU");
 
 struct Q3S {
   int nalloc, nfs, sbtop, status, qhead, qtail;
+  int nins;               // insertions (qh_addpoint calls), for the build's timing record
   unsigned keyc;
   unsigned key0_last;   // the first key of the last insertion's new facets
   int nnew, nvis, nmov, nold;
@@ -2378,6 +2379,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     const int sharp = adopt ? L.sp_sharp : q3_sharpnewfacets(S, L, lane);
     Q3T(20);
     Q3C(21, 1);
+    S.nins++;
     Q3C(31, adopt ? 1 : 0);   // insertions whose horizon and cone wave 1 speculated
     Q3C(22, np2);
     if (np2) {
@@ -2444,17 +2446,61 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
   }
 }
 
+// LQRO_REC_QHMERGE_WIN (a build where Qhull's merge tests fired): does a
+// facet within 1e-6 of the winning distance have a hull vertex other than its
+// own within 1e-9 (|coord|max + 1) of its plane — a facet qconvex's
+// pre-merge may have joined with a neighbour, so that the reference's winner
+// may be a merged facet?  The same test as the oracle's (lqro_oracle.c
+// orc_hull_branch_ref); wave-uniform.
+__device__ inline bool q3_merge_suspect(const Q3W& W, const Q3L& L, const Q3S& S, int lane, const double* vrel,
+                                        double best) {
+  const double T = -1e-9 * (S.MAXabs_coord + 1.0);
+  bool sus = false;
+  for (int f0 = 1; f0 < S.nalloc; f0 += 64) {
+    const int f = f0 + lane;
+    double q[4] = {0.0, 0.0, 0.0, 0.0};
+    bool con = false;
+    if (f < S.nalloc && (q3_fa(W, L, f) & QF_LIVE)) {
+      q3_pl(W, L, f, q);
+      const double* P = W.Pf + 3 * (size_t)W.vv[f].id[0];
+      con = fabs(q[0] * (vrel[0] - P[0]) + q[1] * (vrel[1] - P[1]) + q[2] * (vrel[2] - P[2])) <= best + 1e-6;
+    }
+    unsigned long long m = __ballot(con);
+    while (m) {
+      const int src = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      const int fc = __shfl(f, src);
+      double qc[4];
+      for (int k = 0; k < 4; k++) qc[k] = __shfl(q[k], src);
+      const int a = W.vv[fc].id[0], b = W.vv[fc].id[1], c = W.vv[fc].id[2];
+      for (int g = 1 + lane; g < S.nalloc; g += 64) {
+        if (!(q3_fa(W, L, g) & QF_LIVE)) continue;
+        for (int t = 0; t < 3; t++) {
+          const int id = W.vv[g].id[t];
+          if (id == a || id == b || id == c) continue;
+          if (q3_distq(qc, W.Pr + 3 * (size_t)id) >= T) sus = true;
+        }
+      }
+    }
+  }
+  return __ballot(sus) != 0;
+}
+
 // the reference's selection (LQRO:925-968; lqro_qhull.hpp qh_select) over
 // the finished hull: Qhull's facet order is key order, so a tie goes to the
-// smaller key and facet 0 is the smallest key alive
+// smaller key and facet 0 is the smallest key alive.  The planes are the ones
+// convexHull reads back (16 significant digits, lqro_dec16.hpp): a first pass
+// at full precision bounds every facet's distance within rounding (qsel_bound),
+// a second one evaluates the facets that can still be the minimum with the
+// read-back planes
 // returns (wave-uniform) whether this job closed its row and claimed the
 // row's LP (hull_row_done)
 __device__ inline bool q3_select(const HullArgs& A, const Q3W& W, const Q3L& L, const Q3S& S, int lane,
                                  const double* xi, const double* vrel, int slot) {
   const bool fail = (S.status & (QHS_INPUT | QHS_TOPOLOGY | QHS_CAPACITY)) != 0;
-  double best = INFINITY;
-  unsigned bkey = 0xffffffffu, minkey = 0xffffffffu;
-  int bf = -1, nfac = 0;
+  double ub = INFINITY;
+  unsigned minkey = 0xffffffffu;
+  int nfac = 0;
   if (!fail) {
     for (int f0 = 1; f0 < S.nalloc; f0 += 256) {
       // four slots a lane: their first vertices' points in one round trip
@@ -2475,8 +2521,37 @@ __device__ inline bool q3_select(const HullArgs& A, const Q3W& W, const Q3L& L, 
         double q[4];
         q3_pl(W, L, f, q);
         const double* P = W.Pf + 3 * (size_t)v[u];
-        const double d = fabs(q[0] * (vrel[0] - P[0]) + q[1] * (vrel[1] - P[1]) + q[2] * (vrel[2] - P[2]));
-        if (d < best || (d == best && k < bkey)) { best = d; bkey = k; bf = f; }
+        double b;
+        const double d = qsel_dist(q, P, vrel, &b);
+        ub = fmin(ub, d + b);
+      }
+    }
+  }
+  for (int off = 32; off >= 1; off >>= 1) {
+    const unsigned om = (unsigned)__shfl_xor((int)minkey, off);
+    nfac += __shfl_xor(nfac, off);
+    minkey = om < minkey ? om : minkey;
+    ub = fmin(ub, __shfl_xor(ub, off));
+  }
+  // the facets within rounding of the minimum, with the read-back planes
+  double best = INFINITY, bn[3] = {0.0, 0.0, 0.0};
+  unsigned bkey = 0xffffffffu;
+  int bf = -1;
+  if (!fail) {
+    for (int f = 1 + lane; f < S.nalloc; f += 64) {
+      if (!(q3_fa(W, L, f) & QF_LIVE)) continue;
+      double q[4];
+      q3_pl(W, L, f, q);
+      const double* P = W.Pf + 3 * (size_t)W.vv[f].id[0];
+      double b;
+      const double d0 = qsel_dist(q, P, vrel, &b);
+      if (d0 - b > ub) continue;
+      double n16[3];
+      const double d = qsel_dist16(q, P, vrel, n16);
+      const unsigned k = q3_key(W, L, f);
+      if (d < best || (d == best && k < bkey)) {
+        best = d; bkey = k; bf = f;
+        bn[0] = n16[0]; bn[1] = n16[1]; bn[2] = n16[2];
       }
     }
   }
@@ -2484,27 +2559,23 @@ __device__ inline bool q3_select(const HullArgs& A, const Q3W& W, const Q3L& L, 
     const double ob = __shfl_xor(best, off);
     const unsigned ok = (unsigned)__shfl_xor((int)bkey, off);
     const int of = __shfl_xor(bf, off);
-    const unsigned om = (unsigned)__shfl_xor((int)minkey, off);
-    nfac += __shfl_xor(nfac, off);
-    minkey = om < minkey ? om : minkey;
-    if (ob < best || (ob == best && ok < bkey)) { best = ob; bkey = ok; bf = of; }
+    const double o0 = __shfl_xor(bn[0], off), o1 = __shfl_xor(bn[1], off), o2 = __shfl_xor(bn[2], off);
+    if (ob < best || (ob == best && ok < bkey)) { best = ob; bkey = ok; bf = of; bn[0] = o0; bn[1] = o1; bn[2] = o2; }
   }
   const bool ok = !fail && nfac > 0 && bf >= 0;
   const bool stale = ok && bkey == minkey;
   const bool merged = (S.status & (QHS_COPLANAR | QHS_NONCONVEX | QHS_FLIPPED | QHS_NARROW | QHS_SINGULAR)) != 0;
-  double bq[4] = {0.0, 0.0, 0.0, 0.0};
+  const bool mwin = ok && merged && q3_merge_suspect(W, L, S, lane, vrel, best);
   int bv[3] = {0, 0, 0};
-  if (ok) {
-    q3_pl(W, L, bf, bq);
+  if (ok)
     for (int t = 0; t < 3; t++) bv[t] = W.vv[bf].id[t];
-  }
   int go = 0;
   if (lane == 0) {
     float* pl = A.planes + (size_t)slot * 8;
     double* qn = A.qnrm + (size_t)slot * 4;
     double nrm[3] = {0.0, 0.0, 0.0};
     if (ok && !stale) {
-      nrm[0] = bq[0]; nrm[1] = bq[1]; nrm[2] = bq[2];
+      nrm[0] = bn[0]; nrm[1] = bn[1]; nrm[2] = bn[2];
       const double dh = best * 0.5;                      // :1416
       const double mult = 1.0;                           // :1213
       pl[0] = (float)(xi[3] + mult * dh * nrm[0]);
@@ -2525,11 +2596,13 @@ __device__ inline bool q3_select(const HullArgs& A, const Q3W& W, const Q3L& L, 
       hull_fail_note(A.stats, slot);
     }
     if (ok && merged) atomicAdd(&A.stats[LQRO_ST_MERGED], 1ull);
+    if (mwin) atomicAdd(&A.stats[LQRO_ST_MWIN], 1ull);
     if (A.recs) {
       lqro_pair_record& rec = A.recs[slot];
       rec.flags |= ok ? LQRO_REC_HULL : LQRO_REC_HULLFAIL;
       if (stale) rec.flags |= LQRO_REC_STALE;
       if (merged) rec.flags |= LQRO_REC_QHMERGE;
+      if (mwin) rec.flags |= LQRO_REC_QHMERGE_WIN;
       rec.n_facets = ok ? nfac : -(S.status & 0xffff) - 1;
       if (ok) {
         rec.facet[0] = bv[0]; rec.facet[1] = bv[1]; rec.facet[2] = bv[2];
@@ -2582,6 +2655,7 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
   for (;;) {
     const int slot = hull_take_job(A, L, false);
     if (slot < 0) break;
+    const unsigned long long tjob = __builtin_amdgcn_s_memrealtime();   // (lqro_get_hull_builds)
     // a fresh handshake and wave 1's epochs for this job (ordered by
     // hull_points' barriers)
     if (threadIdx.x == 0) { L.ph = 0; L.sp_done = 0; L.sp_gdone = 0; L.hstate = 0; L.sp_hz = 0; L.pf_done = 0; }
@@ -2700,6 +2774,7 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
 #endif
     S.status = 0;
     S.nalloc = 1;
+    S.nins = 0;
     if (L.fail || n < 4) S.status = QHS_INPUT;
     else q3_build(W, S, L, n, lane);
     hl_sync();
@@ -2710,6 +2785,7 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
         if (S.status & QHS_TIMEOUT) atomicAdd(&A.stats[LQRO_ST_TIMEOUT], 1ull);
         const int r = atomicAdd(A.rcount, 1);
         if (r < A.cap) A.rqueue[r] = slot;
+        hull_build_note(A, slot, 2, tjob, n, S.nins, S.nalloc - 1);
 #ifdef LQRO_QHULL_PROFILE
         // the builds handed to k_qhull_big: count, the caps they hit, slots
         if (A.prof) {
@@ -2725,6 +2801,7 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
     unsigned long long tq_ = __builtin_amdgcn_s_memtime();
 #endif
     lp_go = q3_select(A, W, L, S, lane, xi, vrel, slot);
+    if (lane == 0) hull_build_note(A, slot, 0, tjob, n, S.nins, S.nalloc - 1);
 #ifdef LQRO_QHULL_PROFILE
     S.tph[10] = __builtin_amdgcn_s_memtime() - tq_;
     S.tph[27] = __builtin_amdgcn_s_memtime() - tjob_;   // the whole job (26: its max over jobs)

@@ -425,6 +425,7 @@ struct lqro_ctx {
   char* d_qscratch;
   double* d_qnrm;
   int* d_qstale;
+  unsigned long long* d_hbuild;   // LQRO_HBUILD_CAP x 4 words: the builds' timing records
   double* d_carry;
   // early LP (LQRO_EARLY_LP, default 1): per row open work and LP claim
   // (lqro_hull.hpp hull_row_done)
@@ -468,7 +469,7 @@ const char* lqro_status_string(int s) {
     case LQRO_E_SINGULAR: return "singular C*G_k";
     case LQRO_E_NODEVICE: return "no gfx950 device";
     case LQRO_E_OVERFLOW: return "work queue overflow";
-    case LQRO_E_HULL: return "an inside-hull pair's hull exceeded the kernel's capacity (lqro_get_hull_failures)";
+    case LQRO_E_HULL: return "an inside-hull pair's hull could not be built (degenerate input or capacity; lqro_get_hull_failures)";
   }
   return "unknown";
 }
@@ -497,7 +498,7 @@ void lqro_destroy(lqro_ctx* c) {
   void* ps[] = {c->d_R, c->d_TF, c->d_shash, c->d_T, c->d_NCF, c->d_S, c->d_x, c->d_vgoal, c->d_newv, c->d_A, c->d_B,
                 c->d_L, c->d_E, c->d_planes, c->d_lpscratch, c->d_lpcompact, c->d_recs, c->d_hq, c->d_hcount,
                 c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats, c->d_prof, c->d_rq, c->d_hbig, c->d_hwide, c->d_hbag, c->d_lp4, c->d_hotlist, c->d_hotmark, c->d_nbrlist, c->d_hfbest, c->d_hvpid, c->d_hstack, c->d_lq,
-                c->d_qscratch, c->d_qnrm, c->d_qstale, c->d_carry, c->d_rowpend /* d_rowclaim inside */};
+                c->d_qscratch, c->d_qnrm, c->d_qstale, c->d_hbuild, c->d_carry, c->d_rowpend /* d_rowclaim inside */};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (int k = 0; k < 5; ++k)
@@ -585,6 +586,7 @@ static int ctx_alloc(lqro_ctx* c) {
     HIPCHK(hipMemset(c->d_qscratch, 0, c->qstride * (size_t)c->qworkers));   // k_qhull_big's visit stamps
     HIPCHK(hipMalloc(&c->d_qnrm, sizeof(double) * 4 * (slots ? slots : 1)));
     HIPCHK(hipMalloc(&c->d_qstale, sizeof(int) * (slots ? slots : 1)));
+    HIPCHK(hipMalloc(&c->d_hbuild, sizeof(unsigned long long) * 4 * LQRO_HBUILD_CAP));
   }
   return LQRO_OK;
 }
@@ -968,6 +970,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   Hh.rowpend = P.rowpend; Hh.rowclaim = early ? c->d_rowclaim : nullptr;
   Hh.row_target = P.row_split * LQRO_ROW_BIG;
   Hh.lp_vgoal = d_vgoal; Hh.lp_newv = d_newv; Hh.lp_vmax = g.vmax_lp;
+  Hh.hbuild = c->d_hbuild; Hh.hbuild_cap = LQRO_HBUILD_CAP;
   if (g.x_dim != 16 && g.x_dim != 12) return LQRO_E_ARG;
   // the row launch is submitted before the side stream's work: should the two
   // streams land on one hardware queue (a second context in the process), the
@@ -1409,7 +1412,48 @@ int lqro_get_stats_ex(lqro_ctx* c, int64_t* st, int32_t n) {
   unsigned long long h[LQRO_ST_FAILS];
   HIPCHK(hipMemcpy(h, c->d_stats, sizeof h, hipMemcpyDeviceToHost));
   if (c->nbr_k <= 0) h[0] = (unsigned long long)c->nrows * c->npr;   // else k_nbr counted the kept pairs
-  for (int k = 0; k < n; ++k) st[k] = k < LQRO_ST_NFAIL ? (int64_t)h[k] : 0;
+  // [0..10] the device words; [11] LQRO_REC_QHMERGE_WIN pairs (device word
+  // LQRO_ST_MWIN; word 11 counts the failures lqro_get_hull_failures names)
+  for (int k = 0; k < n; ++k)
+    st[k] = k < LQRO_ST_NFAIL ? (int64_t)h[k] : k == 11 ? (int64_t)h[LQRO_ST_MWIN] : 0;
+  return LQRO_OK;
+}
+
+int lqro_get_hull_builds(lqro_ctx* c, lqro_hull_build* out, int64_t cap, int64_t* n_out) {
+  if (!c || !n_out || (cap > 0 && !out)) return LQRO_E_ARG;
+  if (c->pending) return LQRO_E_STATE;
+  HIPCHK(hipSetDevice(c->cfg.device));
+  HIPCHK(wait_last_step(c));
+  *n_out = 0;
+  if (!c->d_hbuild) return LQRO_OK;   // not in Qhull order: no builds
+  unsigned long long h[LQRO_ST_FAILS];
+  HIPCHK(hipMemcpy(h, c->d_stats, sizeof h, hipMemcpyDeviceToHost));
+  const int64_t n = (int64_t)h[LQRO_ST_NBUILD];
+  *n_out = n;
+  const int64_t m = std::min<int64_t>(std::min<int64_t>(n, LQRO_HBUILD_CAP), cap);
+  if (m <= 0) return LQRO_OK;
+  std::vector<unsigned long long> r(4 * (size_t)m);
+  HIPCHK(hipMemcpy(r.data(), c->d_hbuild, sizeof(unsigned long long) * r.size(), hipMemcpyDeviceToHost));
+  const int npr = c->nbr_k > 0 ? std::min(c->nbr_k, c->npr) : c->npr;
+  std::vector<int> nbr;
+  if (c->nbr_k > 0) {   // culled rows: slot -> neighbour index
+    nbr.resize((size_t)c->nrows * npr);
+    HIPCHK(hipMemcpy(nbr.data(), c->d_nbrlist, sizeof(int) * nbr.size(), hipMemcpyDeviceToHost));
+  }
+  for (int64_t k = 0; k < m; ++k) {
+    const unsigned long long* w = &r[4 * (size_t)k];
+    const long slot = (long)(w[0] & 0xFFFFFFFFFFull);
+    const int lrow = (int)(slot / npr), jj = nbr.empty() ? (int)(slot % npr) : nbr[slot];
+    lqro_hull_build& b = out[k];
+    b.i = c->rb + lrow * c->rs;
+    b.j = jj < b.i ? jj : jj + 1;
+    b.kernel = (int32_t)(w[0] >> 40);
+    b.t_start = w[1];
+    b.t_end = w[2];
+    b.n_points = (int32_t)(w[3] & 0xFFFFF);
+    b.insertions = (int32_t)((w[3] >> 20) & 0xFFFFF);
+    b.facet_slots = (int32_t)((w[3] >> 40) & 0xFFFFF);
+  }
   return LQRO_OK;
 }
 

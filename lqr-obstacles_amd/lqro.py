@@ -25,11 +25,15 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liblqro.so")
 
 LQRO_OK = 0
-LQRO_E_HULL = -8              # an inside-hull pair's hull exceeded the kernels' capacity (no half-plane)
+LQRO_E_HULL = -8              # an inside-hull pair's hull could not be built (degenerate input or capacity; no half-plane)
 LQRO_FLAG_RECORDS = 0x1
 LQRO_FLAG_QHULL_ORDER = 0x2   # the reference's own hull rule over Qhull's build order (k_qhull)
 REC_PLANE, REC_INSIDE, REC_BACKUP, REC_HULL, REC_HULLFAIL, REC_LOCAL = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20
 REC_STALE, REC_QHMERGE = 0x40, 0x80
+REC_QHMERGE_WIN = 0x100       # with REC_QHMERGE: qconvex's pre-merge may have merged the winning facet
+HULL_BUILD_DTYPE = np.dtype([("i", np.int32), ("j", np.int32), ("n_points", np.int32), ("insertions", np.int32),
+                             ("facet_slots", np.int32), ("kernel", np.int32), ("t_start", np.uint64),
+                             ("t_end", np.uint64)])
 
 
 class Config(C.Structure):
@@ -79,7 +83,7 @@ EXPORTS = (
     "lqro_synthesize_gains_x", "lqro_synthesize_gains_batch_x",
     "lqro_set_carry_normal", "lqro_get_carry_normal",
     "lqro_step_device_begin", "lqro_step_device_end",
-    "lqro_get_stats_ex", "lqro_get_hull_failures",
+    "lqro_get_stats_ex", "lqro_get_hull_failures", "lqro_get_hull_builds",
 )
 
 NORMALS_PER_AGENT = 22   # LQRO_NORMALS_PER_AGENT: 16 propagate + 6 observation
@@ -140,8 +144,9 @@ class LqroError(RuntimeError):
 
 
 class HullFailure(LqroError):
-    """lqro_step returned LQRO_E_HULL: inside-hull pairs whose hull exceeded
-    the in-kernel hull's capacity got no half-plane (the reference's qconvex
+    """lqro_step returned LQRO_E_HULL: inside-hull pairs whose hull could not
+    be built (degenerate or too few points, or every hull kernel's capacity
+    exceeded) got no half-plane (the reference's qconvex
     always returns a hull, LQRO:879-880).  .pairs: their (i, j); .newv: the
     step's new velocities, computed without those planes."""
 
@@ -329,11 +334,21 @@ class Context:
         return out[:got.value]   # rows x K with neighbour culling on
 
     def stats(self) -> dict:
-        s = np.zeros(11, dtype=np.int64)
-        _check(lib().lqro_get_stats_ex(self._h, _p(s), 11), "lqro_get_stats_ex")
+        s = np.zeros(12, dtype=np.int64)
+        _check(lib().lqro_get_stats_ex(self._h, _p(s), 12), "lqro_get_stats_ex")
         keys = ("pairs", "planes", "inside", "hull_ok", "hull_fail", "gjk_backups",
-                "sum_n_reach", "sum_gtests", "qhull_merged", "qhull_retried", "qhull_timeouts")
+                "sum_n_reach", "sum_gtests", "qhull_merged", "qhull_retried", "qhull_timeouts",
+                "qhull_merge_win")
         return dict(zip(keys, (int(v) for v in s)))
+
+    def hull_builds(self) -> np.ndarray:
+        """LQRO_FLAG_QHULL_ORDER: the last step's hull builds (lqro_get_hull_builds):
+        i, j, n_points, insertions, facet_slots, kernel (0 k_qhull, 1 k_qhull_big,
+        2 a k_qhull build handed over), t_start / t_end in 100 MHz ticks."""
+        out = np.zeros(16384, dtype=HULL_BUILD_DTYPE)
+        n = C.c_int64()
+        _check(lib().lqro_get_hull_builds(self._h, _p(out), len(out), C.byref(n)), "lqro_get_hull_builds")
+        return out[:min(n.value, len(out))]
 
     def carry_normal(self, n=None):
         """LQRO_FLAG_QHULL_ORDER: get (n=None) the loop-carried normalVector

@@ -1050,6 +1050,7 @@ int orc_hull_branch(int n, const double* pts_full, const double vrel[3], double*
  * facets; the hull was built on merge-free).  Returns the facet count or
  * <= 0 on failure. */
 static int g_hull_rule = 0, g_round16 = 0;
+#define ORC_QH_MERGE_WIN 0x10000   /* orc_hull_branch_ref's *qstatus: LQRO_REC_QHMERGE_WIN */
 static long long g_hull_ns = 0, g_hull_count = 0;
 
 /* time spent in the hull branch and inside-hull pairs since the last reset */
@@ -1098,6 +1099,29 @@ int orc_hull_branch_ref(int n, const double* pts_full, const double vrel[3], dou
   *dist = d;
   *stale = best == 0;
   for (int k = 0; k < 3; k++) facet[k] = o.fv[3 * best + k];
+  /* LQRO_REC_QHMERGE_WIN (reported as *qstatus bit ORC_QH_MERGE_WIN): Qhull's
+   * merge tests fired in this build and a facet within 1e-6 of the winning
+   * distance has another hull vertex within 1e-9 (|coord|max + 1) of its
+   * plane, so qconvex's pre-merge may have joined the winner into a merged
+   * facet (the GPU's q3_merge_suspect / qh_merge_suspect, same arithmetic) */
+  if (o.status) {
+    double maxabs = 0.0;
+    for (int i = 0; i < 3 * n; i++) maxabs = fabs(rp[i]) > maxabs ? fabs(rp[i]) : maxabs;
+    const double T = -1e-9 * (maxabs + 1.0);
+    int sus = 0;
+    for (int f = 0; f < nf && !sus; f++) {
+      const double* q = o.plane + 4 * f;
+      const double* P = pts_full + 3 * (size_t)o.fv[3 * f];
+      if (!(fabs(q[0] * (vrel[0] - P[0]) + q[1] * (vrel[1] - P[1]) + q[2] * (vrel[2] - P[2])) <= d + 1e-6)) continue;
+      for (int g = 0; g < 3 * nf && !sus; g++) {
+        const int id = o.fv[g];
+        if (id == o.fv[3 * f] || id == o.fv[3 * f + 1] || id == o.fv[3 * f + 2]) continue;
+        const double* p = rp + 3 * (size_t)id;
+        if (q[3] + p[0] * q[0] + p[1] * q[1] + p[2] * q[2] >= T) sus = 1;
+      }
+    }
+    if (sus) *qstatus |= ORC_QH_MERGE_WIN;
+  }
   orc_qhull_free(&o);
   free(rp);
   return nf;
@@ -1178,6 +1202,7 @@ int orc_pair(int X, int H, int NP, int min_reach, double vmax_reach, const doubl
       rec->n_facets = nf;
       if (nf > 0) rec->flags |= LQRO_REC_HULL; else rec->flags |= LQRO_REC_HULLFAIL;
       if (qst) rec->flags |= LQRO_REC_QHMERGE;
+      if (qst & ORC_QH_MERGE_WIN) rec->flags |= LQRO_REC_QHMERGE_WIN;
       if (stale) {   /* normalVector keeps the previous pair's value: resolved by the row loop */
         rec->flags |= LQRO_REC_STALE;
         normal[0] = normal[1] = normal[2] = 0.0;

@@ -325,10 +325,12 @@ def qhull(points: np.ndarray, keep_going: bool = False):
     return st, fv, pl, fid
 
 
-def set_hull_rule(rule: int, round16: bool = False):
+def set_hull_rule(rule: int, round16: bool = True):
     """0: the canonical rule (default); 1: the reference's rule over Qhull's
     order (orc_hull_branch_ref), loop-carried normal resolved in row order.
-    round16: planes read back as qconvex prints them (%.16g).  Process-wide."""
+    round16: planes read back as qconvex prints them (%.16g, LQRO:889-899:
+    the reference's own rule and the GPU's, lqro_dec16.hpp; False keeps
+    Qhull's doubles, for diagnostics).  Process-wide."""
     o = lib()
     o.orc_set_hull_rule.argtypes = [C.c_int, C.c_int]
     o.orc_set_hull_rule(int(rule), int(round16))

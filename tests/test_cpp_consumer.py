@@ -61,7 +61,7 @@ def test_cpp_consumer_matches_oracle(demo, lqro_mod, oracle, tmp_path):
     ref["vgoal"][:] = vg
     sd = seed
     # lqro::Simulator takes lqro_config_default: the reference's own hull rule
-    oracle.set_hull_rule(1, round16=False)
+    oracle.set_hull_rule(1, round16=True)
     oracle.carry_normal(np.zeros(3))
     try:
         for t in range(steps):

@@ -156,7 +156,7 @@ def test_c5_qhull_order_largest_hulls(lqro_mod, oracle, c5):
     ctx.close()
     assert st["hull_fail"] == 0 and st["inside"] > 500, st
     S = oracle.sphere(c["NP"])
-    oracle.set_hull_rule(1, round16=False)
+    oracle.set_hull_rule(1, round16=True)
     try:
         for r in (3014, 3155, 5156):
             ctx = lqro_mod.Context(lqro_mod.config(c["N"], c["H"], c["NP"], x_dim=c["X"], row_begin=r, row_end=r + 1,

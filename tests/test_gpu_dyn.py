@@ -215,7 +215,7 @@ def test_simulator_loop(lqro_mod, oracle, tmp_path):
     S = oracle.sphere(NP)
     seed = seed_ref = 3
     # the Simulator runs the reference's own hull rule (LQRO_FLAG_QHULL_ORDER)
-    oracle.set_hull_rule(1, round16=False)
+    oracle.set_hull_rule(1, round16=True)
     oracle.carry_normal(np.zeros(3))
     try:
         for t in range(2):

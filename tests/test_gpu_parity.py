@@ -26,7 +26,7 @@ def _oracle_step(oracle, rule, *a, **kw):
     """oracle.step under the hull rule (Qhull order: the carried normal
     entering the step is 0, as a fresh context's)."""
     if rule == "qhull":
-        oracle.set_hull_rule(1, round16=False)
+        oracle.set_hull_rule(1, round16=True)
         oracle.carry_normal(np.zeros(3))
     try:
         return oracle.step(*a, **kw)

@@ -1,0 +1,181 @@
+"""The default rule (LQRO_FLAG_QHULL_ORDER: Qhull's build order, the planes
+read back at 16 digits, first Fv vertex, strict '<', the loop-carried normal;
+LQRObstacles.cpp:867-969, 1385) pinned at the sizes where the canonical rule
+was pinned:
+
+- C3 (1024 agents, H = 100: 1,047,552 pairs): every record and every row's
+  newV bit for bit against the oracle in set_hull_rule(1), in every schedule
+  the step can take there — the default (hot launch, side builds, early LP:
+  the row-counting protocol of lqro_hull.hpp hull_row_done that closes a row
+  and runs its LP inside k_qhull), LQRO_EARLY_LP=0, LQRO_QSIDE=1 (side
+  workers sweep rows after their builds) and LQRO_HOT=0 (plain);
+- C5 (16384 agents, X = 12, H = 200, per-agent gains): the 8-way shard
+  [0, 2048) in Qhull order on the GPU, 32 rows' newV against the oracle, each
+  entered with the loop-carried normal the shard's rows before it left (the
+  row-normal table of lqro_step_device_begin);
+- qconvex's merged winners (tests/golden/qhull_merge.npz, live Qhull): the
+  pairs are flagged LQRO_REC_QHMERGE_WIN, as the oracle flags them;
+- the per-build timing records (lqro_get_hull_builds)."""
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from test_gpu_parity import _compare
+
+pytestmark = pytest.mark.gpu
+
+QFIELDS = ("n_reach", "reach_hash", "flags", "facet", "n_facets", "dist", "normal", "plane_point", "plane_normal",
+           "gjk_iters", "simplex_n", "simplex", "wpt_vrel", "wpt_hull")
+
+
+def _bits(a):
+    return np.ascontiguousarray(a).view(np.uint8) if a.dtype.kind == "f" else a
+
+
+@pytest.fixture(scope="module")
+def c3_oracle(lqro_mod, oracle, gains):
+    N, H = 1024, 100
+    x, vg = lqro_mod.synthetic_swarm(N)
+    T, NCF = oracle.tables(gains["A"], gains["B"], gains["L"], gains["E"], H)
+    oracle.set_hull_rule(1, round16=True)
+    oracle.carry_normal(np.zeros(3))
+    try:
+        rv, rr = oracle.step(T, NCF, oracle.sphere(100), x, vg, threads=16)
+        carry = oracle.carry_normal()
+    finally:
+        oracle.set_hull_rule(0)
+    return x, vg, rv, rr, carry
+
+
+@pytest.mark.parametrize("sched", ["default", "early_lp_off", "qside", "plain"])
+def test_qhull_order_c3_full_step(lqro_mod, gains, monkeypatch, c3_oracle, sched):
+    x, vg, rv, rr, carry = c3_oracle
+    env = {"default": {}, "early_lp_off": {"LQRO_EARLY_LP": "0"}, "qside": {"LQRO_QSIDE": "1"},
+           "plain": {"LQRO_HOT": "0"}}[sched]
+    for k in ("LQRO_EARLY_LP", "LQRO_QSIDE", "LQRO_HOT", "LQRO_LOCAL_HULL", "LQRO_SIDE_HULL_CUS"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    N = x.shape[0]
+    ctx = lqro_mod.Context(lqro_mod.config(N, 100, 100,
+                                           flags=lqro_mod.LQRO_FLAG_RECORDS | lqro_mod.LQRO_FLAG_QHULL_ORDER))
+    ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
+    try:
+        # three steps, each entered with the normal 0 (as the oracle's): the
+        # schedule adapts to the inside-hull count of the step two before, so
+        # the third is the steady state
+        for t in range(3):
+            ctx.carry_normal(np.zeros(3))
+            v = ctx.step(x, vg)
+            r = ctx.records()
+            st = ctx.stats()
+            assert st["hull_fail"] == 0 and st["qhull_timeouts"] == 0
+            _compare(r, rr)
+            ins = (rr["flags"] & lqro_mod.REC_INSIDE) != 0
+            assert ins.sum() > 100
+            for f in QFIELDS:
+                a, b = r[f], rr[f]
+                if f == "flags":
+                    a = a & ~lqro_mod.REC_LOCAL
+                assert np.array_equal(_bits(a), _bits(b)), (sched, t, f)
+            assert np.array_equal(v.view(np.uint64), rv.view(np.uint64)), (sched, t)
+            assert np.array_equal(ctx.carry_normal(), carry)
+    finally:
+        ctx.close()
+
+
+def test_c5_qhull_order_rows(lqro_mod, oracle):
+    """C5's first 8-way shard in Qhull order: 32 rows spread over it against
+    the oracle, bit for bit, each row entered with the normal the rows before
+    it left (the row-normal table: a facet-0 pair at the top of a row takes
+    the previous rows' last normal, LQRO:1385)."""
+    from test_gpu_dyn import _Hip   # device buffers through liblqro's own HIP runtime
+    N, H, NP, X = 16384, 200, 100, 12
+    rows = (0, 2048)
+    models = lqro_mod.perturbed_models(N)
+    g = lqro_mod.synthesize_gains_batch(models, x_dim=X)
+    g0 = lqro_mod.synthesize_gains(x_dim=X)
+    x, vg = lqro_mod.synthetic_swarm(N, x_dim=X)
+    ctx = lqro_mod.Context(lqro_mod.config(N, H, NP, x_dim=X, row_begin=rows[0], row_end=rows[1],
+                                           flags=lqro_mod.LQRO_FLAG_QHULL_ORDER))
+    ctx.set_gains(g0["A"], g0["B"], g["L"], g["E"], per_agent=True)
+    hip = _Hip()
+    zt, zv = np.zeros((N, 4)), np.zeros((N, 3))
+    d_x, d_vg, d_tab, d_nv = hip.put(x), hip.put(vg), hip.put(zt), hip.put(zv)
+    ctx.step_device_begin(d_x, d_vg, d_tab, 0)
+    ctx.step_device_end(d_tab, d_nv, 0)
+    hip.sync()
+    st = ctx.stats()
+    ctx.close()
+    newv, tab = hip.get(d_nv, zv), hip.get(d_tab, zt)
+    assert st["hull_fail"] == 0 and st["inside"] > 500, st
+    own = newv[rows[0]:rows[1]]
+    assert np.isfinite(own).all()
+    S = oracle.sphere(NP)
+    oracle.set_hull_rule(1, round16=True)
+    T = np.zeros((N, H, 9))
+    NCF = np.zeros((N, H, 3, X))
+    try:
+        for r in range(7, 2048, 64):
+            prev = [q for q in range(rows[0], r) if tab[q, 3] != 0]
+            carry = tab[prev[-1], :3] if prev else np.zeros(3)
+            T[r], NCF[r] = oracle.tables(g0["A"], g0["B"], g["L"][r], g["E"][r], H, X=X)
+            oracle.carry_normal(carry)
+            rv, _ = oracle.step(T, NCF, S, x, vg, rows=(r, r + 1), per_agent=True, threads=16, records=False)
+            assert np.array_equal(newv[r].view(np.uint64), rv[r].view(np.uint64)), r
+            if tab[r, 3] != 0:
+                assert np.array_equal(oracle.carry_normal(), tab[r, :3]), r
+    finally:
+        oracle.set_hull_rule(0)
+
+
+def test_merged_winners_are_flagged(lqro_mod, oracle, gains):
+    """Inputs where qconvex's pre-merge joins the winning facet (coplanar
+    cube faces, a flattened cap; tests/golden/make_golden_merge.py over live
+    Qhull): k_qhull (built merge-free) flags each LQRO_REC_QHMERGE and
+    LQRO_REC_QHMERGE_WIN, exactly as the oracle does, and its selection
+    equals the oracle's merge-free one bit for bit."""
+    d = np.load(f"{GOLDEN}/qhull_merge.npz")
+    ctx = lqro_mod.Context(lqro_mod.config(2, 100, 100))
+    ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
+    oracle.set_hull_rule(1, round16=True)
+    try:
+        for c in ("cube_top", "cube_side", "capped"):
+            assert d[f"{c}_expect"][1] == 1, c           # qconvex's winner is a merged facet
+            rec, st = ctx.debug_qhull(d[f"{c}_rounded"], d[f"{c}_pts"], d[f"{c}_vrel"])
+            nf, dist, nrm, fac, qst = oracle.hull_branch_ref(d[f"{c}_pts"], d[f"{c}_vrel"])
+            assert qst & 0x10000, c
+            assert rec["flags"] & lqro_mod.REC_QHMERGE and rec["flags"] & lqro_mod.REC_QHMERGE_WIN, (c, rec["flags"])
+            assert rec["n_facets"] == nf and list(rec["facet"]) == list(fac) and rec["dist"] == dist, c
+            if nrm is not None:
+                assert np.array_equal(rec["normal"], nrm), c
+    finally:
+        oracle.set_hull_rule(0)
+        ctx.close()
+
+
+def test_hull_build_records(lqro_mod, gains):
+    """lqro_get_hull_builds: one record per inside-hull pair of the step,
+    naming the pair, with its insertions, facets and a positive duration on
+    the 100 MHz clock; the counts agree with the pair records."""
+    N = 256
+    x, vg = lqro_mod.synthetic_swarm(N, box=12.0, seed=3)
+    ctx = lqro_mod.Context(lqro_mod.config(N, 100, 100,
+                                           flags=lqro_mod.LQRO_FLAG_RECORDS | lqro_mod.LQRO_FLAG_QHULL_ORDER))
+    ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
+    try:
+        ctx.step(x, vg)
+        r = ctx.records()
+        b = ctx.hull_builds()
+    finally:
+        ctx.close()
+    ins = r[(r["flags"] & lqro_mod.REC_INSIDE) != 0]
+    assert len(ins) > 10
+    done = b[b["kernel"] != 2]
+    assert len(done) == len(ins)
+    assert sorted(zip(done["i"].tolist(), done["j"].tolist())) == sorted(zip(ins["i"].tolist(), ins["j"].tolist()))
+    assert (done["insertions"] > 4).all() and (done["facet_slots"] > done["insertions"]).all()
+    assert (done["t_end"] > done["t_start"]).all()
+    by = {(int(q["i"]), int(q["j"])): q for q in ins}
+    for q in done:
+        assert q["n_points"] == by[(int(q["i"]), int(q["j"]))]["n_reach"]

@@ -7,8 +7,9 @@ strict '<', the loop-carried normalVector when facet 0 wins
   live Qhull in tests/test_qhull_order.py), bit for bit: records (facet in
   Fv order, distance, normal, flags, half-plane) and new velocities;
 - tests/golden/qhull_order.npz, the reference's pair loop over live Qhull
-  (planes read back as qconvex prints them, %.16g): the same facets, the
-  distances and normals within 1e-12, every row's newV within 1e-5."""
+  (planes read back as qconvex prints them, %.16g — the GPU reads them back
+  the same way, lqro_dec16.hpp): the same facets, distances, normals and
+  every row's newV, bit for bit."""
 import os
 
 import numpy as np
@@ -31,7 +32,7 @@ def test_qhull_hook_on_injected_pairs(lqro_mod, oracle, gains):
     d = _golden()
     ctx = lqro_mod.Context(lqro_mod.config(2, 45, 100))
     ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
-    oracle.set_hull_rule(1, round16=False)
+    oracle.set_hull_rule(1, round16=True)
     try:
         for k in range(6):
             pts, rounded, fv = d[f"inject{k}_pts"], d[f"inject{k}_rounded"], d[f"inject{k}_fv"]
@@ -50,7 +51,7 @@ def test_qhull_hook_on_injected_pairs(lqro_mod, oracle, gains):
             assert bool(rec["flags"] & lqro_mod.REC_STALE) == (nrm_o is None) == bool(stale_g)
             if nrm_o is not None:
                 assert np.array_equal(rec["normal"], nrm_o)
-            assert abs(rec["dist"] - dist_g) <= 1e-12 * max(1.0, dist_g)
+            assert rec["dist"] == dist_g, (k, rec["dist"], dist_g)   # the planes read back at 16 digits
     finally:
         oracle.set_hull_rule(0)
         ctx.close()
@@ -68,7 +69,7 @@ def test_qhull_hook_on_reference_fixture(lqro_mod, oracle, gains):
     pts = np.ascontiguousarray(pts, np.float64)
     ctx = lqro_mod.Context(lqro_mod.config(2, 100, 100))
     ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
-    oracle.set_hull_rule(1, round16=False)
+    oracle.set_hull_rule(1, round16=True)
     try:
         cen = pts.mean(0)
         for k in (None, 0, 100, 517, 1000):
@@ -107,7 +108,7 @@ def test_qhull_order_step_vs_oracle(lqro_mod, oracle, gains, case):
     x, vg, out = _ref_step(lqro_mod, oracle, gains, N, H, box, seed, steps=2)
     T, NCF = oracle.tables(gains["A"], gains["B"], gains["L"], gains["E"], H)
     S = oracle.sphere(100)
-    oracle.set_hull_rule(1, round16=False)
+    oracle.set_hull_rule(1, round16=True)
     oracle.carry_normal(np.zeros(3))
     try:
         for v, r, st, carry in out:
@@ -154,8 +155,11 @@ def test_qhull_order_vs_reference_loop(lqro_mod, oracle, gains, case):
     keep = np.array([(int(a), int(b)) not in qmerged for a, b in zip(ins["i"], ins["j"])], bool)
     assert np.array_equal(ins["n_facets"][keep], g["n_facets"][keep])
     assert np.array_equal((ins["flags"] & lqro_mod.REC_STALE) != 0, g["stale"] != 0)
-    np.testing.assert_allclose(ins["dist"], g["dist"], rtol=1e-12, atol=1e-15)
-    np.testing.assert_allclose(ins["normal"], g["normal"], rtol=0, atol=1e-14)
+    # the planes as convexHull reads them back (16 digits, LQRO:889-899): the
+    # reference loop's distances, normals and new velocities, bit for bit
+    bad_d = np.nonzero(ins["dist"].view(np.uint64) != g["dist"].view(np.uint64))[0]
+    assert len(bad_d) == 0, [(int(ins["i"][k]), int(ins["j"][k]), ins["dist"][k], g["dist"][k]) for k in bad_d[:5]]
+    assert np.array_equal(ins["normal"].view(np.uint64), g["normal"].view(np.uint64))
     gv = d[f"{case}_newv"]
-    rel = np.abs(v - gv).max(1) / np.maximum(np.abs(gv).max(1), 1e-30)
-    assert (rel <= 1e-5).all(), f"rows beyond 1e-5: {np.nonzero(rel > 1e-5)[0][:10]}"
+    bad_v = np.nonzero((v.view(np.uint64) != gv.view(np.uint64)).any(1))[0]
+    assert len(bad_v) == 0, f"rows whose newV differs from the reference loop's: {bad_v[:10]}"

@@ -113,3 +113,28 @@ def test_k_qhull_caps_and_the_wide_insertion(oracle, lqro_mod, gains):
     assert st["st_visible_max"] == 166 and st["st_new_max"] == 116, st
     assert st["st_visible_max"] <= cap["VISCAP"] and st["st_new_max"] <= cap["NEWCAP"]
     assert st["st_horizon_max"] <= cap["HZCAP"] and st["st_cop_max"] <= cap["COPCAP"]
+
+
+def test_oracle_flags_merged_winners(oracle):
+    """tests/golden/qhull_merge.npz (live Qhull, make_golden_merge.py): inputs
+    whose qconvex winner is a merged facet (coplanar cube faces, a flattened
+    cap).  The oracle's merge-free restatement must flag them (Qhull's merge
+    tests fired, and a facet within 1e-6 of the winning distance has another
+    vertex on its plane: LQRO_REC_QHMERGE_WIN, reported as qstatus bit
+    0x10000), and on the reference's fixture (no merge) it must not."""
+    d = np.load(os.path.join(GOLDEN, "qhull_merge.npz"))
+    oracle.set_hull_rule(1, round16=True)
+    try:
+        for c in ("cube_top", "cube_side", "capped"):
+            e = d[f"{c}_expect"]
+            off = d[f"{c}_fvoff"]
+            assert e[1] == 1 and off[int(e[0]) + 1] - off[int(e[0])] > 3, c   # qconvex's winner is merged
+            nf, dist, nrm, fac, qst = oracle.hull_branch_ref(d[f"{c}_pts"], d[f"{c}_vrel"])
+            assert nf > 0 and (qst & 0x7f) and (qst & 0x10000), (c, hex(qst))
+        from test_oracle_golden import _qhull_fixture
+        pts, _, _ = _qhull_fixture()
+        pts = np.ascontiguousarray(pts, np.float64)
+        nf, dist, nrm, fac, qst = oracle.hull_branch_ref(pts, pts.mean(0))
+        assert nf == 62 and qst == 0
+    finally:
+        oracle.set_hull_rule(0)
