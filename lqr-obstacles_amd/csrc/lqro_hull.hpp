@@ -133,6 +133,11 @@ struct HullArgs {
   // Qhull order: one timing record per build (hull_build_note), null: off
   unsigned long long* hbuild;
   int hbuild_cap;
+  // jobs still being produced by a concurrent hot launch: a worker that finds
+  // the queue empty waits until *prod_done reaches prod_total (its workgroups
+  // finished) before it leaves; null: leave at once
+  const int* prod_done;
+  int prod_total;
 };
 
 // (LQRO_ROW_BIG, lqro_device.hpp: the row counter's protocol; the early LP
@@ -436,10 +441,23 @@ __device__ __forceinline__ int hull_take_job(const HullArgs& A, LT& L, bool retr
     // finds the queue empty consumes no index, so entries a concurrent k_pair
     // launch appends later are still taken (by the k_hull after the sweep)
     int job = -1, slot = -1;
+    long waited = 0;
     for (;;) {
+      // (the producers' count first: once it is complete, every job they
+      // appended is in qcount)
+      const int pd = (A.prod_done && !retryq) ? __hip_atomic_load(A.prod_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)
+                                              : A.prod_total;
       const int nx = __hip_atomic_load(qnext, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
       const int cnt = min(__hip_atomic_load(qcount, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT), A.cap);
-      if (nx >= cnt) break;
+      if (nx >= cnt) {
+        // bounded: a worker that gives up leaves later jobs to the k_qhull
+        // after the sweep (results do not depend on who builds)
+        if (pd < A.prod_total && ++waited < (1l << 22)) {
+          __builtin_amdgcn_s_sleep(4);
+          continue;
+        }
+        break;
+      }
       if (atomicCAS(qnext, nx, nx + 1) != nx) continue;
       job = nx;
       // counted before published: wait for k_pair's release store

@@ -73,6 +73,7 @@ struct PairArgs {
   int* hot_next;
   int hot_cap;
   int hot_only;                       // 1: this launch computes the hot list only
+  int* hot_done;                      // hot launch: +1 per finished workgroup (k_qhull workers wait on it), null: none
   const int* nbr_list;                // culling on: per row npr (= K) neighbour jj, ascending, -1 = none
   double* qnrm;                       // LQRO_FLAG_QHULL_ORDER: per slot normal, dist (k_stale reads them)
   int* rowpend;                       // early LP: per row open work (LQRO_ROW_BIG), null: off
@@ -873,6 +874,14 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
     const int dst = threadIdx.x == 0 ? 6 : threadIdx.x == 1 ? 7 : threadIdx.x == 2 ? 1 : threadIdx.x == 3 ? 2 : 5;
     if (sum) atomicAdd(&P.stats[dst], sum);
   }
+  if constexpr (HOT != kRowLaunch) {
+    // every wave's pairs are done (the barrier above) and their hull jobs
+    // published: count the workgroup for the k_qhull workers waiting on it
+    if (P.hot_done && threadIdx.x == 0) {
+      __threadfence();
+      atomicAdd(P.hot_done, 1);
+    }
+  }
 }
 
 // RECS: per-pair records on (LQRO_FLAG_RECORDS); the bench path compiles
@@ -1003,15 +1012,61 @@ struct PrioArgs {
   int* count;
   int cap;
   int* rowpend;   // early LP: +1 per listed pair (null: off)
+  // Qhull order, split hot launch: the last step's inside-hull pairs head the
+  // list (k_prio_prev, marked 2 for k_prio) and form the side stream's first
+  // hot launch; k_prio's own pairs follow (the main stream's hot launch).
+  // null: one hot list
+  const int* prev;
+  const int* prevn;
+  int* hot1n;     // the first launch's pair count
+  int* hot2next;  // the second launch's first list position
 };
+
+// the last step's inside-hull pairs at the head of the hot list (one block)
+__global__ void __launch_bounds__(256) k_prio_prev(PrioArgs A) {
+  const long total = (long)A.nrows * A.npr;
+  const int m = min(*A.prevn, A.cap);
+  for (int q = threadIdx.x; q < m; q += blockDim.x) {
+    const int slot = A.prev[q];
+    A.list[q] = slot;
+    if (slot >= 0 && slot < total) {
+      A.mark[slot] = 2;
+      if (A.rowpend) atomicAdd(&A.rowpend[slot / A.npr], 1);
+    }
+  }
+  if (threadIdx.x == 0) {
+    *A.count = m;
+    *A.hot1n = m;
+    *A.hot2next = m;
+  }
+}
+
+// the step's inside-hull pairs (its hull queue) for the next step's
+// k_prio_prev (one block; the order does not matter: schedule only)
+__global__ void __launch_bounds__(256) k_prio_save(const int* hq, const int* hcount, int cap_hq, int* prev,
+                                                   int* prevn, int cap) {
+  __shared__ int n;
+  if (threadIdx.x == 0) n = 0;
+  __syncthreads();
+  const int c = min(*hcount, cap_hq);
+  for (int q = threadIdx.x; q < c; q += blockDim.x) {
+    const int slot = hq[q];
+    if (slot < 0) continue;
+    const int at = atomicAdd(&n, 1);
+    if (at < cap) prev[at] = slot;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) *prevn = min(n, cap);
+}
 
 __global__ void __launch_bounds__(256) k_prio(PrioArgs A) {
   const long total = (long)A.nrows * A.npr;
   const int lane = threadIdx.x & 63;
   for (long base = (long)blockIdx.x * 256 + (threadIdx.x & ~63); base < total; base += (long)gridDim.x * 256) {
     const long slot = base + lane;
-    bool hot = false;
-    if (slot < total) {
+    bool hot = false, pre = false;
+    if (slot < total && A.prev) pre = A.mark[slot] == 2;   // listed by k_prio_prev
+    if (slot < total && !pre) {
       const int lrow = (int)(slot / A.npr), jj = (int)(slot - (long)lrow * A.npr);
       const int i = A.row_begin + lrow * A.row_stride, j = jj < i ? jj : jj + 1;
       const double* xi = A.x + (size_t)i * A.X;
@@ -1033,7 +1088,7 @@ __global__ void __launch_bounds__(256) k_prio(PrioArgs A) {
       A.list[pos] = (int)slot;
       if (A.rowpend) atomicAdd(&A.rowpend[slot / A.npr], 1);
     }
-    if (slot < total) A.mark[slot] = hot ? 1 : 0;
+    if (slot < total) A.mark[slot] = (hot || pre) ? 1 : 0;
   }
 }
 #endif  // LQRO_PAIR_TU

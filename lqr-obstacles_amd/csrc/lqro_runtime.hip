@@ -377,6 +377,10 @@ struct lqro_ctx {
   int* d_hbag;
   int* d_lp4;                // k_lp_lds -> k_lp4 row list (6 ints per row)
   int* d_hotlist;            // k_prio: likely inside-hull pairs (slots), computed first
+  int* d_prevq;              // Qhull order: the last step's inside-hull pairs (k_prio_save), hot_cap
+  int* d_hot2;               // [0] their count, [1] first hot launch's count, [2] its next, [3] the
+                             // second's next, [4] its finished workgroups
+  int hot_split;             // LQRO_HOT_SPLIT (default 1): the split hot launch in Qhull order
   unsigned char* d_hotmark;  // per slot: in the hot list
   int* d_nbrlist;            // culling on: per row K neighbour slots (lqro_set_neighbors)
   double nbr_r2;
@@ -498,7 +502,8 @@ void lqro_destroy(lqro_ctx* c) {
   void* ps[] = {c->d_R, c->d_TF, c->d_shash, c->d_T, c->d_NCF, c->d_S, c->d_x, c->d_vgoal, c->d_newv, c->d_A, c->d_B,
                 c->d_L, c->d_E, c->d_planes, c->d_lpscratch, c->d_lpcompact, c->d_recs, c->d_hq, c->d_hcount,
                 c->d_err, c->d_hfaces, /* d_hnext points into d_hcount */ c->d_hscratch, c->d_hiscratch, c->d_hfscratch, c->d_stats, c->d_prof, c->d_rq, c->d_hbig, c->d_hwide, c->d_hbag, c->d_lp4, c->d_hotlist, c->d_hotmark, c->d_nbrlist, c->d_hfbest, c->d_hvpid, c->d_hstack, c->d_lq,
-                c->d_qscratch, c->d_qnrm, c->d_qstale, c->d_hbuild, c->d_carry, c->d_rowpend /* d_rowclaim inside */};
+                c->d_qscratch, c->d_qnrm, c->d_qstale, c->d_hbuild, c->d_carry, c->d_rowpend /* d_rowclaim inside */,
+                c->d_prevq, c->d_hot2};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (int k = 0; k < 5; ++k)
@@ -587,6 +592,9 @@ static int ctx_alloc(lqro_ctx* c) {
     HIPCHK(hipMalloc(&c->d_qnrm, sizeof(double) * 4 * (slots ? slots : 1)));
     HIPCHK(hipMalloc(&c->d_qstale, sizeof(int) * (slots ? slots : 1)));
     HIPCHK(hipMalloc(&c->d_hbuild, sizeof(unsigned long long) * 4 * LQRO_HBUILD_CAP));
+    HIPCHK(hipMalloc(&c->d_prevq, sizeof(int) * (size_t)c->hot_cap));
+    HIPCHK(hipMalloc(&c->d_hot2, sizeof(int) * 8));
+    HIPCHK(hipMemset(c->d_hot2, 0, sizeof(int) * 8));
   }
   return LQRO_OK;
 }
@@ -643,6 +651,11 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
     c->hot_max_inside = hm ? atol(hm) : -1L;
     const char* el = getenv("LQRO_EARLY_LP");
     c->early_lp = el ? atoi(el) != 0 : 1;
+    // Qhull order: the last step's inside-hull pairs in a hot launch of their
+    // own on the side stream, so the builds start when they are found rather
+    // than behind the other hot pairs' stragglers (which go to the main stream)
+    const char* hs = getenv("LQRO_HOT_SPLIT");
+    c->hot_split = hs ? atoi(hs) != 0 : 1;
     // off by default: with 3 waves a CU the side workers sweep rows at ~1/5 of a
     // 16-wave workgroup's rate, so where the sweep outlasts the builds (C4:
     // 227 vs 114 ms per step) it loses; at C3 it ties (22.0 ms either way)
@@ -925,13 +938,25 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   const unsigned nblk = (unsigned)std::min(units, c->n_cu - nwait);
   const unsigned nside = (unsigned)std::max(0, std::min(units - (int)nblk, nwait));
   P.hot_list = nullptr; P.hot_mark = nullptr; P.hot_count = nullptr;
-  P.hot_next = nullptr; P.hot_cap = 0; P.hot_only = 0;
+  P.hot_next = nullptr; P.hot_cap = 0; P.hot_only = 0; P.hot_done = nullptr;
+  // Qhull order, split hot launch (every pair of the last step's list gets a
+  // side CU of its own): side: the last step's inside-hull pairs, then
+  // k_qhull; main: k_prio's other hot pairs, then the rows.  k_qhull's workers
+  // wait for the main hot launch before leaving an empty queue.
+  const bool split = hot && c->qhull_order && c->hot_split && !qside && !c->qhull_big && known &&
+                     inside_prev + inside_prev / 16 + 4 <= (unsigned long long)nwait;
   if (hot) {
     PrioArgs Q{};
     Q.npr = c->npr; Q.nrows = c->nrows; Q.row_begin = c->rb; Q.row_stride = c->rs; Q.X = g.x_dim; Q.x = d_x;
     Q.t_hot = c->hot_t; Q.r2_hot = c->hot_r * c->hot_r;   // seconds, metres (scheduling heuristic)
     Q.list = c->d_hotlist; Q.mark = c->d_hotmark; Q.count = c->d_hcount + 6; Q.cap = c->hot_cap;
     Q.rowpend = P.rowpend;
+    if (split) {
+      HIPCHK(hipMemsetAsync(c->d_hot2 + 1, 0, sizeof(int) * 4, s));
+      Q.prev = c->d_prevq; Q.prevn = c->d_hot2; Q.hot1n = c->d_hot2 + 1; Q.hot2next = c->d_hot2 + 3;
+      hipLaunchKernelGGL(k_prio_prev, dim3(1), dim3(256), 0, s, Q);
+      HIPCHK(hipGetLastError());
+    }
     const long nb = std::min<long>((slots + 255) / 256, 8L * c->n_cu);
     hipLaunchKernelGGL(k_prio, dim3((unsigned)nb), dim3(256), 0, s, Q);
     HIPCHK(hipGetLastError());
@@ -977,6 +1002,14 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   // main grid still runs first on its CUs instead of k_side's row tail
   // sweeping every row on the side CUs alone
   if (nwait > 0) HIPCHK(hipEventRecord(c->xev[0], s));
+  if (split) {   // the main stream's hot launch: k_prio's pairs after the last step's
+    PairArgs P2 = P;
+    P2.hot_only = 1;
+    P2.hot_next = c->d_hot2 + 3;
+    P2.hot_done = c->d_hot2 + 4;
+    launch_pair(g.x_dim, dim3(nblk), dim3(P.waves * 64), c->lds_bytes, s, P2);
+    HIPCHK(hipGetLastError());
+  }
   launch_pair(g.x_dim, dim3(nblk), dim3(P.waves * 64), c->lds_bytes, s, P);
   HIPCHK(hipGetLastError());
   if (early) {
@@ -993,6 +1026,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
     HIPCHK(hipStreamWaitEvent(c->side, c->xev[0], 0));
     PairArgs Ph = P;
     Ph.hot_only = 1;
+    if (split) { Ph.hot_count = c->d_hot2 + 1; Ph.hot_next = c->d_hot2 + 2; }
     launch_pair(g.x_dim, dim3(nwait), dim3(P.waves * 64), c->lds_bytes, c->side, Ph);
     HIPCHK(hipGetLastError());
     if (c->qhull_order) {
@@ -1006,7 +1040,9 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
         HIPCHK(hipGetLastError());
       } else {
         if (!c->qhull_big) {
-          launch_qhull(dim3(std::min(nwait, c->qworkers)), c->side, Hh);
+          HullArgs Hs = Hh;
+          if (split) { Hs.prod_done = c->d_hot2 + 4; Hs.prod_total = (int)nblk; }
+          launch_qhull(dim3(std::min(nwait, c->qworkers)), c->side, Hs);
           HIPCHK(hipGetLastError());
         }
         if (nside > 0) {
@@ -1054,6 +1090,10 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
     launch_qhull_big(dim3(c->qworkers), s, Hh);
     HIPCHK(hipGetLastError());
     Hh.big_main = 0;
+    // this step's inside-hull pairs head the next step's hot list
+    hipLaunchKernelGGL(k_prio_save, dim3(1), dim3(256), 0, s, c->d_hq, c->d_hcount, c->hull_cap, c->d_prevq,
+                       c->d_hot2, c->hot_cap);
+    HIPCHK(hipGetLastError());
     if (phase == 0) {
       launch_stale(s, c->d_planes, c->d_qnrm, c->d_qstale, c->d_hcount + 15, c->hull_cap, d_x, g.x_dim, npr, c->rb,
                    c->rs, c->d_carry, c->d_recs, slots);

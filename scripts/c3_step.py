@@ -17,7 +17,21 @@ x, vg = lqro.synthetic_swarm(N, box=box) if box else lqro.synthetic_swarm(N)
 g = lqro.synthesize_gains()
 c = lqro.Context(lqro.config(N, H, NP))
 c.set_gains(g["A"], g["B"], g["L"], g["E"])
+import numpy as np  # noqa: E402
+
+steps = []
 for k in range(K):
     t = time.perf_counter()
     c.step(x, vg)
-    print(f"step {k}: {1e3 * (time.perf_counter() - t):.2f} ms", c.timings(), c.stats(), flush=True)
+    tm = c.timings()
+    b = c.hull_builds()
+    dur = (b["t_end"].astype(np.int64) - b["t_start"].astype(np.int64)) / 1e5 if len(b) else np.zeros(1)
+    span = (int(b["t_end"].max()) - int(b["t_start"].min())) / 1e5 if len(b) else 0.0
+    us_ins = dur.sum() * 1e3 / max(1, int(b["insertions"].sum())) if len(b) else 0.0
+    print(f"step {k}: {1e3 * (time.perf_counter() - t):.2f} ms host, {tm['step_ms']:.3f} ms device, "
+          f"slowest build {dur.max():.3f} ms, builds span {span:.3f} ms, {us_ins:.2f} us/insertion", c.stats(),
+          flush=True)
+    if k >= 2:
+        steps.append(tm["step_ms"])
+if steps:
+    print(f"steady: median {np.median(steps):.3f} ms, min {np.min(steps):.3f} ms over {len(steps)} steps", flush=True)
