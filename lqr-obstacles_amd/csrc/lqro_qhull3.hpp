@@ -21,9 +21,10 @@
 //    in queue order that reaches it); qh_makenew_simplicial runs one horizon
 //    ridge per lane (creation order = the ridges in visible-list order); new
 //    facets reuse the visible facets' slots;
-//  * outside-set entries carry their point's coordinates (one load per
-//    point re-partitioned), and the partition sequence is read straight from
-//    the visible facets' sets;
+//  * outside-set entries are point ids (4 B: the sets' footprint stays in
+//    L2), their coordinates read from Pr when a set is re-partitioned (wave
+//    2's prefetch does both loads for the usual one-chunk sequence), and the
+//    partition sequence is read straight from the visible facets' sets;
 //  * the point search keeps Qhull's sequential semantics as lqro_qhull.hpp
 //    does (order-dependent state changes applied at their point, the rest of
 //    the sequence re-evaluated), and counts each point into its destination
@@ -87,10 +88,9 @@ struct Q3W {
   Q3G* G;                 // FC - Q3_FL spilled slots
   Q3V* vv;                // FC: vertices
   double* ncoord;         // 9 Q3_NEWCAP: the new facets' ridge and opposite points (a cone too wide for registers)
-  HullPt* pseq;           // HNP: the partition sequence's points (a sequence longer than 64)
   int* soff;              // FC: outside set offset in sb
   double* fdist;          // FC: furthest outside distance
-  HullPt* sb;             // SB outside-set entries (point, coordinates)
+  int* sb;                // SB outside-set entries: point ids (coordinates from Pr)
   int* pq;                // HNP: qh_partitionall's remainder
   int* pdst;              // HNP: partition sequence -> destination index
   double* pdd;            // HNP: its distance
@@ -109,8 +109,8 @@ __host__ __device__ inline size_t q3_worker_bytes(int HNP) {
   const size_t FC = 2 * (size_t)HNP + Q3_NEWCAP + 16, SB = (size_t)QH_SBMULT * HNP, QC = 4 * (size_t)HNP + 64;
   const size_t NG = FC > Q3_FL ? FC - Q3_FL : 1;
   return q3_align(24 * (size_t)HNP) * 2 + q3_align(64 * NG) + q3_align(96 * FC) + q3_align(72 * Q3_NEWCAP) +
-         q3_align(32 * (size_t)HNP) + q3_align(4 * FC) +
-         q3_align(8 * FC) + q3_align(32 * SB) + q3_align(4 * (size_t)HNP) * 2 + q3_align(8 * (size_t)HNP) +
+         q3_align(4 * FC) +
+         q3_align(8 * FC) + q3_align(4 * SB) + q3_align(4 * (size_t)HNP) * 2 + q3_align(8 * (size_t)HNP) +
          q3_align(4 * QC) * 2 + q3_align(32 * QC) + q3_align(72 * Q3_NEWCAP) + q3_align(4 * FC) + 256;
 }
 
@@ -128,10 +128,9 @@ __device__ inline Q3W q3_worker(char* base, int HNP) {
   W.G = reinterpret_cast<Q3G*>(take(64 * NG));
   W.vv = reinterpret_cast<Q3V*>(take(96 * (size_t)W.FC));
   W.ncoord = reinterpret_cast<double*>(take(72 * (size_t)Q3_NEWCAP));
-  W.pseq = reinterpret_cast<HullPt*>(take(32 * (size_t)HNP));
   W.soff = reinterpret_cast<int*>(take(4 * (size_t)W.FC));
   W.fdist = reinterpret_cast<double*>(take(8 * (size_t)W.FC));
-  W.sb = reinterpret_cast<HullPt*>(take(32 * (size_t)W.SB));
+  W.sb = reinterpret_cast<int*>(take(4 * (size_t)W.SB));
   W.pq = reinterpret_cast<int*>(take(4 * (size_t)HNP));
   W.pdst = reinterpret_cast<int*>(take(4 * (size_t)HNP));
   W.pdd = reinterpret_cast<double*>(take(8 * (size_t)HNP));
@@ -507,7 +506,7 @@ __device__ __forceinline__ double q3_scan_max(double v) {
 // a data-dependent store count made every chunk wait for all its stores)
 __device__ __forceinline__ void q3_place(unsigned long long grp, int lane, unsigned long long ltmask,
                                          double dd, const HullPt& pt, int off, int lim, int& cnt, double& mx,
-                                         int& champ, double& cx, double& cy, double& cz, int& wpos, HullPt& wr) {
+                                         int& champ, double& cx, double& cy, double& cz, int& wpos, int& wr) {
   const bool mem = (grp >> lane) & 1ull;
   const int cb = cnt + __popcll(grp & ltmask);   // points before this one in the set
   double run = -DBL_MAX;                         // the largest distance among them
@@ -523,22 +522,15 @@ __device__ __forceinline__ void q3_place(unsigned long long grp, int lane, unsig
   const bool rec = mem && (cb == 0 || run < dd);
   const unsigned long long recm = __ballot(rec);
   const unsigned long long prevm = recm & ltmask;
-  double px = 0.0, py = 0.0, pz = 0.0;
   int pq = 0;
   if (recm & (recm - 1ull)) {   // a new furthest point displacing another one of this pass
     const int pl = prevm ? 63 - __clzll((long long)prevm) : lane;
-    px = __shfl(pt.x, pl); py = __shfl(pt.y, pl); pz = __shfl(pt.z, pl);
     pq = __shfl(pt.q, pl);
   }
   if (mem && cb > 0 && off + cb - 1 < lim) {
-    HullPt r = pt;
-    if (rec) {   // the furthest point it displaces: the previous new furthest here, or the held one
-      if (prevm) { r.x = px; r.y = py; r.z = pz; r.q = pq; }
-      else { r.x = cx; r.y = cy; r.z = cz; r.q = champ; }
-      r.pad = 0;
-    }
+    // the furthest point it displaces: the previous new furthest here, or the held one
     wpos = off + cb - 1;
-    wr = r;
+    wr = rec ? (prevm ? pq : champ) : pt.q;
   }
   if (recm) {
     const int l = 63 - __clzll((long long)recm);
@@ -768,7 +760,11 @@ __device__ __forceinline__ HullPt q3_seqpt(const Q3W& W, const Q3L& L, int nvis,
     else a = mid + 1;
   }
   *start = L.repl[a] >= 0 ? L.repl[a] : 0;
-  return W.sb[L.vsoff[a] + pos - (L.vinc[a] - L.vscnt[a])];
+  const int q = W.sb[L.vsoff[a] + pos - (L.vinc[a] - L.vscnt[a])];
+  r.x = W.Pr[3 * (size_t)q]; r.y = W.Pr[3 * (size_t)q + 1]; r.z = W.Pr[3 * (size_t)q + 2];
+  r.q = q;
+  r.pad = 0;
+  return r;
 }
 
 __device__ __forceinline__ int q3_ld_acq(const int* p) {
@@ -839,7 +835,7 @@ __device__ inline void q3_serve_chunk(const Q3W& W, Q3L& L, int lane) {
 // + k for the k-th old facet to receive points) once its result is final.
 // Chunks stay aligned to the lanes (position 64 k + lane), so a sequence of
 // at most 64 points leaves each lane's final destination, distance and point
-// in rg, rd, rpt; a longer one goes through W.pdst, W.pdd, W.pseq.  pre /
+// in rg, rd, rpt; a longer one goes through W.pdst, W.pdd.  pre /
 // prestart: position `lane`'s point, fetched by the caller (havepre).
 // init: qh_partitionall's remainder (the scan list is the facet list; a
 // moved facet goes to its end).
@@ -965,10 +961,9 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
         rg = g;
         rd = d;
         rpt = pt;
-        if (np > 64) {
+        if (np > 64) {   // (the point itself is read again from the sequence)
           W.pdst[pos] = g;
           W.pdd[pos] = d;
-          W.pseq[pos] = pt;
         }
       }
       hl_sync();
@@ -1074,11 +1069,12 @@ __device__ inline void q3_emit_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int ndn
     const int off0 = W.soff[f];
     const int off = L.doff[g];
     for (int t = lane; t < cnt0 - 1; t += 64) W.sb[off + t] = W.sb[off0 + t];
-    const HullPt ch = W.sb[off0 + cnt0 - 1];
+    const int chq = W.sb[off0 + cnt0 - 1];
     const double fd = W.fdist[f];
     if (lane == 0) {
-      L.dchamp[g] = ch.q;
-      L.dchp[3 * g] = ch.x; L.dchp[3 * g + 1] = ch.y; L.dchp[3 * g + 2] = ch.z;
+      L.dchamp[g] = chq;
+      L.dchp[3 * g] = W.Pr[3 * (size_t)chq]; L.dchp[3 * g + 1] = W.Pr[3 * (size_t)chq + 1];
+      L.dchp[3 * g + 2] = W.Pr[3 * (size_t)chq + 2];
       L.dmax[g] = fd;
     }
     hl_sync();
@@ -1099,7 +1095,8 @@ __device__ inline void q3_emit_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int ndn
     if (pos < np) {
       ng = W.pdst[pos];
       ndd = W.pdd[pos];
-      npt = W.pseq[pos];
+      int st;
+      npt = q3_seqpt(W, L, S.nvis, init, pos, &st);
     }
   };
   if (np > 64) ldc(0);
@@ -1120,9 +1117,7 @@ __device__ inline void q3_emit_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int ndn
     Q3T(16);
     unsigned long long todo = __ballot(g >= 0);
     const unsigned long long ltmask = (1ull << lane) - 1ull;
-    int wpos = -1;
-    HullPt wr;
-    wr.x = wr.y = wr.z = 0.0; wr.q = 0; wr.pad = 0;
+    int wpos = -1, wr = 0;
     while (todo) {
       const int lead = __ffsll((long long)todo) - 1;
       const int gg = __builtin_amdgcn_readlane(g, lead);
@@ -1150,9 +1145,7 @@ __device__ inline void q3_emit_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int ndn
     const int g = i < ndnew ? i : Q3_NEWCAP + (i - ndnew);
     if (!L.pcnt[g]) continue;
     const int f = L.dfac[g];
-    HullPt r;
-    r.x = L.dchp[3 * g]; r.y = L.dchp[3 * g + 1]; r.z = L.dchp[3 * g + 2]; r.q = L.dchamp[g]; r.pad = 0;
-    W.sb[L.doff[g] + L.dcnt[g] - 1] = r;
+    W.sb[L.doff[g] + L.dcnt[g] - 1] = L.dchamp[g];
     W.soff[f] = L.doff[g];
     W.fdist[f] = L.dmax[g];
     q3_set_cc(W, L, f, (unsigned)L.dcnt[g] | ((unsigned)L.dchamp[g] << 16));
@@ -1577,7 +1570,12 @@ __device__ inline void q3_prefetch(const Q3W& W, Q3L& L, int lane, int p) {
       base += k;
       ++a;
     }
-    L.pf_pre[lane] = W.sb[L.pf_vsoff[a] + lane - base];
+    const int q = W.sb[L.pf_vsoff[a] + lane - base];
+    HullPt r;
+    r.x = W.Pr[3 * (size_t)q]; r.y = W.Pr[3 * (size_t)q + 1]; r.z = W.Pr[3 * (size_t)q + 2];
+    r.q = q;
+    r.pad = 0;
+    L.pf_pre[lane] = r;
     L.pf_prea[lane] = (unsigned char)a;
   }
   hl_sync();
@@ -1802,8 +1800,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
         w += __popcll(bk);
         const unsigned long long bo = __ballot(out);
         if (bo) {
-          int wpos = -1;
-          HullPt wr;
+          int wpos = -1, wr = 0;
           q3_place(bo, lane, ltmask, d, pt, off, W.SB, cnt, mx, champ, cx, cy, cz, wpos, wr);
           if (wpos >= 0) W.sb[wpos] = wr;
         }
@@ -1812,9 +1809,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
       if (cnt) {
         if (off + cnt > W.SB) { S.status |= QHS_CAPACITY | Q3_CAPBIT(QHS_CAP_SB); return; }
         if (lane == 0) {
-          HullPt r;
-          r.x = cx; r.y = cy; r.z = cz; r.q = champ; r.pad = 0;
-          W.sb[off + cnt - 1] = r;
+          W.sb[off + cnt - 1] = champ;
           W.soff[f] = off;
           W.fdist[f] = mx;
           q3_set_cc(W, L, f, (unsigned)cnt | ((unsigned)champ << 16));

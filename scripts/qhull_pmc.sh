@@ -1,25 +1,15 @@
-# SQ counters of k_qhull (Qhull-order bench, C3): two passes, each its own run
+# k_qhull's HBM traffic per build (stamped, for bench.py's `critical`) and its
+# L2 hit rate (GPU box, repo root):  bash scripts/qhull_pmc.sh TAG
 set -e
 export TMPDIR=/tmp
-O=gpurun_out/${1:-qpmc}
+TAG=${1:-rX}
+O=gpurun_out
 mkdir -p $O
-B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-configs --no-roofline-probe"
-timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR --output-format csv -d $O/p1 -o run -- $B > $O/p1.log 2>&1
-timeout -s KILL 150 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_SMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH --output-format csv -d $O/p2 -o run -- $B > $O/p2.log 2>&1
-python3 - $O <<'P'
-import csv, glob, sys, collections
-O = sys.argv[1]
-agg = collections.defaultdict(lambda: collections.defaultdict(float))
-n = collections.Counter()
-for p in ("p1", "p2"):
-    for f in glob.glob(f"{O}/{p}/**/*counter_collection.csv", recursive=True):
-        for r in csv.DictReader(open(f)):
-            k = r["Kernel_Name"]
-            if "k_qhull" not in k or "big" in k:
-                continue
-            agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
-for k, d in agg.items():
-    print(k)
-    for c, v in sorted(d.items()):
-        print(f"  {c:24s} {v:16.0f}")
-P
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/qt_f -o run -- python3 scripts/qhull_traffic.py run $O/qt_run_f.json > $O/qt_f.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/qt_w -o run -- python3 scripts/qhull_traffic.py run $O/qt_run_w.json > $O/qt_w.log 2>&1
+python3 scripts/qhull_traffic.py summarise $O/qt_f $O/qt_w $O/qt_run_f.json $O/${TAG}_qhull_traffic.json > /dev/null
+cp $O/${TAG}_qhull_traffic.json profiles/${TAG}_qhull_traffic.json
+timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $O/qt_h -o run -- python3 scripts/qhull_traffic.py run $O/qt_run_h.json > $O/qt_h.log 2>&1
+python3 scripts/pmc_any.py $O/${TAG}_qhull_l2.json $O/qt_h > $O/${TAG}_qhull_l2.txt 2>&1 || true
+cat $O/${TAG}_qhull_l2.txt
+echo qhull pmc done
