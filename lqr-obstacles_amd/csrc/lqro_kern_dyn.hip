@@ -1,6 +1,7 @@
 // lqro_kern_dyn.hip — the per-agent dynamics / estimation kernels (the agent
 // loop LQRObstacles.cpp:1437-1446) and their launch function (lqro_kern.hpp).
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "lqro_dyn.hpp"
 #include "lqro_dynw.hpp"
@@ -40,7 +41,7 @@ __global__ void __launch_bounds__(64) k_dyn(const lqro_model* models, int n_mode
 // matrices in LDS, the products, exponentials, solves and Jacobi sweep over
 // the lanes.  The default; LQRO_DYN_LANE=1 selects k_dyn.
 __global__ void __launch_bounds__(64) k_dynw(const lqro_model* models, int n_models, int n, int per_agent,
-                                             lqro_agents A) {
+                                             lqro_agents A, unsigned long long* prof) {
   __shared__ double w[dynw::kWaveDoubles];
   const int a = blockIdx.x;
   if (a >= n) return;
@@ -62,15 +63,33 @@ __global__ void __launch_bounds__(64) k_dynw(const lqro_model* models, int n_mod
   p.time = A.time;
   dynw::agent_step(p, A.x + (size_t)a * dyn::kX, A.rot + (size_t)a * 9, A.x_true + (size_t)a * dyn::kX,
                    A.rot_true + (size_t)a * 9, A.P + (size_t)a * dyn::kX * dyn::kX, A.vgoal + (size_t)a * 3,
-                   A.u ? A.u + (size_t)a * dyn::kU : nullptr, w, lane);
+                   A.u ? A.u + (size_t)a * dyn::kU : nullptr, w, lane, prof);
+}
+
+// LQRO_DYN_PROFILE=1: k_dynw's phases (lqro_dynw.hpp DynProf) into a device
+// buffer read by lqro_debug_dyn_profile (not in lqro.h; scripts/dyn_prof.py)
+static unsigned long long* g_dprof = nullptr;
+
+extern "C" int lqro_debug_dyn_profile(unsigned long long* out32, int reset) {
+  if (!out32) return -1;
+  if (!g_dprof) { for (int k = 0; k < 32; ++k) out32[k] = 0; return 0; }
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  if (hipMemcpy(out32, g_dprof, sizeof(unsigned long long) * 32, hipMemcpyDeviceToHost) != hipSuccess) return -2;
+  if (reset && hipMemset(g_dprof, 0, sizeof(unsigned long long) * 32) != hipSuccess) return -2;
+  return 0;
 }
 
 void launch_dyn(bool lane, const lqro_model* models, int n_models, int n, int per_agent, const lqro_agents& A,
                 hipStream_t s) {
   if (lane)
     hipLaunchKernelGGL(k_dyn, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, models, n_models, n, per_agent, A);
-  else
-    hipLaunchKernelGGL(k_dynw, dim3((unsigned)n), dim3(64), 0, s, models, n_models, n, per_agent, A);
+  else {
+    static const int prof_on = getenv("LQRO_DYN_PROFILE") ? atoi(getenv("LQRO_DYN_PROFILE")) : 0;
+    if (prof_on && !g_dprof && hipMalloc(&g_dprof, sizeof(unsigned long long) * 32) == hipSuccess)
+      (void)hipMemset(g_dprof, 0, sizeof(unsigned long long) * 32);
+    hipLaunchKernelGGL(k_dynw, dim3((unsigned)n), dim3(64), 0, s, models, n_models, n, per_agent, A,
+                       prof_on ? g_dprof : nullptr);
+  }
 }
 
 }  // namespace lqro
