@@ -532,12 +532,11 @@ __device__ __forceinline__ void jacobi(const double* m, double* V, double* D, in
       const int r = dl ? lane : lane - N;
       double* W = dl ? D : V;
       const bool pq = dl && (r == p || r == q);
-      int ia, ib;   // the two entries row/col r of the rotation touches
-      if (!dl) { ia = swz<N>(r, p); ib = swz<N>(r, q); }
-      else if (pq) { ia = swz<N>(p, q); ib = ia; }
-      else if (r < p) { ia = swz<N>(r, p); ib = swz<N>(r, q); }
-      else if (r < q) { ia = swz<N>(p, r); ib = swz<N>(r, q); }
-      else { ia = swz<N>(p, r); ib = swz<N>(q, r); }
+      // the two entries row/col r of the rotation touches: D's {r,p}, {r,q}
+      // in the upper triangle (V's (r,p), (r,q)); lanes p, q zero D(p,q)
+      const int ra = pq ? p : (dl ? min(r, p) : r), ca = pq ? q : (dl ? max(r, p) : p);
+      const int rb = pq ? p : (dl ? min(r, q) : r), cb = pq ? q : (dl ? max(r, q) : q);
+      const int ia = swz<N>(ra, ca), ib = swz<N>(rb, cb);
       const double a = W[ia], b = W[ib];
       const double na = pq ? 0.0 : a - s * (b + tau * a);
       const double nb = pq ? 0.0 : b + s * (a - tau * b);
