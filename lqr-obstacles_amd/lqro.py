@@ -777,6 +777,7 @@ class DeviceLoop:
         self.Nz = 1e-9 * torch.eye(6, **f64)
         self.model_d = torch.frombuffer(bytearray(bytes(self.model)), dtype=torch.uint8).to(self.dev)
         self.nrm = None
+        self._nrm_host = None   # the next update's noise draws, pinned (drawn while the GPU runs)
         self.t = 0
 
     def _sid(self):
@@ -809,11 +810,11 @@ class DeviceLoop:
         torch = self.torch
         rb, re = self.rb, self.re
         block = self.mode == "block"
-        nrm, self.seed = normals(self.seed, self.n * NORMALS_PER_AGENT)
+        if self._nrm_host is None:
+            self._nrm_host = self._draw_normals()
         with torch.cuda.stream(self.stream):
             # pinned + non-blocking: no host wait on the stream's earlier work
-            host = torch.from_numpy(np.ascontiguousarray(nrm.reshape(self.n, NORMALS_PER_AGENT)[self.ids_h]))
-            self.nrm = host.pin_memory().to(self.dev, non_blocking=True)
+            self.nrm = self._nrm_host.to(self.dev, non_blocking=True)
             if block:
                 self.vgoal[rb:re].copy_(self.newv[rb:re])      # vGoal = newV (LQRO:1438)
                 xs, vs = self.x[rb:re], self.vgoal[rb:re]
@@ -836,6 +837,14 @@ class DeviceLoop:
             if self.world > 1:
                 allgather_rows(self.dist, self.x, self.rank, self.world, mode=self.mode)
         self.t += 1
+        # the next step's draws (the reference's rand() stream, in agent order)
+        # on the host while this step's kernels run
+        self._nrm_host = self._draw_normals()
+
+    def _draw_normals(self):
+        nrm, self.seed = normals(self.seed, self.n * NORMALS_PER_AGENT)
+        host = self.torch.from_numpy(np.ascontiguousarray(nrm.reshape(self.n, NORMALS_PER_AGENT)[self.ids_h]))
+        return host.pin_memory()
 
     def close(self):
         self.ctx.close()
