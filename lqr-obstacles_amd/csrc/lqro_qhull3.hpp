@@ -1923,6 +1923,14 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     // the queue's next live one with points and the same furthest point
     bool adopt = false;
     bool pfv = false;   // wave 2's prefetch of this insertion's partition sequence is used
+    bool fast = false;  // adopted in one pass (below): the cone, slots and new facets are in place
+    int nvis = 0, nnew = 0, lm = 0;
+    const double* ncb = W.ncoord;
+    HullPt pre;
+    pre.x = pre.y = pre.z = 0.0;
+    pre.q = -1;
+    pre.pad = 0;
+    int pfa = 0, pfnp = -1;
     if (phase > 0) {
 #ifdef LQRO_QHULL_PROFILE
       const unsigned long long tw_ = __builtin_amdgcn_s_memtime();
@@ -1960,7 +1968,112 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
         S.status |= QHS_CAPACITY | QHS_TIMEOUT;
         return;
       }
-      if (L.sp_ok) {
+      // The usual case, both lists within one pass of the lanes: the check
+      // and the whole adoption — the speculated lists, the slots, the new
+      // facets' fields — as one round of loads, one of dependent loads and
+      // one of stores (the general path below goes a list at a time, a round
+      // trip each).  The same values and the same store order as that path.
+      {
+        const int sok = L.sp_ok, F = L.sp_facet, sfur = L.sp_furthest, spos = L.sp_pos;
+        const int snv = L.sp_nvis, snn = L.sp_nnew, sst = L.sp_status;
+        const unsigned skey = L.sp_key;
+        const double sax = L.sp_apex[0], say = L.sp_apex[1], saz = L.sp_apex[2];
+        const int vf = L.sp_visf[lane], vr = L.sp_repl[lane];
+        const int vv0 = L.sp_vvert[3 * lane], vv1 = L.sp_vvert[3 * lane + 1], vv2 = L.sp_vvert[3 * lane + 2];
+        const int t1 = L.sp_v1[lane], t2 = L.sp_v2[lane], thz = L.sp_nhz[lane], thk = L.sp_nhskip[lane];
+        const int tfl = L.sp_nflag[lane], tn1 = L.sp_nn1[lane], tn2 = L.sp_nn2[lane];
+        const double4 tpl = q3_lds(*reinterpret_cast<const double4*>(L.sp_npl + 4 * lane));
+        const int oldv = lane < Q3_MOVCAP ? L.oldf[lane] : -1;
+        // wave 2's prefetch: its flag, then (in LDS issue order, which the
+        // compiler keeps here) what it released with it
+        const int pfd = hl_ld(&L.pf_done);
+        hl_cfence();
+        const int pso = L.pf_vsoff[lane], psc = L.pf_vscnt[lane], ppnp = L.pf_np, ppfa = L.pf_prea[lane];
+        const HullPt ppre = L.pf_pre[lane];
+        if (sok && F >= 0 && snv >= 1 && snv <= 64 && snn >= 1 && snn <= 64) {
+          const unsigned c = q3_cc(W, L, F), k0 = q3_key(W, L, F);
+          const int fa0 = q3_fa(W, L, F);
+          int vfa = 0;
+          unsigned vkey = 0u;
+          if (lane < snv) { vfa = q3_fa(W, L, vf); vkey = q3_key(W, L, vf); }
+          const int e = lane - snv;
+          int fsl = 0;
+          if (e >= 0 && e < S.nfs) fsl = L.fstk[S.nfs - 1 - e];
+          adopt = (fa0 & QF_LIVE) && k0 == skey && (c & 0xffffu) > 0 && (int)(c >> 16) == sfur;
+          if (adopt) {
+            facet = F;
+            furthest = sfur;
+            apexp[0] = sax; apexp[1] = say; apexp[2] = saz;
+            S.qhead = spos;
+            q3_set_cc(W, L, F, (c & 0xffffu) - 1u);   // qh_setdellast
+            nvis = snv;
+            nnew = snn;
+            bool bad = false;
+            if (lane < nvis) {
+              bad = vkey >= S.key0_last;
+              for (int t = 0; t < S.nold; t++) bad |= __builtin_amdgcn_readlane(oldv, t) == vf;
+            }
+            pfv = pfd == phase && __ballot(bad) == 0ull;
+            if (lane < nvis) {
+              int so = pso, sc = psc;
+              if (!pfv) {   // (F's count as just decremented)
+                so = W.soff[vf];
+                sc = vf == F ? (int)((c & 0xffffu) - 1u) : (int)(q3_cc(W, L, vf) & 0xffffu);
+              }
+              L.visf[lane] = vf;
+              L.repl[lane] = vr;
+              q3_set_fa(W, L, vf, vfa | QF_VISIBLE);
+              L.vvert[3 * lane] = vv0; L.vvert[3 * lane + 1] = vv1; L.vvert[3 * lane + 2] = vv2;
+              L.vsoff[lane] = so;
+              L.vscnt[lane] = sc;
+            }
+            if (lane < nnew) {
+              L.nv[3 * lane] = furthest; L.nv[3 * lane + 1] = t1; L.nv[3 * lane + 2] = t2;
+              L.nhz[lane] = thz;
+              L.nhskip[lane] = thk;
+              L.nflag[lane] = tfl;
+              L.nn1[lane] = tn1;
+              L.nn2[lane] = tn2;
+              q3_lds_st(*reinterpret_cast<double4*>(L.npl + 4 * lane), tpl);
+            }
+            S.status |= sst;
+            S.nvis = nvis;
+            lm = sst & QHS_FLIPPED;
+            ncb = W.ncoord2;
+            fast = true;
+            if (!(S.status & (QHS_TOPOLOGY | QHS_CAPACITY))) {
+              S.nnew = nnew;
+              if (pfv) { pfnp = ppnp; pre = ppre; pfa = ppfa; }
+              // slots: the visible facets', then free ones, then fresh ones (q3_alloc)
+              const int extra = nnew > nvis ? nnew - nvis : 0;
+              const int take = extra < S.nfs ? extra : S.nfs;
+              if (S.nalloc + extra - take > W.FC) {
+                S.status |= QHS_CAPACITY | Q3_CAPBIT(QHS_CAP_FACETS);
+              } else {
+                const int slot = lane < nvis ? vf : (e < S.nfs ? fsl : S.nalloc + (e - S.nfs));
+                if (lane < nnew) L.nslot[lane] = slot;
+                S.nfs -= take;
+                S.nalloc += extra - take;
+                // the new facets' fields (matched by wave 1), the horizon facets' links
+                const unsigned key0 = S.keyc;
+                const int s1 = __builtin_amdgcn_ds_bpermute(tn1 << 2, slot);
+                const int s2 = __builtin_amdgcn_ds_bpermute(tn2 << 2, slot);
+                if (lane < nnew) {
+                  const double q[4] = {tpl.x, tpl.y, tpl.z, tpl.w};
+                  q3_set_facet(W, L, slot, q, thz, s1, s2, tfl | (lane << 8));
+                  q3_set_key(W, L, slot, key0 + (unsigned)lane);
+                  q3_set_cc(W, L, slot, 0u);
+                  q3_set_nb(W, L, thz, thk, slot);
+                }
+                S.keyc += (unsigned)nnew;
+                S.key0_last = key0;
+              }
+            }
+            hl_sync();
+          }
+        }
+      }
+      if (!fast && L.sp_ok) {
         const int F = L.sp_facet;
         const unsigned c = q3_cc(W, L, F);
         adopt = (q3_fa(W, L, F) & QF_LIVE) && q3_key(W, L, F) == L.sp_key && (c & 0xffffu) > 0 &&
@@ -2024,11 +2137,12 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
       if (phase > 0 && q3_wait(&L.sp_gdone, phase, false) != phase) S.status |= QHS_CAPACITY | QHS_TIMEOUT;
       break;
     }
-    int nvis = 0, nnew = 0, ts = 0, lm = 0, my_t = -1;
+    int ts = 0, my_t = -1;
     bool one = false;
-    const double* ncb = W.ncoord;
     double P1[3] = {0.0, 0.0, 0.0}, P2[3] = {0.0, 0.0, 0.0}, PO[3] = {0.0, 0.0, 0.0};
-    if (adopt) {
+    if (fast) {
+      // (adopted above)
+    } else if (adopt) {
       // the speculated visible set (flagged now) and cone
       nvis = L.sp_nvis;
       nnew = L.sp_nnew;
@@ -2233,17 +2347,12 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     hl_sync();
     // wave 2's head of the partition sequence, read before wave 1 may start
     // the next speculation (whose horizon restarts wave 2's prefetch)
-    HullPt pre;
-    pre.x = pre.y = pre.z = 0.0;
-    pre.q = -1;
-    pre.pad = 0;
-    int pfa = 0, pfnp = -1;
-    if (pfv) {
+    if (pfv && !fast) {
       pfnp = L.pf_np;
       pre = L.pf_pre[lane];
       pfa = L.pf_prea[lane];
     }
-    {
+    if (!fast) {
       // slots: the visible facets', then free ones, then fresh ones
       const int extra = nnew > nvis ? nnew - nvis : 0;
       const int take = extra < S.nfs ? extra : S.nfs;
@@ -2295,7 +2404,9 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
       }
       q3_set_nb(W, L, hz, hk, s);
     };
-    if (one) {
+    if (fast) {
+      // (the new facets' fields written above)
+    } else if (one) {
       if (my_t >= 0) finish(my_t, P1, P2);
     } else {
       for (int t = lane; t < nnew; t += 64) {
@@ -2305,8 +2416,10 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
         finish(t, p1, p2);
       }
     }
-    S.keyc += (unsigned)nnew;
-    S.key0_last = key0;
+    if (!fast) {
+      S.keyc += (unsigned)nnew;
+      S.key0_last = key0;
+    }
     hl_sync();
     // qh_checkzero: each new facet clearly convex to its neighbours (an
     // adopted cone's: wave 1's, in its status)
