@@ -1362,7 +1362,7 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
     // the horizon to wave 2, which fetches the partition sequence's head
     if (!cap && lane == 0) {
       L.sp_hnvis = nvis;
-      q3_st_rel(&L.sp_hz, phase);
+      q3_st_rel_lds(&L.sp_hz, phase);   // (LDS only: wave 2 reads no global store of this wave)
     }
     W1T(3);
     // 3. the cone: one new facet per horizon ridge, as wave 0's
