@@ -1031,6 +1031,73 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
 __device__ inline void q3_emit_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int ndnew, bool init, int lane, int rg,
                                    double rd, const HullPt& rpt) {
   if (S.status & QHS_CAPACITY) return;
+  // One chunk with new-facet destinations only (the usual insertion): each
+  // destination is one group of the chunk and starts from an empty set, so
+  // its state lives in lane g from the segment scan to the queue, with no
+  // LDS round trip per group.  The same placement and stores as below.
+  if (!init && np <= 64 && S.nold == 0 && ndnew <= 64) {
+    const int g = lane;
+    int pc = 0, f = 0;
+    if (g < ndnew) { f = L.nslot[g]; pc = L.pcnt[g]; }
+    const int inc = q3_scan_add(pc);
+    const int top = S.sbtop + __builtin_amdgcn_readlane(inc, 63);
+    if (top > W.SB) {
+      S.status |= QHS_CAPACITY | Q3_CAPBIT(QHS_CAP_SB);
+      return;
+    }
+    const int doff = S.sbtop + inc - pc;
+    S.sbtop = top;
+    Q3T(15);
+    int dcnt = 0, dchamp = -1;
+    double dmax = 0.0, dx = 0.0, dy = 0.0, dz = 0.0;
+    const unsigned long long ltmask = (1ull << lane) - 1ull;
+    const int rgl = lane < np ? rg : -1;
+    unsigned long long todo = __ballot(rgl >= 0);
+    int wpos = -1, wr = 0;
+    Q3T(16);
+    while (todo) {
+      const int lead = __ffsll((long long)todo) - 1;
+      const int gg = __builtin_amdgcn_readlane(rgl, lead);
+      const unsigned long long grp = __ballot(rgl == gg);
+      todo &= ~grp;
+      int cnt = 0, champ = -1;
+      double mx = 0.0, cx = 0.0, cy = 0.0, cz = 0.0;
+      q3_place(grp, lane, ltmask, rd, rpt, __builtin_amdgcn_readlane(doff, gg), W.SB, cnt, mx, champ, cx, cy, cz,
+               wpos, wr);
+      Q3C(25, 1);
+      if (lane == gg) { dcnt = cnt; dmax = mx; dchamp = champ; dx = cx; dy = cy; dz = cz; }
+    }
+    if (wpos >= 0) W.sb[wpos] = wr;
+    Q3T(17);
+    // the furthest point ends each set
+    if (g < ndnew && pc) {
+      W.sb[doff + dcnt - 1] = dchamp;
+      W.soff[f] = doff;
+      W.fdist[f] = dmax;
+      q3_set_cc(W, L, f, (unsigned)dcnt | ((unsigned)dchamp << 16));
+    }
+    // the queue: new facets with points in key order (a new facet's key is
+    // this insertion's first key + its index, from the adoption)
+    const bool has = g < ndnew && pc > 0;
+    const unsigned long long b = __ballot(has);
+    int qt = S.qtail;
+    if (has) {
+      const int at = qt + __popcll(b & ltmask);
+      if (at < W.QC) {
+        W.fq[at] = f;
+        W.fqk[at] = S.key0_last + (unsigned)g;
+        HullPt r;
+        r.x = dx; r.y = dy; r.z = dz; r.q = dchamp; r.pad = 0;
+        W.fqc[at] = r;
+      }
+    }
+    qt += __popcll(b);
+    if (qt > W.QC) S.status |= QHS_CAPACITY | Q3_CAPBIT(QHS_CAP_FACETS);
+    S.qtail = qt;
+    hl_sync();
+    Q3T(18);
+    return;
+  }
   // segments: an exclusive scan of the destinations' sizes
   const int nd = ndnew + S.nold;
   int base = S.sbtop;
