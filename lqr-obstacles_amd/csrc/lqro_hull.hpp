@@ -138,6 +138,17 @@ struct HullArgs {
   // finished) before it leaves; null: leave at once
   const int* prod_done;
   int prod_total;
+  // Qhull order, speculative builds (PairArgs::spec_mark): a job whose slot
+  // is marked >= 2 was queued before its pair was evaluated; the build
+  // commits only once the mark is 3.  null: off
+  const unsigned char* spec_mark;
+  // ... and their queue entries 0 .. *spec_n - 1 are handed out by a plain
+  // counter (*spec_next, one atomicAdd a worker: at the step's start every
+  // side worker asks at once, and the head's compare-and-swap would hand
+  // them out one round trip at a time); the queue's own head starts at
+  // *spec_n.  null: off
+  const int* spec_n;
+  int* spec_next;
 };
 
 // (LQRO_ROW_BIG, lqro_device.hpp: the row counter's protocol; the early LP
@@ -442,7 +453,15 @@ __device__ __forceinline__ int hull_take_job(const HullArgs& A, LT& L, bool retr
     // launch appends later are still taken (by the k_hull after the sweep)
     int job = -1, slot = -1;
     long waited = 0;
-    for (;;) {
+    if (A.spec_next && !retryq) {
+      const int m = __hip_atomic_load(A.spec_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int j = m > 0 ? atomicAdd(A.spec_next, 1) : m;
+      if (j < m) {   // (written by k_prio_prev, a kernel before this one)
+        job = j;
+        slot = queue[j];
+      }
+    }
+    for (; job < 0;) {
       // (the producers' count first: once it is complete, every job they
       // appended is in qcount)
       const int pd = (A.prod_done && !retryq) ? __hip_atomic_load(A.prod_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)

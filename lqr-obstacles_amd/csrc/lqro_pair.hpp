@@ -74,6 +74,11 @@ struct PairArgs {
   int hot_cap;
   int hot_only;                       // 1: this launch computes the hot list only
   int* hot_done;                      // hot launch: +1 per finished workgroup (k_qhull workers wait on it), null: none
+  // Qhull order, speculative builds: per slot 2 = the last step's inside-hull
+  // pair, already queued for k_qhull at the step's start; this hot launch
+  // evaluates it and sets 3 (inside: the build may commit) or 4 (not: the
+  // build is discarded), after its plane and record, with a release.  null: off
+  unsigned char* spec_mark;
   const int* nbr_list;                // culling on: per row npr (= K) neighbour jj, ascending, -1 = none
   double* qnrm;                       // LQRO_FLAG_QHULL_ORDER: per slot normal, dist (k_stale reads them)
   int* rowpend;                       // early LP: per row open work (LQRO_ROW_BIG), null: off
@@ -718,7 +723,10 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
       } else {
         if (P.rowpend && inside) atomicAdd(&P.rowpend[lrow], 1);   // before its job is visible
       }
-      if (inside) {
+      // (a speculative pair is in the queue already: its build only waits
+      // for the verdict, stored below after the record)
+      const bool spec = HOT != kRowLaunch && P.spec_mark != nullptr && P.spec_mark[slot] == 2;
+      if (inside && !spec) {
         // published with release: k_hull workers may already be polling
         const int qi = atomicAdd(P.hull_count, 1);
         if (qi < P.hull_cap)
@@ -741,6 +749,11 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
           rec.plane_normal[q] = pl[3 + q];
         }
         P.recs[slot] = rec;
+      }
+      if (spec) {   // the verdict for the speculative build, after the plane and record
+        __threadfence();
+        __hip_atomic_store(P.spec_mark + slot, (unsigned char)(inside ? 3 : 4), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     wave_lds_sync();
@@ -1020,15 +1033,23 @@ struct PrioArgs {
   const int* prevn;
   int* hot1n;     // the first launch's pair count
   int* hot2next;  // the second launch's first list position
+  // speculative builds: the last step's inside-hull pairs also go straight
+  // into the hull queue (hq, hcount); the main hot launch then evaluates the
+  // whole list (null: off)
+  int* hq;
+  int* hcount;
+  int hq_cap;
+  int* spec_n;   // (the speculative entries' count, for hull_take_job)
 };
 
 // the last step's inside-hull pairs at the head of the hot list (one block)
 __global__ void __launch_bounds__(256) k_prio_prev(PrioArgs A) {
   const long total = (long)A.nrows * A.npr;
-  const int m = min(*A.prevn, A.cap);
+  const int m = min(min(*A.prevn, A.cap), A.hq ? A.hq_cap : A.cap);
   for (int q = threadIdx.x; q < m; q += blockDim.x) {
     const int slot = A.prev[q];
     A.list[q] = slot;
+    if (A.hq) A.hq[q] = slot;
     if (slot >= 0 && slot < total) {
       A.mark[slot] = 2;
       if (A.rowpend) atomicAdd(&A.rowpend[slot / A.npr], 1);
@@ -1037,14 +1058,20 @@ __global__ void __launch_bounds__(256) k_prio_prev(PrioArgs A) {
   if (threadIdx.x == 0) {
     *A.count = m;
     *A.hot1n = m;
-    *A.hot2next = m;
+    *A.hot2next = A.hq ? 0 : m;
+    if (A.hq) {
+      A.hcount[0] = m;   // the queue's count
+      A.hcount[1] = m;   // its head, past the entries handed out by spec_next
+      *A.spec_n = m;
+    }
   }
 }
 
 // the step's inside-hull pairs (its hull queue) for the next step's
 // k_prio_prev (one block; the order does not matter: schedule only)
 __global__ void __launch_bounds__(256) k_prio_save(const int* hq, const int* hcount, int cap_hq, int* prev,
-                                                   int* prevn, int cap) {
+                                                   int* prevn, int cap, const unsigned char* mark) {
+  // (mark: speculative builds on — a queued pair marked 4 was not inside)
   __shared__ int n;
   if (threadIdx.x == 0) n = 0;
   __syncthreads();
@@ -1052,6 +1079,7 @@ __global__ void __launch_bounds__(256) k_prio_save(const int* hq, const int* hco
   for (int q = threadIdx.x; q < c; q += blockDim.x) {
     const int slot = hq[q];
     if (slot < 0) continue;
+    if (mark && mark[slot] == 4) continue;
     const int at = atomicAdd(&n, 1);
     if (at < cap) prev[at] = slot;
   }
@@ -1088,7 +1116,7 @@ __global__ void __launch_bounds__(256) k_prio(PrioArgs A) {
       A.list[pos] = (int)slot;
       if (A.rowpend) atomicAdd(&A.rowpend[slot / A.npr], 1);
     }
-    if (slot < total) A.mark[slot] = (hot || pre) ? 1 : 0;
+    if (slot < total) A.mark[slot] = pre ? 2 : (hot ? 1 : 0);
   }
 }
 #endif  // LQRO_PAIR_TU

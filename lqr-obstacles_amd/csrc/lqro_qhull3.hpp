@@ -2831,6 +2831,9 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
     const int slot = hull_take_job(A, L, false);
     if (slot < 0) break;
     const unsigned long long tjob = __builtin_amdgcn_s_memrealtime();   // (lqro_get_hull_builds)
+    // a speculative job (the last step's inside-hull pair, queued before
+    // its evaluation): built now, committed only if the pair is inside
+    const bool spec = A.spec_mark != nullptr && A.spec_mark[slot] >= 2;
     // a fresh handshake and wave 1's epochs for this job (ordered by
     // hull_points' barriers)
     if (threadIdx.x == 0) { L.ph = 0; L.sp_done = 0; L.sp_gdone = 0; L.hstate = 0; L.sp_hz = 0; L.pf_done = 0; }
@@ -2954,7 +2957,27 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
     else q3_build(W, S, L, n, lane);
     hl_sync();
     if (lane == 0) q3_st_rel(&L.ph, -1);   // the build is over: wave 1 stops
-    if (S.status & QHS_CAPACITY) {
+    bool keep = true;
+    if (spec) {
+      // the pair's verdict from the hot launch (3 inside, 4 not; it is
+      // normally in long before the build ends); bounded wait
+      int m = 0;
+      if (lane == 0) {
+        m = __hip_atomic_load(A.spec_mark + slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        for (long w = 0; m == 2 && w < (1l << 26); ++w) {
+          __builtin_amdgcn_s_sleep(8);
+          m = __hip_atomic_load(A.spec_mark + slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (m == 2) {   // never evaluated (not expected): reported, nothing committed
+          atomicAdd(&A.stats[LQRO_ST_TIMEOUT], 1ull);
+          hull_fail_note(A.stats, slot);
+        }
+      }
+      keep = __builtin_amdgcn_readfirstlane(m) == 3;
+    }
+    if (!keep) {
+      // not inside this step: k_pair wrote its plane; the build is dropped
+    } else if (S.status & QHS_CAPACITY) {
       if (lane == 0) {
         atomicAdd(&A.stats[LQRO_ST_RETRY], 1ull);
         if (S.status & QHS_TIMEOUT) atomicAdd(&A.stats[LQRO_ST_TIMEOUT], 1ull);

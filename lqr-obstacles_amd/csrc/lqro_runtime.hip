@@ -381,6 +381,7 @@ struct lqro_ctx {
   int* d_hot2;               // [0] their count, [1] first hot launch's count, [2] its next, [3] the
                              // second's next, [4] its finished workgroups
   int hot_split;             // LQRO_HOT_SPLIT (default 1): the split hot launch in Qhull order
+  int hot_spec;              // LQRO_HOT_SPEC (default 1): with the split, the last step's inside pairs are built speculatively from the step's start
   unsigned char* d_hotmark;  // per slot: in the hot list
   int* d_nbrlist;            // culling on: per row K neighbour slots (lqro_set_neighbors)
   double nbr_r2;
@@ -656,6 +657,8 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
     // than behind the other hot pairs' stragglers (which go to the main stream)
     const char* hs = getenv("LQRO_HOT_SPLIT");
     c->hot_split = hs ? atoi(hs) != 0 : 1;
+    const char* hp = getenv("LQRO_HOT_SPEC");
+    c->hot_spec = hp ? atoi(hp) != 0 : 1;
     // off by default: with 3 waves a CU the side workers sweep rows at ~1/5 of a
     // 16-wave workgroup's rate, so where the sweep outlasts the builds (C4:
     // 227 vs 114 ms per step) it loses; at C3 it ties (22.0 ms either way)
@@ -945,6 +948,12 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   // wait for the main hot launch before leaving an empty queue.
   const bool split = hot && c->qhull_order && c->hot_split && !qside && !c->qhull_big && known &&
                      inside_prev + inside_prev / 16 + 4 <= (unsigned long long)nwait;
+  // speculative builds (with the split): the last step's inside-hull pairs go
+  // straight into the hull queue, so the side's k_qhull workers start building
+  // them at once instead of after their evaluation (~0.5 ms at C3); the main
+  // stream's hot launch evaluates them first, and each build commits only if
+  // its pair is inside (PairArgs::spec_mark)
+  const bool spec = split && c->hot_spec;
   if (hot) {
     PrioArgs Q{};
     Q.npr = c->npr; Q.nrows = c->nrows; Q.row_begin = c->rb; Q.row_stride = c->rs; Q.X = g.x_dim; Q.x = d_x;
@@ -952,8 +961,9 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
     Q.list = c->d_hotlist; Q.mark = c->d_hotmark; Q.count = c->d_hcount + 6; Q.cap = c->hot_cap;
     Q.rowpend = P.rowpend;
     if (split) {
-      HIPCHK(hipMemsetAsync(c->d_hot2 + 1, 0, sizeof(int) * 4, s));
+      HIPCHK(hipMemsetAsync(c->d_hot2 + 1, 0, sizeof(int) * 6, s));
       Q.prev = c->d_prevq; Q.prevn = c->d_hot2; Q.hot1n = c->d_hot2 + 1; Q.hot2next = c->d_hot2 + 3;
+      if (spec) { Q.hq = c->d_hq; Q.hcount = c->d_hcount; Q.hq_cap = c->hull_cap; Q.spec_n = c->d_hot2 + 5; }
       hipLaunchKernelGGL(k_prio_prev, dim3(1), dim3(256), 0, s, Q);
       HIPCHK(hipGetLastError());
     }
@@ -1007,6 +1017,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
     P2.hot_only = 1;
     P2.hot_next = c->d_hot2 + 3;
     P2.hot_done = c->d_hot2 + 4;
+    if (spec) P2.spec_mark = c->d_hotmark;   // (its list from position 0: the speculative pairs first)
     launch_pair(g.x_dim, dim3(nblk), dim3(P.waves * 64), c->lds_bytes, s, P2);
     HIPCHK(hipGetLastError());
   }
@@ -1027,8 +1038,10 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
     PairArgs Ph = P;
     Ph.hot_only = 1;
     if (split) { Ph.hot_count = c->d_hot2 + 1; Ph.hot_next = c->d_hot2 + 2; }
-    launch_pair(g.x_dim, dim3(nwait), dim3(P.waves * 64), c->lds_bytes, c->side, Ph);
-    HIPCHK(hipGetLastError());
+    if (!spec) {   // (speculative builds: the side goes straight to k_qhull)
+      launch_pair(g.x_dim, dim3(nwait), dim3(P.waves * 64), c->lds_bytes, c->side, Ph);
+      HIPCHK(hipGetLastError());
+    }
     if (c->qhull_order) {
       // the hot pairs' hulls in Qhull's order (k_qhull leaves when the queue
       // is empty), then the row sweep
@@ -1042,6 +1055,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
         if (!c->qhull_big) {
           HullArgs Hs = Hh;
           if (split) { Hs.prod_done = c->d_hot2 + 4; Hs.prod_total = (int)nblk; }
+          if (spec) { Hs.spec_mark = c->d_hotmark; Hs.spec_n = c->d_hot2 + 5; Hs.spec_next = c->d_hot2 + 6; }
           launch_qhull(dim3(std::min(nwait, c->qworkers)), c->side, Hs);
           HIPCHK(hipGetLastError());
         }
@@ -1082,6 +1096,9 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   if (c->qhull_order) {
     // every hull job left, the ones beyond k_qhull's caps, then the facet-0
     // pairs' loop-carried normals
+    if (spec) {   // (a speculative job not taken on the side)
+      Hh.spec_mark = c->d_hotmark; Hh.spec_n = c->d_hot2 + 5; Hh.spec_next = c->d_hot2 + 6;
+    }
     if (!c->qhull_big) {
       launch_qhull(dim3(c->qworkers), s, Hh);
       HIPCHK(hipGetLastError());
@@ -1092,7 +1109,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
     Hh.big_main = 0;
     // this step's inside-hull pairs head the next step's hot list
     hipLaunchKernelGGL(k_prio_save, dim3(1), dim3(256), 0, s, c->d_hq, c->d_hcount, c->hull_cap, c->d_prevq,
-                       c->d_hot2, c->hot_cap);
+                       c->d_hot2, c->hot_cap, spec ? (const unsigned char*)c->d_hotmark : nullptr);
     HIPCHK(hipGetLastError());
     if (phase == 0) {
       launch_stale(s, c->d_planes, c->d_qnrm, c->d_qstale, c->d_hcount + 15, c->hull_cap, d_x, g.x_dim, npr, c->rb,

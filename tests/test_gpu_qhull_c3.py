@@ -7,9 +7,11 @@ was pinned:
   newV bit for bit against the oracle in set_hull_rule(1), in every schedule
   the step can take there — the default (hot launch, side builds, early LP:
   the row-counting protocol of lqro_hull.hpp hull_row_done that closes a row
-  and runs its LP inside k_qhull; from the third step the split hot launch:
-  the last step's inside-hull pairs alone on the side stream, k_qhull's
-  workers waiting for the main stream's hot launch), LQRO_EARLY_LP=0,
+  and runs its LP inside k_qhull; from the third step the speculative builds:
+  the last step's inside-hull pairs queued for k_qhull at the step's start,
+  built at once, committed when the main stream's hot launch finds them
+  inside, dropped when it does not), LQRO_HOT_SPEC=0 (the split hot launch:
+  those pairs evaluated alone on the side stream first), LQRO_EARLY_LP=0,
   LQRO_HOT_SPLIT=0, LQRO_QSIDE=1 (side workers sweep rows after their
   builds) and LQRO_HOT=0 (plain);
 - C5 (16384 agents, X = 12, H = 200, per-agent gains): the 8-way shard
@@ -50,12 +52,13 @@ def c3_oracle(lqro_mod, oracle, gains):
     return x, vg, rv, rr, carry
 
 
-@pytest.mark.parametrize("sched", ["default", "early_lp_off", "no_split", "qside", "plain"])
+@pytest.mark.parametrize("sched", ["default", "no_spec", "early_lp_off", "no_split", "qside", "plain"])
 def test_qhull_order_c3_full_step(lqro_mod, gains, monkeypatch, c3_oracle, sched):
     x, vg, rv, rr, carry = c3_oracle
-    env = {"default": {}, "early_lp_off": {"LQRO_EARLY_LP": "0"}, "no_split": {"LQRO_HOT_SPLIT": "0"},
-           "qside": {"LQRO_QSIDE": "1"}, "plain": {"LQRO_HOT": "0"}}[sched]
-    for k in ("LQRO_EARLY_LP", "LQRO_QSIDE", "LQRO_HOT", "LQRO_LOCAL_HULL", "LQRO_SIDE_HULL_CUS", "LQRO_HOT_SPLIT"):
+    env = {"default": {}, "no_spec": {"LQRO_HOT_SPEC": "0"}, "early_lp_off": {"LQRO_EARLY_LP": "0"},
+           "no_split": {"LQRO_HOT_SPLIT": "0"}, "qside": {"LQRO_QSIDE": "1"}, "plain": {"LQRO_HOT": "0"}}[sched]
+    for k in ("LQRO_EARLY_LP", "LQRO_QSIDE", "LQRO_HOT", "LQRO_LOCAL_HULL", "LQRO_SIDE_HULL_CUS", "LQRO_HOT_SPLIT",
+              "LQRO_HOT_SPEC"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
