@@ -381,6 +381,7 @@ struct lqro_ctx {
   int* d_hot2;               // [0] their count, [1] first hot launch's count, [2] its next, [3] the
                              // second's next, [4] its finished workgroups
   int hot_split;             // LQRO_HOT_SPLIT (default 1): the split hot launch in Qhull order
+  int qspare;                // LQRO_QHULL_SPARE: side CUs beyond the last step's inside-hull count (default 4; -1: count/16 + 4)
   int hot_spec;              // LQRO_HOT_SPEC (default 1): with the split, the last step's inside pairs are built speculatively from the step's start
   unsigned char* d_hotmark;  // per slot: in the hot list
   int* d_nbrlist;            // culling on: per row K neighbour slots (lqro_set_neighbors)
@@ -659,6 +660,8 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
     c->hot_split = hs ? atoi(hs) != 0 : 1;
     const char* hp = getenv("LQRO_HOT_SPEC");
     c->hot_spec = hp ? atoi(hp) != 0 : 1;
+    const char* qsp = getenv("LQRO_QHULL_SPARE");
+    c->qspare = qsp ? atoi(qsp) : 4;
     // off by default: with 3 waves a CU the side workers sweep rows at ~1/5 of a
     // 16-wave workgroup's rate, so where the sweep outlasts the builds (C4:
     // 227 vs 114 ms per step) it loses; at C3 it ties (22.0 ms either way)
@@ -889,12 +892,18 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   const bool known = inside_prev != ~0ull;
   const bool lhull = c->local_hull || c->qhull_order;   // k_lhull or k_qhull on the side
   int side = lhull ? c->lside_cus : c->side_cus;
+  const unsigned long long qspare =
+      !known ? 0ull : c->qspare >= 0 ? (unsigned long long)c->qspare : inside_prev / 16 + 4;
   if (c->qhull_order) {
     // Qhull's build is one long dependent chain per pair (one wave per CU):
     // the side takes one CU per expected hull, so every hot hull starts at
-    // once, leaving at least an eighth of the CUs to the sweep (unknown
-    // count: half the CUs)
-    const unsigned long long want = known ? inside_prev + inside_prev / 16 + 4 : (unsigned long long)(c->n_cu / 2);
+    // once, plus a few for pairs new this step (LQRO_QHULL_SPARE, default 4:
+    // a pair beyond them waits for the first build to end), leaving at least
+    // an eighth of the CUs to the sweep (unknown count: half the CUs).  With
+    // speculative builds the main stream's sweep is as long as the slowest
+    // build: each CU given back to it shortens the step (C3: 192 -> 181 side
+    // CUs, 19.85 -> 19.35 ms, profiles/r5ak_ab_qhull_spare.txt)
+    const unsigned long long want = known ? inside_prev + qspare : (unsigned long long)(c->n_cu / 2);
     side = (int)std::min<unsigned long long>((unsigned long long)(c->n_cu - c->n_cu / 8),
                                              std::max<unsigned long long>((unsigned long long)side, want));
   } else if (lhull) {
@@ -947,7 +956,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   // k_qhull; main: k_prio's other hot pairs, then the rows.  k_qhull's workers
   // wait for the main hot launch before leaving an empty queue.
   const bool split = hot && c->qhull_order && c->hot_split && !qside && !c->qhull_big && known &&
-                     inside_prev + inside_prev / 16 + 4 <= (unsigned long long)nwait;
+                     inside_prev + qspare <= (unsigned long long)nwait;
   // speculative builds (with the split): the last step's inside-hull pairs go
   // straight into the hull queue, so the side's k_qhull workers start building
   // them at once instead of after their evaluation (~0.5 ms at C3); the main
