@@ -92,6 +92,62 @@ def test_qhull_order_c3_full_step(lqro_mod, gains, monkeypatch, c3_oracle, sched
         ctx.close()
 
 
+@pytest.fixture(scope="module")
+def c3_oracle_moved(lqro_mod, oracle, gains, c3_oracle):
+    """The C3 swarm 1 s later (positions advanced by their velocities): its
+    inside-hull pairs differ from the first swarm's both ways."""
+    x, vg = c3_oracle[0], c3_oracle[1]
+    x1 = x.copy()
+    x1[:, 0:3] += 1.0 * x[:, 3:6]
+    T, NCF = oracle.tables(gains["A"], gains["B"], gains["L"], gains["E"], 100)
+    oracle.set_hull_rule(1, round16=True)
+    oracle.carry_normal(np.zeros(3))
+    try:
+        rv, rr = oracle.step(T, NCF, oracle.sphere(100), x1, vg, threads=16)
+        carry = oracle.carry_normal()
+    finally:
+        oracle.set_hull_rule(0)
+    return x1, rv, rr, carry
+
+
+def test_speculative_builds_moving_swarm(lqro_mod, gains, monkeypatch, c3_oracle, c3_oracle_moved):
+    """Speculative builds when the inside-hull set changes between steps: the
+    swarm at x0, x0, x1, x0 — the third step's builds were queued for x0's
+    inside pairs (those not inside at x1 are dropped, x1's new ones queued by
+    their evaluation), the fourth's for x1's.  Each step bit for bit against
+    the oracle at its own state, in the default schedule."""
+    x0, vg, rv0, rr0, carry0 = c3_oracle
+    x1, rv1, rr1, carry1 = c3_oracle_moved
+    for k in ("LQRO_EARLY_LP", "LQRO_QSIDE", "LQRO_HOT", "LQRO_LOCAL_HULL", "LQRO_SIDE_HULL_CUS", "LQRO_HOT_SPLIT",
+              "LQRO_HOT_SPEC", "LQRO_QHULL_SPARE"):
+        monkeypatch.delenv(k, raising=False)
+    in0 = (rr0["flags"] & lqro_mod.REC_INSIDE) != 0
+    in1 = (rr1["flags"] & lqro_mod.REC_INSIDE) != 0
+    assert (in0 & ~in1).sum() > 0 and (in1 & ~in0).sum() > 0, ((in0 & ~in1).sum(), (in1 & ~in0).sum())
+    N = x0.shape[0]
+    ctx = lqro_mod.Context(lqro_mod.config(N, 100, 100,
+                                           flags=lqro_mod.LQRO_FLAG_RECORDS | lqro_mod.LQRO_FLAG_QHULL_ORDER))
+    ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
+    try:
+        for t, (x, rv, rr, carry) in enumerate([(x0, rv0, rr0, carry0), (x0, rv0, rr0, carry0),
+                                                (x1, rv1, rr1, carry1), (x0, rv0, rr0, carry0)]):
+            ctx.carry_normal(np.zeros(3))
+            v = ctx.step(x, vg)
+            r = ctx.records()
+            st = ctx.stats()
+            assert st["hull_fail"] == 0 and st["qhull_timeouts"] == 0
+            _compare(r, rr)
+            for f in QFIELDS:
+                a, b = r[f], rr[f]
+                if f == "flags":
+                    a = a & ~lqro_mod.REC_LOCAL
+                assert np.array_equal(_bits(a), _bits(b)), (t, f)
+            assert np.array_equal(v.view(np.uint64), rv.view(np.uint64)), t
+            assert np.array_equal(ctx.carry_normal(), carry), t
+    finally:
+        ctx.close()
+
+
 def test_c5_qhull_order_rows(lqro_mod, oracle):
     """C5's first 8-way shard in Qhull order: 32 rows spread over it against
     the oracle, bit for bit, each row entered with the normal the rows before
