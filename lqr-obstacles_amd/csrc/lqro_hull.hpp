@@ -149,6 +149,10 @@ struct HullArgs {
   // *spec_n.  null: off
   const int* spec_n;
   int* spec_next;
+  // early LP: 1 when a k_qhull job that closes a row may run its LP in its
+  // own LDS (rows of at most LQRO_EARLY_LP_MAX_NPR pairs); 0: such rows are
+  // left to the tail
+  int row_lp;
 };
 
 // (LQRO_ROW_BIG, lqro_device.hpp: the row counter's protocol; the early LP

@@ -1068,11 +1068,19 @@ __global__ void __launch_bounds__(256) k_prio_prev(PrioArgs A) {
 }
 
 // the step's inside-hull pairs (its hull queue) for the next step's
-// k_prio_prev (one block; the order does not matter: schedule only)
+// k_prio_prev (one block; the order is schedule only): longest build first
+// when this step's build records (hbuild: slot | kernel << 40, start, end)
+// are given, so that with fewer side workers than builds the short ones
+// wait (longest-processing-time-first)
+constexpr int kSaveSort = 1024;
 __global__ void __launch_bounds__(256) k_prio_save(const int* hq, const int* hcount, int cap_hq, int* prev,
-                                                   int* prevn, int cap, const unsigned char* mark) {
+                                                   int* prevn, int cap, const unsigned char* mark,
+                                                   const unsigned long long* hbuild,
+                                                   const unsigned long long* nbuild, int hbuild_cap) {
   // (mark: speculative builds on — a queued pair marked 4 was not inside)
   __shared__ int n;
+  __shared__ unsigned long long key[kSaveSort];   // duration << 32 | slot
+  __shared__ unsigned long long rec[kSaveSort];   // the builds: duration << 32 | slot
   if (threadIdx.x == 0) n = 0;
   __syncthreads();
   const int c = min(*hcount, cap_hq);
@@ -1082,9 +1090,34 @@ __global__ void __launch_bounds__(256) k_prio_save(const int* hq, const int* hco
     if (mark && mark[slot] == 4) continue;
     const int at = atomicAdd(&n, 1);
     if (at < cap) prev[at] = slot;
+    if (at < kSaveSort) key[at] = (unsigned)slot;
   }
   __syncthreads();
-  if (threadIdx.x == 0) *prevn = min(n, cap);
+  const int m = min(n, cap);
+  const int nb = hbuild ? (int)min(*nbuild, (unsigned long long)hbuild_cap) : 0;
+  if (hbuild && m > 1 && m <= kSaveSort && nb <= kSaveSort) {
+    for (int k = threadIdx.x; k < nb; k += blockDim.x) {
+      const unsigned long long* r = hbuild + 4 * k;
+      const unsigned long long d = min(r[2] - r[1], 0x7fffffffull);
+      rec[k] = (d << 32) | (unsigned)r[0];
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < m; q += blockDim.x) {
+      const unsigned slot = (unsigned)key[q];
+      unsigned long long d = 0;
+      for (int k = 0; k < nb; ++k)
+        if ((unsigned)rec[k] == slot) d = max(d, rec[k] >> 32);
+      key[q] = (d << 32) | slot;
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < m; q += blockDim.x) {
+      const unsigned long long kq = key[q];
+      int r = 0;
+      for (int p = 0; p < m; ++p) r += key[p] > kq;
+      prev[r] = (int)(unsigned)kq;
+    }
+  }
+  if (threadIdx.x == 0) *prevn = m;
 }
 
 __global__ void __launch_bounds__(256) k_prio(PrioArgs A) {

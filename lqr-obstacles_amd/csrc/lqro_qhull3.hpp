@@ -2789,7 +2789,7 @@ __device__ inline bool q3_select(const HullArgs& A, const Q3W& W, const Q3L& L, 
         }
       }
     }
-    go = hull_row_done(A, slot, stale, true);
+    go = hull_row_done(A, slot, stale, A.row_lp != 0);
   }
   hl_sync();
   return __builtin_amdgcn_readfirstlane(go) != 0;

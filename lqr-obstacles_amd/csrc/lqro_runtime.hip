@@ -381,6 +381,7 @@ struct lqro_ctx {
   int* d_hot2;               // [0] their count, [1] first hot launch's count, [2] its next, [3] the
                              // second's next, [4] its finished workgroups
   int hot_split;             // LQRO_HOT_SPLIT (default 1): the split hot launch in Qhull order
+  int qside_pct;             // LQRO_QHULL_SIDE_PCT: side CUs per 100 of the last step's inside-hull pairs (default 100)
   int qspare;                // LQRO_QHULL_SPARE: side CUs beyond the last step's inside-hull count (default 4; -1: count/16 + 4)
   int hot_spec;              // LQRO_HOT_SPEC (default 1): with the split, the last step's inside pairs are built speculatively from the step's start
   unsigned char* d_hotmark;  // per slot: in the hot list
@@ -662,6 +663,8 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
     c->hot_spec = hp ? atoi(hp) != 0 : 1;
     const char* qsp = getenv("LQRO_QHULL_SPARE");
     c->qspare = qsp ? atoi(qsp) : 4;
+    const char* qpc = getenv("LQRO_QHULL_SIDE_PCT");
+    c->qside_pct = qpc ? std::max(1, std::min(100, atoi(qpc))) : 100;
     // off by default: with 3 waves a CU the side workers sweep rows at ~1/5 of a
     // 16-wave workgroup's rate, so where the sweep outlasts the builds (C4:
     // 227 vs 114 ms per step) it loses; at C3 it ties (22.0 ms either way)
@@ -894,6 +897,10 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   int side = lhull ? c->lside_cus : c->side_cus;
   const unsigned long long qspare =
       !known ? 0ull : c->qspare >= 0 ? (unsigned long long)c->qspare : inside_prev / 16 + 4;
+  // the side's builds (workers): the last step's inside-hull count, or a
+  // share of it (LQRO_QHULL_SIDE_PCT: the longest builds first, k_prio_save)
+  const unsigned long long qwant =
+      known ? (inside_prev * (unsigned long long)c->qside_pct + 99ull) / 100ull + qspare : 0ull;
   if (c->qhull_order) {
     // Qhull's build is one long dependent chain per pair (one wave per CU):
     // the side takes one CU per expected hull, so every hot hull starts at
@@ -903,7 +910,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
     // speculative builds the main stream's sweep is as long as the slowest
     // build: each CU given back to it shortens the step (C3: 192 -> 181 side
     // CUs, 19.85 -> 19.35 ms, profiles/r5ak_ab_qhull_spare.txt)
-    const unsigned long long want = known ? inside_prev + qspare : (unsigned long long)(c->n_cu / 2);
+    const unsigned long long want = known ? qwant : (unsigned long long)(c->n_cu / 2);
     side = (int)std::min<unsigned long long>((unsigned long long)(c->n_cu - c->n_cu / 8),
                                              std::max<unsigned long long>((unsigned long long)side, want));
   } else if (lhull) {
@@ -939,10 +946,11 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   if (qside && !c->per_agent) P.row_split = std::max(P.row_split, std::min(16, std::max(1, npr / 128)));
   // early LP (Qhull order, beside the hulls): a row whose planes are all
   // final runs its LP at once — in a k_lp_lds after the main sweep, or in the
-  // k_qhull job that completes it (lqro_hull.hpp hull_row_done) — and the
+  // k_qhull job that completes it (lqro_hull.hpp hull_row_done; rows of at
+  // most LQRO_EARLY_LP_MAX_NPR pairs, longer ones go to the tail) — and the
   // tail only runs the rest (rows waiting on k_stale, rows closed late)
   const bool early = hot && c->early_lp && c->qhull_order && !c->qhull_big && phase == 0 && c->nbr_k <= 0 &&
-                     (size_t)npr * 32 <= 64 * 1024 && npr <= LQRO_EARLY_LP_MAX_NPR && d_newv != nullptr;
+                     (size_t)npr * 32 <= kLpLdsMax && d_newv != nullptr;
   c->early_step = early ? 1 : 0;
   P.rowpend = early ? c->d_rowpend : nullptr;
   if (early) HIPCHK(hipMemsetAsync(c->d_rowpend, 0, sizeof(int) * 2 * (size_t)c->nrows, s));
@@ -956,7 +964,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   // k_qhull; main: k_prio's other hot pairs, then the rows.  k_qhull's workers
   // wait for the main hot launch before leaving an empty queue.
   const bool split = hot && c->qhull_order && c->hot_split && !qside && !c->qhull_big && known &&
-                     inside_prev + qspare <= (unsigned long long)nwait;
+                     qwant <= (unsigned long long)nwait;
   // speculative builds (with the split): the last step's inside-hull pairs go
   // straight into the hull queue, so the side's k_qhull workers start building
   // them at once instead of after their evaluation (~0.5 ms at C3); the main
@@ -1012,6 +1020,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   Hh.qscratch = c->d_qscratch; Hh.qstride = c->qstride; Hh.qnrm = c->d_qnrm;
   Hh.qstale = c->d_qstale; Hh.qstale_count = c->d_hcount + 15; Hh.qstale_cap = c->hull_cap;
   Hh.rowpend = P.rowpend; Hh.rowclaim = early ? c->d_rowclaim : nullptr;
+  Hh.row_lp = npr <= LQRO_EARLY_LP_MAX_NPR ? 1 : 0;
   Hh.row_target = P.row_split * LQRO_ROW_BIG;
   Hh.lp_vgoal = d_vgoal; Hh.lp_newv = d_newv; Hh.lp_vmax = g.vmax_lp;
   Hh.hbuild = c->d_hbuild; Hh.hbuild_cap = LQRO_HBUILD_CAP;
@@ -1118,7 +1127,9 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
     Hh.big_main = 0;
     // this step's inside-hull pairs head the next step's hot list
     hipLaunchKernelGGL(k_prio_save, dim3(1), dim3(256), 0, s, c->d_hq, c->d_hcount, c->hull_cap, c->d_prevq,
-                       c->d_hot2, c->hot_cap, spec ? (const unsigned char*)c->d_hotmark : nullptr);
+                       c->d_hot2, c->hot_cap, spec ? (const unsigned char*)c->d_hotmark : nullptr,
+                       (const unsigned long long*)c->d_hbuild, (const unsigned long long*)(c->d_stats + LQRO_ST_NBUILD),
+                       (int)LQRO_HBUILD_CAP);
     HIPCHK(hipGetLastError());
     if (phase == 0) {
       launch_stale(s, c->d_planes, c->d_qnrm, c->d_qstale, c->d_hcount + 15, c->hull_cap, d_x, g.x_dim, npr, c->rb,

@@ -1,6 +1,7 @@
 """Time K steps of the C3 swarm (or a denser box) in the default (Qhull-order)
 rule through lqro.Context; prints per-step ms and the step's statistics.
-usage: c3_step.py [steps] [box side]  (LQRO_LIB: a variant library name)"""
+usage: c3_step.py [steps] [box side]  (LQRO_LIB: a variant library name; STEP_C4_SHARD=1: BASELINE
+config 4's rows [0, 512) of 4096 instead, one rank's work at 8 GPUs)"""
 import os
 import sys
 import time
@@ -13,9 +14,12 @@ if os.environ.get("LQRO_LIB"):
 K = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 box = float(sys.argv[2]) if len(sys.argv) > 2 else None
 N, H, NP = 1024, 100, 100
+shard = {}
+if os.environ.get("STEP_C4_SHARD") == "1":
+    N, shard = 4096, {"row_begin": 0, "row_end": 512}
 x, vg = lqro.synthetic_swarm(N, box=box) if box else lqro.synthetic_swarm(N)
 g = lqro.synthesize_gains()
-c = lqro.Context(lqro.config(N, H, NP))
+c = lqro.Context(lqro.config(N, H, NP, **shard))
 c.set_gains(g["A"], g["B"], g["L"], g["E"])
 import numpy as np  # noqa: E402
 
