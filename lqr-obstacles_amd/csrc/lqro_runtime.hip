@@ -328,6 +328,18 @@ __global__ void __launch_bounds__(64) k_lp4(LpArgs A, int proj_in_lds) {
 
 constexpr size_t kLpLdsMax = 160 * 1024;   // one CU's LDS
 
+// lqro_step_device_end after an early LP in _begin: the rows it ran (claimed
+// 1) have their newV in the context's buffer; the tail wrote the others
+__global__ void __launch_bounds__(256) k_copy_claimed(const int* rowclaim, int nrows, int rb, int rs,
+                                                      const double* src, double* dst) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nrows || rowclaim[r] != 1) return;
+  const size_t i = (size_t)rb + (size_t)r * rs;
+  dst[3 * i] = src[3 * i];
+  dst[3 * i + 1] = src[3 * i + 1];
+  dst[3 * i + 2] = src[3 * i + 2];
+}
+
 template <int PS>
 static hipError_t launch_lp_lds(LpArgs La, hipStream_t s) {
   const size_t lds = (size_t)La.npr * 4 * PS;
@@ -438,6 +450,7 @@ struct lqro_ctx {
   // (lqro_hull.hpp hull_row_done)
   int early_lp;
   int early_step;            // the step being enqueued runs the early LP
+  int early_internal;        // ... into d_newv (lqro_step_device_begin: the caller's buffer comes with _end)
   int qside;                 // LQRO_QSIDE=1: k_qhull side workers sweep rows after their builds (default off)
   int* d_rowpend;
   int* d_rowclaim;
@@ -949,9 +962,14 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   // k_qhull job that completes it (lqro_hull.hpp hull_row_done; rows of at
   // most LQRO_EARLY_LP_MAX_NPR pairs, longer ones go to the tail) — and the
   // tail only runs the rest (rows waiting on k_stale, rows closed late)
-  const bool early = hot && c->early_lp && c->qhull_order && !c->qhull_big && phase == 0 && c->nbr_k <= 0 &&
-                     (size_t)npr * 32 <= kLpLdsMax && d_newv != nullptr;
+  // (the split step, lqro_step_device_begin / _end: the early rows' newV go
+  // to the context's own buffer, copied into the caller's by _end; rows with
+  // a facet-0 pair wait for the row-normal exchange in the tail as before)
+  double* d_lpnv = d_newv != nullptr ? d_newv : (phase == 1 ? c->d_newv : nullptr);
+  const bool early = hot && c->early_lp && c->qhull_order && !c->qhull_big && phase != 2 && c->nbr_k <= 0 &&
+                     (size_t)npr * 32 <= kLpLdsMax && d_lpnv != nullptr;
   c->early_step = early ? 1 : 0;
+  c->early_internal = early && d_lpnv != d_newv ? 1 : 0;
   P.rowpend = early ? c->d_rowpend : nullptr;
   if (early) HIPCHK(hipMemsetAsync(c->d_rowpend, 0, sizeof(int) * 2 * (size_t)c->nrows, s));
   const int units = c->nrows * P.row_split;
@@ -1022,7 +1040,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   Hh.rowpend = P.rowpend; Hh.rowclaim = early ? c->d_rowclaim : nullptr;
   Hh.row_lp = npr <= LQRO_EARLY_LP_MAX_NPR ? 1 : 0;
   Hh.row_target = P.row_split * LQRO_ROW_BIG;
-  Hh.lp_vgoal = d_vgoal; Hh.lp_newv = d_newv; Hh.lp_vmax = g.vmax_lp;
+  Hh.lp_vgoal = d_vgoal; Hh.lp_newv = d_lpnv; Hh.lp_vmax = g.vmax_lp;
   Hh.hbuild = c->d_hbuild; Hh.hbuild_cap = LQRO_HBUILD_CAP;
   if (g.x_dim != 16 && g.x_dim != 12) return LQRO_E_ARG;
   // the row launch is submitted before the side stream's work: should the two
@@ -1044,7 +1062,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   if (early) {
     // the rows the main sweep closed (no open hull): their LP on its CUs
     // while the side stream's hulls run
-    LpArgs Le = lp_args(c, npr, d_vgoal, d_newv);
+    LpArgs Le = lp_args(c, npr, d_vgoal, d_lpnv);
     Le.lp4_list = nullptr;
     Le.rowpend = c->d_rowpend; Le.rowclaim = c->d_rowclaim; Le.row_target = Hh.row_target; Le.mode = 1;
     HIPCHK(hipFuncSetAttribute((const void*)k_lp_lds<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLpLdsMax));
@@ -1186,6 +1204,11 @@ static int enqueue_tail(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
     La.mode = 2;
   }
   HIPCHK(launch_lp(La, s));
+  if (c->early_step && c->early_internal && d_newv != c->d_newv) {   // the rows the early LP ran, into the caller's newV
+    hipLaunchKernelGGL(k_copy_claimed, dim3((unsigned)((c->nrows + 255) / 256)), dim3(256), 0, s, c->d_rowclaim,
+                       c->nrows, c->rb, c->rs, (const double*)c->d_newv, d_newv);
+    HIPCHK(hipGetLastError());
+  }
   HIPCHK(hipMemcpyAsync(c->h_inside + slot, c->d_stats + 2, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
   HIPCHK(hipEventRecord(c->iev[slot], s));
   HIPCHK(hipEventRecord(c->ev[3], s));

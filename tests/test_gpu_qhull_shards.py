@@ -24,13 +24,10 @@ def _full(lqro_mod, gains, x, vg, H, steps):
     return out
 
 
-@pytest.mark.parametrize("world,mode", [(2, "block"), (3, "block"), (3, "cyclic")])
-def test_shards_match_one_context(lqro_mod, gains, world, mode):
+def _shards_vs_full(lqro_mod, gains, x, vg, H, steps, world, mode):
     from test_gpu_dyn import _Hip   # device buffers through liblqro's own HIP runtime
-    N, H, steps = 32, 45, 2
-    x, vg = lqro_mod.synthetic_swarm(N, box=3.0, seed=11)
+    N = x.shape[0]
     ref = _full(lqro_mod, gains, x, vg, H, steps)
-    assert sum(int((r["flags"] & lqro_mod.REC_STALE).astype(bool).sum()) for _, r, _ in ref) > 0
     hip = _Hip()
     d_x, d_vg = hip.put(x), hip.put(vg)
     ctxs = []
@@ -69,6 +66,25 @@ def test_shards_match_one_context(lqro_mod, gains, world, mode):
         for c in ctxs:
             c.close()
         hip.free()
+    return ref
+
+
+@pytest.mark.parametrize("world,mode", [(2, "block"), (3, "block"), (3, "cyclic")])
+def test_shards_match_one_context(lqro_mod, gains, world, mode):
+    x, vg = lqro_mod.synthetic_swarm(32, box=3.0, seed=11)
+    ref = _shards_vs_full(lqro_mod, gains, x, vg, 45, 2, world, mode)
+    assert sum(int((r["flags"] & lqro_mod.REC_STALE).astype(bool).sum()) for _, r, _ in ref) > 0
+
+
+def test_shards_match_one_context_c3(lqro_mod, gains, monkeypatch):
+    """The same at C3's size (two shards of 512 rows): the overlap schedule,
+    the speculative builds (third step) and the early LP run inside
+    lqro_step_device_begin, the early rows' newV reaching the caller's buffer
+    through _end."""
+    for k in ("LQRO_EARLY_LP", "LQRO_QSIDE", "LQRO_HOT", "LQRO_HOT_SPLIT", "LQRO_HOT_SPEC", "LQRO_QHULL_SPARE"):
+        monkeypatch.delenv(k, raising=False)
+    x, vg = lqro_mod.synthetic_swarm(1024)
+    _shards_vs_full(lqro_mod, gains, x, vg, 100, 3, 2, "block")
 
 
 def test_begin_end_call_order(lqro_mod, gains):
