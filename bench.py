@@ -325,42 +325,53 @@ def config_runs(lqro, torch, dev, local, world, rank, dist, steps, mode="block",
     return out
 
 
-def rank_shard_run(lqro, torch, dev, local, N, H, X, gains, per_agent, x, vg, steps, flags, whole_ms):
-    """One rank's work at G = 8 on this GPU: rows [0, N/8) with the full
-    schedule of a rank (lqro_step_device_begin, the row-normal table, _end;
-    the all-gathers themselves are not timed: no other rank).  The 8-GPU
-    step cannot be shorter than this; whole_ms / ms_per_step is the strong-
-    scaling ceiling this build has at 8 GPUs."""
-    rows = (0, N // 8)
-    ctx = lqro.Context(lqro.config(N, H, N_POINTS, x_dim=X, device=local, flags=flags,
-                                   row_begin=rows[0], row_end=rows[1]))
-    ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"], per_agent=per_agent)
+def rank_shard_run(lqro, torch, dev, local, N, H, X, gains, per_agent, x, vg, steps, flags, whole_ms, G=8):
+    """Every rank's work at G = 8, on this GPU, one shard after the other:
+    rows [g N/8, (g+1) N/8) with the full schedule of a rank
+    (lqro_step_device_begin, the row-normal table, _end; the all-gathers
+    themselves are not timed: no other rank).  The 8-GPU step is the slowest
+    rank's and cannot be shorter than the slowest shard's step here, so
+    whole_ms / max is the strong-scaling ceiling this build has at 8 GPUs
+    (SURVEY §8e)."""
     d_x = torch.from_numpy(x).to(dev)
     d_vg = torch.from_numpy(vg).to(dev)
     d_newv = torch.zeros((N, 3), dtype=torch.float64, device=dev)
     rowtab = torch.zeros((N, 4), dtype=torch.float64, device=dev)
     s = torch.cuda.current_stream(dev).cuda_stream
+    shards = []
+    for g in range(G):
+        rows = (g * N // G, (g + 1) * N // G)
+        ctx = lqro.Context(lqro.config(N, H, N_POINTS, x_dim=X, device=local, flags=flags,
+                                       row_begin=rows[0], row_end=rows[1]))
+        ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"], per_agent=per_agent)
 
-    def step():
-        ctx.step_device_begin(d_x.data_ptr(), d_vg.data_ptr(), rowtab.data_ptr(), s)
-        ctx.step_device_end(rowtab.data_ptr(), d_newv.data_ptr(), s)
-    for _ in range(2):
-        step()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    torch.cuda.synchronize(dev)
-    el = time.perf_counter() - t0
-    st = ctx.stats()
-    crit = critical_path(ctx) if flags & lqro.LQRO_FLAG_QHULL_ORDER else None
-    ctx.close()
-    ms = el / steps * 1e3
-    return {"rows": list(rows), "pairs_per_step": (rows[1] - rows[0]) * (N - 1), "steps": steps,
-            "ms_per_step": ms, "strong_scaling_ceiling_g8": whole_ms / ms, "inside_hull": st["inside"],
-            "hull_failures": st["hull_fail"],
-            "slowest_build_ms": crit["slowest_build_ms"] if crit else None,
-            "note": "one rank's rows of the 8-GPU strong-scaled swarm, on this one GPU"}
+        def step():
+            ctx.step_device_begin(d_x.data_ptr(), d_vg.data_ptr(), rowtab.data_ptr(), s)
+            ctx.step_device_end(rowtab.data_ptr(), d_newv.data_ptr(), s)
+        for _ in range(2):   # (the schedule follows the inside-hull count of the step two before)
+            step()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        st = ctx.stats()
+        crit = critical_path(ctx) if flags & lqro.LQRO_FLAG_QHULL_ORDER else None
+        ctx.close()
+        shards.append({"rows": list(rows), "ms_per_step": el / steps * 1e3, "inside_hull": st["inside"],
+                       "hull_failures": st["hull_fail"],
+                       "slowest_build_ms": crit["slowest_build_ms"] if crit else None})
+    ms = [q["ms_per_step"] for q in shards]
+    worst = int(np.argmax(ms))
+    return {"shards": G, "pairs_per_shard_step": (N // G) * (N - 1), "steps": steps,
+            "max_ms_per_step": max(ms), "mean_ms_per_step": float(np.mean(ms)),
+            "slowest_shard_rows": shards[worst]["rows"],
+            "strong_scaling_ceiling_g8": whole_ms / max(ms),
+            "hull_failures": sum(q["hull_failures"] for q in shards),
+            "per_shard": [{k: (round(v, 3) if isinstance(v, float) else v) for k, v in q.items()} for q in shards],
+            "note": "every rank's rows of the 8-GPU strong-scaled swarm, one shard after the other on this one GPU; "
+                    "the ceiling is the whole swarm's step on this GPU over the slowest shard's"}
 
 
 CPP_BENCH = os.path.join(ROOT, "tests", "cpp", "lqro_bench_main")
@@ -614,7 +625,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if world > 1 else "none",   # (weak: the swarm grows with the ranks; N = 1: no scaling)
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (SplitMix64 swarm, seed 0x4C51524F, constant density)",

@@ -35,10 +35,18 @@ enum {
   LQRO_E_SINGULAR = -5,  /* singular 3x3 C*G_k (reference asserts, MAT:632) */
   LQRO_E_NODEVICE = -6,  /* no usable gfx950 device                        */
   LQRO_E_OVERFLOW = -7,  /* an internal work queue overflowed              */
-  LQRO_E_HULL = -8       /* an inside-hull pair's hull could not be built    */
+  LQRO_E_HULL = -8,      /* an inside-hull pair's hull could not be built    */
                          /*   (degenerate / too few points, or every hull    */
                          /*   kernel's capacity exceeded): its half-plane is */
                          /*   missing (lqro_get_hull_failures names pairs)   */
+  LQRO_E_QHMERGE = -9    /* the step completed (newv written), but an inside- */
+                         /*   hull pair's winning facet may be one qconvex's  */
+                         /*   default pre-merge joins (LQRO_REC_QHMERGE_WIN): */
+                         /*   this build restates Qhull merge-free, so that   */
+                         /*   pair's facet, distance and half-plane are not   */
+                         /*   pinned to the reference (LQRO:925-939, 956-967; */
+                         /*   lqro_get_qhmerge_pairs names the pairs).        */
+                         /*   LQRO_E_HULL takes precedence when both apply.   */
 };
 
 /* ---- flags ------------------------------------------------------------- */
@@ -195,7 +203,9 @@ int lqro_set_neighbors(lqro_ctx* ctx, double neighbor_dist, int32_t max_neighbor
  * x: n_agents*X agent states (Quadrotor::x), vgoal: n_agents*3,
  * newv: n_agents*3 (only rows [row_begin,row_end) are written).  Host
  * pointers; blocks until newv is ready.  Returns LQRO_E_HULL (newv still
- * written) when an inside-hull pair got no half-plane. */
+ * written) when an inside-hull pair got no half-plane, else LQRO_E_QHMERGE
+ * (newv written) when an inside-hull pair's winner may be a facet qconvex
+ * merges (LQRO_REC_QHMERGE_WIN). */
 int lqro_step(lqro_ctx* ctx, const double* x, const double* vgoal, double* newv);
 
 /* Same, device-resident: d_x, d_vgoal, d_newv are device pointers on the
@@ -208,7 +218,8 @@ int lqro_step(lqro_ctx* ctx, const double* x, const double* vgoal, double* newv)
 int lqro_step_device(lqro_ctx* ctx, const double* d_x, const double* d_vgoal,
                      double* d_newv, void* stream);
 /* (The device-resident calls cannot report a hull failure when they return:
- * lqro_get_stats()[4] / lqro_get_hull_failures after the step do.  While a
+ * lqro_get_stats()[4] / lqro_get_hull_failures after the step do, and
+ * lqro_get_stats_ex()[11] / lqro_get_qhmerge_pairs the merge suspects.  While a
  * lqro_step_device_begin is pending, every call but lqro_step_device_end
  * returns LQRO_E_STATE.) */
 
@@ -260,6 +271,13 @@ int lqro_get_stats(lqro_ctx* ctx, int64_t* stats8);
  * [11] pairs whose winning facet qconvex's pre-merge may have merged
  *     (LQRO_REC_QHMERGE_WIN). */
 int lqro_get_stats_ex(lqro_ctx* ctx, int64_t* stats, int32_t n);
+
+/* The inside-hull pairs of the last step flagged LQRO_REC_QHMERGE_WIN (stats
+ * [11]; lqro_step then returns LQRO_E_QHMERGE): *n_out = their number;
+ * pairs[2k], pairs[2k+1] = (i, j) of the first min(*n_out, 64, capacity).
+ * Replaces nothing in the reference: it names the pairs whose half-plane
+ * may differ from convexHull's over a merged qconvex facet (LQRO:925-967). */
+int lqro_get_qhmerge_pairs(lqro_ctx* ctx, int64_t* pairs, int64_t capacity, int64_t* n_out);
 
 /* One Qhull-order hull build of the last step (LQRO_FLAG_QHULL_ORDER): the
  * in-kernel replacement of convexHull's qconvex run (LQRO:867-969) for the

@@ -18,8 +18,9 @@
 //     hipMemcpyAsync              vGoal = newV (LQRO:1438), own rows
 //     lqro_dynamics_step_device   findU, propagate, kalmanFilter1/2, findVGoal (LQRO:1439-1445), own rows
 //     ncclAllGather               x of every agent, in place
-//     (host)                      the iteration's hull failures, exchanged so every
-//                                 rank throws lqro::Error(LQRO_E_HULL) together
+//     (host)                      the iteration's hull failures and merge suspects,
+//                                 exchanged so every rank throws lqro::Error
+//                                 (LQRO_E_HULL, else LQRO_E_QHMERGE) together
 //
 // The noise draws follow the reference's single rand() stream in agent order
 // (normal(), LQRO:334-350): every rank draws the whole iteration's stream
@@ -98,7 +99,7 @@ class ShardedSimulator {
     alloc(&d_vg_, na * kV);
     alloc(&d_newv_, na * kV);
     alloc(&d_rowtab_, na * 4);
-    alloc(&d_fail_, na);
+    alloc(&d_fail_, na * 2);
     alloc(&d_rot_, r * 9);
     alloc(&d_xt_, r * kX);
     alloc(&d_rott_, r * 9);
@@ -191,28 +192,38 @@ class ShardedSimulator {
     check_hip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
     ++t_;
     // A hull this rank could not build left a pair without its half-plane
-    // (the reference's qconvex always returns one, LQRO:879-880): never
-    // silently.  Every rank learns the swarm's total (one n x 1 exchange:
-    // each rank's count in its first row), so all of them throw together
-    // and none is left waiting in the next iteration's collectives.
-    int64_t st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (ctx_) check(lqro_get_stats(ctx_, st), "lqro_get_stats");
+    // (the reference's qconvex always returns one, LQRO:879-880), and a pair
+    // whose winner qconvex's pre-merge may join has a half-plane not pinned
+    // to the reference (LQRO:925-967): never silently.  Every rank learns the
+    // swarm's totals (one n x 2 exchange: each rank's two counts in its first
+    // row), so all of them throw together and none is left waiting in the
+    // next iteration's collectives.
+    int64_t st[12] = {0};
+    if (ctx_) check(lqro_get_stats_ex(ctx_, st, 12), "lqro_get_stats_ex");
     rank_hull_fail_ = st[4];
-    std::vector<double> f((size_t)n_, 0.0);
+    rank_qhmerge_ = st[11];
+    std::vector<double> f((size_t)n_ * 2, 0.0);
     if (rows_ > 0) {
-      f[(size_t)rb_] = (double)st[4];
-      put(d_fail_ + rb_, f.data() + rb_, (size_t)rows_);
+      f[2 * (size_t)rb_] = (double)st[4];
+      f[2 * (size_t)rb_ + 1] = (double)st[11];
+      put(d_fail_ + 2 * (size_t)rb_, f.data() + 2 * (size_t)rb_, 2 * (size_t)rows_);
     }
-    ex_(d_fail_, 1, stream_);
-    get(f.data(), d_fail_, (size_t)n_);
-    double tot = 0.0;
-    for (double v : f) tot += v;
+    ex_(d_fail_, 2, stream_);
+    get(f.data(), d_fail_, 2 * (size_t)n_);   // (ordered after the exchange on stream_)
+    double tot = 0.0, totm = 0.0;
+    for (int i = 0; i < n_; ++i) { tot += f[2 * (size_t)i]; totm += f[2 * (size_t)i + 1]; }
     hull_fail_ = (int64_t)tot;
+    qhmerge_ = (int64_t)totm;
     if (hull_fail_ > 0)
       throw Error("lqro::ShardedSimulator: " + std::to_string(hull_fail_) +
                       " inside-hull pair(s) left without a half-plane (rank " + std::to_string(rank_) + ": " +
                       std::to_string(rank_hull_fail_) + "; lqro_get_hull_failures)",
                   LQRO_E_HULL);
+    if (qhmerge_ > 0)
+      throw Error("lqro::ShardedSimulator: " + std::to_string(qhmerge_) +
+                      " inside-hull pair(s) whose winning facet qconvex may merge (rank " + std::to_string(rank_) +
+                      ": " + std::to_string(rank_qhmerge_) + "; lqro_get_qhmerge_pairs)",
+                  LQRO_E_QHMERGE);
     return seed;
   }
 
@@ -220,6 +231,10 @@ class ShardedSimulator {
   // the same number) and this rank's own rows'
   int64_t hull_failures() const { return hull_fail_; }
   int64_t rank_hull_failures() const { return rank_hull_fail_; }
+  // merge-suspect pairs (LQRO_REC_QHMERGE_WIN) of the last iteration: the
+  // swarm's and this rank's
+  int64_t qhmerge_pairs() const { return qhmerge_; }
+  int64_t rank_qhmerge_pairs() const { return rank_qhmerge_; }
 
   // The device state back into qlist: every agent's x, this rank's rows'
   // full state and newV.
@@ -284,8 +299,11 @@ class ShardedSimulator {
   void put(double* d, const double* h, size_t n) {
     check_hip(hipMemcpyAsync(d, h, sizeof(double) * n, hipMemcpyHostToDevice, stream_), "hipMemcpyAsync");
   }
+  // stream-ordered: stream_ is non-blocking, so a plain hipMemcpy on the
+  // null stream would not wait for the exchange enqueued on it
   void get(double* h, const double* d, size_t n) {
-    check_hip(hipMemcpy(h, d, sizeof(double) * n, hipMemcpyDeviceToHost), "hipMemcpy");
+    check_hip(hipMemcpyAsync(h, d, sizeof(double) * n, hipMemcpyDeviceToHost, stream_), "hipMemcpyAsync");
+    check_hip(hipStreamSynchronize(stream_), "hipStreamSynchronize");
   }
   // qlist -> device: every agent's x and vGoal, the own rows' state; the
   // noise variances M, N (LQRO:1285-1286)
@@ -327,7 +345,7 @@ class ShardedSimulator {
 
   std::vector<Quadrotor>& q_;
   int n_ = 0, rank_ = 0, world_ = 1, device_ = 0, rb_ = 0, re_ = 0, rows_ = 0, t_ = 0;
-  int64_t hull_fail_ = 0, rank_hull_fail_ = 0;
+  int64_t hull_fail_ = 0, rank_hull_fail_ = 0, qhmerge_ = 0, rank_qhmerge_ = 0;
   lqro_model model_;
   lqro_ctx* ctx_ = nullptr;
   hipStream_t stream_ = nullptr;

@@ -18,8 +18,10 @@
 #ifndef LQRO_SIM_HPP
 #define LQRO_SIM_HPP
 
+#include <algorithm>
 #include <array>
 #include <cstdint>
+#include <utility>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -103,15 +105,26 @@ class Simulator {
   }
 
   // The pair loop LQRO:1393-1436 on the GPU: every Quadrotor::newV.
+  // LQRO_E_HULL (a pair without its half-plane) and LQRO_E_QHMERGE (a pair
+  // whose winning facet qconvex's pre-merge may join: its half-plane is not
+  // pinned to the reference) still write newV: it is stored, then thrown
+  // as lqro::Error (status(), hull_failures(), qhmerge_pairs() say which).
   void step() {
     for (size_t i = 0; i < q_.size(); ++i)
       for (int c = 0; c < kX; ++c) xs_[i * kX + c] = q_[i].x[c];
     for (size_t i = 0; i < q_.size(); ++i)
       for (int c = 0; c < kV; ++c) vg_[i * kV + c] = q_[i].vGoal[c];
-    check(lqro_step(ctx_, xs_.data(), vg_.data(), nv_.data()), "lqro_step");
-    for (size_t i = 0; i < q_.size(); ++i)
-      for (int c = 0; c < kV; ++c) q_[i].newV[c] = nv_[i * kV + c];
+    const int s = lqro_step(ctx_, xs_.data(), vg_.data(), nv_.data());
+    if (s == LQRO_OK || s == LQRO_E_HULL || s == LQRO_E_QHMERGE)
+      for (size_t i = 0; i < q_.size(); ++i)
+        for (int c = 0; c < kV; ++c) q_[i].newV[c] = nv_[i * kV + c];
+    check(s, "lqro_step");
   }
+
+  // (i, j) of the last step's pairs lqro_get_hull_failures /
+  // lqro_get_qhmerge_pairs name (at most 64 each)
+  std::vector<std::pair<int, int>> hull_failures() const { return named(lqro_get_hull_failures); }
+  std::vector<std::pair<int, int>> qhmerge_pairs() const { return named(lqro_get_qhmerge_pairs); }
 
   // The agent loop LQRO:1437-1446 on the GPU: vGoal = newV, findU,
   // propagate, kalmanFilter1, the observation draw, kalmanFilter2,
@@ -157,6 +170,14 @@ class Simulator {
   }
 
  private:
+  std::vector<std::pair<int, int>> named(int (*get)(lqro_ctx*, int64_t*, int64_t, int64_t*)) const {
+    int64_t p[128], n = 0;
+    check(get(ctx_, p, 64, &n), "lqro_get_*_pairs");
+    std::vector<std::pair<int, int>> out;
+    for (int64_t k = 0; k < std::min<int64_t>(n, 64); ++k) out.emplace_back((int)p[2 * k], (int)p[2 * k + 1]);
+    return out;
+  }
+
   std::vector<Quadrotor>& q_;
   int device_;
   lqro_model model_;

@@ -281,7 +281,8 @@ struct HullLdsC {
 #define LQRO_HBUILD_CAP 16384
 #define LQRO_ST_FAILS 16
 #define LQRO_ST_FAILMAX 64
-#define LQRO_ST_WORDS (LQRO_ST_FAILS + LQRO_ST_FAILMAX)
+#define LQRO_ST_MWINS (LQRO_ST_FAILS + LQRO_ST_FAILMAX)   // the first LQRO_ST_FAILMAX MWIN slots
+#define LQRO_ST_WORDS (LQRO_ST_MWINS + LQRO_ST_FAILMAX)
 
 // an inside-hull pair left without its half-plane (a hull capacity): counted
 // in stats[4] and named, so the step reports it (LQRO_E_HULL) instead of
@@ -290,6 +291,14 @@ __device__ __forceinline__ void hull_fail_note(unsigned long long* stats, int sl
   atomicAdd(&stats[4], 1ull);
   const unsigned long long k = atomicAdd(&stats[LQRO_ST_NFAIL], 1ull);
   if (k < LQRO_ST_FAILMAX) stats[LQRO_ST_FAILS + k] = (unsigned long long)slot;
+}
+
+// a pair flagged LQRO_REC_QHMERGE_WIN: counted and named, so that lqro_step
+// returns LQRO_E_QHMERGE instead of a silent difference from qconvex's merged
+// facet (LQRO:925-967)
+__device__ __forceinline__ void qhmerge_note(unsigned long long* stats, int slot) {
+  const unsigned long long k = atomicAdd(&stats[LQRO_ST_MWIN], 1ull);
+  if (k < LQRO_ST_FAILMAX) stats[LQRO_ST_MWINS + k] = (unsigned long long)slot;
 }
 
 // lane 0: a Qhull-order build's timing record (lqro_get_hull_builds):

@@ -1076,8 +1076,13 @@ constexpr int kSaveSort = 1024;
 __global__ void __launch_bounds__(256) k_prio_save(const int* hq, const int* hcount, int cap_hq, int* prev,
                                                    int* prevn, int cap, const unsigned char* mark,
                                                    const unsigned long long* hbuild,
-                                                   const unsigned long long* nbuild, int hbuild_cap) {
+                                                   const unsigned long long* nbuild, int hbuild_cap,
+                                                   const int* hot_list, const int* hot1n, unsigned char* clear,
+                                                   long nslots) {
   // (mark: speculative builds on — a queued pair marked 4 was not inside)
+  // (clear: the split hot launch's marks — k_prio_prev's 2s are reset here,
+  // at the end of their step, so that k_prio never takes a stale 2 of a
+  // pair that was inside two steps back but not last step for "listed")
   __shared__ int n;
   __shared__ unsigned long long key[kSaveSort];   // duration << 32 | slot
   __shared__ unsigned long long rec[kSaveSort];   // the builds: duration << 32 | slot
@@ -1115,6 +1120,14 @@ __global__ void __launch_bounds__(256) k_prio_save(const int* hq, const int* hco
       int r = 0;
       for (int p = 0; p < m; ++p) r += key[p] > kq;
       prev[r] = (int)(unsigned)kq;
+    }
+  }
+  if (clear) {
+    __syncthreads();   // (every mark read above before any is reset)
+    const int h = *hot1n;
+    for (int q = threadIdx.x; q < h; q += blockDim.x) {
+      const int slot = hot_list[q];
+      if (slot >= 0 && slot < nslots && clear[slot] == 2) clear[slot] = 0;
     }
   }
   if (threadIdx.x == 0) *prevn = m;

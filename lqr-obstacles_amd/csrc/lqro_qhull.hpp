@@ -1379,7 +1379,7 @@ __device__ inline void qh_select(const HullArgs& A, const QhW& W, const QhS& S, 
       hull_fail_note(A.stats, slot);
     }
     if (ok && merged) atomicAdd(&A.stats[LQRO_ST_MERGED], 1ull);
-    if (mwin) atomicAdd(&A.stats[LQRO_ST_MWIN], 1ull);
+    if (mwin) qhmerge_note(A.stats, slot);
     if (A.recs) {
       lqro_pair_record& rec = A.recs[slot];
       rec.flags |= ok ? LQRO_REC_HULL : LQRO_REC_HULLFAIL;

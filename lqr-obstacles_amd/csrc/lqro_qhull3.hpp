@@ -2771,7 +2771,7 @@ __device__ inline bool q3_select(const HullArgs& A, const Q3W& W, const Q3L& L, 
       hull_fail_note(A.stats, slot);
     }
     if (ok && merged) atomicAdd(&A.stats[LQRO_ST_MERGED], 1ull);
-    if (mwin) atomicAdd(&A.stats[LQRO_ST_MWIN], 1ull);
+    if (mwin) qhmerge_note(A.stats, slot);
     if (A.recs) {
       lqro_pair_record& rec = A.recs[slot];
       rec.flags |= ok ? LQRO_REC_HULL : LQRO_REC_HULLFAIL;

@@ -490,6 +490,9 @@ const char* lqro_status_string(int s) {
     case LQRO_E_NODEVICE: return "no gfx950 device";
     case LQRO_E_OVERFLOW: return "work queue overflow";
     case LQRO_E_HULL: return "an inside-hull pair's hull could not be built (degenerate input or capacity; lqro_get_hull_failures)";
+    case LQRO_E_QHMERGE:
+      return "an inside-hull pair's winning facet may be one qconvex's pre-merge joins: its half-plane is not pinned "
+             "to the reference (LQRO_REC_QHMERGE_WIN; lqro_get_qhmerge_pairs)";
   }
   return "unknown";
 }
@@ -1147,7 +1150,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
     hipLaunchKernelGGL(k_prio_save, dim3(1), dim3(256), 0, s, c->d_hq, c->d_hcount, c->hull_cap, c->d_prevq,
                        c->d_hot2, c->hot_cap, spec ? (const unsigned char*)c->d_hotmark : nullptr,
                        (const unsigned long long*)c->d_hbuild, (const unsigned long long*)(c->d_stats + LQRO_ST_NBUILD),
-                       (int)LQRO_HBUILD_CAP);
+                       (int)LQRO_HBUILD_CAP, c->d_hotlist, c->d_hot2 + 1, split ? c->d_hotmark : nullptr, slots);
     HIPCHK(hipGetLastError());
     if (phase == 0) {
       launch_stale(s, c->d_planes, c->d_qnrm, c->d_qstale, c->d_hcount + 15, c->hull_cap, d_x, g.x_dim, npr, c->rb,
@@ -1276,9 +1279,12 @@ int lqro_step(lqro_ctx* c, const double* x, const double* vgoal, double* newv) {
   if (hc > c->hull_cap) return LQRO_E_OVERFLOW;
   // a pair whose hull the kernels could not build has no half-plane: the
   // step says so (the reference always gets a hull from qconvex, LQRO:879-880)
-  unsigned long long nf = 0;
-  HIPCHK(hipMemcpy(&nf, c->d_stats + 4, sizeof nf, hipMemcpyDeviceToHost));
-  if (nf) return LQRO_E_HULL;
+  unsigned long long st[LQRO_ST_FAILS];
+  HIPCHK(hipMemcpy(st, c->d_stats, sizeof st, hipMemcpyDeviceToHost));
+  if (st[4]) return LQRO_E_HULL;
+  // a pair whose winner qconvex may have merged (Qhull's pre-merge is not
+  // restated): never a silent difference from the reference (LQRO:925-967)
+  if (st[LQRO_ST_MWIN]) return LQRO_E_QHMERGE;
   return LQRO_OK;
 }
 
@@ -1559,14 +1565,15 @@ int lqro_get_hull_builds(lqro_ctx* c, lqro_hull_build* out, int64_t cap, int64_t
 
 int lqro_get_stats(lqro_ctx* c, int64_t* st) { return lqro_get_stats_ex(c, st, 8); }
 
-int lqro_get_hull_failures(lqro_ctx* c, int64_t* pairs, int64_t cap, int64_t* n_out) {
+// the pairs named in the step's counters: count word `wn`, slots from word `w0`
+static int named_pairs(lqro_ctx* c, int wn, int w0, int64_t* pairs, int64_t cap, int64_t* n_out) {
   if (!c || !n_out || (cap > 0 && !pairs)) return LQRO_E_ARG;
   if (c->pending) return LQRO_E_STATE;
   HIPCHK(hipSetDevice(c->cfg.device));
   HIPCHK(wait_last_step(c));
   unsigned long long h[LQRO_ST_WORDS];
   HIPCHK(hipMemcpy(h, c->d_stats, sizeof h, hipMemcpyDeviceToHost));
-  const int64_t n = (int64_t)h[LQRO_ST_NFAIL];
+  const int64_t n = (int64_t)h[wn];
   *n_out = n;
   const int npr = c->nbr_k > 0 ? std::min(c->nbr_k, c->npr) : c->npr;
   std::vector<int> nbr;
@@ -1576,13 +1583,21 @@ int lqro_get_hull_failures(lqro_ctx* c, int64_t* pairs, int64_t cap, int64_t* n_
     HIPCHK(hipMemcpy(nbr.data(), c->d_nbrlist, sizeof(int) * nbr.size(), hipMemcpyDeviceToHost));
   }
   for (int64_t k = 0; k < m; ++k) {
-    const long slot = (long)h[LQRO_ST_FAILS + k];
+    const long slot = (long)h[w0 + k];
     const int lrow = (int)(slot / npr), jj = nbr.empty() ? (int)(slot % npr) : nbr[slot];
     const int i = c->rb + lrow * c->rs;
     pairs[2 * k] = i;
     pairs[2 * k + 1] = jj < i ? jj : jj + 1;
   }
   return LQRO_OK;
+}
+
+int lqro_get_hull_failures(lqro_ctx* c, int64_t* pairs, int64_t cap, int64_t* n_out) {
+  return named_pairs(c, LQRO_ST_NFAIL, LQRO_ST_FAILS, pairs, cap, n_out);
+}
+
+int lqro_get_qhmerge_pairs(lqro_ctx* c, int64_t* pairs, int64_t cap, int64_t* n_out) {
+  return named_pairs(c, LQRO_ST_MWIN, LQRO_ST_MWINS, pairs, cap, n_out);
 }
 
 /* diagnostic (not in lqro.h): inside-hull pairs of the last step decided by
@@ -1693,6 +1708,11 @@ int lqro_debug_hull_points(lqro_ctx* c, const double* pts, int32_t n, const doub
           *n_facets = qh[7];                 // k_qhull's build status
           if (facets && hipMemcpy(facets, d_f, sizeof(int) * 3 * fmax, hipMemcpyDeviceToHost) != hipSuccess)
             rc = LQRO_E_HIP;
+          // lqro_step's rule: a merge-suspect winner is reported (LQRO_E_QHMERGE)
+          unsigned long long mw = 0;
+          if (rc == LQRO_OK && hipMemcpy(&mw, d_st + LQRO_ST_MWIN, sizeof mw, hipMemcpyDeviceToHost) != hipSuccess)
+            rc = LQRO_E_HIP;
+          if (rc == LQRO_OK && mw) rc = LQRO_E_QHMERGE;
         } else if (local) {
           *n_facets = qh[5] > 0 ? -1 : 0;   // handed over: the full hull would decide
         } else {

@@ -26,6 +26,7 @@ LIB_PATH = os.path.join(_HERE, "liblqro.so")
 
 LQRO_OK = 0
 LQRO_E_HULL = -8              # an inside-hull pair's hull could not be built (degenerate input or capacity; no half-plane)
+LQRO_E_QHMERGE = -9           # the step ran, but a pair's winning facet may be one qconvex's pre-merge joins
 LQRO_FLAG_RECORDS = 0x1
 LQRO_FLAG_QHULL_ORDER = 0x2   # the reference's own hull rule over Qhull's build order (k_qhull)
 REC_PLANE, REC_INSIDE, REC_BACKUP, REC_HULL, REC_HULLFAIL, REC_LOCAL = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20
@@ -83,7 +84,7 @@ EXPORTS = (
     "lqro_synthesize_gains_x", "lqro_synthesize_gains_batch_x",
     "lqro_set_carry_normal", "lqro_get_carry_normal",
     "lqro_step_device_begin", "lqro_step_device_end",
-    "lqro_get_stats_ex", "lqro_get_hull_failures", "lqro_get_hull_builds",
+    "lqro_get_stats_ex", "lqro_get_hull_failures", "lqro_get_hull_builds", "lqro_get_qhmerge_pairs",
 )
 
 NORMALS_PER_AGENT = 22   # LQRO_NORMALS_PER_AGENT: 16 propagate + 6 observation
@@ -127,6 +128,7 @@ def lib() -> C.CDLL:
         L.lqro_get_stats.argtypes = [vp, vp]
         L.lqro_get_stats_ex.argtypes = [vp, vp, i32]
         L.lqro_get_hull_failures.argtypes = [vp, vp, i64, C.POINTER(i64)]
+        L.lqro_get_qhmerge_pairs.argtypes = [vp, vp, i64, C.POINTER(i64)]
         L.lqro_get_timings.argtypes = [vp, vp]
         L.lqro_calculate_new_v.argtypes = [vp, vp, i32, vp, dbl, vp, i32]
         L.lqro_dynamics_step.argtypes = [C.POINTER(Model), i32, i32, i32, C.POINTER(Agents), i32]
@@ -149,6 +151,20 @@ class HullFailure(LqroError):
     exceeded) got no half-plane (the reference's qconvex
     always returns a hull, LQRO:879-880).  .pairs: their (i, j); .newv: the
     step's new velocities, computed without those planes."""
+
+    def __init__(self, msg, pairs, newv):
+        super().__init__(msg)
+        self.pairs, self.newv = pairs, newv
+
+
+class QhullMergeSuspect(LqroError):
+    """lqro_step returned LQRO_E_QHMERGE: the step completed, but for some
+    inside-hull pairs the winning facet may be one that qconvex's default
+    pre-merge joins into a merged facet (LQRO_REC_QHMERGE_WIN; convexHull
+    then measures from the merged facet's first Fv vertex with its merged
+    plane, LQRO:925-939, 956-967).  Qhull's merging is not restated, so those
+    pairs' half-planes are not pinned to the reference.  .pairs: their (i, j);
+    .newv: the step's new velocities."""
 
     def __init__(self, msg, pairs, newv):
         super().__init__(msg)
@@ -293,6 +309,10 @@ class Context:
             pairs = self.hull_failures()
             raise HullFailure(f"lqro_step: {len(pairs)} inside-hull pair(s) without a half-plane: "
                               f"{[tuple(p) for p in pairs[:8]]}", pairs, newv)
+        if rc == LQRO_E_QHMERGE:
+            pairs = self.qhmerge_pairs()
+            raise QhullMergeSuspect(f"lqro_step: {len(pairs)} inside-hull pair(s) whose winning facet qconvex may "
+                                    f"merge: {[tuple(p) for p in pairs[:8]]}", pairs, newv)
         _check(rc, "lqro_step")
         return newv
 
@@ -301,6 +321,13 @@ class Context:
         out = np.zeros((64, 2), np.int64)
         n = C.c_int64()
         _check(lib().lqro_get_hull_failures(self._h, _p(out), 64, C.byref(n)), "lqro_get_hull_failures")
+        return out[:min(n.value, 64)]
+
+    def qhmerge_pairs(self) -> np.ndarray:
+        """(i, j) of the last step's LQRO_REC_QHMERGE_WIN pairs (at most 64)."""
+        out = np.zeros((64, 2), np.int64)
+        n = C.c_int64()
+        _check(lib().lqro_get_qhmerge_pairs(self._h, _p(out), 64, C.byref(n)), "lqro_get_qhmerge_pairs")
         return out[:min(n.value, 64)]
 
     def step_device(self, d_x: int, d_vgoal: int, d_newv: int, stream: int = 0):
@@ -363,7 +390,9 @@ class Context:
     def debug_qhull(self, rounded: np.ndarray, full: np.ndarray, vrel, max_facets: int = 0):
         """Test hook: k_qhull on given points (rounded = qconvex's input, full =
         the distances' points): (record, build status bits[, facet list in
-        Qhull's order, Fv triples, when max_facets > 0])."""
+        Qhull's order, Fv triples, when max_facets > 0]).  self.debug_status:
+        the hook's C-ABI status, LQRO_E_QHMERGE for a merge-suspect winner
+        (lqro_step's rule)."""
         n = rounded.shape[0]
         pts = np.ascontiguousarray(np.concatenate([rounded.reshape(-1), full.reshape(-1)]), dtype=np.float64)
         v = np.ascontiguousarray(vrel, dtype=np.float64)
@@ -373,8 +402,11 @@ class Context:
         fn.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32,
                        C.POINTER(C.c_int32), C.POINTER(PairRecord)]
         fl = np.zeros((max(max_facets, 1), 3), np.int32)
-        _check(fn(self._h, _p(pts), n, _p(v), 2, _p(fl) if max_facets else None, max_facets, C.byref(nf),
-                  C.byref(rec)), "lqro_debug_hull_points")
+        rc = fn(self._h, _p(pts), n, _p(v), 2, _p(fl) if max_facets else None, max_facets, C.byref(nf),
+                C.byref(rec))
+        self.debug_status = rc
+        if rc != LQRO_E_QHMERGE:
+            _check(rc, "lqro_debug_hull_points")
         r = np.frombuffer(bytes(rec), dtype=RECORD_DTYPE)[0]
         if max_facets:
             end = np.nonzero(fl[:, 0] < 0)[0]

@@ -110,17 +110,26 @@ def c3_oracle_moved(lqro_mod, oracle, gains, c3_oracle):
     return x1, rv, rr, carry
 
 
-def test_speculative_builds_moving_swarm(lqro_mod, gains, monkeypatch, c3_oracle, c3_oracle_moved):
+@pytest.mark.parametrize("sched", ["default", "no_spec", "spare0", "side_pct50"])
+def test_speculative_builds_moving_swarm(lqro_mod, gains, monkeypatch, c3_oracle, c3_oracle_moved, sched):
     """Speculative builds when the inside-hull set changes between steps: the
     swarm at x0, x0, x1, x0 — the third step's builds were queued for x0's
     inside pairs (those not inside at x1 are dropped, x1's new ones queued by
     their evaluation), the fourth's for x1's.  Each step bit for bit against
-    the oracle at its own state, in the default schedule."""
+    the oracle at its own state, in every schedule that carries state across
+    steps (the last step's inside-hull list d_prevq, the hot marks, k_prio_save's
+    order): the default, the split hot launch without speculative builds
+    (LQRO_HOT_SPEC=0: at the fourth step a pair inside at x0 but not at x1
+    must not keep the third step's "listed" mark), no spare CU and half a side."""
     x0, vg, rv0, rr0, carry0 = c3_oracle
     x1, rv1, rr1, carry1 = c3_oracle_moved
     for k in ("LQRO_EARLY_LP", "LQRO_QSIDE", "LQRO_HOT", "LQRO_LOCAL_HULL", "LQRO_SIDE_HULL_CUS", "LQRO_HOT_SPLIT",
-              "LQRO_HOT_SPEC", "LQRO_QHULL_SPARE"):
+              "LQRO_HOT_SPEC", "LQRO_QHULL_SPARE", "LQRO_QHULL_SIDE_PCT"):
         monkeypatch.delenv(k, raising=False)
+    env = {"default": {}, "no_spec": {"LQRO_HOT_SPEC": "0"}, "spare0": {"LQRO_QHULL_SPARE": "0"},
+           "side_pct50": {"LQRO_QHULL_SIDE_PCT": "50"}}[sched]
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     in0 = (rr0["flags"] & lqro_mod.REC_INSIDE) != 0
     in1 = (rr1["flags"] & lqro_mod.REC_INSIDE) != 0
     assert (in0 & ~in1).sum() > 0 and (in1 & ~in0).sum() > 0, ((in0 & ~in1).sum(), (in1 & ~in0).sum())
@@ -141,9 +150,9 @@ def test_speculative_builds_moving_swarm(lqro_mod, gains, monkeypatch, c3_oracle
                 a, b = r[f], rr[f]
                 if f == "flags":
                     a = a & ~lqro_mod.REC_LOCAL
-                assert np.array_equal(_bits(a), _bits(b)), (t, f)
-            assert np.array_equal(v.view(np.uint64), rv.view(np.uint64)), t
-            assert np.array_equal(ctx.carry_normal(), carry), t
+                assert np.array_equal(_bits(a), _bits(b)), (sched, t, f)
+            assert np.array_equal(v.view(np.uint64), rv.view(np.uint64)), (sched, t)
+            assert np.array_equal(ctx.carry_normal(), carry), (sched, t)
     finally:
         ctx.close()
 
@@ -197,8 +206,10 @@ def test_merged_winners_are_flagged(lqro_mod, oracle, gains):
     """Inputs where qconvex's pre-merge joins the winning facet (coplanar
     cube faces, a flattened cap; tests/golden/make_golden_merge.py over live
     Qhull): k_qhull (built merge-free) flags each LQRO_REC_QHMERGE and
-    LQRO_REC_QHMERGE_WIN, exactly as the oracle does, and its selection
-    equals the oracle's merge-free one bit for bit."""
+    LQRO_REC_QHMERGE_WIN, exactly as the oracle does, its selection equals
+    the oracle's merge-free one bit for bit, and the C-ABI reports the pair
+    loudly (LQRO_E_QHMERGE, lqro_step's rule) — never the silent LQRO_OK; the
+    reference's own fixture (no merge) reports LQRO_OK."""
     d = np.load(f"{GOLDEN}/qhull_merge.npz")
     ctx = lqro_mod.Context(lqro_mod.config(2, 100, 100))
     ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
@@ -207,12 +218,18 @@ def test_merged_winners_are_flagged(lqro_mod, oracle, gains):
         for c in ("cube_top", "cube_side", "capped"):
             assert d[f"{c}_expect"][1] == 1, c           # qconvex's winner is a merged facet
             rec, st = ctx.debug_qhull(d[f"{c}_rounded"], d[f"{c}_pts"], d[f"{c}_vrel"])
+            assert ctx.debug_status == lqro_mod.LQRO_E_QHMERGE, (c, ctx.debug_status)
             nf, dist, nrm, fac, qst = oracle.hull_branch_ref(d[f"{c}_pts"], d[f"{c}_vrel"])
             assert qst & 0x10000, c
             assert rec["flags"] & lqro_mod.REC_QHMERGE and rec["flags"] & lqro_mod.REC_QHMERGE_WIN, (c, rec["flags"])
             assert rec["n_facets"] == nf and list(rec["facet"]) == list(fac) and rec["dist"] == dist, c
             if nrm is not None:
                 assert np.array_equal(rec["normal"], nrm), c
+        from test_oracle_golden import _qhull_fixture
+        pts, _, _ = _qhull_fixture()
+        pts = np.ascontiguousarray(pts, np.float64)
+        rec, st = ctx.debug_qhull(pts, pts, pts.mean(0))
+        assert ctx.debug_status == lqro_mod.LQRO_OK and not rec["flags"] & lqro_mod.REC_QHMERGE_WIN
     finally:
         oracle.set_hull_rule(0)
         ctx.close()

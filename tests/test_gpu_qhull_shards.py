@@ -109,3 +109,69 @@ def test_begin_end_call_order(lqro_mod, gains):
     finally:
         c.close()
         hip.free()
+
+
+def test_c4_eight_shards_match_one_context(lqro_mod, gains, monkeypatch):
+    """C4 (4096 quadrotors, H = 100) as the 8-GPU strong-scaled run splits it:
+    the 8 block shards of 512 rows, each through lqro_step_device_begin, the
+    row-normal table assembled from the 8 (the all-gather), then _end — over
+    three steps (the third in the speculative-build steady state), each shard
+    entered with the normal the step before left.  Every row's newV, every
+    row's last normal in the table and every shard's carried normal equal one
+    whole-swarm context's bit for bit (LQRO:1385: the loop-carried
+    normalVector runs through all 16.8 M pairs across the shards), and the
+    shards' inside-hull counts add up to the whole swarm's."""
+    from test_gpu_dyn import _Hip
+    for k in ("LQRO_EARLY_LP", "LQRO_QSIDE", "LQRO_HOT", "LQRO_HOT_SPLIT", "LQRO_HOT_SPEC", "LQRO_QHULL_SPARE"):
+        monkeypatch.delenv(k, raising=False)
+    N, H, G, steps = 4096, 100, 8, 3
+    x, vg = lqro_mod.synthetic_swarm(N)
+    hip = _Hip()
+    d_x, d_vg = hip.put(x), hip.put(vg)
+    zt, zv = np.zeros((N, 4)), np.zeros((N, 3))
+    whole = lqro_mod.Context(lqro_mod.config(N, H, 100, flags=lqro_mod.LQRO_FLAG_QHULL_ORDER))
+    whole.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
+    ctxs = []
+    for g in range(G):
+        c = lqro_mod.Context(lqro_mod.config(N, H, 100, flags=lqro_mod.LQRO_FLAG_QHULL_ORDER,
+                                             **lqro_mod.shard_rows(N, g, G, "block")))
+        c.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
+        ctxs.append(c)
+    try:
+        for t in range(steps):
+            w_tab, w_nv = hip.put(zt), hip.put(zv)
+            whole.step_device_begin(d_x, d_vg, w_tab, 0)
+            whole.step_device_end(w_tab, w_nv, 0)
+            hip.sync()
+            ref_tab, ref_nv = hip.get(w_tab, zt), hip.get(w_nv, zv)
+            ref_carry, ref_st = whole.carry_normal(), whole.stats()
+            assert ref_st["hull_fail"] == 0 and ref_st["inside"] > 500, ref_st
+            tabs = [hip.put(zt) for _ in range(G)]
+            nvs = [hip.put(zv) for _ in range(G)]
+            for g, c in enumerate(ctxs):
+                c.step_device_begin(d_x, d_vg, tabs[g], 0)
+            hip.sync()
+            tab = np.zeros((N, 4))
+            for g in range(G):   # the all-gather: each rank's own rows
+                ids = lqro_mod.shard_row_ids(N, g, G, "block")
+                tab[ids] = hip.get(tabs[g], zt)[ids]
+            assert np.array_equal(tab.view(np.uint64), ref_tab.view(np.uint64)), t
+            d_tab = hip.put(tab)
+            for g, c in enumerate(ctxs):
+                c.step_device_end(d_tab, nvs[g], 0)
+            hip.sync()
+            inside = 0
+            for g, c in enumerate(ctxs):
+                ids = lqro_mod.shard_row_ids(N, g, G, "block")
+                got = hip.get(nvs[g], zv)[ids]
+                assert np.array_equal(got.view(np.uint64), ref_nv[ids].view(np.uint64)), (t, g)
+                assert np.array_equal(c.carry_normal(), ref_carry), (t, g)
+                st = c.stats()
+                assert st["hull_fail"] == 0 and st["qhull_timeouts"] == 0, (t, g, st)
+                inside += st["inside"]
+            assert inside == ref_st["inside"], (t, inside, ref_st["inside"])
+    finally:
+        whole.close()
+        for c in ctxs:
+            c.close()
+        hip.free()

@@ -38,9 +38,10 @@ def test_lib_is_gfx950_code_object(lqro_mod):
 def test_version_and_status_strings(lqro_mod):
     L = lqro_mod.lib()
     assert L.lqro_version() >= 1
-    for rc in (0, -1, -2, -3, -4, -5, -6, -7, -8):
+    for rc in (0, -1, -2, -3, -4, -5, -6, -7, -8, -9):
         s = L.lqro_status_string(rc)
-        assert s and len(s) >= 2
+        assert s and len(s) >= 2 and s != b"unknown", rc
+    assert b"merge" in L.lqro_status_string(lqro_mod.LQRO_E_QHMERGE)
 
 
 def test_config_default(lqro_mod):
