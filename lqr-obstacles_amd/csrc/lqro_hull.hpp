@@ -277,6 +277,7 @@ struct HullLdsC {
 #define LQRO_ST_TIMEOUT 10
 #define LQRO_ST_NFAIL 11
 #define LQRO_ST_MWIN 12     // pairs flagged LQRO_REC_QHMERGE_WIN (lqro_get_stats_ex [11])
+#define LQRO_QHMERGE_K 1024.0   // the merge-suspect test's reach, x qh DISTround (q3_merge_suspect)
 #define LQRO_ST_NBUILD 13   // Qhull-order build records written (A.hbuild)
 #define LQRO_HBUILD_CAP 16384
 #define LQRO_ST_FAILS 16

@@ -1253,7 +1253,7 @@ __device__ inline double qsel_dist16(const double* q, const double* P, const dou
 // within 1e-6 of the winning distance with another hull vertex within
 // 1e-9 (|coord|max + 1) of its plane; wave-uniform
 __device__ inline bool qh_merge_suspect(const QhW& W, const QhS& S, int lane, const double* vrel, double best) {
-  const double T = -1e-9 * (S.MAXabs_coord + 1.0);
+  const double T = -LQRO_QHMERGE_K * S.DISTround;   // (lqro_qhull3.hpp q3_merge_suspect)
   bool sus = false;
   for (int f0 = 1; f0 < S.nalloc; f0 += 64) {
     const int f = f0 + lane;
@@ -1261,7 +1261,8 @@ __device__ inline bool qh_merge_suspect(const QhW& W, const QhS& S, int lane, co
     if (f < S.nalloc && (W.fflag[f] & QF_LIVE)) {
       const double* q = W.pl + 4 * (size_t)f;
       const double* P = W.Pf + 3 * (size_t)W.vpt[W.fv[3 * f]];
-      con = fabs(q[0] * (vrel[0] - P[0]) + q[1] * (vrel[1] - P[1]) + q[2] * (vrel[2] - P[2])) <= best + 1e-6;
+      con = fabs(q[0] * (vrel[0] - P[0]) + q[1] * (vrel[1] - P[1]) + q[2] * (vrel[2] - P[2])) <= best + 1e-6 ||
+            f == S.facet_list;
     }
     unsigned long long m = __ballot(con);
     while (m) {

@@ -2622,14 +2622,19 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
 }
 
 // LQRO_REC_QHMERGE_WIN (a build where Qhull's merge tests fired): does a
-// facet within 1e-6 of the winning distance have a hull vertex other than its
-// own within 1e-9 (|coord|max + 1) of its plane — a facet qconvex's
-// pre-merge may have joined with a neighbour, so that the reference's winner
-// may be a merged facet?  The same test as the oracle's (lqro_oracle.c
-// orc_hull_branch_ref); wave-uniform.
+// facet that can decide the rule — one within 1e-6 of the winning distance,
+// or facet 0 (the list head: its merge would change which facet keeps the
+// loop-carried normal) — have a hull vertex other than its own within
+// LQRO_QHMERGE_K x qh DISTround of its plane: a facet qconvex's pre-merge
+// (centrum radius, coplanar horizon and qh_checkzero all at 2 DISTround for
+// C-0) may have joined with a neighbour, so that the reference's winner may
+// be a merged facet?  The same test as the oracle's (lqro_oracle.c
+// orc_hull_branch_ref); wave-uniform.  (Round 5 reached 1e-9 (|coord|max +
+// 1), ~1e6 DISTround: C5 flagged 216 of 4,867 sampled inside pairs, none of
+// 48 checked against live Qhull merged at the winner; this reach flags 1.)
 __device__ inline bool q3_merge_suspect(const Q3W& W, const Q3L& L, const Q3S& S, int lane, const double* vrel,
-                                        double best) {
-  const double T = -1e-9 * (S.MAXabs_coord + 1.0);
+                                        double best, int head) {
+  const double T = -LQRO_QHMERGE_K * S.DISTround;
   bool sus = false;
   for (int f0 = 1; f0 < S.nalloc; f0 += 64) {
     const int f = f0 + lane;
@@ -2638,7 +2643,8 @@ __device__ inline bool q3_merge_suspect(const Q3W& W, const Q3L& L, const Q3S& S
     if (f < S.nalloc && (q3_fa(W, L, f) & QF_LIVE)) {
       q3_pl(W, L, f, q);
       const double* P = W.Pf + 3 * (size_t)W.vv[f].id[0];
-      con = fabs(q[0] * (vrel[0] - P[0]) + q[1] * (vrel[1] - P[1]) + q[2] * (vrel[2] - P[2])) <= best + 1e-6;
+      con = fabs(q[0] * (vrel[0] - P[0]) + q[1] * (vrel[1] - P[1]) + q[2] * (vrel[2] - P[2])) <= best + 1e-6 ||
+            f == head;
     }
     unsigned long long m = __ballot(con);
     while (m) {
@@ -2675,7 +2681,7 @@ __device__ inline bool q3_select(const HullArgs& A, const Q3W& W, const Q3L& L, 
   const bool fail = (S.status & (QHS_INPUT | QHS_TOPOLOGY | QHS_CAPACITY)) != 0;
   double ub = INFINITY;
   unsigned minkey = 0xffffffffu;
-  int nfac = 0;
+  int nfac = 0, head = -1;   // (head: the live facet of the smallest key, Qhull's facet 0)
   if (!fail) {
     for (int f0 = 1; f0 < S.nalloc; f0 += 256) {
       // four slots a lane: their first vertices' points in one round trip
@@ -2692,7 +2698,7 @@ __device__ inline bool q3_select(const HullArgs& A, const Q3W& W, const Q3L& L, 
         const int f = fs[u];
         nfac++;
         const unsigned k = q3_key(W, L, f);
-        minkey = k < minkey ? k : minkey;
+        if (k < minkey) { minkey = k; head = f; }
         double q[4];
         q3_pl(W, L, f, q);
         const double* P = W.Pf + 3 * (size_t)v[u];
@@ -2704,8 +2710,9 @@ __device__ inline bool q3_select(const HullArgs& A, const Q3W& W, const Q3L& L, 
   }
   for (int off = 32; off >= 1; off >>= 1) {
     const unsigned om = (unsigned)__shfl_xor((int)minkey, off);
+    const int oh = __shfl_xor(head, off);
     nfac += __shfl_xor(nfac, off);
-    minkey = om < minkey ? om : minkey;
+    if (om < minkey) { minkey = om; head = oh; }
     ub = fmin(ub, __shfl_xor(ub, off));
   }
   // the facets within rounding of the minimum, with the read-back planes
@@ -2740,7 +2747,7 @@ __device__ inline bool q3_select(const HullArgs& A, const Q3W& W, const Q3L& L, 
   const bool ok = !fail && nfac > 0 && bf >= 0;
   const bool stale = ok && bkey == minkey;
   const bool merged = (S.status & (QHS_COPLANAR | QHS_NONCONVEX | QHS_FLIPPED | QHS_NARROW | QHS_SINGULAR)) != 0;
-  const bool mwin = ok && merged && q3_merge_suspect(W, L, S, lane, vrel, best);
+  const bool mwin = ok && merged && q3_merge_suspect(W, L, S, lane, vrel, best, head);
   int bv[3] = {0, 0, 0};
   if (ok)
     for (int t = 0; t < 3; t++) bv[t] = W.vv[bf].id[t];

@@ -1051,6 +1051,8 @@ int orc_hull_branch(int n, const double* pts_full, const double vrel[3], double*
  * <= 0 on failure. */
 static int g_hull_rule = 0, g_round16 = 0;
 #define ORC_QH_MERGE_WIN 0x10000   /* orc_hull_branch_ref's *qstatus: LQRO_REC_QHMERGE_WIN */
+#define ORC_QH_MERGE_WIN_LOOSE 0x20000   /* diagnostics: round 5's looser test (1e-9 (|coord|max + 1)) */
+#define ORC_QH_MERGE_K 1024.0      /* the suspect test's reach, in units of qh DISTround */
 static long long g_hull_ns = 0, g_hull_count = 0;
 
 /* time spent in the hull branch and inside-hull pairs since the last reset */
@@ -1100,27 +1102,40 @@ int orc_hull_branch_ref(int n, const double* pts_full, const double vrel[3], dou
   *stale = best == 0;
   for (int k = 0; k < 3; k++) facet[k] = o.fv[3 * best + k];
   /* LQRO_REC_QHMERGE_WIN (reported as *qstatus bit ORC_QH_MERGE_WIN): Qhull's
-   * merge tests fired in this build and a facet within 1e-6 of the winning
-   * distance has another hull vertex within 1e-9 (|coord|max + 1) of its
-   * plane, so qconvex's pre-merge may have joined the winner into a merged
-   * facet (the GPU's q3_merge_suspect / qh_merge_suspect, same arithmetic) */
+   * merge tests fired in this build, and a facet that can decide the rule —
+   * one within 1e-6 of the winning distance, or facet 0 (the list head, whose
+   * merge would change which facet keeps the loop-carried normal) — has
+   * another hull vertex within ORC_QH_MERGE_K x qh DISTround of its plane:
+   * qconvex's pre-merge (centrum radius 2 DISTround for C-0, coplanar
+   * horizon 2 DISTround, qh_checkzero 2 DISTround) may have joined it with a
+   * neighbour, so the reference's winner may be a merged facet (LQRO:925-967).
+   * The GPU's q3_merge_suspect / qh_merge_suspect, same arithmetic.  Round 5's
+   * reach of 1e-9 (|coord|max + 1), ~1e6 x DISTround, also flagged hulls
+   * whose qconvex merge is far from the winner (C5: 35 of 2048 rows' pairs,
+   * every one checked against live Qhull simplicial at the winner); it is
+   * kept as a diagnostic bit. */
   if (o.status) {
     double maxabs = 0.0;
     for (int i = 0; i < 3 * n; i++) maxabs = fabs(rp[i]) > maxabs ? fabs(rp[i]) : maxabs;
-    const double T = -1e-9 * (maxabs + 1.0);
-    int sus = 0;
-    for (int f = 0; f < nf && !sus; f++) {
+    const double Tl = -1e-9 * (maxabs + 1.0);
+    const double T = -ORC_QH_MERGE_K * o.distround;
+    int sus = 0, lsus = 0;
+    for (int f = 0; f < nf && !(sus && lsus); f++) {
       const double* q = o.plane + 4 * f;
       const double* P = pts_full + 3 * (size_t)o.fv[3 * f];
-      if (!(fabs(q[0] * (vrel[0] - P[0]) + q[1] * (vrel[1] - P[1]) + q[2] * (vrel[2] - P[2])) <= d + 1e-6)) continue;
-      for (int g = 0; g < 3 * nf && !sus; g++) {
+      const int near = fabs(q[0] * (vrel[0] - P[0]) + q[1] * (vrel[1] - P[1]) + q[2] * (vrel[2] - P[2])) <= d + 1e-6;
+      if (!near && f != 0) continue;
+      for (int g = 0; g < 3 * nf; g++) {
         const int id = o.fv[g];
         if (id == o.fv[3 * f] || id == o.fv[3 * f + 1] || id == o.fv[3 * f + 2]) continue;
         const double* p = rp + 3 * (size_t)id;
-        if (q[3] + p[0] * q[0] + p[1] * q[1] + p[2] * q[2] >= T) sus = 1;
+        const double dv = q[3] + p[0] * q[0] + p[1] * q[1] + p[2] * q[2];
+        if (dv >= T) sus = 1;
+        if (near && dv >= Tl) lsus = 1;
       }
     }
     if (sus) *qstatus |= ORC_QH_MERGE_WIN;
+    if (lsus) *qstatus |= ORC_QH_MERGE_WIN_LOOSE;
   }
   orc_qhull_free(&o);
   free(rp);

@@ -896,6 +896,7 @@ int orc_qhull_ex(const double* pts, int n, orc_qhull_out* out, int keep_going) {
   }
 done:
   out->status |= q->status;
+  out->distround = q->DISTround;
   out->st_facets_created = q->nf - 1;
   for (int f = 0; f < q->nf; f++) free(q->F[f].os);
   free(q->F);

@@ -26,6 +26,7 @@ typedef struct {
   /* build statistics (sizing the GPU restatement) */
   int st_addpoints, st_partition, st_horizon_max, st_horizon_sum, st_cop_max, st_old_append;
   int st_visible_max, st_new_max, st_partition_max, st_facets_created;
+  double distround;  /* qh DISTround of the build (qh_detroundoff) */
 } orc_qhull_out;
 
 /* Qhull 2019.1 on n 3-d points (qconvex defaults).  Returns nfacets, or -1

@@ -294,7 +294,8 @@ class _QhullOut(C.Structure):
                 ("plane", C.POINTER(C.c_double)), ("facet_id", C.POINTER(C.c_int)),
                 ("status", C.c_int)] + [(k, C.c_int) for k in (
                     "st_addpoints", "st_partition", "st_horizon_max", "st_horizon_sum", "st_cop_max",
-                    "st_old_append", "st_visible_max", "st_new_max", "st_partition_max", "st_facets_created")]
+                    "st_old_append", "st_visible_max", "st_new_max", "st_partition_max", "st_facets_created")] + [
+                ("distround", C.c_double)]
 
 
 def qhull(points: np.ndarray, keep_going: bool = False):
