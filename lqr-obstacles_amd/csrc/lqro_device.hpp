@@ -19,6 +19,13 @@ constexpr int kWave = 64;
 // queues, -1 for each hot pair done without a hull and each hull job done:
 // it equals row_split * LQRO_ROW_BIG exactly when the row has nothing open.
 #define LQRO_ROW_BIG (1 << 20)
+// The step's work, for the next steps' schedule (the side's width): the
+// sweep's workgroup time summed over k_pair's workgroups (one a CU), the
+// Qhull-order builds' time summed and their maximum, on the 100 MHz clock
+// (s_memrealtime); words of the context's stats array (lqro_hull.hpp)
+#define LQRO_ST_SWORK 144
+#define LQRO_ST_BWORK 145
+#define LQRO_ST_BMAX 146
 
 // Workgroup-scope fence pair: orders this wave's LDS writes before other
 // lanes' later reads (LDS executes a wave's instructions in order; this keeps

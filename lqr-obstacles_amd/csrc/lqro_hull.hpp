@@ -98,6 +98,7 @@ struct HullArgs {
   int* bag;                         // per block of k_hull: HULL_BAGCAP overflow face ids (-1: empty)
   int block_base;                   // scratch index of this launch's block 0
   int big_main;                     // k_hull_big takes the main queue (H*NP too large for LDS)
+  int big_inline;                   // k_qhull rebuilds a build past its caps in place (q3_big_inline)
   int* lqueue;                      // k_lhull: pairs the local hull hands to the full hull
   int* lcount;
   int* ldone;                       // k_lhull: pairs it decided
@@ -283,7 +284,8 @@ struct HullLdsC {
 #define LQRO_ST_FAILS 16
 #define LQRO_ST_FAILMAX 64
 #define LQRO_ST_MWINS (LQRO_ST_FAILS + LQRO_ST_FAILMAX)   // the first LQRO_ST_FAILMAX MWIN slots
-#define LQRO_ST_WORDS (LQRO_ST_MWINS + LQRO_ST_FAILMAX)
+#define LQRO_ST_WORDS (LQRO_ST_MWINS + LQRO_ST_FAILMAX + 4)   // + LQRO_ST_SWORK, _BWORK, _BMAX (lqro_device.hpp)
+static_assert(LQRO_ST_SWORK == LQRO_ST_MWINS + LQRO_ST_FAILMAX, "the work words follow the named pairs");
 
 // an inside-hull pair left without its half-plane (a hull capacity): counted
 // in stats[4] and named, so the step reports it (LQRO_E_HULL) instead of
@@ -309,6 +311,8 @@ __device__ __forceinline__ void hull_build_note(const HullArgs& A, int slot, int
                                                 int n, int nins, int nfac) {
   if (!A.hbuild) return;
   const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  atomicAdd(&A.stats[LQRO_ST_BWORK], t1 - t0);   // (the next steps' side width)
+  atomicMax(&A.stats[LQRO_ST_BMAX], t1 - t0);
   const unsigned long long k = atomicAdd(&A.stats[LQRO_ST_NBUILD], 1ull);
   if (k >= (unsigned long long)A.hbuild_cap) return;
   unsigned long long* r = A.hbuild + 4 * k;

@@ -24,9 +24,17 @@ void launch_lhull(dim3 grid, hipStream_t s, const HullArgs& A) {
   hipLaunchKernelGGL(k_lhull, grid, dim3(LH_THREADS), 0, s, A);
 }
 
+// (the LDS block is k_qhull's or, for a build past its caps rebuilt in place,
+// k_qhull_big's: q3_big_inline)
+union Q3U {
+  Q3L q3;
+  QhL qh;
+};
+static_assert(sizeof(Q3U) == sizeof(Q3L), "k_qhull_big's LDS fits in k_qhull's");
+
 __global__ void __launch_bounds__(192) k_qhull(HullArgs A) {
-  __shared__ Q3L L;
-  q3_body(A, L);
+  __shared__ Q3U U;
+  q3_body(A, U.q3, A.big_inline ? &U.qh : nullptr);
 }
 
 // the pairs k_qhull's caps turned away (the retry queue), or with
@@ -49,7 +57,7 @@ size_t qhull_lds_doubles() { return sizeof(Q3L) / 8; }
 
 size_t qhull_worker_bytes(int hnp) {
   const size_t a = qh_worker_bytes(hnp), b = q3_worker_bytes(hnp);
-  return a > b ? a : b;
+  return (a > b ? a : b) + QW_TAG_BYTES;   // (+ the owner tag, qw_owner)
 }
 
 void launch_stale(hipStream_t s, float* planes, const double* qnrm, const int* list, const int* count, int cap,

@@ -471,6 +471,7 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: SGPR
   const int H = P.H, NP = P.NP, XP = P.XP;
   __shared__ int s_row, s_next;
+  const unsigned long long t_wg = __builtin_amdgcn_s_memrealtime();   // (LQRO_ST_SWORK)
 
   double* sT = lds + P.lds_T;
   double* sN = lds + P.lds_N;
@@ -887,6 +888,7 @@ __device__ __forceinline__ void pair_block(const PairArgs& P, double* lds) {
     const int dst = threadIdx.x == 0 ? 6 : threadIdx.x == 1 ? 7 : threadIdx.x == 2 ? 1 : threadIdx.x == 3 ? 2 : 5;
     if (sum) atomicAdd(&P.stats[dst], sum);
   }
+  if (threadIdx.x == 64) atomicAdd(&P.stats[LQRO_ST_SWORK], __builtin_amdgcn_s_memrealtime() - t_wg);
   if constexpr (HOT != kRowLaunch) {
     // every wave's pairs are done (the barrier above) and their hull jobs
     // published: count the workgroup for the k_qhull workers waiting on it

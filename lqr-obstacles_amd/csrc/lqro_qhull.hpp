@@ -102,6 +102,19 @@ struct QhW {
   int FC, SB, HNP;
 };
 
+// A worker's scratch block is shared by k_qhull (Q3W) and k_qhull_big (QhW)
+// of the same block index, and each keeps state across its jobs there (wave
+// 1's epochs W.mark2 / W.ctr; the per-lane visit stamps W.vstamp / W.vctr).
+// The block's last word names the kernel whose state it holds: a kernel that
+// finds the other's tag resets its own cross-job state before its job (the
+// wave that uses the state does it, so no other wave has to see the stores).
+#define QW_TAG_BYTES 256
+#define QW_OWNER_Q3 0x51335133u
+#define QW_OWNER_QH 0x51485148u
+__device__ __forceinline__ unsigned* qw_owner(char* block, size_t stride) {
+  return reinterpret_cast<unsigned*>(block + stride - 4);
+}
+
 __host__ __device__ inline size_t qh_worker_bytes(int HNP) {
   const size_t FC = 2 * (size_t)HNP + QH_NEWCAP + 16, SB = (size_t)QH_SBMULT * HNP;
   return 8 * (7 * (size_t)HNP + 5 * FC) + 4 * (15 * FC + 4 * (size_t)HNP + 8 + SB) + 256 +
@@ -1403,6 +1416,15 @@ __device__ inline void qh_select(const HullArgs& A, const QhW& W, const QhS& S, 
   hl_sync();
 }
 
+// the wave that builds (lane = its lane): the scratch's visit stamps are
+// this kernel's, or reset (zero stamps and counters = a fresh scratch)
+__device__ inline void qh_claim_scratch(const QhW& W, unsigned* owner, int lane) {
+  if (*owner == QW_OWNER_QH) return;
+  for (int q = lane; q < (QH_NEWCAP - 256) * 64; q += 64) W.vstamp[q] = 0u;
+  W.vctr[lane] = 0u;
+  if (lane == 0) *owner = QW_OWNER_QH;
+}
+
 // one inside-hull pair per wave, persistent over the hull queue (k_qhull_big:
 // the retry queue k_qhull's caps fill, or the main queue under LQRO_QHULL_BIG)
 __device__ inline void qh_body(const HullArgs& A, QhL& L, bool retryq) {
@@ -1422,6 +1444,7 @@ __device__ inline void qh_body(const HullArgs& A, QhL& L, bool retryq) {
     const double* Ni = A.NCF + (A.per_agent ? (size_t)i * A.H * 3 * A.X : 0);
     const double vrel[3] = {xi[3] - xj[3], xi[4] - xj[4], xi[5] - xj[5]};
     const int n = hull_points(A, L, Ti, Ni, xi, xj, vrel, W.Pr, W.Pf);
+    qh_claim_scratch(W, qw_owner(A.qscratch + (size_t)(A.block_base + blockIdx.x) * A.qstride, A.qstride), lane);
     QhS S;
 #ifdef LQRO_QHULL_PROFILE
     for (int k = 0; k < 12; k++) S.tph[k] = 0;

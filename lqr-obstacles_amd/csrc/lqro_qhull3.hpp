@@ -228,6 +228,7 @@ struct Q3L {
   int hq_c, hq_from, hq_np, hq_sharp, hq_init, hq_prestart;
   int hq_findbestnew, hq_notsharp, hq_nnew, hq_nmov, hq_nvis;
   double hq_max_outside;
+  int big_slot;                      // a build past the caps, rebuilt in place by qh_build (q3_body)
 #ifdef LQRO_QHULL_PROFILE
   unsigned long long pub_t, done_t, done_t2;   // the last publication / speculation end, after its store
   unsigned long long pub_r, start_r, done_r;    // the same on the 100 MHz real-time clock (one clock for all waves)
@@ -2826,10 +2827,51 @@ __device__ inline void q3_row_lp(const HullArgs& A, Q3L& L, int slot, int lane) 
   hl_sync();
 }
 
+// A build past k_qhull's caps, rebuilt at once on the same CU by k_qhull_big's
+// code (qh_build: topology in global memory, caps 2,048 visible / 1,024 new
+// facets) in the LDS the k_qhull build used (LB aliases L), instead of
+// waiting in the retry queue for the k_qhull_big launch after the sweep —
+// C5's largest hulls (~19,000 points) hit k_qhull's caps within ~25 ms and
+// then waited ~4.5 s for that launch (profiles/r6c_c5_shard_timeline.txt).
+// Every wave takes part in hull_points (workgroup barriers), wave 0 builds
+// and selects; the record names kernel 1 and starts at the job's start.
+__device__ inline void q3_big_inline(const HullArgs& A, QhL& LB, int slot, unsigned long long tjob, int wave) {
+  const int lane = threadIdx.x & 63;
+  const int HNP = A.H * A.NP;
+  const QhW W = qh_worker(A.qscratch + (size_t)(A.block_base + blockIdx.x) * A.qstride, HNP);
+  const int lrow = slot / A.npr, jj = A.nbr_list ? A.nbr_list[slot] : slot % A.npr;
+  const int i = A.row_begin + lrow * A.row_stride;
+  const int j = jj < i ? jj : jj + 1;
+  const double* xi = A.x + (size_t)i * A.X;
+  const double* xj = A.x + (size_t)j * A.X;
+  const double* Ti = A.T + (A.per_agent ? (size_t)i * A.H * 9 : 0);
+  const double* Ni = A.NCF + (A.per_agent ? (size_t)i * A.H * 3 * A.X : 0);
+  const double vrel[3] = {xi[3] - xj[3], xi[4] - xj[4], xi[5] - xj[5]};
+  const int n = hull_points(A, LB, Ti, Ni, xi, xj, vrel, W.Pr, W.Pf);
+  unsigned* owner = qw_owner(A.qscratch + (size_t)(A.block_base + blockIdx.x) * A.qstride, A.qstride);
+  if (wave == 0) {
+    qh_claim_scratch(W, owner, lane);
+    QhS S;
+#ifdef LQRO_QHULL_PROFILE
+    for (int k = 0; k < 12; k++) S.tph[k] = 0;
+#endif
+    S.status = 0;
+    S.nalloc = 1;
+    S.nins = 0;
+    S.facet_list = S.facet_tail = 0;
+    if (LB.fail || n < 4) S.status = QHS_INPUT;
+    else qh_build(W, S, LB, n, lane);
+    hl_sync();
+    qh_select(A, W, S, lane, xi, vrel, slot);
+    if (lane == 0) hull_build_note(A, slot, 1, tjob, n, S.nins, S.nalloc - 1);
+  }
+}
+
 // one inside-hull pair per wave (one wave per CU), persistent over the hull
-// queue; a build beyond this kernel's caps goes to the retry queue
-// (k_qhull_big)
-__device__ inline void q3_body(const HullArgs& A, Q3L& L) {
+// queue; a build beyond this kernel's caps is rebuilt in place by
+// q3_big_inline when the kernel passes its LDS as LB (k_qhull), else it goes
+// to the retry queue (k_qhull_big after the sweep)
+__device__ inline void q3_body(const HullArgs& A, Q3L& L, QhL* LB = nullptr) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // 0: the build, 1: its speculation
   const int HNP = A.H * A.NP;
@@ -2843,7 +2885,10 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
     const bool spec = A.spec_mark != nullptr && A.spec_mark[slot] >= 2;
     // a fresh handshake and wave 1's epochs for this job (ordered by
     // hull_points' barriers)
-    if (threadIdx.x == 0) { L.ph = 0; L.sp_done = 0; L.sp_gdone = 0; L.hstate = 0; L.sp_hz = 0; L.pf_done = 0; }
+    if (threadIdx.x == 0) {
+      L.ph = 0; L.sp_done = 0; L.sp_gdone = 0; L.hstate = 0; L.sp_hz = 0; L.pf_done = 0;
+      L.big_slot = -1;
+    }
     for (int q = threadIdx.x; q < Q3_FL / 2; q += blockDim.x) reinterpret_cast<unsigned*>(L.mark)[q] = 0u;
     const int lrow = slot / A.npr, jj = A.nbr_list ? A.nbr_list[slot] : slot % A.npr;
     const int i = A.row_begin + lrow * A.row_stride;
@@ -2873,6 +2918,12 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
       }
     } else if (wave == 1) {
       // speculate each published phase until the build ends (ph = -1)
+      // (wave 1's epochs: reset when k_qhull_big's code used the scratch)
+      unsigned* owner = qw_owner(A.qscratch + (size_t)(A.block_base + blockIdx.x) * A.qstride, A.qstride);
+      if (*owner != QW_OWNER_Q3) {
+        for (int q = lane; q < W.FC; q += 64) W.mark2[q] = 0u;
+        if (lane == 0) { W.ctr[0] = 0u; *owner = QW_OWNER_Q3; }
+      }
       unsigned ep2 = W.ctr[0];
       unsigned short ep = 0;
       int last = 0;
@@ -2988,8 +3039,12 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
       if (lane == 0) {
         atomicAdd(&A.stats[LQRO_ST_RETRY], 1ull);
         if (S.status & QHS_TIMEOUT) atomicAdd(&A.stats[LQRO_ST_TIMEOUT], 1ull);
-        const int r = atomicAdd(A.rcount, 1);
-        if (r < A.cap) A.rqueue[r] = slot;
+        if (LB) {
+          L.big_slot = slot;   // rebuilt below, on this CU
+        } else {
+          const int r = atomicAdd(A.rcount, 1);
+          if (r < A.cap) A.rqueue[r] = slot;
+        }
         hull_build_note(A, slot, 2, tjob, n, S.nins, S.nalloc - 1);
 #ifdef LQRO_QHULL_PROFILE
         // the builds handed to k_qhull_big: count, the caps they hit, slots
@@ -3059,6 +3114,15 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L) {
     }
     }   // the build was not handed over
     }   // wave 0
+    if (LB) {
+      __syncthreads();   // waves 1 and 2 are done with the build's LDS; big_slot is set
+      const int bs = L.big_slot;
+      __syncthreads();   // (read by every wave before LB, which aliases L, is written)
+      if (bs >= 0) {
+        q3_big_inline(A, *LB, bs, tjob, wave);
+        __syncthreads();
+      }
+    }
     if (A.rowpend) {
       // this job closed its row: wave 0 runs the row's LP in the facet
       // planes' LDS once waves 1 and 2 (which read them while speculating)

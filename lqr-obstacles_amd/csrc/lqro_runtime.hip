@@ -394,6 +394,8 @@ struct lqro_ctx {
                              // second's next, [4] its finished workgroups
   int hot_split;             // LQRO_HOT_SPLIT (default 1): the split hot launch in Qhull order
   int qside_pct;             // LQRO_QHULL_SIDE_PCT: side CUs per 100 of the last step's inside-hull pairs (default 100)
+  int qhull_inline;          // LQRO_QHULL_INLINE_BIG: k_qhull rebuilds a capped build in place (default 1)
+  int qbalance;              // LQRO_QHULL_BALANCE: the side's width from the measured work (default 1)
   int qspare;                // LQRO_QHULL_SPARE: side CUs beyond the last step's inside-hull count (default 4; -1: count/16 + 4)
   int hot_spec;              // LQRO_HOT_SPEC (default 1): with the split, the last step's inside pairs are built speculatively from the step's start
   unsigned char* d_hotmark;  // per slot: in the hot list
@@ -412,7 +414,8 @@ struct lqro_ctx {
   // by a third (at most half the CUs), beyond 4 per (widened) side CU the
   // side CUs cannot keep up with the hulls and the plain schedule (every CU
   // on the hulls after the sweep) is faster (scripts/crowded.py)
-  unsigned long long* h_inside;   // 2 pinned slots: step t writes slot t & 1
+  unsigned long long* h_inside;   // 2 pinned slots of 4 words: step t writes slot t & 1: inside-hull
+                                  //   pairs, then LQRO_ST_SWORK, _BWORK, _BMAX (100 MHz ticks)
   hipEvent_t iev[2];              // recorded after the copy into slot k
   long long nstep;                // steps enqueued
   long hot_max_inside;       // LQRO_HOT_MAX_INSIDE (-1: 4 x the side CUs)
@@ -575,8 +578,8 @@ static int ctx_alloc(lqro_ctx* c) {
   HIPCHK(hipMalloc(&c->d_lq, sizeof(int) * c->hull_cap));
   HIPCHK(hipMalloc(&c->d_err, sizeof(int)));
   HIPCHK(hipMalloc(&c->d_stats, sizeof(unsigned long long) * LQRO_ST_WORDS));
-  HIPCHK(hipHostMalloc((void**)&c->h_inside, 2 * sizeof(unsigned long long), hipHostMallocDefault));
-  c->h_inside[0] = c->h_inside[1] = ~0ull;
+  HIPCHK(hipHostMalloc((void**)&c->h_inside, 8 * sizeof(unsigned long long), hipHostMallocDefault));
+  for (int k = 0; k < 8; ++k) c->h_inside[k] = k % 4 ? 0ull : ~0ull;
   for (int k = 0; k < 2; ++k) HIPCHK(hipEventCreateWithFlags(&c->iev[k], hipEventDisableTiming));
   HIPCHK(hipMalloc(&c->d_prof, sizeof(unsigned long long) * LQRO_PROF_WORDS));
   HIPCHK(hipMemset(c->d_prof, 0, sizeof(unsigned long long) * LQRO_PROF_WORDS));
@@ -686,6 +689,16 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
     // 227 vs 114 ms per step) it loses; at C3 it ties (22.0 ms either way)
     const char* qs = getenv("LQRO_QSIDE");
     c->qside = qs ? atoi(qs) != 0 : 0;
+    // a build past k_qhull's caps rebuilt at once on its CU (q3_big_inline)
+    // instead of in the k_qhull_big launch after the sweep
+    const char* qi = getenv("LQRO_QHULL_INLINE_BIG");
+    c->qhull_inline = qi ? atoi(qi) != 0 : 1;
+    // the side's width from the measured work of the step two before (the
+    // sweep's CU time, the builds' total and longest): no wider than leaves
+    // the sweep no longer than the builds (LQRO_QHULL_BALANCE=0: one CU per
+    // expected build, round 5's rule)
+    const char* qbal = getenv("LQRO_QHULL_BALANCE");
+    c->qbalance = qbal ? atoi(qbal) != 0 : 1;
   }
   c->rb = g.row_begin;
   c->re = (g.row_end > g.row_begin) ? g.row_end : g.n_agents;
@@ -816,6 +829,7 @@ int lqro_set_gains(lqro_ctx* c, const double* A, const double* B, const double* 
 
 static int enqueue_tail(lqro_ctx* c, const double* d_x, const double* d_vgoal, double* d_newv, hipStream_t s,
                         const double* d_rowtab);
+static int qhull_side_balance(int n, double w_sweep, double w_build, double b_max);
 
 // the LP launch's arguments for this context's rows (every row, the tail's
 // k_lp4 list)
@@ -904,9 +918,13 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   // GPU here), so the schedule does not depend on host/GPU timing.
   const int slot = (int)(c->nstep & 1);
   unsigned long long inside_prev = ~0ull;
+  double w_sweep = 0.0, w_build = 0.0, b_max = 0.0;   // CU-ms, ms (the step two before)
   if (c->nstep >= 2) {
     HIPCHK(hipEventSynchronize(c->iev[slot]));
-    inside_prev = c->h_inside[slot];
+    inside_prev = c->h_inside[4 * slot];
+    w_sweep = 1e-5 * (double)c->h_inside[4 * slot + 1];
+    w_build = 1e-5 * (double)c->h_inside[4 * slot + 2];
+    b_max = 1e-5 * (double)c->h_inside[4 * slot + 3];
   }
   const bool known = inside_prev != ~0ull;
   const bool lhull = c->local_hull || c->qhull_order;   // k_lhull or k_qhull on the side
@@ -915,8 +933,10 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
       !known ? 0ull : c->qspare >= 0 ? (unsigned long long)c->qspare : inside_prev / 16 + 4;
   // the side's builds (workers): the last step's inside-hull count, or a
   // share of it (LQRO_QHULL_SIDE_PCT: the longest builds first, k_prio_save)
-  const unsigned long long qwant =
+  unsigned long long qwant =
       known ? (inside_prev * (unsigned long long)c->qside_pct + 99ull) / 100ull + qspare : 0ull;
+  if (c->qhull_order && c->qbalance && known && w_sweep > 0.0 && b_max > 0.0)
+    qwant = std::min(qwant, (unsigned long long)qhull_side_balance(c->n_cu, w_sweep, w_build, b_max));
   if (c->qhull_order) {
     // Qhull's build is one long dependent chain per pair (one wave per CU):
     // the side takes one CU per expected hull, so every hot hull starts at
@@ -1045,6 +1065,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   Hh.row_target = P.row_split * LQRO_ROW_BIG;
   Hh.lp_vgoal = d_vgoal; Hh.lp_newv = d_lpnv; Hh.lp_vmax = g.vmax_lp;
   Hh.hbuild = c->d_hbuild; Hh.hbuild_cap = LQRO_HBUILD_CAP;
+  Hh.big_inline = c->qhull_inline && !c->qhull_big ? 1 : 0;
   if (g.x_dim != 16 && g.x_dim != 12) return LQRO_E_ARG;
   // the row launch is submitted before the side stream's work: should the two
   // streams land on one hardware queue (a second context in the process), the
@@ -1189,6 +1210,27 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   return enqueue_tail(c, d_x, d_vgoal, d_newv, s, nullptr);
 }
 
+// The side's width in Qhull order from the work measured two steps before:
+// with k side CUs the builds end no sooner than max(b_max, 1.15 w_build / k)
+// (LPT packing of chains, 15 % margin) and the sweep's rows no sooner than
+// w_sweep / (n - k).  The widest k within 2 % of the best such bound: where
+// the builds bound the step (C3: the slowest build) every build keeps a CU
+// of its own as long as the sweep stays shorter; where the sweep does (C5: its
+// 2048-row shard is ~86 CU-s of sweep against ~21 CU-s of builds) the side
+// shrinks to what the builds need (224 -> ~60 CUs: 4.7 s -> ~0.6 s a step).
+static int qhull_side_balance(int n, double w_sweep, double w_build, double b_max) {
+  const int kmax = n - n / 8;
+  double best = 1e300;
+  std::vector<double> t((size_t)kmax + 1, 0.0);
+  for (int k = 1; k <= kmax; ++k) {
+    t[k] = std::max(std::max(b_max, 1.15 * w_build / k), w_sweep / (double)(n - k));
+    best = std::min(best, t[k]);
+  }
+  for (int k = kmax; k >= 1; --k)
+    if (t[k] <= 1.02 * best) return k;
+  return kmax;
+}
+
 static int enqueue_tail(lqro_ctx* c, const double* d_x, const double* d_vgoal, double* d_newv, hipStream_t s,
                         const double* d_rowtab) {
   const lqro_config& g = c->cfg;
@@ -1212,7 +1254,9 @@ static int enqueue_tail(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
                        c->nrows, c->rb, c->rs, (const double*)c->d_newv, d_newv);
     HIPCHK(hipGetLastError());
   }
-  HIPCHK(hipMemcpyAsync(c->h_inside + slot, c->d_stats + 2, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(c->h_inside + 4 * slot, c->d_stats + 2, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(c->h_inside + 4 * slot + 1, c->d_stats + LQRO_ST_SWORK, 3 * sizeof(unsigned long long),
+                        hipMemcpyDeviceToHost, s));
   HIPCHK(hipEventRecord(c->iev[slot], s));
   HIPCHK(hipEventRecord(c->ev[3], s));
   c->stepped = 1;
