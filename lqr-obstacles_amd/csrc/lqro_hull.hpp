@@ -307,20 +307,21 @@ __device__ __forceinline__ void qhmerge_note(unsigned long long* stats, int slot
 // lane 0: a Qhull-order build's timing record (lqro_get_hull_builds):
 // slot | kernel << 40, start, end (s_memrealtime, 100 MHz), points |
 // insertions << 20 | facet slots << 40
-__device__ __forceinline__ void hull_build_note(const HullArgs& A, int slot, int kernel, unsigned long long t0,
+__device__ __forceinline__ int hull_build_note(const HullArgs& A, int slot, int kernel, unsigned long long t0,
                                                 int n, int nins, int nfac) {
-  if (!A.hbuild) return;
+  if (!A.hbuild) return -1;
   const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
   atomicAdd(&A.stats[LQRO_ST_BWORK], t1 - t0);   // (the next steps' side width)
   atomicMax(&A.stats[LQRO_ST_BMAX], t1 - t0);
   const unsigned long long k = atomicAdd(&A.stats[LQRO_ST_NBUILD], 1ull);
-  if (k >= (unsigned long long)A.hbuild_cap) return;
+  if (k >= (unsigned long long)A.hbuild_cap) return -1;
   unsigned long long* r = A.hbuild + 4 * k;
   r[0] = (unsigned long long)(unsigned)slot | ((unsigned long long)kernel << 40);
   r[1] = t0;
   r[2] = t1;
   r[3] = (unsigned long long)(n & 0xFFFFF) | ((unsigned long long)(nins & 0xFFFFF) << 20) |
          ((unsigned long long)(nfac & 0xFFFFF) << 40);
+  return (int)k;
 }
 
 __device__ __forceinline__ void hl_sync() {

@@ -1,0 +1,44 @@
+"""Where the slowest Qhull-order builds spend their partitions: long
+sequences (more than one 64-point chunk) against one-chunk ones, per build,
+from a LQRO_QHULL_LONGPROF library (scripts/build_variant.sh liblqro_qlong.so
+-DLQRO_QHULL_LONGPROF).  usage: LQRO_LIB=liblqro_qlong.so qhull_long.py [steps]"""
+import ctypes as C
+import os
+import sys
+
+sys.path[:0] = [os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "lqr-obstacles_amd")]
+import lqro  # noqa: E402
+import numpy as np  # noqa: E402
+
+if os.environ.get("LQRO_LIB"):
+    lqro.LIB_PATH = os.path.join(os.path.dirname(lqro.LIB_PATH), os.environ["LQRO_LIB"])
+Q3_PROF_W1 = 32 + 2 * 4096 + 48 + 4 * 4096
+Q3_PROF_LONG = Q3_PROF_W1 + 64
+K = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+N, H, NP = 1024, 100, 100
+x, vg = lqro.synthetic_swarm(N)
+g = lqro.synthesize_gains()
+c = lqro.Context(lqro.config(N, H, NP))
+c.set_gains(g["A"], g["B"], g["L"], g["E"])
+for k in range(K):
+    c.step(x, vg)
+b = c.hull_builds()
+w = np.zeros(4 * 1024, np.uint64)
+fn = lqro.lib().lqro_debug_prof_words
+fn.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]
+assert fn(c._h, Q3_PROF_LONG, 4 * 1024, w.ctypes.data_as(C.c_void_p)) == 0
+c.close()
+w = w.reshape(-1, 4)[:len(b)]
+d = (b["t_end"] - b["t_start"]) / 1e5
+ok = b["kernel"] == 0
+tot = d[ok].sum()
+print(f"builds {ok.sum()}: {tot:.1f} ms; long-sequence insertions {w[ok, 0].sum() / ok.sum():.1f} per build, "
+      f"{w[ok, 2].sum() / 1e5 / tot * 100:.1f} % of build time; all partitions {w[ok, 3].sum() / 1e5 / tot * 100:.1f} %")
+print("slowest builds: ms, insertions, long insertions, long points, long ms, all partitions ms, us/ins one-chunk")
+for i in np.argsort(-d)[:8]:
+    if not ok[i]:
+        continue
+    n_l, p_l, t_l, t_a = (int(v) for v in w[i])
+    rest = d[i] - t_l / 1e5
+    print(f"  {d[i]:7.2f} {b['insertions'][i]:5d} {n_l:4d} {p_l:6d} {t_l / 1e5:6.2f} {t_a / 1e5:6.2f} "
+          f"{1e3 * rest / max(1, b['insertions'][i] - n_l):6.2f}")
