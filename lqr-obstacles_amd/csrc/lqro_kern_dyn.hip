@@ -67,15 +67,25 @@ __global__ void __launch_bounds__(64) k_dynw(const lqro_model* models, int n_mod
 }
 
 // LQRO_DYN_PROFILE=1: k_dynw's phases (lqro_dynw.hpp DynProf) into a device
-// buffer read by lqro_debug_dyn_profile (not in lqro.h; scripts/dyn_prof.py)
-static unsigned long long* g_dprof = nullptr;
+// buffer per device (the current one at each launch), read by
+// lqro_debug_dyn_profile for the current device (not in lqro.h;
+// scripts/dyn_prof.py)
+constexpr int kDynProfDevices = 64;
+static unsigned long long* g_dprof[kDynProfDevices] = {nullptr};
+
+static unsigned long long** dyn_prof_slot() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kDynProfDevices) return nullptr;
+  return &g_dprof[dev];
+}
 
 extern "C" int lqro_debug_dyn_profile(unsigned long long* out32, int reset) {
   if (!out32) return -1;
-  if (!g_dprof) { for (int k = 0; k < 32; ++k) out32[k] = 0; return 0; }
+  unsigned long long** slot = dyn_prof_slot();
+  if (!slot || !*slot) { for (int k = 0; k < 32; ++k) out32[k] = 0; return 0; }
   if (hipDeviceSynchronize() != hipSuccess) return -2;
-  if (hipMemcpy(out32, g_dprof, sizeof(unsigned long long) * 32, hipMemcpyDeviceToHost) != hipSuccess) return -2;
-  if (reset && hipMemset(g_dprof, 0, sizeof(unsigned long long) * 32) != hipSuccess) return -2;
+  if (hipMemcpy(out32, *slot, sizeof(unsigned long long) * 32, hipMemcpyDeviceToHost) != hipSuccess) return -2;
+  if (reset && hipMemset(*slot, 0, sizeof(unsigned long long) * 32) != hipSuccess) return -2;
   return 0;
 }
 
@@ -85,10 +95,14 @@ void launch_dyn(bool lane, const lqro_model* models, int n_models, int n, int pe
     hipLaunchKernelGGL(k_dyn, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, models, n_models, n, per_agent, A);
   else {
     static const int prof_on = getenv("LQRO_DYN_PROFILE") ? atoi(getenv("LQRO_DYN_PROFILE")) : 0;
-    if (prof_on && !g_dprof && hipMalloc(&g_dprof, sizeof(unsigned long long) * 32) == hipSuccess)
-      (void)hipMemset(g_dprof, 0, sizeof(unsigned long long) * 32);
-    hipLaunchKernelGGL(k_dynw, dim3((unsigned)n), dim3(64), 0, s, models, n_models, n, per_agent, A,
-                       prof_on ? g_dprof : nullptr);
+    unsigned long long* prof = nullptr;
+    if (prof_on) {   // (the launching device's own buffer)
+      unsigned long long** slot = dyn_prof_slot();
+      if (slot && !*slot && hipMalloc(slot, sizeof(unsigned long long) * 32) == hipSuccess)
+        (void)hipMemset(*slot, 0, sizeof(unsigned long long) * 32);
+      if (slot) prof = *slot;
+    }
+    hipLaunchKernelGGL(k_dynw, dim3((unsigned)n), dim3(64), 0, s, models, n_models, n, per_agent, A, prof);
   }
 }
 
