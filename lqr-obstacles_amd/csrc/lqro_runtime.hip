@@ -968,7 +968,12 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   const bool crowded = known && inside_prev > (unsigned long long)max_inside;
   // with the local hull the side stream is k_pair(hot) -> k_lhull -> k_pair
   // (rows, the same row queue): no LDS-topology condition
+  // (Qhull order: until the work of a step is known — a context's first two
+  // steps — the plain schedule: every CU sweeps, then the builds.  A side
+  // guessed at half the CUs starved the sweep where it outweighs the builds:
+  // C5's whole swarm took 11.7 s per unknown step against 3.4 s plain)
   const bool hot = c->hot_on && c->n_cu >= 64 && slots >= 65536 && c->nbr_k <= 0 && !crowded && side >= 1 &&
+                   (known || !c->qhull_order) &&
                    (lhull || (lds_ok && (size_t)g.horizon * g.n_points <= 16383 && side_waves >= 1));
   const int nwait = hot ? side : 0;
   P.row_split = std::max(1, std::min(16, (2 * c->n_cu + c->nrows - 1) / c->nrows));
