@@ -32,9 +32,14 @@ union Q3U {
 };
 static_assert(sizeof(Q3U) == sizeof(Q3L), "k_qhull_big's LDS fits in k_qhull's");
 
+// BIG: a build past the caps is rebuilt in place (q3_big_inline).  A kernel of
+// its own: the rebuild's code in the same kernel costs the common path its
+// registers (C3 step 19.7 -> 20.1 ms), so it runs only where builds reach the
+// caps (the runtime's choice, HullArgs::big_inline)
+template <bool BIG>
 __global__ void __launch_bounds__(192) k_qhull(HullArgs A) {
   __shared__ Q3U U;
-  q3_body(A, U.q3, A.big_inline ? &U.qh : nullptr);
+  q3_body(A, U.q3, BIG ? &U.qh : nullptr);
 }
 
 // the pairs k_qhull's caps turned away (the retry queue), or with
@@ -46,7 +51,8 @@ __global__ void __launch_bounds__(64) k_qhull_big(HullArgs A) {
 
 void launch_qhull(dim3 grid, hipStream_t s, const HullArgs& A) {
   // wave 0 builds, wave 1 speculates the next insertion, wave 2 prefetches its partition sequence
-  hipLaunchKernelGGL(k_qhull, grid, dim3(192), 0, s, A);
+  if (A.big_inline) hipLaunchKernelGGL(k_qhull<true>, grid, dim3(192), 0, s, A);
+  else hipLaunchKernelGGL(k_qhull<false>, grid, dim3(192), 0, s, A);
 }
 
 void launch_qhull_big(dim3 grid, hipStream_t s, const HullArgs& A) {

@@ -94,7 +94,6 @@ struct Q3W {
   int* pq;                // HNP: qh_partitionall's remainder
   int* pdst;              // HNP: partition sequence -> destination index
   double* pdd;            // HNP: its distance
-  HullPt* ppt;            // HNP: its point (the emit pass reads it back, no second fetch)
   double* ncoord2;        // 9 Q3_NEWCAP: the speculated cone's ridge and opposite points (wave 1)
   unsigned* mark2;        // FC: wave 1's visit epochs of slots >= Q3_FL
   unsigned* ctr;          // wave 1's last epoch (across jobs; zeroed with the scratch)
@@ -112,8 +111,7 @@ __host__ __device__ inline size_t q3_worker_bytes(int HNP) {
   return q3_align(24 * (size_t)HNP) * 2 + q3_align(64 * NG) + q3_align(96 * FC) + q3_align(72 * Q3_NEWCAP) +
          q3_align(4 * FC) +
          q3_align(8 * FC) + q3_align(4 * SB) + q3_align(4 * (size_t)HNP) * 2 + q3_align(8 * (size_t)HNP) +
-         q3_align(4 * QC) * 2 + q3_align(32 * QC) + q3_align(72 * Q3_NEWCAP) + q3_align(4 * FC) + 256 +
-         q3_align(32 * (size_t)HNP);
+         q3_align(4 * QC) * 2 + q3_align(32 * QC) + q3_align(72 * Q3_NEWCAP) + q3_align(4 * FC) + 256;
 }
 
 __device__ inline Q3W q3_worker(char* base, int HNP) {
@@ -142,7 +140,6 @@ __device__ inline Q3W q3_worker(char* base, int HNP) {
   W.ncoord2 = reinterpret_cast<double*>(take(72 * (size_t)Q3_NEWCAP));
   W.mark2 = reinterpret_cast<unsigned*>(take(4 * (size_t)W.FC));
   W.ctr = reinterpret_cast<unsigned*>(take(256));
-  W.ppt = reinterpret_cast<HullPt*>(take(32 * (size_t)HNP));
   return W;
 }
 
@@ -751,33 +748,6 @@ __device__ __forceinline__ bool q3_in_movf(const Q3S& S, const Q3L& L, int f) {
   return false;
 }
 
-// the partition sequence's point id at pos and its start facet (new-facet
-// index), then its coordinates: two dependent loads, which q3_locate_seq
-// issues chunks apart
-__device__ __forceinline__ int q3_seqid(const Q3W& W, const Q3L& L, int nvis, bool init, int pos, int* start) {
-  if (init) {
-    *start = 0;
-    return W.pq[pos];
-  }
-  int a = 0, b = nvis - 1;
-  while (a < b) {
-    const int mid = (a + b) >> 1;
-    if (L.vinc[mid] > pos) b = mid;
-    else a = mid + 1;
-  }
-  *start = L.repl[a] >= 0 ? L.repl[a] : 0;
-  return W.sb[L.vsoff[a] + pos - (L.vinc[a] - L.vscnt[a])];
-}
-// (q < 0: no point; the start facet rides in pad)
-__device__ __forceinline__ HullPt q3_ptof(const Q3W& W, int q, int start) {
-  HullPt r;
-  r.x = r.y = r.z = 0.0;
-  r.q = q;
-  r.pad = start;
-  if (q >= 0) { r.x = W.Pr[3 * (size_t)q]; r.y = W.Pr[3 * (size_t)q + 1]; r.z = W.Pr[3 * (size_t)q + 2]; }
-  return r;
-}
-
 // the partition sequence's point at pos and its start facet (new-facet
 // index): qh_partitionall's remainder (W.pq), or the visible facets' outside
 // sets in visible order (qh_partitionvisible)
@@ -846,8 +816,7 @@ __device__ __forceinline__ void q3_chunk_locate(const Q3W& W, const Q3S& S, cons
   }
 }
 
-// wave 1: serve a chunk request (the state wave 0 had when it asked; the
-// chunk's points and start facets in hr_pt, fetched by wave 0 ahead)
+// wave 1: serve a chunk request (the state wave 0 had when it asked)
 __device__ inline void q3_serve_chunk(const Q3W& W, Q3L& L, int lane) {
   Q3S S;
   S.MINvisible = L.c_dist[0]; S.MAXcoplanar = L.c_dist[1]; S.DISTround = L.c_dist[2];
@@ -855,12 +824,13 @@ __device__ inline void q3_serve_chunk(const Q3W& W, Q3L& L, int lane) {
   S.findbestnew = L.hq_findbestnew; S.notsharp = L.hq_notsharp;
   S.nnew = L.hq_nnew; S.nmov = L.hq_nmov; S.nvis = L.hq_nvis;
   S.max_outside = L.hq_max_outside;
-  HullPt pt;
-  const HullPt pre = L.hr_pt[lane];
+  HullPt pt, pre;
+  pre.x = pre.y = pre.z = 0.0; pre.q = -1; pre.pad = 0;
   int f, isout, trig, ls = 0;
   double d;
-  q3_chunk_locate(W, S, L, L.hq_c, L.hq_from, L.hq_np, L.hq_sharp, L.hq_init != 0, lane, pre, pre.pad, L.hq_c,
+  q3_chunk_locate(W, S, L, L.hq_c, L.hq_from, L.hq_np, L.hq_sharp, L.hq_init != 0, lane, pre, L.hq_prestart, -1,
                   pt, f, d, isout, trig, ls);
+  L.hr_pt[lane] = pt;
   L.hr_d[lane] = d;
   L.hr_f[lane] = f;
   L.hr_k[lane] = isout | (trig << 1);
@@ -891,37 +861,10 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
   // before an event changed the state is never asked for)
   const bool help = np > 128;
   int req = L.hstate >> 2, req_c = -1;   // the last request and its chunk
-  // The sequence's points (they do not change while it is located), fetched
-  // by this wave for every chunk, its own and wave 1's: the ids two chunks
-  // ahead, their coordinates one chunk ahead (two dependent loads a chunk
-  // apart, so neither is waited for).  Chunk ca's points in pa (ready),
-  // ca + 64's in pb (issued one chunk ago), ca + 128's ids in ib / ibs.
-  int ca = 0, ib = -1, ibs = 0;
-  HullPt pa, pb;
-  auto fetch_id = [&](int cc, int& q, int& st) {
-    q = -1;
-    st = 0;
-    if (cc + lane < np) q = q3_seqid(W, L, S.nvis, init, cc + lane, &st);
-  };
-  const bool multi = np > 64;   // (one chunk: no pipeline)
-  auto refill = [&](int cc) {   // (synchronous: the sequence's start, or after an event)
-    ca = cc;
-    int q, st;
-    if (cc == 0 && havepre) {
-      pa = pre;
-      pa.pad = prestart;
-    } else {
-      fetch_id(cc, q, st);
-      pa = q3_ptof(W, q, st);
-    }
-    pb = pa;
-    if (multi) {
-      fetch_id(cc + 64, q, st);
-      pb = q3_ptof(W, q, st);
-      fetch_id(cc + 128, ib, ibs);
-    }
-  };
-  refill(0);
+  // the next chunk this wave locates itself, its points fetched one chunk
+  // ahead (the sequence's points do not change while it is located)
+  HullPt cpre = pre;
+  int cstart = prestart, cprec = havepre ? 0 : -1;
   auto resolve = [&]() -> bool {   // true: wave 1 answered request `req`
     if (req_c < 0) return false;
     req_c = -1;
@@ -937,19 +880,16 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
     if (st != 4 * req + 3) S.status |= QHS_CAPACITY | QHS_TIMEOUT;
     return st == 4 * req + 3;
   };
-  auto post = [&](int c2, int from2, const HullPt& p2) {
+  auto post = [&](int c2, int from2) {
     resolve();
     if (S.status & QHS_CAPACITY) return;
     ++req;
-    L.hr_pt[lane] = p2;   // (the points and start facets; wave 1 is not reading them: no request is out)
     if (lane == 0) {
       L.hq_c = c2; L.hq_from = from2; L.hq_np = np; L.hq_sharp = sharp; L.hq_init = init ? 1 : 0;
       L.hq_prestart = prestart;
       L.hq_findbestnew = S.findbestnew; L.hq_notsharp = S.notsharp; L.hq_nnew = S.nnew; L.hq_nmov = S.nmov;
       L.hq_nvis = S.nvis; L.hq_max_outside = S.max_outside;
-      // (an LDS-only release: everything wave 1 reads for the request is in
-      // LDS, and a full one would wait for this wave's loads in flight)
-      q3_st_rel_lds(&L.hstate, 4 * req + 1);
+      q3_st_rel(&L.hstate, 4 * req + 1);
     }
     req_c = c2;
   };
@@ -963,40 +903,30 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
       const bool act = pos >= from && pos < np;
       int kind = 0, ls = 0, dst = -1, dfa = 0;
       double d = 0.0;
-      if (c != ca) {   // (restarted past the chunk in pa: the next one)
-        if (c == ca + 64) {
-          pa = pb;
-          pb = q3_ptof(W, ib, ibs);
-          fetch_id(c + 128, ib, ibs);
-          ca = c;
-        } else {
-          refill(c);
-        }
-      }
-      // the next chunk's coordinates and the one after's ids, in flight
-      // while this chunk is located
-      HullPt pc = pb;
-      int ic = -1, ics = 0;
-      if (multi) {
-        pc = q3_ptof(W, ib, ibs);
-        fetch_id(c + 192, ic, ics);
-      }
-      HullPt pt = pa;
+      HullPt pt = pre;
       int f = -1, isout = 0, trig = 0;
       bool got = false;
       if (help && req_c == c) {
         got = resolve();
         if (got) {
-          d = L.hr_d[lane]; f = L.hr_f[lane];
+          pt = L.hr_pt[lane]; d = L.hr_d[lane]; f = L.hr_f[lane];
           isout = L.hr_k[lane] & 1; trig = (L.hr_k[lane] >> 1) & 1;
           ls = L.hr_ls;
         }
       } else if (help && c + 64 < np) {
-        post(c + 64, from, pb);   // the next chunk to wave 1, with its points
+        post(c + 64, from);   // the next chunk to wave 1
       }
       Q3T(12);
-      if (!got) q3_chunk_locate(W, S, L, c, from, np, sharp, init, lane, pa, pa.pad, c, pt, f, d, isout, trig, ls);
-      // (the pipeline moves on to c + 64; an event below restarts at c or c + 64)
+      if (!got) {
+        const int nc = c + (help ? 128 : 64);
+        HullPt npt = pre;
+        int nst = 0;
+        if (nc + lane < np) npt = q3_seqpt(W, L, S.nvis, init, nc + lane, &nst);
+        q3_chunk_locate(W, S, L, c, from, np, sharp, init, lane, cpre, cstart, cprec, pt, f, d, isout, trig, ls);
+        cpre = npt;
+        cstart = nst;
+        cprec = nc;
+      }
       Q3T(13);
       if (act) {
         if (isout) {
@@ -1039,21 +969,13 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
         rg = g;
         rd = d;
         rpt = pt;
-        if (np > 64) {   // (for the emit pass)
+        if (np > 64) {   // (the point itself is read again from the sequence)
           W.pdst[pos] = g;
           W.pdd[pos] = d;
-          W.ppt[pos] = pt;
         }
       }
       hl_sync();
       Q3T(14);
-      if (!b) {   // the pipeline's next chunk
-        pa = pb;
-        pb = pc;
-        ib = ic;
-        ibs = ics;
-        ca = c + 64;
-      }
       if (b) {
         ev_pos = c + last;
         ev_kind = __builtin_amdgcn_readlane(kind, last);
@@ -1248,7 +1170,8 @@ __device__ inline void q3_emit_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int ndn
     if (pos < np) {
       ng = W.pdst[pos];
       ndd = W.pdd[pos];
-      npt = W.ppt[pos];
+      int st;
+      npt = q3_seqpt(W, L, S.nvis, init, pos, &st);
     }
   };
   if (np > 64) ldc(0);
@@ -2929,7 +2852,12 @@ __device__ inline void q3_row_lp(const HullArgs& A, Q3L& L, int slot, int lane) 
 // then waited ~4.5 s for that launch (profiles/r6c_c5_shard_timeline.txt).
 // Every wave takes part in hull_points (workgroup barriers), wave 0 builds
 // and selects; the record names kernel 1 and starts at the job's start.
+#ifdef LQRO_QBIG_NOINLINE
+__device__ __attribute__((noinline)) void q3_big_inline(const HullArgs& A, QhL& LB, int slot, unsigned long long tjob,
+                                                        int wave) {
+#else
 __device__ inline void q3_big_inline(const HullArgs& A, QhL& LB, int slot, unsigned long long tjob, int wave) {
+#endif
   const int lane = threadIdx.x & 63;
   const int HNP = A.H * A.NP;
   const QhW W = qh_worker(A.qscratch + (size_t)(A.block_base + blockIdx.x) * A.qstride, HNP);
@@ -2965,7 +2893,7 @@ __device__ inline void q3_big_inline(const HullArgs& A, QhL& LB, int slot, unsig
 // queue; a build beyond this kernel's caps is rebuilt in place by
 // q3_big_inline when the kernel passes its LDS as LB (k_qhull), else it goes
 // to the retry queue (k_qhull_big after the sweep)
-__device__ inline void q3_body(const HullArgs& A, Q3L& L, QhL* LB = nullptr) {
+__device__ __forceinline__ void q3_body(const HullArgs& A, Q3L& L, QhL* LB = nullptr) {   // (inlined into each kernel)
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // 0: the build, 1: its speculation
   const int HNP = A.H * A.NP;
@@ -3219,6 +3147,7 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L, QhL* LB = nullptr) {
     }
     }   // the build was not handed over
     }   // wave 0
+#ifndef LQRO_QHULL_NO_INLINE_BIG
     if (LB) {
       __syncthreads();   // waves 1 and 2 are done with the build's LDS; big_slot is set
       const int bs = L.big_slot;
@@ -3228,6 +3157,7 @@ __device__ inline void q3_body(const HullArgs& A, Q3L& L, QhL* LB = nullptr) {
         __syncthreads();
       }
     }
+#endif
     if (A.rowpend) {
       // this job closed its row: wave 0 runs the row's LP in the facet
       // planes' LDS once waves 1 and 2 (which read them while speculating)

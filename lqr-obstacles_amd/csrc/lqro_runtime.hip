@@ -414,8 +414,9 @@ struct lqro_ctx {
   // by a third (at most half the CUs), beyond 4 per (widened) side CU the
   // side CUs cannot keep up with the hulls and the plain schedule (every CU
   // on the hulls after the sweep) is faster (scripts/crowded.py)
-  unsigned long long* h_inside;   // 2 pinned slots of 4 words: step t writes slot t & 1: inside-hull
-                                  //   pairs, then LQRO_ST_SWORK, _BWORK, _BMAX (100 MHz ticks)
+  unsigned long long* h_inside;   // 2 pinned slots of 8 words: step t writes slot t & 1: inside-hull
+                                  //   pairs, then LQRO_ST_SWORK, _BWORK, _BMAX (100 MHz ticks),
+                                  //   then LQRO_ST_RETRY (builds past k_qhull's caps)
   hipEvent_t iev[2];              // recorded after the copy into slot k
   long long nstep;                // steps enqueued
   long hot_max_inside;       // LQRO_HOT_MAX_INSIDE (-1: 4 x the side CUs)
@@ -578,8 +579,8 @@ static int ctx_alloc(lqro_ctx* c) {
   HIPCHK(hipMalloc(&c->d_lq, sizeof(int) * c->hull_cap));
   HIPCHK(hipMalloc(&c->d_err, sizeof(int)));
   HIPCHK(hipMalloc(&c->d_stats, sizeof(unsigned long long) * LQRO_ST_WORDS));
-  HIPCHK(hipHostMalloc((void**)&c->h_inside, 8 * sizeof(unsigned long long), hipHostMallocDefault));
-  for (int k = 0; k < 8; ++k) c->h_inside[k] = k % 4 ? 0ull : ~0ull;
+  HIPCHK(hipHostMalloc((void**)&c->h_inside, 16 * sizeof(unsigned long long), hipHostMallocDefault));
+  for (int k = 0; k < 16; ++k) c->h_inside[k] = k % 8 ? 0ull : ~0ull;
   for (int k = 0; k < 2; ++k) HIPCHK(hipEventCreateWithFlags(&c->iev[k], hipEventDisableTiming));
   HIPCHK(hipMalloc(&c->d_prof, sizeof(unsigned long long) * LQRO_PROF_WORDS));
   HIPCHK(hipMemset(c->d_prof, 0, sizeof(unsigned long long) * LQRO_PROF_WORDS));
@@ -919,12 +920,14 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   const int slot = (int)(c->nstep & 1);
   unsigned long long inside_prev = ~0ull;
   double w_sweep = 0.0, w_build = 0.0, b_max = 0.0;   // CU-ms, ms (the step two before)
+  unsigned long long retried_prev = 0;
   if (c->nstep >= 2) {
     HIPCHK(hipEventSynchronize(c->iev[slot]));
-    inside_prev = c->h_inside[4 * slot];
-    w_sweep = 1e-5 * (double)c->h_inside[4 * slot + 1];
-    w_build = 1e-5 * (double)c->h_inside[4 * slot + 2];
-    b_max = 1e-5 * (double)c->h_inside[4 * slot + 3];
+    inside_prev = c->h_inside[8 * slot];
+    w_sweep = 1e-5 * (double)c->h_inside[8 * slot + 1];
+    w_build = 1e-5 * (double)c->h_inside[8 * slot + 2];
+    b_max = 1e-5 * (double)c->h_inside[8 * slot + 3];
+    retried_prev = c->h_inside[8 * slot + 4];
   }
   const bool known = inside_prev != ~0ull;
   const bool lhull = c->local_hull || c->qhull_order;   // k_lhull or k_qhull on the side
@@ -1070,7 +1073,10 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   Hh.row_target = P.row_split * LQRO_ROW_BIG;
   Hh.lp_vgoal = d_vgoal; Hh.lp_newv = d_lpnv; Hh.lp_vmax = g.vmax_lp;
   Hh.hbuild = c->d_hbuild; Hh.hbuild_cap = LQRO_HBUILD_CAP;
-  Hh.big_inline = c->qhull_inline && !c->qhull_big ? 1 : 0;
+  // (k_qhull's in-place rebuild of capped builds where they happen: hulls of
+  // more than 10,000 points (C5's ~19,000), or builds capped two steps before)
+  Hh.big_inline =
+      c->qhull_inline && !c->qhull_big && ((size_t)g.horizon * g.n_points > 10000 || retried_prev > 0) ? 1 : 0;
   if (g.x_dim != 16 && g.x_dim != 12) return LQRO_E_ARG;
   // the row launch is submitted before the side stream's work: should the two
   // streams land on one hardware queue (a second context in the process), the
@@ -1259,8 +1265,10 @@ static int enqueue_tail(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
                        c->nrows, c->rb, c->rs, (const double*)c->d_newv, d_newv);
     HIPCHK(hipGetLastError());
   }
-  HIPCHK(hipMemcpyAsync(c->h_inside + 4 * slot, c->d_stats + 2, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(c->h_inside + 4 * slot + 1, c->d_stats + LQRO_ST_SWORK, 3 * sizeof(unsigned long long),
+  HIPCHK(hipMemcpyAsync(c->h_inside + 8 * slot, c->d_stats + 2, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(c->h_inside + 8 * slot + 1, c->d_stats + LQRO_ST_SWORK, 3 * sizeof(unsigned long long),
+                        hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(c->h_inside + 8 * slot + 4, c->d_stats + LQRO_ST_RETRY, sizeof(unsigned long long),
                         hipMemcpyDeviceToHost, s));
   HIPCHK(hipEventRecord(c->iev[slot], s));
   HIPCHK(hipEventRecord(c->ev[3], s));

@@ -128,7 +128,8 @@ def lib() -> C.CDLL:
         L.lqro_get_stats.argtypes = [vp, vp]
         L.lqro_get_stats_ex.argtypes = [vp, vp, i32]
         L.lqro_get_hull_failures.argtypes = [vp, vp, i64, C.POINTER(i64)]
-        L.lqro_get_qhmerge_pairs.argtypes = [vp, vp, i64, C.POINTER(i64)]
+        if hasattr(L, "lqro_get_qhmerge_pairs"):   # (older libraries in A/B runs lack it)
+            L.lqro_get_qhmerge_pairs.argtypes = [vp, vp, i64, C.POINTER(i64)]
         L.lqro_get_timings.argtypes = [vp, vp]
         L.lqro_calculate_new_v.argtypes = [vp, vp, i32, vp, dbl, vp, i32]
         L.lqro_dynamics_step.argtypes = [C.POINTER(Model), i32, i32, i32, C.POINTER(Agents), i32]
