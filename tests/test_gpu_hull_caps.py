@@ -6,7 +6,10 @@ with k_qhull's and k_qhull_big's per-insertion caps cut to 4 visible / 8 new
 facets: on a dense swarm in the default rule (Qhull order) most hulls exceed
 them.  lqro_step must then return LQRO_E_HULL (lqro.HullFailure), name the
 pairs (lqro_get_hull_failures), count them (stats hull_fail) and mark their
-records; every other pair's record must equal the full library's."""
+records; every other pair's record must equal the full library's.  One step:
+the capped builds go to k_qhull_big through the retry queue; the third step
+(builds were capped two steps before): k_qhull<true> rebuilds them in place
+(q3_big_inline) — the same failures, the same records."""
 import json
 import os
 import subprocess
@@ -33,12 +36,13 @@ x, vg = lqro.synthetic_swarm(a["n"], box=a["box"], seed=a["seed"])
 g = lqro.synthesize_gains()
 c = lqro.Context(lqro.config(a["n"], a["H"], 100, flags=lqro.LQRO_FLAG_RECORDS | lqro.LQRO_FLAG_QHULL_ORDER))
 c.set_gains(g["A"], g["B"], g["L"], g["E"])
-out = {"raised": False, "pairs": []}
-try:
-    c.step(x, vg)
-except lqro.HullFailure as e:
-    out["raised"] = True
-    out["pairs"] = [[int(i), int(j)] for i, j in e.pairs]
+for t in range(a["steps"]):
+    out = {"raised": False, "pairs": []}
+    try:
+        c.step(x, vg)
+    except lqro.HullFailure as e:
+        out["raised"] = True
+        out["pairs"] = [[int(i), int(j)] for i, j in e.pairs]
 r = c.records()
 st = c.stats()
 out["hull_fail"] = st["hull_fail"]
@@ -48,12 +52,13 @@ print(json.dumps(out))
 """
 
 
-def test_capacity_failures_are_reported(lqro_mod, tmp_path):
+@pytest.mark.parametrize("steps", [1, 3])
+def test_capacity_failures_are_reported(lqro_mod, tmp_path, steps):
     lib = os.path.join(PKG, "liblqro_tinycap.so")
     assert os.path.exists(lib), "liblqro_tinycap.so not built (__graft_entry__.build)"
     rp = str(tmp_path / "recs.npy")
-    res = subprocess.run([sys.executable, "-c", CHILD, PKG, lib, json.dumps(SWARM), rp], capture_output=True,
-                         text=True, timeout=300)
+    res = subprocess.run([sys.executable, "-c", CHILD, PKG, lib, json.dumps(dict(SWARM, steps=steps)), rp],
+                         capture_output=True, text=True, timeout=300)
     assert res.returncode == 0, res.stderr[-3000:]
     out = json.loads(res.stdout.strip().splitlines()[-1])
     small = np.load(rp)

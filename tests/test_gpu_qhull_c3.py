@@ -14,7 +14,9 @@ was pinned:
   those pairs evaluated alone on the side stream first), LQRO_EARLY_LP=0,
   LQRO_HOT_SPLIT=0, LQRO_QSIDE=1 (side workers sweep rows after their
   builds), LQRO_QHULL_SPARE=0 (one side CU per last-step inside pair: a pair
-  new this step waits for the first build to end) and LQRO_HOT=0 (plain);
+  new this step waits for the first build to end), LQRO_HOT=0 (plain),
+  LQRO_QHULL_BALANCE=0 (round 5's side width, one CU per expected build) and
+  LQRO_QHULL_INLINE_BIG=0 (capped builds to k_qhull_big after the sweep);
 - C5 (16384 agents, X = 12, H = 200, per-agent gains): the 8-way shard
   [0, 2048) in Qhull order on the GPU, 32 rows' newV against the oracle, each
   entered with the loop-carried normal the shard's rows before it left (the
@@ -53,14 +55,16 @@ def c3_oracle(lqro_mod, oracle, gains):
     return x, vg, rv, rr, carry
 
 
-@pytest.mark.parametrize("sched", ["default", "no_spec", "spare0", "early_lp_off", "no_split", "qside", "plain"])
+@pytest.mark.parametrize("sched", ["default", "no_spec", "spare0", "early_lp_off", "no_split", "qside", "plain",
+                                   "balance_off", "inline_big"])
 def test_qhull_order_c3_full_step(lqro_mod, gains, monkeypatch, c3_oracle, sched):
     x, vg, rv, rr, carry = c3_oracle
     env = {"default": {}, "no_spec": {"LQRO_HOT_SPEC": "0"}, "spare0": {"LQRO_QHULL_SPARE": "0"},
            "early_lp_off": {"LQRO_EARLY_LP": "0"},
-           "no_split": {"LQRO_HOT_SPLIT": "0"}, "qside": {"LQRO_QSIDE": "1"}, "plain": {"LQRO_HOT": "0"}}[sched]
+           "no_split": {"LQRO_HOT_SPLIT": "0"}, "qside": {"LQRO_QSIDE": "1"}, "plain": {"LQRO_HOT": "0"},
+           "balance_off": {"LQRO_QHULL_BALANCE": "0"}, "inline_big": {"LQRO_QHULL_INLINE_BIG": "0"}}[sched]
     for k in ("LQRO_EARLY_LP", "LQRO_QSIDE", "LQRO_HOT", "LQRO_LOCAL_HULL", "LQRO_SIDE_HULL_CUS", "LQRO_HOT_SPLIT",
-              "LQRO_HOT_SPEC", "LQRO_QHULL_SPARE"):
+              "LQRO_HOT_SPEC", "LQRO_QHULL_SPARE", "LQRO_QHULL_BALANCE", "LQRO_QHULL_INLINE_BIG"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
