@@ -37,7 +37,7 @@ static_assert(sizeof(Q3U) == sizeof(Q3L), "k_qhull_big's LDS fits in k_qhull's")
 // registers (C3 step 19.7 -> 20.1 ms), so it runs only where builds reach the
 // caps (the runtime's choice, HullArgs::big_inline)
 template <bool BIG>
-__global__ void __launch_bounds__(192) k_qhull(HullArgs A) {
+__global__ void __launch_bounds__(64 * Q3_WAVES) k_qhull(HullArgs A) {
   __shared__ Q3U U;
   q3_body(A, U.q3, BIG ? &U.qh : nullptr);
 }
@@ -50,9 +50,10 @@ __global__ void __launch_bounds__(64) k_qhull_big(HullArgs A) {
 }
 
 void launch_qhull(dim3 grid, hipStream_t s, const HullArgs& A) {
-  // wave 0 builds, wave 1 speculates the next insertion, wave 2 prefetches its partition sequence
-  if (A.big_inline) hipLaunchKernelGGL(k_qhull<true>, grid, dim3(192), 0, s, A);
-  else hipLaunchKernelGGL(k_qhull<false>, grid, dim3(192), 0, s, A);
+  // wave 0 builds, wave 1 speculates the next insertion, wave 2 prefetches its
+  // partition sequence, waves 1-3 locate a long sequence's chunks
+  if (A.big_inline) hipLaunchKernelGGL(k_qhull<true>, grid, dim3(64 * Q3_WAVES), 0, s, A);
+  else hipLaunchKernelGGL(k_qhull<false>, grid, dim3(64 * Q3_WAVES), 0, s, A);
 }
 
 void launch_qhull_big(dim3 grid, hipStream_t s, const HullArgs& A) {

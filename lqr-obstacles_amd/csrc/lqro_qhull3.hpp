@@ -46,6 +46,8 @@ namespace lqro {
 #define Q3_COPCAP 8       // its coplanar facet set
 #define Q3_FSTK 512       // free facet slots kept for reuse (more are left unused)
 #define Q3_ND (Q3_NEWCAP + Q3_MOVCAP)
+#define Q3_WAVES 4        // wave 0 builds, 1 speculates, 2 prefetches; 1-3 locate a long sequence's chunks
+#define Q3_HR 4           // chunk results held for wave 0 (chunk k in buffer k % Q3_HR)
 // poll intervals (s_sleep units of 64 clocks): wave 0 waiting on wave 1, and
 // the idle loops of waves 1 and 2
 #ifndef Q3_W0_SLEEP
@@ -97,6 +99,8 @@ struct Q3W {
   double* ncoord2;        // 9 Q3_NEWCAP: the speculated cone's ridge and opposite points (wave 1)
   unsigned* mark2;        // FC: wave 1's visit epochs of slots >= Q3_FL
   unsigned* ctr;          // wave 1's last epoch (across jobs; zeroed with the scratch)
+  unsigned short* hvis;   // (Q3_WAVES - 1) x Q3_HZCAP x 64: the helper waves' visited-facet columns (Q3Col)
+  int* hcop;              // (Q3_WAVES - 1) x Q3_COPCAP x 64: their coplanar-set columns
   int* fq;                // QC: facets that received points, key order
   unsigned* fqk;          // QC: their key then
   HullPt* fqc;            // QC: their furthest point then (q = -1: not recorded)
@@ -111,7 +115,8 @@ __host__ __device__ inline size_t q3_worker_bytes(int HNP) {
   return q3_align(24 * (size_t)HNP) * 2 + q3_align(64 * NG) + q3_align(96 * FC) + q3_align(72 * Q3_NEWCAP) +
          q3_align(4 * FC) +
          q3_align(8 * FC) + q3_align(4 * SB) + q3_align(4 * (size_t)HNP) * 2 + q3_align(8 * (size_t)HNP) +
-         q3_align(4 * QC) * 2 + q3_align(32 * QC) + q3_align(72 * Q3_NEWCAP) + q3_align(4 * FC) + 256;
+         q3_align(4 * QC) * 2 + q3_align(32 * QC) + q3_align(72 * Q3_NEWCAP) + q3_align(4 * FC) + 256 +
+         q3_align(2 * (Q3_WAVES - 1) * Q3_HZCAP * 64) + q3_align(4 * (Q3_WAVES - 1) * Q3_COPCAP * 64);
 }
 
 __device__ inline Q3W q3_worker(char* base, int HNP) {
@@ -140,6 +145,8 @@ __device__ inline Q3W q3_worker(char* base, int HNP) {
   W.ncoord2 = reinterpret_cast<double*>(take(72 * (size_t)Q3_NEWCAP));
   W.mark2 = reinterpret_cast<unsigned*>(take(4 * (size_t)W.FC));
   W.ctr = reinterpret_cast<unsigned*>(take(256));
+  W.hvis = reinterpret_cast<unsigned short*>(take(2 * (Q3_WAVES - 1) * Q3_HZCAP * 64));
+  W.hcop = reinterpret_cast<int*>(take(4 * (Q3_WAVES - 1) * Q3_COPCAP * 64));
   return W;
 }
 
@@ -218,16 +225,24 @@ struct Q3L {
   unsigned sp_key;
   int pub_qhead, pub_qtail;
   int pub_adopt, pub_nnew;           // the published cone was wave 1's: it writes the vertex records
-  // wave 1 locating a long partition sequence's odd chunks (request hq_*,
-  // results hr_*, sequence numbers hreq / hres, hbusy: the request it took)
-  HullPt hr_pt[64];
-  double hr_d[64];
-  int hr_f[64], hr_k[64];
-  int hr_ls;
-  int hstate;                        // request r: 4 r + 1 posted, + 2 taken, + 3 done; 4 r cancelled
-  int hq_c, hq_from, hq_np, hq_sharp, hq_init, hq_prestart;
+  // Waves 1-3 locate a partition sequence's chunks beside wave 0 (q3_help):
+  // the sequence and wave 0's state (hq_*) posted with hctl = generation << 16
+  // | the next chunk to claim (0: none); a wave claims a chunk with a CAS on
+  // hctl, holding hbusy meanwhile, once its buffer is free (chunk < hcons +
+  // Q3_HR), and releases its results with hr_st = chunk + 1.  Wave 0 stops
+  // the claims (hctl = 0) and waits for hbusy = 0 before its state changes.
+  double hr_d[Q3_HR * 64];
+  unsigned short hr_f[Q3_HR * 64];   // the destination facet (0xffff: none)
+  unsigned short hr_k[Q3_HR * 64];   // the event kind | an old destination << 3 | (new-facet index + 1) << 8
+  int hr_ls[Q3_HR], hr_st[Q3_HR];
+  unsigned hctl;
+  int hbusy, hcons;
+  int hq_end, hq_from, hq_np, hq_sharp, hq_init;
   int hq_findbestnew, hq_notsharp, hq_nnew, hq_nmov, hq_nvis;
   double hq_max_outside;
+#ifdef LQRO_QHULL_LONGPROF
+  unsigned long long hprof[4];       // helper chunks, their ticks locating, claim to release
+#endif
   int big_slot;                      // a build past the caps, rebuilt in place by qh_build (q3_body)
 #ifdef LQRO_QHULL_PROFILE
   unsigned long long pub_t, done_t, done_t2;   // the last publication / speculation end, after its store
@@ -243,6 +258,7 @@ struct Q3S {
   unsigned key0_last;   // the first key of the last insertion's new facets
   int nnew, nvis, nmov, nold;
   int findbestnew, notsharp;
+  int hgen;               // q3_locate_seq's posts to the helper waves (hctl's generation)
   double MAXabs_coord, MAXsumcoord, MAXwidth, NEARzero[3];
   double DISTround, MINvisible, MAXcoplanar, MINoutside, MINdenom, MINdenom_2, max_outside;
   double interior[3];
@@ -258,7 +274,8 @@ struct Q3S {
   unsigned long long tseen, tpre, npre, tstart;
   int prev1;
   unsigned long long tps[24], nps;   // LQRO_QHULL_PROFILE: phases of the one-chunk insertions
-  unsigned long long lp_n, lp_pts, lp_t, lp_all;   // LQRO_QHULL_LONGPROF
+  unsigned long long lp_n, lp_pts, lp_t, lp_all, lp_tloc, lp_wait, lp_adopt, lp_tail, lp_tw;   // LQRO_QHULL_LONGPROF
+  unsigned long long lp_own, lp_got, lp_hwait, lp_stop, lp_ev, lp_posts;
 };
 
 #if defined(LQRO_QHULL_PROFILE) && defined(LQRO_QHULL_PROF_LIGHT)
@@ -283,9 +300,13 @@ struct Q3S {
 #define Q3_PROF_W1 (32 + 2 * 4096 + 48 + 4 * 4096)
 // LQRO_QHULL_LONGPROF (a diagnostic build, scripts/build_variant.sh): per
 // build record k (lqro_get_hull_builds order, k < 1024), prof words
-// Q3_PROF_LONG + 4 k: insertions whose partition sequence is longer than one
+// Q3_PROF_LONG + 16 k: insertions whose partition sequence is longer than one
 // chunk, their points, their ticks (100 MHz, from the publication to the end
-// of the emit), the ticks of all the build's partitions
+// of the emit), the ticks of all the build's partitions, the long ones' ticks
+// to the end of their locate; wave 0's ticks waiting for the speculation,
+// from the wait to the publication, from the emit's end to the next wait;
+// chunks of helped sequences wave 0 located, chunks the helpers did, ticks
+// waiting for them, ticks stopping them, events, posts
 #define Q3_PROF_LONG (Q3_PROF_W1 + 64)
 struct Q3P {
   unsigned long long tq2 = 0;   // LQRO_QHULL_PROFILE: the last speculation's end (this wave's clock)
@@ -354,6 +375,35 @@ __device__ __forceinline__ int4 q3_glb(const int4& r) {
 __device__ __forceinline__ void q3_glb_st(int4& r, const int4& v) {
   q3_v4i t; t.x = v.x; t.y = v.y; t.z = v.z; t.w = v.w;
   *(Q3_AS1 q3_v4i*)(&r) = t;
+}
+
+// A lane's columns for qh_findbesthorizon's visited facets and coplanar set
+// ([k][lane], stride 64): wave 0's in LDS (L.hvis, L.cop), each helper
+// wave's in its worker scratch (W.hvis, W.hcop) — one column per lane of
+// every wave that locates points at the same time
+struct Q3Col {
+  unsigned short* vis;
+  int* cop;
+};
+template <bool G, class T> __device__ __forceinline__ T q3_col(const T& r) {
+  if constexpr (G) return q3_glb(r);
+  else return q3_lds(r);
+}
+template <bool G, class T> __device__ __forceinline__ void q3_col_st(T& r, const T& v) {
+  if constexpr (G) q3_glb_st(r, v);
+  else q3_lds_st(r, v);
+}
+__device__ __forceinline__ Q3Col q3_col0(const Q3L& L, int lane) {
+  Q3Col C;
+  C.vis = const_cast<unsigned short*>(L.hvis) + lane;
+  C.cop = const_cast<int*>(L.cop) + lane;
+  return C;
+}
+__device__ __forceinline__ Q3Col q3_colh(const Q3W& W, int wave, int lane) {   // helper waves 1..Q3_WAVES-1
+  Q3Col C;
+  C.vis = W.hvis + (size_t)(wave - 1) * Q3_HZCAP * 64 + lane;
+  C.cop = W.hcop + (size_t)(wave - 1) * Q3_COPCAP * 64 + lane;
+  return C;
 }
 
 __device__ __forceinline__ void q3_get(const Q3W& W, const Q3L& L, int f, double* q, int* nb, int* fa) {
@@ -552,19 +602,21 @@ __device__ __forceinline__ void q3_place(unsigned long long grp, int lane, unsig
 // ---- point location, per lane (geom_r.c) ----
 // qh_findbesthorizon; a step reads the three neighbours together, and the
 // one the walk moves to brings its own neighbours along
+template <bool G>
 __device__ inline int q3_findbesthorizon(const Q3W& W, const Q3S& S, const Q3L& L, const double* p, int startfacet,
-                                         double* bestdist, int& lstatus) {
+                                         double* bestdist, int& lstatus, const Q3Col& C) {
   int bestfacet = startfacet;
   const double searchdist = S.max_outside + 2 * S.DISTround + fmax(S.MINvisible, S.MAXcoplanar);
   double minsearch = *bestdist - searchdist;
-  // the facets visited (qh.visit_id), in the lane's LDS column: a register
-  // array with a run-time length compiles to a select per slot and check
-  unsigned short* vis = const_cast<unsigned short*>(L.hvis) + (threadIdx.x & 63);
+  // the facets visited (qh.visit_id), in the lane's column (a register array
+  // with a run-time length compiles to a select per slot and check), and
+  // qh.coplanarfacetset
+  unsigned short* vis = C.vis;
   int nvis = 0;
-  int* cop = const_cast<int*>(L.cop) + (threadIdx.x & 63);   // qh.coplanarfacetset
+  int* cop = C.cop;
   int ncop = 0;
   int nextfacet = -1, nextnb[3] = {-1, -1, -1};
-  q3_lds_st(vis[0], (unsigned short)startfacet);
+  q3_col_st<G>(vis[0], (unsigned short)startfacet);
   nvis = 1;
   int cur[3] = {q3_nb(W, L, startfacet, 0), q3_nb(W, L, startfacet, 1), q3_nb(W, L, startfacet, 2)};
   for (;;) {
@@ -573,7 +625,7 @@ __device__ inline int q3_findbesthorizon(const Q3W& W, const Q3S& S, const Q3L& 
     for (int k = 0; k < 3; k++) q3_get(W, L, cur[k], q[k], nn[k], &fl[k]);
     bool seen3[3] = {false, false, false};
     for (int t = 0; t < nvis; t++) {
-      const int v = q3_lds(vis[64 * t]);
+      const int v = q3_col<G>(vis[64 * t]);
       seen3[0] |= v == cur[0]; seen3[1] |= v == cur[1]; seen3[2] |= v == cur[2];
     }
     for (int k = 0; k < 3; k++) {
@@ -582,7 +634,7 @@ __device__ inline int q3_findbesthorizon(const Q3W& W, const Q3S& S, const Q3L& 
       const bool seen = seen3[k] || (k >= 1 && nb == cur[0]) || (k == 2 && nb == cur[1]);
       if (seen) continue;
       if (nvis == Q3_HZCAP) { lstatus |= QHS_CAPACITY | Q3_CAPBIT(QHS_CAP_HZ); return bestfacet; }
-      q3_lds_st(vis[64 * nvis], (unsigned short)nb);
+      q3_col_st<G>(vis[64 * nvis], (unsigned short)nb);
       nvis++;
       if (!(fl[k] & QF_FLIPPED)) {
         const double dist = q3_distq(q[k], p);
@@ -597,7 +649,7 @@ __device__ inline int q3_findbesthorizon(const Q3W& W, const Q3S& S, const Q3L& 
       }
       if (nextfacet >= 0) {
         if (ncop == Q3_COPCAP) { lstatus |= QHS_CAPACITY | Q3_CAPBIT(QHS_CAP_COP); return bestfacet; }
-        cop[64 * ncop++] = nextfacet;
+        q3_col_st<G>(cop[64 * ncop++], nextfacet);
       }
       nextfacet = nb;
       nextnb[0] = nn[k][0]; nextnb[1] = nn[k][1]; nextnb[2] = nn[k][2];
@@ -609,8 +661,8 @@ __device__ inline int q3_findbesthorizon(const Q3W& W, const Q3S& S, const Q3L& 
     }
     if (!ncop) break;
     int facet;
-    if (ncop == 1) { facet = cop[0]; ncop = 0; }
-    else facet = cop[64 * --ncop];
+    if (ncop == 1) { facet = q3_col<G>(cop[0]); ncop = 0; }
+    else facet = q3_col<G>(cop[64 * --ncop]);
     cur[0] = q3_nb(W, L, facet, 0); cur[1] = q3_nb(W, L, facet, 1); cur[2] = q3_nb(W, L, facet, 2);
   }
   return bestfacet;
@@ -619,8 +671,9 @@ __device__ inline int q3_findbesthorizon(const Q3W& W, const Q3S& S, const Q3L& 
 // qh_findbestnew over the scan list: the new facets from index s0, the moved
 // old facets, the new facets before s0 (the facet list from startfacet to
 // its end, then from qh.newfacet_list)
+template <bool G>
 __device__ inline int q3_findbestnew(const Q3W& W, const Q3S& S, const Q3L& L, const double* p, int s0,
-                                     double* dist, int bestoutside, int* isoutside, int& lstatus) {
+                                     double* dist, int bestoutside, int* isoutside, int& lstatus, const Q3Col& C) {
   double bestdist = -DBL_MAX / 2;
   int bestfacet = -1;
   const double distoutside = fmax(2 * S.MINoutside, S.max_outside);    // qh_DISToutside
@@ -660,7 +713,7 @@ __device__ inline int q3_findbestnew(const Q3W& W, const Q3S& S, const Q3L& L, c
       }
     }
   }
-  bestfacet = q3_findbesthorizon(W, S, L, p, bestfacet >= 0 ? bestfacet : L.nslot[s0], &bestdist, lstatus);
+  bestfacet = q3_findbesthorizon<G>(W, S, L, p, bestfacet >= 0 ? bestfacet : L.nslot[s0], &bestdist, lstatus, C);
   *dist = bestdist;
   if (bestdist < S.MINoutside) *isoutside = 0;
   return bestfacet;
@@ -682,11 +735,12 @@ __device__ inline int q3_sharpnewfacets(const Q3S& S, const Q3L& L, int lane) {
 // facet and distance, and whether it changes the state (lqro_qhull.hpp
 // qh_locate).  s0: the start facet's new-facet index; sharp = 2:
 // qh_findbestnew(bestoutside) for a deleted vertex.
+template <bool G>
 __device__ inline int q3_locate(const Q3W& W, const Q3S& S, const Q3L& L, const double* p, int s0, int sharp,
-                                double* bestdist_out, int* isoutside, int* trigger, int& lstatus) {
+                                double* bestdist_out, int* isoutside, int* trigger, int& lstatus, const Q3Col& C) {
   *trigger = 0;
-  if (sharp == 2) return q3_findbestnew(W, S, L, p, s0, bestdist_out, 1, isoutside, lstatus);
-  if (S.findbestnew) return q3_findbestnew(W, S, L, p, s0, bestdist_out, 0, isoutside, lstatus);
+  if (sharp == 2) return q3_findbestnew<G>(W, S, L, p, s0, bestdist_out, 1, isoutside, lstatus, C);
+  if (S.findbestnew) return q3_findbestnew<G>(W, S, L, p, s0, bestdist_out, 0, isoutside, lstatus, C);
   // qh_findbest(point, startfacet, bestoutside 0, isnewfacets 1, noupper 0):
   // the new facets only, their neighbours nb1 / nb2 (nb0 is the horizon facet)
   double bestdist = -DBL_MAX / 2;
@@ -731,12 +785,12 @@ __device__ inline int q3_locate(const Q3W& W, const Q3S& S, const Q3L& L, const 
     }
     u = nxt;
   }
-  if (bestu < 0) return q3_findbestnew(W, S, L, p, 0, bestdist_out, 0, isoutside, lstatus);
+  if (bestu < 0) return q3_findbestnew<G>(W, S, L, p, 0, bestdist_out, 0, isoutside, lstatus, C);
   if (!S.notsharp && bestdist < -S.DISTround) {
     *trigger = 1;
-    if (sharp) return q3_findbestnew(W, S, L, p, bestu, bestdist_out, 0, isoutside, lstatus);
+    if (sharp) return q3_findbestnew<G>(W, S, L, p, bestu, bestdist_out, 0, isoutside, lstatus, C);
   }
-  const int bf = q3_findbesthorizon(W, S, L, p, L.nslot[bestu], &bestdist, lstatus);
+  const int bf = q3_findbesthorizon<G>(W, S, L, p, L.nslot[bestu], &bestdist, lstatus, C);
   *bestdist_out = bestdist;
   if (bestdist < S.MINoutside) *isoutside = 0;
   return bf;
@@ -799,12 +853,13 @@ __device__ __forceinline__ int q3_wait(const int* p, int v, bool ne) {
 
 // One chunk of the partition sequence located under the state S: the point
 // at position c + lane (when from <= pos < np), its facet, distance and
-// flags (qh_locate).  Wave 0 runs it for its chunks, wave 1 for the odd
-// chunks of a long sequence under a copy of wave 0's state.
+// flags (qh_locate).  Wave 0 runs it for the chunks it claims, waves 1-3 for
+// theirs under a copy of wave 0's state (q3_help).
+template <bool G>
 __device__ __forceinline__ void q3_chunk_locate(const Q3W& W, const Q3S& S, const Q3L& L, int c, int from, int np,
                                                 int sharp, bool init, int lane, const HullPt& pre, int prestart,
                                                 int prec, HullPt& pt, int& f, double& d, int& isout, int& trig,
-                                                int& ls) {
+                                                int& ls, const Q3Col& C) {
   const int pos = c + lane;
   pt = pre;
   f = -1; d = 0.0; isout = 0; trig = 0;
@@ -812,12 +867,29 @@ __device__ __forceinline__ void q3_chunk_locate(const Q3W& W, const Q3S& S, cons
     int start = prestart;
     if (c != prec) pt = q3_seqpt(W, L, S.nvis, init, pos, &start);   // (prec: the chunk pre holds)
     const double p[3] = {pt.x, pt.y, pt.z};
-    f = q3_locate(W, S, L, p, start, sharp, &d, &isout, &trig, ls);
+    f = q3_locate<G>(W, S, L, p, start, sharp, &d, &isout, &trig, ls, C);
   }
 }
 
-// wave 1: serve a chunk request (the state wave 0 had when it asked)
-__device__ inline void q3_serve_chunk(const Q3W& W, Q3L& L, int lane) {
+// Waves 1-3: claim and locate the posted sequence's next chunk, if any is
+// free (the state wave 0 had when it posted); true when one was located
+__device__ inline bool q3_help(const Q3W& W, Q3L& L, int lane, const Q3Col& C) {
+  const unsigned v = (unsigned)q3_ld_acq(reinterpret_cast<const int*>(&L.hctl));
+  if (v == 0u) return false;
+  const int k = (int)(v & 0xffffu);
+  if (k >= L.hq_end || k >= hl_ld(&L.hcons) + Q3_HR) return false;
+  int got = 0;
+  if (lane == 0) {
+    __hip_atomic_fetch_add(&L.hbusy, 1, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP);
+    unsigned e = v;
+    got = __hip_atomic_compare_exchange_strong(&L.hctl, &e, v + 1u, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (!got) __hip_atomic_fetch_add(&L.hbusy, -1, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  if (!__builtin_amdgcn_readfirstlane(got)) return false;
+#ifdef LQRO_QHULL_LONGPROF
+  const unsigned long long th0 = __builtin_amdgcn_s_memrealtime();
+#endif
   Q3S S;
   S.MINvisible = L.c_dist[0]; S.MAXcoplanar = L.c_dist[1]; S.DISTround = L.c_dist[2];
   S.MINoutside = 2 * S.MINvisible;
@@ -828,14 +900,44 @@ __device__ inline void q3_serve_chunk(const Q3W& W, Q3L& L, int lane) {
   pre.x = pre.y = pre.z = 0.0; pre.q = -1; pre.pad = 0;
   int f, isout, trig, ls = 0;
   double d;
-  q3_chunk_locate(W, S, L, L.hq_c, L.hq_from, L.hq_np, L.hq_sharp, L.hq_init != 0, lane, pre, L.hq_prestart, -1,
-                  pt, f, d, isout, trig, ls);
-  L.hr_pt[lane] = pt;
-  L.hr_d[lane] = d;
-  L.hr_f[lane] = f;
-  L.hr_k[lane] = isout | (trig << 1);
+  const int from = L.hq_from, np = L.hq_np, pos = 64 * k + lane;
+  q3_chunk_locate<true>(W, S, L, 64 * k, from, np, L.hq_sharp, L.hq_init != 0, lane, pre, 0, -1, pt, f, d, isout,
+                        trig, ls, C);
+#ifdef LQRO_QHULL_LONGPROF
+  const unsigned long long th1 = __builtin_amdgcn_s_memrealtime();
+#endif
+  // what wave 0 does with each result (q3_locate_seq), under the same state:
+  // the event kind and the destination (a new facet's index; an old facet's
+  // is wave 0's to give)
+  int kind = 0, dst = -1, dfa = 0;
+  if (pos >= from && pos < np) {
+    if (isout) {
+      dst = f;
+      dfa = q3_fa(W, L, f);
+      if (!(dfa & QF_NEW) && (q3_cc(W, L, f) & 0xffffu) == 0 && !q3_in_movf(S, L, f)) kind |= 4;
+    } else if (d >= -S.MAXcoplanar && d > S.max_outside) {
+      kind |= 2;
+    }
+    if (trig) kind |= 1;
+  }
+  const bool old = dst >= 0 && !(dfa & QF_NEW);
+  const int b = k % Q3_HR;
+  L.hr_d[64 * b + lane] = d;
+  L.hr_f[64 * b + lane] = (unsigned short)dst;
+  L.hr_k[64 * b + lane] = (unsigned short)(kind | (old ? 8 : 0) | ((dst >= 0 && !old ? (dfa >> 8) + 1 : 0) << 8));
   const int st = qh_wave_or(ls);
-  if (lane == 0) L.hr_ls = st;
+  if (lane == 0) {
+    L.hr_ls[b] = st;
+    q3_st_rel_lds(&L.hr_st[b], k + 1);   // (the results are in LDS)
+    __hip_atomic_fetch_add(&L.hbusy, -1, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef LQRO_QHULL_LONGPROF
+    const unsigned long long th2 = __builtin_amdgcn_s_memrealtime();
+    atomicAdd(&L.hprof[0], 1ull);
+    atomicAdd(&L.hprof[1], th1 - th0);
+    atomicAdd(&L.hprof[2], th2 - th0);
+#endif
+  }
+  return true;
 }
 
 // Locate the partition sequence in order (lqro_qhull.hpp qh_locate_seq) and
@@ -856,47 +958,39 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
   rd = 0.0;
   rpt = pre;
   hl_sync();
-  // a sequence of more than two chunks: wave 1 locates every other chunk
-  // (requested one chunk ahead under the current state; a result computed
-  // before an event changed the state is never asked for)
-  const bool help = np > 128;
-  int req = L.hstate >> 2, req_c = -1;   // the last request and its chunk
-  // the next chunk this wave locates itself, its points fetched one chunk
-  // ahead (the sequence's points do not change while it is located)
-  HullPt cpre = pre;
-  int cstart = prestart, cprec = havepre ? 0 : -1;
-  auto resolve = [&]() -> bool {   // true: wave 1 answered request `req`
-    if (req_c < 0) return false;
-    req_c = -1;
-    int st = q3_ld_acq(&L.hstate);
-    if (st == 4 * req + 1) {   // not taken yet: withdraw it
-      const int o = lane == 0 ? atomicCAS(&L.hstate, 4 * req + 1, 4 * req) : 0;
-      st = __builtin_amdgcn_readlane(o, 0);
-      if (st == 4 * req + 1) return false;
-    }
-    st = q3_wait(&L.hstate, 4 * req + 3, false);
-    // wave 1 took the request and never answered: it may still write the
-    // results, so the build stops here and k_qhull_big rebuilds the pair
-    if (st != 4 * req + 3) S.status |= QHS_CAPACITY | QHS_TIMEOUT;
-    return st == 4 * req + 3;
-  };
-  auto post = [&](int c2, int from2) {
-    resolve();
-    if (S.status & QHS_CAPACITY) return;
-    ++req;
+  // a sequence of more than one chunk: waves 1-3 locate chunks ahead of wave
+  // 0 under its current state, posted from `from` on; an event (a state
+  // change) stops them and posts the rest again under the new state
+  const bool help = np > 64;
+  const Q3Col C0 = q3_col0(L, lane);
+  auto post = [&](int from2) {   // (no helper holds a claim: hctl = 0, hbusy = 0)
+    S.hgen = S.hgen % 32767 + 1;
     if (lane == 0) {
-      L.hq_c = c2; L.hq_from = from2; L.hq_np = np; L.hq_sharp = sharp; L.hq_init = init ? 1 : 0;
-      L.hq_prestart = prestart;
+      L.hq_end = (np + 63) >> 6; L.hq_from = from2; L.hq_np = np; L.hq_sharp = sharp; L.hq_init = init ? 1 : 0;
       L.hq_findbestnew = S.findbestnew; L.hq_notsharp = S.notsharp; L.hq_nnew = S.nnew; L.hq_nmov = S.nmov;
       L.hq_nvis = S.nvis; L.hq_max_outside = S.max_outside;
-      q3_st_rel(&L.hstate, 4 * req + 1);
+      L.hcons = from2 >> 6;
+      for (int b = 0; b < Q3_HR; b++) L.hr_st[b] = 0;
+      // (a full release: the new facets' spilled records are global)
+      q3_st_rel(reinterpret_cast<int*>(&L.hctl), (int)(((unsigned)S.hgen << 16) | (unsigned)(from2 >> 6)));
     }
-    req_c = c2;
+  };
+  auto stop = [&]() {   // no further claims; the held ones answered
+    if (lane == 0) __hip_atomic_exchange(&L.hctl, 0u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP);
+    int b = __hip_atomic_load(&L.hbusy, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP);
+    for (long w = 0; b != 0 && w < (1l << 24); ++w) {
+      __builtin_amdgcn_s_sleep(Q3_W0_SLEEP);
+      b = __hip_atomic_load(&L.hbusy, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    // a helper that never answered may still write: the build stops here and
+    // is rebuilt (k_qhull_big)
+    if (b != 0) S.status |= QHS_CAPACITY | QHS_TIMEOUT;
   };
   int from = 0;
   while (from < np && !(S.status & QHS_CAPACITY)) {
     int ev_pos = np, ev_kind = 0, ev_dst = -1;
     double ev_d = 0.0;
+    if (help) post(from);
     for (int c = from & ~63; c < np; c += 64) {
       Q3C(23, 1);
       const int pos = c + lane;
@@ -905,30 +999,49 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
       double d = 0.0;
       HullPt pt = pre;
       int f = -1, isout = 0, trig = 0;
-      bool got = false;
-      if (help && req_c == c) {
-        got = resolve();
-        if (got) {
-          pt = L.hr_pt[lane]; d = L.hr_d[lane]; f = L.hr_f[lane];
-          isout = L.hr_k[lane] & 1; trig = (L.hr_k[lane] >> 1) & 1;
-          ls = L.hr_ls;
+      bool mine = !help;
+      if (help) {
+        // this chunk's results from a helper, or claimed and located here
+        const int k = c >> 6, b = k % Q3_HR;
+        int st = q3_ld_acq(&L.hr_st[b]);
+        if (st != k + 1) {
+          int m = 0;
+          if (lane == 0) {
+            unsigned e = __hip_atomic_load(&L.hctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if ((e & 0xffffu) == (unsigned)k)
+              m = __hip_atomic_compare_exchange_strong(&L.hctl, &e, e + 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+          mine = __builtin_amdgcn_readfirstlane(m) != 0;
+#ifdef LQRO_QHULL_LONGPROF
+          const unsigned long long tw0 = __builtin_amdgcn_s_memrealtime();
+#endif
+          if (!mine) st = q3_wait(&L.hr_st[b], k + 1, false);
+#ifdef LQRO_QHULL_LONGPROF
+          if (!mine) S.lp_hwait += __builtin_amdgcn_s_memrealtime() - tw0;
+#endif
         }
-      } else if (help && c + 64 < np) {
-        post(c + 64, from);   // the next chunk to wave 1
+#ifdef LQRO_QHULL_LONGPROF
+        if (mine) S.lp_own++; else S.lp_got++;
+#endif
+        int kv = 0;
+        if (!mine) {
+          if (st != k + 1) { S.status |= QHS_CAPACITY | QHS_TIMEOUT; break; }
+          const int fv = L.hr_f[64 * b + lane];
+          kv = L.hr_k[64 * b + lane];
+          ls = L.hr_ls[b];
+          dst = fv == 0xffff ? -1 : fv;
+          kind = act ? kv & 7 : 0;
+          // (a new destination's index: dfa's bits; an old one's: QF_NEW clear)
+          dfa = (kv & 8) ? 0 : (((kv >> 8) - 1) << 8) | QF_NEW;
+          d = L.hr_d[64 * b + lane];
+        }
       }
       Q3T(12);
-      if (!got) {
-        const int nc = c + (help ? 128 : 64);
-        HullPt npt = pre;
-        int nst = 0;
-        if (nc + lane < np) npt = q3_seqpt(W, L, S.nvis, init, nc + lane, &nst);
-        q3_chunk_locate(W, S, L, c, from, np, sharp, init, lane, cpre, cstart, cprec, pt, f, d, isout, trig, ls);
-        cpre = npt;
-        cstart = nst;
-        cprec = nc;
-      }
+      if (mine) q3_chunk_locate<false>(W, S, L, c, from, np, sharp, init, lane, pre, prestart, havepre ? 0 : -1, pt, f,
+                                       d, isout, trig, ls, C0);
       Q3T(13);
-      if (act) {
+      if (mine && act) {
         if (isout) {
           dst = f;
           dfa = q3_fa(W, L, f);
@@ -939,6 +1052,7 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
         if (trig) kind |= 1;
       }
       S.status |= qh_wave_or(ls);
+      if (help && lane == 0) q3_st_rel_lds(&L.hcons, (c >> 6) + 1);   // (its buffer is read)
       const unsigned long long b = __ballot(kind != 0);
       const int last = b ? __ffsll((long long)b) - 1 : 63;   // positions up to c+last are final
       const bool fin = act && lane <= last;
@@ -984,9 +1098,16 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
         break;
       }
     }
+#ifdef LQRO_QHULL_LONGPROF
+    const unsigned long long ts0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    if (help) stop();   // (the rest, if any, is posted again under the new state)
+#ifdef LQRO_QHULL_LONGPROF
+    if (help) { S.lp_stop += __builtin_amdgcn_s_memrealtime() - ts0; S.lp_posts++; if (ev_pos < np) S.lp_ev++; }
+#endif
+    if (S.status & QHS_CAPACITY) return;
     if (ev_pos < np) {
       Q3C(24, 1);
-      resolve();   // (a chunk wave 1 located under the old state is not used)
       if (ev_kind & 1) {
         if (sharp) S.findbestnew = 1;
         else S.notsharp = 1;
@@ -1027,7 +1148,6 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
     }
     from = ev_pos + 1;
   }
-  resolve();   // wave 1 is not left working on this sequence
 }
 
 // The located points into their destinations' outside sets, in sequence
@@ -1156,6 +1276,20 @@ __device__ inline void q3_emit_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int ndn
   }
   hl_sync();
   Q3T(15);
+  // at most 64 destinations (the usual long sequence): destination i's state
+  // in lane i (new facet i, then the old ones) from here to the end of the
+  // sequence, read by the group with lane reads — no LDS round trip and no
+  // wave barrier per destination group
+  const bool inl = nd <= 64;
+  int Rc = 0, Rch = -1, Ro = 0;
+  double Rm = 0.0, Rx = 0.0, Ry = 0.0, Rz = 0.0;
+  if (inl && lane < nd) {
+    const int g = lane < ndnew ? lane : Q3_NEWCAP + (lane - ndnew);
+    if (L.pcnt[g]) {
+      Rc = L.dcnt[g]; Rm = L.dmax[g]; Rch = L.dchamp[g]; Ro = L.doff[g];
+      Rx = L.dchp[3 * g]; Ry = L.dchp[3 * g + 1]; Rz = L.dchp[3 * g + 2];
+    }
+  }
   // the sequence in order: a chunk's lanes, grouped by destination (a long
   // sequence's next chunk loaded while this one is placed)
   int ng = -1;
@@ -1198,20 +1332,36 @@ __device__ inline void q3_emit_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int ndn
       const int gg = __builtin_amdgcn_readlane(g, lead);
       const unsigned long long grp = __ballot(g == gg);
       todo &= ~grp;
-      int cnt = L.dcnt[gg];
-      double mx = L.dmax[gg];
-      int champ = L.dchamp[gg];
-      double cx = L.dchp[3 * gg], cy = L.dchp[3 * gg + 1], cz = L.dchp[3 * gg + 2];
-      const int off = L.doff[gg];
-      q3_place(grp, lane, ltmask, dd, pt, off, W.SB, cnt, mx, champ, cx, cy, cz, wpos, wr);
-      Q3C(25, 1);
-      if (lane == 0) {
-        L.dcnt[gg] = cnt; L.dmax[gg] = mx; L.dchamp[gg] = champ;
-        L.dchp[3 * gg] = cx; L.dchp[3 * gg + 1] = cy; L.dchp[3 * gg + 2] = cz;
+      if (inl) {
+        const int l = gg < Q3_NEWCAP ? gg : ndnew + (gg - Q3_NEWCAP);
+        int cnt = __builtin_amdgcn_readlane(Rc, l), champ = __builtin_amdgcn_readlane(Rch, l);
+        double mx = hl_rl(Rm, l), cx = hl_rl(Rx, l), cy = hl_rl(Ry, l), cz = hl_rl(Rz, l);
+        q3_place(grp, lane, ltmask, dd, pt, __builtin_amdgcn_readlane(Ro, l), W.SB, cnt, mx, champ, cx, cy, cz, wpos,
+                 wr);
+        if (lane == l) { Rc = cnt; Rm = mx; Rch = champ; Rx = cx; Ry = cy; Rz = cz; }
+      } else {
+        int cnt = L.dcnt[gg];
+        double mx = L.dmax[gg];
+        int champ = L.dchamp[gg];
+        double cx = L.dchp[3 * gg], cy = L.dchp[3 * gg + 1], cz = L.dchp[3 * gg + 2];
+        const int off = L.doff[gg];
+        q3_place(grp, lane, ltmask, dd, pt, off, W.SB, cnt, mx, champ, cx, cy, cz, wpos, wr);
+        if (lane == 0) {
+          L.dcnt[gg] = cnt; L.dmax[gg] = mx; L.dchamp[gg] = champ;
+          L.dchp[3 * gg] = cx; L.dchp[3 * gg + 1] = cy; L.dchp[3 * gg + 2] = cz;
+        }
+        hl_sync();
       }
-      hl_sync();
+      Q3C(25, 1);
     }
     if (wpos >= 0) W.sb[wpos] = wr;
+  }
+  if (inl && lane < nd) {   // (the lanes' state back for the sets' ends and the queue)
+    const int g = lane < ndnew ? lane : Q3_NEWCAP + (lane - ndnew);
+    if (L.pcnt[g]) {
+      L.dcnt[g] = Rc; L.dmax[g] = Rm; L.dchamp[g] = Rch;
+      L.dchp[3 * g] = Rx; L.dchp[3 * g + 1] = Ry; L.dchp[3 * g + 2] = Rz;
+    }
   }
   hl_sync();
   Q3T(17);
@@ -1673,6 +1823,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
   S.sbtop = 0;
   S.nnew = S.nvis = S.nmov = S.nold = 0;
   S.findbestnew = S.notsharp = 0;
+  S.hgen = 0;
   S.keyc = 1;
   S.key0_last = 0;
   S.qhead = S.qtail = 0;
@@ -2006,6 +2157,10 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     pre.q = -1;
     pre.pad = 0;
     int pfa = 0, pfnp = -1;
+#ifdef LQRO_QHULL_LONGPROF
+    const unsigned long long lp_ta = __builtin_amdgcn_s_memrealtime();
+    S.lp_tail += S.lp_tw ? lp_ta - S.lp_tw : 0ull;
+#endif
     if (phase > 0) {
 #ifdef LQRO_QHULL_PROFILE
       const unsigned long long tw_ = __builtin_amdgcn_s_memtime();
@@ -2038,6 +2193,9 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
           S.r_start += L.start_r - L.pub_r; S.r_done += L.done_r - L.pub_r; S.r_seen += nr_ - L.pub_r;
         }
       }
+#endif
+#ifdef LQRO_QHULL_LONGPROF
+      S.lp_wait += __builtin_amdgcn_s_memrealtime() - lp_ta;
 #endif
       if (dn != phase) {   // wave 1 still speculating (it writes vertex records from L.nslot): stop
         S.status |= QHS_CAPACITY | QHS_TIMEOUT;
@@ -2533,6 +2691,10 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
     if (lane == 0) { L.pub_t = __builtin_amdgcn_s_memtime(); L.pub_r = __builtin_amdgcn_s_memrealtime(); }
     if (S.tseen) { S.tpre += __builtin_amdgcn_s_memtime() - S.tseen; S.npre += 1; }   // (this wave's clock) seen -> publication
 #endif
+#ifdef LQRO_QHULL_LONGPROF
+    const unsigned long long lp_t0 = __builtin_amdgcn_s_memrealtime();
+    S.lp_adopt += lp_t0 - lp_ta;   // (less the wait, in lp_wait)
+#endif
     if (lane == 0) q3_st_rel(&L.ph, phase);
 #ifdef LQRO_QHULL_PROFILE
     if (lane == 0) S.trel += __builtin_amdgcn_s_memtime() - L.pub_t;   // the release's own cost
@@ -2552,9 +2714,6 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
       np2 += __builtin_amdgcn_readlane(inc, 63);
     }
     hl_sync();
-#ifdef LQRO_QHULL_LONGPROF
-    const unsigned long long lp_t0 = __builtin_amdgcn_s_memrealtime();
-#endif
     int prestart = 0;
     if (pfv && np2 == pfnp) {   // wave 2's head of the sequence
       if (lane < np2) prestart = L.repl[pfa] >= 0 ? L.repl[pfa] : 0;
@@ -2573,6 +2732,9 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
       double rd;
       HullPt rpt;
       q3_locate_seq(W, S, L, np2, sharp, false, lane, pre, prestart, true, rg, rd, rpt);
+#ifdef LQRO_QHULL_LONGPROF
+      if (np2 > 64) S.lp_tloc += __builtin_amdgcn_s_memrealtime() - lp_t0;
+#endif
       Q3T(6);
       q3_emit_seq(W, S, L, np2, nnew, false, lane, rg, rd, rpt);
       Q3T(7);
@@ -2582,6 +2744,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
       const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - lp_t0;
       S.lp_all += dt;
       if (np2 > 64) { S.lp_n += 1; S.lp_pts += (unsigned long long)np2; S.lp_t += dt; }
+      S.lp_tw = lp_t0 + dt;
     }
 #endif
     if (S.status & QHS_CAPACITY) return;
@@ -2604,7 +2767,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
         const double p[3] = {W.Pr[3 * (size_t)v], W.Pr[3 * (size_t)v + 1], W.Pr[3 * (size_t)v + 2]};
         double d;
         int iso, trig;
-        q3_locate(W, S, L, p, 0, 2, &d, &iso, &trig, lsd);
+        q3_locate<false>(W, S, L, p, 0, 2, &d, &iso, &trig, lsd, q3_col0(L, lane));
         if (d >= -S.MAXcoplanar) lsd |= QHS_COPLANAR;
       }
       S.status |= qh_wave_or(lsd);
@@ -2908,7 +3071,10 @@ __device__ __forceinline__ void q3_body(const HullArgs& A, Q3L& L, QhL* LB = nul
     // a fresh handshake and wave 1's epochs for this job (ordered by
     // hull_points' barriers)
     if (threadIdx.x == 0) {
-      L.ph = 0; L.sp_done = 0; L.sp_gdone = 0; L.hstate = 0; L.sp_hz = 0; L.pf_done = 0;
+      L.ph = 0; L.sp_done = 0; L.sp_gdone = 0; L.hctl = 0u; L.hbusy = 0; L.sp_hz = 0; L.pf_done = 0;
+#ifdef LQRO_QHULL_LONGPROF
+      L.hprof[0] = L.hprof[1] = L.hprof[2] = L.hprof[3] = 0ull;
+#endif
       L.big_slot = -1;
     }
     for (int q = threadIdx.x; q < Q3_FL / 2; q += blockDim.x) reinterpret_cast<unsigned*>(L.mark)[q] = 0u;
@@ -2922,18 +3088,23 @@ __device__ __forceinline__ void q3_body(const HullArgs& A, Q3L& L, QhL* LB = nul
     const double vrel[3] = {xi[3] - xj[3], xi[4] - xj[4], xi[5] - xj[5]};
     const int n = hull_points(A, L, Ti, Ni, xi, xj, vrel, W.Pr, W.Pf);
     bool lp_go = false;
-    if (wave == 2) {
-      // prefetch each horizon wave 1 publishes until the build ends
+    if (wave >= 2) {
+      // wave 2: prefetch each horizon wave 1 publishes; waves 2 and 3: locate
+      // posted chunks; until the build ends
+      const Q3Col CH = q3_colh(W, wave, lane);
       int last = 0;
       long idle = 0;
       for (;;) {
-        const int hz = q3_ld_acq(&L.sp_hz);
-        if (hz != last && hz > 0) {
-          last = hz;
-          q3_prefetch(W, L, lane, hz);
-          idle = 0;
-          continue;
+        if (wave == 2) {
+          const int hz = q3_ld_acq(&L.sp_hz);
+          if (hz != last && hz > 0) {
+            last = hz;
+            q3_prefetch(W, L, lane, hz);
+            idle = 0;
+            continue;
+          }
         }
+        if (q3_help(W, L, lane, CH)) { idle = 0; continue; }
         if (q3_ld_acq(&L.ph) < 0) break;
         if (++idle > (1l << 24)) break;
         __builtin_amdgcn_s_sleep(Q3_W2_SLEEP);
@@ -2948,6 +3119,7 @@ __device__ __forceinline__ void q3_body(const HullArgs& A, Q3L& L, QhL* LB = nul
       }
       unsigned ep2 = W.ctr[0];
       unsigned short ep = 0;
+      const Q3Col CH = q3_colh(W, 1, lane);
       int last = 0;
       Q3QC Q;
       Q.qcb = 0; Q.qcn = 0; Q.qf = 0; Q.qp = -1; Q.qk = 0u; Q.qx = Q.qy = Q.qz = 0.0;
@@ -2986,23 +3158,18 @@ __device__ __forceinline__ void q3_body(const HullArgs& A, Q3L& L, QhL* LB = nul
           idle = 0;
           continue;
         }
-        const int hs = q3_ld_acq(&L.hstate);
-        if ((hs & 3) == 1) {   // a chunk request: take it unless wave 0 withdrew it
-          const int o = lane == 0 ? atomicCAS(&L.hstate, hs, hs + 1) : 0;
-          if (__builtin_amdgcn_readlane(o, 0) == hs) {
+        {
 #ifdef LQRO_QHULL_PROFILE
-            const unsigned long long t0_ = __builtin_amdgcn_s_memtime();
+          const unsigned long long t0_ = __builtin_amdgcn_s_memtime();
 #endif
-            q3_serve_chunk(W, L, lane);
-            hl_sync();
-            if (lane == 0) q3_st_rel_lds(&L.hstate, hs + 2);   // (the results are in LDS)
+          if (q3_help(W, L, lane, CH)) {   // a posted chunk
 #ifdef LQRO_QHULL_PROFILE
             P.t[6] += __builtin_amdgcn_s_memtime() - t0_;
             P.t[8] += 1;
 #endif
+            idle = 0;
+            continue;
           }
-          idle = 0;
-          continue;
         }
         if (++idle > (1l << 24)) break;
         __builtin_amdgcn_s_sleep(Q3_W1_SLEEP);
@@ -3033,7 +3200,8 @@ __device__ __forceinline__ void q3_body(const HullArgs& A, Q3L& L, QhL* LB = nul
     S.status = 0;
     S.nalloc = 1;
     S.nins = 0;
-    S.lp_n = S.lp_pts = S.lp_t = S.lp_all = 0;
+    S.lp_n = S.lp_pts = S.lp_t = S.lp_all = S.lp_tloc = S.lp_wait = S.lp_adopt = S.lp_tail = S.lp_tw = 0;
+    S.lp_own = S.lp_got = S.lp_hwait = S.lp_stop = S.lp_ev = S.lp_posts = 0;
     if (L.fail || n < 4) S.status = QHS_INPUT;
     else q3_build(W, S, L, n, lane);
     hl_sync();
@@ -3088,8 +3256,11 @@ __device__ __forceinline__ void q3_body(const HullArgs& A, Q3L& L, QhL* LB = nul
       const int k = hull_build_note(A, slot, 0, tjob, n, S.nins, S.nalloc - 1);
 #ifdef LQRO_QHULL_LONGPROF
       if (A.prof && k >= 0 && k < 1024) {
-        unsigned long long* r = A.prof + Q3_PROF_LONG + 4 * k;
+        unsigned long long* r = A.prof + Q3_PROF_LONG + 16 * k;
         r[0] = S.lp_n; r[1] = S.lp_pts; r[2] = S.lp_t; r[3] = S.lp_all;
+        r[4] = S.lp_tloc; r[5] = S.lp_wait; r[6] = S.lp_adopt - S.lp_wait; r[7] = S.lp_tail;
+        r[8] = S.lp_own; r[9] = S.lp_got; r[10] = S.lp_hwait; r[11] = S.lp_stop; r[12] = S.lp_ev; r[13] = S.lp_posts;
+        r[14] = L.hprof[0]; r[15] = L.hprof[1] | (L.hprof[2] << 32);
       }
 #else
       (void)k;

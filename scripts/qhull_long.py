@@ -23,22 +23,31 @@ c.set_gains(g["A"], g["B"], g["L"], g["E"])
 for k in range(K):
     c.step(x, vg)
 b = c.hull_builds()
-w = np.zeros(4 * 1024, np.uint64)
+w = np.zeros(16 * 1024, np.uint64)
 fn = lqro.lib().lqro_debug_prof_words
 fn.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]
-assert fn(c._h, Q3_PROF_LONG, 4 * 1024, w.ctypes.data_as(C.c_void_p)) == 0
+assert fn(c._h, Q3_PROF_LONG, 16 * 1024, w.ctypes.data_as(C.c_void_p)) == 0
 c.close()
-w = w.reshape(-1, 4)[:len(b)]
+w = w.reshape(-1, 16)[:len(b)]
 d = (b["t_end"] - b["t_start"]) / 1e5
 ok = b["kernel"] == 0
 tot = d[ok].sum()
 print(f"builds {ok.sum()}: {tot:.1f} ms; long-sequence insertions {w[ok, 0].sum() / ok.sum():.1f} per build, "
       f"{w[ok, 2].sum() / 1e5 / tot * 100:.1f} % of build time; all partitions {w[ok, 3].sum() / 1e5 / tot * 100:.1f} %")
-print("slowest builds: ms, insertions, long insertions, long points, long ms, all partitions ms, us/ins one-chunk")
+print("wave 0 over all builds (% of build time): waiting for the speculation "
+      f"{w[ok, 5].sum() / 1e5 / tot * 100:.1f}, adoption to publication {w[ok, 6].sum() / 1e5 / tot * 100:.1f}, "
+      f"partitions {w[ok, 3].sum() / 1e5 / tot * 100:.1f} (long ones' locate {w[ok, 4].sum() / 1e5 / tot * 100:.1f}), "
+      f"after the emit {w[ok, 7].sum() / 1e5 / tot * 100:.1f}")
+print("slowest builds: ms, insertions, long insertions, long points, long ms (locate), all partitions ms, "
+      "us/ins one-chunk; wave 0 ms: wait, adopt, tail")
 for i in np.argsort(-d)[:8]:
     if not ok[i]:
         continue
-    n_l, p_l, t_l, t_a = (int(v) for v in w[i])
+    n_l, p_l, t_l, t_a, t_loc, t_w, t_ad, t_tl = (int(v) for v in w[i][:8])
     rest = d[i] - t_l / 1e5
-    print(f"  {d[i]:7.2f} {b['insertions'][i]:5d} {n_l:4d} {p_l:6d} {t_l / 1e5:6.2f} {t_a / 1e5:6.2f} "
-          f"{1e3 * rest / max(1, b['insertions'][i] - n_l):6.2f}")
+    print(f"  {d[i]:7.2f} {b['insertions'][i]:5d} {n_l:4d} {p_l:6d} {t_l / 1e5:6.2f} ({t_loc / 1e5:5.2f}) {t_a / 1e5:6.2f} "
+          f"{1e3 * rest / max(1, b['insertions'][i] - n_l):6.2f}; {t_w / 1e5:6.2f} {t_ad / 1e5:6.2f} {t_tl / 1e5:6.2f}")
+    own, got, hw, hs, ev, po, hn, ht = (int(v) for v in w[i][8:16])
+    print(f"      helped sequences: chunks wave 0 {own}, helpers {got}, waiting for helpers {hw / 1e5:.2f} ms, "
+          f"stopping them {hs / 1e5:.2f} ms, events {ev}, posts {po}; helper chunks {hn}: "
+          f"{(ht & 0xffffffff) / 1e2 / max(hn, 1):.2f} us locating, {(ht >> 32) / 1e2 / max(hn, 1):.2f} us claimed")
