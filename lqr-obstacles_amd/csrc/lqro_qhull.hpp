@@ -157,9 +157,9 @@ struct QhL {
   int n, fail, job, slot;
   double eps;
   double tr[3 * 128];
-  double rk[1];
-  int ri[1];
-  int scan[1];
+  double rk[4];            // (four: q3_big_inline runs hull_points on all of k_qhull's waves)
+  int ri[4];
+  int scan[4];
   int newf[QH_NEWCAP];     // new facets, creation (= list) order
   int visf[QH_VISCAP];     // visible facets, qh_findhorizon order
   int movf[QH_MOVCAP];     // old facets moved behind the new ones this partition (scan order)

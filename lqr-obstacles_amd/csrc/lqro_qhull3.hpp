@@ -244,6 +244,7 @@ struct Q3L {
   unsigned long long hprof[4];       // helper chunks, their ticks locating, claim to release
 #endif
   int big_slot;                      // a build past the caps, rebuilt in place by qh_build (q3_body)
+  int qflags;                        // HullArgs::qflags
 #ifdef LQRO_QHULL_PROFILE
   unsigned long long pub_t, done_t, done_t2;   // the last publication / speculation end, after its store
   unsigned long long pub_r, start_r, done_r;    // the same on the 100 MHz real-time clock (one clock for all waves)
@@ -961,7 +962,7 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
   // a sequence of more than one chunk: waves 1-3 locate chunks ahead of wave
   // 0 under its current state, posted from `from` on; an event (a state
   // change) stops them and posts the rest again under the new state
-  const bool help = np > 64;
+  const bool help = np > 64 && (L.qflags & 1);
   const Q3Col C0 = q3_col0(L, lane);
   auto post = [&](int from2) {   // (no helper holds a claim: hctl = 0, hbusy = 0)
     S.hgen = S.hgen % 32767 + 1;
@@ -1280,7 +1281,7 @@ __device__ inline void q3_emit_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int ndn
   // in lane i (new facet i, then the old ones) from here to the end of the
   // sequence, read by the group with lane reads — no LDS round trip and no
   // wave barrier per destination group
-  const bool inl = nd <= 64;
+  const bool inl = nd <= 64 && (L.qflags & 2);
   int Rc = 0, Rch = -1, Ro = 0;
   double Rm = 0.0, Rx = 0.0, Ry = 0.0, Rz = 0.0;
   if (inl && lane < nd) {
@@ -3072,6 +3073,7 @@ __device__ __forceinline__ void q3_body(const HullArgs& A, Q3L& L, QhL* LB = nul
     // hull_points' barriers)
     if (threadIdx.x == 0) {
       L.ph = 0; L.sp_done = 0; L.sp_gdone = 0; L.hctl = 0u; L.hbusy = 0; L.sp_hz = 0; L.pf_done = 0;
+      L.qflags = A.qflags;
 #ifdef LQRO_QHULL_LONGPROF
       L.hprof[0] = L.hprof[1] = L.hprof[2] = L.hprof[3] = 0ull;
 #endif

@@ -395,6 +395,7 @@ struct lqro_ctx {
   int hot_split;             // LQRO_HOT_SPLIT (default 1): the split hot launch in Qhull order
   int qside_pct;             // LQRO_QHULL_SIDE_PCT: side CUs per 100 of the last step's inside-hull pairs (default 100)
   int qhull_inline;          // LQRO_QHULL_INLINE_BIG: k_qhull rebuilds a capped build in place (default 1)
+  int qhull_flags;           // LQRO_QHULL_FLAGS: k_qhull's helper waves (1) and emit lane state (2), default 3
   int qbalance;              // LQRO_QHULL_BALANCE: the side's width from the measured work (default 1)
   int qspare;                // LQRO_QHULL_SPARE: side CUs beyond the last step's inside-hull count (default 4; -1: count/16 + 4)
   int hot_spec;              // LQRO_HOT_SPEC (default 1): with the split, the last step's inside pairs are built speculatively from the step's start
@@ -694,6 +695,8 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
     // instead of in the k_qhull_big launch after the sweep
     const char* qi = getenv("LQRO_QHULL_INLINE_BIG");
     c->qhull_inline = qi ? atoi(qi) != 0 : 1;
+    const char* qf = getenv("LQRO_QHULL_FLAGS");
+    c->qhull_flags = qf ? atoi(qf) : 3;
     // the side's width from the measured work of the step two before (the
     // sweep's CU time, the builds' total and longest): no wider than leaves
     // the sweep no longer than the builds (LQRO_QHULL_BALANCE=0: one CU per
@@ -1077,6 +1080,7 @@ static int enqueue_step(lqro_ctx* c, const double* d_x, const double* d_vgoal, d
   // more than 10,000 points (C5's ~19,000), or builds capped two steps before)
   Hh.big_inline =
       c->qhull_inline && !c->qhull_big && ((size_t)g.horizon * g.n_points > 10000 || retried_prev > 0) ? 1 : 0;
+  Hh.qflags = c->qhull_flags;
   if (g.x_dim != 16 && g.x_dim != 12) return LQRO_E_ARG;
   // the row launch is submitted before the side stream's work: should the two
   // streams land on one hardware queue (a second context in the process), the
@@ -1745,7 +1749,7 @@ int lqro_debug_hull_points(lqro_ctx* c, const double* pts, int32_t n, const doub
       Hh.ext_pts = d_pts; Hh.ext_n = n; Hh.ext_max = fmax;
       Hh.ext_facets = (local == 1 || !facets) ? nullptr : d_f; Hh.ext_nf = d_q + 7;
       Hh.ext_full = local == 2;   // k_qhull: rounded points, then the full-precision ones
-      Hh.qscratch = d_qw; Hh.qstride = qstride; Hh.qnrm = d_qn;
+      Hh.qscratch = d_qw; Hh.qstride = qstride; Hh.qnrm = d_qn; Hh.qflags = c->qhull_flags;
       Hh.qstale = d_q + 14; Hh.qstale_count = d_q + 9; Hh.qstale_cap = 1;
       if (local == 2) {
         Hh.big_main = c->qhull_big;

@@ -14,6 +14,9 @@ import numpy as np  # noqa: E402
 
 import lqro  # noqa: E402
 import pyoracle  # noqa: E402
+
+if os.environ.get("LQRO_LIB"):   # a variant library (its name in lqr-obstacles_amd/)
+    lqro.LIB_PATH = os.path.join(os.path.dirname(lqro.LIB_PATH), os.environ["LQRO_LIB"])
 from dyn_bench import states  # noqa: E402
 from test_gpu_dyn import STATE, _Hip  # noqa: E402
 
