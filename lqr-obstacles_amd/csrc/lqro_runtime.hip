@@ -601,11 +601,17 @@ static int ctx_alloc(lqro_ctx* c) {
   c->hot_cap = (int)std::max<size_t>(16384, slots / 32);
   HIPCHK(hipMalloc(&c->d_hotlist, sizeof(int) * c->hot_cap));
   HIPCHK(hipMalloc(&c->d_hotmark, slots ? slots : 1));
+  // (k_prio keeps a mark of 2 it finds — k_prio_prev's "listed" — so the marks
+  // start at 0: the first split step after the plain ones would otherwise
+  // take recycled device memory's bytes for marks and skip those pairs)
+  HIPCHK(hipMemset(c->d_hotmark, 0, slots ? slots : 1));
   HIPCHK(hipMalloc(&c->d_lp4, sizeof(int) * 6 * (size_t)std::max(1, c->nrows)));
   HIPCHK(hipMalloc(&c->d_carry, sizeof(double) * 6));
   HIPCHK(hipMalloc(&c->d_rowpend, sizeof(int) * 2 * (size_t)std::max(1, c->nrows)));
   c->d_rowclaim = c->d_rowpend + std::max(1, c->nrows);
   HIPCHK(hipMemset(c->d_carry, 0, sizeof(double) * 6));
+  HIPCHK(hipMemset(c->d_lp4, 0, sizeof(int) * 6 * (size_t)std::max(1, c->nrows)));
+  HIPCHK(hipMemset(c->d_rowpend, 0, sizeof(int) * 2 * (size_t)std::max(1, c->nrows)));
   if (c->qhull_order) {
     // k_qhull: one one-wave worker per CU (the build's facets fill the CU's
     // LDS), each with its own build scratch
@@ -619,6 +625,9 @@ static int ctx_alloc(lqro_ctx* c) {
     HIPCHK(hipMalloc(&c->d_prevq, sizeof(int) * (size_t)c->hot_cap));
     HIPCHK(hipMalloc(&c->d_hot2, sizeof(int) * 8));
     HIPCHK(hipMemset(c->d_hot2, 0, sizeof(int) * 8));
+    HIPCHK(hipMemset(c->d_prevq, 0xFF, sizeof(int) * (size_t)c->hot_cap));
+    HIPCHK(hipMemset(c->d_qstale, 0xFF, sizeof(int) * (slots ? slots : 1)));
+    HIPCHK(hipMemset(c->d_hbuild, 0, sizeof(unsigned long long) * 4 * LQRO_HBUILD_CAP));
   }
   return LQRO_OK;
 }

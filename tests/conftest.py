@@ -27,6 +27,8 @@ def oracle():
 @pytest.fixture(scope="session")
 def lqro_mod():
     import lqro
+    if os.environ.get("LQRO_LIB"):   # a variant library in lqr-obstacles_amd/ (A/B and regression runs)
+        lqro.LIB_PATH = os.path.join(os.path.dirname(lqro.LIB_PATH), os.environ["LQRO_LIB"])
     if not os.path.exists(lqro.LIB_PATH):
         import __graft_entry__ as ge
         ge.build_lib()

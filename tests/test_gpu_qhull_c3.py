@@ -264,3 +264,41 @@ def test_hull_build_records(lqro_mod, gains):
     by = {(int(q["i"]), int(q["j"])): q for q in ins}
     for q in done:
         assert q["n_points"] == by[(int(q["i"]), int(q["j"]))]["n_reach"]
+
+
+def test_recycled_device_memory(lqro_mod, gains, monkeypatch, c3_oracle):
+    """A context on device memory that held other data: the hot marks start
+    at 0 whatever the allocator hands back (k_prio keeps a mark of 2, k_prio_prev's
+    "listed", so recycled bytes of 2 made the first split step skip those
+    pairs).  1.3 GiB are filled with 2s and freed first; the third step (the
+    first with the split hot launch) bit for bit against the oracle."""
+    from test_gpu_dyn import _Hip
+    import ctypes as C
+    x, vg, rv, rr, carry = c3_oracle
+    for k in ("LQRO_EARLY_LP", "LQRO_QSIDE", "LQRO_HOT", "LQRO_LOCAL_HULL", "LQRO_SIDE_HULL_CUS", "LQRO_HOT_SPLIT",
+              "LQRO_HOT_SPEC", "LQRO_QHULL_SPARE", "LQRO_QHULL_BALANCE", "LQRO_QHULL_INLINE_BIG"):
+        monkeypatch.delenv(k, raising=False)
+    hip = _Hip()
+    blocks = []
+    slots = 1024 * 1023
+    for size in [32 << 20] * 32 + [slots] * 256:   # (large blocks, and blocks of the marks' own size)
+        p = C.c_void_p()
+        if hip.h.hipMalloc(C.byref(p), C.c_size_t(size)) != 0:
+            break
+        assert hip.h.hipMemset(p, 2, C.c_size_t(size)) == 0
+        blocks.append(p)
+    assert hip.h.hipDeviceSynchronize() == 0
+    for p in blocks:
+        assert hip.h.hipFree(p) == 0
+    ctx = lqro_mod.Context(lqro_mod.config(1024, 100, 100,
+                                           flags=lqro_mod.LQRO_FLAG_RECORDS | lqro_mod.LQRO_FLAG_QHULL_ORDER))
+    ctx.set_gains(gains["A"], gains["B"], gains["L"], gains["E"])
+    try:
+        for t in range(3):
+            ctx.carry_normal(np.zeros(3))
+            v = ctx.step(x, vg)
+        r = ctx.records()
+        _compare(r, rr)
+        assert np.array_equal(v.view(np.uint64), rv.view(np.uint64))
+    finally:
+        ctx.close()
