@@ -241,7 +241,9 @@ struct Q3L {
   int hq_findbestnew, hq_notsharp, hq_nnew, hq_nmov, hq_nvis;
   double hq_max_outside;
 #ifdef LQRO_QHULL_LONGPROF
-  unsigned long long hprof[4];       // helper chunks, their ticks locating, claim to release
+  unsigned long long hprof[8];       // helper chunks, their ticks locating, claim to release; wave 1:
+                                     // speculations, publication -> seen, seen -> done; wave 0: done -> seen
+  unsigned long long lp_pubr, lp_doner;   // the last publication's / speculation end's real time
 #endif
   int big_slot;                      // a build past the caps, rebuilt in place by qh_build (q3_body)
   int qflags;                        // HullArgs::qflags
@@ -301,13 +303,15 @@ struct Q3S {
 #define Q3_PROF_W1 (32 + 2 * 4096 + 48 + 4 * 4096)
 // LQRO_QHULL_LONGPROF (a diagnostic build, scripts/build_variant.sh): per
 // build record k (lqro_get_hull_builds order, k < 1024), prof words
-// Q3_PROF_LONG + 16 k: insertions whose partition sequence is longer than one
+// Q3_PROF_LONG + 24 k: insertions whose partition sequence is longer than one
 // chunk, their points, their ticks (100 MHz, from the publication to the end
 // of the emit), the ticks of all the build's partitions, the long ones' ticks
 // to the end of their locate; wave 0's ticks waiting for the speculation,
 // from the wait to the publication, from the emit's end to the next wait;
 // chunks of helped sequences wave 0 located, chunks the helpers did, ticks
-// waiting for them, ticks stopping them, events, posts
+// waiting for them, ticks stopping them, events, posts; helper chunks and
+// their ticks; wave 1's speculations, publication -> seen and seen -> done
+// ticks; wave 0's waits and their speculation-end -> seen ticks
 #define Q3_PROF_LONG (Q3_PROF_W1 + 64)
 struct Q3P {
   unsigned long long tq2 = 0;   // LQRO_QHULL_PROFILE: the last speculation's end (this wave's clock)
@@ -2179,6 +2183,13 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
 #else
       const int dn = q3_wait(&L.sp_done, phase, false);
 #endif
+#ifdef LQRO_QHULL_LONGPROF
+      {   // (wave 0 waited: the speculation's end -> seen here)
+        const unsigned long long tn = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long de = q3_lds(L.lp_doner);
+        if (tn - lp_ta > 20 && tn > de && lane == 0) { L.hprof[6] += tn - de; L.hprof[7] += 1; }
+      }
+#endif
 #ifdef LQRO_QHULL_PROFILE
       {
         const unsigned long long tn_ = __builtin_amdgcn_s_memtime();
@@ -2695,6 +2706,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
 #ifdef LQRO_QHULL_LONGPROF
     const unsigned long long lp_t0 = __builtin_amdgcn_s_memrealtime();
     S.lp_adopt += lp_t0 - lp_ta;   // (less the wait, in lp_wait)
+    if (lane == 0) L.lp_pubr = lp_t0;
 #endif
     if (lane == 0) q3_st_rel(&L.ph, phase);
 #ifdef LQRO_QHULL_PROFILE
@@ -3075,7 +3087,8 @@ __device__ __forceinline__ void q3_body(const HullArgs& A, Q3L& L, QhL* LB = nul
       L.ph = 0; L.sp_done = 0; L.sp_gdone = 0; L.hctl = 0u; L.hbusy = 0; L.sp_hz = 0; L.pf_done = 0;
       L.qflags = A.qflags;
 #ifdef LQRO_QHULL_LONGPROF
-      L.hprof[0] = L.hprof[1] = L.hprof[2] = L.hprof[3] = 0ull;
+      for (int k = 0; k < 8; k++) L.hprof[k] = 0ull;
+      L.lp_pubr = L.lp_doner = 0ull;
 #endif
       L.big_slot = -1;
     }
@@ -3144,8 +3157,18 @@ __device__ __forceinline__ void q3_body(const HullArgs& A, Q3L& L, QhL* LB = nul
           if (P.tq2) P.t[15] += t0_ - P.tq2;   // (this wave's clock) its last speculation's end -> this start
           if (lane == 0) L.start_r = __builtin_amdgcn_s_memrealtime();
 #endif
+#ifdef LQRO_QHULL_LONGPROF
+          const unsigned long long ts_ = __builtin_amdgcn_s_memrealtime();
+#endif
           q3_spec(W, L, lane, ep, ep2, Q, P, p);
           hl_sync();
+#ifdef LQRO_QHULL_LONGPROF
+          if (lane == 0) {
+            const unsigned long long te_ = __builtin_amdgcn_s_memrealtime();
+            L.hprof[3] += 1; L.hprof[4] += ts_ - q3_lds(L.lp_pubr); L.hprof[5] += te_ - ts_;
+            L.lp_doner = te_;
+          }
+#endif
 #ifdef LQRO_QHULL_PROFILE
           if (lane == 0) L.done_t = __builtin_amdgcn_s_memtime();
 #endif
@@ -3258,11 +3281,12 @@ __device__ __forceinline__ void q3_body(const HullArgs& A, Q3L& L, QhL* LB = nul
       const int k = hull_build_note(A, slot, 0, tjob, n, S.nins, S.nalloc - 1);
 #ifdef LQRO_QHULL_LONGPROF
       if (A.prof && k >= 0 && k < 1024) {
-        unsigned long long* r = A.prof + Q3_PROF_LONG + 16 * k;
+        unsigned long long* r = A.prof + Q3_PROF_LONG + 24 * k;
         r[0] = S.lp_n; r[1] = S.lp_pts; r[2] = S.lp_t; r[3] = S.lp_all;
         r[4] = S.lp_tloc; r[5] = S.lp_wait; r[6] = S.lp_adopt - S.lp_wait; r[7] = S.lp_tail;
         r[8] = S.lp_own; r[9] = S.lp_got; r[10] = S.lp_hwait; r[11] = S.lp_stop; r[12] = S.lp_ev; r[13] = S.lp_posts;
         r[14] = L.hprof[0]; r[15] = L.hprof[1] | (L.hprof[2] << 32);
+        for (int q = 3; q < 8; q++) r[13 + q] = L.hprof[q];   // r[16..20]
       }
 #else
       (void)k;

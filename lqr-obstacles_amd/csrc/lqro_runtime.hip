@@ -39,7 +39,7 @@
 
 // hull: 32 counters + 2 words per job; pair: 16; hull wave phases: 16; local hull hand-overs: 16;
 // local-hull per-job words 4 x 4096
-#define LQRO_PROF_WORDS (32 + 2 * 4096 + 16 + 16 + 16 + 4 * 4096 + 64 + 16 * 1024)   // + 64: k_qhull's wave 1 (Q3_PROF_W1); + 16 x 1024: LQRO_QHULL_LONGPROF
+#define LQRO_PROF_WORDS (32 + 2 * 4096 + 16 + 16 + 16 + 4 * 4096 + 64 + 24 * 1024)   // + 64: k_qhull's wave 1 (Q3_PROF_W1); + 24 x 1024: LQRO_QHULL_LONGPROF
 #define LQRO_PROF_HULL_WORDS (32 + 2 * 4096 + 32)   // what lqro_debug_hull_profile returns
 
 using namespace lqro;

@@ -23,12 +23,12 @@ c.set_gains(g["A"], g["B"], g["L"], g["E"])
 for k in range(K):
     c.step(x, vg)
 b = c.hull_builds()
-w = np.zeros(16 * 1024, np.uint64)
+w = np.zeros(24 * 1024, np.uint64)
 fn = lqro.lib().lqro_debug_prof_words
 fn.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]
-assert fn(c._h, Q3_PROF_LONG, 16 * 1024, w.ctypes.data_as(C.c_void_p)) == 0
+assert fn(c._h, Q3_PROF_LONG, 24 * 1024, w.ctypes.data_as(C.c_void_p)) == 0
 c.close()
-w = w.reshape(-1, 16)[:len(b)]
+w = w.reshape(-1, 24)[:len(b)]
 d = (b["t_end"] - b["t_start"]) / 1e5
 ok = b["kernel"] == 0
 tot = d[ok].sum()
@@ -51,3 +51,6 @@ for i in np.argsort(-d)[:8]:
     print(f"      helped sequences: chunks wave 0 {own}, helpers {got}, waiting for helpers {hw / 1e5:.2f} ms, "
           f"stopping them {hs / 1e5:.2f} ms, events {ev}, posts {po}; helper chunks {hn}: "
           f"{(ht & 0xffffffff) / 1e2 / max(hn, 1):.2f} us locating, {(ht >> 32) / 1e2 / max(hn, 1):.2f} us claimed")
+    ns, tps, tsd, tw0, nw0 = (int(v) for v in w[i][16:21])
+    print(f"      wave 1: {ns} speculations, publication -> seen {tps / 1e2 / max(ns, 1):.2f} us, seen -> done "
+          f"{tsd / 1e2 / max(ns, 1):.2f} us; wave 0: {nw0} waits, speculation end -> seen {tw0 / 1e2 / max(nw0, 1):.2f} us")
