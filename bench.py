@@ -116,8 +116,13 @@ def critical_path(ctx):
             "mean_build_ms": float(dur.mean()),
             "mean_us_per_insertion": float(dur.sum() * 1e3 / max(1, int(b["insertions"].sum()))),
             "last_build_end_ms": float((int(b["t_end"].max()) - t0) / 1e5),
-            "hbm_bytes_per_build": tr[0]["hbm_bytes_per_build"] if tr else None,
-            "algorithmic_bytes_per_build": tr[0]["algorithmic_bytes_per_build"] if tr else None,
+            # (the steady steps' builds, as the timed step's; the first two
+            # steps' plain-schedule builds beside it)
+            "hbm_bytes_per_build": (tr[0].get("steady_hbm_bytes_per_build", tr[0]["hbm_bytes_per_build"])
+                                    if tr else None),
+            "hbm_bytes_per_build_all_steps": tr[0]["hbm_bytes_per_build"] if tr else None,
+            "algorithmic_bytes_per_build": (tr[0].get("steady_algorithmic_bytes_per_build",
+                                                      tr[0]["algorithmic_bytes_per_build"]) if tr else None),
             "traffic_source": tr[1] if tr else None,
             "note": "LQRO:867-969 per inside-hull pair (qconvex's build restated in-kernel); times from each "
                     "build's job start to its half-plane, s_memrealtime; last_build_end_ms from the first build's start"}
