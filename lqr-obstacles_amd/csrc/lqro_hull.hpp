@@ -99,7 +99,8 @@ struct HullArgs {
   int block_base;                   // scratch index of this launch's block 0
   int big_main;                     // k_hull_big takes the main queue (H*NP too large for LDS)
   int big_inline;                   // k_qhull rebuilds a build past its caps in place (q3_big_inline)
-  int qflags;                       // k_qhull: 1 helper waves locate long sequences, 2 the emit's lane state
+  int qflags;                       // k_qhull: 1 helper waves locate long sequences, 2 the emit's lane state,
+                                    // 4 wave 1 pre-scans the next speculation's queue entry
   int* lqueue;                      // k_lhull: pairs the local hull hands to the full hull
   int* lcount;
   int* ldone;                       // k_lhull: pairs it decided

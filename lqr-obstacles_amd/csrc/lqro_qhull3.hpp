@@ -241,8 +241,9 @@ struct Q3L {
   int hq_findbestnew, hq_notsharp, hq_nnew, hq_nmov, hq_nvis;
   double hq_max_outside;
 #ifdef LQRO_QHULL_LONGPROF
-  unsigned long long hprof[8];       // helper chunks, their ticks locating, claim to release; wave 1:
-                                     // speculations, publication -> seen, seen -> done; wave 0: done -> seen
+  unsigned long long hprof[12];      // helper chunks, their ticks locating, claim to release; wave 1:
+                                     // speculations, publication -> seen, seen -> done; wave 0: done -> seen;
+                                     // wave 1: queue-window reloads, ticks in the queue scan, in the horizon
   unsigned long long lp_pubr, lp_doner;   // the last publication's / speculation end's real time
 #endif
   int big_slot;                      // a build past the caps, rebuilt in place by qh_build (q3_body)
@@ -976,8 +977,10 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
       L.hq_nvis = S.nvis; L.hq_max_outside = S.max_outside;
       L.hcons = from2 >> 6;
       for (int b = 0; b < Q3_HR; b++) L.hr_st[b] = 0;
-      // (a full release: the new facets' spilled records are global)
-      q3_st_rel(reinterpret_cast<int*>(&L.hctl), (int)(((unsigned)S.hgen << 16) | (unsigned)(from2 >> 6)));
+      // (a full release: the new facets' spilled records are global); the
+      // first chunk is wave 0's own (it would wait for it anyway, and it
+      // locates it with its LDS columns)
+      q3_st_rel(reinterpret_cast<int*>(&L.hctl), (int)(((unsigned)S.hgen << 16) | (unsigned)((from2 >> 6) + 1)));
     }
   };
   auto stop = [&]() {   // no further claims; the held ones answered
@@ -996,6 +999,7 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
     int ev_pos = np, ev_kind = 0, ev_dst = -1;
     double ev_d = 0.0;
     if (help) post(from);
+    bool first = help;   // (the posted sequence's first chunk: claimed by the post)
     for (int c = from & ~63; c < np; c += 64) {
       Q3C(23, 1);
       const int pos = c + lane;
@@ -1004,8 +1008,8 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
       double d = 0.0;
       HullPt pt = pre;
       int f = -1, isout = 0, trig = 0;
-      bool mine = !help;
-      if (help) {
+      bool mine = !help || first;
+      if (help && !first) {
         // this chunk's results from a helper, or claimed and located here
         const int k = c >> 6, b = k % Q3_HR;
         int st = q3_ld_acq(&L.hr_st[b]);
@@ -1042,6 +1046,7 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
           d = L.hr_d[64 * b + lane];
         }
       }
+      first = false;
       Q3T(12);
       if (mine) q3_chunk_locate<false>(W, S, L, c, from, np, sharp, init, lane, pre, prestart, havepre ? 0 : -1, pt, f,
                                        d, isout, trig, ls, C0);
@@ -1446,6 +1451,13 @@ struct Q3QC {
   // wave 0 adopts the cone (no reload of ncoord2 from global memory)
   int one, rt;
   double r[6];
+  // the next speculation's queue entry, scanned after this one (q3_prescan):
+  // from position pc_from (this speculation's facet), the first entry valid
+  // then (pc_pos, facet pc_f, key pc_k, recorded furthest point pc_p at pc_x
+  // .. pc_z), or none before pc_end (pc_pos = -1); pc_from = -1: no scan
+  int pc_from, pc_pos, pc_end, pc_f, pc_p;
+  unsigned pc_k;
+  double pc_x, pc_y, pc_z;
 };
 
 __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep, unsigned ep2, Q3QC& Q, Q3P& P,
@@ -1492,14 +1504,51 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
   Q.one = 0;
   Q.rt = -1;
   W1T(1);
+#ifdef LQRO_QHULL_LONGPROF
+  const unsigned long long tq0_ = __builtin_amdgcn_s_memrealtime();
+  int reloads_ = 0;
+#endif
   int ok = 0;
   // 1. the queue's next live facet with points (not one insertion k made visible)
   const int qt = L.pub_qtail;
   int facet = -1, furthest = -1, fpos = -1;
   unsigned fkey = 0;
   double apex[3] = {0.0, 0.0, 0.0};
-  for (int qh = L.pub_qhead; qh < qt;) {
+  int qh0 = L.pub_qhead;
+  if (Q.pc_from >= 0 && Q.pc_from == qh0 && L.pub_adopt) {
+    // the entries q3_prescan found invalid stay invalid (a dead facet stays
+    // dead, a key only changes to a fresh one — an old facet's first point
+    // included —, and cc > 0 only ever comes with a fresh key), so its
+    // candidate, checked now, is the scan's answer; else the scan resumes
+    // after it
+    if (Q.pc_pos >= 0) {
+      const int fa = q3_fa(W, L, Q.pc_f);
+      const unsigned c = q3_cc(W, L, Q.pc_f);
+      if ((fa & QF_LIVE) && !(fa & QF_VISIBLE) && q3_key(W, L, Q.pc_f) == Q.pc_k && (c & 0xffffu) > 0) {
+        fpos = Q.pc_pos;
+        facet = Q.pc_f;
+        fkey = Q.pc_k;
+        furthest = (int)(c >> 16);
+        if (Q.pc_p == furthest) {
+          apex[0] = Q.pc_x; apex[1] = Q.pc_y; apex[2] = Q.pc_z;
+        } else {
+          apex[0] = W.Pr[3 * (size_t)furthest];
+          apex[1] = W.Pr[3 * (size_t)furthest + 1];
+          apex[2] = W.Pr[3 * (size_t)furthest + 2];
+        }
+      } else {
+        qh0 = Q.pc_pos + 1;
+      }
+    } else {
+      qh0 = max(qh0, Q.pc_end);
+    }
+  }
+  Q.pc_from = -1;
+  for (int qh = qh0; facet < 0 && qh < qt;) {
     if (qh >= Q.qcb + Q.qcn || qh < Q.qcb) {
+#ifdef LQRO_QHULL_LONGPROF
+      ++reloads_;
+#endif
       Q.qcb = qh;
       Q.qcn = min(64, qt - qh);
       if (lane < Q.qcn) {
@@ -1536,6 +1585,10 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
   }
   int ls = 0, nvis = 0, nnew = 0, ts = 0, lm = 0;
   W1T(2);
+#ifdef LQRO_QHULL_LONGPROF
+  const unsigned long long tq1_ = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0) { L.hprof[8] += (unsigned long long)reloads_; L.hprof[9] += tq1_ - tq0_; }
+#endif
   if (facet >= 0) {
     // 2. qh_findhorizon, as wave 0's (level order, first occurrence), visits as epochs
     if (lane == 0) L.sp_visf[0] = facet;
@@ -1589,6 +1642,9 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
       P.t[11] += 1;
 #endif
     }
+#ifdef LQRO_QHULL_LONGPROF
+    if (lane == 0) L.hprof[10] += __builtin_amdgcn_s_memrealtime() - tq1_;
+#endif
     // the horizon to wave 2, which fetches the partition sequence's head
     if (!cap && lane == 0) {
       L.sp_hnvis = nvis;
@@ -1759,6 +1815,7 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
   const int st = qh_wave_or(ls | ts | lm);
   W1T(5);
   hl_sync();
+  Q.pc_end = qt;   // (q3_prescan's range: the entries this publication released)
   if (lane == 0) {
     L.sp_ok = ok;
     L.sp_facet = facet;
@@ -1770,6 +1827,51 @@ __device__ inline void q3_spec(const Q3W& W, Q3L& L, int lane, unsigned short ep
     L.sp_status = st;
     L.sp_apex[0] = apex[0]; L.sp_apex[1] = apex[1]; L.sp_apex[2] = apex[2];
   }
+}
+
+// Wave 1, after releasing speculation k+1 (while wave 0 partitions k and
+// adopts k+1): the queue scan of speculation k+2, from k+1's facet, facets
+// k+1 makes visible (this speculation's marks) counted as dead.  The facet
+// fields are read while wave 0 changes them; q3_spec checks the candidate
+// after the next publication (an entry found invalid here stays invalid).
+__device__ inline void q3_prescan(const Q3W& W, Q3L& L, int lane, unsigned short ep, unsigned ep2, Q3QC& Q) {
+  Q.pc_from = -1;
+  const int from = L.sp_pos, qt = Q.pc_end;
+  if (!L.sp_ok || L.sp_facet < 0 || from < 0) return;
+  auto marked = [&](int f) -> bool {
+    return f < Q3_FL ? q3_lds(L.mark[f]) == ep : q3_glb(W.mark2[f]) == ep2;
+  };
+  Q.pc_pos = -1;
+  for (int qh = from; qh < qt;) {
+    if (qh >= Q.qcb + Q.qcn || qh < Q.qcb) {
+      Q.qcb = qh;
+      Q.qcn = min(64, qt - qh);
+      if (lane < Q.qcn) {
+        Q.qf = W.fq[qh + lane];
+        Q.qk = W.fqk[qh + lane];
+        const HullPt e = W.fqc[qh + lane];
+        Q.qx = e.x; Q.qy = e.y; Q.qz = e.z; Q.qp = e.q;
+      }
+    }
+    bool good = false;
+    if (lane < Q.qcn && Q.qcb + lane >= qh && Q.qcb + lane < qt) {
+      const int fa = q3_fa(W, L, Q.qf);
+      const unsigned c = q3_cc(W, L, Q.qf);
+      good = (fa & QF_LIVE) && !marked(Q.qf) && q3_key(W, L, Q.qf) == Q.qk && (c & 0xffffu) > 0;
+    }
+    const unsigned long long b = __ballot(good);
+    if (b) {
+      const int l = __ffsll((long long)b) - 1;
+      Q.pc_pos = Q.qcb + l;
+      Q.pc_f = __builtin_amdgcn_readlane(Q.qf, l);
+      Q.pc_k = (unsigned)__builtin_amdgcn_readlane((int)Q.qk, l);
+      Q.pc_p = __builtin_amdgcn_readlane(Q.qp, l);
+      Q.pc_x = hl_rl(Q.qx, l); Q.pc_y = hl_rl(Q.qy, l); Q.pc_z = hl_rl(Q.qz, l);
+      break;
+    }
+    qh = Q.qcb + Q.qcn;
+  }
+  Q.pc_from = from;
 }
 
 // wave 2: the head of the next partition sequence (qh_partitionvisible: the
@@ -3087,7 +3189,7 @@ __device__ __forceinline__ void q3_body(const HullArgs& A, Q3L& L, QhL* LB = nul
       L.ph = 0; L.sp_done = 0; L.sp_gdone = 0; L.hctl = 0u; L.hbusy = 0; L.sp_hz = 0; L.pf_done = 0;
       L.qflags = A.qflags;
 #ifdef LQRO_QHULL_LONGPROF
-      for (int k = 0; k < 8; k++) L.hprof[k] = 0ull;
+      for (int k = 0; k < 12; k++) L.hprof[k] = 0ull;
       L.lp_pubr = L.lp_doner = 0ull;
 #endif
       L.big_slot = -1;
@@ -3138,6 +3240,8 @@ __device__ __forceinline__ void q3_body(const HullArgs& A, Q3L& L, QhL* LB = nul
       int last = 0;
       Q3QC Q;
       Q.qcb = 0; Q.qcn = 0; Q.qf = 0; Q.qp = -1; Q.qk = 0u; Q.qx = Q.qy = Q.qz = 0.0;
+      Q.pc_from = -1; Q.pc_pos = -1; Q.pc_end = 0; Q.pc_f = 0; Q.pc_p = -1; Q.pc_k = 0u;
+      Q.pc_x = Q.pc_y = Q.pc_z = 0.0;
       Q.one = 0; Q.rt = -1;
       for (int k = 0; k < 6; k++) Q.r[k] = 0.0;
       long idle = 0;
@@ -3174,6 +3278,7 @@ __device__ __forceinline__ void q3_body(const HullArgs& A, Q3L& L, QhL* LB = nul
 #endif
           if (lane == 0) q3_st_rel_lds(&L.sp_done, p);
           if (lane == 0) q3_st_rel(&L.sp_gdone, p);
+          if (L.qflags & 4) q3_prescan(W, L, lane, ep, ep2, Q);
 #ifdef LQRO_QHULL_PROFILE
           if (lane == 0) { L.done_t2 = __builtin_amdgcn_s_memtime(); L.done_r = __builtin_amdgcn_s_memrealtime(); }
           P.tq2 = __builtin_amdgcn_s_memtime();
@@ -3286,7 +3391,7 @@ __device__ __forceinline__ void q3_body(const HullArgs& A, Q3L& L, QhL* LB = nul
         r[4] = S.lp_tloc; r[5] = S.lp_wait; r[6] = S.lp_adopt - S.lp_wait; r[7] = S.lp_tail;
         r[8] = S.lp_own; r[9] = S.lp_got; r[10] = S.lp_hwait; r[11] = S.lp_stop; r[12] = S.lp_ev; r[13] = S.lp_posts;
         r[14] = L.hprof[0]; r[15] = L.hprof[1] | (L.hprof[2] << 32);
-        for (int q = 3; q < 8; q++) r[13 + q] = L.hprof[q];   // r[16..20]
+        for (int q = 3; q < 11; q++) r[13 + q] = L.hprof[q];   // r[16..23]
       }
 #else
       (void)k;

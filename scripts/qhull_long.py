@@ -51,6 +51,7 @@ for i in np.argsort(-d)[:8]:
     print(f"      helped sequences: chunks wave 0 {own}, helpers {got}, waiting for helpers {hw / 1e5:.2f} ms, "
           f"stopping them {hs / 1e5:.2f} ms, events {ev}, posts {po}; helper chunks {hn}: "
           f"{(ht & 0xffffffff) / 1e2 / max(hn, 1):.2f} us locating, {(ht >> 32) / 1e2 / max(hn, 1):.2f} us claimed")
-    ns, tps, tsd, tw0, nw0 = (int(v) for v in w[i][16:21])
+    ns, tps, tsd, tw0, nw0, nrl, tqs, thz = (int(v) for v in w[i][16:24])
     print(f"      wave 1: {ns} speculations, publication -> seen {tps / 1e2 / max(ns, 1):.2f} us, seen -> done "
-          f"{tsd / 1e2 / max(ns, 1):.2f} us; wave 0: {nw0} waits, speculation end -> seen {tw0 / 1e2 / max(nw0, 1):.2f} us")
+          f"{tsd / 1e2 / max(ns, 1):.2f} us (queue scan {tqs / 1e2 / max(ns, 1):.2f}, {nrl} window reloads; horizon "
+          f"{thz / 1e2 / max(ns, 1):.2f}); wave 0: {nw0} waits, speculation end -> seen {tw0 / 1e2 / max(nw0, 1):.2f} us")
