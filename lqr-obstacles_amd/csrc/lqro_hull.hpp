@@ -100,7 +100,8 @@ struct HullArgs {
   int big_main;                     // k_hull_big takes the main queue (H*NP too large for LDS)
   int big_inline;                   // k_qhull rebuilds a build past its caps in place (q3_big_inline)
   int qflags;                       // k_qhull: 1 helper waves locate long sequences, 2 the emit's lane state,
-                                    // 4 wave 1 pre-scans the next speculation's queue entry
+                                    // 4 wave 1 pre-scans the next speculation's queue entry, 16 a long
+                                    // emit split over the waves
   int* lqueue;                      // k_lhull: pairs the local hull hands to the full hull
   int* lcount;
   int* ldone;                       // k_lhull: pairs it decided

@@ -237,6 +237,12 @@ struct Q3L {
   int hr_ls[Q3_HR], hr_st[Q3_HR];
   unsigned hctl;
   int hbusy, hcons;
+  // a long sequence's emit split over the waves (q3_emit_bucket): bucket b is
+  // the destinations i with i % 4 == b (each destination's points are placed
+  // in sequence order by one wave); ectl = generation << 8 | the next bucket
+  // to claim (0: none), edone the buckets finished
+  unsigned ectl;
+  int edone, ej_np, ej_nd, ej_ndnew, ej_init, ej_nvis;
   int hq_end, hq_from, hq_np, hq_sharp, hq_init;
   int hq_findbestnew, hq_notsharp, hq_nnew, hq_nmov, hq_nvis;
   double hq_max_outside;
@@ -263,6 +269,7 @@ struct Q3S {
   int nnew, nvis, nmov, nold;
   int findbestnew, notsharp;
   int hgen;               // q3_locate_seq's posts to the helper waves (hctl's generation)
+  int egen;               // q3_emit_seq's posts (ectl's generation)
   double MAXabs_coord, MAXsumcoord, MAXwidth, NEARzero[3];
   double DISTround, MINvisible, MAXcoplanar, MINoutside, MINdenom, MINdenom_2, max_outside;
   double interior[3];
@@ -1160,6 +1167,102 @@ __device__ inline void q3_locate_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int s
   }
 }
 
+// One bucket of a long sequence's emit (q3_emit_seq): the destinations i
+// with i % 4 == b, their state in their lanes (destination i in lane i),
+// every chunk of the sequence read, this bucket's destination groups placed
+// in sequence order — the same placement as the single-wave loop, each
+// destination's points by one wave
+__device__ inline void q3_emit_bucket(const Q3W& W, Q3L& L, int lane, int b) {
+  const int np = L.ej_np, nd = L.ej_nd, ndnew = L.ej_ndnew, nvis = L.ej_nvis;
+  const bool init = L.ej_init != 0;
+  const int gl = lane < ndnew ? lane : Q3_NEWCAP + (lane - ndnew);
+  const bool has = lane < nd && (lane & 3) == b && L.pcnt[gl];
+  int Rc = 0, Rch = -1, Ro = 0;
+  double Rm = 0.0, Rx = 0.0, Ry = 0.0, Rz = 0.0;
+  if (has) {
+    Rc = L.dcnt[gl]; Rm = L.dmax[gl]; Rch = L.dchamp[gl]; Ro = L.doff[gl];
+    Rx = L.dchp[3 * gl]; Ry = L.dchp[3 * gl + 1]; Rz = L.dchp[3 * gl + 2];
+  }
+  const unsigned long long ltmask = (1ull << lane) - 1ull;
+  int ng = -1;
+  double ndd = 0.0;
+  HullPt npt;
+  npt.x = npt.y = npt.z = 0.0; npt.q = -1; npt.pad = 0;
+  auto ldc = [&](int c) {
+    const int pos = c + lane;
+    ng = -1;
+    ndd = 0.0;
+    if (pos < np) {
+      ng = W.pdst[pos];
+      ndd = W.pdd[pos];
+      int st;
+      npt = q3_seqpt(W, L, nvis, init, pos, &st);
+    }
+  };
+  ldc(0);
+  for (int c = 0; c < np; c += 64) {
+    const int g = ng;
+    const double dd = ndd;
+    const HullPt pt = npt;
+    if (c + 64 < np) ldc(c + 64);
+    const int i = g < 0 ? -1 : (g < Q3_NEWCAP ? g : ndnew + (g - Q3_NEWCAP));
+    const bool mine = i >= 0 && (i & 3) == b;
+    unsigned long long todo = __ballot(mine);
+    int wpos = -1, wr = 0;
+    while (todo) {
+      const int lead = __ffsll((long long)todo) - 1;
+      const int gg = __builtin_amdgcn_readlane(g, lead);
+      const unsigned long long grp = __ballot(mine && g == gg);
+      todo &= ~grp;
+      const int l = __builtin_amdgcn_readlane(i, lead);
+      int cnt = __builtin_amdgcn_readlane(Rc, l), champ = __builtin_amdgcn_readlane(Rch, l);
+      double mx = hl_rl(Rm, l), cx = hl_rl(Rx, l), cy = hl_rl(Ry, l), cz = hl_rl(Rz, l);
+      q3_place(grp, lane, ltmask, dd, pt, __builtin_amdgcn_readlane(Ro, l), W.SB, cnt, mx, champ, cx, cy, cz, wpos,
+               wr);
+      if (lane == l) { Rc = cnt; Rm = mx; Rch = champ; Rx = cx; Ry = cy; Rz = cz; }
+    }
+    if (wpos >= 0) W.sb[wpos] = wr;
+  }
+  if (has) {
+    L.dcnt[gl] = Rc; L.dmax[gl] = Rm; L.dchamp[gl] = Rch;
+    L.dchp[3 * gl] = Rx; L.dchp[3 * gl + 1] = Ry; L.dchp[3 * gl + 2] = Rz;
+  }
+}
+
+// claim the posted emit's next bucket (-1: none left)
+__device__ __forceinline__ int q3_emit_claim(Q3L& L, int lane) {
+  int k = -1;
+  if (lane == 0) {
+    for (;;) {
+      unsigned v = (unsigned)q3_ld_acq(reinterpret_cast<const int*>(&L.ectl));
+      if (v == 0u || (v & 0xffu) >= 4u) break;
+      unsigned e = v;
+      if (__hip_atomic_compare_exchange_strong(&L.ectl, &e, v + 1u, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP)) {
+        k = (int)(v & 0xffu);
+        break;
+      }
+    }
+  }
+  return __builtin_amdgcn_readfirstlane(k);
+}
+
+// waves 1-3: a bucket of a posted emit, if one is left
+__device__ inline bool q3_emit_help(const Q3W& W, Q3L& L, int lane) {
+  const unsigned v = (unsigned)q3_ld_acq(reinterpret_cast<const int*>(&L.ectl));
+  if (v == 0u || (v & 0xffu) >= 4u) return false;
+  const int k = q3_emit_claim(L, lane);
+  if (k < 0) return false;
+  q3_emit_bucket(W, L, lane, k);
+  if (lane == 0) {
+    // (its set entries before the count: wave 0 reads the count, then the
+    // next partition and the other waves read the sets)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __hip_atomic_fetch_add(&L.edone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  return true;
+}
+
 // The located points into their destinations' outside sets, in sequence
 // order, with Qhull's placement (lqro_qhull.hpp qh_emit_seq: the furthest
 // point so far held aside, a displaced one stays where it was).  Old
@@ -1286,6 +1389,32 @@ __device__ inline void q3_emit_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int ndn
   }
   hl_sync();
   Q3T(15);
+  // a long sequence with at most 64 destinations: the destinations in four
+  // buckets, placed by wave 0 and whichever helper waves are free
+  if (np > 64 && nd <= 64 && (L.qflags & 16)) {
+    S.egen = S.egen % 0xffffff + 1;
+    if (lane == 0) {
+      L.ej_np = np; L.ej_nd = nd; L.ej_ndnew = ndnew; L.ej_init = init ? 1 : 0; L.ej_nvis = S.nvis;
+      L.edone = 0;
+      // (a full release: pdst / pdd are global stores of this wave)
+      q3_st_rel(reinterpret_cast<int*>(&L.ectl), (int)((unsigned)S.egen << 8));
+    }
+    int mine = 0;
+    for (int k = q3_emit_claim(L, lane); k >= 0; k = q3_emit_claim(L, lane)) {
+      q3_emit_bucket(W, L, lane, k);
+      ++mine;
+    }
+    hl_sync();
+    int dn = q3_ld_acq(&L.edone);
+    for (long w = 0; dn != 4 - mine && w < (1l << 24); ++w) {
+      __builtin_amdgcn_s_sleep(Q3_W0_SLEEP);
+      dn = q3_ld_acq(&L.edone);
+    }
+    if (lane == 0) __hip_atomic_store(&L.ectl, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    // a helper that never finished may still write: the build stops
+    // (k_qhull_big rebuilds the pair)
+    if (dn != 4 - mine) { S.status |= QHS_CAPACITY | QHS_TIMEOUT; return; }
+  } else {
   // at most 64 destinations (the usual long sequence): destination i's state
   // in lane i (new facet i, then the old ones) from here to the end of the
   // sequence, read by the group with lane reads — no LDS round trip and no
@@ -1373,6 +1502,7 @@ __device__ inline void q3_emit_seq(const Q3W& W, Q3S& S, Q3L& L, int np, int ndn
       L.dchp[3 * g] = Rx; L.dchp[3 * g + 1] = Ry; L.dchp[3 * g + 2] = Rz;
     }
   }
+  }   // (the single-wave emit)
   hl_sync();
   Q3T(17);
   // the furthest point ends each set
@@ -1931,6 +2061,7 @@ __device__ inline void q3_build(const Q3W& W, Q3S& S, Q3L& L, int n, int lane) {
   S.nnew = S.nvis = S.nmov = S.nold = 0;
   S.findbestnew = S.notsharp = 0;
   S.hgen = 0;
+  S.egen = 0;
   S.keyc = 1;
   S.key0_last = 0;
   S.qhead = S.qtail = 0;
@@ -3187,6 +3318,7 @@ __device__ __forceinline__ void q3_body(const HullArgs& A, Q3L& L, QhL* LB = nul
     // hull_points' barriers)
     if (threadIdx.x == 0) {
       L.ph = 0; L.sp_done = 0; L.sp_gdone = 0; L.hctl = 0u; L.hbusy = 0; L.sp_hz = 0; L.pf_done = 0;
+      L.ectl = 0u; L.edone = 0;
       L.qflags = A.qflags;
 #ifdef LQRO_QHULL_LONGPROF
       for (int k = 0; k < 12; k++) L.hprof[k] = 0ull;
@@ -3222,6 +3354,7 @@ __device__ __forceinline__ void q3_body(const HullArgs& A, Q3L& L, QhL* LB = nul
           }
         }
         if (q3_help(W, L, lane, CH)) { idle = 0; continue; }
+        if (q3_emit_help(W, L, lane)) { idle = 0; continue; }
         if (q3_ld_acq(&L.ph) < 0) break;
         if (++idle > (1l << 24)) break;
         __builtin_amdgcn_s_sleep(Q3_W2_SLEEP);
@@ -3301,6 +3434,7 @@ __device__ __forceinline__ void q3_body(const HullArgs& A, Q3L& L, QhL* LB = nul
             continue;
           }
         }
+        if (q3_emit_help(W, L, lane)) { idle = 0; continue; }   // a posted emit's bucket
         if (++idle > (1l << 24)) break;
         __builtin_amdgcn_s_sleep(Q3_W1_SLEEP);
       }

@@ -395,7 +395,8 @@ struct lqro_ctx {
   int hot_split;             // LQRO_HOT_SPLIT (default 1): the split hot launch in Qhull order
   int qside_pct;             // LQRO_QHULL_SIDE_PCT: side CUs per 100 of the last step's inside-hull pairs (default 100)
   int qhull_inline;          // LQRO_QHULL_INLINE_BIG: k_qhull rebuilds a capped build in place (default 1)
-  int qhull_flags;           // LQRO_QHULL_FLAGS: k_qhull's helper waves (1), emit lane state (2), queue pre-scan (4); default 7
+  int qhull_flags;           // LQRO_QHULL_FLAGS: k_qhull's helper waves (1), emit lane state (2), queue pre-scan (4),
+                             // a long emit over the waves (16); default 23
   int qbalance;              // LQRO_QHULL_BALANCE: the side's width from the measured work (default 1)
   int qspare;                // LQRO_QHULL_SPARE: side CUs beyond the last step's inside-hull count (default 4; -1: count/16 + 4)
   int hot_spec;              // LQRO_HOT_SPEC (default 1): with the split, the last step's inside pairs are built speculatively from the step's start
@@ -705,7 +706,7 @@ int lqro_create(const lqro_config* cfg, lqro_ctx** out) {
     const char* qi = getenv("LQRO_QHULL_INLINE_BIG");
     c->qhull_inline = qi ? atoi(qi) != 0 : 1;
     const char* qf = getenv("LQRO_QHULL_FLAGS");
-    c->qhull_flags = qf ? atoi(qf) : 7;
+    c->qhull_flags = qf ? atoi(qf) : 23;
     // the side's width from the measured work of the step two before (the
     // sweep's CU time, the builds' total and longest): no wider than leaves
     // the sweep no longer than the builds (LQRO_QHULL_BALANCE=0: one CU per
