@@ -56,15 +56,17 @@ def c3_oracle(lqro_mod, oracle, gains):
 
 
 @pytest.mark.parametrize("sched", ["default", "no_spec", "spare0", "early_lp_off", "no_split", "qside", "plain",
-                                   "balance_off", "inline_big"])
+                                   "balance_off", "inline_big", "qflags0"])
 def test_qhull_order_c3_full_step(lqro_mod, gains, monkeypatch, c3_oracle, sched):
     x, vg, rv, rr, carry = c3_oracle
     env = {"default": {}, "no_spec": {"LQRO_HOT_SPEC": "0"}, "spare0": {"LQRO_QHULL_SPARE": "0"},
            "early_lp_off": {"LQRO_EARLY_LP": "0"},
            "no_split": {"LQRO_HOT_SPLIT": "0"}, "qside": {"LQRO_QSIDE": "1"}, "plain": {"LQRO_HOT": "0"},
-           "balance_off": {"LQRO_QHULL_BALANCE": "0"}, "inline_big": {"LQRO_QHULL_INLINE_BIG": "0"}}[sched]
+           "balance_off": {"LQRO_QHULL_BALANCE": "0"}, "inline_big": {"LQRO_QHULL_INLINE_BIG": "0"},
+           # (k_qhull without its round-6 helpers, lane state, queue pre-scan and bucketed emit)
+           "qflags0": {"LQRO_QHULL_FLAGS": "0"}}[sched]
     for k in ("LQRO_EARLY_LP", "LQRO_QSIDE", "LQRO_HOT", "LQRO_LOCAL_HULL", "LQRO_SIDE_HULL_CUS", "LQRO_HOT_SPLIT",
-              "LQRO_HOT_SPEC", "LQRO_QHULL_SPARE", "LQRO_QHULL_BALANCE", "LQRO_QHULL_INLINE_BIG"):
+              "LQRO_HOT_SPEC", "LQRO_QHULL_SPARE", "LQRO_QHULL_BALANCE", "LQRO_QHULL_INLINE_BIG", "LQRO_QHULL_FLAGS"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
